@@ -1,0 +1,289 @@
+/*
+ * snapgpu.h -- C ABI of the MI355X-native SNAP seed-and-extend hot path.
+ *
+ * This is the drop-in boundary for SNAPLib's `Aligner` / `BaseAligner` surface
+ * (reference: SNAPLib/Aligner.h:54-80, SNAPLib/BaseAligner.h:44-142).  Every entry
+ * point is plain C (pointers + sizes, no C++ or torch types) so that the
+ * reference's C++ (apps/snap, SingleAlignerContext via AlignerExtension,
+ * SNAPLib/AlignerContext.h:132-163) -- or ctypes / any FFI -- can bind it.
+ * INTEGRATION.md shows the adapter a SNAPLib maintainer would add.
+ *
+ * Conventions
+ *  - Functions returning int return SNAPGPU_OK (0) on success, a negative
+ *    SNAPGPU_E* code on failure; snapgpu_last_error() gives the message.  The
+ *    reference calls soft_exit() (SNAPLib/exit.cpp:27-31) where this API returns
+ *    an error code instead (e.g. a read longer than maxReadSize,
+ *    BaseAligner.cpp:609-613 -> per-read flag SNAPGPU_FLAG_READ_TOO_LONG).
+ *  - Handles are opaque; an aligner handle is bound to one GPU and must be used
+ *    from one host thread at a time (the reference's BaseAligner is likewise not
+ *    thread safe, Aligner.h:19-20).
+ *  - Genome locations are the reference's 0-based offsets into the padded
+ *    whole-genome string (Genome.h:29, FASTA.cpp:67-125).
+ */
+#ifndef SNAPGPU_H
+#define SNAPGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SNAPGPU_ABI_VERSION 1
+
+enum {
+    SNAPGPU_OK = 0,
+    SNAPGPU_EINVAL = -1,      /* bad argument */
+    SNAPGPU_EIO = -2,         /* file could not be read/written */
+    SNAPGPU_ENOMEM = -3,      /* host or device allocation failed */
+    SNAPGPU_EDEVICE = -4,     /* HIP runtime error / no GPU */
+    SNAPGPU_EFORMAT = -5,     /* index/genome file format error */
+    SNAPGPU_EUNSUPPORTED = -6 /* parameter combination not supported */
+};
+
+/* AlignmentResult (SNAPLib/Read.h:41) */
+enum { SNAPGPU_NOT_FOUND = 0, SNAPGPU_SINGLE_HIT = 1, SNAPGPU_MULTIPLE_HITS = 2, SNAPGPU_UNKNOWN = 3 };
+/* Direction (SNAPLib/directions.h:26-35) */
+enum { SNAPGPU_FORWARD = 0, SNAPGPU_RC = 1 };
+
+/* per-read flags in snapgpu_result_t.flags */
+#define SNAPGPU_FLAG_READ_TOO_LONG  0x01u  /* reference: soft_exit(1), BaseAligner.cpp:609-613 */
+#define SNAPGPU_FLAG_MAPQ_FIXED     0x02u  /* MAPQ re-derived on host with libm log10 (boundary case) */
+#define SNAPGPU_FLAG_SPILLED        0x04u  /* candidate set exceeded the LDS arena; re-run in HBM arena */
+#define SNAPGPU_FLAG_TOO_MANY_NS    0x08u  /* countOfNs > maxK (BaseAligner.cpp:652-655) */
+
+/*
+ * Result of one AlignRead call (BaseAligner.cpp:510-938).  location / direction /
+ * score / mapq are exactly what AlignRead writes through its out-pointers,
+ * including the "written before the result is known" conventions
+ * (BaseAligner.cpp:582-584, 1357-1360): location=0xffffffff, direction=FORWARD,
+ * score=0xffff when nothing was scored.  mapq is 0 when AlignRead returns before
+ * writing it (short read / too many Ns).  The remaining fields are the per-read
+ * deltas of BaseAligner's statistics getters (BaseAligner.h:113-117) and its
+ * private MAPQ inputs (BaseAligner.h:284-285,333), exported for parity checking
+ * and roofline accounting.
+ */
+typedef struct snapgpu_result {
+    uint32_t location;
+    int32_t  score;
+    int32_t  mapq;
+    uint8_t  result;      /* SNAPGPU_NOT_FOUND .. */
+    uint8_t  direction;   /* SNAPGPU_FORWARD / SNAPGPU_RC */
+    uint8_t  flags;       /* SNAPGPU_FLAG_* */
+    uint8_t  reserved;
+    uint32_t nLookups;            /* getNHashTableLookups() delta */
+    uint32_t nLocationsScored;    /* getLocationsScored() delta */
+    uint16_t popularSeedsSkipped; /* BaseAligner::popularSeedsSkipped */
+    uint16_t nHitsIgnored;        /* getNHitsIgnoredBecauseOfTooHighPopularity() delta */
+    uint32_t nProbes;             /* hash-table entries probed (roofline P) */
+    uint32_t nHitWords;           /* hit words consumed (roofline H) */
+    uint32_t nOverflowLists;      /* overflow lists visited (roofline V) */
+    double   probabilityOfAllCandidates;
+    double   probabilityOfBestCandidate;
+} snapgpu_result_t;   /* 56 bytes */
+
+/* BaseAligner constructor parameters (BaseAligner.h:44-55, defaults of
+ * AlignerOptions.cpp:33-85 / SingleAligner.cpp:167-179). */
+typedef struct snapgpu_aligner_params {
+    uint32_t maxHitsToConsider;  /* -h, default 300 */
+    uint32_t maxK;               /* -d, default 14 */
+    uint32_t maxReadSize;        /* MAX_READ_LENGTH (Read.h:45), default 500 */
+    uint32_t maxSeedsToUse;      /* -n, default 25 (0 => use seedCoverage) */
+    double   maxSeedCoverage;    /* -sc, used iff maxSeedsToUse == 0 */
+    uint32_t extraSearchDepth;   /* default 2 */
+    uint32_t explorePopularSeeds;/* setExplorePopularSeeds (BaseAligner.h:139) */
+    uint32_t stopOnFirstHit;     /* setStopOnFirstHit (BaseAligner.h:142) */
+} snapgpu_aligner_params_t;
+
+void snapgpu_aligner_params_default(snapgpu_aligner_params_t *p);
+
+/* ------------------------------------------------------------------ genome */
+typedef struct snapgpu_genome snapgpu_genome_t;
+
+/* ReadFASTAGenome (SNAPLib/FASTA.cpp:31-130): upper-cases, N -> 'n',
+ * `chromosomePadding` 'n's before every contig and at the end. */
+snapgpu_genome_t *snapgpu_genome_from_fasta(const char *path, uint32_t chromosomePadding);
+
+/* Deterministic synthetic genome (no reference equivalent; stands in for
+ * GRCh38 data that is not available offline).  See DESIGN.md "Synthetic data". */
+typedef struct snapgpu_synth_genome_params {
+    uint64_t seed;               /* PRNG seed (e.g. 2121) */
+    uint64_t totalBases;         /* sum of contig lengths (excl. padding) */
+    uint32_t nContigs;
+    uint32_t nRepeatFamilies;    /* 0 => uniform random genome */
+    double   repeatFraction;     /* target fraction of repeat-derived bases */
+    double   maxDivergence;      /* per-copy divergence ~ U(0, maxDivergence) */
+    double   nRunFraction;       /* fraction of bases in runs of N */
+    uint32_t chromosomePadding;  /* default 500 */
+} snapgpu_synth_genome_params_t;
+snapgpu_genome_t *snapgpu_genome_synthetic(const snapgpu_synth_genome_params_t *p);
+int  snapgpu_genome_write_fasta(const snapgpu_genome_t *g, const char *path);
+void snapgpu_genome_free(snapgpu_genome_t *g);
+uint32_t snapgpu_genome_nbases(const snapgpu_genome_t *g);
+/* pointer to base 0 of the padded genome string; bytes [-256, nBases+256) are readable */
+const char *snapgpu_genome_bases(const snapgpu_genome_t *g);
+int snapgpu_genome_npieces(const snapgpu_genome_t *g);
+uint32_t snapgpu_genome_piece_offset(const snapgpu_genome_t *g, int i);
+const char *snapgpu_genome_piece_name(const snapgpu_genome_t *g, int i);
+
+/* ------------------------------------------------------------------- index */
+typedef struct snapgpu_index snapgpu_index_t;
+
+/* GenomeIndex::BuildIndexToDirectory semantics (GenomeIndex.cpp:348-720): every
+ * genome offset in [0, nBases - seedLen - 1) whose seedLen bases are all ACGT is
+ * indexed under its canonical (smaller of seed / reverse complement) seed;
+ * overflow lists are sorted descending (GenomeIndex.cpp:616-618).  The layout of
+ * the SNAPHashTable slots differs from the reference's multi-threaded builder
+ * (as it does between two reference builds), the lookup results do not.
+ * Takes ownership of `genome`.  nThreads <= 0 => hardware concurrency. */
+snapgpu_index_t *snapgpu_index_build(snapgpu_genome_t *genome, int seedLen, int nThreads);
+/* GenomeIndex::loadFromDirectory (GenomeIndex.cpp:844-963), reference on-disk format. */
+snapgpu_index_t *snapgpu_index_load(const char *directory);
+/* Write the reference on-disk format (GenomeIndex.cpp:646-710, Genome.cpp:125-158,
+ * HashTable.cpp:180-215) so the reference `snap-rna` can load our index. */
+int  snapgpu_index_save(const snapgpu_index_t *idx, const char *directory);
+void snapgpu_index_free(snapgpu_index_t *idx);
+
+typedef struct snapgpu_index_info {
+    uint32_t nBases;
+    uint32_t seedLen;
+    uint32_t nHashTables;
+    uint32_t chromosomePadding;
+    uint64_t overflowTableSize;   /* u32 words */
+    uint64_t totalHashSlots;      /* sum of tableSize */
+    uint64_t totalUsedSlots;
+    int32_t  nPieces;
+    uint32_t hasIupac;            /* genome holds bytes other than ACGTn */
+} snapgpu_index_info_t;
+int snapgpu_index_get_info(const snapgpu_index_t *idx, snapgpu_index_info_t *info);
+
+/* Raw read-only view of the index tables (SNAPHashTable entries are
+ * {u32 key, u32 value1, u32 value2}, HashTable.h:117-123). */
+typedef struct snapgpu_index_view {
+    const uint32_t *slots;          /* all tables concatenated, 3 words per slot */
+    const uint64_t *tableBase;      /* [nHashTables] slot index of table start */
+    const uint64_t *tableSize;      /* [nHashTables] */
+    const uint32_t *overflow;       /* overflow table (count, hits... descending) */
+    const char     *genome;         /* base 0 of padded genome, [-256, nBases+256) readable */
+    const uint32_t *pieceOffsets;   /* [nPieces] */
+    uint32_t nBases, seedLen, nHashTables, chromosomePadding;
+    int32_t  nPieces;
+    uint32_t pad_;
+    uint64_t overflowTableSize;
+} snapgpu_index_view_t;
+int snapgpu_index_get_view(const snapgpu_index_t *idx, snapgpu_index_view_t *view);
+
+/* GenomeIndex::lookupSeed (GenomeIndex.cpp:971-1011), host side.  Writes up to
+ * `cap` hits per direction; returns the true counts in nHits[2]. */
+int snapgpu_index_lookup(const snapgpu_index_t *idx, const char *seedBases,
+                         uint32_t nHits[2], uint32_t *hitsFwd, uint32_t *hitsRc, uint32_t cap);
+
+/* ------------------------------------------------------------------- reads */
+/* A batch of reads in host memory: read i has bases[offsets[i] .. +lengths[i])
+ * and the same range of quals (Phred+33), as Read::getData/getQuality expose
+ * them (Read.h:289-328).  Buffers carry >= 16 bytes of zero slack at the end. */
+typedef struct snapgpu_reads {
+    uint64_t  n;
+    uint64_t  totalBytes;
+    char     *bases;
+    char     *quals;
+    uint64_t *offsets;
+    uint32_t *lengths;
+    uint32_t *truthLocation;   /* generator ground truth (genome offset of read start), or NULL */
+    uint8_t  *truthDirection;
+} snapgpu_reads_t;
+
+/* wgsim-like simulator: uniform start, 50/50 strand,
+ * haplotype mutations (rate, indel fraction) then per-base substitution errors,
+ * constant quality char. */
+typedef struct snapgpu_synth_reads_params {
+    uint64_t seed;              /* e.g. 99 */
+    uint64_t nReads;
+    uint32_t readLength;        /* 100 */
+    uint32_t qualityChar;       /* '2' = Q17, as wgsim writes for 2% error */
+    double   baseErrorRate;     /* 0.02 */
+    double   mutationRate;      /* 0.001 */
+    double   indelFraction;     /* 0.15 */
+    double   indelExtend;       /* 0.3 */
+    double   randomReadFraction;/* fraction of reads of pure noise (NotFound) */
+} snapgpu_synth_reads_params_t;
+snapgpu_reads_t *snapgpu_reads_synthetic(const snapgpu_genome_t *g, const snapgpu_synth_reads_params_t *p);
+snapgpu_reads_t *snapgpu_reads_from_fastq(const char *path);
+/* Build a batch from caller arrays (copies them). */
+snapgpu_reads_t *snapgpu_reads_from_arrays(uint64_t n, const char *bases, const char *quals,
+                                           const uint64_t *offsets, const uint32_t *lengths);
+int  snapgpu_reads_write_fastq(const snapgpu_reads_t *r, const char *path);
+void snapgpu_reads_free(snapgpu_reads_t *r);
+
+/* ----------------------------------------------------------------- aligner */
+typedef struct snapgpu_aligner snapgpu_aligner_t;
+
+int  snapgpu_device_count(void);
+/* BaseAligner::BaseAligner (BaseAligner.cpp:46-194) + index upload to HBM.  The
+ * index must outlive the aligner. */
+snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx,
+                                          const snapgpu_aligner_params_t *params);
+void snapgpu_aligner_free(snapgpu_aligner_t *a);
+
+/* Batched BaseAligner::AlignRead (BaseAligner.cpp:196-200 / 510-938) over host
+ * buffers: H2D of the reads, the GPU passes, D2H of the records. */
+int snapgpu_align_batch(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, snapgpu_result_t *out);
+
+/* Device-resident variant: reads are uploaded once with snapgpu_reads_upload;
+ * snapgpu_align_resident runs only the GPU passes (inputs already in HBM, output
+ * left in HBM); snapgpu_results_download copies the records back. */
+typedef struct snapgpu_device_reads snapgpu_device_reads_t;
+snapgpu_device_reads_t *snapgpu_reads_upload(snapgpu_aligner_t *a, const snapgpu_reads_t *reads);
+void snapgpu_device_reads_free(snapgpu_device_reads_t *d);
+int  snapgpu_align_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d);
+int  snapgpu_results_download(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, snapgpu_result_t *out);
+int  snapgpu_synchronize(snapgpu_aligner_t *a);
+
+/* Timing of the dominant kernel (HIP events on the aligner's own stream), in ms,
+ * for the last snapgpu_align_resident / snapgpu_align_batch call. */
+typedef struct snapgpu_timing {
+    double mainKernelMs;     /* pass 1: LDS-arena aligner kernel */
+    double spillKernelMs;    /* pass 2: HBM-arena aligner kernel (spilled reads) */
+    double fixupMs;          /* host MAPQ fix-ups */
+    uint64_t nSpilled;
+    uint64_t nMapqFixed;
+} snapgpu_timing_t;
+int snapgpu_last_timing(snapgpu_aligner_t *a, snapgpu_timing_t *t);
+
+/* Aggregated getters of the reference aligner (Aligner.h:62-70). */
+typedef struct snapgpu_aligner_stats {
+    int64_t nHashTableLookups;
+    int64_t nLocationsScored;
+    int64_t nHitsIgnoredBecauseOfTooHighPopularity;
+    int64_t nReadsIgnoredBecauseOfTooManyNs;
+    int64_t nIndelsMerged;
+    int64_t nReads;
+} snapgpu_aligner_stats_t;
+int snapgpu_aligner_get_stats(const snapgpu_aligner_t *a, snapgpu_aligner_stats_t *s);
+int snapgpu_aligner_max_k(const snapgpu_aligner_t *a);           /* getMaxK() */
+const char *snapgpu_aligner_name(const snapgpu_aligner_t *a);    /* getName() */
+
+/* -------------------------------------------------------- Landau-Vishkin */
+/* LandauVishkin<dir>::computeEditDistance (LandauVishkin.h:211-455) on the GPU,
+ * one call per task, for unit parity (reference tests/LandauVishkinTest.cpp).
+ * Task i: text = texts[textOff[i] .. +textLen[i]) (for dir=-1 the text is
+ * walked backwards from its last byte, as a reverse LV called with a pointer
+ * one past the end), pattern/quals = patterns/quals[patOff[i] .. +patLen[i]).
+ * Out: edit distance or -1, netIndel, matchProbability. */
+int snapgpu_lv_batch(int device, int direction, uint32_t n,
+                     const char *texts, const uint64_t *textOff, const uint32_t *textLen,
+                     const char *patterns, const char *quals, const uint64_t *patOff,
+                     const uint32_t *patLen, const int32_t *k,
+                     int32_t *outScore, int32_t *outNetIndel, double *outProb);
+
+/* MAPQ (mapq.h:32-65) as the host computes it; exported for tests. */
+int snapgpu_compute_mapq(double pAll, double pBest, int score, int popularSeedsSkipped);
+
+const char *snapgpu_last_error(void);
+int snapgpu_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SNAPGPU_H */

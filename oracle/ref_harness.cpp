@@ -1,0 +1,127 @@
+// ref_harness.cpp -- TEST INFRASTRUCTURE ONLY (never shipped, never on the GPU box).
+//
+// A small driver linked against the REFERENCE's own SNAPLib objects (built by
+// oracle/Makefile.ref from /root/reference) so that the C restatement in
+// oracle/snap_oracle.c and the HIP path can be pinned against the real
+// BaseAligner / LandauVishkin / GenomeIndex::lookupSeed.
+//
+// Construction mirrors SNAPLib/SingleAligner.cpp:165-185 (maxReadSize =
+// MAX_READ_LENGTH, LV objects owned by the aligner, BigAllocator-backed), and
+// the LV tables are initialised as AlignerOptions.cpp:84 does.
+//
+// Modes:
+//   align  <indexDir> <reads.fq> [maxHits maxK numSeeds extraSearchDepth]
+//          -> one TSV line per read:
+//             i result loc dir score mapq lookups scored popularSkipped pAll_hex pBest_hex
+//   lv     <calls.tsv>   lines: dir k text pattern quals   -> e netIndel prob_hex
+//   lookup <indexDir> <seeds.txt>  one seed string per line -> nF nRC sumF sumRC firstF firstRC
+#define private public          // read-only access to BaseAligner's private scoring state
+#include "stdafx.h"
+#include "BaseAligner.h"
+#undef private
+#include "GenomeIndex.h"
+#include "LandauVishkin.h"
+#include "Read.h"
+#include "Seed.h"
+#include "BigAlloc.h"
+#include <string>
+#include <vector>
+#include <fstream>
+#include <iostream>
+#include <sstream>
+
+static void hexd(double d, char *buf) { sprintf(buf, "%a", d); }
+
+static int mode_align(int argc, char **argv) {
+    if (argc < 4) { fprintf(stderr, "align <indexDir> <reads.fq> [maxHits maxK numSeeds extra]\n"); return 2; }
+    unsigned maxHits = argc > 4 ? atoi(argv[4]) : 300;
+    unsigned maxK = argc > 5 ? atoi(argv[5]) : 14;
+    unsigned numSeeds = argc > 6 ? atoi(argv[6]) : 25;
+    unsigned extra = argc > 7 ? atoi(argv[7]) : 2;
+    initializeLVProbabilitiesToPhredPlus33();
+    GenomeIndex *idx = GenomeIndex::loadFromDirectory(argv[2]);
+    if (!idx) { fprintf(stderr, "cannot load index %s\n", argv[2]); return 1; }
+    BigAllocator *al = new BigAllocator(BaseAligner::getBigAllocatorReservation(
+        true, maxHits, MAX_READ_LENGTH, idx->getSeedLength(), numSeeds, 0));
+    BaseAligner *ba = new (al) BaseAligner(idx, maxHits, maxK, MAX_READ_LENGTH, numSeeds, 0, extra,
+                                           NULL, NULL, NULL, al);
+    std::ifstream in(argv[3]);
+    std::string id, bases, plus, quals;
+    unsigned i = 0;
+    char b1[64], b2[64];
+    while (std::getline(in, id) && std::getline(in, bases) && std::getline(in, plus) && std::getline(in, quals)) {
+        std::string b = bases + std::string(16, '\0');   // LV reads up to 8 bytes past the end
+        std::string q = quals + std::string(16, '\0');
+        Read r;
+        r.init(id.c_str() + 1, (unsigned)id.size() - 1, b.c_str(), q.c_str(), (unsigned)bases.size());
+        unsigned loc = 0; Direction dir = 0; int score = 0, mapq = 0;
+        _int64 l0 = ba->getNHashTableLookups(), s0 = ba->getLocationsScored();
+        ba->popularSeedsSkipped = 0;
+        ba->probabilityOfAllCandidates = 0; ba->probabilityOfBestCandidate = 0;
+        AlignmentResult res = ba->AlignRead(&r, &loc, &dir, &score, &mapq);
+        hexd(ba->probabilityOfAllCandidates, b1);
+        hexd(ba->probabilityOfBestCandidate, b2);
+        printf("%u\t%d\t%u\t%d\t%d\t%d\t%lld\t%lld\t%u\t%s\t%s\n", i, (int)res, loc, dir, score, mapq,
+               (long long)(ba->getNHashTableLookups() - l0), (long long)(ba->getLocationsScored() - s0),
+               ba->popularSeedsSkipped, b1, b2);
+        i++;
+    }
+    return 0;
+}
+
+static int mode_lv(int argc, char **argv) {
+    if (argc < 3) { fprintf(stderr, "lv <calls.tsv>\n"); return 2; }
+    initializeLVProbabilitiesToPhredPlus33();
+    LandauVishkin<1> *fwd = new LandauVishkin<1>;
+    LandauVishkin<-1> *rev = new LandauVishkin<-1>;
+    std::ifstream in(argv[2]);
+    std::string line;
+    while (std::getline(in, line)) {
+        std::istringstream ss(line);
+        int dir, k; std::string text, pattern, quals;
+        ss >> dir >> k >> text >> pattern >> quals;
+        // Reverse text is walked backwards from its END (LandauVishkin.h:261-263): put
+        // the text in a padded buffer and pass a pointer one past its last byte.
+        std::string tbuf = std::string(64, 'n') + text + std::string(64, 'n');
+        std::string pbuf = pattern + std::string(16, '\0');
+        std::string qbuf = quals + std::string(16, '\0');
+        double p = 0; int indel = 0; int e;
+        if (dir >= 0) e = fwd->computeEditDistance(tbuf.c_str() + 64, (int)text.size(), pbuf.c_str(), qbuf.c_str(),
+                                                    (int)pattern.size(), k, &p, 0, &indel);
+        else e = rev->computeEditDistance(tbuf.c_str() + 64 + text.size(), (int)text.size(), pbuf.c_str(), qbuf.c_str(),
+                                          (int)pattern.size(), k, &p, 0, &indel);
+        char b[64]; hexd(p, b);
+        printf("%d\t%d\t%s\n", e, indel, b);
+    }
+    return 0;
+}
+
+static int mode_lookup(int argc, char **argv) {
+    if (argc < 4) { fprintf(stderr, "lookup <indexDir> <seeds.txt>\n"); return 2; }
+    GenomeIndex *idx = GenomeIndex::loadFromDirectory(argv[2]);
+    if (!idx) return 1;
+    std::ifstream in(argv[3]);
+    std::string s;
+    while (std::getline(in, s)) {
+        Seed seed(s.c_str(), idx->getSeedLength());
+        unsigned n[2]; const unsigned *h[2];
+        idx->lookupSeed(seed, &n[0], &h[0], &n[1], &h[1]);
+        unsigned long long sum[2] = {0, 0}; long long first[2] = {-1, -1};
+        for (int d = 0; d < 2; d++) {
+            for (unsigned j = 0; j < n[d]; j++) sum[d] = sum[d] * 1000003ULL + h[d][j];
+            if (n[d]) first[d] = h[d][0];
+        }
+        printf("%u\t%u\t%llu\t%llu\t%lld\t%lld\n", n[0], n[1], sum[0], sum[1], first[0], first[1]);
+    }
+    return 0;
+}
+
+int main(int argc, char **argv) {
+    if (argc < 2) { fprintf(stderr, "usage: ref_harness align|lv|lookup ...\n"); return 2; }
+    std::string m = argv[1];
+    if (m == "align") return mode_align(argc, argv);
+    if (m == "lv") return mode_lv(argc, argv);
+    if (m == "lookup") return mode_lookup(argc, argv);
+    fprintf(stderr, "unknown mode %s\n", argv[1]);
+    return 2;
+}

@@ -1,0 +1,665 @@
+/*
+ * snap_oracle.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * A plain-C, single-threaded-per-aligner restatement of the reference hot path
+ *   BaseAligner::AlignRead        (SNAPLib/BaseAligner.cpp:510-938)
+ *   BaseAligner::score            (SNAPLib/BaseAligner.cpp:977-1399)
+ *   LandauVishkin<+-1>::computeEditDistance (SNAPLib/LandauVishkin.h:211-455)
+ *   GenomeIndex::lookupSeed       (SNAPLib/GenomeIndex.cpp:971-1086)
+ *   SNAPHashTable::Lookup         (SNAPLib/HashTable.h:74-105)
+ *   computeMAPQ                   (SNAPLib/mapq.h:32-65)
+ * used ONLY as the parity checker by tests/, __graft_entry__.smoke() and as the
+ * `cpu_baseline` leg of bench.py.  The product path (snap-rnaseq_amd/) never
+ * links or calls it.  Parity of this restatement is pinned against the
+ * reference itself (oracle/_ref, built from /root/reference by
+ * oracle/Makefile.ref) and the golden fixtures under tests/golden/.
+ *
+ * Data structures are deliberately different from both the reference (chained
+ * anchors with epochs) and the GPU path (timestamped LDS arena): candidate
+ * elements live in an open-addressed map keyed by (direction, 48-aligned
+ * location) and the weight lists are explicit circular doubly-linked lists, the
+ * FIFO order of the reference.
+ *
+ * Build: gcc -O2 -ffp-contract=off -fPIC -shared (oracle/Makefile).
+ */
+#include <math.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "snapgpu.h"
+
+#define MAX_K 31                 /* LandauVishkin.h:9 */
+#define MAX_READ_LENGTH 500      /* Read.h:45 */
+#define ELEM_SIZE 48             /* BaseAligner.h:163,196 maxMergeDist == hashTableElementSize */
+#define UNUSED_SCORE 0xffffu     /* BaseAligner.h:261 */
+#define INVALID_LOC 0xffffffffu  /* Genome.h:29 */
+#define N_PADDING 100u           /* Genome.h:175 */
+#define SNP_PROB 0.001           /* BaseAligner.h:264-266 */
+#define GAP_OPEN_PROB 0.001
+#define GAP_EXTEND_PROB 0.5
+#define MAPQ_LIMIT_FOR_SINGLE_HIT 10   /* AlignerOptions.h:34 */
+
+/* ---------------------------------------------------------------- tables */
+/* initializeLVProbabilitiesToPhredPlus33 (LandauVishkin.cpp:601-649) */
+static double g_indel[64];
+static double g_phred[256];
+static double g_perfect[MAX_READ_LENGTH + 1];
+static double g_seedProb[33];    /* pow(1 - SNP_PROB, seedLen), BaseAligner.cpp:1227 */
+static pthread_once_t g_once = PTHREAD_ONCE_INIT;
+
+/* BaseAligner.cpp:1227 calls pow(double, int) with an `int seedLen`
+ * (BaseAligner.cpp:1200).  The reference is C++98, where
+ * libstdc++'s std::pow(double, int) is __builtin_powi, i.e. libgcc's __powidf2:
+ * binary exponentiation by squaring -- NOT libm pow.  Restated here. */
+static double powi_libgcc(double x, int m) {
+    unsigned n = m < 0 ? -(unsigned)m : (unsigned)m;
+    double y = (n % 2) ? x : 1;
+    while (n >>= 1) {
+        x = x * x;
+        if (n % 2) y = y * x;
+    }
+    return m < 0 ? 1 / y : y;
+}
+
+static void init_tables(void) {
+    g_indel[0] = 1.0;
+    g_indel[1] = GAP_OPEN_PROB;
+    for (int i = 2; i < 64; i++) g_indel[i] = g_indel[i - 1] * GAP_EXTEND_PROB;
+    for (int i = 0; i < 33; i++) g_phred[i] = SNP_PROB;
+    for (int i = 33; i <= 93 + 33; i++) g_phred[i] = 1.0 - (1.0 - pow(10.0, -1.0 * (i - 33.0) / 10.0)) * (1.0 - SNP_PROB);
+    for (int i = 93 + 33 + 1; i < 256; i++) g_phred[i] = SNP_PROB;
+    g_perfect[0] = 1.0;
+    for (int i = 1; i <= MAX_READ_LENGTH; i++) g_perfect[i] = g_perfect[i - 1] * (1 - SNP_PROB);
+    for (int i = 0; i < 33; i++) g_seedProb[i] = powi_libgcc(1 - SNP_PROB, i);
+}
+
+/* computeMAPQ, mapq.h:32-65 */
+int oracle_compute_mapq(double pAll, double pBest, int score, int popular) {
+    if (pAll < pBest) pAll = pBest;
+    if (pAll == pBest && popular == 0 && score < 5) return 70;
+    double c = pBest / pAll;
+    int base;
+    if (c >= 1) base = 69;
+    else {
+        base = (int)(-10 * log10(1 - c));
+        if (base > 69) base = 69;
+    }
+    int pen = popular - 10;
+    if (pen < 0) pen = 0;
+    base -= pen / 2;
+    return base < 0 ? 0 : base;
+}
+
+/* --------------------------------------------------------- Landau-Vishkin */
+/* Text accessor: forward texts are read ascending from `text`; reverse texts are
+ * read descending from text[-1] (LandauVishkin.h:261-263, 326, 336). */
+static inline char lv_t(const char *text, int dir, int j) { return dir > 0 ? text[j] : text[-1 - j]; }
+
+/* LandauVishkin<dir>::computeEditDistance, LandauVishkin.h:211-455.  The 8-byte
+ * XOR/ctz match extension is restated byte-wise: the reference clips every
+ * extension with min(., end), so the bytes it over-reads past `end` only matter
+ * through the `*p == *t` pre-test when best > end (kept below). */
+int oracle_lv(int dir, const char *text, int textLen, const char *pattern, const char *qual,
+              int patternLen, int k, double *prob, int *netIndel) {
+    pthread_once(&g_once, init_tables);
+    int L[MAX_K + 1][2 * MAX_K + 1];
+    char A[MAX_K + 1][2 * MAX_K + 1];
+    for (int e = 0; e <= MAX_K; e++)
+        for (int d = 0; d < 2 * MAX_K + 1; d++) L[e][d] = -2;   /* LandauVishkin.h:168 */
+    *netIndel = 0;
+    if (k > MAX_K - 1) k = MAX_K - 1;
+    if (!text) { *prob = 0.0; return -1; }
+    *prob = 1.0;
+    int end = patternLen < textLen ? patternLen : textLen;
+    int i = 0;
+    while (i < end && pattern[i] == lv_t(text, dir, i)) i++;
+    L[0][MAX_K] = i;
+    if (i == end) {
+        int result = patternLen > end ? patternLen - end : 0;
+        *prob = g_perfect[patternLen];
+        return result > k ? -1 : result;
+    }
+    for (int e = 1; e <= k; e++) {
+        /* d order 0, 1, -1, 2, -2, ... (LandauVishkin.h:180-182, 311) */
+        for (int j = 0; j < 2 * e + 1; j++) {
+            int d = (j == 0) ? 0 : ((j & 1) ? (j + 1) / 2 : -(j / 2));
+            int best = L[e - 1][MAX_K + d] + 1;
+            char act = 'X';
+            int left = L[e - 1][MAX_K + d - 1];
+            if (left > best) { best = left; act = 'D'; }
+            int right = L[e - 1][MAX_K + d + 1] + 1;
+            if (right > best) { best = right; act = 'I'; }
+            A[e][MAX_K + d] = act;
+            int endd = patternLen < textLen - d ? patternLen : textLen - d;
+            if (pattern[best] == lv_t(text, dir, best + d)) {
+                if (best < endd) {
+                    int m = best + 1;
+                    while (m < endd && pattern[m] == lv_t(text, dir, m + d)) m++;
+                    best = m;
+                } else {
+                    best = endd;
+                }
+            }
+            if (best == patternLen) {
+                /* backtrace (LandauVishkin.h:376-431) */
+                char bAct[MAX_K + 1];
+                int bMatched[MAX_K + 1];
+                L[e][MAX_K + d] = best;
+                int curD = d;
+                for (int ce = e; ce >= 1; ce--) {
+                    char a = A[ce][MAX_K + curD];
+                    bAct[ce] = a;
+                    int src;
+                    if (a == 'I') { src = curD + 1; bMatched[ce] = L[ce][MAX_K + curD] - L[ce - 1][MAX_K + src] - 1; }
+                    else if (a == 'D') { src = curD - 1; bMatched[ce] = L[ce][MAX_K + curD] - L[ce - 1][MAX_K + src]; }
+                    else { src = curD; bMatched[ce] = L[ce][MAX_K + curD] - L[ce - 1][MAX_K + src] - 1; }
+                    curD = src;
+                }
+                double p = 1.0;
+                int ce = 1, offset = L[0][MAX_K];
+                while (ce <= e) {
+                    char a = bAct[ce];
+                    int cnt = 1;
+                    while (ce + 1 <= e && bMatched[ce] == 0 && bAct[ce + 1] == a) { cnt++; ce++; }
+                    if (a == 'I') { p *= g_indel[cnt]; offset += cnt; *netIndel += cnt; }
+                    else if (a == 'D') { p *= g_indel[cnt]; offset -= cnt; *netIndel -= cnt; }
+                    else {
+                        for (int r = 0; r < cnt; r++) {
+                            int qi = offset < 0 ? 0 : offset;
+                            if (qi > patternLen - 1) qi = patternLen - 1;
+                            p *= g_phred[(unsigned char)qual[qi]];
+                            offset++;
+                        }
+                    }
+                    offset += bMatched[ce];
+                    ce++;
+                }
+                p *= g_perfect[patternLen - e];
+                *prob = p;
+                return e;
+            }
+            L[e][MAX_K + d] = best;
+        }
+    }
+    return -1;
+}
+
+/* ------------------------------------------------------------ index view */
+static inline uint32_t fmix32(uint32_t k) {   /* HashTable.h:60-72 */
+    k ^= k >> 16; k *= 0x85ebca6bu; k ^= k >> 13; k *= 0xc2b2ae35u; k ^= k >> 16;
+    return k;
+}
+
+/* SNAPHashTable::Lookup, HashTable.h:74-105 -> pointer to value1 or NULL */
+static const uint32_t *ht_lookup(const snapgpu_index_view_t *v, uint32_t table, uint32_t key, uint32_t *probes) {
+    uint64_t size = v->tableSize[table];
+    const uint32_t *t = v->slots + 3 * v->tableBase[table];
+    uint64_t i = fmix32(key) % size;
+    *probes += 1;
+    if (t[3 * i] == key && t[3 * i + 1] != INVALID_LOC) return t + 3 * i + 1;
+    uint64_t n = 0;
+    for (;;) {
+        n++;
+        if (n > size + 5) return NULL;
+        i = (n < 5) ? (i + n * n) % size : (i + 1) % size;
+        *probes += 1;
+        if (t[3 * i] == key || t[3 * i + 1] == INVALID_LOC) break;
+    }
+    return t[3 * i + 1] == INVALID_LOC ? NULL : t + 3 * i + 1;
+}
+
+/* ------------------------------------------------------------- aligner */
+typedef struct Elem {
+    struct Elem *wnext, *wprev;
+    uint64_t used, scored;
+    uint32_t base, weight, lps, bestScore, bestLoc;
+    int dir, allScored;
+    double prob;
+    int seedOffset[ELEM_SIZE];
+} Elem;
+
+typedef struct {
+    uint32_t key;     /* (base/48) << 1 | dir, +1 so that 0 is empty */
+    uint32_t epoch;
+    Elem *elem;
+} Slot;
+
+typedef struct {
+    const snapgpu_index_view_t *ix;
+    snapgpu_aligner_params_t p;
+    unsigned maxSeedsFromCmd, numWeightLists;
+    Elem *pool; unsigned poolSize, nUsed;
+    Slot *map; unsigned mapMask; uint32_t epoch;
+    Elem *lists;                      /* sentinels [numWeightLists] */
+    /* read buffers (+32 bytes of zero slack: LV over-reads, LandauVishkin.h:271) */
+    char fwd[MAX_READ_LENGTH + 32], fwdQ[MAX_READ_LENGTH + 32];
+    char rc[MAX_READ_LENGTH + 32], rcQ[MAX_READ_LENGTH + 32];
+    char rev[2][MAX_READ_LENGTH + 32];
+    uint8_t seedUsed[(MAX_READ_LENGTH + 7) / 8 + 8];
+    /* per-read state, BaseAligner.h:273-289 */
+    unsigned lps[2], mostSeeds[2], nSeedsApplied[2];
+    unsigned bestScore, bestLoc, scoreLimit, popular;
+    double pAll, pBest;
+    snapgpu_result_t *out;
+} Oracle;
+
+static inline int base_value(char c) {   /* Tables.cpp:41-48 */
+    switch (c) { case 'A': return 0; case 'G': return 1; case 'C': return 2; case 'T': return 3; default: return 4; }
+}
+
+static Elem *find_elem(Oracle *o, uint32_t loc, int dir) {   /* findElement, BaseAligner.cpp:1415-1442 */
+    uint32_t base = loc - loc % ELEM_SIZE;
+    uint32_t key = ((base / ELEM_SIZE) << 1 | (uint32_t)dir) + 1;
+    uint32_t h = (key * 2654435761u) & o->mapMask;
+    for (;;) {
+        Slot *s = &o->map[h];
+        if (s->epoch != o->epoch) return NULL;
+        if (s->key == key) return s->elem;
+        h = (h + 1) & o->mapMask;
+    }
+}
+
+static void map_insert(Oracle *o, Elem *e) {
+    uint32_t key = ((e->base / ELEM_SIZE) << 1 | (uint32_t)e->dir) + 1;
+    uint32_t h = (key * 2654435761u) & o->mapMask;
+    while (o->map[h].epoch == o->epoch) h = (h + 1) & o->mapMask;
+    o->map[h].epoch = o->epoch; o->map[h].key = key; o->map[h].elem = e;
+}
+
+static inline void list_unlink(Elem *e) { e->wnext->wprev = e->wprev; e->wprev->wnext = e->wnext; }
+static inline void list_append(Elem *sentinel, Elem *e) {
+    e->wnext = sentinel; e->wprev = sentinel->wprev; e->wnext->wprev = e; e->wprev->wnext = e;
+}
+
+/* incrementWeight, BaseAligner.cpp:1689-1727 */
+static void increment_weight(Oracle *o, Elem *e) {
+    if (e->allScored) return;
+    if (e->weight >= o->numWeightLists - 1) return;
+    list_unlink(e);
+    e->weight++;
+    list_append(&o->lists[e->weight], e);
+}
+
+/* Genome::getSubstring, Genome.h:78-148 */
+static const char *get_substring(const snapgpu_index_view_t *v, uint32_t offset, uint32_t len) {
+    if (offset > v->nBases || (uint64_t)offset + len > (uint64_t)v->nBases + N_PADDING) return NULL;
+    if (len <= v->chromosomePadding) return v->genome + offset;
+    if (v->nPieces > 100) {
+        if (v->pieceOffsets[v->nPieces - 1] <= offset) return v->genome + offset;
+        int lo = 0, hi = v->nPieces - 2;
+        while (lo <= hi) {
+            int m = (lo + hi) / 2;
+            if (v->pieceOffsets[m] <= offset) {
+                if (v->pieceOffsets[m + 1] > offset)
+                    return v->pieceOffsets[m + 1] <= offset + len - 1 ? NULL : v->genome + offset;
+                lo = m + 1;
+            } else hi = m - 1;
+        }
+        return NULL;
+    }
+    for (int i = 0; i < v->nPieces; i++)
+        if (offset + len - 1 >= v->pieceOffsets[i]) return offset < v->pieceOffsets[i] ? NULL : v->genome + offset;
+    return NULL;
+}
+
+static int next_piece_after(const snapgpu_index_view_t *v, uint32_t loc) {  /* Genome.cpp:376-401 */
+    int lo = 0, hi = v->nPieces - 1;
+    while (lo <= hi) {
+        int m = (lo + hi) / 2;
+        if (v->pieceOffsets[m] <= loc && (m == v->nPieces - 1 || v->pieceOffsets[m + 1] > loc))
+            return m >= v->nPieces - 1 ? -1 : m + 1;
+        else if (v->pieceOffsets[m] <= loc) lo = m + 1;
+        else hi = m - 1;
+    }
+    return -1;
+}
+
+/* BaseAligner::score, BaseAligner.cpp:977-1399.  Returns 1 iff a result was reached. */
+static int score(Oracle *o, int force, unsigned readLen, int *result) {
+    snapgpu_result_t *out = o->out;
+    const unsigned seedLen = o->ix->seedLen;
+    for (int d = 0; d < 2; d++)
+        if (o->mostSeeds[d]) {
+            unsigned v = o->nSeedsApplied[d] / o->mostSeeds[d];
+            if (v > o->lps[d]) o->lps[d] = v;
+        }
+    unsigned w = o->numWeightLists - 1;
+    do {
+        while (w > 0 && o->lists[w].wnext == &o->lists[w]) w--;
+        unsigned minLps = o->lps[0] < o->lps[1] ? o->lps[0] : o->lps[1];
+        if (minLps > o->scoreLimit || force) {
+            if (w == 0) {
+                out->score = (int)o->bestScore;
+                if (o->bestScore <= o->p.maxK) {
+                    out->location = o->bestLoc;
+                    out->mapq = oracle_compute_mapq(o->pAll, o->pBest, (int)o->bestScore, (int)o->popular);
+                    *result = out->mapq >= MAPQ_LIMIT_FOR_SINGLE_HIT ? SNAPGPU_SINGLE_HIT : SNAPGPU_MULTIPLE_HITS;
+                } else {
+                    *result = (o->nSeedsApplied[0] == 0 && o->nSeedsApplied[1] == 0) ? SNAPGPU_MULTIPLE_HITS : SNAPGPU_NOT_FOUND;
+                    out->mapq = 0;
+                }
+                return 1;
+            }
+            force = 1;
+        } else if (w == 0) {
+            return 0;
+        }
+        Elem *el = o->lists[w].wnext;
+        if (el->lps <= o->scoreLimit) {
+            uint64_t mask = el->used;
+            while (mask) {
+                unsigned bit = (unsigned)__builtin_ctzll(mask);
+                uint64_t cbit = 1ull << bit;
+                mask &= ~cbit;
+                if (el->scored & cbit) continue;
+                int anyNearby = el->scored != 0;
+                el->scored |= cbit;
+                uint32_t loc = el->base + bit;
+                uint32_t elemLoc = loc;
+                unsigned sc = 0xffffffffu;
+                double prob = 0;
+                const char *data = get_substring(o->ix, loc, readLen + MAX_K);
+                unsigned gLen = readLen + MAX_K;
+                if (!data) {   /* BaseAligner.cpp:1163-1185 */
+                    uint32_t endOffset;
+                    int np = -1;
+                    if ((uint64_t)loc + readLen + MAX_K >= o->ix->nBases) endOffset = o->ix->nBases;
+                    else { np = next_piece_after(o->ix, loc); endOffset = np >= 0 ? o->ix->pieceOffsets[np] : 0; }
+                    if (np >= 0 || endOffset == o->ix->nBases) {
+                        gLen = endOffset - loc - 1;
+                        if (gLen >= readLen - (unsigned)MAX_K) data = get_substring(o->ix, loc, gLen);
+                    }
+                }
+                if (data) {
+                    const char *rd = el->dir ? o->rc : o->fwd;
+                    const char *rq = el->dir ? o->rcQ : o->fwdQ;
+                    const char *oppQ = el->dir ? o->fwdQ : o->rcQ;
+                    int s = el->seedOffset[bit];
+                    int tail = s + (int)seedLen;
+                    double p1, p2; int ni1, ni2;
+                    int s1 = oracle_lv(1, data + tail, (int)gLen - tail, rd + tail, rq + tail, (int)readLen - tail,
+                                       (int)o->scoreLimit, &p1, &ni1);
+                    if (s1 != -1) {
+                        int limitLeft = (int)o->scoreLimit - s1;
+                        int s2 = oracle_lv(-1, data + s, s + MAX_K, o->rev[el->dir] + readLen - s, oppQ + readLen - s, s,
+                                           limitLeft, &p2, &ni2);
+                        if (s2 != -1) {
+                            sc = (unsigned)(s1 + s2);
+                            prob = p1 * p2 * g_seedProb[seedLen];
+                            loc += (uint32_t)ni2;
+                        }
+                    }
+                }
+                out->nLocationsScored++;
+                if (anyNearby) {
+                    if (el->bestScore < sc || (el->bestScore == sc && prob <= el->prob)) continue;
+                }
+                el->bestLoc = loc;
+                Elem *nb = NULL;
+                if (sc != 0xffffffffu) {
+                    uint32_t nl = elemLoc + (2 * (elemLoc % ELEM_SIZE / (ELEM_SIZE / 2)) - 1) * (ELEM_SIZE / 2);
+                    nb = find_elem(o, nl, el->dir);
+                }
+                if (nb && nb->scored != 0) {
+                    if (!((nb->base > el->base && loc - nb->bestLoc <= ELEM_SIZE) ||
+                          (nb->base < el->base && nb->bestLoc <= ELEM_SIZE)))   /* sic, BaseAligner.cpp:1311-1312 */
+                        nb = NULL;
+                    if (nb) {
+                        if (nb->bestScore < sc || (nb->bestScore == sc && nb->prob >= prob)) continue;
+                        anyNearby = 1;
+                        o->pAll = o->pAll - nb->prob > 0.0 ? o->pAll - nb->prob : 0.0;
+                        nb->prob = 0;
+                    }
+                }
+                o->pAll = o->pAll - el->prob > 0.0 ? o->pAll - el->prob : 0.0;
+                o->pAll += prob;
+                el->prob = prob;
+                el->bestScore = sc;
+                if (o->bestScore > sc || (o->bestScore == sc && prob > o->pBest)) {
+                    o->bestScore = sc;
+                    o->pBest = prob;
+                    o->bestLoc = loc;
+                    out->location = loc;
+                    out->score = (int)sc;
+                    out->direction = (uint8_t)el->dir;
+                }
+                if (o->p.stopOnFirstHit && o->bestScore <= o->p.maxK) {
+                    *result = SNAPGPU_MULTIPLE_HITS;
+                    out->mapq = 0;
+                    return 1;
+                }
+                o->scoreLimit = (o->bestScore < o->p.maxK ? o->bestScore : o->p.maxK) + o->p.extraSearchDepth;
+            }
+        }
+        el->allScored = 1;
+        list_unlink(el);
+        el->wnext = el->wprev = el;
+    } while (force);
+    return 0;
+}
+
+/* SeedSequencer.h:28-287, GetWrappedNextSeedToTest: the wrap order per seed length. */
+static const unsigned char kWrap[10][25] = {
+    /* 16 */ {0, 8, 4, 12, 2, 6, 10, 14, 1, 3, 5, 7, 9, 11, 13, 15},
+    /* 17 */ {0, 8, 4, 12, 2, 6, 10, 14, 1, 3, 5, 7, 9, 11, 13, 15, 16},
+    /* 18 */ {0, 9, 4, 13, 2, 6, 11, 15, 1, 3, 5, 7, 8, 10, 12, 14, 16, 17},
+    /* 19 */ {0, 10, 4, 14, 2, 6, 8, 12, 16, 18, 1, 3, 5, 7, 9, 11, 13, 15, 17},
+    /* 20 */ {0, 10, 5, 15, 2, 7, 12, 17, 3, 9, 11, 13, 19, 1, 4, 6, 8, 14, 18, 16},
+    /* 21 */ {0, 11, 6, 16, 3, 9, 13, 17, 18, 2, 5, 8, 15, 20, 1, 4, 7, 10, 12, 14, 19},
+    /* 22 */ {0, 11, 6, 16, 3, 9, 14, 19, 2, 7, 12, 17, 20, 4, 1, 10, 13, 15, 18, 21, 5, 8},
+    /* 23 */ {0, 12, 6, 17, 3, 9, 20, 14, 1, 4, 7, 10, 15, 18, 21, 4, 2, 5, 11, 16, 19, 22, 8},
+    /* 24 */ {0, 12, 6, 18, 3, 15, 21, 9, 1, 13, 19, 7, 16, 4, 22, 10, 2, 14, 20, 5, 17, 8, 23, 11},
+    /* 25 */ {0, 13, 6, 19, 3, 16, 22, 9, 11, 1, 14, 7, 20, 4, 17, 23, 2, 15, 5, 21, 8, 24, 10, 18, 12},
+};
+static unsigned wrapped_next_seed(unsigned seedLen, unsigned wrapCount) {
+    return kWrap[seedLen - 16][wrapCount];
+}
+
+/* BaseAligner::AlignRead, BaseAligner.cpp:510-938 (searchRadius == 0, maxHitsToGet == 0) */
+static void align_read(Oracle *o, const char *bases, const char *quals, unsigned readLen, snapgpu_result_t *out) {
+    const snapgpu_index_view_t *ix = o->ix;
+    const unsigned seedLen = ix->seedLen;
+    memset(out, 0, sizeof(*out));
+    o->out = out;
+    unsigned maxSeeds = o->maxSeedsFromCmd ? o->maxSeedsFromCmd
+                                           : (unsigned)(int)(o->p.maxSeedCoverage * readLen / seedLen);
+    out->location = INVALID_LOC;
+    out->direction = SNAPGPU_FORWARD;
+    out->score = (int)UNUSED_SCORE;
+    o->popular = 0;
+    o->pAll = o->pBest = 0;
+    if (readLen > o->p.maxReadSize) { out->flags |= SNAPGPU_FLAG_READ_TOO_LONG; out->result = SNAPGPU_NOT_FOUND; return; }
+    if ((int)readLen < (int)seedLen) { out->result = SNAPGPU_NOT_FOUND; return; }
+    /* Read::init upper-cases (Read.h:303-325); RC / reversed copies (BaseAligner.cpp:636-650) */
+    unsigned countOfNs = 0;
+    for (unsigned i = 0; i < readLen; i++) {
+        char c = bases[i];
+        if (c >= 'a' && c <= 'z') c = (char)(c - 0x20);
+        char comp = c == 'A' ? 'T' : c == 'G' ? 'C' : c == 'C' ? 'G' : c == 'T' ? 'A' : c == 'N' ? 'N' : 0;
+        o->fwd[i] = c; o->fwdQ[i] = quals[i];
+        o->rc[readLen - i - 1] = comp; o->rcQ[readLen - i - 1] = quals[i];
+        o->rev[0][readLen - i - 1] = c;
+        o->rev[1][i] = comp;
+        countOfNs += c == 'N';
+    }
+    memset(o->fwd + readLen, 0, 32); memset(o->fwdQ + readLen, 0, 32);
+    memset(o->rc + readLen, 0, 32); memset(o->rcQ + readLen, 0, 32);
+    memset(o->rev[0] + readLen, 0, 32); memset(o->rev[1] + readLen, 0, 32);
+    if (countOfNs > o->p.maxK) { out->flags |= SNAPGPU_FLAG_TOO_MANY_NS; out->result = SNAPGPU_NOT_FOUND; return; }
+    /* clearCandidates, BaseAligner.cpp:1679-1687 */
+    o->epoch++;
+    o->nUsed = 0;
+    for (unsigned i = 1; i < o->numWeightLists; i++) o->lists[i].wnext = o->lists[i].wprev = &o->lists[i];
+    memset(o->seedUsed, 0, sizeof(o->seedUsed));
+    unsigned nPossible = readLen - seedLen + 1, next = 0, wrapCount = 0;
+    o->lps[0] = o->lps[1] = 0;
+    o->mostSeeds[0] = o->mostSeeds[1] = 1;
+    o->bestScore = UNUSED_SCORE;
+    o->nSeedsApplied[0] = o->nSeedsApplied[1] = 0;
+    o->scoreLimit = o->p.maxK + o->p.extraSearchDepth;
+    int result = SNAPGPU_NOT_FOUND;
+    while (o->nSeedsApplied[0] + o->nSeedsApplied[1] < maxSeeds) {
+        if (next >= nPossible) {
+            wrapCount++;
+            if (wrapCount >= seedLen) {
+                score(o, 1, readLen, &result);
+                goto finish;
+            }
+            next = wrapped_next_seed(seedLen, wrapCount);
+            o->mostSeeds[0] = o->mostSeeds[1] = wrapCount + 1;
+        }
+        while (next < nPossible && (o->seedUsed[next / 8] & (1 << (next % 8)))) next++;
+        if (next >= nPossible) continue;
+        o->seedUsed[next / 8] |= (uint8_t)(1 << (next % 8));
+        /* Seed::DoesTextRepresentASeed + Seed::Seed (Seed.cpp:28-42, Seed.h:38-51) */
+        uint64_t f = 0, r = 0;
+        int valid = 1;
+        for (unsigned i = 0; i < seedLen; i++) {
+            int v = base_value(o->fwd[next + i]);
+            if (v > 3) { valid = 0; break; }
+            f |= (uint64_t)v << ((seedLen - i - 1) * 2);
+            r |= (uint64_t)(v ^ 3) << (i * 2);
+        }
+        if (!valid) continue;
+        /* GenomeIndex::lookupSeed, GenomeIndex.cpp:971-1011 */
+        unsigned nHits[2] = {0, 0};
+        const uint32_t *hits[2] = {NULL, NULL};
+        uint32_t singleton[2];
+        int comp = (int64_t)f > (int64_t)r;
+        uint64_t canon = comp ? r : f;
+        const uint32_t *e = ht_lookup(ix, (uint32_t)(canon >> 32), (uint32_t)canon, &out->nProbes);
+        if (e) {
+            for (int side = 0; side < 2; side++) {
+                uint32_t v = (side == 0) == !comp ? e[0] : e[1];   /* fwd: value1 unless complemented */
+                if (side == 1 && f == r) { nHits[1] = nHits[0]; hits[1] = hits[0]; break; }
+                if (v < ix->nBases) { singleton[side] = v; nHits[side] = 1; hits[side] = &singleton[side]; }
+                else if (v == 0xfffffffeu) nHits[side] = 0;
+                else {
+                    uint32_t off = v - ix->nBases;
+                    nHits[side] = ix->overflow[off];
+                    hits[side] = ix->overflow + off + 1;
+                    out->nOverflowLists++;
+                }
+            }
+        }
+        out->nLookups++;
+        int applied = 0;
+        for (int dir = 0; dir < 2; dir++) {
+            if (nHits[dir] > o->p.maxHitsToConsider && !o->p.explorePopularSeeds) {
+                out->nHitsIgnored++;
+                o->popular++;
+            } else {
+                unsigned offset = dir == 0 ? next : readLen - seedLen - next;
+                unsigned lim = nHits[dir] < o->p.maxHitsToConsider ? nHits[dir] : o->p.maxHitsToConsider;
+                out->nHitWords += lim;
+                for (unsigned i = 0; i < lim; i++) {
+                    uint32_t h = hits[dir][i];
+                    uint32_t loc = h - offset;
+                    if (h < offset) continue;
+                    Elem *el = find_elem(o, loc, dir);
+                    unsigned bit = loc % ELEM_SIZE;
+                    if (el) {
+                        /* findCandidate (BaseAligner.cpp:1474-1479) then incrementWeight */
+                        uint64_t cb = 1ull << bit;
+                        el->allScored = el->allScored && (el->used & cb);
+                        el->used |= cb;
+                        increment_weight(o, el);
+                        el->seedOffset[bit] = (int)offset;
+                    } else if (o->lps[dir] <= o->scoreLimit) {
+                        /* allocateNewCandidate, BaseAligner.cpp:1485-1568 */
+                        el = &o->pool[o->nUsed++];
+                        el->used = 1ull << bit;
+                        el->scored = 0;
+                        el->lps = o->lps[dir];
+                        el->dir = dir;
+                        el->weight = 1;
+                        el->base = loc - bit;
+                        el->bestScore = UNUSED_SCORE;
+                        el->allScored = 0;
+                        el->prob = 0;
+                        list_append(&o->lists[1], el);
+                        el->seedOffset[bit] = (int)offset;
+                        map_insert(o, el);
+                    }
+                }
+                o->nSeedsApplied[dir]++;
+                applied = 1;
+            }
+        }
+        next += seedLen;
+        if (applied && score(o, 0, readLen, &result)) goto finish;
+    }
+    score(o, 1, readLen, &result);
+finish:
+    out->result = (uint8_t)result;
+    out->popularSeedsSkipped = (uint16_t)o->popular;
+    out->probabilityOfAllCandidates = o->pAll;
+    out->probabilityOfBestCandidate = o->pBest;
+}
+
+static Oracle *oracle_new(const snapgpu_index_view_t *ix, const snapgpu_aligner_params_t *p) {
+    pthread_once(&g_once, init_tables);
+    Oracle *o = (Oracle *)calloc(1, sizeof(Oracle));
+    o->ix = ix;
+    o->p = *p;
+    o->maxSeedsFromCmd = p->maxSeedsToUse;
+    unsigned maxSeeds = p->maxSeedsToUse ? p->maxSeedsToUse
+                                         : (unsigned)(int)(p->maxSeedCoverage * p->maxReadSize / ix->seedLen);
+    o->numWeightLists = maxSeeds + 1;   /* BaseAligner.cpp:120-127 */
+    o->poolSize = p->maxHitsToConsider * maxSeeds * 2 + 2 * p->maxHitsToConsider + 64;
+    o->pool = (Elem *)calloc(o->poolSize, sizeof(Elem));
+    unsigned m = 1;
+    while (m < 2 * o->poolSize) m <<= 1;
+    o->map = (Slot *)calloc(m, sizeof(Slot));
+    o->mapMask = m - 1;
+    o->lists = (Elem *)calloc(o->numWeightLists + 1, sizeof(Elem));
+    for (unsigned i = 0; i <= o->numWeightLists; i++) o->lists[i].wnext = o->lists[i].wprev = &o->lists[i];
+    return o;
+}
+
+static void oracle_delete(Oracle *o) {
+    free(o->pool); free(o->map); free(o->lists); free(o);
+}
+
+typedef struct {
+    const snapgpu_index_view_t *ix;
+    const snapgpu_aligner_params_t *p;
+    const char *bases, *quals;
+    const uint64_t *offsets;
+    const uint32_t *lengths;
+    uint64_t n;
+    snapgpu_result_t *out;
+    volatile uint64_t *cursor;
+} Job;
+
+static void *worker(void *arg) {
+    Job *j = (Job *)arg;
+    Oracle *o = oracle_new(j->ix, j->p);
+    for (;;) {
+        uint64_t b = __atomic_fetch_add(j->cursor, 64, __ATOMIC_RELAXED);
+        if (b >= j->n) break;
+        uint64_t e = b + 64 < j->n ? b + 64 : j->n;
+        for (uint64_t i = b; i < e; i++)
+            align_read(o, j->bases + j->offsets[i], j->quals + j->offsets[i], j->lengths[i], &j->out[i]);
+    }
+    oracle_delete(o);
+    return NULL;
+}
+
+/* Align a batch of reads on `nThreads` host threads (one private aligner each,
+ * as ParallelTask gives each thread its own BaseAligner, ParallelTask.h:127-137). */
+int oracle_align_batch(const snapgpu_index_view_t *ix, const snapgpu_aligner_params_t *p,
+                       const char *bases, const char *quals, const uint64_t *offsets, const uint32_t *lengths,
+                       uint64_t n, snapgpu_result_t *out, int nThreads) {
+    if (ix->seedLen < 16 || ix->seedLen > 25) return -1;
+    if (nThreads < 1) nThreads = 1;
+    volatile uint64_t cursor = 0;
+    Job job = {ix, p, bases, quals, offsets, lengths, n, out, &cursor};
+    pthread_t *th = (pthread_t *)calloc((size_t)nThreads, sizeof(pthread_t));
+    for (int t = 0; t < nThreads; t++) pthread_create(&th[t], NULL, worker, &job);
+    for (int t = 0; t < nThreads; t++) pthread_join(th[t], NULL);
+    free(th);
+    return 0;
+}

@@ -1,0 +1,88 @@
+// internal.h -- host-side data structures behind the opaque handles of include/snapgpu.h.
+#pragma once
+#include "snapgpu.h"
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace snapgpu {
+
+// Guard bytes of 'n' before base 0 and after the last base.  The reference keeps
+// N_PADDING = 100 (Genome.h:175); we keep more so that every device/host window
+// [loc - 64, loc + readLen + 64) stays inside the buffer.
+constexpr uint32_t kGenomeGuard = 256;
+constexpr uint32_t kInvalidLocation = 0xffffffffu;   // InvalidGenomeLocation, Genome.h:29
+constexpr uint32_t kUnusedSide = 0xfffffffeu;        // GenomeIndex.cpp:1511-1518
+constexpr uint32_t kHashMagic = 0xb111b010u;         // HashTable.cpp:298
+constexpr unsigned kQuadraticChainingDepth = 5;      // HashTable.h:115
+
+void setError(const std::string &msg);
+
+struct Genome {
+    std::vector<char> buf;          // guard + bases + guard
+    uint32_t nBases = 0;
+    uint32_t chromosomePadding = 500;
+    std::vector<uint32_t> pieceOffsets;
+    std::vector<std::string> pieceNames;
+    const char *bases() const { return buf.data() + kGenomeGuard; }
+    char *bases() { return buf.data() + kGenomeGuard; }
+    // Append a contig the way ReadFASTAGenome does (FASTA.cpp:93-120): padding,
+    // then the (already upper-cased, N->n) sequence.
+    void reserve(uint64_t n);
+    void startPiece(const std::string &name);
+    void append(const char *data, size_t len);
+    void appendPadding();
+    void finish();                  // trailing padding + guards
+};
+
+struct Index {
+    Genome *genome = nullptr;       // owned
+    uint32_t seedLen = 20;
+    uint32_t nTables = 0;
+    std::vector<uint32_t> slots;    // 3 words per slot: key, value1, value2
+    std::vector<uint64_t> tableBase;
+    std::vector<uint64_t> tableSize;
+    std::vector<uint64_t> tableUsed;
+    std::vector<uint32_t> overflow;
+    bool hasIupac = false;
+    ~Index() { delete genome; }
+};
+
+// SNAPHashTable::hash (HashTable.h:60-72): MurmurHash3 fmix32.
+inline uint32_t hashKey(uint32_t key) {
+    key ^= key >> 16;
+    key *= 0x85ebca6bu;
+    key ^= key >> 13;
+    key *= 0xc2b2ae35u;
+    key ^= key >> 16;
+    return key;
+}
+
+// Base encoding of Tables.cpp:41-48: A=0 G=1 C=2 T=3, anything else invalid (4).
+inline int baseValue(char c) {
+    switch (c) {
+        case 'A': return 0;
+        case 'G': return 1;
+        case 'C': return 2;
+        case 'T': return 3;
+        default: return 4;
+    }
+}
+
+// Host lookup with the exact probe semantics of SNAPHashTable::Lookup
+// (HashTable.h:74-105).  Returns pointer to value1 or nullptr; adds probes.
+const uint32_t *lookupSlot(const Index &idx, uint32_t table, uint32_t key, uint32_t *nProbes);
+
+// xoshiro256** seeded with splitmix64: deterministic on every host.
+struct Rng {
+    uint64_t s[4];
+    explicit Rng(uint64_t seed);
+    uint64_t next();
+    double uniform() { return (next() >> 11) * (1.0 / 9007199254740992.0); }
+    uint64_t below(uint64_t n) { return n ? next() % n : 0; }
+};
+
+}  // namespace snapgpu
+
+struct snapgpu_genome : snapgpu::Genome {};
+struct snapgpu_index : snapgpu::Index {};

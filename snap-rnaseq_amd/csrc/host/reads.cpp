@@ -1,0 +1,188 @@
+// reads.cpp -- read batches: wgsim-like simulator, FASTQ in/out, caller arrays.
+#include "internal.h"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+using namespace snapgpu;
+
+namespace {
+
+snapgpu_reads_t *allocReads(uint64_t n, uint64_t totalBytes, bool truth) {
+    auto *r = new snapgpu_reads_t();
+    r->n = n;
+    r->totalBytes = totalBytes;
+    r->bases = new char[totalBytes + 64]();
+    r->quals = new char[totalBytes + 64]();
+    r->offsets = new uint64_t[n + 1]();
+    r->lengths = new uint32_t[n + 1]();
+    r->truthLocation = truth ? new uint32_t[n + 1]() : nullptr;
+    r->truthDirection = truth ? new uint8_t[n + 1]() : nullptr;
+    return r;
+}
+
+inline char complement(char c) {
+    switch (c) { case 'A': return 'T'; case 'C': return 'G'; case 'G': return 'C'; case 'T': return 'A'; default: return 'N'; }
+}
+
+}  // namespace
+
+extern "C" {
+
+snapgpu_reads_t *snapgpu_reads_synthetic(const snapgpu_genome_t *g, const snapgpu_synth_reads_params_t *p) {
+    if (!g || !p || p->readLength == 0 || g->pieceOffsets.empty()) { setError("bad read params"); return nullptr; }
+    const uint32_t L = p->readLength;
+    snapgpu_reads_t *r = allocReads(p->nReads, p->nReads * (uint64_t)L, true);
+    Rng rng(p->seed);
+    static const char kBases[4] = {'A', 'C', 'G', 'T'};
+    // contig extents
+    std::vector<uint64_t> cStart, cLen, cum;
+    uint64_t total = 0;
+    for (size_t i = 0; i < g->pieceOffsets.size(); i++) {
+        uint64_t s = g->pieceOffsets[i];
+        uint64_t e = i + 1 < g->pieceOffsets.size() ? g->pieceOffsets[i + 1] - g->chromosomePadding : g->nBases - g->chromosomePadding;
+        cStart.push_back(s); cLen.push_back(e - s);
+        total += e - s > 2 * L + 64 ? e - s : 0;
+        cum.push_back(total);
+    }
+    if (total == 0) { setError("contigs too short"); snapgpu_reads_free(r); return nullptr; }
+    const char *gb = g->bases();
+    std::string frag;
+    for (uint64_t i = 0; i < p->nReads; i++) {
+        char *out = r->bases + i * L;
+        r->offsets[i] = i * L;
+        r->lengths[i] = L;
+        memset(r->quals + i * L, (int)p->qualityChar, L);
+        if (p->randomReadFraction > 0 && rng.uniform() < p->randomReadFraction) {
+            for (uint32_t j = 0; j < L; j++) out[j] = kBases[rng.next() >> 62];
+            r->truthLocation[i] = kInvalidLocation;
+            continue;
+        }
+        for (int attempt = 0;; attempt++) {
+            uint64_t x = rng.below(total);
+            size_t c = 0;
+            while (cum[c] <= x) c++;
+            uint64_t start = cStart[c] + rng.below(cLen[c] - L - 48);
+            // haplotype walk with mutations (wgsim: substitution / indel with extension)
+            frag.clear();
+            uint64_t pos = start;
+            while (frag.size() < L) {
+                char base = gb[pos];
+                if (base == 'n') base = 'N';
+                double u = rng.uniform();
+                if (u < p->mutationRate) {
+                    if (rng.uniform() < p->indelFraction) {
+                        uint32_t len = 1;
+                        while (rng.uniform() < p->indelExtend && len < 10) len++;
+                        if (rng.next() >> 63) { pos += len; continue; }        // deletion
+                        frag.push_back(base);
+                        for (uint32_t k = 0; k < len && frag.size() < L; k++) frag.push_back(kBases[rng.next() >> 62]);
+                        pos++;
+                        continue;
+                    }
+                    char nb;
+                    do { nb = kBases[rng.next() >> 62]; } while (nb == base);
+                    frag.push_back(nb);
+                } else {
+                    frag.push_back(base);
+                }
+                pos++;
+            }
+            frag.resize(L);
+            uint32_t nN = 0;
+            for (char ch : frag) nN += ch == 'N';
+            if (nN > L / 20 && attempt < 16) continue;   // wgsim -A 0.05: discard ambiguous reads
+            bool rc = rng.next() >> 63;
+            if (rc) {
+                std::string t(frag.rbegin(), frag.rend());
+                for (auto &ch : t) ch = complement(ch);
+                frag.swap(t);
+            }
+            for (uint32_t j = 0; j < L; j++) {
+                char ch = frag[j];
+                if (ch != 'N' && rng.uniform() < p->baseErrorRate) {
+                    char nb;
+                    do { nb = kBases[rng.next() >> 62]; } while (nb == ch);
+                    ch = nb;
+                }
+                out[j] = ch;
+            }
+            r->truthLocation[i] = (uint32_t)start;
+            r->truthDirection[i] = rc ? 1 : 0;
+            break;
+        }
+    }
+    return r;
+}
+
+snapgpu_reads_t *snapgpu_reads_from_arrays(uint64_t n, const char *bases, const char *quals,
+                                           const uint64_t *offsets, const uint32_t *lengths) {
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < n; i++) total += lengths[i];
+    snapgpu_reads_t *r = allocReads(n, total, false);
+    uint64_t o = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        memcpy(r->bases + o, bases + offsets[i], lengths[i]);
+        memcpy(r->quals + o, quals + offsets[i], lengths[i]);
+        r->offsets[i] = o;
+        r->lengths[i] = lengths[i];
+        o += lengths[i];
+    }
+    return r;
+}
+
+snapgpu_reads_t *snapgpu_reads_from_fastq(const char *path) {
+    FILE *f = fopen(path, "r");
+    if (!f) { setError(std::string("cannot open ") + path); return nullptr; }
+    std::vector<std::string> b, q;
+    std::string lines[4];
+    char buf[1 << 16];
+    int k = 0;
+    while (fgets(buf, sizeof(buf), f)) {
+        std::string s(buf);
+        while (!s.empty() && (s.back() == '\n' || s.back() == '\r')) s.pop_back();
+        lines[k++] = s;
+        if (k == 4) { b.push_back(lines[1]); q.push_back(lines[3]); k = 0; }
+    }
+    fclose(f);
+    uint64_t total = 0;
+    for (auto &s : b) total += s.size();
+    snapgpu_reads_t *r = allocReads(b.size(), total, false);
+    uint64_t o = 0;
+    for (size_t i = 0; i < b.size(); i++) {
+        memcpy(r->bases + o, b[i].data(), b[i].size());
+        memcpy(r->quals + o, q[i].data(), std::min(q[i].size(), b[i].size()));
+        r->offsets[i] = o;
+        r->lengths[i] = (uint32_t)b[i].size();
+        o += b[i].size();
+    }
+    return r;
+}
+
+int snapgpu_reads_write_fastq(const snapgpu_reads_t *r, const char *path) {
+    FILE *f = fopen(path, "w");
+    if (!f) { setError(std::string("cannot write ") + path); return SNAPGPU_EIO; }
+    for (uint64_t i = 0; i < r->n; i++) {
+        fprintf(f, "@read%llu", (unsigned long long)i);
+        if (r->truthLocation) fprintf(f, "_%u_%u", r->truthLocation[i], (unsigned)r->truthDirection[i]);
+        fputc('\n', f);
+        fwrite(r->bases + r->offsets[i], 1, r->lengths[i], f);
+        fputs("\n+\n", f);
+        fwrite(r->quals + r->offsets[i], 1, r->lengths[i], f);
+        fputc('\n', f);
+    }
+    int ok = ferror(f) == 0;
+    fclose(f);
+    return ok ? SNAPGPU_OK : SNAPGPU_EIO;
+}
+
+void snapgpu_reads_free(snapgpu_reads_t *r) {
+    if (!r) return;
+    delete[] r->bases; delete[] r->quals; delete[] r->offsets; delete[] r->lengths;
+    delete[] r->truthLocation; delete[] r->truthDirection;
+    delete r;
+}
+
+}  // extern "C"

@@ -1,0 +1,216 @@
+"""ctypes declarations of the C ABI in include/snapgpu.h.
+
+The product library is ``libsnapgpu.so`` built in-tree next to this file by
+``snap-rnaseq_amd/Makefile`` (hipcc for gfx950 + g++ for the host side).  There is
+no Python or CPU fallback for the aligner: if the library (or a GPU) is missing,
+creating an aligner raises.
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("SNAPGPU_LIB", os.path.join(_HERE, "libsnapgpu.so"))
+
+
+class Result(C.Structure):
+    """snapgpu_result_t -- one BaseAligner::AlignRead outcome (BaseAligner.cpp:510-938)."""
+    _fields_ = [
+        ("location", C.c_uint32),
+        ("score", C.c_int32),
+        ("mapq", C.c_int32),
+        ("result", C.c_uint8),
+        ("direction", C.c_uint8),
+        ("flags", C.c_uint8),
+        ("reserved", C.c_uint8),
+        ("nLookups", C.c_uint32),
+        ("nLocationsScored", C.c_uint32),
+        ("popularSeedsSkipped", C.c_uint16),
+        ("nHitsIgnored", C.c_uint16),
+        ("nProbes", C.c_uint32),
+        ("nHitWords", C.c_uint32),
+        ("nOverflowLists", C.c_uint32),
+        ("probabilityOfAllCandidates", C.c_double),
+        ("probabilityOfBestCandidate", C.c_double),
+    ]
+
+
+class AlignerParams(C.Structure):
+    _fields_ = [
+        ("maxHitsToConsider", C.c_uint32),
+        ("maxK", C.c_uint32),
+        ("maxReadSize", C.c_uint32),
+        ("maxSeedsToUse", C.c_uint32),
+        ("maxSeedCoverage", C.c_double),
+        ("extraSearchDepth", C.c_uint32),
+        ("explorePopularSeeds", C.c_uint32),
+        ("stopOnFirstHit", C.c_uint32),
+    ]
+
+
+class SynthGenomeParams(C.Structure):
+    _fields_ = [
+        ("seed", C.c_uint64),
+        ("totalBases", C.c_uint64),
+        ("nContigs", C.c_uint32),
+        ("nRepeatFamilies", C.c_uint32),
+        ("repeatFraction", C.c_double),
+        ("maxDivergence", C.c_double),
+        ("nRunFraction", C.c_double),
+        ("chromosomePadding", C.c_uint32),
+    ]
+
+
+class SynthReadsParams(C.Structure):
+    _fields_ = [
+        ("seed", C.c_uint64),
+        ("nReads", C.c_uint64),
+        ("readLength", C.c_uint32),
+        ("qualityChar", C.c_uint32),
+        ("baseErrorRate", C.c_double),
+        ("mutationRate", C.c_double),
+        ("indelFraction", C.c_double),
+        ("indelExtend", C.c_double),
+        ("randomReadFraction", C.c_double),
+    ]
+
+
+class Reads(C.Structure):
+    _fields_ = [
+        ("n", C.c_uint64),
+        ("totalBytes", C.c_uint64),
+        ("bases", C.c_void_p),
+        ("quals", C.c_void_p),
+        ("offsets", C.POINTER(C.c_uint64)),
+        ("lengths", C.POINTER(C.c_uint32)),
+        ("truthLocation", C.POINTER(C.c_uint32)),
+        ("truthDirection", C.POINTER(C.c_uint8)),
+    ]
+
+
+class IndexInfo(C.Structure):
+    _fields_ = [
+        ("nBases", C.c_uint32),
+        ("seedLen", C.c_uint32),
+        ("nHashTables", C.c_uint32),
+        ("chromosomePadding", C.c_uint32),
+        ("overflowTableSize", C.c_uint64),
+        ("totalHashSlots", C.c_uint64),
+        ("totalUsedSlots", C.c_uint64),
+        ("nPieces", C.c_int32),
+        ("hasIupac", C.c_uint32),
+    ]
+
+
+class IndexView(C.Structure):
+    _fields_ = [
+        ("slots", C.c_void_p),
+        ("tableBase", C.c_void_p),
+        ("tableSize", C.c_void_p),
+        ("overflow", C.c_void_p),
+        ("genome", C.c_void_p),
+        ("pieceOffsets", C.c_void_p),
+        ("nBases", C.c_uint32),
+        ("seedLen", C.c_uint32),
+        ("nHashTables", C.c_uint32),
+        ("chromosomePadding", C.c_uint32),
+        ("nPieces", C.c_int32),
+        ("pad_", C.c_uint32),
+        ("overflowTableSize", C.c_uint64),
+    ]
+
+
+class Timing(C.Structure):
+    _fields_ = [
+        ("mainKernelMs", C.c_double),
+        ("spillKernelMs", C.c_double),
+        ("fixupMs", C.c_double),
+        ("nSpilled", C.c_uint64),
+        ("nMapqFixed", C.c_uint64),
+    ]
+
+
+class AlignerStats(C.Structure):
+    _fields_ = [
+        ("nHashTableLookups", C.c_int64),
+        ("nLocationsScored", C.c_int64),
+        ("nHitsIgnoredBecauseOfTooHighPopularity", C.c_int64),
+        ("nReadsIgnoredBecauseOfTooManyNs", C.c_int64),
+        ("nIndelsMerged", C.c_int64),
+        ("nReads", C.c_int64),
+    ]
+
+
+assert C.sizeof(Result) == 56, C.sizeof(Result)
+
+# (name, restype, argtypes)
+_PROTOS = [
+    ("snapgpu_abi_version", C.c_int, []),
+    ("snapgpu_last_error", C.c_char_p, []),
+    ("snapgpu_aligner_params_default", None, [C.POINTER(AlignerParams)]),
+    ("snapgpu_genome_from_fasta", C.c_void_p, [C.c_char_p, C.c_uint32]),
+    ("snapgpu_genome_synthetic", C.c_void_p, [C.POINTER(SynthGenomeParams)]),
+    ("snapgpu_genome_write_fasta", C.c_int, [C.c_void_p, C.c_char_p]),
+    ("snapgpu_genome_free", None, [C.c_void_p]),
+    ("snapgpu_genome_nbases", C.c_uint32, [C.c_void_p]),
+    ("snapgpu_genome_bases", C.c_void_p, [C.c_void_p]),
+    ("snapgpu_genome_npieces", C.c_int, [C.c_void_p]),
+    ("snapgpu_genome_piece_offset", C.c_uint32, [C.c_void_p, C.c_int]),
+    ("snapgpu_genome_piece_name", C.c_char_p, [C.c_void_p, C.c_int]),
+    ("snapgpu_index_build", C.c_void_p, [C.c_void_p, C.c_int, C.c_int]),
+    ("snapgpu_index_load", C.c_void_p, [C.c_char_p]),
+    ("snapgpu_index_save", C.c_int, [C.c_void_p, C.c_char_p]),
+    ("snapgpu_index_free", None, [C.c_void_p]),
+    ("snapgpu_index_get_info", C.c_int, [C.c_void_p, C.POINTER(IndexInfo)]),
+    ("snapgpu_index_get_view", C.c_int, [C.c_void_p, C.POINTER(IndexView)]),
+    ("snapgpu_index_lookup", C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(C.c_uint32),
+                                       C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.c_uint32]),
+    ("snapgpu_reads_synthetic", C.POINTER(Reads), [C.c_void_p, C.POINTER(SynthReadsParams)]),
+    ("snapgpu_reads_from_fastq", C.POINTER(Reads), [C.c_char_p]),
+    ("snapgpu_reads_from_arrays", C.POINTER(Reads), [C.c_uint64, C.c_char_p, C.c_char_p,
+                                                     C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]),
+    ("snapgpu_reads_write_fastq", C.c_int, [C.POINTER(Reads), C.c_char_p]),
+    ("snapgpu_reads_free", None, [C.POINTER(Reads)]),
+    ("snapgpu_device_count", C.c_int, []),
+    ("snapgpu_aligner_create", C.c_void_p, [C.c_int, C.c_void_p, C.POINTER(AlignerParams)]),
+    ("snapgpu_aligner_free", None, [C.c_void_p]),
+    ("snapgpu_align_batch", C.c_int, [C.c_void_p, C.POINTER(Reads), C.POINTER(Result)]),
+    ("snapgpu_reads_upload", C.c_void_p, [C.c_void_p, C.POINTER(Reads)]),
+    ("snapgpu_device_reads_free", None, [C.c_void_p]),
+    ("snapgpu_align_resident", C.c_int, [C.c_void_p, C.c_void_p]),
+    ("snapgpu_results_download", C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(Result)]),
+    ("snapgpu_synchronize", C.c_int, [C.c_void_p]),
+    ("snapgpu_last_timing", C.c_int, [C.c_void_p, C.POINTER(Timing)]),
+    ("snapgpu_aligner_get_stats", C.c_int, [C.c_void_p, C.POINTER(AlignerStats)]),
+    ("snapgpu_aligner_max_k", C.c_int, [C.c_void_p]),
+    ("snapgpu_aligner_name", C.c_char_p, [C.c_void_p]),
+    ("snapgpu_lv_batch", C.c_int, [C.c_int, C.c_int, C.c_uint32, C.c_char_p, C.POINTER(C.c_uint64),
+                                   C.POINTER(C.c_uint32), C.c_char_p, C.c_char_p, C.POINTER(C.c_uint64),
+                                   C.POINTER(C.c_uint32), C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                   C.POINTER(C.c_int32), C.POINTER(C.c_double)]),
+    ("snapgpu_compute_mapq", C.c_int, [C.c_double, C.c_double, C.c_int, C.c_int]),
+]
+
+EXPORTED_SYMBOLS = [p[0] for p in _PROTOS]
+
+_lib = None
+
+
+def lib():
+    """Load libsnapgpu.so (raises OSError if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OSError(f"{LIB_PATH} not built: run `make -C snap-rnaseq_amd` or __graft_entry__.build()")
+        l = C.CDLL(LIB_PATH)
+        for name, res, args in _PROTOS:
+            if not hasattr(l, name):
+                continue   # tests/test_capi.py asserts every symbol is exported
+            f = getattr(l, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = l
+    return _lib
+
+
+def last_error():
+    return lib().snapgpu_last_error().decode(errors="replace")
