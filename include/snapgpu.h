@@ -79,9 +79,11 @@ typedef struct snapgpu_result {
     uint32_t nProbes;             /* hash-table entries probed (roofline P) */
     uint32_t nHitWords;           /* hit words consumed (roofline H) */
     uint32_t nOverflowLists;      /* overflow lists visited (roofline V) */
+    uint32_t nElements;           /* candidate elements allocated (BaseAligner.cpp:1485-1568) */
+    uint32_t reserved2;
     double   probabilityOfAllCandidates;
     double   probabilityOfBestCandidate;
-} snapgpu_result_t;   /* 56 bytes */
+} snapgpu_result_t;   /* 64 bytes */
 
 /* BaseAligner constructor parameters (BaseAligner.h:44-55, defaults of
  * AlignerOptions.cpp:33-85 / SingleAligner.cpp:167-179). */

@@ -97,6 +97,24 @@ int oracle_compute_mapq(double pAll, double pBest, int score, int popular) {
  * read descending from text[-1] (LandauVishkin.h:261-263, 326, 336). */
 static inline char lv_t(const char *text, int dir, int j) { return dir > 0 ? text[j] : text[-1 - j]; }
 
+
+/* First m in [from, endd) with pattern[m] != T(m + d), else endd -- the
+ * clipped result of the reference's 8-byte XOR/ctz loop (LandauVishkin.h:268-288,
+ * 331-353). */
+static inline int lv_extend(const char *text, int dir, const char *pattern, int m, int d, int endd) {
+    while (m + 8 <= endd) {
+        uint64_t pv, tv;
+        memcpy(&pv, pattern + m, 8);
+        if (dir > 0) memcpy(&tv, text + m + d, 8);
+        else { memcpy(&tv, text - (m + d) - 8, 8); tv = __builtin_bswap64(tv); }
+        uint64_t x = pv ^ tv;
+        if (x) return m + (__builtin_ctzll(x) >> 3);
+        m += 8;
+    }
+    while (m < endd && pattern[m] == lv_t(text, dir, m + d)) m++;
+    return m;
+}
+
 /* LandauVishkin<dir>::computeEditDistance, LandauVishkin.h:211-455.  The 8-byte
  * XOR/ctz match extension is restated byte-wise: the reference clips every
  * extension with min(., end), so the bytes it over-reads past `end` only matter
@@ -104,17 +122,17 @@ static inline char lv_t(const char *text, int dir, int j) { return dir > 0 ? tex
 int oracle_lv(int dir, const char *text, int textLen, const char *pattern, const char *qual,
               int patternLen, int k, double *prob, int *netIndel) {
     pthread_once(&g_once, init_tables);
-    int L[MAX_K + 1][2 * MAX_K + 1];
-    char A[MAX_K + 1][2 * MAX_K + 1];
-    for (int e = 0; e <= MAX_K; e++)
-        for (int d = 0; d < 2 * MAX_K + 1; d++) L[e][d] = -2;   /* LandauVishkin.h:168 */
+    int L[MAX_K + 1][2 * MAX_K + 3];
+    char A[MAX_K + 1][2 * MAX_K + 3];
+    /* The reference fills L with -2 once (LandauVishkin.h:168) and row e only
+     * ever writes |d| <= e, so every read outside the band sees -2.  Setting
+     * just the cells row e reads outside row e-1's band is equivalent. */
     *netIndel = 0;
     if (k > MAX_K - 1) k = MAX_K - 1;
     if (!text) { *prob = 0.0; return -1; }
     *prob = 1.0;
     int end = patternLen < textLen ? patternLen : textLen;
-    int i = 0;
-    while (i < end && pattern[i] == lv_t(text, dir, i)) i++;
+    int i = lv_extend(text, dir, pattern, 0, 0, end);
     L[0][MAX_K] = i;
     if (i == end) {
         int result = patternLen > end ? patternLen - end : 0;
@@ -122,6 +140,8 @@ int oracle_lv(int dir, const char *text, int textLen, const char *pattern, const
         return result > k ? -1 : result;
     }
     for (int e = 1; e <= k; e++) {
+        L[e - 1][MAX_K - e - 1] = L[e - 1][MAX_K - e] = -2;
+        L[e - 1][MAX_K + e] = L[e - 1][MAX_K + e + 1] = -2;
         /* d order 0, 1, -1, 2, -2, ... (LandauVishkin.h:180-182, 311) */
         for (int j = 0; j < 2 * e + 1; j++) {
             int d = (j == 0) ? 0 : ((j & 1) ? (j + 1) / 2 : -(j / 2));
@@ -135,9 +155,7 @@ int oracle_lv(int dir, const char *text, int textLen, const char *pattern, const
             int endd = patternLen < textLen - d ? patternLen : textLen - d;
             if (pattern[best] == lv_t(text, dir, best + d)) {
                 if (best < endd) {
-                    int m = best + 1;
-                    while (m < endd && pattern[m] == lv_t(text, dir, m + d)) m++;
-                    best = m;
+                    best = lv_extend(text, dir, pattern, best + 1, d, endd);
                 } else {
                     best = endd;
                 }
@@ -570,6 +588,7 @@ static void align_read(Oracle *o, const char *bases, const char *quals, unsigned
                     } else if (o->lps[dir] <= o->scoreLimit) {
                         /* allocateNewCandidate, BaseAligner.cpp:1485-1568 */
                         el = &o->pool[o->nUsed++];
+                        out->nElements++;
                         el->used = 1ull << bit;
                         el->scored = 0;
                         el->lps = o->lps[dir];

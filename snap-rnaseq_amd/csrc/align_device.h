@@ -1,0 +1,422 @@
+// align_device.h -- gfx950 device code for the batched BaseAligner::AlignRead.
+//
+// One wavefront (64 lanes) aligns one read at a time; waves pull reads from a
+// device work counter (persistent grid).  Per wave:
+//   * LDS: the read in both orientations + qualities, the genome window of the
+//     candidate being scored, the Landau-Vishkin row history, the candidate
+//     element hash buckets, insertion-batch scratch, per-lane selection maxima.
+//   * HBM: a private element arena (worst-case sized: (maxSeeds+1)*maxHits
+//     elements), 192-byte elements, one read = one arena lifetime.
+//
+// Reference semantics restated (all citations SNAPLib/...):
+//   AlignRead   BaseAligner.cpp:510-938   score  BaseAligner.cpp:977-1399
+//   LV          LandauVishkin.h:211-455   lookup GenomeIndex.cpp:971-1086, HashTable.h:74-105
+//   MAPQ        mapq.h:32-65
+//
+// Lane roles:
+//   * hash-probe: lane j loads probe j of SNAPHashTable's probe sequence.
+//   * hit insertion: lane i handles hit i of a 64-hit batch; duplicates inside
+//     the batch are grouped through an LDS table and applied in hit order by
+//     the group's first lane (so FIFO/weight semantics are exactly sequential).
+//   * LV: lane 31+d (forward) / 31-d (reverse) holds diagonal d; the per-lane
+//     mismatch bitmap F_x[m] = read[m] != genome[g+x+m] is built with one
+//     compare+ballot per (x, 64-position block) and v_writelane.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "snapgpu.h"
+
+namespace sgk {
+
+constexpr int WAVE = 64;
+constexpr int MAX_K = 31;                 // LandauVishkin.h:9
+constexpr uint32_t INVALID = 0xffffffffu; // InvalidGenomeLocation
+constexpr uint32_t UNUSED_SIDE = 0xfffffffeu;
+constexpr uint32_t UNUSED_SCORE = 0xffffu;
+constexpr uint32_t FAIL_SCORE = 0xffffffffu;
+constexpr int ELEM = 48;                  // hashTableElementSize == maxMergeDist
+constexpr uint32_t NPAD = 100;            // Genome::N_PADDING
+constexpr int NBUCKET = 1024;             // element hash buckets (LDS)
+constexpr int BT = 128;                   // insertion-batch dedupe table (LDS)
+constexpr uint32_t NONE = 0xffffffffu;
+
+struct DevTables {
+    double indel[64];
+    double phred[256];
+    double perfect[512];
+    double seedProb;          // __powidf2(0.999, seedLen), BaseAligner.cpp:1227
+    uint32_t wrap[32];        // GetWrappedNextSeedToTest order (SeedSequencer.h)
+};
+
+struct Elem {                 // 192 bytes, 64-byte aligned slots in HBM
+    uint64_t used;            // candidatesUsed
+    uint64_t scored;          // candidatesScored
+    double prob;              // matchProbabilityForBestScore
+    uint32_t key;             // (base/48)<<1 | direction
+    uint32_t next;            // hash chain
+    uint32_t bestScore;
+    uint32_t bestLoc;         // bestScoreGenomeLocation
+    uint32_t sortkey;         // linked ? weight<<24 | (0xffffff - ts) : 0
+    uint8_t weight, lps, allScored, pad;
+    uint16_t seedOffset[ELEM];
+    uint8_t pad2[48];
+};
+static_assert(sizeof(Elem) == 192, "Elem layout");
+
+struct KArgs {
+    // index (HBM)
+    const uint32_t *slots;
+    const uint64_t *tableBase;
+    const uint64_t *tableSize;
+    const uint32_t *overflow;
+    const char *genome;          // base 0; >= 256 guard bytes each side
+    const uint32_t *pieces;
+    int32_t nPieces;
+    uint32_t nBases, seedLen, nTables, padding;
+    // params
+    uint32_t maxHits, maxK, maxReadSize, maxSeedsCmd;
+    double seedCoverage;
+    uint32_t extra, explore, stopOnFirst, kRows;
+    const DevTables *tab;
+    // reads
+    const char *bases;
+    const char *quals;
+    const uint64_t *offsets;
+    const uint32_t *lengths;
+    uint32_t nReads;
+    snapgpu_result_t *out;
+    // work queue + arenas
+    uint32_t *counter;
+    Elem *arena;
+    uint64_t arenaElems;         // per-wave capacity
+};
+
+// ------------------------------------------------------------ wave helpers
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ int unii(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+    return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
+}
+__device__ __forceinline__ double unid(double v) { return __longlong_as_double((long long)uni64((uint64_t)__double_as_longlong(v))); }
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ int readlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ uint32_t readlaneu(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+
+__device__ __forceinline__ void wave_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); __builtin_amdgcn_wave_barrier(); }
+__device__ __forceinline__ int shfl_up1(int v) { return __shfl_up(v, 1); }     // lane i <- lane i-1
+__device__ __forceinline__ int shfl_down1(int v) { return __shfl_down(v, 1); } // lane i <- lane i+1
+
+__device__ __forceinline__ uint64_t max_reduce64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        uint64_t w = __shfl_xor(v, o);
+        v = w > v ? w : v;
+    }
+    return v;
+}
+__device__ __forceinline__ uint64_t or_reduce64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v |= __shfl_xor(v, o);
+    return v;
+}
+
+__device__ __forceinline__ uint32_t fmix32(uint32_t k) {   // HashTable.h:60-72
+    k ^= k >> 16; k *= 0x85ebca6bu; k ^= k >> 13; k *= 0xc2b2ae35u; k ^= k >> 16;
+    return k;
+}
+__device__ __forceinline__ int base_value(uint32_t c) {     // Tables.cpp:41-48
+    return c == 'A' ? 0 : c == 'G' ? 1 : c == 'C' ? 2 : c == 'T' ? 3 : 4;
+}
+__device__ __forceinline__ uint32_t complement_of(uint32_t c) {   // BaseAligner.cpp:148-152 (others -> 0)
+    return c == 'A' ? 'T' : c == 'G' ? 'C' : c == 'C' ? 'G' : c == 'T' ? 'A' : c == 'N' ? 'N' : 0;
+}
+
+// ------------------------------------------------------------------ LDS
+template <int MAXLEN>
+struct Lds {
+    static constexpr int NB = MAXLEN / 64;          // 64-position blocks
+    char fwd[MAXLEN + 64];                          // read[FORWARD], zero slack
+    char rc[MAXLEN + 64];                           // read[RC]
+    char fwdQ[MAXLEN + 64];
+    char rcQ[MAXLEN + 64];
+    uint32_t win[(MAXLEN + 192) / 4];               // genome window [g-64, g+n+64+64)
+    uint32_t head[NBUCKET];                         // element hash chains
+    uint32_t btKey[BT];
+    uint64_t btMask[BT];
+    uint64_t laneMax[WAVE];                         // per-owner-lane max (sortkey<<32 | idx)
+    uint32_t scrLoc[WAVE];                          // batch scratch: hit location per lane
+    uint32_t nElems;
+    uint32_t pad_[3];
+    uint64_t seedUsed[NB + 1];                      // BaseAligner::seedUsed bit vector
+    int16_t btAct[MAX_K + 1];                       // LV backtrace scratch
+    int16_t btMatched[MAX_K + 1];
+    uint16_t rows[MAX_K][WAVE];                     // LV rows: (L+2) | action<<12
+};
+
+// ------------------------------------------------------------ LV engine
+// Per-lane mismatch bitmap over read positions m in [0, NB*64):
+// bit m of F[m>>6] = (read[m] != genome[g + x + m]) with x = lane - 31, and
+// positions m >= n forced to 1 (the byte past a pattern never matches genome).
+template <int NB>
+struct Bitmap { uint64_t w[NB]; };
+
+// first set bit at position >= m0 (m0 >= 0); returns NB*64 if none
+template <int NB>
+__device__ __forceinline__ int bm_first_from(const Bitmap<NB> &F, int m0) {
+    int r = NB * 64;
+    bool found = false;
+#pragma unroll
+    for (int j = NB - 1; j >= 0; j--) {
+        uint64_t x = F.w[j];
+        int lo = j * 64;
+        if (m0 > lo + 63) x = 0;
+        else if (m0 > lo) x &= ~0ull << (m0 - lo);
+        if (x) { r = lo + __builtin_ctzll(x); found = true; }
+    }
+    (void)found;
+    return r;
+}
+// highest set bit at position <= m0; returns -1 if none (m0 may be < 0)
+template <int NB>
+__device__ __forceinline__ int bm_last_upto(const Bitmap<NB> &F, int m0) {
+    int r = -1;
+#pragma unroll
+    for (int j = 0; j < NB; j++) {
+        uint64_t x = F.w[j];
+        int lo = j * 64;
+        if (m0 < lo) x = 0;
+        else if (m0 < lo + 63) x &= (2ull << (m0 - lo)) - 1;
+        if (x) r = lo + 63 - __builtin_clzll(x);
+    }
+    return r;
+}
+template <int NB>
+__device__ __forceinline__ bool bm_bit(const Bitmap<NB> &F, int m) {
+    if (m < 0 || m >= NB * 64) return true;
+    bool b = false;
+#pragma unroll
+    for (int j = 0; j < NB; j++)
+        if ((m >> 6) == j) b = (F.w[j] >> (m & 63)) & 1;
+    return b;
+}
+
+// Build F for lanes x in [-kmax, kmax]; lane i of block b holds read byte rb[b].
+// win: LDS bytes with win[w0 + p] = genome[g + p] for p in [-64, n + 64).
+template <int NB>
+__device__ __forceinline__ void build_bitmap(Bitmap<NB> &F, const uint32_t (&rbF)[NB], const uint32_t (&rbR)[NB],
+                                             bool useR, const char *win, int w0, int n, int kmax) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int b = 0; b < NB; b++) { F.w[b] = ~0ull; }
+    for (int x = -kmax; x <= kmax; x++) {
+        const int tl = 31 + x;
+#pragma unroll
+        for (int b = 0; b < NB; b++) {
+            if (b * 64 < n) {
+                int m = b * 64 + lane;
+                uint32_t gbyte = (uint8_t)win[w0 + x + m];
+                uint32_t rbyte = useR ? rbR[b] : rbF[b];
+                bool mm = (m >= n) || (gbyte != rbyte);
+                uint64_t mask = ballot(mm);
+                if (lane == tl) F.w[b] = mask;   // v_cndmask from the SGPR ballot
+            }
+        }
+    }
+}
+
+struct LvOut { int score; int netIndel; double prob; };
+
+// LandauVishkin<DIR>::computeEditDistance on the wave.  Pattern index i maps to
+// read position m = p0 + DIR*i; text position j of diagonal d maps to the
+// bitmap of x = DIR*d.  textLen only bounds end_d = min(patternLen, textLen-d).
+// qual: LDS quality in read coordinates.  rows: LDS row history.
+template <int DIR, int NB>
+__device__ __forceinline__ LvOut lv_wave(const Bitmap<NB> &F, int p0, int patternLen, int textLen, int k,
+                                         const char *qual, uint16_t (*rows)[WAVE], int16_t *btAct,
+                                         int16_t *btMatched, const DevTables *tab) {
+    const int lane = lane_id();
+    LvOut r;
+    r.netIndel = 0;
+    if (k > MAX_K - 1) k = MAX_K - 1;
+    const int d = DIR > 0 ? lane - 31 : 31 - lane;   // diagonal held by this lane
+    // row 0 (exact prefix), diagonal 0 lives on lane 31
+    int end0 = patternLen < textLen ? patternLen : textLen;
+    int L0;
+    {
+        int fm;
+        if (DIR > 0) fm = bm_first_from(F, p0) - p0;
+        else fm = p0 - bm_last_upto(F, p0);
+        int v = fm < end0 ? fm : end0;
+        L0 = unii(readlane(v, 31));
+    }
+    if (L0 == end0) {
+        int result = patternLen > end0 ? patternLen - end0 : 0;
+        r.prob = tab->perfect[patternLen];
+        r.score = result > k ? -1 : result;
+        return r;
+    }
+    int Lp = (lane == 31) ? L0 : -2;
+    if (lane == 31) rows[0][31] = (uint16_t)(L0 + 2);
+    int endd = patternLen < textLen - d ? patternLen : textLen - d;
+    for (int e = 1; e <= k; e++) {
+        // neighbours: diagonal d-1 and d+1
+        int nUp = shfl_up1(Lp), nDn = shfl_down1(Lp);
+        int left = DIR > 0 ? nUp : nDn;           // L[e-1][d-1]
+        int right = (DIR > 0 ? nDn : nUp) + 1;    // L[e-1][d+1] + 1
+        int best = Lp + 1, act = 0;               // 0 = X, 1 = D, 2 = I
+        if (left > best) { best = left; act = 1; }
+        if (right > best) { best = right; act = 2; }
+        bool active = (d <= e) && (d >= -e);
+        // extension (LandauVishkin.h:325-354)
+        int mpos = p0 + DIR * best;
+        if (best < endd) {
+            int fm;
+            if (DIR > 0) fm = bm_first_from(F, mpos) - p0;
+            else fm = p0 - bm_last_upto(F, mpos);
+            best = fm < endd ? fm : endd;
+        } else {
+            if (!bm_bit(F, mpos)) best = endd;
+        }
+        int Ln = active ? best : Lp;
+        if (active) rows[e][lane] = (uint16_t)((Ln + 2) | (act << 12));
+        uint64_t done = ballot(active && Ln == patternLen);
+        if (done) {
+            // first d in the order 0, 1, -1, 2, -2, ... (LandauVishkin.h:180-182)
+            int wd = 0;
+            for (int j = 0; j <= e; j++) {
+                int lp = DIR > 0 ? 31 + j : 31 - j;
+                int ln = DIR > 0 ? 31 - j : 31 + j;
+                if ((done >> lp) & 1) { wd = j; break; }
+                if (j > 0 && ((done >> ln) & 1)) { wd = -j; break; }
+            }
+            wd = unii(wd);
+            wave_sync();
+            // backtrace (LandauVishkin.h:376-431); uniform work, scratch in LDS
+            int curD = wd;
+            for (int ce = e; ce >= 1; ce--) {
+                int ln = DIR > 0 ? 31 + curD : 31 - curD;
+                uint32_t cell = uni(rows[ce][ln]);
+                int a = (int)(cell >> 12);
+                int Lcur = (int)(cell & 0xfff) - 2;
+                int src = a == 2 ? curD + 1 : (a == 1 ? curD - 1 : curD);
+                int ls = DIR > 0 ? 31 + src : 31 - src;
+                int Lsrc = (ce - 1 == 0) ? (src == 0 ? L0 : -2) : ((int)(uni(rows[ce - 1][ls]) & 0xfff) - 2);
+                if (lane == 0) {
+                    btAct[ce] = (int16_t)a;
+                    btMatched[ce] = (int16_t)(a == 1 ? Lcur - Lsrc : Lcur - Lsrc - 1);
+                }
+                curD = src;
+            }
+            wave_sync();
+            double p = 1.0;
+            int ce = 1, offset = L0, net = 0;
+            while (ce <= e) {
+                int a = unii(btAct[ce]);
+                int cnt = 1;
+                while (ce + 1 <= e && unii(btMatched[ce]) == 0 && unii(btAct[ce + 1]) == a) { cnt++; ce++; }
+                if (a == 2) { p *= tab->indel[cnt]; offset += cnt; net += cnt; }
+                else if (a == 1) { p *= tab->indel[cnt]; offset -= cnt; net -= cnt; }
+                else {
+                    for (int q = 0; q < cnt; q++) {
+                        int qi = offset < 0 ? 0 : offset;
+                        if (qi > patternLen - 1) qi = patternLen - 1;
+                        uint32_t qc = uni((uint8_t)qual[p0 + DIR * qi]);
+                        p *= tab->phred[qc];
+                        offset++;
+                    }
+                }
+                offset += unii(btMatched[ce]);
+                ce++;
+            }
+            p *= tab->perfect[patternLen - e];
+            r.score = e;
+            r.prob = p;
+            r.netIndel = net;
+            return r;
+        }
+        Lp = Ln;
+    }
+    r.score = -1;
+    r.prob = 0.0;
+    return r;
+}
+
+// Stage genome bytes [g - 64, g + n + 128) into LDS window (4-byte aligned start).
+// Returns w0 such that win[w0 + p] == genome[g + p].
+template <int MAXLEN>
+__device__ __forceinline__ int stage_window(Lds<MAXLEN> &S, const char *genome, uint32_t g, int n) {
+    const int lane = lane_id();
+    int64_t start = (int64_t)g - 64;
+    int64_t astart = start & ~(int64_t)3;
+    int nwords = (n + 192 + 4) / 4;
+    const uint32_t *src = (const uint32_t *)(genome + astart);
+    for (int i = lane; i < nwords && i < (MAXLEN + 192) / 4; i += WAVE) S.win[i] = src[i];
+    wave_sync();
+    return (int)((int64_t)g - astart);
+}
+
+// Genome::getSubstring (Genome.h:78-148): is [offset, offset+len) servable?
+__device__ __forceinline__ bool substring_ok(const KArgs &A, uint32_t offset, uint32_t len) {
+    if (offset > A.nBases || (uint64_t)offset + len > (uint64_t)A.nBases + NPAD) return false;
+    if (len <= A.padding) return true;
+    if (A.nPieces > 100) {
+        if (A.pieces[A.nPieces - 1] <= offset) return true;
+        int lo = 0, hi = A.nPieces - 2;
+        while (lo <= hi) {
+            int m = (lo + hi) / 2;
+            if (A.pieces[m] <= offset) {
+                if (A.pieces[m + 1] > offset) return !(A.pieces[m + 1] <= offset + len - 1);
+                lo = m + 1;
+            } else hi = m - 1;
+        }
+        return false;
+    }
+    for (int i = 0; i < A.nPieces; i++)
+        if (offset + len - 1 >= A.pieces[i]) return !(offset < A.pieces[i]);
+    return false;
+}
+__device__ __forceinline__ int next_piece_after(const KArgs &A, uint32_t loc) {   // Genome.cpp:376-401
+    int lo = 0, hi = A.nPieces - 1;
+    while (lo <= hi) {
+        int m = (lo + hi) / 2;
+        if (A.pieces[m] <= loc && (m == A.nPieces - 1 || A.pieces[m + 1] > loc)) return m >= A.nPieces - 1 ? -1 : m + 1;
+        else if (A.pieces[m] <= loc) lo = m + 1;
+        else hi = m - 1;
+    }
+    return -1;
+}
+
+// ------------------------------------------------------------ per-read state
+struct ReadState {
+    uint32_t lps[2], mostSeeds[2], nSeedsApplied[2];
+    uint32_t bestScore, bestLoc, scoreLimit, popular;
+    double pAll, pBest;
+    uint32_t outLoc, outDir;
+    int32_t outScore, outMapq;
+    uint32_t ts;                 // running hit counter (FIFO timestamps)
+    uint32_t nLookups, nScored, nHitsIgnored, nProbes, nHitWords, nOvf, nElems;
+};
+
+__device__ __forceinline__ uint32_t elem_hash(uint32_t key) { return (key * 2654435761u) >> (32 - 10); }
+
+// find element with `key`; NONE if absent
+__device__ __forceinline__ uint32_t chain_find(const uint32_t *head, const Elem *ar, uint32_t key) {
+    uint32_t e = head[elem_hash(key)];
+    while (e != NONE && ar[e].key != key) e = ar[e].next;
+    return e;
+}
+
+// owner-lane recompute of its selection maximum (elements e == lane mod 64)
+__device__ __forceinline__ void recompute_lane_max(uint64_t *laneMax, const Elem *ar, uint32_t nElems, int lane) {
+    uint64_t best = 0;
+    for (uint32_t e = lane; e < nElems; e += WAVE) {
+        uint32_t k = ar[e].sortkey;
+        uint64_t v = ((uint64_t)k << 32) | e;
+        if (k && v > best) best = v;
+    }
+    laneMax[lane] = best;
+}
+
+}  // namespace sgk

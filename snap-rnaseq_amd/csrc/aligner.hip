@@ -1,0 +1,895 @@
+// aligner.hip -- gfx950 kernels for batched BaseAligner::AlignRead and the C-ABI
+// aligner of include/snapgpu.h.  See align_device.h for the device data layout.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "align_device.h"
+#include "internal.h"
+
+using namespace sgk;
+
+namespace sgk {
+
+// ------------------------------------------------------------------ score()
+// BaseAligner::score, BaseAligner.cpp:977-1399.  Returns true iff a final
+// result was produced (written into st / *result).
+template <int MAXLEN>
+__device__ __forceinline__ bool score_wave(const KArgs &A, Lds<MAXLEN> &S, Elem *ar, ReadState &st, bool force,
+                                           uint32_t n, const uint32_t (&rbF)[MAXLEN / 64],
+                                           const uint32_t (&rbR)[MAXLEN / 64], int *result, uint32_t *flags) {
+    constexpr int NB = MAXLEN / 64;
+    const int lane = lane_id();
+    const DevTables *tab = A.tab;
+    for (int d = 0; d < 2; d++)
+        if (st.mostSeeds[d]) {
+            uint32_t v = st.nSeedsApplied[d] / st.mostSeeds[d];
+            if (v > st.lps[d]) st.lps[d] = v;
+        }
+    do {
+        // head of the highest non-empty weight list == max sortkey over linked elements
+        uint64_t sel = uni64(max_reduce64(S.laneMax[lane]));
+        uint32_t minLps = st.lps[0] < st.lps[1] ? st.lps[0] : st.lps[1];
+        if (minLps > st.scoreLimit || force) {
+            if (sel == 0) {
+                st.outScore = (int32_t)st.bestScore;
+                if (st.bestScore <= A.maxK) {
+                    st.outLoc = st.bestLoc;
+                    // computeMAPQ, mapq.h:32-65 (log10 on device; boundary cases re-derived on host)
+                    double pAll = st.pAll > st.pBest ? st.pAll : st.pBest;
+                    int mq;
+                    if (pAll == st.pBest && st.popular == 0 && st.bestScore < 5) mq = 70;
+                    else {
+                        double c = st.pBest / pAll;
+                        if (c >= 1) mq = 69;
+                        else {
+                            double v = -10 * log10(1 - c);
+                            mq = v < 69.0 ? (int)v : 69;
+                            if (v < 70.0 && fabs(v - rint(v)) < 1e-6) *flags |= SNAPGPU_FLAG_MAPQ_FIXED;
+                        }
+                        int pen = (int)st.popular - 10;
+                        if (pen < 0) pen = 0;
+                        mq -= pen / 2;
+                        if (mq < 0) mq = 0;
+                    }
+                    st.outMapq = mq;
+                    *result = mq >= 10 ? SNAPGPU_SINGLE_HIT : SNAPGPU_MULTIPLE_HITS;
+                } else {
+                    *result = (st.nSeedsApplied[0] == 0 && st.nSeedsApplied[1] == 0) ? SNAPGPU_MULTIPLE_HITS
+                                                                                      : SNAPGPU_NOT_FOUND;
+                    st.outMapq = 0;
+                }
+                return true;
+            }
+            force = true;
+        } else if (sel == 0) {
+            return false;
+        }
+        const uint32_t e = (uint32_t)sel;
+        Elem *el = ar + e;
+        const uint32_t ekey = uni(el->key);
+        const uint32_t dir = ekey & 1;
+        const uint32_t ebase = (ekey >> 1) * ELEM;
+        if (uni(el->lps) <= st.scoreLimit) {
+            uint64_t used = uni64(el->used);
+            uint64_t mask = used;
+            while (mask) {
+                const int bit = __builtin_ctzll(mask);
+                const uint64_t cb = 1ull << bit;
+                mask &= ~cb;
+                uint64_t scored = uni64(el->scored);
+                if (scored & cb) continue;
+                bool anyNearby = scored != 0;
+                el->scored = scored | cb;
+                uint32_t loc = ebase + bit;
+                const uint32_t elemLoc = loc;
+                uint32_t sc = FAIL_SCORE;
+                double prob = 0;
+                uint32_t glen = n + MAX_K;
+                bool ok = substring_ok(A, loc, glen);
+                if (!ok) {   // BaseAligner.cpp:1163-1185
+                    uint32_t endOffset = 0;
+                    bool have = false;
+                    if ((uint64_t)loc + n + MAX_K >= A.nBases) { endOffset = A.nBases; have = true; }
+                    else {
+                        int np = next_piece_after(A, loc);
+                        if (np >= 0) { endOffset = A.pieces[np]; have = true; }
+                    }
+                    if (have) {
+                        glen = endOffset - loc - 1;
+                        if (glen >= n - (uint32_t)MAX_K) ok = substring_ok(A, loc, glen);
+                    }
+                }
+                if (ok) {
+                    const int s = (int)uni(el->seedOffset[bit]);
+                    const int t = s + (int)A.seedLen;
+                    int w0 = stage_window(S, A.genome, loc, (int)n);
+                    int kmax = st.scoreLimit < (uint32_t)(MAX_K - 1) ? (int)st.scoreLimit : MAX_K - 1;
+                    Bitmap<NB> F;
+                    build_bitmap<NB>(F, rbF, rbR, dir != 0, (const char *)S.win, w0, (int)n, kmax);
+                    const char *q = dir ? S.rcQ : S.fwdQ;
+                    LvOut r1 = lv_wave<1, NB>(F, t, (int)n - t, (int)glen - t, (int)st.scoreLimit, q, S.rows,
+                                              S.btAct, S.btMatched, tab);
+                    if (r1.score != -1) {
+                        int limitLeft = (int)st.scoreLimit - r1.score;
+                        LvOut r2 = lv_wave<-1, NB>(F, s - 1, s, s + MAX_K, limitLeft, q, S.rows, S.btAct,
+                                                   S.btMatched, tab);
+                        if (r2.score != -1) {
+                            sc = (uint32_t)(r1.score + r2.score);
+                            prob = r1.prob * r2.prob * tab->seedProb;
+                            loc += (uint32_t)r2.netIndel;
+                        }
+                    }
+                }
+                st.nScored++;
+                if (anyNearby) {
+                    uint32_t ebs = uni(el->bestScore);
+                    if (ebs < sc || (ebs == sc && prob <= unid(el->prob))) continue;
+                }
+                el->bestLoc = loc;
+                uint32_t nb = NONE;
+                if (sc != FAIL_SCORE) {
+                    uint32_t nl = elemLoc + (2 * (elemLoc % ELEM / (ELEM / 2)) - 1) * (ELEM / 2);
+                    uint32_t nkey = ((nl / ELEM) << 1) | dir;
+                    nb = uni(chain_find(S.head, ar, nkey));
+                }
+                if (nb != NONE && uni64(ar[nb].scored) != 0) {
+                    Elem *ne = ar + nb;
+                    uint32_t nbase = (uni(ne->key) >> 1) * ELEM;
+                    uint32_t nbl = uni(ne->bestLoc);
+                    if (!((nbase > ebase && loc - nbl <= (uint32_t)ELEM) || (nbase < ebase && nbl <= (uint32_t)ELEM)))
+                        nb = NONE;   // sic: BaseAligner.cpp:1311-1312
+                    if (nb != NONE) {
+                        uint32_t nbs = uni(ne->bestScore);
+                        double np = unid(ne->prob);
+                        if (nbs < sc || (nbs == sc && np >= prob)) continue;
+                        anyNearby = true;
+                        st.pAll = st.pAll - np > 0.0 ? st.pAll - np : 0.0;
+                        ne->prob = 0;
+                    }
+                }
+                double ep = unid(el->prob);
+                st.pAll = st.pAll - ep > 0.0 ? st.pAll - ep : 0.0;
+                st.pAll += prob;
+                el->prob = prob;
+                el->bestScore = sc;
+                if (st.bestScore > sc || (st.bestScore == sc && prob > st.pBest)) {
+                    st.bestScore = sc;
+                    st.pBest = prob;
+                    st.bestLoc = loc;
+                    st.outLoc = loc;
+                    st.outScore = (int32_t)sc;
+                    st.outDir = dir;
+                }
+                if (A.stopOnFirst && st.bestScore <= A.maxK) {
+                    *result = SNAPGPU_MULTIPLE_HITS;
+                    st.outMapq = 0;
+                    return true;
+                }
+                st.scoreLimit = (st.bestScore < A.maxK ? st.bestScore : A.maxK) + A.extra;
+            }
+        }
+        // unlink (allExtantCandidatesScored = true, BaseAligner.cpp:1391-1394)
+        el->allScored = 1;
+        el->sortkey = 0;
+        wave_sync();
+        if ((int)(e % WAVE) == lane) recompute_lane_max(S.laneMax, ar, S.nElems, lane);
+        wave_sync();
+    } while (force);
+    return false;
+}
+
+// ------------------------------------------------------------ hit insertion
+// The per-hit loop of BaseAligner.cpp:829-869 (findCandidate / incrementWeight /
+// allocateNewCandidate) for one seed in one direction.
+template <int MAXLEN>
+__device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem *ar, ReadState &st, uint32_t dir,
+                                            uint32_t offset, uint32_t lim, const uint32_t *list, uint32_t single,
+                                            uint32_t numWeightLists, uint32_t lpsNow) {
+    const int lane = lane_id();
+    const bool allowAlloc = lpsNow <= st.scoreLimit;
+    for (uint32_t b0 = 0; b0 < lim; b0 += WAVE) {
+        uint32_t i = b0 + lane;
+        bool valid = i < lim;
+        uint32_t h = valid ? (list ? list[i] : single) : 0;
+        valid = valid && h >= offset;
+        uint32_t loc = h - offset;
+        uint32_t key = ((loc / ELEM) << 1) | dir;
+        S.scrLoc[lane] = loc;
+        uint32_t slot = 0;
+        if (valid) {
+            uint32_t s = (key * 2654435761u) >> 25;
+            for (;;) {
+                uint32_t old = atomicCAS(&S.btKey[s], NONE, key);
+                if (old == NONE || old == key) break;
+                s = (s + 1) & (BT - 1);
+            }
+            slot = s;
+        }
+        wave_sync();
+        if (valid) atomicOr((unsigned long long *)&S.btMask[slot], 1ull << lane);
+        wave_sync();
+        uint64_t grp = valid ? S.btMask[slot] : 0;
+        bool leader = valid && (__builtin_ctzll(grp) == lane);
+        wave_sync();
+        if (leader) {
+            S.btKey[slot] = NONE;
+            S.btMask[slot] = 0;
+            uint32_t e = chain_find(S.head, ar, key);
+            if (e != NONE || allowAlloc) {
+                uint64_t used = 0;
+                uint32_t weight = 0, allScored = 0, sortkey = 0;
+                if (e != NONE) {
+                    used = ar[e].used; weight = ar[e].weight; allScored = ar[e].allScored; sortkey = ar[e].sortkey;
+                }
+                uint64_t m = grp;
+                while (m) {
+                    int j = __builtin_ctzll(m);
+                    m &= m - 1;
+                    uint32_t bit = S.scrLoc[j] % ELEM;
+                    uint32_t t = st.ts + b0 + j;
+                    if (e == NONE) {
+                        // allocateNewCandidate (BaseAligner.cpp:1485-1568): tail of weight list 1
+                        e = atomicAdd(&S.nElems, 1u);
+                        Elem *ne = ar + e;
+                        ne->key = key;
+                        ne->scored = 0;
+                        ne->lps = (uint8_t)lpsNow;
+                        ne->bestScore = UNUSED_SCORE;
+                        ne->bestLoc = 0;
+                        ne->prob = 0;
+                        ne->next = atomicExch(&S.head[elem_hash(key)], e);
+                        used = 1ull << bit;
+                        weight = 1;
+                        allScored = 0;
+                        sortkey = (1u << 24) | (0xffffffu - t);
+                    } else {
+                        // findCandidate (BaseAligner.cpp:1474-1479) + incrementWeight (1689-1727)
+                        uint64_t cb = 1ull << bit;
+                        allScored = (allScored && (used & cb)) ? 1 : 0;
+                        used |= cb;
+                        if (!allScored && weight < numWeightLists - 1) {
+                            weight++;
+                            sortkey = (weight << 24) | (0xffffffu - t);
+                        }
+                    }
+                    ar[e].seedOffset[bit] = (uint16_t)offset;
+                }
+                ar[e].used = used;
+                ar[e].weight = (uint8_t)weight;
+                ar[e].allScored = (uint8_t)allScored;
+                ar[e].sortkey = sortkey;
+                if (sortkey) atomicMax((unsigned long long *)&S.laneMax[e % WAVE], ((uint64_t)sortkey << 32) | e);
+            }
+        }
+        wave_sync();
+    }
+    st.ts += lim;
+}
+
+// ------------------------------------------------------------- AlignRead
+template <int MAXLEN>
+__device__ void align_one(const KArgs &A, Lds<MAXLEN> &S, Elem *ar, uint32_t r) {
+    constexpr int NB = MAXLEN / 64;
+    const int lane = lane_id();
+    const uint32_t n = A.lengths[r];
+    const uint64_t off = A.offsets[r];
+    const uint32_t seedLen = A.seedLen;
+    ReadState st;
+    st.outLoc = INVALID; st.outDir = 0; st.outScore = (int32_t)UNUSED_SCORE; st.outMapq = 0;
+    st.popular = 0; st.pAll = 0; st.pBest = 0;
+    st.nLookups = st.nScored = st.nHitsIgnored = st.nProbes = st.nHitWords = st.nOvf = 0;
+    st.ts = 0;
+    st.nSeedsApplied[0] = st.nSeedsApplied[1] = 0;
+    uint32_t flags = 0;
+    int result = SNAPGPU_NOT_FOUND;
+    const uint32_t maxSeeds = A.maxSeedsCmd ? A.maxSeedsCmd : (uint32_t)(int)(A.seedCoverage * n / seedLen);
+    const uint32_t numWeightLists = maxSeeds + 1;
+    bool run = true;
+    if (n > A.maxReadSize || n > (uint32_t)MAXLEN) { flags |= SNAPGPU_FLAG_READ_TOO_LONG; run = false; }
+    else if (n < seedLen) run = false;
+    uint32_t rbF[NB], rbR[NB];
+    if (run) {
+        // Read::init upper-casing + BaseAligner.cpp:636-650 (RC read, qualities)
+        uint32_t nN = 0;
+        for (int i = lane; i < MAXLEN + 64; i += WAVE) {
+            uint32_t c = 0, q = 0;
+            if (i < (int)n) {
+                c = (uint8_t)A.bases[off + i];
+                q = (uint8_t)A.quals[off + i];
+                if (c >= 'a' && c <= 'z') c -= 0x20;
+                S.rc[n - 1 - i] = (char)complement_of(c);
+                S.rcQ[n - 1 - i] = (char)q;
+            } else {
+                S.rc[i] = 0;
+                S.rcQ[i] = 0;
+            }
+            S.fwd[i] = (char)c;
+            S.fwdQ[i] = (char)q;
+            nN += __popcll(ballot(i < (int)n && c == 'N'));
+        }
+        for (int i = lane; i < NBUCKET; i += WAVE) S.head[i] = NONE;
+        for (int i = lane; i < BT; i += WAVE) { S.btKey[i] = NONE; S.btMask[i] = 0; }
+        S.laneMax[lane] = 0;
+        if (lane == 0) S.nElems = 0;
+        wave_sync();
+#pragma unroll
+        for (int b = 0; b < NB; b++) { rbF[b] = (uint8_t)S.fwd[b * 64 + lane]; rbR[b] = (uint8_t)S.rc[b * 64 + lane]; }
+        if (nN > A.maxK) { flags |= SNAPGPU_FLAG_TOO_MANY_NS; run = false; }
+    }
+    if (run) {
+        st.lps[0] = st.lps[1] = 0;
+        st.mostSeeds[0] = st.mostSeeds[1] = 1;
+        st.bestScore = UNUSED_SCORE;
+        st.bestLoc = 0;
+        st.scoreLimit = A.maxK + A.extra;
+        const uint32_t nPossible = n - seedLen + 1;
+        uint64_t *seedUsed = S.seedUsed;
+        if (lane <= NB) seedUsed[lane] = 0;
+        wave_sync();
+        uint32_t next = 0, wrapCount = 0;
+        bool done = false;
+        while (st.nSeedsApplied[0] + st.nSeedsApplied[1] < maxSeeds) {
+            if (next >= nPossible) {
+                wrapCount++;
+                if (wrapCount >= seedLen) {
+                    score_wave<MAXLEN>(A, S, ar, st, true, n, rbF, rbR, &result, &flags);
+                    done = true;
+                    break;
+                }
+                next = A.tab->wrap[wrapCount];
+                st.mostSeeds[0] = st.mostSeeds[1] = wrapCount + 1;
+            }
+            while (next < nPossible && ((uni64(seedUsed[next >> 6]) >> (next & 63)) & 1)) next++;
+            if (next >= nPossible) continue;
+            {
+                uint64_t w = uni64(seedUsed[next >> 6]) | (1ull << (next & 63));
+                wave_sync();
+                seedUsed[next >> 6] = w;
+                wave_sync();
+            }
+            // Seed::DoesTextRepresentASeed + Seed::Seed (Seed.cpp:28-42, Seed.h:38-51)
+            int v = lane < (int)seedLen ? base_value((uint8_t)S.fwd[next + lane]) : 0;
+            if (ballot(lane < (int)seedLen && v > 3)) continue;
+            uint64_t fpart = lane < (int)seedLen ? (uint64_t)v << ((seedLen - lane - 1) * 2) : 0;
+            uint64_t rpart = lane < (int)seedLen ? (uint64_t)(v ^ 3) << (lane * 2) : 0;
+            const uint64_t f = uni64(or_reduce64(fpart));
+            const uint64_t rcv = uni64(or_reduce64(rpart));
+            // GenomeIndex::lookupSeed + SNAPHashTable::Lookup
+            const bool comp = (int64_t)f > (int64_t)rcv;
+            const uint64_t canon = comp ? rcv : f;
+            const uint32_t table = (uint32_t)(canon >> 32);
+            const uint32_t key = (uint32_t)canon;
+            const uint64_t size = A.tableSize[table];
+            const uint32_t *T = A.slots + 3 * A.tableBase[table];
+            const uint64_t h0 = fmix32(key) % size;
+            bool found = false;
+            uint32_t v1 = 0, v2 = 0;
+            for (uint32_t j0 = 0;; j0 += 8) {
+                uint32_t j = j0 + (lane & 7);
+                uint64_t S_j = j <= 4 ? (uint64_t)j * (j + 1) * (2 * j + 1) / 6 : 30 + (uint64_t)(j - 4);
+                uint64_t pos = (h0 + S_j) % size;
+                uint32_t kj = 0, v1j = INVALID, v2j = 0;
+                bool beyond = j > size + 5;
+                if (lane < 8 && !beyond) { kj = T[3 * pos]; v1j = T[3 * pos + 1]; v2j = T[3 * pos + 2]; }
+                bool stop = (j == 0) ? (kj == key && v1j != INVALID) : (kj == key || v1j == INVALID);
+                uint64_t m = ballot(lane < 8 && (stop || beyond)) & 0xffull;
+                if (m) {
+                    int jl = __builtin_ctzll(m);
+                    uint32_t jj = j0 + jl;
+                    bool bey = readlane(beyond ? 1 : 0, jl);
+                    st.nProbes += bey ? jj : jj + 1;
+                    uint32_t kv1 = readlaneu(v1j, jl);
+                    if (!bey && (jj == 0 || kv1 != INVALID)) { found = true; v1 = kv1; v2 = readlaneu(v2j, jl); }
+                    break;
+                }
+            }
+            // fillInLookedUpResults (GenomeIndex.cpp:1013-1086), both directions
+            uint32_t nH0 = 0, nH1 = 0, sg0 = 0, sg1 = 0;
+            const uint32_t *ls0 = nullptr, *ls1 = nullptr;
+            if (found) {
+                uint32_t vf = comp ? v2 : v1, vr = comp ? v1 : v2;
+                if (vf < A.nBases) { nH0 = 1; sg0 = vf; }
+                else if (vf != UNUSED_SIDE) { uint32_t o = vf - A.nBases; nH0 = uni(A.overflow[o]); ls0 = A.overflow + o + 1; st.nOvf++; }
+                if (f == rcv) { nH1 = nH0; sg1 = sg0; ls1 = ls0; }   // palindrome (GenomeIndex.cpp:1003-1006)
+                else if (vr < A.nBases) { nH1 = 1; sg1 = vr; }
+                else if (vr != UNUSED_SIDE) { uint32_t o = vr - A.nBases; nH1 = uni(A.overflow[o]); ls1 = A.overflow + o + 1; st.nOvf++; }
+            }
+            st.nLookups++;
+            bool applied = false;
+#pragma unroll
+            for (uint32_t dir = 0; dir < 2; dir++) {
+                const uint32_t nh = dir ? nH1 : nH0;
+                if (nh > A.maxHits && !A.explore) {
+                    st.nHitsIgnored++;
+                    st.popular++;
+                } else {
+                    uint32_t offset = dir == 0 ? next : n - seedLen - next;
+                    uint32_t lim = nh < A.maxHits ? nh : A.maxHits;
+                    st.nHitWords += lim;
+                    insert_hits<MAXLEN>(A, S, ar, st, dir, offset, lim, dir ? ls1 : ls0, dir ? sg1 : sg0,
+                                        numWeightLists, dir ? st.lps[1] : st.lps[0]);
+                    if (dir) st.nSeedsApplied[1]++; else st.nSeedsApplied[0]++;
+                    applied = true;
+                }
+            }
+            next += seedLen;
+            if (applied && score_wave<MAXLEN>(A, S, ar, st, false, n, rbF, rbR, &result, &flags)) { done = true; break; }
+        }
+        if (!done) score_wave<MAXLEN>(A, S, ar, st, true, n, rbF, rbR, &result, &flags);
+    }
+    if (lane == 0) {
+        snapgpu_result_t o;
+        o.location = st.outLoc;
+        o.score = st.outScore;
+        o.mapq = st.outMapq;
+        o.result = (uint8_t)result;
+        o.direction = (uint8_t)st.outDir;
+        o.flags = (uint8_t)flags;
+        o.reserved = 0;
+        o.nLookups = st.nLookups;
+        o.nLocationsScored = st.nScored;
+        o.popularSeedsSkipped = (uint16_t)st.popular;
+        o.nHitsIgnored = (uint16_t)st.nHitsIgnored;
+        o.nProbes = st.nProbes;
+        o.nHitWords = st.nHitWords;
+        o.nOverflowLists = st.nOvf;
+        o.nElements = run ? S.nElems : 0;
+        o.reserved2 = 0;
+        o.probabilityOfAllCandidates = st.pAll;
+        o.probabilityOfBestCandidate = st.pBest;
+        A.out[r] = o;
+    }
+    wave_sync();
+}
+
+template <int MAXLEN>
+__global__ __launch_bounds__(64) void align_kernel(KArgs A) {
+    __shared__ Lds<MAXLEN> S;
+    Elem *ar = A.arena + (uint64_t)blockIdx.x * A.arenaElems;
+    const int lane = lane_id();
+    for (;;) {
+        uint32_t r = 0;
+        if (lane == 0) r = atomicAdd(A.counter, 1u);
+        r = uni((uint32_t)readlane((int)r, 0));
+        if (r >= A.nReads) break;
+        align_one<MAXLEN>(A, S, ar, r);
+    }
+}
+
+// LV parity kernel: one wave per task; the task's "read" and virtual genome are
+// prepared on the host (see snapgpu_lv_batch).
+struct LvTask {
+    uint64_t readOff;   // into reads / quals buffers
+    uint64_t genOff;    // into genome buffer: position of virtual genome coordinate 0
+    int32_t n, p0, patternLen, textLen, k, g, dir, pad;
+};
+
+__global__ __launch_bounds__(64) void lv_kernel(const LvTask *tasks, const char *reads, const char *quals,
+                                                const char *gbuf, const DevTables *tab, int32_t *outScore,
+                                                int32_t *outNet, double *outProb) {
+    __shared__ Lds<512> S;
+    const int lane = lane_id();
+    const LvTask T = tasks[blockIdx.x];
+    for (int i = lane; i < 512 + 64; i += WAVE) {
+        S.fwd[i] = i < T.n ? reads[T.readOff + i] : 0;
+        S.fwdQ[i] = i < T.n ? quals[T.readOff + i] : 0;
+    }
+    wave_sync();
+    uint32_t rb[8];
+#pragma unroll
+    for (int b = 0; b < 8; b++) rb[b] = (uint8_t)S.fwd[b * 64 + lane];
+    int w0 = stage_window(S, gbuf + T.genOff, (uint32_t)T.g, T.n);
+    Bitmap<8> F;
+    int kmax = T.k < MAX_K - 1 ? T.k : MAX_K - 1;
+    if (kmax < 0) kmax = 0;
+    build_bitmap<8>(F, rb, rb, false, (const char *)S.win, w0, T.n, kmax);
+    LvOut r = T.dir > 0 ? lv_wave<1, 8>(F, T.p0, T.patternLen, T.textLen, T.k, S.fwdQ, S.rows, S.btAct, S.btMatched, tab)
+                        : lv_wave<-1, 8>(F, T.p0, T.patternLen, T.textLen, T.k, S.fwdQ, S.rows, S.btAct, S.btMatched, tab);
+    if (lane == 0) { outScore[blockIdx.x] = r.score; outNet[blockIdx.x] = r.netIndel; outProb[blockIdx.x] = r.prob; }
+}
+
+}  // namespace sgk
+
+// ======================================================================= host
+namespace {
+
+std::mutex g_errMu;
+
+#define HIPCHK(x)                                                                       \
+    do {                                                                                \
+        hipError_t e_ = (x);                                                            \
+        if (e_ != hipSuccess) {                                                         \
+            snapgpu::setError(std::string(#x) + ": " + hipGetErrorString(e_));          \
+            return SNAPGPU_EDEVICE;                                                     \
+        }                                                                               \
+    } while (0)
+#define HIPCHKN(x)                                                                      \
+    do {                                                                                \
+        hipError_t e_ = (x);                                                            \
+        if (e_ != hipSuccess) {                                                         \
+            snapgpu::setError(std::string(#x) + ": " + hipGetErrorString(e_));          \
+            return nullptr;                                                             \
+        }                                                                               \
+    } while (0)
+
+// libgcc __powidf2 (see oracle / DESIGN.md): the reference's pow(double, int).
+double powi_libgcc(double x, int m) {
+    unsigned nn = m < 0 ? -(unsigned)m : (unsigned)m;
+    double y = (nn % 2) ? x : 1;
+    while (nn >>= 1) { x = x * x; if (nn % 2) y = y * x; }
+    return m < 0 ? 1 / y : y;
+}
+
+const uint8_t kWrap[10][25] = {   // SeedSequencer.h:28-287
+    {0, 8, 4, 12, 2, 6, 10, 14, 1, 3, 5, 7, 9, 11, 13, 15},
+    {0, 8, 4, 12, 2, 6, 10, 14, 1, 3, 5, 7, 9, 11, 13, 15, 16},
+    {0, 9, 4, 13, 2, 6, 11, 15, 1, 3, 5, 7, 8, 10, 12, 14, 16, 17},
+    {0, 10, 4, 14, 2, 6, 8, 12, 16, 18, 1, 3, 5, 7, 9, 11, 13, 15, 17},
+    {0, 10, 5, 15, 2, 7, 12, 17, 3, 9, 11, 13, 19, 1, 4, 6, 8, 14, 18, 16},
+    {0, 11, 6, 16, 3, 9, 13, 17, 18, 2, 5, 8, 15, 20, 1, 4, 7, 10, 12, 14, 19},
+    {0, 11, 6, 16, 3, 9, 14, 19, 2, 7, 12, 17, 20, 4, 1, 10, 13, 15, 18, 21, 5, 8},
+    {0, 12, 6, 17, 3, 9, 20, 14, 1, 4, 7, 10, 15, 18, 21, 4, 2, 5, 11, 16, 19, 22, 8},
+    {0, 12, 6, 18, 3, 15, 21, 9, 1, 13, 19, 7, 16, 4, 22, 10, 2, 14, 20, 5, 17, 8, 23, 11},
+    {0, 13, 6, 19, 3, 16, 22, 9, 11, 1, 14, 7, 20, 4, 17, 23, 2, 15, 5, 21, 8, 24, 10, 18, 12},
+};
+
+// initializeLVProbabilitiesToPhredPlus33 (LandauVishkin.cpp:601-649), host glibc.
+void fillTables(DevTables &t, uint32_t seedLen) {
+    memset(&t, 0, sizeof(t));
+    t.indel[0] = 1.0;
+    t.indel[1] = 0.001;
+    for (int i = 2; i < 64; i++) t.indel[i] = t.indel[i - 1] * 0.5;
+    for (int i = 0; i < 33; i++) t.phred[i] = 0.001;
+    for (int i = 33; i <= 93 + 33; i++) t.phred[i] = 1.0 - (1.0 - pow(10.0, -1.0 * (i - 33.0) / 10.0)) * (1.0 - 0.001);
+    for (int i = 93 + 33 + 1; i < 256; i++) t.phred[i] = 0.001;
+    t.perfect[0] = 1.0;
+    for (int i = 1; i < 512; i++) t.perfect[i] = t.perfect[i - 1] * (1 - 0.001);
+    t.seedProb = powi_libgcc(1 - 0.001, (int)seedLen);
+    if (seedLen >= 16 && seedLen <= 25)
+        for (int i = 0; i < 25; i++) t.wrap[i] = kWrap[seedLen - 16][i];
+}
+
+int hostMapq(double pAll, double pBest, int score, int popular) {   // mapq.h:32-65
+    if (pAll < pBest) pAll = pBest;
+    if (pAll == pBest && popular == 0 && score < 5) return 70;
+    double c = pBest / pAll;
+    int base;
+    if (c >= 1) base = 69;
+    else { base = (int)(-10 * log10(1 - c)); if (base > 69) base = 69; }
+    int pen = popular - 10;
+    if (pen < 0) pen = 0;
+    base -= pen / 2;
+    return base < 0 ? 0 : base;
+}
+
+}  // namespace
+
+struct snapgpu_device_reads {
+    char *dBases = nullptr, *dQuals = nullptr;
+    uint64_t *dOffsets = nullptr;
+    uint32_t *dLengths = nullptr;
+    snapgpu_result_t *dOut = nullptr;
+    uint64_t n = 0;
+    uint32_t maxLen = 0;
+    int device = 0;
+};
+
+struct snapgpu_aligner {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    const snapgpu_index_t *idx = nullptr;
+    snapgpu_aligner_params_t p{};
+    uint32_t *dSlots = nullptr, *dOverflow = nullptr, *dPieces = nullptr, *dCounter = nullptr;
+    uint64_t *dTableBase = nullptr, *dTableSize = nullptr;
+    char *dGenomeAlloc = nullptr;
+    const char *dGenome = nullptr;
+    DevTables *dTab = nullptr;
+    Elem *dArena = nullptr;
+    uint64_t arenaElems = 0;
+    int grid = 0;
+    hipEvent_t ev[4] = {};
+    snapgpu_timing_t timing{};
+    snapgpu_aligner_stats_t stats{};
+    snapgpu_device_reads_t *lastReads = nullptr;
+};
+
+static const size_t kDevGuard = 1024;
+
+extern "C" {
+
+void snapgpu_aligner_params_default(snapgpu_aligner_params_t *p) {
+    // AlignerOptions.cpp:33-85 defaults used by SingleAligner.cpp:167-179
+    p->maxHitsToConsider = 300;
+    p->maxK = 14;
+    p->maxReadSize = 500;
+    p->maxSeedsToUse = 25;
+    p->maxSeedCoverage = 0;
+    p->extraSearchDepth = 2;
+    p->explorePopularSeeds = 0;
+    p->stopOnFirstHit = 0;
+}
+
+int snapgpu_compute_mapq(double pAll, double pBest, int score, int popular) { return hostMapq(pAll, pBest, score, popular); }
+
+int snapgpu_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+void snapgpu_aligner_free(snapgpu_aligner_t *a) {
+    if (!a) return;
+    hipSetDevice(a->device);
+    hipFree(a->dSlots); hipFree(a->dOverflow); hipFree(a->dPieces); hipFree(a->dCounter);
+    hipFree(a->dTableBase); hipFree(a->dTableSize); hipFree(a->dGenomeAlloc); hipFree(a->dTab); hipFree(a->dArena);
+    for (auto &e : a->ev) if (e) hipEventDestroy(e);
+    if (a->stream) hipStreamDestroy(a->stream);
+    delete a;
+}
+
+snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx, const snapgpu_aligner_params_t *params) {
+    if (!idx || !params) { snapgpu::setError("aligner_create: null argument"); return nullptr; }
+    if (params->maxK + params->extraSearchDepth > (uint32_t)MAX_K) {   // SingleAligner.cpp:117-121
+        snapgpu::setError("maxK + extraSearchDepth must be <= MAX_K (31)");
+        return nullptr;
+    }
+    if (params->maxReadSize > 512) { snapgpu::setError("maxReadSize > 512 unsupported"); return nullptr; }
+    if (idx->seedLen < 16 || idx->seedLen > 25) { snapgpu::setError("seedLen must be 16..25 (SeedSequencer.h)"); return nullptr; }
+    int ndev = snapgpu_device_count();
+    if (ndev <= 0 || device < 0 || device >= ndev) { snapgpu::setError("no such HIP device"); return nullptr; }
+    auto *a = new snapgpu_aligner_t();
+    a->device = device;
+    a->idx = idx;
+    a->p = *params;
+    auto fail = [&](const char *what, hipError_t e) {
+        snapgpu::setError(std::string(what) + ": " + hipGetErrorString(e));
+        snapgpu_aligner_free(a);
+        return (snapgpu_aligner_t *)nullptr;
+    };
+    hipError_t e;
+    if ((e = hipSetDevice(device)) != hipSuccess) return fail("hipSetDevice", e);
+    if ((e = hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking)) != hipSuccess) return fail("stream", e);
+    for (auto &ev : a->ev) if ((e = hipEventCreate(&ev)) != hipSuccess) return fail("event", e);
+    // index upload: genome with guards, tables, overflow, pieces
+    const uint32_t nBases = idx->genome->nBases;
+    size_t gbytes = kDevGuard + nBases + kDevGuard;
+    if ((e = hipMalloc(&a->dGenomeAlloc, gbytes)) != hipSuccess) return fail("hipMalloc genome", e);
+    {
+        std::vector<char> pad(kDevGuard, 'n');
+        hipMemcpy(a->dGenomeAlloc, pad.data(), kDevGuard, hipMemcpyHostToDevice);
+        hipMemcpy(a->dGenomeAlloc + kDevGuard, idx->genome->bases(), nBases, hipMemcpyHostToDevice);
+        if ((e = hipMemcpy(a->dGenomeAlloc + kDevGuard + nBases, pad.data(), kDevGuard, hipMemcpyHostToDevice)) != hipSuccess)
+            return fail("genome upload", e);
+    }
+    a->dGenome = a->dGenomeAlloc + kDevGuard;
+    if ((e = hipMalloc(&a->dSlots, idx->slots.size() * 4)) != hipSuccess) return fail("hipMalloc slots", e);
+    if ((e = hipMemcpy(a->dSlots, idx->slots.data(), idx->slots.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return fail("slots", e);
+    if ((e = hipMalloc(&a->dOverflow, idx->overflow.size() * 4 + 16)) != hipSuccess) return fail("hipMalloc ovf", e);
+    if (!idx->overflow.empty() &&
+        (e = hipMemcpy(a->dOverflow, idx->overflow.data(), idx->overflow.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return fail("ovf", e);
+    if ((e = hipMalloc(&a->dTableBase, idx->nTables * 8)) != hipSuccess) return fail("tb", e);
+    if ((e = hipMalloc(&a->dTableSize, idx->nTables * 8)) != hipSuccess) return fail("ts", e);
+    hipMemcpy(a->dTableBase, idx->tableBase.data(), idx->nTables * 8, hipMemcpyHostToDevice);
+    hipMemcpy(a->dTableSize, idx->tableSize.data(), idx->nTables * 8, hipMemcpyHostToDevice);
+    size_t np = idx->genome->pieceOffsets.size();
+    if ((e = hipMalloc(&a->dPieces, np * 4 + 16)) != hipSuccess) return fail("pieces", e);
+    if (np) hipMemcpy(a->dPieces, idx->genome->pieceOffsets.data(), np * 4, hipMemcpyHostToDevice);
+    DevTables t;
+    fillTables(t, idx->seedLen);
+    if ((e = hipMalloc(&a->dTab, sizeof(DevTables))) != hipSuccess) return fail("tables", e);
+    hipMemcpy(a->dTab, &t, sizeof(t), hipMemcpyHostToDevice);
+    if ((e = hipMalloc(&a->dCounter, 64)) != hipSuccess) return fail("counter", e);
+    // persistent grid: waves resident on the device; element arena per wave
+    hipDeviceProp_t prop;
+    hipGetDeviceProperties(&prop, device);
+    int perCU = 0;
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, (const void *)align_kernel<128>, 64, 0);
+    if (perCU <= 0) perCU = 8;
+    a->grid = prop.multiProcessorCount * perCU;
+    uint32_t maxSeeds = params->maxSeedsToUse ? params->maxSeedsToUse
+                                              : (uint32_t)(params->maxSeedCoverage * params->maxReadSize / idx->seedLen);
+    a->arenaElems = (uint64_t)(maxSeeds + 2) * params->maxHitsToConsider + 64;
+    const uint64_t budget = 24ull << 30;   // HBM for arenas
+    while (a->grid > 64 && (uint64_t)a->grid * a->arenaElems * sizeof(Elem) > budget) a->grid /= 2;
+    if ((e = hipMalloc(&a->dArena, (uint64_t)a->grid * a->arenaElems * sizeof(Elem))) != hipSuccess) return fail("arena", e);
+    if ((e = hipDeviceSynchronize()) != hipSuccess) return fail("sync", e);
+    return a;
+}
+
+snapgpu_device_reads_t *snapgpu_reads_upload(snapgpu_aligner_t *a, const snapgpu_reads_t *r) {
+    if (!a || !r) { snapgpu::setError("reads_upload: null"); return nullptr; }
+    HIPCHKN(hipSetDevice(a->device));
+    auto *d = new snapgpu_device_reads_t();
+    d->n = r->n;
+    d->device = a->device;
+    uint64_t bytes = 0;
+    for (uint64_t i = 0; i < r->n; i++) {
+        uint64_t endb = r->offsets[i] + r->lengths[i];
+        if (endb > bytes) bytes = endb;
+        if (r->lengths[i] > d->maxLen) d->maxLen = r->lengths[i];
+    }
+    bytes += 64;
+    HIPCHKN(hipMalloc(&d->dBases, bytes));
+    HIPCHKN(hipMalloc(&d->dQuals, bytes));
+    HIPCHKN(hipMalloc(&d->dOffsets, (r->n + 1) * 8));
+    HIPCHKN(hipMalloc(&d->dLengths, (r->n + 1) * 4));
+    HIPCHKN(hipMalloc(&d->dOut, (r->n + 1) * sizeof(snapgpu_result_t)));
+    HIPCHKN(hipMemsetAsync(d->dBases, 0, bytes, a->stream));
+    HIPCHKN(hipMemsetAsync(d->dQuals, 0, bytes, a->stream));
+    HIPCHKN(hipMemcpyAsync(d->dBases, r->bases, bytes - 64, hipMemcpyHostToDevice, a->stream));
+    HIPCHKN(hipMemcpyAsync(d->dQuals, r->quals, bytes - 64, hipMemcpyHostToDevice, a->stream));
+    HIPCHKN(hipMemcpyAsync(d->dOffsets, r->offsets, r->n * 8, hipMemcpyHostToDevice, a->stream));
+    HIPCHKN(hipMemcpyAsync(d->dLengths, r->lengths, r->n * 4, hipMemcpyHostToDevice, a->stream));
+    HIPCHKN(hipStreamSynchronize(a->stream));
+    return d;
+}
+
+void snapgpu_device_reads_free(snapgpu_device_reads_t *d) {
+    if (!d) return;
+    hipSetDevice(d->device);
+    hipFree(d->dBases); hipFree(d->dQuals); hipFree(d->dOffsets); hipFree(d->dLengths); hipFree(d->dOut);
+    delete d;
+}
+
+int snapgpu_align_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d) {
+    if (!a || !d) return SNAPGPU_EINVAL;
+    HIPCHK(hipSetDevice(a->device));
+    if (d->n == 0) return SNAPGPU_OK;
+    if (d->n > 0xffffffffull) { snapgpu::setError("batch too large"); return SNAPGPU_EINVAL; }
+    KArgs A;
+    memset(&A, 0, sizeof(A));
+    const snapgpu_index_t *idx = a->idx;
+    A.slots = a->dSlots; A.tableBase = a->dTableBase; A.tableSize = a->dTableSize; A.overflow = a->dOverflow;
+    A.genome = a->dGenome; A.pieces = a->dPieces; A.nPieces = (int32_t)idx->genome->pieceOffsets.size();
+    A.nBases = idx->genome->nBases; A.seedLen = idx->seedLen; A.nTables = idx->nTables;
+    A.padding = idx->genome->chromosomePadding;
+    A.maxHits = a->p.maxHitsToConsider; A.maxK = a->p.maxK; A.maxReadSize = a->p.maxReadSize;
+    A.maxSeedsCmd = a->p.maxSeedsToUse; A.seedCoverage = a->p.maxSeedCoverage; A.extra = a->p.extraSearchDepth;
+    A.explore = a->p.explorePopularSeeds; A.stopOnFirst = a->p.stopOnFirstHit; A.kRows = 31;
+    A.tab = a->dTab;
+    A.bases = d->dBases; A.quals = d->dQuals; A.offsets = d->dOffsets; A.lengths = d->dLengths;
+    A.nReads = (uint32_t)d->n; A.out = d->dOut;
+    A.counter = a->dCounter; A.arena = a->dArena; A.arenaElems = a->arenaElems;
+    int grid = a->grid;
+    if ((uint64_t)grid > d->n) grid = (int)d->n;
+    HIPCHK(hipMemsetAsync(a->dCounter, 0, 64, a->stream));
+    HIPCHK(hipEventRecord(a->ev[0], a->stream));
+    if (d->maxLen <= 128) hipLaunchKernelGGL(align_kernel<128>, dim3(grid), dim3(64), 0, a->stream, A);
+    else hipLaunchKernelGGL(align_kernel<512>, dim3(grid), dim3(64), 0, a->stream, A);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(a->ev[1], a->stream));
+    a->lastReads = d;
+    return SNAPGPU_OK;
+}
+
+int snapgpu_synchronize(snapgpu_aligner_t *a) {
+    if (!a) return SNAPGPU_EINVAL;
+    HIPCHK(hipStreamSynchronize(a->stream));
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, a->ev[0], a->ev[1]) == hipSuccess) a->timing.mainKernelMs = ms;
+    return SNAPGPU_OK;
+}
+
+int snapgpu_results_download(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, snapgpu_result_t *out) {
+    if (!a || !d || !out) return SNAPGPU_EINVAL;
+    HIPCHK(hipSetDevice(a->device));
+    HIPCHK(hipMemcpyAsync(out, d->dOut, d->n * sizeof(snapgpu_result_t), hipMemcpyDeviceToHost, a->stream));
+    int rc = snapgpu_synchronize(a);
+    if (rc) return rc;
+    // host MAPQ fix-ups (device log10 within 1e-6 of an integer boundary)
+    auto t0 = std::chrono::steady_clock::now();
+    uint64_t fixed = 0;
+    for (uint64_t i = 0; i < d->n; i++) {
+        snapgpu_result_t &o = out[i];
+        if (o.flags & SNAPGPU_FLAG_MAPQ_FIXED) {
+            o.mapq = hostMapq(o.probabilityOfAllCandidates, o.probabilityOfBestCandidate, o.score, o.popularSeedsSkipped);
+            o.result = o.mapq >= 10 ? SNAPGPU_SINGLE_HIT : SNAPGPU_MULTIPLE_HITS;
+            fixed++;
+        }
+        a->stats.nHashTableLookups += o.nLookups;
+        a->stats.nLocationsScored += o.nLocationsScored;
+        a->stats.nHitsIgnoredBecauseOfTooHighPopularity += o.nHitsIgnored;
+        a->stats.nReadsIgnoredBecauseOfTooManyNs += (o.flags & SNAPGPU_FLAG_TOO_MANY_NS) ? 1 : 0;
+        a->stats.nReads++;
+    }
+    a->timing.nMapqFixed = fixed;
+    a->timing.fixupMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return SNAPGPU_OK;
+}
+
+int snapgpu_align_batch(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, snapgpu_result_t *out) {
+    if (!a || !reads || !out) return SNAPGPU_EINVAL;
+    snapgpu_device_reads_t *d = snapgpu_reads_upload(a, reads);
+    if (!d) return SNAPGPU_EDEVICE;
+    int rc = snapgpu_align_resident(a, d);
+    if (!rc) rc = snapgpu_results_download(a, d, out);
+    snapgpu_device_reads_free(d);
+    a->lastReads = nullptr;
+    return rc;
+}
+
+int snapgpu_last_timing(snapgpu_aligner_t *a, snapgpu_timing_t *t) {
+    if (!a || !t) return SNAPGPU_EINVAL;
+    *t = a->timing;
+    return SNAPGPU_OK;
+}
+
+int snapgpu_aligner_get_stats(const snapgpu_aligner_t *a, snapgpu_aligner_stats_t *s) {
+    if (!a || !s) return SNAPGPU_EINVAL;
+    *s = a->stats;
+    return SNAPGPU_OK;
+}
+int snapgpu_aligner_max_k(const snapgpu_aligner_t *a) { return a ? (int)a->p.maxK : -1; }
+const char *snapgpu_aligner_name(const snapgpu_aligner_t *) { return "Base Aligner (MI355X)"; }
+
+int snapgpu_lv_batch(int device, int direction, uint32_t n, const char *texts, const uint64_t *textOff,
+                     const uint32_t *textLen, const char *patterns, const char *quals, const uint64_t *patOff,
+                     const uint32_t *patLen, const int32_t *k, int32_t *outScore, int32_t *outNetIndel,
+                     double *outProb) {
+    if (n == 0) return SNAPGPU_OK;
+    int ndev = snapgpu_device_count();
+    if (ndev <= 0 || device >= ndev) { snapgpu::setError("no such HIP device"); return SNAPGPU_EDEVICE; }
+    HIPCHK(hipSetDevice(device));
+    std::vector<LvTask> tasks(n);
+    std::vector<char> rbuf, qbuf, gbuf;
+    const int PADG = 512;
+    for (uint32_t i = 0; i < n; i++) {
+        int pl = (int)patLen[i], tl = (int)textLen[i];
+        if (pl > 500) { snapgpu::setError("lv_batch: pattern longer than 500"); return SNAPGPU_EINVAL; }
+        LvTask &T = tasks[i];
+        T.readOff = rbuf.size();
+        // "read" in read coordinates: forward = pattern, reverse = reversed pattern
+        for (int j = 0; j < pl; j++) {
+            int src = direction > 0 ? j : pl - 1 - j;
+            rbuf.push_back(patterns[patOff[i] + src]);
+            qbuf.push_back(quals[patOff[i] + src]);
+        }
+        for (int j = 0; j < 64; j++) { rbuf.push_back(0); qbuf.push_back(0); }
+        // virtual genome: 'n' * PADG + text + 'n' * PADG (the reference harness pads with 'n')
+        uint64_t gstart = gbuf.size();
+        gbuf.insert(gbuf.end(), PADG, 'n');
+        gbuf.insert(gbuf.end(), texts + textOff[i], texts + textOff[i] + tl);
+        gbuf.insert(gbuf.end(), PADG, 'n');
+        while (gbuf.size() % 4) gbuf.push_back('n');
+        T.n = pl;
+        T.patternLen = pl;
+        T.textLen = tl;
+        T.k = k[i];
+        T.dir = direction > 0 ? 1 : -1;
+        if (direction > 0) { T.p0 = 0; T.g = PADG; }
+        else { T.p0 = pl - 1; T.g = PADG + tl - pl; }
+        T.genOff = gstart;
+    }
+    LvTask *dT; char *dR, *dQ, *dG; DevTables *dTab; int32_t *dS, *dN; double *dP;
+    DevTables t;
+    fillTables(t, 20);
+    HIPCHK(hipMalloc(&dT, n * sizeof(LvTask)));
+    HIPCHK(hipMalloc(&dR, rbuf.size() + 64));
+    HIPCHK(hipMalloc(&dQ, qbuf.size() + 64));
+    HIPCHK(hipMalloc(&dG, gbuf.size() + 64));
+    HIPCHK(hipMalloc(&dTab, sizeof(DevTables)));
+    HIPCHK(hipMalloc(&dS, n * 4));
+    HIPCHK(hipMalloc(&dN, n * 4));
+    HIPCHK(hipMalloc(&dP, n * 8));
+    hipMemcpy(dT, tasks.data(), n * sizeof(LvTask), hipMemcpyHostToDevice);
+    hipMemcpy(dR, rbuf.data(), rbuf.size(), hipMemcpyHostToDevice);
+    hipMemcpy(dQ, qbuf.data(), qbuf.size(), hipMemcpyHostToDevice);
+    hipMemcpy(dG, gbuf.data(), gbuf.size(), hipMemcpyHostToDevice);
+    hipMemcpy(dTab, &t, sizeof(t), hipMemcpyHostToDevice);
+    hipLaunchKernelGGL(lv_kernel, dim3(n), dim3(64), 0, 0, dT, dR, dQ, dG, dTab, dS, dN, dP);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipDeviceSynchronize());
+    hipMemcpy(outScore, dS, n * 4, hipMemcpyDeviceToHost);
+    hipMemcpy(outNetIndel, dN, n * 4, hipMemcpyDeviceToHost);
+    hipMemcpy(outProb, dP, n * 8, hipMemcpyDeviceToHost);
+    hipFree(dT); hipFree(dR); hipFree(dQ); hipFree(dG); hipFree(dTab); hipFree(dS); hipFree(dN); hipFree(dP);
+    return SNAPGPU_OK;
+}
+
+}  // extern "C"

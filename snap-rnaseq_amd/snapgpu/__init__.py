@@ -1,0 +1,356 @@
+"""snapgpu -- MI355X-native drop-in for SNAP's BaseAligner hot path.
+
+Python mirror of the reference's C++ surface (SNAPLib/Aligner.h:54-80,
+SNAPLib/BaseAligner.h:44-142, SNAPLib/GenomeIndex.h) over the C ABI of
+include/snapgpu.h.  Every call goes to the native library: genome/index work is
+host C++, alignment is HIP on gfx950.  There is no CPU fallback -- creating a
+BaseAligner without a GPU raises.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _ffi
+from ._ffi import lib, last_error
+
+NotFound, SingleHit, MultipleHits, UnknownAlignment = 0, 1, 2, 3   # Read.h:41
+FORWARD, RC = 0, 1                                                  # directions.h:26-35
+InvalidGenomeLocation = 0xFFFFFFFF                                  # Genome.h:29
+UnusedScoreValue = 0xFFFF                                           # BaseAligner.h:261
+
+FLAG_READ_TOO_LONG = 0x01
+FLAG_MAPQ_FIXED = 0x02
+FLAG_TOO_MANY_NS = 0x08
+
+RESULT_DTYPE = np.dtype([
+    ("location", "<u4"), ("score", "<i4"), ("mapq", "<i4"), ("result", "u1"), ("direction", "u1"),
+    ("flags", "u1"), ("reserved", "u1"), ("nLookups", "<u4"), ("nLocationsScored", "<u4"),
+    ("popularSeedsSkipped", "<u2"), ("nHitsIgnored", "<u2"), ("nProbes", "<u4"), ("nHitWords", "<u4"),
+    ("nOverflowLists", "<u4"), ("nElements", "<u4"), ("reserved2", "<u4"),
+    ("probabilityOfAllCandidates", "<f8"), ("probabilityOfBestCandidate", "<f8"),
+])
+assert RESULT_DTYPE.itemsize == C.sizeof(_ffi.Result)
+
+
+class SnapGpuError(RuntimeError):
+    pass
+
+
+_PTR_CALLS = ("genome_from_fasta", "genome_synthetic", "index_build", "index_load", "reads_synthetic",
+              "reads_from_fastq", "reads_from_arrays", "aligner_create", "reads_upload")
+
+
+def _check(value, what):
+    """Pointer-returning calls fail on NULL; int-returning calls on a non-zero code."""
+    if what in _PTR_CALLS:
+        if not value:
+            raise SnapGpuError(f"{what} failed: {last_error()}")
+        return value
+    if value != 0:
+        raise SnapGpuError(f"{what} failed ({value}): {last_error()}")
+    return value
+
+
+def device_count():
+    return lib().snapgpu_device_count()
+
+
+class Genome:
+    """Whole-genome byte string with contig padding (SNAPLib/Genome.h)."""
+
+    def __init__(self, handle):
+        self._h = handle
+
+    @classmethod
+    def from_fasta(cls, path, chromosome_padding=500):
+        return cls(_check(lib().snapgpu_genome_from_fasta(str(path).encode(), chromosome_padding), "genome_from_fasta"))
+
+    @classmethod
+    def synthetic(cls, total_bases, seed=2121, n_contigs=1, n_repeat_families=200, repeat_fraction=0.45,
+                  max_divergence=0.15, n_run_fraction=0.002, chromosome_padding=500):
+        p = _ffi.SynthGenomeParams(seed=seed, totalBases=total_bases, nContigs=n_contigs,
+                                   nRepeatFamilies=n_repeat_families, repeatFraction=repeat_fraction,
+                                   maxDivergence=max_divergence, nRunFraction=n_run_fraction,
+                                   chromosomePadding=chromosome_padding)
+        return cls(_check(lib().snapgpu_genome_synthetic(C.byref(p)), "genome_synthetic"))
+
+    def write_fasta(self, path):
+        _check(lib().snapgpu_genome_write_fasta(self._h, str(path).encode()), "write_fasta")
+
+    @property
+    def n_bases(self):
+        return lib().snapgpu_genome_nbases(self._h)
+
+    def bases(self, start=0, length=None):
+        n = self.n_bases
+        if length is None:
+            length = n - start
+        return C.string_at(lib().snapgpu_genome_bases(self._h) + start, length)
+
+    @property
+    def pieces(self):
+        L = lib()
+        return [(L.snapgpu_genome_piece_name(self._h, i).decode(), L.snapgpu_genome_piece_offset(self._h, i))
+                for i in range(L.snapgpu_genome_npieces(self._h))]
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().snapgpu_genome_free(self._h)
+            self._h = None
+
+
+class GenomeIndex:
+    """Seed index with GenomeIndex::lookupSeed semantics (SNAPLib/GenomeIndex.cpp:971-1086)."""
+
+    def __init__(self, handle, genome_keepalive=None):
+        self._h = handle
+
+    @classmethod
+    def build(cls, genome, seed_len=20, n_threads=0):
+        h = genome._h
+        genome._h = None          # ownership moves to the index
+        return cls(_check(lib().snapgpu_index_build(h, seed_len, n_threads), "index_build"))
+
+    @classmethod
+    def load(cls, directory):
+        return cls(_check(lib().snapgpu_index_load(str(directory).encode()), "index_load"))
+
+    def save(self, directory):
+        _check(lib().snapgpu_index_save(self._h, str(directory).encode()), "index_save")
+
+    def info(self):
+        i = _ffi.IndexInfo()
+        _check(lib().snapgpu_index_get_info(self._h, C.byref(i)), "index_info")
+        return {f: getattr(i, f) for f, _ in i._fields_}
+
+    def view(self):
+        v = _ffi.IndexView()
+        _check(lib().snapgpu_index_get_view(self._h, C.byref(v)), "index_view")
+        return v
+
+    def getSeedLength(self):
+        return self.info()["seedLen"]
+
+    def genome_bases(self, start, length):
+        v = self.view()
+        return C.string_at(v.genome + start, length)
+
+    def lookupSeed(self, seed, cap=1 << 20):
+        """-> (hits, rcHits): lists of genome offsets (overflow lists descending)."""
+        n = (C.c_uint32 * 2)()
+        buf = max(1, cap)
+        f = (C.c_uint32 * buf)()
+        r = (C.c_uint32 * buf)()
+        rc = lib().snapgpu_index_lookup(self._h, seed.encode() if isinstance(seed, str) else seed, n, f, r, buf)
+        if rc != 0:
+            raise SnapGpuError(f"lookup failed: {last_error()}")
+        return list(f[:min(n[0], buf)]), list(r[:min(n[1], buf)]), (n[0], n[1])
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().snapgpu_index_free(self._h)
+            self._h = None
+
+
+class Reads:
+    """A host batch of reads (bases + Phred+33 qualities), Read.h:289-328 contract."""
+
+    def __init__(self, ptr):
+        self._p = ptr
+
+    @classmethod
+    def synthetic(cls, genome, n_reads, seed=99, read_length=100, quality_char="2", base_error_rate=0.02,
+                  mutation_rate=0.001, indel_fraction=0.15, indel_extend=0.3, random_read_fraction=0.0):
+        p = _ffi.SynthReadsParams(seed=seed, nReads=n_reads, readLength=read_length,
+                                  qualityChar=ord(quality_char), baseErrorRate=base_error_rate,
+                                  mutationRate=mutation_rate, indelFraction=indel_fraction,
+                                  indelExtend=indel_extend, randomReadFraction=random_read_fraction)
+        g = genome._h if isinstance(genome, Genome) else genome
+        return cls(_check(lib().snapgpu_reads_synthetic(g, C.byref(p)), "reads_synthetic"))
+
+    @classmethod
+    def from_fastq(cls, path):
+        return cls(_check(lib().snapgpu_reads_from_fastq(str(path).encode()), "reads_from_fastq"))
+
+    @classmethod
+    def from_list(cls, reads):
+        """reads: iterable of (bases, quals) str/bytes pairs."""
+        bases, quals, offs, lens = bytearray(), bytearray(), [], []
+        for b, q in reads:
+            b = b.encode() if isinstance(b, str) else bytes(b)
+            q = q.encode() if isinstance(q, str) else bytes(q)
+            if len(q) < len(b):
+                q = q + b"!" * (len(b) - len(q))
+            offs.append(len(bases))
+            lens.append(len(b))
+            bases += b
+            quals += q[:len(b)]
+        n = len(lens)
+        bases += b"\0" * 16
+        quals += b"\0" * 16
+        o = (C.c_uint64 * max(1, n))(*offs)
+        l = (C.c_uint32 * max(1, n))(*lens)
+        return cls(_check(lib().snapgpu_reads_from_arrays(n, bytes(bases), bytes(quals), o, l), "reads_from_arrays"))
+
+    @property
+    def n(self):
+        return self._p.contents.n
+
+    def __len__(self):
+        return self.n
+
+    def get(self, i):
+        r = self._p.contents
+        o, l = r.offsets[i], r.lengths[i]
+        return C.string_at(r.bases + o, l), C.string_at(r.quals + o, l)
+
+    def truth(self):
+        r = self._p.contents
+        if not r.truthLocation:
+            return None
+        n = r.n
+        loc = np.ctypeslib.as_array(r.truthLocation, shape=(n,)).copy()
+        d = np.ctypeslib.as_array(r.truthDirection, shape=(n,)).copy()
+        return loc, d
+
+    def write_fastq(self, path):
+        _check(lib().snapgpu_reads_write_fastq(self._p, str(path).encode()), "write_fastq")
+
+    def __del__(self):
+        if getattr(self, "_p", None):
+            lib().snapgpu_reads_free(self._p)
+            self._p = None
+
+
+def default_params():
+    p = _ffi.AlignerParams()
+    lib().snapgpu_aligner_params_default(C.byref(p))
+    return p
+
+
+class BaseAligner:
+    """GPU BaseAligner (SNAPLib/BaseAligner.h:41-142).
+
+    Constructor arguments follow BaseAligner::BaseAligner (BaseAligner.h:44-55);
+    AlignRead follows BaseAligner::AlignRead (BaseAligner.cpp:196-200); AlignReads
+    is the batched form the GPU is built for.
+    """
+
+    def __init__(self, index, maxHitsToConsider=300, maxK=14, maxReadSize=500, maxSeedsToUse=25,
+                 maxSeedCoverage=0.0, extraSearchDepth=2, explorePopularSeeds=False, stopOnFirstHit=False,
+                 device=0):
+        self.index = index
+        self.params = _ffi.AlignerParams(maxHitsToConsider=maxHitsToConsider, maxK=maxK, maxReadSize=maxReadSize,
+                                         maxSeedsToUse=maxSeedsToUse, maxSeedCoverage=maxSeedCoverage,
+                                         extraSearchDepth=extraSearchDepth,
+                                         explorePopularSeeds=int(explorePopularSeeds),
+                                         stopOnFirstHit=int(stopOnFirstHit))
+        self._h = _check(lib().snapgpu_aligner_create(device, index._h, C.byref(self.params)), "aligner_create")
+
+    def AlignReads(self, reads):
+        """Batched AlignRead -> numpy structured array of RESULT_DTYPE."""
+        n = reads.n
+        out = np.zeros(max(1, n), dtype=RESULT_DTYPE)
+        if n:
+            _check(lib().snapgpu_align_batch(self._h, reads._p, out.ctypes.data_as(C.POINTER(_ffi.Result))),
+                   "align_batch")
+        return out[:n]
+
+    def AlignRead(self, bases, quals=None):
+        """-> (AlignmentResult, genomeLocation, direction, score, mapq) for one read."""
+        if quals is None:
+            quals = "I" * len(bases)
+        r = self.AlignReads(Reads.from_list([(bases, quals)]))[0]
+        return int(r["result"]), int(r["location"]), int(r["direction"]), int(r["score"]), int(r["mapq"])
+
+    # resident path (bench): upload once, time only the GPU passes
+    def upload(self, reads):
+        return DeviceReads(self, reads)
+
+    def timing(self):
+        t = _ffi.Timing()
+        lib().snapgpu_last_timing(self._h, C.byref(t))
+        return {f: getattr(t, f) for f, _ in t._fields_}
+
+    def stats(self):
+        s = _ffi.AlignerStats()
+        lib().snapgpu_aligner_get_stats(self._h, C.byref(s))
+        return {f: getattr(s, f) for f, _ in s._fields_}
+
+    # getters of SNAPLib/Aligner.h:62-77
+    def getNHashTableLookups(self):
+        return self.stats()["nHashTableLookups"]
+
+    def getLocationsScored(self):
+        return self.stats()["nLocationsScored"]
+
+    def getNHitsIgnoredBecauseOfTooHighPopularity(self):
+        return self.stats()["nHitsIgnoredBecauseOfTooHighPopularity"]
+
+    def getNReadsIgnoredBecauseOfTooManyNs(self):
+        return self.stats()["nReadsIgnoredBecauseOfTooManyNs"]
+
+    def getNIndelsMerged(self):
+        return self.stats()["nIndelsMerged"]
+
+    def getMaxK(self):
+        return lib().snapgpu_aligner_max_k(self._h)
+
+    def getName(self):
+        return lib().snapgpu_aligner_name(self._h).decode()
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().snapgpu_aligner_free(self._h)
+            self._h = None
+
+
+class DeviceReads:
+    def __init__(self, aligner, reads):
+        self.aligner = aligner
+        self.n = reads.n
+        self._h = _check(lib().snapgpu_reads_upload(aligner._h, reads._p), "reads_upload")
+
+    def run(self):
+        """Launch the GPU passes (asynchronous)."""
+        _check(lib().snapgpu_align_resident(self.aligner._h, self._h), "align_resident")
+
+    def synchronize(self):
+        _check(lib().snapgpu_synchronize(self.aligner._h), "synchronize")
+
+    def results(self):
+        out = np.zeros(max(1, self.n), dtype=RESULT_DTYPE)
+        _check(lib().snapgpu_results_download(self.aligner._h, self._h,
+                                              out.ctypes.data_as(C.POINTER(_ffi.Result))), "results_download")
+        return out[:self.n]
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().snapgpu_device_reads_free(self._h)
+            self._h = None
+
+
+def lv_batch(direction, tasks, device=0):
+    """LandauVishkin<direction>::computeEditDistance on the GPU.
+
+    tasks: list of (text, pattern, quals, k) (str/bytes).  -> list of (score, netIndel, prob)."""
+    n = len(tasks)
+    texts, pats, quals = bytearray(), bytearray(), bytearray()
+    toff, tlen, poff, plen, ks = [], [], [], [], []
+    for t, p, q, k in tasks:
+        t = t.encode() if isinstance(t, str) else bytes(t)
+        p = p.encode() if isinstance(p, str) else bytes(p)
+        q = q.encode() if isinstance(q, str) else bytes(q)
+        toff.append(len(texts)); tlen.append(len(t)); texts += t
+        poff.append(len(pats)); plen.append(len(p)); pats += p; quals += q[:len(p)].ljust(len(p), b"!")
+        ks.append(k)
+    texts += b"\0" * 16; pats += b"\0" * 16; quals += b"\0" * 16
+    A64, A32, AI = C.c_uint64 * n, C.c_uint32 * n, C.c_int32 * n
+    os_, on, op = AI(), AI(), (C.c_double * n)()
+    _check(lib().snapgpu_lv_batch(device, direction, n, bytes(texts), A64(*toff), A32(*tlen), bytes(pats),
+                                  bytes(quals), A64(*poff), A32(*plen), AI(*ks), os_, on, op), "lv_batch")
+    return [(os_[i], on[i], op[i]) for i in range(n)]
+
+
+def compute_mapq(pAll, pBest, score, popularSeedsSkipped):
+    return lib().snapgpu_compute_mapq(pAll, pBest, score, popularSeedsSkipped)

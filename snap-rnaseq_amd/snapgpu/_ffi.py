@@ -29,6 +29,8 @@ class Result(C.Structure):
         ("nProbes", C.c_uint32),
         ("nHitWords", C.c_uint32),
         ("nOverflowLists", C.c_uint32),
+        ("nElements", C.c_uint32),
+        ("reserved2", C.c_uint32),
         ("probabilityOfAllCandidates", C.c_double),
         ("probabilityOfBestCandidate", C.c_double),
     ]
@@ -140,7 +142,7 @@ class AlignerStats(C.Structure):
     ]
 
 
-assert C.sizeof(Result) == 56, C.sizeof(Result)
+assert C.sizeof(Result) == 64, C.sizeof(Result)
 
 # (name, restype, argtypes)
 _PROTOS = [

@@ -1,0 +1,177 @@
+#!/usr/bin/env python3
+"""Regenerate the golden fixtures under tests/golden/ from the REFERENCE itself.
+
+Runs only in the build container (needs /root/reference and oracle/_ref, built by
+`make -f oracle/Makefile.ref`).  Inputs are produced by this repo's deterministic
+generators; expected outputs come from the reference's own snap-rna indexer and
+BaseAligner / LandauVishkin / GenomeIndex::lookupSeed (driven by
+oracle/ref_harness.cpp).  Everything written here is data: FASTA/FASTQ inputs and
+TSV/JSON expected outputs.
+
+    python3 tests/golden/make_golden.py
+"""
+import hashlib
+import json
+import os
+import random
+import shutil
+import subprocess
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "snap-rnaseq_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import snapgpu  # noqa: E402
+from readsets import edge_reads  # noqa: E402
+from golden_common import PARAM_SETS, C1, C2, ref_tsv_to_canonical, digest  # noqa: E402
+
+REF_BIN = os.path.join(ROOT, "oracle", "_ref")
+SNAP = os.path.join(REF_BIN, "snap-rna")
+HARNESS = os.path.join(REF_BIN, "ref_harness")
+
+
+def run(cmd, **kw):
+    return subprocess.run(cmd, check=True, capture_output=True, text=True, **kw).stdout
+
+
+def ref_index(fasta, outdir):
+    shutil.rmtree(outdir, ignore_errors=True)
+    run([SNAP, "index", fasta, outdir])
+
+
+def ref_align(idxdir, fq, params):
+    args = [str(params[k]) for k in ("maxHits", "maxK", "numSeeds", "extra")]
+    return ref_tsv_to_canonical(run([HARNESS, "align", idxdir, fq] + args))
+
+
+def write_fastq(path, reads):
+    with open(path, "w") as f:
+        for i, (b, q) in enumerate(reads):
+            f.write(f"@r{i}\n{b}\n+\n{q}\n")
+
+
+def small_genome_fasta(path):
+    """300 kb, 3 contigs, repeat-rich; FASTA with mixed case, N runs and a few
+    IUPAC bytes (FASTA.cpp:104-116 keeps those upper-cased)."""
+    g = snapgpu.Genome.synthetic(300_000, seed=7, n_contigs=3, n_repeat_families=40, n_run_fraction=0.003)
+    tmp = path + ".tmp"
+    g.write_fasta(tmp)
+    rng = random.Random(5)
+    out = []
+    for line in open(tmp):
+        if not line.startswith(">"):
+            s = list(line.rstrip("\n"))
+            if rng.random() < 0.02:
+                s[rng.randrange(len(s))] = rng.choice("RYKM")
+            s = "".join(s)
+            if rng.random() < 0.05:
+                s = s.lower()
+            line = s + "\n"
+        out.append(line)
+    os.remove(tmp)
+    with open(path, "w") as f:
+        f.writelines(out)
+
+
+def main():
+    work = tempfile.mkdtemp(prefix="golden_")
+    meta = {"generator": "tests/golden/make_golden.py", "reference": "oracle/_ref (andrewmagis/snap-rna SNAPLib)"}
+
+    # 1. small genome + edge/synthetic reads, several parameter sets
+    fa = os.path.join(HERE, "small.fa")
+    small_genome_fasta(fa)
+    g = snapgpu.Genome.from_fasta(fa, 500)
+    rd = edge_reads(g, n_random=600, seed=17)
+    syn = snapgpu.Reads.synthetic(g, 1500, seed=3, random_read_fraction=0.02)
+    rd += [tuple(x.decode() for x in syn.get(i)) for i in range(syn.n)]
+    fq = os.path.join(HERE, "small_reads.fq")
+    write_fastq(fq, rd)
+    idxdir = os.path.join(work, "small_idx")
+    ref_index(fa, idxdir)
+    for name, params in PARAM_SETS.items():
+        with open(os.path.join(HERE, f"expected_small_{name}.tsv"), "w") as f:
+            f.write(ref_align(idxdir, fq, params))
+
+    # 2. lookupSeed golden: seeds from the genome, their RCs, mutated and random seeds
+    rng = random.Random(9)
+    seeds = []
+    nb = g.n_bases
+    while len(seeds) < 3000:
+        p = rng.randrange(0, nb - 20)
+        s = g.bases(p, 20).decode().upper()
+        if set(s) <= set("ACGT"):
+            seeds.append(s)
+            seeds.append(s.translate(str.maketrans("ACGT", "TGCA"))[::-1])
+    seeds += ["".join(rng.choice("ACGT") for _ in range(20)) for _ in range(1000)]
+    seeds += ["A" * 20, "T" * 20, "ACGT" * 5, "AATT" * 5, "GATC" * 5]
+    with open(os.path.join(HERE, "lookup_seeds.txt"), "w") as f:
+        f.write("\n".join(seeds) + "\n")
+    with open(os.path.join(HERE, "expected_lookups.tsv"), "w") as f:
+        f.write(run([HARNESS, "lookup", idxdir, os.path.join(HERE, "lookup_seeds.txt")]))
+
+    # 3. LV golden vectors (both text directions)
+    for direction in (1, -1):
+        rows = []
+        for _ in range(800):
+            L = rng.choice([3, 5, 12, 30, 60, 80, 100, 130])
+            t = "".join(rng.choice("ACGT") for _ in range(L + 35))
+            p = list(t[:L] if direction > 0 else t[::-1][:L])   # reverse LV walks the text backwards
+            for _ in range(rng.randrange(0, 10)):
+                op, i = rng.random(), rng.randrange(len(p))
+                if op < 0.6:
+                    p[i] = rng.choice("ACGTN")
+                elif op < 0.8:
+                    p.insert(i, rng.choice("ACGT"))
+                elif len(p) > 1:
+                    del p[i]
+            p = "".join(p)
+            q = "".join(chr(33 + rng.randrange(0, 45)) for _ in p)
+            k = rng.choice([0, 1, 2, 3, 5, 8, 14, 16, 22, 30])
+            tl = rng.choice([len(t), len(p) + 31])
+            tt = t[:tl] if direction > 0 else t[-tl:]
+            rows.append((direction, k, tt, p, q))
+        inp = os.path.join(work, f"lv{direction}.tsv")
+        with open(inp, "w") as f:
+            for r in rows:
+                f.write("\t".join(map(str, r)) + "\n")
+        out = run([HARNESS, "lv", inp]).splitlines()
+        with open(os.path.join(HERE, f"lv_{'fwd' if direction > 0 else 'rev'}.tsv"), "w") as f:
+            for r, o in zip(rows, out):
+                e, net, prob = o.split("\t")
+                f.write("\t".join(map(str, r)) + f"\t{e}\t{net}\t{float.fromhex(prob).hex()}\n")
+
+    # 4. the reference's own datatest fixture (tests/datatest/datatest.{fa,fq})
+    for fn in ("datatest.fa", "datatest.fq"):
+        shutil.copy(os.path.join("/root/reference/tests/datatest", fn), os.path.join(HERE, fn))
+    dt_idx = os.path.join(work, "dt_idx")
+    ref_index(os.path.join(HERE, "datatest.fa"), dt_idx)
+    with open(os.path.join(HERE, "expected_datatest.tsv"), "w") as f:
+        f.write(ref_align(dt_idx, os.path.join(HERE, "datatest.fq"), PARAM_SETS["default"]))
+
+    # 5. digests of the C1 / C2 synthetic configs (inputs regenerated on any host)
+    digests = {}
+    for cfg in (C1, C2):
+        gg = snapgpu.Genome.synthetic(**cfg["genome"])
+        gfa = os.path.join(work, f"{cfg['name']}.fa")
+        gg.write_fasta(gfa)
+        reads = snapgpu.Reads.synthetic(gg, **cfg["reads"])
+        rfq = os.path.join(work, f"{cfg['name']}.fq")
+        reads.write_fastq(rfq)
+        d = os.path.join(work, f"{cfg['name']}_idx")
+        ref_index(gfa, d)
+        tsv = ref_align(d, rfq, PARAM_SETS["default"])
+        digests[cfg["name"]] = {"sha256": digest(tsv), "n": reads.n}
+        with open(os.path.join(HERE, f"expected_{cfg['name']}_head.tsv"), "w") as f:
+            f.write("".join(tsv.splitlines(True)[:2000]))
+    meta["digests"] = digests
+    with open(os.path.join(HERE, "golden.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+    shutil.rmtree(work, ignore_errors=True)
+    print("golden fixtures written to", HERE)
+
+
+if __name__ == "__main__":
+    main()

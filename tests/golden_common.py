@@ -1,0 +1,41 @@
+"""Shared definitions for the golden fixtures (tests/golden/) and their tests."""
+import hashlib
+
+# Parameter sets: (maxHits, maxK, numSeeds, extraSearchDepth) as the reference
+# harness takes them (oracle/ref_harness.cpp mode_align).
+PARAM_SETS = {
+    "default": dict(maxHits=300, maxK=14, numSeeds=25, extra=2),
+    "h16": dict(maxHits=16, maxK=14, numSeeds=25, extra=2),
+    "k5": dict(maxHits=300, maxK=5, numSeeds=25, extra=1),
+    "s4": dict(maxHits=50, maxK=8, numSeeds=4, extra=0),
+    "k20": dict(maxHits=300, maxK=20, numSeeds=40, extra=5),
+}
+
+# C1: the reference's CPU-runnable config (BASELINE.json configs[0]): 1 Mb, 10k reads.
+C1 = dict(name="C1",
+          genome=dict(total_bases=1_000_000, seed=2121, n_contigs=1, n_repeat_families=60),
+          reads=dict(n_reads=10_000, seed=99))
+# C2: chr21-sized (46,709,983 bp) repeat-rich genome, 1M reads (configs[1], the bench workload).
+C2 = dict(name="C2",
+          genome=dict(total_bases=46_709_983, seed=2121, n_contigs=1, n_repeat_families=200),
+          reads=dict(n_reads=1_000_000, seed=99))
+
+
+def params_to_aligner_kwargs(p):
+    return dict(maxHitsToConsider=p["maxHits"], maxK=p["maxK"], maxSeedsToUse=p["numSeeds"],
+                extraSearchDepth=p["extra"])
+
+
+def ref_tsv_to_canonical(text):
+    """ref_harness align output (doubles as C %a) -> canonical lines (doubles as IEEE bits)."""
+    import struct
+    out = []
+    for line in text.splitlines():
+        x = line.split("\t")
+        bits = [struct.unpack("<Q", struct.pack("<d", float.fromhex(v)))[0] for v in x[9:11]]
+        out.append("\t".join(x[:9]) + f"\t{bits[0]:016x}\t{bits[1]:016x}")
+    return "\n".join(out) + "\n"
+
+
+def digest(text):
+    return hashlib.sha256(text.encode()).hexdigest()

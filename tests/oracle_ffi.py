@@ -1,0 +1,94 @@
+"""ctypes binding of oracle/liboracle.so -- TEST INFRASTRUCTURE (the checker).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "liboracle.so")
+
+_orc = None
+
+
+def oracle_lib():
+    global _orc
+    if _orc is None:
+        if not os.path.exists(ORACLE_SO):
+            subprocess.run(["make", "-s", "-f", os.path.join(ROOT, "oracle", "Makefile")], check=True, cwd=ROOT)
+        import snapgpu._ffi as F
+        o = C.CDLL(ORACLE_SO)
+        o.oracle_align_batch.argtypes = [C.POINTER(F.IndexView), C.POINTER(F.AlignerParams), C.c_void_p, C.c_void_p,
+                                         C.POINTER(C.c_uint64), C.POINTER(C.c_uint32), C.c_uint64,
+                                         C.c_void_p, C.c_int]
+        o.oracle_align_batch.restype = C.c_int
+        o.oracle_lv.argtypes = [C.c_int, C.c_char_p, C.c_int, C.c_char_p, C.c_char_p, C.c_int, C.c_int,
+                                C.POINTER(C.c_double), C.POINTER(C.c_int)]
+        o.oracle_lv.restype = C.c_int
+        o.oracle_compute_mapq.argtypes = [C.c_double, C.c_double, C.c_int, C.c_int]
+        o.oracle_compute_mapq.restype = C.c_int
+        _orc = o
+    return _orc
+
+
+def oracle_align(index, reads, params, n_threads=8):
+    """CPU restatement of BaseAligner::AlignRead over the same index and reads."""
+    import snapgpu
+    from snapgpu import _ffi as F
+    v = index.view()
+    n = reads.n
+    out = np.zeros(max(1, n), dtype=snapgpu.RESULT_DTYPE)
+    r = reads._p.contents
+    rc = oracle_lib().oracle_align_batch(C.byref(v), C.byref(params), r.bases, r.quals, r.offsets, r.lengths, n,
+                                         out.ctypes.data, n_threads)
+    assert rc == 0
+    return out[:n]
+
+
+def oracle_lv(direction, text, pattern, quals, k):
+    """LandauVishkin<direction>::computeEditDistance; text padded with 'n' as the
+    reference harness does (oracle/ref_harness.cpp mode_lv)."""
+    t = text.encode() if isinstance(text, str) else bytes(text)
+    p = pattern.encode() if isinstance(pattern, str) else bytes(pattern)
+    q = quals.encode() if isinstance(quals, str) else bytes(quals)
+    tbuf = C.create_string_buffer(b"n" * 64 + t + b"n" * 64)
+    pbuf = C.create_string_buffer(p + b"\0" * 16)
+    qbuf = C.create_string_buffer(q.ljust(len(p), b"!") + b"\0" * 16)
+    prob = C.c_double()
+    net = C.c_int()
+    base = C.addressof(tbuf) + 64 + (0 if direction > 0 else len(t))
+    e = oracle_lib().oracle_lv(direction, C.c_char_p(base), len(t), pbuf, qbuf, len(p), k, C.byref(prob),
+                               C.byref(net))
+    return e, net.value, prob.value
+
+
+COMPARE_FIELDS = ("result", "location", "direction", "score", "mapq", "nLookups", "nLocationsScored",
+                  "popularSeedsSkipped", "nHitsIgnored", "nProbes", "nHitWords", "nOverflowLists", "nElements",
+                  "probabilityOfAllCandidates", "probabilityOfBestCandidate")
+
+
+def mismatches(a, b, fields=COMPARE_FIELDS):
+    """Indices where two result arrays differ in any field (doubles compared bitwise)."""
+    bad = np.zeros(len(a), dtype=bool)
+    for f in fields:
+        if a.dtype[f].kind == "f":
+            bad |= a[f].view(np.uint64) != b[f].view(np.uint64)
+        else:
+            bad |= a[f] != b[f]
+    return np.nonzero(bad)[0]
+
+
+def canonical_tsv(res):
+    """Canonical text form of results (golden fixtures / digests): doubles as IEEE bits."""
+    pa = res["probabilityOfAllCandidates"].view(np.uint64)
+    pb = res["probabilityOfBestCandidate"].view(np.uint64)
+    lines = []
+    for i in range(len(res)):
+        r = res[i]
+        lines.append(f"{i}\t{r['result']}\t{r['location']}\t{r['direction']}\t{r['score']}\t{r['mapq']}\t"
+                     f"{r['nLookups']}\t{r['nLocationsScored']}\t{r['popularSeedsSkipped']}\t"
+                     f"{int(pa[i]):016x}\t{int(pb[i]):016x}")
+    return "\n".join(lines) + "\n"
