@@ -1,0 +1,174 @@
+#!/usr/bin/env python3
+"""Benchmark: aligned reads/s of the MI355X BaseAligner::AlignRead hot path.
+
+Workload (BASELINE.json configs[1] shape): a chr21-sized
+(46,709,983 bp) synthetic repeat-rich genome indexed with seed 20 and resident in
+HBM; 1,000,000 wgsim-like 100 bp single-end reads per GPU, already resident in
+HBM when the timed region starts; defaults maxHits 300, maxK 14, 25 seeds,
+extraSearchDepth 2.  One step = one batched AlignRead pass over the rank's reads.
+
+Multi-GPU: one process per GPU (torch.distributed.run), reads sharded by rank, the
+index built and uploaded by every rank (replicas); no data-path collective --
+gloo carries only the timing barrier and the max-over-ranks reduction.
+
+Prints ONE JSON line on rank 0 (contract in the task statement), including
+`roofline` (algorithmic bytes of the alignment kernel / its HIP-event time) and
+`cpu_baseline` (the oracle/ C restatement on host threads, same reads).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "snap-rnaseq_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md: 8.0 TB/s spec
+GENOME_BASES = 46_709_983
+READS_PER_GPU = 1_000_000
+READ_LEN = 100
+MAX_K = 31
+
+
+def algorithmic_bytes(res):
+    """B_read = 2*readLen + 16 + 12*P + 4*(H + V) + (readLen + MAX_K)*S."""
+    P = res["nProbes"].astype(np.int64).sum()
+    H = res["nHitWords"].astype(np.int64).sum()
+    V = res["nOverflowLists"].astype(np.int64).sum()
+    S = res["nLocationsScored"].astype(np.int64).sum()
+    n = len(res)
+    return int(n * (2 * READ_LEN + 16) + 12 * P + 4 * (H + V) + (READ_LEN + MAX_K) * S), dict(
+        P=P / n, H=H / n, V=V / n, S=S / n)
+
+
+def load_pmc_traffic():
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if present."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(p):
+        try:
+            return json.load(open(p)).get("bytes_per_launch")
+        except Exception:
+            return None
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--reads", type=int, default=READS_PER_GPU, help="reads per GPU")
+    ap.add_argument("--genome-bases", type=int, default=GENOME_BASES)
+    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    import snapgpu
+    t0 = time.time()
+    genome = snapgpu.Genome.synthetic(args.genome_bases, seed=2121, n_contigs=1, n_repeat_families=200)
+    # reads: rank r takes shard r of a world*reads global batch (distinct seed per shard)
+    reads = snapgpu.Reads.synthetic(genome, args.reads, seed=99 + rank)
+    idx = snapgpu.GenomeIndex.build(genome, 20, min(16, os.cpu_count() or 8))
+    t_index = time.time() - t0
+    aligner = snapgpu.BaseAligner(idx, device=local)
+    dev = aligner.upload(reads)
+
+    for _ in range(args.warmup):
+        dev.run()
+        dev.synchronize()
+    kernel_ms = []
+    if dist:
+        dist.barrier()
+    dev.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        dev.run()
+        dev.synchronize()
+        kernel_ms.append(aligner.timing()["mainKernelMs"])
+    dev.synchronize()
+    t_end = time.perf_counter()
+    if dist:
+        dist.barrier()
+    elapsed = t_end - t_start
+    res = dev.results()
+
+    if dist:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    total_reads = args.reads * world * args.steps
+    value = total_reads / elapsed
+    ms_per_step = elapsed * 1000.0 / args.steps
+
+    out = None
+    if rank == 0:
+        bytes_launch, per_read = algorithmic_bytes(res)
+        avg_kernel_s = float(np.mean(kernel_ms)) / 1000.0
+        achieved = bytes_launch / avg_kernel_s / 1e9
+        traffic = load_pmc_traffic()
+        counts = {int(k): int(v) for k, v in zip(*np.unique(res["result"], return_counts=True))}
+        cpu = None
+        parity = None
+        if not args.no_cpu_baseline:
+            from oracle_ffi import mismatches, oracle_align
+            nthr = max(1, args.cpu_threads)
+            c0 = time.perf_counter()
+            cres = oracle_align(idx, reads, aligner.params, n_threads=nthr)
+            cdt = time.perf_counter() - c0
+            cpu = {"value": args.reads / cdt, "unit": "reads/s", "cores": nthr, "kind": "port",
+                   "sample": f"the rank-0 shard ({args.reads} reads) of the timed workload, oracle/snap_oracle.c "
+                             f"(bit-exact C restatement of BaseAligner), {nthr} host threads, {cdt:.2f} s wall"}
+            parity = {"reads_compared": len(res), "mismatches": int(len(mismatches(res, cres)))}
+        out = {
+            "metric": "aligned reads/sec (100 bp SE, k=20 seed) at 1/2/4/8 GPUs + CPU baseline",
+            "value": value,
+            "unit": "reads/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (deterministic repeat-rich genome + wgsim-like reads generated in-process)",
+            "config": {
+                "workload": "C2: chr21-sized (46,709,983 bp) synthetic repeat-rich genome, seed-20 index in HBM, "
+                            f"{args.reads} x 100 bp SE reads per GPU (configs[1] shape)",
+                "genome_bases": args.genome_bases, "reads_per_gpu": args.reads, "read_len": READ_LEN,
+                "seed_len": 20, "maxHits": 300, "maxK": 14, "numSeeds": 25, "extraSearchDepth": 2,
+                "parallelism": f"reads sharded over {world} GPU(s), index replicated",
+                "results": {"SingleHit": counts.get(1, 0), "MultipleHits": counts.get(2, 0),
+                            "NotFound": counts.get(0, 0)},
+                "per_read": {k: round(float(v), 2) for k, v in per_read.items()},
+                "index_build_s": round(t_index, 2),
+            },
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "align_kernel<128>", "kernel_ms": float(np.mean(kernel_ms)),
+                         "algorithmic_bytes_per_launch": bytes_launch},
+            "cpu_baseline": cpu,
+            "parity": parity,
+        }
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+    return out
+
+
+if __name__ == "__main__":
+    main()

@@ -365,6 +365,10 @@ static int score(Oracle *o, int force, unsigned readLen, int *result) {
             return 0;
         }
         Elem *el = o->lists[w].wnext;
+        /* BaseAligner.cpp:1121-1127: prefetch the next element and its genome data */
+        __builtin_prefetch(el->wnext->wnext);
+        __builtin_prefetch(o->ix->genome + el->wnext->base);
+        __builtin_prefetch(o->ix->genome + el->wnext->base + 64);
         if (el->lps <= o->scoreLimit) {
             uint64_t mask = el->used;
             while (mask) {
@@ -573,6 +577,13 @@ static void align_read(Oracle *o, const char *bases, const char *quals, unsigned
                 unsigned lim = nHits[dir] < o->p.maxHitsToConsider ? nHits[dir] : o->p.maxHitsToConsider;
                 out->nHitWords += lim;
                 for (unsigned i = 0; i < lim; i++) {
+                    if (i % 16 == 0) {   /* prefetch candidate-map slots (BaseAligner.cpp:829-842) */
+                        for (unsigned j = i; j < i + 16 && j < lim; j++) {
+                            uint32_t l2 = hits[dir][j] - offset;
+                            uint32_t key = (((l2 - l2 % ELEM_SIZE) / ELEM_SIZE) << 1 | (uint32_t)dir) + 1;
+                            __builtin_prefetch(&o->map[(key * 2654435761u) & o->mapMask]);
+                        }
+                    }
                     uint32_t h = hits[dir][i];
                     uint32_t loc = h - offset;
                     if (h < offset) continue;

@@ -339,7 +339,7 @@ __device__ __forceinline__ LvOut lv_wave(const Bitmap<NB> &F, int p0, int patter
         Lp = Ln;
     }
     r.score = -1;
-    r.prob = 0.0;
+    r.prob = 1.0;   // LandauVishkin.h:259: left at 1.0 when no alignment within k
     return r;
 }
 
