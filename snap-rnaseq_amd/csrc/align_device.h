@@ -37,7 +37,10 @@ constexpr uint32_t UNUSED_SCORE = 0xffffu;
 constexpr uint32_t FAIL_SCORE = 0xffffffffu;
 constexpr int ELEM = 48;                  // hashTableElementSize == maxMergeDist
 constexpr uint32_t NPAD = 100;            // Genome::N_PADDING
-constexpr int NBUCKET = 1024;             // element hash buckets (LDS)
+constexpr int NBUCKET_LOG2 = 9;
+constexpr int NBUCKET = 1 << NBUCKET_LOG2;  // element hash buckets (LDS)
+constexpr uint32_t SKCAP = 512;           // selection keys kept in LDS
+constexpr int ELEM_DWORDS = 36;           // meaningful dwords of Elem
 constexpr int BT = 128;                   // insertion-batch dedupe table (LDS)
 constexpr uint32_t NONE = 0xffffffffu;
 
@@ -149,6 +152,7 @@ struct Lds {
     uint32_t scrLoc[WAVE];                          // batch scratch: hit location per lane
     uint32_t nElems;
     uint32_t pad_[3];
+    uint32_t sk[SKCAP];                             // selection keys of elements < SKCAP
     uint64_t seedUsed[NB + 1];                      // BaseAligner::seedUsed bit vector
     int16_t btAct[MAX_K + 1];                       // LV backtrace scratch
     int16_t btMatched[MAX_K + 1];
@@ -399,7 +403,7 @@ struct ReadState {
     uint32_t nLookups, nScored, nHitsIgnored, nProbes, nHitWords, nOvf, nElems;
 };
 
-__device__ __forceinline__ uint32_t elem_hash(uint32_t key) { return (key * 2654435761u) >> (32 - 10); }
+__device__ __forceinline__ uint32_t elem_hash(uint32_t key) { return (key * 2654435761u) >> (32 - NBUCKET_LOG2); }
 
 // find element with `key`; NONE if absent
 __device__ __forceinline__ uint32_t chain_find(const uint32_t *head, const Elem *ar, uint32_t key) {
@@ -408,15 +412,33 @@ __device__ __forceinline__ uint32_t chain_find(const uint32_t *head, const Elem 
     return e;
 }
 
+// selection keys: LDS for the first SKCAP elements of a read, HBM beyond
+template <int MAXLEN>
+__device__ __forceinline__ uint32_t sk_get(const Lds<MAXLEN> &S, const Elem *ar, uint32_t e) {
+    return e < SKCAP ? S.sk[e] : ar[e].sortkey;
+}
+template <int MAXLEN>
+__device__ __forceinline__ void sk_set(Lds<MAXLEN> &S, Elem *ar, uint32_t e, uint32_t v) {
+    if (e < SKCAP) S.sk[e] = v;
+    else ar[e].sortkey = v;
+}
+
 // owner-lane recompute of its selection maximum (elements e == lane mod 64)
-__device__ __forceinline__ void recompute_lane_max(uint64_t *laneMax, const Elem *ar, uint32_t nElems, int lane) {
+template <int MAXLEN>
+__device__ __forceinline__ void recompute_lane_max(Lds<MAXLEN> &S, const Elem *ar, int lane) {
     uint64_t best = 0;
+    const uint32_t nElems = S.nElems;
     for (uint32_t e = lane; e < nElems; e += WAVE) {
-        uint32_t k = ar[e].sortkey;
+        uint32_t k = sk_get(S, ar, e);
         uint64_t v = ((uint64_t)k << 32) | e;
         if (k && v > best) best = v;
     }
-    laneMax[lane] = best;
+    S.laneMax[lane] = best;
 }
+
+// uniform field extraction from a cooperatively loaded element (lane i = dword i)
+__device__ __forceinline__ uint32_t rl(uint32_t v, int k) { return (uint32_t)__builtin_amdgcn_readlane((int)v, k); }
+__device__ __forceinline__ uint64_t rl64(uint32_t v, int k) { return ((uint64_t)rl(v, k + 1) << 32) | rl(v, k); }
+__device__ __forceinline__ double rld(uint32_t v, int k) { return __longlong_as_double((long long)rl64(v, k)); }
 
 }  // namespace sgk

@@ -71,21 +71,33 @@ __device__ __forceinline__ bool score_wave(const KArgs &A, Lds<MAXLEN> &S, Elem 
             return false;
         }
         const uint32_t e = (uint32_t)sel;
-        Elem *el = ar + e;
-        const uint32_t ekey = uni(el->key);
+        // One round trip for the whole element: lane i holds dword i (Elem layout,
+        // align_device.h); fields are read into SGPRs with v_readlane.
+        const uint32_t *ew = (const uint32_t *)(ar + e);
+        const uint32_t ev = lane < ELEM_DWORDS ? ew[lane] : 0u;
+        const uint64_t used = rl64(ev, 0);
+        uint64_t scored = rl64(ev, 2);
+        double eprob = rld(ev, 4);
+        const uint32_t ekey = rl(ev, 6);
+        uint32_t ebest = rl(ev, 8);
+        uint32_t ebestLoc = rl(ev, 9);
+        const uint32_t ewl = rl(ev, 11);
         const uint32_t dir = ekey & 1;
         const uint32_t ebase = (ekey >> 1) * ELEM;
-        if (uni(el->lps) <= st.scoreLimit) {
-            uint64_t used = uni64(el->used);
+        // unlink now (allExtantCandidatesScored = true, BaseAligner.cpp:1391-1394): no
+        // insertion happens while an element is scored, so the next selection is known
+        sk_set(S, ar, e, 0);
+        wave_sync();
+        if ((int)(e % WAVE) == lane) recompute_lane_max(S, ar, lane);
+        if (((ewl >> 8) & 0xff) <= st.scoreLimit) {
             uint64_t mask = used;
             while (mask) {
                 const int bit = __builtin_ctzll(mask);
                 const uint64_t cb = 1ull << bit;
                 mask &= ~cb;
-                uint64_t scored = uni64(el->scored);
                 if (scored & cb) continue;
                 bool anyNearby = scored != 0;
-                el->scored = scored | cb;
+                scored |= cb;
                 uint32_t loc = ebase + bit;
                 const uint32_t elemLoc = loc;
                 uint32_t sc = FAIL_SCORE;
@@ -106,7 +118,7 @@ __device__ __forceinline__ bool score_wave(const KArgs &A, Lds<MAXLEN> &S, Elem 
                     }
                 }
                 if (ok) {
-                    const int s = (int)uni(el->seedOffset[bit]);
+                    const int s = (int)((rl(ev, 12 + bit / 2) >> (16 * (bit & 1))) & 0xffff);
                     const int t = s + (int)A.seedLen;
                     int w0 = stage_window(S, A.genome, loc, (int)n);
                     int kmax = st.scoreLimit < (uint32_t)(MAX_K - 1) ? (int)st.scoreLimit : MAX_K - 1;
@@ -128,36 +140,38 @@ __device__ __forceinline__ bool score_wave(const KArgs &A, Lds<MAXLEN> &S, Elem 
                 }
                 st.nScored++;
                 if (anyNearby) {
-                    uint32_t ebs = uni(el->bestScore);
-                    if (ebs < sc || (ebs == sc && prob <= unid(el->prob))) continue;
+                    if (ebest < sc || (ebest == sc && prob <= eprob)) continue;
                 }
-                el->bestLoc = loc;
+                ebestLoc = loc;
                 uint32_t nb = NONE;
                 if (sc != FAIL_SCORE) {
                     uint32_t nl = elemLoc + (2 * (elemLoc % ELEM / (ELEM / 2)) - 1) * (ELEM / 2);
                     uint32_t nkey = ((nl / ELEM) << 1) | dir;
                     nb = uni(chain_find(S.head, ar, nkey));
                 }
-                if (nb != NONE && uni64(ar[nb].scored) != 0) {
-                    Elem *ne = ar + nb;
-                    uint32_t nbase = (uni(ne->key) >> 1) * ELEM;
-                    uint32_t nbl = uni(ne->bestLoc);
-                    if (!((nbase > ebase && loc - nbl <= (uint32_t)ELEM) || (nbase < ebase && nbl <= (uint32_t)ELEM)))
-                        nb = NONE;   // sic: BaseAligner.cpp:1311-1312
+                if (nb != NONE) {
+                    const uint32_t *nw = (const uint32_t *)(ar + nb);
+                    const uint32_t nv = lane < 12 ? nw[lane] : 0u;
+                    if (rl64(nv, 2) == 0) nb = NONE;   // nearby element not scored yet
                     if (nb != NONE) {
-                        uint32_t nbs = uni(ne->bestScore);
-                        double np = unid(ne->prob);
+                        uint32_t nbase = (rl(nv, 6) >> 1) * ELEM;
+                        uint32_t nbl = rl(nv, 9);
+                        if (!((nbase > ebase && loc - nbl <= (uint32_t)ELEM) || (nbase < ebase && nbl <= (uint32_t)ELEM)))
+                            nb = NONE;   // sic: BaseAligner.cpp:1311-1312
+                    }
+                    if (nb != NONE) {
+                        uint32_t nbs = rl(nv, 8);
+                        double np = rld(nv, 4);
                         if (nbs < sc || (nbs == sc && np >= prob)) continue;
                         anyNearby = true;
                         st.pAll = st.pAll - np > 0.0 ? st.pAll - np : 0.0;
-                        ne->prob = 0;
+                        if (lane == 4 || lane == 5) ((uint32_t *)(ar + nb))[lane] = 0u;   // nearby prob = 0
                     }
                 }
-                double ep = unid(el->prob);
-                st.pAll = st.pAll - ep > 0.0 ? st.pAll - ep : 0.0;
+                st.pAll = st.pAll - eprob > 0.0 ? st.pAll - eprob : 0.0;
                 st.pAll += prob;
-                el->prob = prob;
-                el->bestScore = sc;
+                eprob = prob;
+                ebest = sc;
                 if (st.bestScore > sc || (st.bestScore == sc && prob > st.pBest)) {
                     st.bestScore = sc;
                     st.pBest = prob;
@@ -174,11 +188,21 @@ __device__ __forceinline__ bool score_wave(const KArgs &A, Lds<MAXLEN> &S, Elem 
                 st.scoreLimit = (st.bestScore < A.maxK ? st.bestScore : A.maxK) + A.extra;
             }
         }
-        // unlink (allExtantCandidatesScored = true, BaseAligner.cpp:1391-1394)
-        el->allScored = 1;
-        el->sortkey = 0;
-        wave_sync();
-        if ((int)(e % WAVE) == lane) recompute_lane_max(S.laneMax, ar, S.nElems, lane);
+        // write back the element in one store: scored, prob, bestScore, bestLoc, allScored
+        {
+            const uint64_t pb = (uint64_t)__double_as_longlong(eprob);
+            uint32_t w = ev;
+            bool st_ = true;
+            if (lane == 2) w = (uint32_t)scored;
+            else if (lane == 3) w = (uint32_t)(scored >> 32);
+            else if (lane == 4) w = (uint32_t)pb;
+            else if (lane == 5) w = (uint32_t)(pb >> 32);
+            else if (lane == 8) w = ebest;
+            else if (lane == 9) w = ebestLoc;
+            else if (lane == 11) w = (ewl & ~0x00ff0000u) | (1u << 16);
+            else st_ = false;
+            if (st_) ((uint32_t *)(ar + e))[lane] = w;
+        }
         wave_sync();
     } while (force);
     return false;
@@ -225,7 +249,7 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
                 uint64_t used = 0;
                 uint32_t weight = 0, allScored = 0, sortkey = 0;
                 if (e != NONE) {
-                    used = ar[e].used; weight = ar[e].weight; allScored = ar[e].allScored; sortkey = ar[e].sortkey;
+                    used = ar[e].used; weight = ar[e].weight; allScored = ar[e].allScored; sortkey = sk_get(S, ar, e);
                 }
                 uint64_t m = grp;
                 while (m) {
@@ -263,7 +287,7 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
                 ar[e].used = used;
                 ar[e].weight = (uint8_t)weight;
                 ar[e].allScored = (uint8_t)allScored;
-                ar[e].sortkey = sortkey;
+                sk_set(S, ar, e, sortkey);
                 if (sortkey) atomicMax((unsigned long long *)&S.laneMax[e % WAVE], ((uint64_t)sortkey << 32) | e);
             }
         }
@@ -597,6 +621,7 @@ struct snapgpu_aligner {
     snapgpu_timing_t timing{};
     snapgpu_aligner_stats_t stats{};
     snapgpu_device_reads_t *lastReads = nullptr;
+    bool pendingTiming = false;
 };
 
 static const size_t kDevGuard = 1024;
@@ -758,6 +783,7 @@ int snapgpu_align_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d) {
     A.counter = a->dCounter; A.arena = a->dArena; A.arenaElems = a->arenaElems;
     int grid = a->grid;
     if ((uint64_t)grid > d->n) grid = (int)d->n;
+    (void)hipGetLastError();   // clear any stale error of an unrelated earlier runtime call
     HIPCHK(hipMemsetAsync(a->dCounter, 0, 64, a->stream));
     HIPCHK(hipEventRecord(a->ev[0], a->stream));
     if (d->maxLen <= 128) hipLaunchKernelGGL(align_kernel<128>, dim3(grid), dim3(64), 0, a->stream, A);
@@ -765,14 +791,19 @@ int snapgpu_align_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d) {
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(a->ev[1], a->stream));
     a->lastReads = d;
+    a->pendingTiming = true;
     return SNAPGPU_OK;
 }
 
 int snapgpu_synchronize(snapgpu_aligner_t *a) {
     if (!a) return SNAPGPU_EINVAL;
     HIPCHK(hipStreamSynchronize(a->stream));
-    float ms = 0;
-    if (hipEventElapsedTime(&ms, a->ev[0], a->ev[1]) == hipSuccess) a->timing.mainKernelMs = ms;
+    if (a->pendingTiming) {
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, a->ev[0], a->ev[1]));
+        a->timing.mainKernelMs = ms;
+        a->pendingTiming = false;
+    }
     return SNAPGPU_OK;
 }
 
