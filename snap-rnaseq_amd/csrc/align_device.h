@@ -93,6 +93,11 @@ struct KArgs {
     uint32_t *counter;
     Elem *arena;
     uint64_t arenaElems;         // per-wave capacity
+    // 2-bit packed genome (align_grouped.h)
+    const uint32_t *gcode;
+    const uint32_t *gmask;
+    uint32_t hasIupac;
+    uint32_t grouped;            // use the grouped scorer (MAXLEN 128)
 };
 
 // ------------------------------------------------------------ wave helpers
@@ -137,6 +142,26 @@ __device__ __forceinline__ uint32_t complement_of(uint32_t c) {   // BaseAligner
 }
 
 // ------------------------------------------------------------------ LDS
+constexpr int64_t PACK_GUARD = 1024;     // packed word 0 = genome position -1024
+constexpr int EB = 8;                    // elements popped per batch
+constexpr int CAND_TARGET = 8;           // forced mode: pop until this many candidates
+constexpr int CANDCAP = EB * ELEM;       // candidate list capacity
+constexpr int FBS = 9;                   // per-lane bitmap stride (dwords), bank-conflict free
+
+struct GroupLds {
+    uint32_t rcode[2][128 / 16 + 2];     // read[dir] 2-bit codes, 16 bases per dword
+    uint32_t rmsk[2][128 / 16 + 2];      // spaced mask: bit 2i set if base i is not ACGT or i >= n
+    uint32_t wcode[4][(128 + 192) / 16 + 2];
+    uint32_t wmsk[4][(128 + 192) / 16 + 2];
+    uint32_t fb[WAVE * FBS];             // per-lane spaced bitmap words
+    uint32_t ecache[EB][ELEM_DWORDS];    // popped elements (authoritative while in the batch)
+    uint32_t eidx[EB];
+    uint16_t cand[CANDCAP];              // slot << 8 | bit
+    int32_t gdesc[4][8];                 // per-group: loc, dir, s, glen, ok
+    int16_t btA[4][32];
+    int16_t btM[4][32];
+};
+
 template <int MAXLEN>
 struct Lds {
     static constexpr int NB = MAXLEN / 64;          // 64-position blocks
@@ -157,6 +182,7 @@ struct Lds {
     int16_t btAct[MAX_K + 1];                       // LV backtrace scratch
     int16_t btMatched[MAX_K + 1];
     uint16_t rows[MAX_K][WAVE];                     // LV rows: (L+2) | action<<12
+    GroupLds grp;                                   // grouped scorer (align_grouped.h)
 };
 
 // ------------------------------------------------------------ LV engine
@@ -393,6 +419,17 @@ __device__ __forceinline__ int next_piece_after(const KArgs &A, uint32_t loc) { 
 }
 
 // ------------------------------------------------------------ per-read state
+// Device watchdog: loops whose bound rests on data-structure invariants carry an
+// iteration cap; tripping one records (code, read, detail) here, ends the read and
+// makes the host call fail instead of hanging the GPU.
+enum : uint32_t { DIAG_SEED_LOOP = 1, DIAG_SCORE_LOOP = 2, DIAG_CHAIN = 3, DIAG_BATCH_TABLE = 4, DIAG_OVERDUE = 16 };
+// A read that runs longer than this (100 MHz s_memrealtime ticks, 2 s) is abandoned.
+constexpr uint64_t READ_DEADLINE_TICKS = 200000000ull;
+__device__ uint32_t g_diag[4];
+__device__ __forceinline__ void diag_report(uint32_t code, uint32_t a, uint32_t b) {
+    if (atomicCAS(&g_diag[0], 0u, code) == 0u) { g_diag[1] = a; g_diag[2] = b; }
+}
+
 struct ReadState {
     uint32_t lps[2], mostSeeds[2], nSeedsApplied[2];
     uint32_t bestScore, bestLoc, scoreLimit, popular;
@@ -401,14 +438,29 @@ struct ReadState {
     int32_t outScore, outMapq;
     uint32_t ts;                 // running hit counter (FIFO timestamps)
     uint32_t nLookups, nScored, nHitsIgnored, nProbes, nHitWords, nOvf, nElems;
+    uint32_t rid;                // read index (watchdog reports)
+    uint32_t abort;              // watchdog tripped: finish the read now
+    uint64_t t0;                 // s_memrealtime at read start
 };
+
+// time watchdog: true (once reported) when the read has overrun its deadline
+__device__ __forceinline__ bool overdue(ReadState &st, uint32_t site) {
+    if (st.abort) return true;
+    if (__builtin_amdgcn_s_memrealtime() - st.t0 < READ_DEADLINE_TICKS) return false;
+    if (lane_id() == 0) diag_report(DIAG_OVERDUE + site, st.rid, (uint32_t)((__builtin_amdgcn_s_memrealtime() - st.t0) >> 10));
+    st.abort = 1;
+    return true;
+}
 
 __device__ __forceinline__ uint32_t elem_hash(uint32_t key) { return (key * 2654435761u) >> (32 - NBUCKET_LOG2); }
 
 // find element with `key`; NONE if absent
-__device__ __forceinline__ uint32_t chain_find(const uint32_t *head, const Elem *ar, uint32_t key) {
+__device__ __forceinline__ uint32_t chain_find(const uint32_t *head, const Elem *ar, uint32_t key, uint32_t cap) {
     uint32_t e = head[elem_hash(key)];
-    while (e != NONE && ar[e].key != key) e = ar[e].next;
+    for (uint32_t steps = 0; e != NONE && ar[e].key != key; steps++) {
+        if (steps > cap) { diag_report(DIAG_CHAIN, key, e); return NONE; }
+        e = ar[e].next;
+    }
     return e;
 }
 

@@ -7,9 +7,11 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "align_device.h"
+#include "align_grouped.h"
 #include "internal.h"
 
 using namespace sgk;
@@ -32,6 +34,7 @@ __device__ __forceinline__ bool score_wave(const KArgs &A, Lds<MAXLEN> &S, Elem 
             if (v > st.lps[d]) st.lps[d] = v;
         }
     do {
+        if (overdue(st, 4)) return true;
         // head of the highest non-empty weight list == max sortkey over linked elements
         uint64_t sel = uni64(max_reduce64(S.laneMax[lane]));
         uint32_t minLps = st.lps[0] < st.lps[1] ? st.lps[0] : st.lps[1];
@@ -147,7 +150,7 @@ __device__ __forceinline__ bool score_wave(const KArgs &A, Lds<MAXLEN> &S, Elem 
                 if (sc != FAIL_SCORE) {
                     uint32_t nl = elemLoc + (2 * (elemLoc % ELEM / (ELEM / 2)) - 1) * (ELEM / 2);
                     uint32_t nkey = ((nl / ELEM) << 1) | dir;
-                    nb = uni(chain_find(S.head, ar, nkey));
+                    nb = uni(chain_find(S.head, ar, nkey, (uint32_t)A.arenaElems));
                 }
                 if (nb != NONE) {
                     const uint32_t *nw = (const uint32_t *)(ar + nb);
@@ -208,6 +211,309 @@ __device__ __forceinline__ bool score_wave(const KArgs &A, Lds<MAXLEN> &S, Elem 
     return false;
 }
 
+// ---------------------------------------------------- grouped scorer (MAXLEN 128)
+// Terminal branch of score() (BaseAligner.cpp:1081-1103) + computeMAPQ (mapq.h:32-65).
+__device__ __forceinline__ void finalize_read(const KArgs &A, ReadState &st, int *result, uint32_t *flags) {
+    st.outScore = (int32_t)st.bestScore;
+    if (st.bestScore <= A.maxK) {
+        st.outLoc = st.bestLoc;
+        double pAll = st.pAll > st.pBest ? st.pAll : st.pBest;
+        int mq;
+        if (pAll == st.pBest && st.popular == 0 && st.bestScore < 5) mq = 70;
+        else {
+            double c = st.pBest / pAll;
+            if (c >= 1) mq = 69;
+            else {
+                double v = -10 * log10(1 - c);
+                mq = v < 69.0 ? (int)v : 69;
+                if (v < 70.0 && fabs(v - rint(v)) < 1e-6) *flags |= SNAPGPU_FLAG_MAPQ_FIXED;
+            }
+            int pen = (int)st.popular - 10;
+            if (pen < 0) pen = 0;
+            mq -= pen / 2;
+            if (mq < 0) mq = 0;
+        }
+        st.outMapq = mq;
+        *result = mq >= 10 ? SNAPGPU_SINGLE_HIT : SNAPGPU_MULTIPLE_HITS;
+    } else {
+        *result = (st.nSeedsApplied[0] == 0 && st.nSeedsApplied[1] == 0) ? SNAPGPU_MULTIPLE_HITS : SNAPGPU_NOT_FOUND;
+        st.outMapq = 0;
+    }
+}
+
+// One speculative pass over up to G = 64/GS candidates: builds the per-lane bitmaps
+// from the packed genome and runs forward then reverse LV in lane groups.  Lane
+// results are group-uniform; the caller reads them with readlane(gi * GS).
+template <int GS>
+__device__ __forceinline__ void lv_pass(const KArgs &A, Lds<128> &S, int m, int k, uint32_t n, int &e1, int &e2,
+                                        double &p1, double &p2, int &net2) {
+    GroupLds &G = S.grp;
+    const int lane = lane_id();
+    const int gi = lane / GS, li = lane & (GS - 1), c = GS / 2 - 1;
+    const bool gact = gi < m && G.gdesc[gi < 4 ? gi : 0][4] != 0;
+    // stage the packed windows: genome [loc - 64, loc + n + 128) of every group
+    constexpr int WW = (128 + 192) / 16 + 2;
+    for (int idx = lane; idx < m * 2 * WW; idx += WAVE) {
+        int g = idx / (2 * WW), r = idx % (2 * WW);
+        int w = r % WW;
+        int64_t ws = (((int64_t)(uint32_t)G.gdesc[g][0] - 64 + PACK_GUARD) >> 4) + w;
+        if (r < WW) G.wcode[g][w] = A.gcode[ws];
+        else G.wmsk[g][w] = A.gmask[ws];
+    }
+    wave_sync();
+    const int gsel = gi < 4 ? gi : 0;
+    // groups past m hold stale (or, on a fresh kernel, uninitialised) descriptors
+    const uint32_t loc = gact ? (uint32_t)G.gdesc[gsel][0] : 0u;
+    const int dir = gact ? G.gdesc[gsel][1] & 1 : 0;
+    const int s = gact ? G.gdesc[gsel][2] : 0;
+    const int glen = gact ? G.gdesc[gsel][3] : (int)n;
+    // F_x[m] = read[dir][m] != genome[loc + x + m], 2 bits per position (bit 2m)
+    {
+        const int x = li - c;
+        const int64_t wbase = ((int64_t)loc - 64 + PACK_GUARD) & ~(int64_t)15;   // genome pos of wcode word 0, +guard
+        const int rel0 = (int)((int64_t)loc + PACK_GUARD - wbase) + x;
+        uint32_t *fb = G.fb + lane * FBS;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            int r = rel0 + 16 * j;
+            int wi = r >> 4;
+            uint32_t sh = 2 * (r & 15);
+            uint32_t gc = __builtin_amdgcn_alignbit(G.wcode[gsel][wi + 1], G.wcode[gsel][wi], sh);
+            uint32_t gm = __builtin_amdgcn_alignbit(G.wmsk[gsel][wi + 1], G.wmsk[gsel][wi], sh);
+            uint32_t dd = gc ^ G.rcode[dir][j];
+            uint32_t y = (dd | (dd >> 1)) & 0x55555555u;
+            fb[j] = y | gm | G.rmsk[dir][j];
+        }
+    }
+    wave_sync();
+    const char *q = dir ? S.rcQ : S.fwdQ;
+    const int t = s + (int)A.seedLen;
+    int n1;
+    double pp1;
+    lv_group<1, GS>(G, gact, t, (int)n - t, glen - t, k, k, q, S.rows, A.tab, e1, pp1, n1);
+    int k2 = k - e1;
+    const bool ract = gact && e1 >= 0;
+    int kmax2 = 0;
+    {
+        // largest reverse limit over the groups that need a reverse pass
+        int v = ract ? k2 : -1;
+        for (int o = 32; o >= 1; o >>= 1) { int w2 = __shfl_xor(v, o); v = w2 > v ? w2 : v; }
+        kmax2 = unii(v);
+    }
+    e2 = -1; p2 = 1.0; net2 = 0;
+    if (kmax2 >= 0) lv_group<-1, GS>(G, ract, s - 1, s, s + MAX_K, k2, kmax2, q, S.rows, A.tab, e2, p2, net2);
+    p1 = pp1;
+    (void)li;
+}
+
+// BaseAligner::score (BaseAligner.cpp:977-1399) over batches of popped elements.
+template <int MAXLEN>
+__device__ bool score_wave_v2(const KArgs &A, Lds<MAXLEN> &S, Elem *ar, ReadState &st, bool force, uint32_t n,
+                              int *result, uint32_t *flags) {
+    const int lane = lane_id();
+    GroupLds &G = S.grp;
+    const DevTables *tab = A.tab;
+    for (int d = 0; d < 2; d++)
+        if (st.mostSeeds[d]) {
+            uint32_t v = st.nSeedsApplied[d] / st.mostSeeds[d];
+            if (v > st.lps[d]) st.lps[d] = v;
+        }
+    const uint32_t minLps = st.lps[0] < st.lps[1] ? st.lps[0] : st.lps[1];
+    const bool forced = force || minLps > st.scoreLimit;
+    for (uint32_t guard = 0;; guard++) {
+        if (guard > (uint32_t)A.arenaElems) {   // every batch unlinks >= 1 element
+            if (lane == 0) diag_report(DIAG_SCORE_LOOP, st.rid, S.nElems);
+            st.abort = 1;
+        }
+        if (overdue(st, 1)) return true;
+        // ---- pop elements in weight-list order (head of highest list first)
+        uint32_t nb = 0, ncand = 0;
+        while (nb < (uint32_t)EB) {
+            uint64_t sel = uni64(max_reduce64(S.laneMax[lane]));
+            if (sel == 0) break;
+            const uint32_t e = (uint32_t)sel;
+            sk_set(S, ar, e, 0);                       // unlink (BaseAligner.cpp:1391-1394)
+            wave_sync();
+            if ((int)(e % WAVE) == lane) recompute_lane_max(S, ar, lane);
+            const uint32_t *ew = (const uint32_t *)(ar + e);
+            const uint32_t ev = lane < ELEM_DWORDS ? ew[lane] : 0u;
+            if (lane < ELEM_DWORDS) G.ecache[nb][lane] = ev;
+            if (lane == 0) G.eidx[nb] = e;
+            const uint64_t pend = rl64(ev, 0) & ~rl64(ev, 2);
+            if (((rl(ev, 11) >> 8) & 0xff) <= st.scoreLimit) ncand += (uint32_t)__popcll(pend);
+            nb++;
+            wave_sync();
+            if (!forced || ncand >= (uint32_t)CAND_TARGET) break;
+        }
+        if (nb == 0) {
+            if (forced) { finalize_read(A, st, result, flags); return true; }
+            return false;
+        }
+        // ---- candidate list in the reference's order: elements, then ascending bit
+        uint32_t nc = 0;
+        for (uint32_t sl = 0; sl < nb; sl++) {
+            const uint32_t lpsv = (G.ecache[sl][11] >> 8) & 0xff;
+            if (lpsv > st.scoreLimit) continue;          // cannot be scored (limit only shrinks)
+            uint64_t pend = ((uint64_t)G.ecache[sl][1] << 32 | G.ecache[sl][0]) &
+                            ~((uint64_t)G.ecache[sl][3] << 32 | G.ecache[sl][2]);
+            while (pend) {
+                int bit = __builtin_ctzll(pend);
+                pend &= pend - 1;
+                if (lane == 0) G.cand[nc] = (uint16_t)(sl << 8 | bit);
+                nc++;
+            }
+        }
+        wave_sync();
+        uint32_t curSlot = 0xffffffffu;
+        bool slotSkip = false;
+        for (uint32_t i0 = 0; i0 < nc;) {
+            if (overdue(st, 2)) return true;
+            const int k = st.scoreLimit < (uint32_t)(MAX_K - 1) ? (int)st.scoreLimit : MAX_K - 1;
+            const int GS = k <= 7 ? 16 : (k <= 15 ? 32 : 64);
+            const int Gn = 64 / GS;
+            const int m = (int)(nc - i0) < Gn ? (int)(nc - i0) : Gn;
+            // group descriptors
+            for (int g = 0; g < m; g++) {
+                const uint32_t cw = uni(G.cand[i0 + g]);
+                const uint32_t sl = cw >> 8, bit = cw & 0xff;
+                const uint32_t key = uni(G.ecache[sl][6]);
+                const uint32_t loc = (key >> 1) * ELEM + bit;
+                const uint32_t s = (uni(G.ecache[sl][12 + bit / 2]) >> (16 * (bit & 1))) & 0xffff;
+                uint32_t glen = n + MAX_K;
+                bool ok = substring_ok(A, loc, glen);
+                if (!ok) {   // BaseAligner.cpp:1163-1185
+                    uint32_t endOffset = 0;
+                    bool have = false;
+                    if ((uint64_t)loc + n + MAX_K >= A.nBases) { endOffset = A.nBases; have = true; }
+                    else {
+                        int np = next_piece_after(A, loc);
+                        if (np >= 0) { endOffset = A.pieces[np]; have = true; }
+                    }
+                    if (have) {
+                        glen = endOffset - loc - 1;
+                        if (glen >= n - (uint32_t)MAX_K) ok = substring_ok(A, loc, glen);
+                    }
+                }
+                if (lane == 0) {
+                    G.gdesc[g][0] = (int32_t)loc; G.gdesc[g][1] = (int32_t)(key & 1);
+                    G.gdesc[g][2] = (int32_t)s; G.gdesc[g][3] = (int32_t)glen; G.gdesc[g][4] = ok ? 1 : 0;
+                }
+            }
+            wave_sync();
+            int e1, e2, net2;
+            double p1, p2;
+            if (GS == 16) lv_pass<16>(A, S, m, k, n, e1, e2, p1, p2, net2);
+            else if (GS == 32) lv_pass<32>(A, S, m, k, n, e1, e2, p1, p2, net2);
+            else lv_pass<64>(A, S, m, k, n, e1, e2, p1, p2, net2);
+            // ---- apply in order with the limit in force at each candidate
+            for (int g = 0; g < m; g++) {
+                const uint32_t cw = uni(G.cand[i0 + g]);
+                const uint32_t sl = cw >> 8, bit = cw & 0xff;
+                if (sl != curSlot) {                  // element entered: lps check (BaseAligner.cpp:1129)
+                    curSlot = sl;
+                    slotSkip = ((uni(G.ecache[sl][11]) >> 8) & 0xff) > st.scoreLimit;
+                }
+                if (slotSkip) continue;
+                const int ln = g * GS;
+                const int r1 = readlane(e1, ln), r2 = readlane(e2, ln);
+                const bool ok = uni((uint32_t)G.gdesc[g][4]) != 0;
+                const int kNow = (int)(st.scoreLimit < (uint32_t)(MAX_K - 1) ? st.scoreLimit : MAX_K - 1);
+                uint32_t sc = FAIL_SCORE;
+                double prob = 0;
+                const uint32_t key = uni(G.ecache[sl][6]);
+                const uint32_t dir = key & 1;
+                const uint32_t ebase = (key >> 1) * ELEM;
+                uint32_t loc = ebase + bit;
+                const uint32_t elemLoc = loc;
+                if (ok && r1 >= 0 && r1 <= kNow) {
+                    // the reverse call runs with limit scoreLimit - score1 (BaseAligner.cpp:1216-1220)
+                    const int lim2 = (int)st.scoreLimit - r1 > MAX_K - 1 ? MAX_K - 1 : (int)st.scoreLimit - r1;
+                    if (r2 >= 0 && r2 <= lim2) {
+                        sc = (uint32_t)(r1 + r2);
+                        double q1 = unid(__shfl(p1, ln)), q2 = unid(__shfl(p2, ln));
+                        prob = q1 * q2 * tab->seedProb;
+                        loc += (uint32_t)readlane(net2, ln);
+                    }
+                }
+                // candidate bookkeeping (BaseAligner.cpp:1253-1384) on the cached element
+                uint64_t scored = ((uint64_t)uni(G.ecache[sl][3]) << 32) | uni(G.ecache[sl][2]);
+                const uint64_t cb = 1ull << bit;
+                bool anyNearby = scored != 0;
+                scored |= cb;
+                if (lane == 0) { G.ecache[sl][2] = (uint32_t)scored; G.ecache[sl][3] = (uint32_t)(scored >> 32); }
+                st.nScored++;
+                const uint32_t ebest = uni(G.ecache[sl][8]);
+                const double eprob = __longlong_as_double(((long long)uni(G.ecache[sl][5]) << 32) | uni(G.ecache[sl][4]));
+                if (anyNearby) {
+                    if (ebest < sc || (ebest == sc && prob <= eprob)) { wave_sync(); continue; }
+                }
+                if (lane == 0) G.ecache[sl][9] = loc;   // bestScoreGenomeLocation
+                uint32_t nb2 = NONE;
+                if (sc != FAIL_SCORE) {
+                    uint32_t nl = elemLoc + (2 * (elemLoc % ELEM / (ELEM / 2)) - 1) * (ELEM / 2);
+                    uint32_t nkey = ((nl / ELEM) << 1) | dir;
+                    nb2 = uni(chain_find(S.head, ar, nkey, (uint32_t)A.arenaElems));
+                }
+                if (nb2 != NONE) {
+                    int cs = -1;   // the nearby element may be in this batch: its cache is authoritative
+                    for (uint32_t q = 0; q < nb; q++) if (uni(G.eidx[q]) == nb2) cs = (int)q;
+                    uint32_t nv;
+                    if (cs >= 0) nv = lane < 12 ? G.ecache[cs][lane] : 0u;
+                    else nv = lane < 12 ? ((const uint32_t *)(ar + nb2))[lane] : 0u;
+                    if (rl64(nv, 2) == 0) nb2 = NONE;
+                    if (nb2 != NONE) {
+                        uint32_t nbase = (rl(nv, 6) >> 1) * ELEM;
+                        uint32_t nbl = rl(nv, 9);
+                        if (!((nbase > ebase && loc - nbl <= (uint32_t)ELEM) || (nbase < ebase && nbl <= (uint32_t)ELEM)))
+                            nb2 = NONE;   // sic: BaseAligner.cpp:1311-1312
+                    }
+                    if (nb2 != NONE) {
+                        uint32_t nbs = rl(nv, 8);
+                        double np = rld(nv, 4);
+                        if (nbs < sc || (nbs == sc && np >= prob)) { wave_sync(); continue; }
+                        anyNearby = true;
+                        st.pAll = st.pAll - np > 0.0 ? st.pAll - np : 0.0;
+                        if (cs >= 0) { if (lane == 4 || lane == 5) G.ecache[cs][lane] = 0u; }
+                        else if (lane == 4 || lane == 5) ((uint32_t *)(ar + nb2))[lane] = 0u;
+                    }
+                }
+                st.pAll = st.pAll - eprob > 0.0 ? st.pAll - eprob : 0.0;
+                st.pAll += prob;
+                {
+                    const uint64_t pb = (uint64_t)__double_as_longlong(prob);
+                    if (lane == 0) { G.ecache[sl][4] = (uint32_t)pb; G.ecache[sl][5] = (uint32_t)(pb >> 32); G.ecache[sl][8] = sc; }
+                }
+                if (st.bestScore > sc || (st.bestScore == sc && prob > st.pBest)) {
+                    st.bestScore = sc;
+                    st.pBest = prob;
+                    st.bestLoc = loc;
+                    st.outLoc = loc;
+                    st.outScore = (int32_t)sc;
+                    st.outDir = dir;
+                }
+                wave_sync();
+                if (A.stopOnFirst && st.bestScore <= A.maxK) {
+                    *result = SNAPGPU_MULTIPLE_HITS;
+                    st.outMapq = 0;
+                    return true;
+                }
+                st.scoreLimit = (st.bestScore < A.maxK ? st.bestScore : A.maxK) + A.extra;
+            }
+            i0 += (uint32_t)m;
+        }
+        // ---- write the batch back (scored, prob, bestScore, bestLoc, allScored = 1)
+        for (uint32_t sl = 0; sl < nb; sl++) {
+            const uint32_t e = uni(G.eidx[sl]);
+            uint32_t w = lane < ELEM_DWORDS ? G.ecache[sl][lane] : 0u;
+            if (lane == 11) w = (w & ~0x00ff0000u) | (1u << 16);
+            if (lane == 2 || lane == 3 || lane == 4 || lane == 5 || lane == 8 || lane == 9 || lane == 11)
+                ((uint32_t *)(ar + e))[lane] = w;
+        }
+        wave_sync();
+        if (!forced) return false;
+    }
+}
+
 // ------------------------------------------------------------ hit insertion
 // The per-hit loop of BaseAligner.cpp:829-869 (findCandidate / incrementWeight /
 // allocateNewCandidate) for one seed in one direction.
@@ -218,6 +524,7 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
     const int lane = lane_id();
     const bool allowAlloc = lpsNow <= st.scoreLimit;
     for (uint32_t b0 = 0; b0 < lim; b0 += WAVE) {
+        if (overdue(st, 5)) break;
         uint32_t i = b0 + lane;
         bool valid = i < lim;
         uint32_t h = valid ? (list ? list[i] : single) : 0;
@@ -228,9 +535,10 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
         uint32_t slot = 0;
         if (valid) {
             uint32_t s = (key * 2654435761u) >> 25;
-            for (;;) {
+            for (int probe = 0;; probe++) {
                 uint32_t old = atomicCAS(&S.btKey[s], NONE, key);
                 if (old == NONE || old == key) break;
+                if (probe >= BT) { diag_report(DIAG_BATCH_TABLE, st.rid, key); valid = false; break; }
                 s = (s + 1) & (BT - 1);
             }
             slot = s;
@@ -244,7 +552,7 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
         if (leader) {
             S.btKey[slot] = NONE;
             S.btMask[slot] = 0;
-            uint32_t e = chain_find(S.head, ar, key);
+            uint32_t e = chain_find(S.head, ar, key, (uint32_t)A.arenaElems);
             if (e != NONE || allowAlloc) {
                 uint64_t used = 0;
                 uint32_t weight = 0, allScored = 0, sortkey = 0;
@@ -296,6 +604,16 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
     st.ts += lim;
 }
 
+template <int MAXLEN>
+__device__ __forceinline__ bool do_score(bool grouped, const KArgs &A, Lds<MAXLEN> &S, Elem *ar, ReadState &st,
+                                         bool force, uint32_t n, const uint32_t (&rbF)[MAXLEN / 64],
+                                         const uint32_t (&rbR)[MAXLEN / 64], int *result, uint32_t *flags) {
+    if constexpr (MAXLEN == 128) {
+        if (grouped) return score_wave_v2<MAXLEN>(A, S, ar, st, force, n, result, flags);
+    }
+    return score_wave<MAXLEN>(A, S, ar, st, force, n, rbF, rbR, result, flags);
+}
+
 // ------------------------------------------------------------- AlignRead
 template <int MAXLEN>
 __device__ void align_one(const KArgs &A, Lds<MAXLEN> &S, Elem *ar, uint32_t r) {
@@ -309,6 +627,9 @@ __device__ void align_one(const KArgs &A, Lds<MAXLEN> &S, Elem *ar, uint32_t r) 
     st.popular = 0; st.pAll = 0; st.pBest = 0;
     st.nLookups = st.nScored = st.nHitsIgnored = st.nProbes = st.nHitWords = st.nOvf = 0;
     st.ts = 0;
+    st.rid = r;
+    st.abort = 0;
+    st.t0 = __builtin_amdgcn_s_memrealtime();
     st.nSeedsApplied[0] = st.nSeedsApplied[1] = 0;
     uint32_t flags = 0;
     int result = SNAPGPU_NOT_FOUND;
@@ -318,9 +639,11 @@ __device__ void align_one(const KArgs &A, Lds<MAXLEN> &S, Elem *ar, uint32_t r) 
     if (n > A.maxReadSize || n > (uint32_t)MAXLEN) { flags |= SNAPGPU_FLAG_READ_TOO_LONG; run = false; }
     else if (n < seedLen) run = false;
     uint32_t rbF[NB], rbR[NB];
+    bool grouped = false;
     if (run) {
         // Read::init upper-casing + BaseAligner.cpp:636-650 (RC read, qualities)
         uint32_t nN = 0;
+        bool other = false;
         for (int i = lane; i < MAXLEN + 64; i += WAVE) {
             uint32_t c = 0, q = 0;
             if (i < (int)n) {
@@ -336,6 +659,7 @@ __device__ void align_one(const KArgs &A, Lds<MAXLEN> &S, Elem *ar, uint32_t r) 
             S.fwd[i] = (char)c;
             S.fwdQ[i] = (char)q;
             nN += __popcll(ballot(i < (int)n && c == 'N'));
+            other |= ballot(i < (int)n && c != 'A' && c != 'C' && c != 'G' && c != 'T' && c != 'N') != 0;
         }
         for (int i = lane; i < NBUCKET; i += WAVE) S.head[i] = NONE;
         for (int i = lane; i < BT; i += WAVE) { S.btKey[i] = NONE; S.btMask[i] = 0; }
@@ -345,6 +669,24 @@ __device__ void align_one(const KArgs &A, Lds<MAXLEN> &S, Elem *ar, uint32_t r) 
 #pragma unroll
         for (int b = 0; b < NB; b++) { rbF[b] = (uint8_t)S.fwd[b * 64 + lane]; rbR[b] = (uint8_t)S.rc[b * 64 + lane]; }
         if (nN > A.maxK) { flags |= SNAPGPU_FLAG_TOO_MANY_NS; run = false; }
+        // grouped scorer: packed-code comparison is byte-exact unless both the read and
+        // the genome hold non-ACGTN bytes (an IUPAC code could then match itself)
+        grouped = MAXLEN == 128 && A.grouped && !(A.hasIupac && other);
+        if (MAXLEN == 128) {
+            for (int idx = lane; idx < 2 * (128 / 16 + 2); idx += WAVE) {
+                const int dr = idx / (128 / 16 + 2), w = idx % (128 / 16 + 2);
+                const char *src = dr ? S.rc : S.fwd;
+                uint32_t code = 0, msk = 0;
+                for (int i = 0; i < 16; i++) {
+                    uint32_t v = sgk::packed_code((uint8_t)src[16 * w + i]);   // zero slack past n -> non-ACGT
+                    code |= (v & 3u) << (2 * i);
+                    if (v > 3) msk |= 1u << (2 * i);
+                }
+                S.grp.rcode[dr][w] = code;
+                S.grp.rmsk[dr][w] = msk;
+            }
+            wave_sync();
+        }
     }
     if (run) {
         st.lps[0] = st.lps[1] = 0;
@@ -357,95 +699,106 @@ __device__ void align_one(const KArgs &A, Lds<MAXLEN> &S, Elem *ar, uint32_t r) 
         if (lane <= NB) seedUsed[lane] = 0;
         wave_sync();
         uint32_t next = 0, wrapCount = 0;
-        bool done = false;
-        while (st.nSeedsApplied[0] + st.nSeedsApplied[1] < maxSeeds) {
-            if (next >= nPossible) {
+        // One call site for the scorer (it is large): `force` marks the final scoring
+        // pass after the seed loop ends (BaseAligner.cpp:707-723, 879-891).
+        const uint32_t seedGuard = (nPossible + 2) * (seedLen + 2) + maxSeeds;
+        for (uint32_t guard = 0;; guard++) {
+            bool force = st.nSeedsApplied[0] + st.nSeedsApplied[1] >= maxSeeds;
+            if (guard > seedGuard) {   // each pass consumes a seed position or a wrap
+                if (lane == 0) diag_report(DIAG_SEED_LOOP, r, next);
+                st.abort = 1;
+            }
+            if (overdue(st, 3)) break;
+            if (!force && next >= nPossible) {
                 wrapCount++;
-                if (wrapCount >= seedLen) {
-                    score_wave<MAXLEN>(A, S, ar, st, true, n, rbF, rbR, &result, &flags);
-                    done = true;
-                    break;
-                }
-                next = A.tab->wrap[wrapCount];
-                st.mostSeeds[0] = st.mostSeeds[1] = wrapCount + 1;
-            }
-            while (next < nPossible && ((uni64(seedUsed[next >> 6]) >> (next & 63)) & 1)) next++;
-            if (next >= nPossible) continue;
-            {
-                uint64_t w = uni64(seedUsed[next >> 6]) | (1ull << (next & 63));
-                wave_sync();
-                seedUsed[next >> 6] = w;
-                wave_sync();
-            }
-            // Seed::DoesTextRepresentASeed + Seed::Seed (Seed.cpp:28-42, Seed.h:38-51)
-            int v = lane < (int)seedLen ? base_value((uint8_t)S.fwd[next + lane]) : 0;
-            if (ballot(lane < (int)seedLen && v > 3)) continue;
-            uint64_t fpart = lane < (int)seedLen ? (uint64_t)v << ((seedLen - lane - 1) * 2) : 0;
-            uint64_t rpart = lane < (int)seedLen ? (uint64_t)(v ^ 3) << (lane * 2) : 0;
-            const uint64_t f = uni64(or_reduce64(fpart));
-            const uint64_t rcv = uni64(or_reduce64(rpart));
-            // GenomeIndex::lookupSeed + SNAPHashTable::Lookup
-            const bool comp = (int64_t)f > (int64_t)rcv;
-            const uint64_t canon = comp ? rcv : f;
-            const uint32_t table = (uint32_t)(canon >> 32);
-            const uint32_t key = (uint32_t)canon;
-            const uint64_t size = A.tableSize[table];
-            const uint32_t *T = A.slots + 3 * A.tableBase[table];
-            const uint64_t h0 = fmix32(key) % size;
-            bool found = false;
-            uint32_t v1 = 0, v2 = 0;
-            for (uint32_t j0 = 0;; j0 += 8) {
-                uint32_t j = j0 + (lane & 7);
-                uint64_t S_j = j <= 4 ? (uint64_t)j * (j + 1) * (2 * j + 1) / 6 : 30 + (uint64_t)(j - 4);
-                uint64_t pos = (h0 + S_j) % size;
-                uint32_t kj = 0, v1j = INVALID, v2j = 0;
-                bool beyond = j > size + 5;
-                if (lane < 8 && !beyond) { kj = T[3 * pos]; v1j = T[3 * pos + 1]; v2j = T[3 * pos + 2]; }
-                bool stop = (j == 0) ? (kj == key && v1j != INVALID) : (kj == key || v1j == INVALID);
-                uint64_t m = ballot(lane < 8 && (stop || beyond)) & 0xffull;
-                if (m) {
-                    int jl = __builtin_ctzll(m);
-                    uint32_t jj = j0 + jl;
-                    bool bey = readlane(beyond ? 1 : 0, jl);
-                    st.nProbes += bey ? jj : jj + 1;
-                    uint32_t kv1 = readlaneu(v1j, jl);
-                    if (!bey && (jj == 0 || kv1 != INVALID)) { found = true; v1 = kv1; v2 = readlaneu(v2j, jl); }
-                    break;
+                if (wrapCount >= seedLen) force = true;
+                else {
+                    next = A.tab->wrap[wrapCount];
+                    st.mostSeeds[0] = st.mostSeeds[1] = wrapCount + 1;
                 }
             }
-            // fillInLookedUpResults (GenomeIndex.cpp:1013-1086), both directions
-            uint32_t nH0 = 0, nH1 = 0, sg0 = 0, sg1 = 0;
-            const uint32_t *ls0 = nullptr, *ls1 = nullptr;
-            if (found) {
-                uint32_t vf = comp ? v2 : v1, vr = comp ? v1 : v2;
-                if (vf < A.nBases) { nH0 = 1; sg0 = vf; }
-                else if (vf != UNUSED_SIDE) { uint32_t o = vf - A.nBases; nH0 = uni(A.overflow[o]); ls0 = A.overflow + o + 1; st.nOvf++; }
-                if (f == rcv) { nH1 = nH0; sg1 = sg0; ls1 = ls0; }   // palindrome (GenomeIndex.cpp:1003-1006)
-                else if (vr < A.nBases) { nH1 = 1; sg1 = vr; }
-                else if (vr != UNUSED_SIDE) { uint32_t o = vr - A.nBases; nH1 = uni(A.overflow[o]); ls1 = A.overflow + o + 1; st.nOvf++; }
-            }
-            st.nLookups++;
-            bool applied = false;
-#pragma unroll
-            for (uint32_t dir = 0; dir < 2; dir++) {
-                const uint32_t nh = dir ? nH1 : nH0;
-                if (nh > A.maxHits && !A.explore) {
-                    st.nHitsIgnored++;
-                    st.popular++;
-                } else {
-                    uint32_t offset = dir == 0 ? next : n - seedLen - next;
-                    uint32_t lim = nh < A.maxHits ? nh : A.maxHits;
-                    st.nHitWords += lim;
-                    insert_hits<MAXLEN>(A, S, ar, st, dir, offset, lim, dir ? ls1 : ls0, dir ? sg1 : sg0,
-                                        numWeightLists, dir ? st.lps[1] : st.lps[0]);
-                    if (dir) st.nSeedsApplied[1]++; else st.nSeedsApplied[0]++;
-                    applied = true;
+            if (!force) {
+                while (next < nPossible && ((uni64(seedUsed[next >> 6]) >> (next & 63)) & 1)) next++;
+                if (next >= nPossible) continue;
+                {
+                    uint64_t w = uni64(seedUsed[next >> 6]) | (1ull << (next & 63));
+                    wave_sync();
+                    seedUsed[next >> 6] = w;
+                    wave_sync();
                 }
+                // Seed::DoesTextRepresentASeed + Seed::Seed (Seed.cpp:28-42, Seed.h:38-51)
+                int v = lane < (int)seedLen ? base_value((uint8_t)S.fwd[next + lane]) : 0;
+                if (ballot(lane < (int)seedLen && v > 3)) continue;
+                uint64_t fpart = lane < (int)seedLen ? (uint64_t)v << ((seedLen - lane - 1) * 2) : 0;
+                uint64_t rpart = lane < (int)seedLen ? (uint64_t)(v ^ 3) << (lane * 2) : 0;
+                const uint64_t f = uni64(or_reduce64(fpart));
+                const uint64_t rcv = uni64(or_reduce64(rpart));
+                // GenomeIndex::lookupSeed + SNAPHashTable::Lookup
+                const bool comp = (int64_t)f > (int64_t)rcv;
+                const uint64_t canon = comp ? rcv : f;
+                const uint32_t table = (uint32_t)(canon >> 32);
+                const uint32_t key = (uint32_t)canon;
+                const uint64_t size = A.tableSize[table];
+                const uint32_t *T = A.slots + 3 * A.tableBase[table];
+                const uint64_t h0 = fmix32(key) % size;
+                bool found = false;
+                uint32_t v1 = 0, v2 = 0;
+                for (uint32_t j0 = 0;; j0 += 8) {
+                    uint32_t j = j0 + (lane & 7);
+                    uint64_t S_j = j <= 4 ? (uint64_t)j * (j + 1) * (2 * j + 1) / 6 : 30 + (uint64_t)(j - 4);
+                    uint64_t pos = (h0 + S_j) % size;
+                    uint32_t kj = 0, v1j = INVALID, v2j = 0;
+                    bool beyond = j > size + 5;
+                    if (lane < 8 && !beyond) { kj = T[3 * pos]; v1j = T[3 * pos + 1]; v2j = T[3 * pos + 2]; }
+                    bool stop = (j == 0) ? (kj == key && v1j != INVALID) : (kj == key || v1j == INVALID);
+                    uint64_t m = ballot(lane < 8 && (stop || beyond)) & 0xffull;
+                    if (m) {
+                        int jl = __builtin_ctzll(m);
+                        uint32_t jj = j0 + jl;
+                        bool bey = readlane(beyond ? 1 : 0, jl);
+                        st.nProbes += bey ? jj : jj + 1;
+                        uint32_t kv1 = readlaneu(v1j, jl);
+                        if (!bey && (jj == 0 || kv1 != INVALID)) { found = true; v1 = kv1; v2 = readlaneu(v2j, jl); }
+                        break;
+                    }
+                }
+                if (overdue(st, 6)) break;
+                // fillInLookedUpResults (GenomeIndex.cpp:1013-1086), both directions
+                uint32_t nH0 = 0, nH1 = 0, sg0 = 0, sg1 = 0;
+                const uint32_t *ls0 = nullptr, *ls1 = nullptr;
+                if (found) {
+                    uint32_t vf = comp ? v2 : v1, vr = comp ? v1 : v2;
+                    if (vf < A.nBases) { nH0 = 1; sg0 = vf; }
+                    else if (vf != UNUSED_SIDE) { uint32_t o = vf - A.nBases; nH0 = uni(A.overflow[o]); ls0 = A.overflow + o + 1; st.nOvf++; }
+                    if (f == rcv) { nH1 = nH0; sg1 = sg0; ls1 = ls0; }   // palindrome (GenomeIndex.cpp:1003-1006)
+                    else if (vr < A.nBases) { nH1 = 1; sg1 = vr; }
+                    else if (vr != UNUSED_SIDE) { uint32_t o = vr - A.nBases; nH1 = uni(A.overflow[o]); ls1 = A.overflow + o + 1; st.nOvf++; }
+                }
+                st.nLookups++;
+                bool applied = false;
+    #pragma unroll
+                for (uint32_t dir = 0; dir < 2; dir++) {
+                    const uint32_t nh = dir ? nH1 : nH0;
+                    if (nh > A.maxHits && !A.explore) {
+                        st.nHitsIgnored++;
+                        st.popular++;
+                    } else {
+                        uint32_t offset = dir == 0 ? next : n - seedLen - next;
+                        uint32_t lim = nh < A.maxHits ? nh : A.maxHits;
+                        st.nHitWords += lim;
+                        insert_hits<MAXLEN>(A, S, ar, st, dir, offset, lim, dir ? ls1 : ls0, dir ? sg1 : sg0,
+                                            numWeightLists, dir ? st.lps[1] : st.lps[0]);
+                        if (dir) st.nSeedsApplied[1]++; else st.nSeedsApplied[0]++;
+                        applied = true;
+                    }
+                }
+                next += seedLen;
+                if (!applied) continue;
             }
-            next += seedLen;
-            if (applied && score_wave<MAXLEN>(A, S, ar, st, false, n, rbF, rbR, &result, &flags)) { done = true; break; }
+            if (overdue(st, 7)) break;
+            if (do_score<MAXLEN>(grouped, A, S, ar, st, force, n, rbF, rbR, &result, &flags) || force) break;
+            if (overdue(st, 8)) break;
         }
-        if (!done) score_wave<MAXLEN>(A, S, ar, st, true, n, rbF, rbR, &result, &flags);
     }
     if (lane == 0) {
         snapgpu_result_t o;
@@ -482,6 +835,7 @@ __global__ __launch_bounds__(64) void align_kernel(KArgs A) {
         if (lane == 0) r = atomicAdd(A.counter, 1u);
         r = uni((uint32_t)readlane((int)r, 0));
         if (r >= A.nReads) break;
+        if (__hip_atomic_load(&g_diag[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;   // watchdog: drain
         align_one<MAXLEN>(A, S, ar, r);
     }
 }
@@ -579,6 +933,10 @@ void fillTables(DevTables &t, uint32_t seedLen) {
         for (int i = 0; i < 25; i++) t.wrap[i] = kWrap[seedLen - 16][i];
 }
 
+uint32_t packedCode(char c) {   // 2-bit code of the packed genome (4 = not ACGT)
+    return c == 'A' ? 0u : c == 'C' ? 1u : c == 'G' ? 2u : c == 'T' ? 3u : 4u;
+}
+
 int hostMapq(double pAll, double pBest, int score, int popular) {   // mapq.h:32-65
     if (pAll < pBest) pAll = pBest;
     if (pAll == pBest && popular == 0 && score < 5) return 70;
@@ -612,6 +970,7 @@ struct snapgpu_aligner {
     uint32_t *dSlots = nullptr, *dOverflow = nullptr, *dPieces = nullptr, *dCounter = nullptr;
     uint64_t *dTableBase = nullptr, *dTableSize = nullptr;
     char *dGenomeAlloc = nullptr;
+    uint32_t *dGCode = nullptr, *dGMask = nullptr;
     const char *dGenome = nullptr;
     DevTables *dTab = nullptr;
     Elem *dArena = nullptr;
@@ -622,6 +981,9 @@ struct snapgpu_aligner {
     snapgpu_aligner_stats_t stats{};
     snapgpu_device_reads_t *lastReads = nullptr;
     bool pendingTiming = false;
+    uint32_t grouped = 1;         // SNAPGPU_GROUPED=0 selects the one-candidate-per-wave scorer
+    uint32_t *dDiag = nullptr;    // g_diag (watchdog record)
+    double timeoutSec = 0;        // SNAPGPU_TIMEOUT_S
 };
 
 static const size_t kDevGuard = 1024;
@@ -653,6 +1015,7 @@ void snapgpu_aligner_free(snapgpu_aligner_t *a) {
     hipSetDevice(a->device);
     hipFree(a->dSlots); hipFree(a->dOverflow); hipFree(a->dPieces); hipFree(a->dCounter);
     hipFree(a->dTableBase); hipFree(a->dTableSize); hipFree(a->dGenomeAlloc); hipFree(a->dTab); hipFree(a->dArena);
+    hipFree(a->dGCode); hipFree(a->dGMask);
     for (auto &e : a->ev) if (e) hipEventDestroy(e);
     if (a->stream) hipStreamDestroy(a->stream);
     delete a;
@@ -672,6 +1035,8 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
     a->device = device;
     a->idx = idx;
     a->p = *params;
+    if (const char *g = getenv("SNAPGPU_GROUPED")) a->grouped = atoi(g) != 0;
+    if (const char *t = getenv("SNAPGPU_TIMEOUT_S")) a->timeoutSec = atof(t);
     auto fail = [&](const char *what, hipError_t e) {
         snapgpu::setError(std::string(what) + ": " + hipGetErrorString(e));
         snapgpu_aligner_free(a);
@@ -681,6 +1046,7 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
     if ((e = hipSetDevice(device)) != hipSuccess) return fail("hipSetDevice", e);
     if ((e = hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking)) != hipSuccess) return fail("stream", e);
     for (auto &ev : a->ev) if ((e = hipEventCreate(&ev)) != hipSuccess) return fail("event", e);
+    if ((e = hipGetSymbolAddress((void **)&a->dDiag, HIP_SYMBOL(g_diag))) != hipSuccess) return fail("g_diag", e);
     // index upload: genome with guards, tables, overflow, pieces
     const uint32_t nBases = idx->genome->nBases;
     size_t gbytes = kDevGuard + nBases + kDevGuard;
@@ -693,6 +1059,26 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
             return fail("genome upload", e);
     }
     a->dGenome = a->dGenomeAlloc + kDevGuard;
+    {
+        // 2-bit packed genome + spaced non-ACGT mask (16 bases per u32 word), covering
+        // genome positions [-kDevGuard, nBases + kDevGuard): the LV bitmaps of the
+        // grouped scorer are built from these with funnel shifts.
+        const uint64_t span = (uint64_t)nBases + 2 * kDevGuard;
+        const uint64_t nw = (span + 15) / 16 + 8;
+        std::vector<uint32_t> code(nw, 0), msk(nw, 0);
+        const char *b = idx->genome->bases();
+        for (uint64_t i = 0; i < span; i++) {
+            int64_t p = (int64_t)i - (int64_t)kDevGuard;
+            char c = (p >= 0 && p < (int64_t)nBases) ? b[p] : 'n';
+            uint32_t v = packedCode(c);
+            code[i >> 4] |= (v & 3u) << (2 * (i & 15));
+            if (v > 3) msk[i >> 4] |= 1u << (2 * (i & 15));
+        }
+        if ((e = hipMalloc(&a->dGCode, nw * 4)) != hipSuccess) return fail("hipMalloc gcode", e);
+        if ((e = hipMalloc(&a->dGMask, nw * 4)) != hipSuccess) return fail("hipMalloc gmask", e);
+        hipMemcpy(a->dGCode, code.data(), nw * 4, hipMemcpyHostToDevice);
+        if ((e = hipMemcpy(a->dGMask, msk.data(), nw * 4, hipMemcpyHostToDevice)) != hipSuccess) return fail("gmask", e);
+    }
     if ((e = hipMalloc(&a->dSlots, idx->slots.size() * 4)) != hipSuccess) return fail("hipMalloc slots", e);
     if ((e = hipMemcpy(a->dSlots, idx->slots.data(), idx->slots.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return fail("slots", e);
     if ((e = hipMalloc(&a->dOverflow, idx->overflow.size() * 4 + 16)) != hipSuccess) return fail("hipMalloc ovf", e);
@@ -772,6 +1158,8 @@ int snapgpu_align_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d) {
     const snapgpu_index_t *idx = a->idx;
     A.slots = a->dSlots; A.tableBase = a->dTableBase; A.tableSize = a->dTableSize; A.overflow = a->dOverflow;
     A.genome = a->dGenome; A.pieces = a->dPieces; A.nPieces = (int32_t)idx->genome->pieceOffsets.size();
+    A.gcode = a->dGCode; A.gmask = a->dGMask; A.hasIupac = idx->hasIupac ? 1u : 0u;
+    A.grouped = a->grouped;
     A.nBases = idx->genome->nBases; A.seedLen = idx->seedLen; A.nTables = idx->nTables;
     A.padding = idx->genome->chromosomePadding;
     A.maxHits = a->p.maxHitsToConsider; A.maxK = a->p.maxK; A.maxReadSize = a->p.maxReadSize;
@@ -785,6 +1173,7 @@ int snapgpu_align_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d) {
     if ((uint64_t)grid > d->n) grid = (int)d->n;
     (void)hipGetLastError();   // clear any stale error of an unrelated earlier runtime call
     HIPCHK(hipMemsetAsync(a->dCounter, 0, 64, a->stream));
+    HIPCHK(hipMemsetAsync(a->dDiag, 0, sizeof(uint32_t) * 4, a->stream));
     HIPCHK(hipEventRecord(a->ev[0], a->stream));
     if (d->maxLen <= 128) hipLaunchKernelGGL(align_kernel<128>, dim3(grid), dim3(64), 0, a->stream, A);
     else hipLaunchKernelGGL(align_kernel<512>, dim3(grid), dim3(64), 0, a->stream, A);
@@ -797,12 +1186,34 @@ int snapgpu_align_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d) {
 
 int snapgpu_synchronize(snapgpu_aligner_t *a) {
     if (!a) return SNAPGPU_EINVAL;
+    HIPCHK(hipSetDevice(a->device));
+    if (a->timeoutSec > 0) {   // SNAPGPU_TIMEOUT_S: fail the call instead of waiting forever
+        const auto t0 = std::chrono::steady_clock::now();
+        for (;;) {
+            hipError_t q = hipStreamQuery(a->stream);
+            if (q == hipSuccess) break;
+            if (q != hipErrorNotReady) HIPCHK(q);
+            if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > a->timeoutSec) {
+                snapgpu::setError("align kernel did not finish within SNAPGPU_TIMEOUT_S");
+                return SNAPGPU_EDEVICE;
+            }
+            std::this_thread::sleep_for(std::chrono::microseconds(200));
+        }
+    }
     HIPCHK(hipStreamSynchronize(a->stream));
     if (a->pendingTiming) {
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, a->ev[0], a->ev[1]));
         a->timing.mainKernelMs = ms;
         a->pendingTiming = false;
+        uint32_t diag[4];
+        HIPCHK(hipMemcpy(diag, a->dDiag, sizeof(diag), hipMemcpyDeviceToHost));
+        if (diag[0]) {
+            char msg[160];
+            snprintf(msg, sizeof msg, "device watchdog tripped: code %u read %u detail %u", diag[0], diag[1], diag[2]);
+            snapgpu::setError(msg);
+            return SNAPGPU_EDEVICE;
+        }
     }
     return SNAPGPU_OK;
 }
@@ -810,9 +1221,10 @@ int snapgpu_synchronize(snapgpu_aligner_t *a) {
 int snapgpu_results_download(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, snapgpu_result_t *out) {
     if (!a || !d || !out) return SNAPGPU_EINVAL;
     HIPCHK(hipSetDevice(a->device));
-    HIPCHK(hipMemcpyAsync(out, d->dOut, d->n * sizeof(snapgpu_result_t), hipMemcpyDeviceToHost, a->stream));
-    int rc = snapgpu_synchronize(a);
+    int rc = snapgpu_synchronize(a);   // before the copy: a pageable-destination copy blocks
     if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(out, d->dOut, d->n * sizeof(snapgpu_result_t), hipMemcpyDeviceToHost, a->stream));
+    HIPCHK(hipStreamSynchronize(a->stream));
     // host MAPQ fix-ups (device log10 within 1e-6 of an integer boundary)
     auto t0 = std::chrono::steady_clock::now();
     uint64_t fixed = 0;
