@@ -245,10 +245,10 @@ int  snapgpu_synchronize(snapgpu_aligner_t *a);
 /* Timing of the dominant kernel (HIP events on the aligner's own stream), in ms,
  * for the last snapgpu_align_resident / snapgpu_align_batch call. */
 typedef struct snapgpu_timing {
-    double mainKernelMs;     /* pass 1: LDS-arena aligner kernel */
-    double spillKernelMs;    /* pass 2: HBM-arena aligner kernel (spilled reads) */
+    double mainKernelMs;     /* pass 1: align_kernel<128> (reads <= 128 bases, bit-plane LV) */
+    double spillKernelMs;    /* pass 2: align_kernel<512> over the reads pass 1 deferred */
     double fixupMs;          /* host MAPQ fix-ups */
-    uint64_t nSpilled;
+    uint64_t nSpilled;       /* reads deferred to pass 2 */
     uint64_t nMapqFixed;
 } snapgpu_timing_t;
 int snapgpu_last_timing(snapgpu_aligner_t *a, snapgpu_timing_t *t);
@@ -264,6 +264,11 @@ typedef struct snapgpu_aligner_stats {
 } snapgpu_aligner_stats_t;
 int snapgpu_aligner_get_stats(const snapgpu_aligner_t *a, snapgpu_aligner_stats_t *s);
 int snapgpu_aligner_max_k(const snapgpu_aligner_t *a);           /* getMaxK() */
+/* Diagnostic (no reference equivalent): with SNAPGPU_PHASES=1 in the environment at
+ * snapgpu_aligner_create, the aligner kernel sums shader cycles per phase (setup,
+ * lookup, insert, score, pop, desc, stage, lv-fwd, lv-rev, apply, writeback, out) and
+ * counters (passes, candidates, reads) into out16[0..14]; reset != 0 zeroes them. */
+int snapgpu_phase_cycles(snapgpu_aligner_t *a, uint64_t *out16, int reset);
 const char *snapgpu_aligner_name(const snapgpu_aligner_t *a);    /* getName() */
 
 /* -------------------------------------------------------- Landau-Vishkin */

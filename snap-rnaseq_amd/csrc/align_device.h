@@ -39,7 +39,7 @@ constexpr int ELEM = 48;                  // hashTableElementSize == maxMergeDis
 constexpr uint32_t NPAD = 100;            // Genome::N_PADDING
 constexpr int NBUCKET_LOG2 = 9;
 constexpr int NBUCKET = 1 << NBUCKET_LOG2;  // element hash buckets (LDS)
-constexpr uint32_t SKCAP = 512;           // selection keys kept in LDS
+constexpr uint32_t SKCAP = 256;           // selection keys kept in LDS
 constexpr int ELEM_DWORDS = 36;           // meaningful dwords of Elem
 constexpr int BT = 128;                   // insertion-batch dedupe table (LDS)
 constexpr uint32_t NONE = 0xffffffffu;
@@ -50,6 +50,7 @@ struct DevTables {
     double perfect[512];
     double seedProb;          // __powidf2(0.999, seedLen), BaseAligner.cpp:1227
     uint32_t wrap[32];        // GetWrappedNextSeedToTest order (SeedSequencer.h)
+    double mapqT[72];         // mapqT[q] = 10^(-q/10) (glibc pow): MAPQ thresholds, no device log10
 };
 
 struct Elem {                 // 192 bytes, 64-byte aligned slots in HBM
@@ -93,15 +94,26 @@ struct KArgs {
     uint32_t *counter;
     Elem *arena;
     uint64_t arenaElems;         // per-wave capacity
-    // 2-bit packed genome (align_grouped.h)
-    const uint32_t *gcode;
-    const uint32_t *gmask;
+    // genome bit planes {hi, lo, notACGT, 0} per 32 bases, word 0 = position -PACK_GUARD
+    const uint4 *gpl;
     uint32_t hasIupac;
-    uint32_t grouped;            // use the grouped scorer (MAXLEN 128)
+    // two-pass dispatch: align_kernel<128> defers reads it cannot take (longer than
+    // 128 bases, or IUPAC codes on both sides) to align_kernel<512>
+    uint32_t *deferList;         // pass 1 appends read indices here
+    uint32_t *deferCount;        // pass 1: atomic append count; pass 2: number of reads
+    const uint32_t *readList;    // pass 2: read indices (nullptr in pass 1)
+    uint32_t phases;             // diagnostic: accumulate per-phase shader cycles (SNAPGPU_PHASES=1)
 };
 
 // ------------------------------------------------------------ wave helpers
-__device__ __forceinline__ int lane_id() { return __lane_id(); }
+// Lane id through volatile asm: the compiler cannot hoist it (or the per-lane LDS
+// addresses derived from it) out of the persistent loop, which would otherwise keep
+// ~100 lane-invariant VGPRs live for the whole kernel and halve occupancy.
+__device__ __forceinline__ int lane_id() {
+    int v;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(v));
+    return v;
+}
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 __device__ __forceinline__ int unii(int v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint64_t uni64(uint64_t v) {
@@ -111,24 +123,48 @@ __device__ __forceinline__ double unid(double v) { return __longlong_as_double((
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 __device__ __forceinline__ int readlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 __device__ __forceinline__ uint32_t readlaneu(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+__device__ __forceinline__ double readlaned(double v, int l) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    return __longlong_as_double((long long)(((uint64_t)readlaneu((uint32_t)(b >> 32), l) << 32) | readlaneu((uint32_t)b, l)));
+}
+// value of lane `src` (any lane id; ds_bpermute)
+__device__ __forceinline__ int shfl_idx(int v, int src) { return __builtin_amdgcn_ds_bpermute(src << 2, v); }
 
 __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); __builtin_amdgcn_wave_barrier(); }
-__device__ __forceinline__ int shfl_up1(int v) { return __shfl_up(v, 1); }     // lane i <- lane i-1
-__device__ __forceinline__ int shfl_down1(int v) { return __shfl_down(v, 1); } // lane i <- lane i+1
+__device__ __forceinline__ int shfl_up1(int v) {     // lane i <- lane i-1 (lane 0 keeps its own)
+    const int l = lane_id();
+    return shfl_idx(v, l == 0 ? 0 : l - 1);
+}
+__device__ __forceinline__ int shfl_down1(int v) {   // lane i <- lane i+1 (lane 63 keeps its own)
+    const int l = lane_id();
+    return shfl_idx(v, l == 63 ? 63 : l + 1);
+}
 
-__device__ __forceinline__ uint64_t max_reduce64(uint64_t v) {
+// 64-bit wave reductions without LDS: DPP butterflies inside rows, readlane across rows
+template <int CTRL, bool MAX>
+__device__ __forceinline__ uint64_t dpp_step64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, 0xf, 0xf, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL, 0xf, 0xf, false);
+    const uint64_t w = ((uint64_t)hi << 32) | lo;
+    return MAX ? (w > v ? w : v) : (w | v);
+}
+template <bool MAX>
+__device__ __forceinline__ uint64_t wave_reduce64(uint64_t v) {
+    v = dpp_step64<0xB1, MAX>(v);    // quad_perm [1,0,3,2]
+    v = dpp_step64<0x4E, MAX>(v);    // quad_perm [2,3,0,1]
+    v = dpp_step64<0x141, MAX>(v);   // row_half_mirror
+    v = dpp_step64<0x140, MAX>(v);   // row_mirror
+    uint64_t m = 0;
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        uint64_t w = __shfl_xor(v, o);
-        v = w > v ? w : v;
+    for (int r = 0; r < 4; r++) {
+        const uint64_t x = ((uint64_t)readlaneu((uint32_t)(v >> 32), 16 * r) << 32) | readlaneu((uint32_t)v, 16 * r);
+        m = MAX ? (x > m ? x : m) : (m | x);
     }
-    return v;
+    return m;
 }
-__device__ __forceinline__ uint64_t or_reduce64(uint64_t v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v |= __shfl_xor(v, o);
-    return v;
-}
+// uniform results (SGPR)
+__device__ __forceinline__ uint64_t max_reduce64(uint64_t v) { return wave_reduce64<true>(v); }
+__device__ __forceinline__ uint64_t or_reduce64(uint64_t v) { return wave_reduce64<false>(v); }
 
 __device__ __forceinline__ uint32_t fmix32(uint32_t k) {   // HashTable.h:60-72
     k ^= k >> 16; k *= 0x85ebca6bu; k ^= k >> 13; k *= 0xc2b2ae35u; k ^= k >> 16;
@@ -137,39 +173,37 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t k) {   // HashTable.h:60-72
 __device__ __forceinline__ int base_value(uint32_t c) {     // Tables.cpp:41-48
     return c == 'A' ? 0 : c == 'G' ? 1 : c == 'C' ? 2 : c == 'T' ? 3 : 4;
 }
+__device__ __forceinline__ uint32_t packed_code(uint32_t c) {   // bit-plane code (4 = not ACGT)
+    return c == 'A' ? 0u : c == 'C' ? 1u : c == 'G' ? 2u : c == 'T' ? 3u : 4u;
+}
 __device__ __forceinline__ uint32_t complement_of(uint32_t c) {   // BaseAligner.cpp:148-152 (others -> 0)
     return c == 'A' ? 'T' : c == 'G' ? 'C' : c == 'C' ? 'G' : c == 'T' ? 'A' : c == 'N' ? 'N' : 0;
 }
 
 // ------------------------------------------------------------------ LDS
-constexpr int64_t PACK_GUARD = 1024;     // packed word 0 = genome position -1024
-constexpr int EB = 8;                    // elements popped per batch
-constexpr int CAND_TARGET = 8;           // forced mode: pop until this many candidates
+constexpr int64_t PACK_GUARD = 1024;     // bit-plane word 0 = genome position -1024
+constexpr int EB = 8;                    // elements popped per batch (forced mode)
 constexpr int CANDCAP = EB * ELEM;       // candidate list capacity
-constexpr int FBS = 9;                   // per-lane bitmap stride (dwords), bank-conflict free
 
+// Scorer state of align_kernel<128> (align_score.h).
 struct GroupLds {
-    uint32_t rcode[2][128 / 16 + 2];     // read[dir] 2-bit codes, 16 bases per dword
-    uint32_t rmsk[2][128 / 16 + 2];      // spaced mask: bit 2i set if base i is not ACGT or i >= n
-    uint32_t wcode[4][(128 + 192) / 16 + 2];
-    uint32_t wmsk[4][(128 + 192) / 16 + 2];
-    uint32_t fb[WAVE * FBS];             // per-lane spaced bitmap words
+    uint64_t rpl[2][3][2];               // read[dir] bit planes {hi, lo, notACGT}, positions 0..127
     uint32_t ecache[EB][ELEM_DWORDS];    // popped elements (authoritative while in the batch)
     uint32_t eidx[EB];
     uint16_t cand[CANDCAP];              // slot << 8 | bit
-    int32_t gdesc[4][8];                 // per-group: loc, dir, s, glen, ok
-    int16_t btA[4][32];
+    int16_t btA[4][32];                  // per-group backtrace scratch
     int16_t btM[4][32];
 };
 
 template <int MAXLEN>
 struct Lds {
     static constexpr int NB = MAXLEN / 64;          // 64-position blocks
+    static constexpr bool BYTE_PATH = MAXLEN > 128; // byte-compare LV (align_device.h) vs bit planes
     char fwd[MAXLEN + 64];                          // read[FORWARD], zero slack
     char rc[MAXLEN + 64];                           // read[RC]
     char fwdQ[MAXLEN + 64];
     char rcQ[MAXLEN + 64];
-    uint32_t win[(MAXLEN + 192) / 4];               // genome window [g-64, g+n+64+64)
+    uint32_t win[BYTE_PATH ? (MAXLEN + 192) / 4 : 1];   // genome window [g-64, g+n+64+64)
     uint32_t head[NBUCKET];                         // element hash chains
     uint32_t btKey[BT];
     uint64_t btMask[BT];
@@ -179,10 +213,11 @@ struct Lds {
     uint32_t pad_[3];
     uint32_t sk[SKCAP];                             // selection keys of elements < SKCAP
     uint64_t seedUsed[NB + 1];                      // BaseAligner::seedUsed bit vector
-    int16_t btAct[MAX_K + 1];                       // LV backtrace scratch
-    int16_t btMatched[MAX_K + 1];
+    int16_t btAct[BYTE_PATH ? MAX_K + 1 : 1];       // LV backtrace scratch (byte path)
+    int16_t btMatched[BYTE_PATH ? MAX_K + 1 : 1];
     uint16_t rows[MAX_K][WAVE];                     // LV rows: (L+2) | action<<12
-    GroupLds grp;                                   // grouped scorer (align_grouped.h)
+    GroupLds grp[BYTE_PATH ? 0 : 1];                // scorer of align_kernel<128>
+    uint64_t ph[16];                                // diagnostic per-phase cycle sums (KArgs::phases)
 };
 
 // ------------------------------------------------------------ LV engine
@@ -416,6 +451,44 @@ __device__ __forceinline__ int next_piece_after(const KArgs &A, uint32_t loc) { 
         else hi = m - 1;
     }
     return -1;
+}
+
+// ------------------------------------------------------- phase diagnostics
+// With KArgs::phases set, each wave sums s_memtime deltas per phase in LDS and adds
+// them to g_phase at exit (snapgpu_phase_cycles).  Off: one SGPR test per site.
+enum : int { PH_SETUP = 0, PH_LOOKUP, PH_INSERT, PH_SCORE, PH_POP, PH_DESC, PH_STAGE, PH_LVF, PH_LVR, PH_APPLY,
+             PH_WB, PH_OUT, PH_NPASS, PH_NCAND, PH_NREAD, PH_N };
+__device__ unsigned long long g_phase[16];
+__device__ __forceinline__ uint64_t clk() { return __builtin_amdgcn_s_memtime(); }
+#define PH_T(A, v) const uint64_t v = (A).phases ? sgk::clk() : 0
+#define PH_ADD(A, S, i, v) do { if ((A).phases && sgk::lane_id() == 0) (S).ph[i] += sgk::clk() - (v); } while (0)
+#define PH_CNT(A, S, i, n) do { if ((A).phases && sgk::lane_id() == 0) (S).ph[i] += (n); } while (0)
+
+// computeMAPQ (mapq.h:32-65) without log10: floor(-10*log10(x)) >= q  <=>  x <= 10^(-q/10).
+// A ratio within 1e-9 (relative) of a threshold is flagged and re-derived on the host
+// with glibc log10 (SNAPGPU_FLAG_MAPQ_FIXED), so boundary rounding cannot differ.
+__device__ __forceinline__ int mapq_dev(const DevTables *tab, double pAll, double pBest, uint32_t score,
+                                        uint32_t popular, uint32_t *flags) {
+    if (pAll < pBest) pAll = pBest;
+    if (pAll == pBest && popular == 0 && score < 5) return 70;
+    const double c = pBest / pAll;
+    int mq;
+    if (c >= 1) mq = 69;
+    else {
+        const double x = 1 - c;
+        int lo = 0, hi = 69;                 // largest q in [0, 69] with x <= T[q] (T[0] = 1 >= x)
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (x <= tab->mapqT[mid]) lo = mid; else hi = mid - 1;
+        }
+        mq = lo;
+        const double t0 = tab->mapqT[lo], t1 = tab->mapqT[lo + 1];
+        if (fabs(x - t0) <= 1e-9 * t0 || fabs(x - t1) <= 1e-9 * t1) *flags |= SNAPGPU_FLAG_MAPQ_FIXED;
+    }
+    int pen = (int)popular - 10;
+    if (pen < 0) pen = 0;
+    mq -= pen / 2;
+    return mq < 0 ? 0 : mq;
 }
 
 // ------------------------------------------------------------ per-read state

@@ -1,0 +1,509 @@
+// align_score.h -- BaseAligner::score (BaseAligner.cpp:977-1399) for align_kernel<128>.
+//
+// Batching.  The reference scores one candidate at a time and scoreLimit shrinks as
+// better hits appear.  Landau-Vishkin with limit k' returns exactly what it returns
+// with a limit k >= k' when the answer is <= k', and -1 otherwise (the row loop is
+// the same up to the answer; LandauVishkin.h:307-449).  So candidates are scored
+// speculatively, several per pass, with the scoreLimit current at the start of the
+// pass, and then applied in the reference's order, each result clamped to the
+// scoreLimit in force at that candidate: bit-exact.
+//
+// Order.  In forced mode the reference pops the head of the highest non-empty weight
+// list until all lists are empty (BaseAligner.cpp:1071-1396); no insertion happens
+// meanwhile and scoring never relinks an element, so the pop order is fixed when
+// forced mode starts.  A batch pops up to EB elements (selection touches only the
+// LDS sort keys), fetches them from the HBM arena in one round trip, lists their
+// unscored candidates (element order, then ascending bit, BaseAligner.cpp:1133) and
+// scores the list in passes.
+//
+// One pass scores G = 64/GS candidates, one lane group of GS lanes each (GS = 16
+// for k <= 7, 32 for k <= 15, else 64).  Lane `li` of a group holds diagonal
+// x = li - (GS/2-1) as a 128-bit mismatch mask in registers,
+//   F_x[m] = read[dir][m] != genome[loc + x + m],
+// built from the genome's bit planes (hi, lo, notACGT; 32 bases per dword) with
+// funnel shifts; both the forward and the reverse LV read it.  Byte-exact: a base
+// that is not ACGT never matches, which equals the byte comparison unless read and
+// genome both hold IUPAC codes -- such reads are deferred to align_kernel<512>.
+#pragma once
+#include "align_device.h"
+
+namespace sgk {
+
+// ------------------------------------------------------------ 128-bit masks
+struct Mask128 { uint64_t lo, hi; };
+
+// first set position >= m0 (positions outside [0, 128) count as set)
+__device__ __forceinline__ int mk_first(const Mask128 &F, int m0) {
+    if (m0 >= 128 || m0 < 0) return m0;
+    const uint64_t a = m0 < 64 ? F.lo & (~0ull << m0) : 0ull;
+    const uint64_t b = m0 < 64 ? F.hi : F.hi & (~0ull << (m0 - 64));
+    return a ? __builtin_ctzll(a) : (b ? 64 + __builtin_ctzll(b) : 128);
+}
+// last set position <= m0 (positions outside [0, 128) count as set)
+__device__ __forceinline__ int mk_last(const Mask128 &F, int m0) {
+    if (m0 < 0 || m0 >= 128) return m0;
+    const uint64_t b = m0 >= 64 ? F.hi & (~0ull >> (127 - m0)) : 0ull;
+    const uint64_t a = m0 >= 64 ? F.lo : F.lo & (~0ull >> (63 - m0));
+    return b ? 127 - __builtin_clzll(b) : (a ? 63 - __builtin_clzll(a) : -1);
+}
+__device__ __forceinline__ bool mk_bit(const Mask128 &F, int m) {
+    if (m < 0 || m >= 128) return true;
+    return ((m < 64 ? F.lo >> m : F.hi >> (m - 64)) & 1) != 0;
+}
+
+// ------------------------------------------------------------ group shifts
+// lane i <- lane i-1 of its group (-2 at the group start), DPP only
+template <int GS>
+__device__ __forceinline__ int from_lower(int v) {
+    if constexpr (GS == 16) return __builtin_amdgcn_update_dpp(-2, v, 0x111, 0xf, 0xf, false);   // row_shr:1
+    else {
+        const int r = __builtin_amdgcn_update_dpp(-2, v, 0x138, 0xf, 0xf, false);               // wave_shr:1
+        return (lane_id() & (GS - 1)) == 0 ? -2 : r;
+    }
+}
+// lane i <- lane i+1 of its group (-2 at the group end)
+template <int GS>
+__device__ __forceinline__ int from_upper(int v) {
+    if constexpr (GS == 16) return __builtin_amdgcn_update_dpp(-2, v, 0x101, 0xf, 0xf, false);   // row_shl:1
+    else {
+        const int r = __builtin_amdgcn_update_dpp(-2, v, 0x130, 0xf, 0xf, false);               // wave_shl:1
+        return (lane_id() & (GS - 1)) == GS - 1 ? -2 : r;
+    }
+}
+
+// ------------------------------------------------------------ LV per group
+// LandauVishkin<DIR>::computeEditDistance (LandauVishkin.h:211-455) for every active
+// group at once; the group's answer ends up in every lane of the group.
+template <int DIR, int GS>
+__device__ __forceinline__ void lv_group(GroupLds &G, const Mask128 &F, bool gact, int p0, int patternLen,
+                                         int textLen, int k, int kmaxAll, const char *qual,
+                                         uint16_t (*rows)[WAVE], const DevTables *tab, int &outE, double &outP,
+                                         int &outNet) {
+    const int lane = lane_id();
+    const int li = lane & (GS - 1), gi = lane / GS, c = GS / 2 - 1;
+    const int d = DIR > 0 ? li - c : c - li;
+    if (k > MAX_K - 1) k = MAX_K - 1;
+    outE = -1; outP = 1.0; outNet = 0;
+    bool done = !gact;
+    const int end0 = patternLen < textLen ? patternLen : textLen;
+    const int fm = DIR > 0 ? mk_first(F, p0) - p0 : p0 - mk_last(F, p0);
+    const int v0 = fm < end0 ? fm : end0;
+    const int L0 = shfl_idx(v0, gi * GS + c);            // exact prefix on diagonal 0
+    if (!done && L0 == end0) {                          // LandauVishkin.h:290-305
+        const int result = patternLen > end0 ? patternLen - end0 : 0;
+        outP = tab->perfect[patternLen];
+        outE = result > k ? -1 : result;
+        done = true;
+    }
+    int Lp = (li == c) ? L0 : -2;
+    const int endd = patternLen < textLen - d ? patternLen : textLen - d;
+    for (int e = 1; e <= kmaxAll; e++) {
+        if (!done && e > k) done = true;                // limit reached: -1
+        if (ballot(!done) == 0) break;
+        const int lower = from_lower<GS>(Lp), upper = from_upper<GS>(Lp);
+        const int left = DIR > 0 ? lower : upper;       // L[e-1][d-1]
+        const int right = (DIR > 0 ? upper : lower) + 1;   // L[e-1][d+1] + 1
+        int best = Lp + 1, act = 0;                     // X, then D, then I if strictly greater
+        if (left > best) { best = left; act = 1; }
+        if (right > best) { best = right; act = 2; }
+        const bool active = !done && d <= e && d >= -e;
+        if (active) {
+            const int mpos = p0 + DIR * best;
+            if (best < endd) {                          // slide (LandauVishkin.h:325-354)
+                const int f = DIR > 0 ? mk_first(F, mpos) - p0 : p0 - mk_last(F, mpos);
+                best = f < endd ? f : endd;
+            } else if (!mk_bit(F, mpos)) {
+                best = endd;
+            }
+            rows[e][lane] = (uint16_t)((best + 2) | (act << 12));
+        }
+        const int Ln = active ? best : Lp;
+        const uint64_t hit = ballot(active && Ln == patternLen);
+        const uint64_t gm = GS == 64 ? hit : (hit >> (gi * GS)) & ((1ull << (GS & 63)) - 1);
+        if (gm != 0 && !done) {
+            // first diagonal in the order 0, 1, -1, 2, -2, ... (LandauVishkin.h:180-182)
+            int wd = 0;
+            for (int j = 0; j <= e; j++) {
+                const int lp = DIR > 0 ? c + j : c - j, ln = DIR > 0 ? c - j : c + j;
+                if ((gm >> lp) & 1) { wd = j; break; }
+                if (j > 0 && ((gm >> ln) & 1)) { wd = -j; break; }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            // backtrace (LandauVishkin.h:376-431), group-uniform
+            int curD = wd;
+            for (int ce = e; ce >= 1; ce--) {
+                const int ln = gi * GS + (DIR > 0 ? c + curD : c - curD);
+                const uint32_t cell = rows[ce][ln];
+                const int a = (int)(cell >> 12);
+                const int Lcur = (int)(cell & 0xfff) - 2;
+                const int src = a == 2 ? curD + 1 : (a == 1 ? curD - 1 : curD);
+                const int ls = gi * GS + (DIR > 0 ? c + src : c - src);
+                const int Lsrc = (ce - 1 == 0) ? (src == 0 ? L0 : -2) : ((int)(rows[ce - 1][ls] & 0xfff) - 2);
+                G.btA[gi][ce] = (int16_t)a;
+                G.btM[gi][ce] = (int16_t)(a == 1 ? Lcur - Lsrc : Lcur - Lsrc - 1);
+                curD = src;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            double p = 1.0;
+            int ce = 1, offset = L0, net = 0;
+            while (ce <= e) {
+                const int a = G.btA[gi][ce];
+                int cnt = 1;
+                while (ce + 1 <= e && G.btM[gi][ce] == 0 && G.btA[gi][ce + 1] == a) { cnt++; ce++; }
+                if (a == 2) { p *= tab->indel[cnt]; offset += cnt; net += cnt; }
+                else if (a == 1) { p *= tab->indel[cnt]; offset -= cnt; net -= cnt; }
+                else {
+                    for (int q = 0; q < cnt; q++) {
+                        int qi = offset < 0 ? 0 : offset;
+                        if (qi > patternLen - 1) qi = patternLen - 1;
+                        p *= tab->phred[(uint8_t)qual[p0 + DIR * qi]];
+                        offset++;
+                    }
+                }
+                offset += G.btM[gi][ce];
+                ce++;
+            }
+            p *= tab->perfect[patternLen - e];
+            outE = e; outP = p; outNet = net;
+            done = true;
+        }
+        Lp = Ln;
+    }
+}
+
+// Terminal branch of score() (BaseAligner.cpp:1081-1103) + computeMAPQ (mapq.h:32-65).
+__device__ __forceinline__ void finalize_read(const KArgs &A, ReadState &st, int *result, uint32_t *flags) {
+    st.outScore = (int32_t)st.bestScore;
+    if (st.bestScore <= A.maxK) {
+        st.outLoc = st.bestLoc;
+        const int mq = mapq_dev(A.tab, st.pAll, st.pBest, st.bestScore, st.popular, flags);
+        st.outMapq = mq;
+        *result = mq >= 10 ? SNAPGPU_SINGLE_HIT : SNAPGPU_MULTIPLE_HITS;
+    } else {
+        *result = (st.nSeedsApplied[0] == 0 && st.nSeedsApplied[1] == 0) ? SNAPGPU_MULTIPLE_HITS : SNAPGPU_NOT_FOUND;
+        st.outMapq = 0;
+    }
+}
+
+// Per-lane pass inputs: this lane's group candidate and its mismatch mask.
+struct PassLane {
+    uint32_t loc;      // genome location of the candidate (element base + bit)
+    int s;             // seed offset
+    int glen;          // genome bytes available (BaseAligner.cpp:1161-1185)
+    bool act;          // group holds a candidate whose genome window is servable
+    int dir;
+};
+
+// One speculative pass over up to G = 64/GS candidates [i0, i0+m) of the list.
+template <int GS>
+__device__ __forceinline__ void lv_pass(const KArgs &A, Lds<128> &S, uint32_t i0, int m, int k, uint32_t n,
+                                        PassLane &P, int &e1, int &e2, double &p1, double &p2, int &net2) {
+    GroupLds &G = S.grp[0];
+    const int lane = lane_id();
+    const int gi = lane / GS, li = lane & (GS - 1), c = GS / 2 - 1;
+    PH_T(A, tst);
+    P.act = gi < m;
+    P.loc = 0; P.s = 0; P.glen = (int)n; P.dir = 0;
+    if (P.act) {
+        const uint32_t cw = G.cand[i0 + gi];
+        const uint32_t sl = cw >> 8, bit = cw & 0xff;
+        const uint32_t key = G.ecache[sl][6];
+        P.loc = (key >> 1) * ELEM + bit;
+        P.dir = (int)(key & 1);
+        P.s = (int)((G.ecache[sl][12 + bit / 2] >> (16 * (bit & 1))) & 0xffff);
+        uint32_t glen = n + MAX_K;
+        bool ok = substring_ok(A, P.loc, glen);
+        if (!ok) {   // BaseAligner.cpp:1163-1185
+            uint32_t endOffset = 0;
+            bool have = false;
+            if ((uint64_t)P.loc + n + MAX_K >= A.nBases) { endOffset = A.nBases; have = true; }
+            else {
+                const int np = next_piece_after(A, P.loc);
+                if (np >= 0) { endOffset = A.pieces[np]; have = true; }
+            }
+            if (have) {
+                glen = endOffset - P.loc - 1;
+                if (glen >= n - (uint32_t)MAX_K) ok = substring_ok(A, P.loc, glen);
+            }
+        }
+        P.glen = (int)glen;
+        P.act = ok;
+    }
+    // F_x from the genome bit planes: positions loc + x + [0, 128)
+    Mask128 F;
+    {
+        const int64_t gp = (int64_t)P.loc + (li - c) + PACK_GUARD;
+        const uint4 *src = A.gpl + (gp >> 5);
+        const uint32_t sh = (uint32_t)gp & 31;
+        uint4 w[5];
+#pragma unroll
+        for (int j = 0; j < 5; j++) w[j] = src[j];
+        const uint64_t *rp = &G.rpl[P.dir][0][0];
+        const uint64_t rh0 = rp[0], rh1 = rp[1], rl0 = rp[2], rl1 = rp[3], rm0 = rp[4], rm1 = rp[5];
+        uint32_t f[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t gh = __builtin_amdgcn_alignbit(w[j + 1].x, w[j].x, sh);
+            const uint32_t gl = __builtin_amdgcn_alignbit(w[j + 1].y, w[j].y, sh);
+            const uint32_t gm = __builtin_amdgcn_alignbit(w[j + 1].z, w[j].z, sh);
+            const uint64_t RH = j < 2 ? rh0 : rh1, RL = j < 2 ? rl0 : rl1, RM = j < 2 ? rm0 : rm1;
+            const uint32_t sft = 32 * (j & 1);
+            f[j] = (gh ^ (uint32_t)(RH >> sft)) | (gl ^ (uint32_t)(RL >> sft)) | gm | (uint32_t)(RM >> sft);
+        }
+        F.lo = ((uint64_t)f[1] << 32) | f[0];
+        F.hi = ((uint64_t)f[3] << 32) | f[2];
+    }
+    PH_ADD(A, S, PH_STAGE, tst);
+    PH_T(A, tf);
+    const char *q = P.dir ? S.rcQ : S.fwdQ;
+    const int t = P.s + (int)A.seedLen;
+    int n1;
+    lv_group<1, GS>(G, F, P.act, t, (int)n - t, P.glen - t, k, k, q, S.rows, A.tab, e1, p1, n1);
+    PH_ADD(A, S, PH_LVF, tf);
+    PH_T(A, tr);
+    const int k2 = k - e1;
+    const bool ract = P.act && e1 >= 0;
+    int v = ract ? k2 : -1;   // largest reverse limit over the groups that need a reverse pass
+    v = (int)(max_reduce64((uint64_t)(uint32_t)(v + 1)) ) - 1;
+    const int kmax2 = unii(v);
+    e2 = -1; p2 = 1.0; net2 = 0;
+    if (kmax2 >= 0) lv_group<-1, GS>(G, F, ract, P.s - 1, P.s, P.s + MAX_K, k2, kmax2, q, S.rows, A.tab, e2, p2, net2);
+    PH_ADD(A, S, PH_LVR, tr);
+}
+
+// BaseAligner::score (BaseAligner.cpp:977-1399) over batches of popped elements.
+__device__ __forceinline__ bool score_batched(const KArgs &A, Lds<128> &S, Elem *ar, ReadState &st, bool force,
+                                           uint32_t n, int *result, uint32_t *flags) {
+    const int lane = lane_id();
+    GroupLds &G = S.grp[0];
+    const DevTables *tab = A.tab;
+    for (int d = 0; d < 2; d++)
+        if (st.mostSeeds[d]) {
+            const uint32_t v = st.nSeedsApplied[d] / st.mostSeeds[d];
+            if (v > st.lps[d]) st.lps[d] = v;
+        }
+    const uint32_t minLps = st.lps[0] < st.lps[1] ? st.lps[0] : st.lps[1];
+    const bool forced = force || minLps > st.scoreLimit;
+    for (uint32_t guard = 0;; guard++) {
+        if (guard > (uint32_t)A.arenaElems) {   // every batch unlinks >= 1 element
+            if (lane == 0) diag_report(DIAG_SCORE_LOOP, st.rid, S.nElems);
+            st.abort = 1;
+        }
+        if (overdue(st, 1)) return true;
+        PH_T(A, tpop);
+        // ---- pop in weight-list order (head of the highest list first); LDS only
+        uint32_t nb = 0;
+        while (nb < (uint32_t)EB) {
+            const uint64_t sel = max_reduce64(S.laneMax[lane]);
+            if (sel == 0) break;
+            const uint32_t e = (uint32_t)sel;
+            sk_set(S, ar, e, 0);                       // unlink (BaseAligner.cpp:1391-1394)
+            wave_sync();
+            if ((int)(e % WAVE) == lane) recompute_lane_max(S, ar, lane);
+            if (lane == 0) G.eidx[nb] = e;
+            nb++;
+            wave_sync();
+            if (!forced) break;
+        }
+        if (nb == 0) {
+            PH_ADD(A, S, PH_POP, tpop);
+            if (forced) { finalize_read(A, st, result, flags); return true; }
+            return false;
+        }
+        // ---- fetch the batch from the arena in one round trip
+        {
+            constexpr int NLD = (EB * ELEM_DWORDS + WAVE - 1) / WAVE;
+            const uint32_t tot = nb * ELEM_DWORDS;
+            uint32_t v[NLD];
+#pragma unroll
+            for (int j = 0; j < NLD; j++) {
+                const uint32_t idx = (uint32_t)(j * WAVE + lane);
+                v[j] = idx < tot ? ((const uint32_t *)(ar + G.eidx[idx / ELEM_DWORDS]))[idx % ELEM_DWORDS] : 0u;
+            }
+#pragma unroll
+            for (int j = 0; j < NLD; j++) {
+                const uint32_t idx = (uint32_t)(j * WAVE + lane);
+                if (idx < tot) G.ecache[idx / ELEM_DWORDS][idx % ELEM_DWORDS] = v[j];
+            }
+            wave_sync();
+        }
+        // ---- candidate list: elements in pop order, ascending bit; lane sl owns element sl
+        uint32_t nc;
+        {
+            uint64_t pend = 0;
+            if ((uint32_t)lane < nb) {
+                const uint32_t *ec = G.ecache[lane];
+                if (((ec[11] >> 8) & 0xff) <= st.scoreLimit)   // cannot be scored (the limit only shrinks)
+                    pend = (((uint64_t)ec[1] << 32) | ec[0]) & ~(((uint64_t)ec[3] << 32) | ec[2]);
+            }
+            const uint32_t cnt = (uint32_t)__popcll(pend);
+            // exclusive prefix sum over lanes 0..EB-1
+            uint32_t pos = 0;
+#pragma unroll
+            for (int j = 0; j < EB; j++) {
+                const uint32_t cj = (uint32_t)__builtin_amdgcn_readlane((int)cnt, j);
+                if (j < lane) pos += cj;
+            }
+            nc = (uint32_t)__builtin_amdgcn_readlane((int)(pos + cnt), EB - 1);
+            while (pend) {
+                const int bit = __builtin_ctzll(pend);
+                pend &= pend - 1;
+                G.cand[pos++] = (uint16_t)(lane << 8 | bit);
+            }
+            wave_sync();
+        }
+        PH_ADD(A, S, PH_POP, tpop);
+        PH_CNT(A, S, PH_NCAND, nc);
+        // current element state (SGPRs), written back to ecache on slot change
+        int curSlot = -1;
+        bool slotSkip = false;
+        uint64_t cScored = 0;
+        double cProb = 0;
+        uint32_t cBest = 0, cBestLoc = 0, cKey = 0;
+        auto flush = [&]() {
+            if (curSlot >= 0) {
+                const uint64_t pb = (uint64_t)__double_as_longlong(cProb);
+                uint32_t *ec = G.ecache[curSlot];
+                if (lane == 2) ec[2] = (uint32_t)cScored;
+                else if (lane == 3) ec[3] = (uint32_t)(cScored >> 32);
+                else if (lane == 4) ec[4] = (uint32_t)pb;
+                else if (lane == 5) ec[5] = (uint32_t)(pb >> 32);
+                else if (lane == 8) ec[8] = cBest;
+                else if (lane == 9) ec[9] = cBestLoc;
+                wave_sync();
+            }
+        };
+        for (uint32_t i0 = 0; i0 < nc;) {
+            if (overdue(st, 2)) return true;
+            const int k = st.scoreLimit < (uint32_t)(MAX_K - 1) ? (int)st.scoreLimit : MAX_K - 1;
+            const int GS = k <= 7 ? 16 : (k <= 15 ? 32 : 64);
+            const int Gn = 64 / GS;
+            const int m = (int)(nc - i0) < Gn ? (int)(nc - i0) : Gn;
+            PH_CNT(A, S, PH_NPASS, 1);
+            PassLane P;
+            int e1, e2, net2;
+            double p1, p2;
+            if (GS == 16) lv_pass<16>(A, S, i0, m, k, n, P, e1, e2, p1, p2, net2);
+            else if (GS == 32) lv_pass<32>(A, S, i0, m, k, n, P, e1, e2, p1, p2, net2);
+            else lv_pass<64>(A, S, i0, m, k, n, P, e1, e2, p1, p2, net2);
+            PH_T(A, tapp);
+            // ---- apply in order with the limit in force at each candidate
+            for (int g = 0; g < m; g++) {
+                const int ln = g * GS;
+                const uint32_t cw = uni(G.cand[i0 + g]);
+                const int sl = (int)(cw >> 8);
+                const uint32_t bit = cw & 0xff;
+                if (sl != curSlot) {                  // element entered: lps check (BaseAligner.cpp:1129)
+                    flush();
+                    curSlot = sl;
+                    const uint32_t ev = lane < 12 ? G.ecache[sl][lane] : 0u;
+                    slotSkip = ((rl(ev, 11) >> 8) & 0xff) > st.scoreLimit;
+                    cScored = rl64(ev, 2);
+                    cProb = rld(ev, 4);
+                    cKey = rl(ev, 6);
+                    cBest = rl(ev, 8);
+                    cBestLoc = rl(ev, 9);
+                }
+                if (slotSkip) continue;
+                const int r1 = readlane(e1, ln), r2 = readlane(e2, ln);
+                const bool ok = readlane(P.act ? 1 : 0, ln) != 0;
+                const int kNow = (int)(st.scoreLimit < (uint32_t)(MAX_K - 1) ? st.scoreLimit : MAX_K - 1);
+                uint32_t sc = FAIL_SCORE;
+                double prob = 0;
+                const uint32_t dir = cKey & 1;
+                const uint32_t ebase = (cKey >> 1) * ELEM;
+                uint32_t loc = ebase + bit;
+                const uint32_t elemLoc = loc;
+                if (ok && r1 >= 0 && r1 <= kNow) {
+                    // the reverse call runs with limit scoreLimit - score1 (BaseAligner.cpp:1216-1220)
+                    const int lim2 = (int)st.scoreLimit - r1 > MAX_K - 1 ? MAX_K - 1 : (int)st.scoreLimit - r1;
+                    if (r2 >= 0 && r2 <= lim2) {
+                        sc = (uint32_t)(r1 + r2);
+                        const double q1 = readlaned(p1, ln), q2 = readlaned(p2, ln);
+                        prob = q1 * q2 * tab->seedProb;
+                        loc += (uint32_t)readlane(net2, ln);
+                    }
+                }
+                // candidate bookkeeping (BaseAligner.cpp:1253-1384)
+                const uint64_t cb = 1ull << bit;
+                bool anyNearby = cScored != 0;
+                cScored |= cb;
+                st.nScored++;
+                if (anyNearby) {
+                    if (cBest < sc || (cBest == sc && prob <= cProb)) continue;
+                }
+                cBestLoc = loc;   // bestScoreGenomeLocation
+                uint32_t nb2 = NONE;
+                if (sc != FAIL_SCORE) {
+                    const uint32_t nl = elemLoc + (2 * (elemLoc % ELEM / (ELEM / 2)) - 1) * (ELEM / 2);
+                    const uint32_t nkey = ((nl / ELEM) << 1) | dir;
+                    nb2 = uni(chain_find(S.head, ar, nkey, (uint32_t)A.arenaElems));
+                }
+                if (nb2 != NONE) {
+                    // the nearby element may be in this batch: its cache is authoritative
+                    const uint64_t inb = ballot((uint32_t)lane < nb && G.eidx[lane < EB ? lane : 0] == nb2);
+                    const int cs = inb ? (int)__builtin_ctzll(inb) : -1;
+                    uint32_t nv;
+                    if (cs >= 0) nv = lane < 12 ? G.ecache[cs][lane] : 0u;
+                    else nv = lane < 12 ? ((const uint32_t *)(ar + nb2))[lane] : 0u;
+                    if (rl64(nv, 2) == 0) nb2 = NONE;   // nearby element not scored yet
+                    if (nb2 != NONE) {
+                        const uint32_t nbase = (rl(nv, 6) >> 1) * ELEM;
+                        const uint32_t nbl = rl(nv, 9);
+                        if (!((nbase > ebase && loc - nbl <= (uint32_t)ELEM) || (nbase < ebase && nbl <= (uint32_t)ELEM)))
+                            nb2 = NONE;   // sic: BaseAligner.cpp:1311-1312
+                    }
+                    if (nb2 != NONE) {
+                        const uint32_t nbs = rl(nv, 8);
+                        const double np = rld(nv, 4);
+                        if (nbs < sc || (nbs == sc && np >= prob)) continue;
+                        anyNearby = true;
+                        st.pAll = st.pAll - np > 0.0 ? st.pAll - np : 0.0;
+                        if (cs >= 0) { if (lane == 4 || lane == 5) G.ecache[cs][lane] = 0u; }
+                        else if (lane == 4 || lane == 5) ((uint32_t *)(ar + nb2))[lane] = 0u;
+                        wave_sync();
+                    }
+                }
+                st.pAll = st.pAll - cProb > 0.0 ? st.pAll - cProb : 0.0;
+                st.pAll += prob;
+                cProb = prob;
+                cBest = sc;
+                if (st.bestScore > sc || (st.bestScore == sc && prob > st.pBest)) {
+                    st.bestScore = sc;
+                    st.pBest = prob;
+                    st.bestLoc = loc;
+                    st.outLoc = loc;
+                    st.outScore = (int32_t)sc;
+                    st.outDir = dir;
+                }
+                if (A.stopOnFirst && st.bestScore <= A.maxK) {
+                    *result = SNAPGPU_MULTIPLE_HITS;
+                    st.outMapq = 0;
+                    return true;
+                }
+                st.scoreLimit = (st.bestScore < A.maxK ? st.bestScore : A.maxK) + A.extra;
+            }
+            PH_ADD(A, S, PH_APPLY, tapp);
+            i0 += (uint32_t)m;
+        }
+        flush();
+        PH_T(A, twb);
+        // ---- write the batch back (scored, prob, bestScore, bestLoc, allScored = 1)
+        for (uint32_t idx = lane; idx < nb * 8; idx += WAVE) {
+            const uint32_t sl = idx >> 3, f = idx & 7;
+            const uint32_t dw = f < 4 ? 2 + f : (f == 4 ? 8 : (f == 5 ? 9 : 11));
+            if (f < 7) {
+                uint32_t w = G.ecache[sl][dw];
+                if (dw == 11) w = (w & ~0x00ff0000u) | (1u << 16);
+                ((uint32_t *)(ar + G.eidx[sl]))[dw] = w;
+            }
+        }
+        wave_sync();
+        PH_ADD(A, S, PH_WB, twb);
+        if (!forced) return false;
+    }
+}
+
+}  // namespace sgk

@@ -11,7 +11,7 @@
 #include <vector>
 
 #include "align_device.h"
-#include "align_grouped.h"
+#include "align_score.h"
 #include "internal.h"
 
 using namespace sgk;
@@ -43,23 +43,7 @@ __device__ __forceinline__ bool score_wave(const KArgs &A, Lds<MAXLEN> &S, Elem 
                 st.outScore = (int32_t)st.bestScore;
                 if (st.bestScore <= A.maxK) {
                     st.outLoc = st.bestLoc;
-                    // computeMAPQ, mapq.h:32-65 (log10 on device; boundary cases re-derived on host)
-                    double pAll = st.pAll > st.pBest ? st.pAll : st.pBest;
-                    int mq;
-                    if (pAll == st.pBest && st.popular == 0 && st.bestScore < 5) mq = 70;
-                    else {
-                        double c = st.pBest / pAll;
-                        if (c >= 1) mq = 69;
-                        else {
-                            double v = -10 * log10(1 - c);
-                            mq = v < 69.0 ? (int)v : 69;
-                            if (v < 70.0 && fabs(v - rint(v)) < 1e-6) *flags |= SNAPGPU_FLAG_MAPQ_FIXED;
-                        }
-                        int pen = (int)st.popular - 10;
-                        if (pen < 0) pen = 0;
-                        mq -= pen / 2;
-                        if (mq < 0) mq = 0;
-                    }
+                    const int mq = mapq_dev(A.tab, st.pAll, st.pBest, st.bestScore, st.popular, flags);
                     st.outMapq = mq;
                     *result = mq >= 10 ? SNAPGPU_SINGLE_HIT : SNAPGPU_MULTIPLE_HITS;
                 } else {
@@ -211,309 +195,6 @@ __device__ __forceinline__ bool score_wave(const KArgs &A, Lds<MAXLEN> &S, Elem 
     return false;
 }
 
-// ---------------------------------------------------- grouped scorer (MAXLEN 128)
-// Terminal branch of score() (BaseAligner.cpp:1081-1103) + computeMAPQ (mapq.h:32-65).
-__device__ __forceinline__ void finalize_read(const KArgs &A, ReadState &st, int *result, uint32_t *flags) {
-    st.outScore = (int32_t)st.bestScore;
-    if (st.bestScore <= A.maxK) {
-        st.outLoc = st.bestLoc;
-        double pAll = st.pAll > st.pBest ? st.pAll : st.pBest;
-        int mq;
-        if (pAll == st.pBest && st.popular == 0 && st.bestScore < 5) mq = 70;
-        else {
-            double c = st.pBest / pAll;
-            if (c >= 1) mq = 69;
-            else {
-                double v = -10 * log10(1 - c);
-                mq = v < 69.0 ? (int)v : 69;
-                if (v < 70.0 && fabs(v - rint(v)) < 1e-6) *flags |= SNAPGPU_FLAG_MAPQ_FIXED;
-            }
-            int pen = (int)st.popular - 10;
-            if (pen < 0) pen = 0;
-            mq -= pen / 2;
-            if (mq < 0) mq = 0;
-        }
-        st.outMapq = mq;
-        *result = mq >= 10 ? SNAPGPU_SINGLE_HIT : SNAPGPU_MULTIPLE_HITS;
-    } else {
-        *result = (st.nSeedsApplied[0] == 0 && st.nSeedsApplied[1] == 0) ? SNAPGPU_MULTIPLE_HITS : SNAPGPU_NOT_FOUND;
-        st.outMapq = 0;
-    }
-}
-
-// One speculative pass over up to G = 64/GS candidates: builds the per-lane bitmaps
-// from the packed genome and runs forward then reverse LV in lane groups.  Lane
-// results are group-uniform; the caller reads them with readlane(gi * GS).
-template <int GS>
-__device__ __forceinline__ void lv_pass(const KArgs &A, Lds<128> &S, int m, int k, uint32_t n, int &e1, int &e2,
-                                        double &p1, double &p2, int &net2) {
-    GroupLds &G = S.grp;
-    const int lane = lane_id();
-    const int gi = lane / GS, li = lane & (GS - 1), c = GS / 2 - 1;
-    const bool gact = gi < m && G.gdesc[gi < 4 ? gi : 0][4] != 0;
-    // stage the packed windows: genome [loc - 64, loc + n + 128) of every group
-    constexpr int WW = (128 + 192) / 16 + 2;
-    for (int idx = lane; idx < m * 2 * WW; idx += WAVE) {
-        int g = idx / (2 * WW), r = idx % (2 * WW);
-        int w = r % WW;
-        int64_t ws = (((int64_t)(uint32_t)G.gdesc[g][0] - 64 + PACK_GUARD) >> 4) + w;
-        if (r < WW) G.wcode[g][w] = A.gcode[ws];
-        else G.wmsk[g][w] = A.gmask[ws];
-    }
-    wave_sync();
-    const int gsel = gi < 4 ? gi : 0;
-    // groups past m hold stale (or, on a fresh kernel, uninitialised) descriptors
-    const uint32_t loc = gact ? (uint32_t)G.gdesc[gsel][0] : 0u;
-    const int dir = gact ? G.gdesc[gsel][1] & 1 : 0;
-    const int s = gact ? G.gdesc[gsel][2] : 0;
-    const int glen = gact ? G.gdesc[gsel][3] : (int)n;
-    // F_x[m] = read[dir][m] != genome[loc + x + m], 2 bits per position (bit 2m)
-    {
-        const int x = li - c;
-        const int64_t wbase = ((int64_t)loc - 64 + PACK_GUARD) & ~(int64_t)15;   // genome pos of wcode word 0, +guard
-        const int rel0 = (int)((int64_t)loc + PACK_GUARD - wbase) + x;
-        uint32_t *fb = G.fb + lane * FBS;
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            int r = rel0 + 16 * j;
-            int wi = r >> 4;
-            uint32_t sh = 2 * (r & 15);
-            uint32_t gc = __builtin_amdgcn_alignbit(G.wcode[gsel][wi + 1], G.wcode[gsel][wi], sh);
-            uint32_t gm = __builtin_amdgcn_alignbit(G.wmsk[gsel][wi + 1], G.wmsk[gsel][wi], sh);
-            uint32_t dd = gc ^ G.rcode[dir][j];
-            uint32_t y = (dd | (dd >> 1)) & 0x55555555u;
-            fb[j] = y | gm | G.rmsk[dir][j];
-        }
-    }
-    wave_sync();
-    const char *q = dir ? S.rcQ : S.fwdQ;
-    const int t = s + (int)A.seedLen;
-    int n1;
-    double pp1;
-    lv_group<1, GS>(G, gact, t, (int)n - t, glen - t, k, k, q, S.rows, A.tab, e1, pp1, n1);
-    int k2 = k - e1;
-    const bool ract = gact && e1 >= 0;
-    int kmax2 = 0;
-    {
-        // largest reverse limit over the groups that need a reverse pass
-        int v = ract ? k2 : -1;
-        for (int o = 32; o >= 1; o >>= 1) { int w2 = __shfl_xor(v, o); v = w2 > v ? w2 : v; }
-        kmax2 = unii(v);
-    }
-    e2 = -1; p2 = 1.0; net2 = 0;
-    if (kmax2 >= 0) lv_group<-1, GS>(G, ract, s - 1, s, s + MAX_K, k2, kmax2, q, S.rows, A.tab, e2, p2, net2);
-    p1 = pp1;
-    (void)li;
-}
-
-// BaseAligner::score (BaseAligner.cpp:977-1399) over batches of popped elements.
-template <int MAXLEN>
-__device__ bool score_wave_v2(const KArgs &A, Lds<MAXLEN> &S, Elem *ar, ReadState &st, bool force, uint32_t n,
-                              int *result, uint32_t *flags) {
-    const int lane = lane_id();
-    GroupLds &G = S.grp;
-    const DevTables *tab = A.tab;
-    for (int d = 0; d < 2; d++)
-        if (st.mostSeeds[d]) {
-            uint32_t v = st.nSeedsApplied[d] / st.mostSeeds[d];
-            if (v > st.lps[d]) st.lps[d] = v;
-        }
-    const uint32_t minLps = st.lps[0] < st.lps[1] ? st.lps[0] : st.lps[1];
-    const bool forced = force || minLps > st.scoreLimit;
-    for (uint32_t guard = 0;; guard++) {
-        if (guard > (uint32_t)A.arenaElems) {   // every batch unlinks >= 1 element
-            if (lane == 0) diag_report(DIAG_SCORE_LOOP, st.rid, S.nElems);
-            st.abort = 1;
-        }
-        if (overdue(st, 1)) return true;
-        // ---- pop elements in weight-list order (head of highest list first)
-        uint32_t nb = 0, ncand = 0;
-        while (nb < (uint32_t)EB) {
-            uint64_t sel = uni64(max_reduce64(S.laneMax[lane]));
-            if (sel == 0) break;
-            const uint32_t e = (uint32_t)sel;
-            sk_set(S, ar, e, 0);                       // unlink (BaseAligner.cpp:1391-1394)
-            wave_sync();
-            if ((int)(e % WAVE) == lane) recompute_lane_max(S, ar, lane);
-            const uint32_t *ew = (const uint32_t *)(ar + e);
-            const uint32_t ev = lane < ELEM_DWORDS ? ew[lane] : 0u;
-            if (lane < ELEM_DWORDS) G.ecache[nb][lane] = ev;
-            if (lane == 0) G.eidx[nb] = e;
-            const uint64_t pend = rl64(ev, 0) & ~rl64(ev, 2);
-            if (((rl(ev, 11) >> 8) & 0xff) <= st.scoreLimit) ncand += (uint32_t)__popcll(pend);
-            nb++;
-            wave_sync();
-            if (!forced || ncand >= (uint32_t)CAND_TARGET) break;
-        }
-        if (nb == 0) {
-            if (forced) { finalize_read(A, st, result, flags); return true; }
-            return false;
-        }
-        // ---- candidate list in the reference's order: elements, then ascending bit
-        uint32_t nc = 0;
-        for (uint32_t sl = 0; sl < nb; sl++) {
-            const uint32_t lpsv = (G.ecache[sl][11] >> 8) & 0xff;
-            if (lpsv > st.scoreLimit) continue;          // cannot be scored (limit only shrinks)
-            uint64_t pend = ((uint64_t)G.ecache[sl][1] << 32 | G.ecache[sl][0]) &
-                            ~((uint64_t)G.ecache[sl][3] << 32 | G.ecache[sl][2]);
-            while (pend) {
-                int bit = __builtin_ctzll(pend);
-                pend &= pend - 1;
-                if (lane == 0) G.cand[nc] = (uint16_t)(sl << 8 | bit);
-                nc++;
-            }
-        }
-        wave_sync();
-        uint32_t curSlot = 0xffffffffu;
-        bool slotSkip = false;
-        for (uint32_t i0 = 0; i0 < nc;) {
-            if (overdue(st, 2)) return true;
-            const int k = st.scoreLimit < (uint32_t)(MAX_K - 1) ? (int)st.scoreLimit : MAX_K - 1;
-            const int GS = k <= 7 ? 16 : (k <= 15 ? 32 : 64);
-            const int Gn = 64 / GS;
-            const int m = (int)(nc - i0) < Gn ? (int)(nc - i0) : Gn;
-            // group descriptors
-            for (int g = 0; g < m; g++) {
-                const uint32_t cw = uni(G.cand[i0 + g]);
-                const uint32_t sl = cw >> 8, bit = cw & 0xff;
-                const uint32_t key = uni(G.ecache[sl][6]);
-                const uint32_t loc = (key >> 1) * ELEM + bit;
-                const uint32_t s = (uni(G.ecache[sl][12 + bit / 2]) >> (16 * (bit & 1))) & 0xffff;
-                uint32_t glen = n + MAX_K;
-                bool ok = substring_ok(A, loc, glen);
-                if (!ok) {   // BaseAligner.cpp:1163-1185
-                    uint32_t endOffset = 0;
-                    bool have = false;
-                    if ((uint64_t)loc + n + MAX_K >= A.nBases) { endOffset = A.nBases; have = true; }
-                    else {
-                        int np = next_piece_after(A, loc);
-                        if (np >= 0) { endOffset = A.pieces[np]; have = true; }
-                    }
-                    if (have) {
-                        glen = endOffset - loc - 1;
-                        if (glen >= n - (uint32_t)MAX_K) ok = substring_ok(A, loc, glen);
-                    }
-                }
-                if (lane == 0) {
-                    G.gdesc[g][0] = (int32_t)loc; G.gdesc[g][1] = (int32_t)(key & 1);
-                    G.gdesc[g][2] = (int32_t)s; G.gdesc[g][3] = (int32_t)glen; G.gdesc[g][4] = ok ? 1 : 0;
-                }
-            }
-            wave_sync();
-            int e1, e2, net2;
-            double p1, p2;
-            if (GS == 16) lv_pass<16>(A, S, m, k, n, e1, e2, p1, p2, net2);
-            else if (GS == 32) lv_pass<32>(A, S, m, k, n, e1, e2, p1, p2, net2);
-            else lv_pass<64>(A, S, m, k, n, e1, e2, p1, p2, net2);
-            // ---- apply in order with the limit in force at each candidate
-            for (int g = 0; g < m; g++) {
-                const uint32_t cw = uni(G.cand[i0 + g]);
-                const uint32_t sl = cw >> 8, bit = cw & 0xff;
-                if (sl != curSlot) {                  // element entered: lps check (BaseAligner.cpp:1129)
-                    curSlot = sl;
-                    slotSkip = ((uni(G.ecache[sl][11]) >> 8) & 0xff) > st.scoreLimit;
-                }
-                if (slotSkip) continue;
-                const int ln = g * GS;
-                const int r1 = readlane(e1, ln), r2 = readlane(e2, ln);
-                const bool ok = uni((uint32_t)G.gdesc[g][4]) != 0;
-                const int kNow = (int)(st.scoreLimit < (uint32_t)(MAX_K - 1) ? st.scoreLimit : MAX_K - 1);
-                uint32_t sc = FAIL_SCORE;
-                double prob = 0;
-                const uint32_t key = uni(G.ecache[sl][6]);
-                const uint32_t dir = key & 1;
-                const uint32_t ebase = (key >> 1) * ELEM;
-                uint32_t loc = ebase + bit;
-                const uint32_t elemLoc = loc;
-                if (ok && r1 >= 0 && r1 <= kNow) {
-                    // the reverse call runs with limit scoreLimit - score1 (BaseAligner.cpp:1216-1220)
-                    const int lim2 = (int)st.scoreLimit - r1 > MAX_K - 1 ? MAX_K - 1 : (int)st.scoreLimit - r1;
-                    if (r2 >= 0 && r2 <= lim2) {
-                        sc = (uint32_t)(r1 + r2);
-                        double q1 = unid(__shfl(p1, ln)), q2 = unid(__shfl(p2, ln));
-                        prob = q1 * q2 * tab->seedProb;
-                        loc += (uint32_t)readlane(net2, ln);
-                    }
-                }
-                // candidate bookkeeping (BaseAligner.cpp:1253-1384) on the cached element
-                uint64_t scored = ((uint64_t)uni(G.ecache[sl][3]) << 32) | uni(G.ecache[sl][2]);
-                const uint64_t cb = 1ull << bit;
-                bool anyNearby = scored != 0;
-                scored |= cb;
-                if (lane == 0) { G.ecache[sl][2] = (uint32_t)scored; G.ecache[sl][3] = (uint32_t)(scored >> 32); }
-                st.nScored++;
-                const uint32_t ebest = uni(G.ecache[sl][8]);
-                const double eprob = __longlong_as_double(((long long)uni(G.ecache[sl][5]) << 32) | uni(G.ecache[sl][4]));
-                if (anyNearby) {
-                    if (ebest < sc || (ebest == sc && prob <= eprob)) { wave_sync(); continue; }
-                }
-                if (lane == 0) G.ecache[sl][9] = loc;   // bestScoreGenomeLocation
-                uint32_t nb2 = NONE;
-                if (sc != FAIL_SCORE) {
-                    uint32_t nl = elemLoc + (2 * (elemLoc % ELEM / (ELEM / 2)) - 1) * (ELEM / 2);
-                    uint32_t nkey = ((nl / ELEM) << 1) | dir;
-                    nb2 = uni(chain_find(S.head, ar, nkey, (uint32_t)A.arenaElems));
-                }
-                if (nb2 != NONE) {
-                    int cs = -1;   // the nearby element may be in this batch: its cache is authoritative
-                    for (uint32_t q = 0; q < nb; q++) if (uni(G.eidx[q]) == nb2) cs = (int)q;
-                    uint32_t nv;
-                    if (cs >= 0) nv = lane < 12 ? G.ecache[cs][lane] : 0u;
-                    else nv = lane < 12 ? ((const uint32_t *)(ar + nb2))[lane] : 0u;
-                    if (rl64(nv, 2) == 0) nb2 = NONE;
-                    if (nb2 != NONE) {
-                        uint32_t nbase = (rl(nv, 6) >> 1) * ELEM;
-                        uint32_t nbl = rl(nv, 9);
-                        if (!((nbase > ebase && loc - nbl <= (uint32_t)ELEM) || (nbase < ebase && nbl <= (uint32_t)ELEM)))
-                            nb2 = NONE;   // sic: BaseAligner.cpp:1311-1312
-                    }
-                    if (nb2 != NONE) {
-                        uint32_t nbs = rl(nv, 8);
-                        double np = rld(nv, 4);
-                        if (nbs < sc || (nbs == sc && np >= prob)) { wave_sync(); continue; }
-                        anyNearby = true;
-                        st.pAll = st.pAll - np > 0.0 ? st.pAll - np : 0.0;
-                        if (cs >= 0) { if (lane == 4 || lane == 5) G.ecache[cs][lane] = 0u; }
-                        else if (lane == 4 || lane == 5) ((uint32_t *)(ar + nb2))[lane] = 0u;
-                    }
-                }
-                st.pAll = st.pAll - eprob > 0.0 ? st.pAll - eprob : 0.0;
-                st.pAll += prob;
-                {
-                    const uint64_t pb = (uint64_t)__double_as_longlong(prob);
-                    if (lane == 0) { G.ecache[sl][4] = (uint32_t)pb; G.ecache[sl][5] = (uint32_t)(pb >> 32); G.ecache[sl][8] = sc; }
-                }
-                if (st.bestScore > sc || (st.bestScore == sc && prob > st.pBest)) {
-                    st.bestScore = sc;
-                    st.pBest = prob;
-                    st.bestLoc = loc;
-                    st.outLoc = loc;
-                    st.outScore = (int32_t)sc;
-                    st.outDir = dir;
-                }
-                wave_sync();
-                if (A.stopOnFirst && st.bestScore <= A.maxK) {
-                    *result = SNAPGPU_MULTIPLE_HITS;
-                    st.outMapq = 0;
-                    return true;
-                }
-                st.scoreLimit = (st.bestScore < A.maxK ? st.bestScore : A.maxK) + A.extra;
-            }
-            i0 += (uint32_t)m;
-        }
-        // ---- write the batch back (scored, prob, bestScore, bestLoc, allScored = 1)
-        for (uint32_t sl = 0; sl < nb; sl++) {
-            const uint32_t e = uni(G.eidx[sl]);
-            uint32_t w = lane < ELEM_DWORDS ? G.ecache[sl][lane] : 0u;
-            if (lane == 11) w = (w & ~0x00ff0000u) | (1u << 16);
-            if (lane == 2 || lane == 3 || lane == 4 || lane == 5 || lane == 8 || lane == 9 || lane == 11)
-                ((uint32_t *)(ar + e))[lane] = w;
-        }
-        wave_sync();
-        if (!forced) return false;
-    }
-}
-
 // ------------------------------------------------------------ hit insertion
 // The per-hit loop of BaseAligner.cpp:829-869 (findCandidate / incrementWeight /
 // allocateNewCandidate) for one seed in one direction.
@@ -604,14 +285,9 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
     st.ts += lim;
 }
 
-template <int MAXLEN>
-__device__ __forceinline__ bool do_score(bool grouped, const KArgs &A, Lds<MAXLEN> &S, Elem *ar, ReadState &st,
-                                         bool force, uint32_t n, const uint32_t (&rbF)[MAXLEN / 64],
-                                         const uint32_t (&rbR)[MAXLEN / 64], int *result, uint32_t *flags) {
-    if constexpr (MAXLEN == 128) {
-        if (grouped) return score_wave_v2<MAXLEN>(A, S, ar, st, force, n, result, flags);
-    }
-    return score_wave<MAXLEN>(A, S, ar, st, force, n, rbF, rbR, result, flags);
+// pass 1 -> pass 2 hand-off (KArgs::deferList)
+__device__ __forceinline__ void defer_read(const KArgs &A, uint32_t r) {
+    if (lane_id() == 0) A.deferList[atomicAdd(A.deferCount, 1u)] = r;
 }
 
 // ------------------------------------------------------------- AlignRead
@@ -619,6 +295,7 @@ template <int MAXLEN>
 __device__ void align_one(const KArgs &A, Lds<MAXLEN> &S, Elem *ar, uint32_t r) {
     constexpr int NB = MAXLEN / 64;
     const int lane = lane_id();
+    PH_T(A, tsetup);
     const uint32_t n = A.lengths[r];
     const uint64_t off = A.offsets[r];
     const uint32_t seedLen = A.seedLen;
@@ -636,10 +313,12 @@ __device__ void align_one(const KArgs &A, Lds<MAXLEN> &S, Elem *ar, uint32_t r) 
     const uint32_t maxSeeds = A.maxSeedsCmd ? A.maxSeedsCmd : (uint32_t)(int)(A.seedCoverage * n / seedLen);
     const uint32_t numWeightLists = maxSeeds + 1;
     bool run = true;
+    if constexpr (MAXLEN == 128) {
+        if (n > 128) { defer_read(A, r); return; }
+    }
     if (n > A.maxReadSize || n > (uint32_t)MAXLEN) { flags |= SNAPGPU_FLAG_READ_TOO_LONG; run = false; }
     else if (n < seedLen) run = false;
     uint32_t rbF[NB], rbR[NB];
-    bool grouped = false;
     if (run) {
         // Read::init upper-casing + BaseAligner.cpp:636-650 (RC read, qualities)
         uint32_t nN = 0;
@@ -661,33 +340,36 @@ __device__ void align_one(const KArgs &A, Lds<MAXLEN> &S, Elem *ar, uint32_t r) 
             nN += __popcll(ballot(i < (int)n && c == 'N'));
             other |= ballot(i < (int)n && c != 'A' && c != 'C' && c != 'G' && c != 'T' && c != 'N') != 0;
         }
+        if constexpr (MAXLEN == 128) {
+            // bit planes compare bytes exactly unless both the read and the genome hold
+            // non-ACGTN bytes (an IUPAC code could then match itself): byte path
+            if (A.hasIupac && other) { defer_read(A, r); return; }
+        }
         for (int i = lane; i < NBUCKET; i += WAVE) S.head[i] = NONE;
         for (int i = lane; i < BT; i += WAVE) { S.btKey[i] = NONE; S.btMask[i] = 0; }
         S.laneMax[lane] = 0;
         if (lane == 0) S.nElems = 0;
         wave_sync();
+        if constexpr (Lds<MAXLEN>::BYTE_PATH) {
 #pragma unroll
-        for (int b = 0; b < NB; b++) { rbF[b] = (uint8_t)S.fwd[b * 64 + lane]; rbR[b] = (uint8_t)S.rc[b * 64 + lane]; }
-        if (nN > A.maxK) { flags |= SNAPGPU_FLAG_TOO_MANY_NS; run = false; }
-        // grouped scorer: packed-code comparison is byte-exact unless both the read and
-        // the genome hold non-ACGTN bytes (an IUPAC code could then match itself)
-        grouped = MAXLEN == 128 && A.grouped && !(A.hasIupac && other);
-        if (MAXLEN == 128) {
-            for (int idx = lane; idx < 2 * (128 / 16 + 2); idx += WAVE) {
-                const int dr = idx / (128 / 16 + 2), w = idx % (128 / 16 + 2);
-                const char *src = dr ? S.rc : S.fwd;
-                uint32_t code = 0, msk = 0;
-                for (int i = 0; i < 16; i++) {
-                    uint32_t v = sgk::packed_code((uint8_t)src[16 * w + i]);   // zero slack past n -> non-ACGT
-                    code |= (v & 3u) << (2 * i);
-                    if (v > 3) msk |= 1u << (2 * i);
+            for (int b = 0; b < NB; b++) { rbF[b] = (uint8_t)S.fwd[b * 64 + lane]; rbR[b] = (uint8_t)S.rc[b * 64 + lane]; }
+        } else {
+            // read bit planes {hi, lo, notACGT} of both directions; zero slack past n is not ACGT
+#pragma unroll
+            for (int dr = 0; dr < 2; dr++)
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const uint32_t code = packed_code((uint8_t)(dr ? S.rc : S.fwd)[h * 64 + lane]);
+                    const uint64_t bh = ballot(code < 4 && (code & 2)), bl = ballot(code < 4 && (code & 1));
+                    const uint64_t bm = ballot(code > 3);
+                    if (lane == 0) { S.grp[0].rpl[dr][0][h] = bh; S.grp[0].rpl[dr][1][h] = bl; S.grp[0].rpl[dr][2][h] = bm; }
                 }
-                S.grp.rcode[dr][w] = code;
-                S.grp.rmsk[dr][w] = msk;
-            }
             wave_sync();
         }
+        if (nN > A.maxK) { flags |= SNAPGPU_FLAG_TOO_MANY_NS; run = false; }
     }
+    PH_ADD(A, S, PH_SETUP, tsetup);
+    PH_CNT(A, S, PH_NREAD, 1);
     if (run) {
         st.lps[0] = st.lps[1] = 0;
         st.mostSeeds[0] = st.mostSeeds[1] = 1;
@@ -718,6 +400,7 @@ __device__ void align_one(const KArgs &A, Lds<MAXLEN> &S, Elem *ar, uint32_t r) 
                 }
             }
             if (!force) {
+                PH_T(A, tlk);
                 while (next < nPossible && ((uni64(seedUsed[next >> 6]) >> (next & 63)) & 1)) next++;
                 if (next >= nPossible) continue;
                 {
@@ -775,6 +458,7 @@ __device__ void align_one(const KArgs &A, Lds<MAXLEN> &S, Elem *ar, uint32_t r) 
                     else if (vr != UNUSED_SIDE) { uint32_t o = vr - A.nBases; nH1 = uni(A.overflow[o]); ls1 = A.overflow + o + 1; st.nOvf++; }
                 }
                 st.nLookups++;
+                PH_ADD(A, S, PH_LOOKUP, tlk);
                 bool applied = false;
     #pragma unroll
                 for (uint32_t dir = 0; dir < 2; dir++) {
@@ -786,8 +470,10 @@ __device__ void align_one(const KArgs &A, Lds<MAXLEN> &S, Elem *ar, uint32_t r) 
                         uint32_t offset = dir == 0 ? next : n - seedLen - next;
                         uint32_t lim = nh < A.maxHits ? nh : A.maxHits;
                         st.nHitWords += lim;
+                        PH_T(A, tins);
                         insert_hits<MAXLEN>(A, S, ar, st, dir, offset, lim, dir ? ls1 : ls0, dir ? sg1 : sg0,
                                             numWeightLists, dir ? st.lps[1] : st.lps[0]);
+                        PH_ADD(A, S, PH_INSERT, tins);
                         if (dir) st.nSeedsApplied[1]++; else st.nSeedsApplied[0]++;
                         applied = true;
                     }
@@ -796,10 +482,16 @@ __device__ void align_one(const KArgs &A, Lds<MAXLEN> &S, Elem *ar, uint32_t r) 
                 if (!applied) continue;
             }
             if (overdue(st, 7)) break;
-            if (do_score<MAXLEN>(grouped, A, S, ar, st, force, n, rbF, rbR, &result, &flags) || force) break;
+            PH_T(A, tsc);
+            bool fin;
+            if constexpr (Lds<MAXLEN>::BYTE_PATH) fin = score_wave<MAXLEN>(A, S, ar, st, force, n, rbF, rbR, &result, &flags);
+            else fin = score_batched(A, S, ar, st, force, n, &result, &flags);
+            PH_ADD(A, S, PH_SCORE, tsc);
+            if (fin || force) break;
             if (overdue(st, 8)) break;
         }
     }
+    PH_T(A, tout);
     if (lane == 0) {
         snapgpu_result_t o;
         o.location = st.outLoc;
@@ -823,6 +515,7 @@ __device__ void align_one(const KArgs &A, Lds<MAXLEN> &S, Elem *ar, uint32_t r) 
         A.out[r] = o;
     }
     wave_sync();
+    PH_ADD(A, S, PH_OUT, tout);
 }
 
 template <int MAXLEN>
@@ -830,14 +523,18 @@ __global__ __launch_bounds__(64) void align_kernel(KArgs A) {
     __shared__ Lds<MAXLEN> S;
     Elem *ar = A.arena + (uint64_t)blockIdx.x * A.arenaElems;
     const int lane = lane_id();
+    if (A.phases && lane < 16) S.ph[lane] = 0;
+    const uint32_t total = A.readList ? uni(*A.deferCount) : A.nReads;
     for (;;) {
-        uint32_t r = 0;
-        if (lane == 0) r = atomicAdd(A.counter, 1u);
-        r = uni((uint32_t)readlane((int)r, 0));
-        if (r >= A.nReads) break;
+        uint32_t i = 0;
+        if (lane == 0) i = atomicAdd(A.counter, 1u);
+        i = uni((uint32_t)readlane((int)i, 0));
+        if (i >= total) break;
+        const uint32_t r = A.readList ? uni(A.readList[i]) : i;
         if (__hip_atomic_load(&g_diag[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;   // watchdog: drain
         align_one<MAXLEN>(A, S, ar, r);
     }
+    if (A.phases && lane < 16) atomicAdd(&g_phase[lane], (unsigned long long)S.ph[lane]);
 }
 
 // LV parity kernel: one wave per task; the task's "read" and virtual genome are
@@ -929,6 +626,7 @@ void fillTables(DevTables &t, uint32_t seedLen) {
     t.perfect[0] = 1.0;
     for (int i = 1; i < 512; i++) t.perfect[i] = t.perfect[i - 1] * (1 - 0.001);
     t.seedProb = powi_libgcc(1 - 0.001, (int)seedLen);
+    for (int q = 0; q < 72; q++) t.mapqT[q] = q < 70 ? pow(10.0, -q / 10.0) : 0.0;
     if (seedLen >= 16 && seedLen <= 25)
         for (int i = 0; i < 25; i++) t.wrap[i] = kWrap[seedLen - 16][i];
 }
@@ -957,6 +655,7 @@ struct snapgpu_device_reads {
     uint64_t *dOffsets = nullptr;
     uint32_t *dLengths = nullptr;
     snapgpu_result_t *dOut = nullptr;
+    uint32_t *dDefer = nullptr;   // pass 1 -> pass 2 read list
     uint64_t n = 0;
     uint32_t maxLen = 0;
     int device = 0;
@@ -970,19 +669,20 @@ struct snapgpu_aligner {
     uint32_t *dSlots = nullptr, *dOverflow = nullptr, *dPieces = nullptr, *dCounter = nullptr;
     uint64_t *dTableBase = nullptr, *dTableSize = nullptr;
     char *dGenomeAlloc = nullptr;
-    uint32_t *dGCode = nullptr, *dGMask = nullptr;
+    uint4 *dGPlanes = nullptr;    // genome bit planes (KArgs::gpl)
     const char *dGenome = nullptr;
     DevTables *dTab = nullptr;
     Elem *dArena = nullptr;
     uint64_t arenaElems = 0;
-    int grid = 0;
+    int grid = 0, grid512 = 0;
     hipEvent_t ev[4] = {};
     snapgpu_timing_t timing{};
     snapgpu_aligner_stats_t stats{};
     snapgpu_device_reads_t *lastReads = nullptr;
     bool pendingTiming = false;
-    uint32_t grouped = 1;         // SNAPGPU_GROUPED=0 selects the one-candidate-per-wave scorer
     uint32_t *dDiag = nullptr;    // g_diag (watchdog record)
+    unsigned long long *dPhase = nullptr;   // g_phase (SNAPGPU_PHASES=1 diagnostics)
+    uint32_t phases = 0;
     double timeoutSec = 0;        // SNAPGPU_TIMEOUT_S
 };
 
@@ -1015,7 +715,7 @@ void snapgpu_aligner_free(snapgpu_aligner_t *a) {
     hipSetDevice(a->device);
     hipFree(a->dSlots); hipFree(a->dOverflow); hipFree(a->dPieces); hipFree(a->dCounter);
     hipFree(a->dTableBase); hipFree(a->dTableSize); hipFree(a->dGenomeAlloc); hipFree(a->dTab); hipFree(a->dArena);
-    hipFree(a->dGCode); hipFree(a->dGMask);
+    hipFree(a->dGPlanes);
     for (auto &e : a->ev) if (e) hipEventDestroy(e);
     if (a->stream) hipStreamDestroy(a->stream);
     delete a;
@@ -1035,8 +735,8 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
     a->device = device;
     a->idx = idx;
     a->p = *params;
-    if (const char *g = getenv("SNAPGPU_GROUPED")) a->grouped = atoi(g) != 0;
     if (const char *t = getenv("SNAPGPU_TIMEOUT_S")) a->timeoutSec = atof(t);
+    if (const char *t = getenv("SNAPGPU_PHASES")) a->phases = atoi(t) != 0;
     auto fail = [&](const char *what, hipError_t e) {
         snapgpu::setError(std::string(what) + ": " + hipGetErrorString(e));
         snapgpu_aligner_free(a);
@@ -1047,6 +747,7 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
     if ((e = hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking)) != hipSuccess) return fail("stream", e);
     for (auto &ev : a->ev) if ((e = hipEventCreate(&ev)) != hipSuccess) return fail("event", e);
     if ((e = hipGetSymbolAddress((void **)&a->dDiag, HIP_SYMBOL(g_diag))) != hipSuccess) return fail("g_diag", e);
+    if ((e = hipGetSymbolAddress((void **)&a->dPhase, HIP_SYMBOL(g_phase))) != hipSuccess) return fail("g_phase", e);
     // index upload: genome with guards, tables, overflow, pieces
     const uint32_t nBases = idx->genome->nBases;
     size_t gbytes = kDevGuard + nBases + kDevGuard;
@@ -1060,24 +761,24 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
     }
     a->dGenome = a->dGenomeAlloc + kDevGuard;
     {
-        // 2-bit packed genome + spaced non-ACGT mask (16 bases per u32 word), covering
-        // genome positions [-kDevGuard, nBases + kDevGuard): the LV bitmaps of the
-        // grouped scorer are built from these with funnel shifts.
+        // genome bit planes {hi, lo, notACGT, 0}, 32 bases per uint4, covering genome
+        // positions [-kDevGuard, nBases + kDevGuard): the per-lane LV mismatch masks of
+        // align_kernel<128> are built from these with funnel shifts (align_score.h).
         const uint64_t span = (uint64_t)nBases + 2 * kDevGuard;
-        const uint64_t nw = (span + 15) / 16 + 8;
-        std::vector<uint32_t> code(nw, 0), msk(nw, 0);
+        const uint64_t nw = (span + 31) / 32 + 8;
+        std::vector<uint32_t> pl(nw * 4, 0);
         const char *b = idx->genome->bases();
         for (uint64_t i = 0; i < span; i++) {
-            int64_t p = (int64_t)i - (int64_t)kDevGuard;
-            char c = (p >= 0 && p < (int64_t)nBases) ? b[p] : 'n';
-            uint32_t v = packedCode(c);
-            code[i >> 4] |= (v & 3u) << (2 * (i & 15));
-            if (v > 3) msk[i >> 4] |= 1u << (2 * (i & 15));
+            const int64_t p = (int64_t)i - (int64_t)kDevGuard;
+            const char c = (p >= 0 && p < (int64_t)nBases) ? b[p] : 'n';
+            const uint32_t v = packedCode(c), bit = 1u << (i & 31);
+            uint32_t *w = &pl[(i >> 5) * 4];
+            if (v > 3) w[2] |= bit;
+            else { if (v & 2) w[0] |= bit; if (v & 1) w[1] |= bit; }
         }
-        if ((e = hipMalloc(&a->dGCode, nw * 4)) != hipSuccess) return fail("hipMalloc gcode", e);
-        if ((e = hipMalloc(&a->dGMask, nw * 4)) != hipSuccess) return fail("hipMalloc gmask", e);
-        hipMemcpy(a->dGCode, code.data(), nw * 4, hipMemcpyHostToDevice);
-        if ((e = hipMemcpy(a->dGMask, msk.data(), nw * 4, hipMemcpyHostToDevice)) != hipSuccess) return fail("gmask", e);
+        for (uint64_t i = span; i < nw * 32; i++) pl[(i >> 5) * 4 + 2] |= 1u << (i & 31);
+        if ((e = hipMalloc(&a->dGPlanes, nw * 16)) != hipSuccess) return fail("hipMalloc planes", e);
+        if ((e = hipMemcpy(a->dGPlanes, pl.data(), nw * 16, hipMemcpyHostToDevice)) != hipSuccess) return fail("planes", e);
     }
     if ((e = hipMalloc(&a->dSlots, idx->slots.size() * 4)) != hipSuccess) return fail("hipMalloc slots", e);
     if ((e = hipMemcpy(a->dSlots, idx->slots.data(), idx->slots.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return fail("slots", e);
@@ -1109,6 +810,11 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
     const uint64_t budget = 24ull << 30;   // HBM for arenas
     while (a->grid > 64 && (uint64_t)a->grid * a->arenaElems * sizeof(Elem) > budget) a->grid /= 2;
     if ((e = hipMalloc(&a->dArena, (uint64_t)a->grid * a->arenaElems * sizeof(Elem))) != hipSuccess) return fail("arena", e);
+    int perCU512 = 0;   // pass 2 (deferred reads) reuses the arenas of the first a->grid blocks
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU512, (const void *)align_kernel<512>, 64, 0);
+    if (perCU512 <= 0) perCU512 = 4;
+    a->grid512 = prop.multiProcessorCount * perCU512;
+    if (a->grid512 > a->grid) a->grid512 = a->grid;
     if ((e = hipDeviceSynchronize()) != hipSuccess) return fail("sync", e);
     return a;
 }
@@ -1131,6 +837,7 @@ snapgpu_device_reads_t *snapgpu_reads_upload(snapgpu_aligner_t *a, const snapgpu
     HIPCHKN(hipMalloc(&d->dOffsets, (r->n + 1) * 8));
     HIPCHKN(hipMalloc(&d->dLengths, (r->n + 1) * 4));
     HIPCHKN(hipMalloc(&d->dOut, (r->n + 1) * sizeof(snapgpu_result_t)));
+    HIPCHKN(hipMalloc(&d->dDefer, (r->n + 1) * sizeof(uint32_t)));
     HIPCHKN(hipMemsetAsync(d->dBases, 0, bytes, a->stream));
     HIPCHKN(hipMemsetAsync(d->dQuals, 0, bytes, a->stream));
     HIPCHKN(hipMemcpyAsync(d->dBases, r->bases, bytes - 64, hipMemcpyHostToDevice, a->stream));
@@ -1145,6 +852,7 @@ void snapgpu_device_reads_free(snapgpu_device_reads_t *d) {
     if (!d) return;
     hipSetDevice(d->device);
     hipFree(d->dBases); hipFree(d->dQuals); hipFree(d->dOffsets); hipFree(d->dLengths); hipFree(d->dOut);
+    hipFree(d->dDefer);
     delete d;
 }
 
@@ -1158,8 +866,8 @@ int snapgpu_align_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d) {
     const snapgpu_index_t *idx = a->idx;
     A.slots = a->dSlots; A.tableBase = a->dTableBase; A.tableSize = a->dTableSize; A.overflow = a->dOverflow;
     A.genome = a->dGenome; A.pieces = a->dPieces; A.nPieces = (int32_t)idx->genome->pieceOffsets.size();
-    A.gcode = a->dGCode; A.gmask = a->dGMask; A.hasIupac = idx->hasIupac ? 1u : 0u;
-    A.grouped = a->grouped;
+    A.gpl = a->dGPlanes; A.hasIupac = idx->hasIupac ? 1u : 0u;
+    A.phases = a->phases;
     A.nBases = idx->genome->nBases; A.seedLen = idx->seedLen; A.nTables = idx->nTables;
     A.padding = idx->genome->chromosomePadding;
     A.maxHits = a->p.maxHitsToConsider; A.maxK = a->p.maxK; A.maxReadSize = a->p.maxReadSize;
@@ -1169,16 +877,26 @@ int snapgpu_align_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d) {
     A.bases = d->dBases; A.quals = d->dQuals; A.offsets = d->dOffsets; A.lengths = d->dLengths;
     A.nReads = (uint32_t)d->n; A.out = d->dOut;
     A.counter = a->dCounter; A.arena = a->dArena; A.arenaElems = a->arenaElems;
+    // dCounter: [0] pass-1 work counter, [1] pass-2 work counter, [2] deferred-read count
+    A.deferList = d->dDefer; A.deferCount = a->dCounter + 2; A.readList = nullptr;
     int grid = a->grid;
     if ((uint64_t)grid > d->n) grid = (int)d->n;
     (void)hipGetLastError();   // clear any stale error of an unrelated earlier runtime call
     HIPCHK(hipMemsetAsync(a->dCounter, 0, 64, a->stream));
     HIPCHK(hipMemsetAsync(a->dDiag, 0, sizeof(uint32_t) * 4, a->stream));
     HIPCHK(hipEventRecord(a->ev[0], a->stream));
-    if (d->maxLen <= 128) hipLaunchKernelGGL(align_kernel<128>, dim3(grid), dim3(64), 0, a->stream, A);
-    else hipLaunchKernelGGL(align_kernel<512>, dim3(grid), dim3(64), 0, a->stream, A);
+    hipLaunchKernelGGL(align_kernel<128>, dim3(grid), dim3(64), 0, a->stream, A);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(a->ev[1], a->stream));
+    // pass 2: reads longer than 128 bases or needing the byte-compare LV
+    KArgs B = A;
+    B.counter = a->dCounter + 1;
+    B.readList = d->dDefer;
+    int grid2 = a->grid512;
+    if ((uint64_t)grid2 > d->n) grid2 = (int)d->n;
+    hipLaunchKernelGGL(align_kernel<512>, dim3(grid2), dim3(64), 0, a->stream, B);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(a->ev[2], a->stream));
     a->lastReads = d;
     a->pendingTiming = true;
     return SNAPGPU_OK;
@@ -1205,6 +923,11 @@ int snapgpu_synchronize(snapgpu_aligner_t *a) {
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, a->ev[0], a->ev[1]));
         a->timing.mainKernelMs = ms;
+        HIPCHK(hipEventElapsedTime(&ms, a->ev[1], a->ev[2]));
+        a->timing.spillKernelMs = ms;
+        uint32_t cnt[4];
+        HIPCHK(hipMemcpy(cnt, a->dCounter, sizeof(cnt), hipMemcpyDeviceToHost));
+        a->timing.nSpilled = cnt[2];
         a->pendingTiming = false;
         uint32_t diag[4];
         HIPCHK(hipMemcpy(diag, a->dDiag, sizeof(diag), hipMemcpyDeviceToHost));
@@ -1225,7 +948,7 @@ int snapgpu_results_download(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, sn
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(out, d->dOut, d->n * sizeof(snapgpu_result_t), hipMemcpyDeviceToHost, a->stream));
     HIPCHK(hipStreamSynchronize(a->stream));
-    // host MAPQ fix-ups (device log10 within 1e-6 of an integer boundary)
+    // host MAPQ fix-ups (ratio within 1e-9 of a threshold 10^(-q/10), mapq_dev)
     auto t0 = std::chrono::steady_clock::now();
     uint64_t fixed = 0;
     for (uint64_t i = 0; i < d->n; i++) {
@@ -1266,6 +989,14 @@ int snapgpu_last_timing(snapgpu_aligner_t *a, snapgpu_timing_t *t) {
 int snapgpu_aligner_get_stats(const snapgpu_aligner_t *a, snapgpu_aligner_stats_t *s) {
     if (!a || !s) return SNAPGPU_EINVAL;
     *s = a->stats;
+    return SNAPGPU_OK;
+}
+int snapgpu_phase_cycles(snapgpu_aligner_t *a, uint64_t *out16, int reset) {
+    if (!a || !out16) return SNAPGPU_EINVAL;
+    HIPCHK(hipSetDevice(a->device));
+    HIPCHK(hipStreamSynchronize(a->stream));
+    HIPCHK(hipMemcpy(out16, a->dPhase, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    if (reset) HIPCHK(hipMemset(a->dPhase, 0, 16 * sizeof(uint64_t)));
     return SNAPGPU_OK;
 }
 int snapgpu_aligner_max_k(const snapgpu_aligner_t *a) { return a ? (int)a->p.maxK : -1; }

@@ -272,6 +272,15 @@ class BaseAligner:
         lib().snapgpu_last_timing(self._h, C.byref(t))
         return {f: getattr(t, f) for f, _ in t._fields_}
 
+    PHASES = ("setup", "lookup", "insert", "score", "pop", "desc", "stage", "lv_fwd", "lv_rev", "apply",
+              "writeback", "out", "n_pass", "n_cand", "n_read")
+
+    def phase_cycles(self, reset=True):
+        """Diagnostic per-phase shader-cycle sums (needs SNAPGPU_PHASES=1 at construction)."""
+        buf = (C.c_uint64 * 16)()
+        _check(lib().snapgpu_phase_cycles(self._h, buf, int(reset)), "phase_cycles")
+        return {k: int(buf[i]) for i, k in enumerate(self.PHASES)}
+
     def stats(self):
         s = _ffi.AlignerStats()
         lib().snapgpu_aligner_get_stats(self._h, C.byref(s))

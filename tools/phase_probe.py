@@ -1,0 +1,34 @@
+#!/usr/bin/env python3
+"""Diagnostic: per-phase cycle breakdown of align_kernel on the bench workload.
+
+Run on the GPU box: SNAPGPU_PHASES=1 python tools/phase_probe.py [--reads N]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "snap-rnaseq_amd"))
+os.environ.setdefault("SNAPGPU_PHASES", "1")
+import snapgpu  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--reads", type=int, default=1_000_000)
+ap.add_argument("--genome-bases", type=int, default=46_709_983)
+args = ap.parse_args()
+g = snapgpu.Genome.synthetic(args.genome_bases, seed=2121, n_contigs=1, n_repeat_families=200)
+reads = snapgpu.Reads.synthetic(g, args.reads, seed=99)
+idx = snapgpu.GenomeIndex.build(g, 20, 16)
+al = snapgpu.BaseAligner(idx, device=0)
+dev = al.upload(reads)
+dev.run(); dev.synchronize()
+al.phase_cycles(reset=True)
+dev.run(); dev.synchronize()
+ph = al.phase_cycles(reset=True)
+ms = al.timing()["mainKernelMs"]
+tot = sum(ph[k] for k in ("setup", "lookup", "insert", "score", "out"))
+out = {"kernel_ms": ms, "reads": args.reads, "cycles_per_read": {k: ph[k] / args.reads for k in ph}}
+out["share_of_wave_time"] = {k: round(ph[k] / tot, 4) for k in ("setup", "lookup", "insert", "score", "pop", "desc",
+                                                                 "stage", "lv_fwd", "lv_rev", "apply", "writeback", "out")}
+print(json.dumps(out, indent=1))
