@@ -265,10 +265,9 @@ typedef struct snapgpu_aligner_stats {
 int snapgpu_aligner_get_stats(const snapgpu_aligner_t *a, snapgpu_aligner_stats_t *s);
 int snapgpu_aligner_max_k(const snapgpu_aligner_t *a);           /* getMaxK() */
 /* Diagnostic (no reference equivalent): with SNAPGPU_PHASES=1 in the environment at
- * snapgpu_aligner_create, the aligner kernel sums shader cycles per phase (setup,
- * lookup, insert, score, pop, desc, stage, lv-fwd, lv-rev, apply, writeback, out) and
- * counters (passes, candidates, reads) into out16[0..14]; reset != 0 zeroes them. */
-int snapgpu_phase_cycles(snapgpu_aligner_t *a, uint64_t *out16, int reset);
+ * snapgpu_aligner_create, align_kernel<128> sums shader cycles per phase and event
+ * counts into out32[0..31] (order: snapgpu.BaseAligner.PHASES); reset != 0 zeroes them. */
+int snapgpu_phase_cycles(snapgpu_aligner_t *a, uint64_t *out32, int reset);
 const char *snapgpu_aligner_name(const snapgpu_aligner_t *a);    /* getName() */
 
 /* -------------------------------------------------------- Landau-Vishkin */

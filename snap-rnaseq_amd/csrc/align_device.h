@@ -102,7 +102,7 @@ struct KArgs {
     uint32_t *deferList;         // pass 1 appends read indices here
     uint32_t *deferCount;        // pass 1: atomic append count; pass 2: number of reads
     const uint32_t *readList;    // pass 2: read indices (nullptr in pass 1)
-    uint32_t phases;             // diagnostic: accumulate per-phase shader cycles (SNAPGPU_PHASES=1)
+    unsigned long long *phaseBuf;   // diagnostic (SNAPGPU_PHASES=1): per-block [PH_SLOTS] cycle sums, else null
 };
 
 // ------------------------------------------------------------ wave helpers
@@ -191,8 +191,10 @@ struct GroupLds {
     uint32_t ecache[EB][ELEM_DWORDS];    // popped elements (authoritative while in the batch)
     uint32_t eidx[EB];
     uint16_t cand[CANDCAP];              // slot << 8 | bit
-    int16_t btA[4][32];                  // per-group backtrace scratch
-    int16_t btM[4][32];
+    int16_t pm[2][4][32];                // LV path per [direction][group][row]: matched-run length
+    int8_t pa[2][4][32];                 //   and action (0 X, 1 D, 2 I); probabilities in apply
+    int16_t pL0[2][4];                   //   exact prefix L[0][0]
+    int8_t plen[2][4];                   //   path length (0: exact match, prob = perfect[patternLen])
 };
 
 template <int MAXLEN>
@@ -217,7 +219,6 @@ struct Lds {
     int16_t btMatched[BYTE_PATH ? MAX_K + 1 : 1];
     uint16_t rows[MAX_K][WAVE];                     // LV rows: (L+2) | action<<12
     GroupLds grp[BYTE_PATH ? 0 : 1];                // scorer of align_kernel<128>
-    uint64_t ph[16];                                // diagnostic per-phase cycle sums (KArgs::phases)
 };
 
 // ------------------------------------------------------------ LV engine
@@ -454,15 +455,18 @@ __device__ __forceinline__ int next_piece_after(const KArgs &A, uint32_t loc) { 
 }
 
 // ------------------------------------------------------- phase diagnostics
-// With KArgs::phases set, each wave sums s_memtime deltas per phase in LDS and adds
-// them to g_phase at exit (snapgpu_phase_cycles).  Off: one SGPR test per site.
+// With KArgs::phaseBuf set, lane 0 of each wave adds s_memtime deltas per phase (and
+// event counts) to its block's slice with no-return atomics (snapgpu_phase_cycles).
+// Off: one SGPR test per site.
 enum : int { PH_SETUP = 0, PH_LOOKUP, PH_INSERT, PH_SCORE, PH_POP, PH_DESC, PH_STAGE, PH_LVF, PH_LVR, PH_APPLY,
-             PH_WB, PH_OUT, PH_NPASS, PH_NCAND, PH_NREAD, PH_N };
-__device__ unsigned long long g_phase[16];
+             PH_WB, PH_OUT, PH_NPASS, PH_NCAND, PH_NREAD, PH_NPASS16, PH_NPASS32, PH_NPASS64, PH_ROWSF, PH_ROWSR,
+             PH_NSCORECALL, PH_NFORCED, PH_NPOPPED, PH_NSUCC, PH_SLOTS = 32 };
 __device__ __forceinline__ uint64_t clk() { return __builtin_amdgcn_s_memtime(); }
-#define PH_T(A, v) const uint64_t v = (A).phases ? sgk::clk() : 0
-#define PH_ADD(A, S, i, v) do { if ((A).phases && sgk::lane_id() == 0) (S).ph[i] += sgk::clk() - (v); } while (0)
-#define PH_CNT(A, S, i, n) do { if ((A).phases && sgk::lane_id() == 0) (S).ph[i] += (n); } while (0)
+#define PH_T(A, v) const uint64_t v = (A).phaseBuf ? sgk::clk() : 0
+#define PH_ADD(A, S, i, v) do { if ((A).phaseBuf && sgk::lane_id() == 0) \
+    atomicAdd((A).phaseBuf + blockIdx.x * sgk::PH_SLOTS + (i), (unsigned long long)(sgk::clk() - (v))); } while (0)
+#define PH_CNT(A, S, i, n) do { if ((A).phaseBuf && sgk::lane_id() == 0) \
+    atomicAdd((A).phaseBuf + blockIdx.x * sgk::PH_SLOTS + (i), (unsigned long long)(n)); } while (0)
 
 // computeMAPQ (mapq.h:32-65) without log10: floor(-10*log10(x)) >= q  <=>  x <= 10^(-q/10).
 // A ratio within 1e-9 (relative) of a threshold is flagged and re-derived on the host

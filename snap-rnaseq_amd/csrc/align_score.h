@@ -30,25 +30,42 @@
 namespace sgk {
 
 // ------------------------------------------------------------ 128-bit masks
+// Bit m of a mask = mismatch at read position m.  The reverse LV scans the read
+// backwards, so it runs on the bit-reversed mask R[m'] = F[127 - m'] and both
+// directions only need "first set bit at or after m0" (positions >= 128 count as
+// set, which is "before position 0" for R).
 struct Mask128 { uint64_t lo, hi; };
 
-// first set position >= m0 (positions outside [0, 128) count as set)
-__device__ __forceinline__ int mk_first(const Mask128 &F, int m0) {
-    if (m0 >= 128 || m0 < 0) return m0;
-    const uint64_t a = m0 < 64 ? F.lo & (~0ull << m0) : 0ull;
-    const uint64_t b = m0 < 64 ? F.hi : F.hi & (~0ull << (m0 - 64));
-    return a ? __builtin_ctzll(a) : (b ? 64 + __builtin_ctzll(b) : 128);
+__device__ __forceinline__ Mask128 mk_reverse(const Mask128 &F) {
+    Mask128 R;
+    R.lo = ((uint64_t)__builtin_bitreverse32((uint32_t)F.hi) << 32) | __builtin_bitreverse32((uint32_t)(F.hi >> 32));
+    R.hi = ((uint64_t)__builtin_bitreverse32((uint32_t)F.lo) << 32) | __builtin_bitreverse32((uint32_t)(F.lo >> 32));
+    return R;
 }
-// last set position <= m0 (positions outside [0, 128) count as set)
-__device__ __forceinline__ int mk_last(const Mask128 &F, int m0) {
-    if (m0 < 0 || m0 >= 128) return m0;
-    const uint64_t b = m0 >= 64 ? F.hi & (~0ull >> (127 - m0)) : 0ull;
-    const uint64_t a = m0 >= 64 ? F.lo : F.lo & (~0ull >> (63 - m0));
-    return b ? 127 - __builtin_clzll(b) : (a ? 63 - __builtin_clzll(a) : -1);
+// v_ffbl_b32: index of the lowest set bit, 0xffffffff for 0
+__device__ __forceinline__ uint32_t ffbl(uint32_t x) {
+    uint32_t r;
+    asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+// first set position >= m0, m0 in [0, 128]; 128 if none.  Branch-free.
+__device__ __forceinline__ int mk_first(const Mask128 &F, int m0) {
+    const uint64_t S = ~0ull << (m0 & 63);
+    const bool low = m0 < 64;
+    const uint64_t a = F.lo & (low ? S : 0ull);
+    const uint64_t b = F.hi & (low ? ~0ull : S);
+    // OR-ing the word base keeps ffbl's 0xffffffff "none" sentinel
+    uint32_t r = ffbl((uint32_t)a);
+    const uint32_t p1 = ffbl((uint32_t)(a >> 32)) | 32u, p2 = ffbl((uint32_t)b) | 64u, p3 = ffbl((uint32_t)(b >> 32)) | 96u;
+    r = p1 < r ? p1 : r;
+    r = p2 < r ? p2 : r;
+    r = p3 < r ? p3 : r;
+    r = r < 128u ? r : 128u;
+    return m0 >= 128 ? m0 : (int)r;
 }
 __device__ __forceinline__ bool mk_bit(const Mask128 &F, int m) {
-    if (m < 0 || m >= 128) return true;
-    return ((m < 64 ? F.lo >> m : F.hi >> (m - 64)) & 1) != 0;
+    const uint64_t w = m < 64 ? F.lo : F.hi;
+    return m >= 128 || ((w >> (m & 63)) & 1) != 0;
 }
 
 // ------------------------------------------------------------ group shifts
@@ -73,104 +90,143 @@ __device__ __forceinline__ int from_upper(int v) {
 
 // ------------------------------------------------------------ LV per group
 // LandauVishkin<DIR>::computeEditDistance (LandauVishkin.h:211-455) for every active
-// group at once; the group's answer ends up in every lane of the group.
+// group at once, in "forward" coordinates: pattern index i is mask position q0 + i
+// (M = F for DIR = 1, M = R with q0 = 127 - p0 for DIR = -1).  Lane li holds
+// diagonal d = DIR * (li - c).  Returns the rows run; outE (group-uniform) is the
+// distance or -1.  A group that succeeds records its backtrace (LandauVishkin.h:
+// 376-431) in G.pa / G.pm / G.pL0 / G.plen[dx]; the match probability is formed
+// later, only for candidates the scorer applies (lv_prob).
 template <int DIR, int GS>
-__device__ __forceinline__ void lv_group(GroupLds &G, const Mask128 &F, bool gact, int p0, int patternLen,
-                                         int textLen, int k, int kmaxAll, const char *qual,
-                                         uint16_t (*rows)[WAVE], const DevTables *tab, int &outE, double &outP,
-                                         int &outNet) {
+__device__ __forceinline__ int lv_group(GroupLds &G, const Mask128 &M, bool gact, int q0, int patternLen,
+                                        int textLen, int k, int kmaxAll, uint16_t (*rows)[WAVE], int &outE) {
+    constexpr int dx = DIR > 0 ? 0 : 1;
     const int lane = lane_id();
     const int li = lane & (GS - 1), gi = lane / GS, c = GS / 2 - 1;
     const int d = DIR > 0 ? li - c : c - li;
     if (k > MAX_K - 1) k = MAX_K - 1;
-    outE = -1; outP = 1.0; outNet = 0;
+    outE = -1;
     bool done = !gact;
     const int end0 = patternLen < textLen ? patternLen : textLen;
-    const int fm = DIR > 0 ? mk_first(F, p0) - p0 : p0 - mk_last(F, p0);
+    const int fm = mk_first(M, q0) - q0;
     const int v0 = fm < end0 ? fm : end0;
-    const int L0 = shfl_idx(v0, gi * GS + c);            // exact prefix on diagonal 0
+    const int L0 = shfl_idx(v0, gi * GS + c);           // exact prefix on diagonal 0
     if (!done && L0 == end0) {                          // LandauVishkin.h:290-305
         const int result = patternLen > end0 ? patternLen - end0 : 0;
-        outP = tab->perfect[patternLen];
         outE = result > k ? -1 : result;
+        if (li == 0) { G.plen[dx][gi] = 0; G.pL0[dx][gi] = (int16_t)L0; }
         done = true;
     }
     int Lp = (li == c) ? L0 : -2;
     const int endd = patternLen < textLen - d ? patternLen : textLen - d;
+    int rowsRun = 0;
     for (int e = 1; e <= kmaxAll; e++) {
-        if (!done && e > k) done = true;                // limit reached: -1
+        done = done || e > k;                           // limit reached: -1
         if (ballot(!done) == 0) break;
+        rowsRun = e;
         const int lower = from_lower<GS>(Lp), upper = from_upper<GS>(Lp);
         const int left = DIR > 0 ? lower : upper;       // L[e-1][d-1]
         const int right = (DIR > 0 ? upper : lower) + 1;   // L[e-1][d+1] + 1
-        int best = Lp + 1, act = 0;                     // X, then D, then I if strictly greater
-        if (left > best) { best = left; act = 1; }
-        if (right > best) { best = right; act = 2; }
+        const int x1 = Lp + 1;
+        // X, then D if strictly greater, then I if strictly greater
+        const int bxd = left > x1 ? left : x1;
+        const int act = right > bxd ? 2 : (left > x1 ? 1 : 0);
+        const int best = right > bxd ? right : bxd;
         const bool active = !done && d <= e && d >= -e;
-        if (active) {
-            const int mpos = p0 + DIR * best;
-            if (best < endd) {                          // slide (LandauVishkin.h:325-354)
-                const int f = DIR > 0 ? mk_first(F, mpos) - p0 : p0 - mk_last(F, mpos);
-                best = f < endd ? f : endd;
-            } else if (!mk_bit(F, mpos)) {
-                best = endd;
-            }
-            rows[e][lane] = (uint16_t)((best + 2) | (act << 12));
-        }
-        const int Ln = active ? best : Lp;
+        // slide along the diagonal (LandauVishkin.h:325-354)
+        const int mpos = q0 + best;
+        const int f = mk_first(M, mpos < 128 ? mpos : 128) - q0;
+        const int slid = f < endd ? f : endd;
+        const int bnew = best < endd ? slid : (mk_bit(M, mpos) ? best : endd);
+        const int Ln = active ? bnew : Lp;
+        if (active) rows[e][lane] = (uint16_t)((bnew + 2) | (act << 12));
         const uint64_t hit = ballot(active && Ln == patternLen);
-        const uint64_t gm = GS == 64 ? hit : (hit >> (gi * GS)) & ((1ull << (GS & 63)) - 1);
-        if (gm != 0 && !done) {
-            // first diagonal in the order 0, 1, -1, 2, -2, ... (LandauVishkin.h:180-182)
-            int wd = 0;
-            for (int j = 0; j <= e; j++) {
-                const int lp = DIR > 0 ? c + j : c - j, ln = DIR > 0 ? c - j : c + j;
-                if ((gm >> lp) & 1) { wd = j; break; }
-                if (j > 0 && ((gm >> ln) & 1)) { wd = -j; break; }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            // backtrace (LandauVishkin.h:376-431), group-uniform
-            int curD = wd;
-            for (int ce = e; ce >= 1; ce--) {
-                const int ln = gi * GS + (DIR > 0 ? c + curD : c - curD);
-                const uint32_t cell = rows[ce][ln];
-                const int a = (int)(cell >> 12);
-                const int Lcur = (int)(cell & 0xfff) - 2;
-                const int src = a == 2 ? curD + 1 : (a == 1 ? curD - 1 : curD);
-                const int ls = gi * GS + (DIR > 0 ? c + src : c - src);
-                const int Lsrc = (ce - 1 == 0) ? (src == 0 ? L0 : -2) : ((int)(rows[ce - 1][ls] & 0xfff) - 2);
-                G.btA[gi][ce] = (int16_t)a;
-                G.btM[gi][ce] = (int16_t)(a == 1 ? Lcur - Lsrc : Lcur - Lsrc - 1);
-                curD = src;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            double p = 1.0;
-            int ce = 1, offset = L0, net = 0;
-            while (ce <= e) {
-                const int a = G.btA[gi][ce];
-                int cnt = 1;
-                while (ce + 1 <= e && G.btM[gi][ce] == 0 && G.btA[gi][ce + 1] == a) { cnt++; ce++; }
-                if (a == 2) { p *= tab->indel[cnt]; offset += cnt; net += cnt; }
-                else if (a == 1) { p *= tab->indel[cnt]; offset -= cnt; net -= cnt; }
-                else {
-                    for (int q = 0; q < cnt; q++) {
-                        int qi = offset < 0 ? 0 : offset;
-                        if (qi > patternLen - 1) qi = patternLen - 1;
-                        p *= tab->phred[(uint8_t)qual[p0 + DIR * qi]];
-                        offset++;
-                    }
+        if (hit) {
+            const uint64_t gm = GS == 64 ? hit : (hit >> (gi * GS)) & ((1ull << (GS & 63)) - 1);
+            if (gm != 0) {
+                // first diagonal in the order 0, 1, -1, 2, -2, ... (LandauVishkin.h:180-182)
+                int wd = 0;
+                for (int j = 0; j <= e; j++) {
+                    const int lp = DIR > 0 ? c + j : c - j, ln = DIR > 0 ? c - j : c + j;
+                    if ((gm >> lp) & 1) { wd = j; break; }
+                    if (j > 0 && ((gm >> ln) & 1)) { wd = -j; break; }
                 }
-                offset += G.btM[gi][ce];
-                ce++;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                int curD = wd;
+                for (int ce = e; ce >= 1; ce--) {
+                    const int ln = gi * GS + (DIR > 0 ? c + curD : c - curD);
+                    const uint32_t cell = rows[ce][ln];
+                    const int a = (int)(cell >> 12);
+                    const int Lcur = (int)(cell & 0xfff) - 2;
+                    const int src = a == 2 ? curD + 1 : (a == 1 ? curD - 1 : curD);
+                    const int ls = gi * GS + (DIR > 0 ? c + src : c - src);
+                    const int Lsrc = (ce - 1 == 0) ? (src == 0 ? L0 : -2) : ((int)(rows[ce - 1][ls] & 0xfff) - 2);
+                    if (li == 0) {
+                        G.pa[dx][gi][ce] = (int8_t)a;
+                        G.pm[dx][gi][ce] = (int16_t)(a == 1 ? Lcur - Lsrc : Lcur - Lsrc - 1);
+                    }
+                    curD = src;
+                }
+                if (li == 0) { G.plen[dx][gi] = (int8_t)e; G.pL0[dx][gi] = (int16_t)L0; }
+                outE = e;
+                done = true;
             }
-            p *= tab->perfect[patternLen - e];
-            outE = e; outP = p; outNet = net;
-            done = true;
         }
         Lp = Ln;
     }
+    return rowsRun;
+}
+
+// Match probabilities of the recorded forward and reverse LV paths of group g
+// (LandauVishkin.h:376-431), lane-parallel: lanes 0..30 take forward path steps
+// 1..31, lanes 32..62 reverse steps.  The reference merges runs of one action
+// (continuing while the matched run between them is empty); an indel run gives one
+// factor indel[cnt], X steps one phred factor each at offset L0 + sum of earlier
+// steps' (+-1 + matched).  Factors are fetched in parallel and multiplied in the
+// reference's order (x * 1.0 == x, so steps without a factor multiply by 1.0).
+__device__ __forceinline__ void lv_prob_pair(const DevTables *tab, const GroupLds &G, int g, int n, int s0, int t0,
+                                             const char *qual, double &p1, double &p2, int &net2) {
+    const int lane = lane_id();
+    const int dx = lane >> 5, j = (lane & 31) + 1;               // step j of direction dx
+    const int e = G.plen[dx][g];
+    const int L0 = G.pL0[dx][g];
+    const bool valid = j <= e;
+    const int a = valid ? G.pa[dx][g][j] : -1;
+    const int pmv = valid ? G.pm[dx][g][j] : 0;
+    const int an = j + 1 <= e ? G.pa[dx][g][j + 1] : -2;
+    const bool runEnd = valid && (j == e || pmv != 0 || an != a);
+    // offset before step j: inclusive scan of delta over the half-wave, minus own delta
+    const int delta = valid ? (a == 1 ? -1 : 1) + pmv : 0;
+    int incl = delta;
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+        const int v = shfl_idx(incl, lane - o < 0 ? lane : lane - o);
+        if ((lane & 31) >= o) incl += v;
+    }
+    const int offset = L0 + incl - delta;
+    // indel run length = distance to the previous run end of this direction
+    const uint64_t ends = ballot(runEnd);
+    const uint64_t below = (ends >> (lane & 32)) & ((1ull << (lane & 31)) - 1);
+    const int prevEnd = below ? 63 - __builtin_clzll(below) : -1;   // lane index within the half
+    const int cnt = (lane & 31) - prevEnd;
+    const int patternLen = dx ? s0 : n - t0;
+    const int p0 = dx ? s0 - 1 : t0;
+    int qi = offset < 0 ? 0 : offset;
+    if (qi > patternLen - 1) qi = patternLen - 1;
+    const int DIR = dx ? -1 : 1;
+    double f = 1.0;
+    if (valid && a == 0) f = tab->phred[(uint8_t)qual[p0 + DIR * qi]];
+    else if (runEnd) f = tab->indel[cnt];
+    const double perf = lane == 0 || lane == 32 ? tab->perfect[patternLen - e] : 1.0;
+    const int e1 = G.plen[0][g], e2 = G.plen[1][g];
+    double q = 1.0;
+    for (int i = 0; i < e1; i++) q *= readlaned(f, i);
+    p1 = q * readlaned(perf, 0);
+    q = 1.0;
+    for (int i = 0; i < e2; i++) q *= readlaned(f, 32 + i);
+    p2 = q * readlaned(perf, 32);
+    const uint64_t ins = ballot(valid && dx == 1 && a == 2), del = ballot(valid && dx == 1 && a == 1);
+    net2 = __popcll(ins) - __popcll(del);
 }
 
 // Terminal branch of score() (BaseAligner.cpp:1081-1103) + computeMAPQ (mapq.h:32-65).
@@ -194,22 +250,24 @@ struct PassLane {
     int glen;          // genome bytes available (BaseAligner.cpp:1161-1185)
     bool act;          // group holds a candidate whose genome window is servable
     int dir;
+    uint32_t cw;       // candidate list entry (slot << 8 | bit)
 };
 
 // One speculative pass over up to G = 64/GS candidates [i0, i0+m) of the list.
 template <int GS>
 __device__ __forceinline__ void lv_pass(const KArgs &A, Lds<128> &S, uint32_t i0, int m, int k, uint32_t n,
-                                        PassLane &P, int &e1, int &e2, double &p1, double &p2, int &net2) {
+                                        PassLane &P, int &e1, int &e2) {
     GroupLds &G = S.grp[0];
     const int lane = lane_id();
     const int gi = lane / GS, li = lane & (GS - 1), c = GS / 2 - 1;
     PH_T(A, tst);
     P.act = gi < m;
-    P.loc = 0; P.s = 0; P.glen = (int)n; P.dir = 0;
+    P.loc = 0; P.s = 0; P.glen = (int)n; P.dir = 0; P.cw = 0;
     if (P.act) {
         const uint32_t cw = G.cand[i0 + gi];
         const uint32_t sl = cw >> 8, bit = cw & 0xff;
         const uint32_t key = G.ecache[sl][6];
+        P.cw = cw;
         P.loc = (key >> 1) * ELEM + bit;
         P.dir = (int)(key & 1);
         P.s = (int)((G.ecache[sl][12 + bit / 2] >> (16 * (bit & 1))) & 0xffff);
@@ -257,19 +315,22 @@ __device__ __forceinline__ void lv_pass(const KArgs &A, Lds<128> &S, uint32_t i0
     }
     PH_ADD(A, S, PH_STAGE, tst);
     PH_T(A, tf);
-    const char *q = P.dir ? S.rcQ : S.fwdQ;
     const int t = P.s + (int)A.seedLen;
-    int n1;
-    lv_group<1, GS>(G, F, P.act, t, (int)n - t, P.glen - t, k, k, q, S.rows, A.tab, e1, p1, n1);
+    const int rf = lv_group<1, GS>(G, F, P.act, t, (int)n - t, P.glen - t, k, k, S.rows, e1);
     PH_ADD(A, S, PH_LVF, tf);
+    PH_CNT(A, S, PH_ROWSF, rf);
+    PH_CNT(A, S, GS == 16 ? PH_NPASS16 : (GS == 32 ? PH_NPASS32 : PH_NPASS64), 1);
     PH_T(A, tr);
     const int k2 = k - e1;
     const bool ract = P.act && e1 >= 0;
-    int v = ract ? k2 : -1;   // largest reverse limit over the groups that need a reverse pass
-    v = (int)(max_reduce64((uint64_t)(uint32_t)(v + 1)) ) - 1;
-    const int kmax2 = unii(v);
-    e2 = -1; p2 = 1.0; net2 = 0;
-    if (kmax2 >= 0) lv_group<-1, GS>(G, F, ract, P.s - 1, P.s, P.s + MAX_K, k2, kmax2, q, S.rows, A.tab, e2, p2, net2);
+    const int kmax2 = (int)max_reduce64((uint64_t)(uint32_t)(ract ? k2 + 1 : 0)) - 1;   // largest reverse limit
+    e2 = -1;
+    if (kmax2 >= 0) {
+        // reverse LV: pattern = read[s-1 .. 0], text = genome backwards from loc+s-1 (BaseAligner.cpp:1216-1220)
+        const Mask128 R = mk_reverse(F);
+        const int rr = lv_group<-1, GS>(G, R, ract, 127 - (P.s - 1), P.s, P.s + MAX_K, k2, kmax2, S.rows, e2);
+        PH_CNT(A, S, PH_ROWSR, rr);
+    }
     PH_ADD(A, S, PH_LVR, tr);
 }
 
@@ -286,6 +347,8 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<128> &S, Elem 
         }
     const uint32_t minLps = st.lps[0] < st.lps[1] ? st.lps[0] : st.lps[1];
     const bool forced = force || minLps > st.scoreLimit;
+    PH_CNT(A, S, PH_NSCORECALL, 1);
+    PH_CNT(A, S, PH_NFORCED, forced ? 1 : 0);
     for (uint32_t guard = 0;; guard++) {
         if (guard > (uint32_t)A.arenaElems) {   // every batch unlinks >= 1 element
             if (lane == 0) diag_report(DIAG_SCORE_LOOP, st.rid, S.nElems);
@@ -356,25 +419,7 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<128> &S, Elem 
         }
         PH_ADD(A, S, PH_POP, tpop);
         PH_CNT(A, S, PH_NCAND, nc);
-        // current element state (SGPRs), written back to ecache on slot change
-        int curSlot = -1;
-        bool slotSkip = false;
-        uint64_t cScored = 0;
-        double cProb = 0;
-        uint32_t cBest = 0, cBestLoc = 0, cKey = 0;
-        auto flush = [&]() {
-            if (curSlot >= 0) {
-                const uint64_t pb = (uint64_t)__double_as_longlong(cProb);
-                uint32_t *ec = G.ecache[curSlot];
-                if (lane == 2) ec[2] = (uint32_t)cScored;
-                else if (lane == 3) ec[3] = (uint32_t)(cScored >> 32);
-                else if (lane == 4) ec[4] = (uint32_t)pb;
-                else if (lane == 5) ec[5] = (uint32_t)(pb >> 32);
-                else if (lane == 8) ec[8] = cBest;
-                else if (lane == 9) ec[9] = cBestLoc;
-                wave_sync();
-            }
-        };
+        PH_CNT(A, S, PH_NPOPPED, nb);
         for (uint32_t i0 = 0; i0 < nc;) {
             if (overdue(st, 2)) return true;
             const int k = st.scoreLimit < (uint32_t)(MAX_K - 1) ? (int)st.scoreLimit : MAX_K - 1;
@@ -383,60 +428,90 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<128> &S, Elem 
             const int m = (int)(nc - i0) < Gn ? (int)(nc - i0) : Gn;
             PH_CNT(A, S, PH_NPASS, 1);
             PassLane P;
-            int e1, e2, net2;
-            double p1, p2;
-            if (GS == 16) lv_pass<16>(A, S, i0, m, k, n, P, e1, e2, p1, p2, net2);
-            else if (GS == 32) lv_pass<32>(A, S, i0, m, k, n, P, e1, e2, p1, p2, net2);
-            else lv_pass<64>(A, S, i0, m, k, n, P, e1, e2, p1, p2, net2);
+            int e1, e2;
+            if (GS == 16) lv_pass<16>(A, S, i0, m, k, n, P, e1, e2);
+            else if (GS == 32) lv_pass<32>(A, S, i0, m, k, n, P, e1, e2);
+            else lv_pass<64>(A, S, i0, m, k, n, P, e1, e2);
             PH_T(A, tapp);
-            // ---- apply in order with the limit in force at each candidate
-            for (int g = 0; g < m; g++) {
-                const int ln = g * GS;
-                const uint32_t cw = uni(G.cand[i0 + g]);
-                const int sl = (int)(cw >> 8);
-                const uint32_t bit = cw & 0xff;
-                if (sl != curSlot) {                  // element entered: lps check (BaseAligner.cpp:1129)
-                    flush();
-                    curSlot = sl;
-                    const uint32_t ev = lane < 12 ? G.ecache[sl][lane] : 0u;
-                    slotSkip = ((rl(ev, 11) >> 8) & 0xff) > st.scoreLimit;
-                    cScored = rl64(ev, 2);
-                    cProb = rld(ev, 4);
-                    cKey = rl(ev, 6);
-                    cBest = rl(ev, 8);
-                    cBestLoc = rl(ev, 9);
-                }
-                if (slotSkip) continue;
-                const int r1 = readlane(e1, ln), r2 = readlane(e2, ln);
-                const bool ok = readlane(P.act ? 1 : 0, ln) != 0;
+            // ---- apply in order with the limit in force at each candidate.  Group
+            // leaders (lane g*GS) hold candidate g.  A failure only sets its scored bit
+            // and, for an element's first scored candidate, bestLoc/bestScore/prob
+            // (BaseAligner.cpp:1253-1265 with score -1: nothing else changes), so the
+            // failures before the next success are applied together, lane-parallel.
+            const int gq = lane / GS;
+            const bool leader = (lane & (GS - 1)) == 0 && gq < m;
+            const uint32_t sl = P.cw >> 8, bit = P.cw & 0xff;
+            const uint32_t ew11 = leader ? G.ecache[sl][11] : 0u;
+            for (int g0 = 0; g0 < m;) {
                 const int kNow = (int)(st.scoreLimit < (uint32_t)(MAX_K - 1) ? st.scoreLimit : MAX_K - 1);
-                uint32_t sc = FAIL_SCORE;
-                double prob = 0;
-                const uint32_t dir = cKey & 1;
-                const uint32_t ebase = (cKey >> 1) * ELEM;
-                uint32_t loc = ebase + bit;
-                const uint32_t elemLoc = loc;
-                if (ok && r1 >= 0 && r1 <= kNow) {
-                    // the reverse call runs with limit scoreLimit - score1 (BaseAligner.cpp:1216-1220)
-                    const int lim2 = (int)st.scoreLimit - r1 > MAX_K - 1 ? MAX_K - 1 : (int)st.scoreLimit - r1;
-                    if (r2 >= 0 && r2 <= lim2) {
-                        sc = (uint32_t)(r1 + r2);
-                        const double q1 = readlaned(p1, ln), q2 = readlaned(p2, ln);
-                        prob = q1 * q2 * tab->seedProb;
-                        loc += (uint32_t)readlane(net2, ln);
+                const bool skip = ((ew11 >> 8) & 0xff) > st.scoreLimit;   // element lps (BaseAligner.cpp:1129)
+                const int lim2 = (int)st.scoreLimit - e1 > MAX_K - 1 ? MAX_K - 1 : (int)st.scoreLimit - e1;
+                const bool succ = leader && !skip && P.act && e1 >= 0 && e1 <= kNow && e2 >= 0 && e2 <= lim2;
+                const uint64_t sm = ballot(succ && gq >= g0);
+                const int gs = sm ? (int)__builtin_ctzll(sm) / GS : m;
+                const bool fail = leader && !skip && gq >= g0 && gq < gs;
+                const uint64_t fm = ballot(fail);
+                if (fm) {
+                    // per element: OR of the failing bits; the first failing lane of the element writes
+                    uint64_t acc = 0;
+                    bool first = true;
+#pragma unroll
+                    for (int jg = 0; jg < 4; jg++) {
+                        const int lj = jg * GS;
+                        if (lj < WAVE && ((fm >> (lj & 63)) & 1)) {
+                            const uint32_t slj = readlaneu(sl, lj & 63), bj = readlaneu(bit, lj & 63);
+                            if (fail && slj == sl) {
+                                acc |= 1ull << bj;
+                                if (jg < gq) first = false;
+                            }
+                        }
                     }
+                    if (fail && first) {
+                        uint32_t *ec = G.ecache[sl];
+                        const uint64_t old = ((uint64_t)ec[3] << 32) | ec[2];
+                        const uint64_t nw = old | acc;
+                        ec[2] = (uint32_t)nw;
+                        ec[3] = (uint32_t)(nw >> 32);
+                        if (old == 0) {   // first scored candidate of the element: score -1 recorded
+                            ec[9] = (ec[6] >> 1) * ELEM + bit;
+                            ec[8] = FAIL_SCORE;
+                            ec[4] = 0u;
+                            ec[5] = 0u;
+                        }
+                    }
+                    st.nScored += (uint32_t)__popcll(fm);
+                    wave_sync();
                 }
-                // candidate bookkeeping (BaseAligner.cpp:1253-1384)
-                const uint64_t cb = 1ull << bit;
-                bool anyNearby = cScored != 0;
-                cScored |= cb;
+                if (gs >= m) break;
+                // ---- the success at group gs: full bookkeeping (BaseAligner.cpp:1227-1384)
+                const int ln = gs * GS;
+                const uint32_t csl = readlaneu(sl, ln), cbit = readlaneu(bit, ln);
+                const int r1 = readlane(e1, ln), r2 = readlane(e2, ln);
+                const uint32_t ev = lane < 12 ? G.ecache[csl][lane] : 0u;
+                uint64_t cScored = rl64(ev, 2);
+                const double cProb = rld(ev, 4);
+                const uint32_t cKey = rl(ev, 6), cBest = rl(ev, 8);
+                const uint32_t sc = (uint32_t)(r1 + r2);
+                PH_CNT(A, S, PH_NSUCC, 1);
+                const int s0 = readlane(P.s, ln), t0 = s0 + (int)A.seedLen;
+                const uint32_t dir = cKey & 1;
+                double q1, q2;
+                int net2;
+                lv_prob_pair(tab, G, gs, (int)n, s0, t0, dir ? S.rcQ : S.fwdQ, q1, q2, net2);
+                const double prob = q1 * q2 * tab->seedProb;
+                const uint32_t ebase = (cKey >> 1) * ELEM;
+                const uint32_t elemLoc = ebase + cbit;
+                const uint32_t loc = elemLoc + (uint32_t)net2;
+                const bool anyNearby0 = cScored != 0;
+                cScored |= 1ull << cbit;
                 st.nScored++;
-                if (anyNearby) {
-                    if (cBest < sc || (cBest == sc && prob <= cProb)) continue;
-                }
-                cBestLoc = loc;   // bestScoreGenomeLocation
+                g0 = gs + 1;
+                const bool passA = !(anyNearby0 && (cBest < sc || (cBest == sc && prob <= cProb)));
+                bool take = passA;
                 uint32_t nb2 = NONE;
-                if (sc != FAIL_SCORE) {
+                int cs = -1;
+                uint32_t nv = 0;
+                if (take) {
                     const uint32_t nl = elemLoc + (2 * (elemLoc % ELEM / (ELEM / 2)) - 1) * (ELEM / 2);
                     const uint32_t nkey = ((nl / ELEM) << 1) | dir;
                     nb2 = uni(chain_find(S.head, ar, nkey, (uint32_t)A.arenaElems));
@@ -444,8 +519,7 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<128> &S, Elem 
                 if (nb2 != NONE) {
                     // the nearby element may be in this batch: its cache is authoritative
                     const uint64_t inb = ballot((uint32_t)lane < nb && G.eidx[lane < EB ? lane : 0] == nb2);
-                    const int cs = inb ? (int)__builtin_ctzll(inb) : -1;
-                    uint32_t nv;
+                    cs = inb ? (int)__builtin_ctzll(inb) : -1;
                     if (cs >= 0) nv = lane < 12 ? G.ecache[cs][lane] : 0u;
                     else nv = lane < 12 ? ((const uint32_t *)(ar + nb2))[lane] : 0u;
                     if (rl64(nv, 2) == 0) nb2 = NONE;   // nearby element not scored yet
@@ -458,18 +532,32 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<128> &S, Elem 
                     if (nb2 != NONE) {
                         const uint32_t nbs = rl(nv, 8);
                         const double np = rld(nv, 4);
-                        if (nbs < sc || (nbs == sc && np >= prob)) continue;
-                        anyNearby = true;
-                        st.pAll = st.pAll - np > 0.0 ? st.pAll - np : 0.0;
-                        if (cs >= 0) { if (lane == 4 || lane == 5) G.ecache[cs][lane] = 0u; }
-                        else if (lane == 4 || lane == 5) ((uint32_t *)(ar + nb2))[lane] = 0u;
-                        wave_sync();
+                        if (nbs < sc || (nbs == sc && np >= prob)) take = false;
+                        else {
+                            st.pAll = st.pAll - np > 0.0 ? st.pAll - np : 0.0;
+                            if (cs >= 0) { if (lane == 4 || lane == 5) G.ecache[cs][lane] = 0u; }
+                            else if (lane == 4 || lane == 5) ((uint32_t *)(ar + nb2))[lane] = 0u;
+                        }
                     }
                 }
+                // write the element back (scored always; the rest only when taken)
+                {
+                    const uint64_t pb = (uint64_t)__double_as_longlong(prob);
+                    uint32_t *ec = G.ecache[csl];
+                    if (lane == 2) ec[2] = (uint32_t)cScored;
+                    else if (lane == 3) ec[3] = (uint32_t)(cScored >> 32);
+                    // bestScoreGenomeLocation is set once the candidate passed the first check (:1266-1268)
+                    if (lane == 9 && passA) ec[9] = loc;
+                    if (take) {
+                        if (lane == 4) ec[4] = (uint32_t)pb;
+                        else if (lane == 5) ec[5] = (uint32_t)(pb >> 32);
+                        else if (lane == 8) ec[8] = sc;
+                    }
+                    wave_sync();
+                }
+                if (!take) continue;
                 st.pAll = st.pAll - cProb > 0.0 ? st.pAll - cProb : 0.0;
                 st.pAll += prob;
-                cProb = prob;
-                cBest = sc;
                 if (st.bestScore > sc || (st.bestScore == sc && prob > st.pBest)) {
                     st.bestScore = sc;
                     st.pBest = prob;
@@ -488,7 +576,6 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<128> &S, Elem 
             PH_ADD(A, S, PH_APPLY, tapp);
             i0 += (uint32_t)m;
         }
-        flush();
         PH_T(A, twb);
         // ---- write the batch back (scored, prob, bestScore, bestLoc, allScored = 1)
         for (uint32_t idx = lane; idx < nb * 8; idx += WAVE) {

@@ -523,7 +523,6 @@ __global__ __launch_bounds__(64) void align_kernel(KArgs A) {
     __shared__ Lds<MAXLEN> S;
     Elem *ar = A.arena + (uint64_t)blockIdx.x * A.arenaElems;
     const int lane = lane_id();
-    if (A.phases && lane < 16) S.ph[lane] = 0;
     const uint32_t total = A.readList ? uni(*A.deferCount) : A.nReads;
     for (;;) {
         uint32_t i = 0;
@@ -534,7 +533,6 @@ __global__ __launch_bounds__(64) void align_kernel(KArgs A) {
         if (__hip_atomic_load(&g_diag[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;   // watchdog: drain
         align_one<MAXLEN>(A, S, ar, r);
     }
-    if (A.phases && lane < 16) atomicAdd(&g_phase[lane], (unsigned long long)S.ph[lane]);
 }
 
 // LV parity kernel: one wave per task; the task's "read" and virtual genome are
@@ -681,8 +679,7 @@ struct snapgpu_aligner {
     snapgpu_device_reads_t *lastReads = nullptr;
     bool pendingTiming = false;
     uint32_t *dDiag = nullptr;    // g_diag (watchdog record)
-    unsigned long long *dPhase = nullptr;   // g_phase (SNAPGPU_PHASES=1 diagnostics)
-    uint32_t phases = 0;
+    unsigned long long *dPhase = nullptr;   // [grid][PH_SLOTS] (SNAPGPU_PHASES=1 diagnostics)
     double timeoutSec = 0;        // SNAPGPU_TIMEOUT_S
 };
 
@@ -715,7 +712,7 @@ void snapgpu_aligner_free(snapgpu_aligner_t *a) {
     hipSetDevice(a->device);
     hipFree(a->dSlots); hipFree(a->dOverflow); hipFree(a->dPieces); hipFree(a->dCounter);
     hipFree(a->dTableBase); hipFree(a->dTableSize); hipFree(a->dGenomeAlloc); hipFree(a->dTab); hipFree(a->dArena);
-    hipFree(a->dGPlanes);
+    hipFree(a->dGPlanes); hipFree(a->dPhase);
     for (auto &e : a->ev) if (e) hipEventDestroy(e);
     if (a->stream) hipStreamDestroy(a->stream);
     delete a;
@@ -736,7 +733,6 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
     a->idx = idx;
     a->p = *params;
     if (const char *t = getenv("SNAPGPU_TIMEOUT_S")) a->timeoutSec = atof(t);
-    if (const char *t = getenv("SNAPGPU_PHASES")) a->phases = atoi(t) != 0;
     auto fail = [&](const char *what, hipError_t e) {
         snapgpu::setError(std::string(what) + ": " + hipGetErrorString(e));
         snapgpu_aligner_free(a);
@@ -747,7 +743,6 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
     if ((e = hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking)) != hipSuccess) return fail("stream", e);
     for (auto &ev : a->ev) if ((e = hipEventCreate(&ev)) != hipSuccess) return fail("event", e);
     if ((e = hipGetSymbolAddress((void **)&a->dDiag, HIP_SYMBOL(g_diag))) != hipSuccess) return fail("g_diag", e);
-    if ((e = hipGetSymbolAddress((void **)&a->dPhase, HIP_SYMBOL(g_phase))) != hipSuccess) return fail("g_phase", e);
     // index upload: genome with guards, tables, overflow, pieces
     const uint32_t nBases = idx->genome->nBases;
     size_t gbytes = kDevGuard + nBases + kDevGuard;
@@ -815,6 +810,11 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
     if (perCU512 <= 0) perCU512 = 4;
     a->grid512 = prop.multiProcessorCount * perCU512;
     if (a->grid512 > a->grid) a->grid512 = a->grid;
+    if (const char *t = getenv("SNAPGPU_PHASES"); t && atoi(t)) {
+        const size_t pb = (size_t)a->grid * PH_SLOTS * sizeof(unsigned long long);
+        if ((e = hipMalloc(&a->dPhase, pb)) != hipSuccess) return fail("phase buffer", e);
+        hipMemset(a->dPhase, 0, pb);
+    }
     if ((e = hipDeviceSynchronize()) != hipSuccess) return fail("sync", e);
     return a;
 }
@@ -867,7 +867,7 @@ int snapgpu_align_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d) {
     A.slots = a->dSlots; A.tableBase = a->dTableBase; A.tableSize = a->dTableSize; A.overflow = a->dOverflow;
     A.genome = a->dGenome; A.pieces = a->dPieces; A.nPieces = (int32_t)idx->genome->pieceOffsets.size();
     A.gpl = a->dGPlanes; A.hasIupac = idx->hasIupac ? 1u : 0u;
-    A.phases = a->phases;
+    A.phaseBuf = a->dPhase;
     A.nBases = idx->genome->nBases; A.seedLen = idx->seedLen; A.nTables = idx->nTables;
     A.padding = idx->genome->chromosomePadding;
     A.maxHits = a->p.maxHitsToConsider; A.maxK = a->p.maxK; A.maxReadSize = a->p.maxReadSize;
@@ -991,12 +991,16 @@ int snapgpu_aligner_get_stats(const snapgpu_aligner_t *a, snapgpu_aligner_stats_
     *s = a->stats;
     return SNAPGPU_OK;
 }
-int snapgpu_phase_cycles(snapgpu_aligner_t *a, uint64_t *out16, int reset) {
-    if (!a || !out16) return SNAPGPU_EINVAL;
+int snapgpu_phase_cycles(snapgpu_aligner_t *a, uint64_t *out, int reset) {
+    if (!a || !out) return SNAPGPU_EINVAL;
+    memset(out, 0, PH_SLOTS * sizeof(uint64_t));
+    if (!a->dPhase) { snapgpu::setError("phase diagnostics off (set SNAPGPU_PHASES=1 before aligner_create)"); return SNAPGPU_EINVAL; }
     HIPCHK(hipSetDevice(a->device));
     HIPCHK(hipStreamSynchronize(a->stream));
-    HIPCHK(hipMemcpy(out16, a->dPhase, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
-    if (reset) HIPCHK(hipMemset(a->dPhase, 0, 16 * sizeof(uint64_t)));
+    std::vector<uint64_t> buf((size_t)a->grid * PH_SLOTS);
+    HIPCHK(hipMemcpy(buf.data(), a->dPhase, buf.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < buf.size(); i++) out[i % PH_SLOTS] += buf[i];
+    if (reset) HIPCHK(hipMemset(a->dPhase, 0, buf.size() * sizeof(uint64_t)));
     return SNAPGPU_OK;
 }
 int snapgpu_aligner_max_k(const snapgpu_aligner_t *a) { return a ? (int)a->p.maxK : -1; }
