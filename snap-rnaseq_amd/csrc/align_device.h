@@ -184,6 +184,7 @@ __device__ __forceinline__ uint32_t complement_of(uint32_t c) {   // BaseAligner
 constexpr int64_t PACK_GUARD = 1024;     // bit-plane word 0 = genome position -1024
 constexpr int EB = 8;                    // elements popped per batch (forced mode)
 constexpr int CANDCAP = EB * ELEM;       // candidate list capacity
+constexpr uint32_t ORDCAP = 512;         // forced-mode pop order (u16, overlays Lds::btMask)
 
 // Scorer state of align_kernel<128> (align_score.h).
 struct GroupLds {
@@ -213,7 +214,7 @@ struct Lds {
     uint32_t scrLoc[WAVE];                          // batch scratch: hit location per lane
     uint32_t nElems;
     uint32_t pad_[3];
-    uint32_t sk[SKCAP];                             // selection keys of elements < SKCAP
+    alignas(16) uint32_t sk[SKCAP];                 // selection keys of elements < SKCAP
     uint64_t seedUsed[NB + 1];                      // BaseAligner::seedUsed bit vector
     int16_t btAct[BYTE_PATH ? MAX_K + 1 : 1];       // LV backtrace scratch (byte path)
     int16_t btMatched[BYTE_PATH ? MAX_K + 1 : 1];
@@ -460,7 +461,7 @@ __device__ __forceinline__ int next_piece_after(const KArgs &A, uint32_t loc) { 
 // Off: one SGPR test per site.
 enum : int { PH_SETUP = 0, PH_LOOKUP, PH_INSERT, PH_SCORE, PH_POP, PH_DESC, PH_STAGE, PH_LVF, PH_LVR, PH_APPLY,
              PH_WB, PH_OUT, PH_NPASS, PH_NCAND, PH_NREAD, PH_NPASS16, PH_NPASS32, PH_NPASS64, PH_ROWSF, PH_ROWSR,
-             PH_NSCORECALL, PH_NFORCED, PH_NPOPPED, PH_NSUCC, PH_SLOTS = 32 };
+             PH_NSCORECALL, PH_NFORCED, PH_NPOPPED, PH_NSUCC, PH_PASSLOOP, PH_SEL, PH_FETCH, PH_SEEDLOOP, PH_SLOTS = 32 };
 __device__ __forceinline__ uint64_t clk() { return __builtin_amdgcn_s_memtime(); }
 #define PH_T(A, v) const uint64_t v = (A).phaseBuf ? sgk::clk() : 0
 #define PH_ADD(A, S, i, v) do { if ((A).phaseBuf && sgk::lane_id() == 0) \
@@ -517,12 +518,16 @@ struct ReadState {
     uint32_t nLookups, nScored, nHitsIgnored, nProbes, nHitWords, nOvf, nElems;
     uint32_t rid;                // read index (watchdog reports)
     uint32_t abort;              // watchdog tripped: finish the read now
+    uint32_t tick;               // overdue(): calls left until the next clock read
     uint64_t t0;                 // s_memrealtime at read start
 };
 
-// time watchdog: true (once reported) when the read has overrun its deadline
+// time watchdog: true (once reported) when the read has overrun its deadline.  The
+// clock (an SMEM round trip) is read on every 32nd call only.
 __device__ __forceinline__ bool overdue(ReadState &st, uint32_t site) {
     if (st.abort) return true;
+    if (--st.tick != 0) return false;
+    st.tick = 32;
     if (__builtin_amdgcn_s_memrealtime() - st.t0 < READ_DEADLINE_TICKS) return false;
     if (lane_id() == 0) diag_report(DIAG_OVERDUE + site, st.rid, (uint32_t)((__builtin_amdgcn_s_memrealtime() - st.t0) >> 10));
     st.abort = 1;

@@ -349,6 +349,11 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<128> &S, Elem 
     const bool forced = force || minLps > st.scoreLimit;
     PH_CNT(A, S, PH_NSCORECALL, 1);
     PH_CNT(A, S, PH_NFORCED, forced ? 1 : 0);
+    // Forced mode pops every linked element in descending sort-key order and the read
+    // ends with it, so the order is computed once (ranks, ORDCAP at a time) and the
+    // elements are not unlinked one by one.
+    uint16_t *order = reinterpret_cast<uint16_t *>(S.btMask);   // insertion scratch is idle now
+    uint32_t fDone = 0, fAvail = 0, ordBase = 0;
     for (uint32_t guard = 0;; guard++) {
         if (guard > (uint32_t)A.arenaElems) {   // every batch unlinks >= 1 element
             if (lane == 0) diag_report(DIAG_SCORE_LOOP, st.rid, S.nElems);
@@ -358,23 +363,52 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<128> &S, Elem 
         PH_T(A, tpop);
         // ---- pop in weight-list order (head of the highest list first); LDS only
         uint32_t nb = 0;
-        while (nb < (uint32_t)EB) {
+        if (!forced) {
             const uint64_t sel = max_reduce64(S.laneMax[lane]);
-            if (sel == 0) break;
-            const uint32_t e = (uint32_t)sel;
-            sk_set(S, ar, e, 0);                       // unlink (BaseAligner.cpp:1391-1394)
+            if (sel != 0) {
+                const uint32_t e = (uint32_t)sel;
+                sk_set(S, ar, e, 0);                       // unlink (BaseAligner.cpp:1391-1394)
+                wave_sync();
+                if ((int)(e % WAVE) == lane) recompute_lane_max(S, ar, lane);
+                if (lane == 0) G.eidx[0] = e;
+                nb = 1;
+                wave_sync();
+            }
+        } else {
+            if (fDone == fAvail) {
+                // rank[e] = number of linked elements with a larger key (keys are unique)
+                ordBase = fDone;
+                const uint32_t nE = S.nElems;
+                uint32_t inRange = 0;
+                for (uint32_t e0 = 0; e0 < nE; e0 += WAVE) {
+                    const uint32_t e = e0 + lane;
+                    const uint32_t ke = e < nE ? sk_get(S, ar, e) : 0u;
+                    uint32_t rank = 0;
+                    uint32_t f = 0;
+                    for (; f + 4 <= nE && f + 4 <= SKCAP; f += 4) {
+                        const uint4 k4 = *reinterpret_cast<const uint4 *>(&S.sk[f]);
+                        rank += (k4.x > ke) + (k4.y > ke) + (k4.z > ke) + (k4.w > ke);
+                    }
+                    for (; f < nE; f++) rank += sk_get(S, ar, f) > ke;
+                    const bool in = ke != 0 && rank >= ordBase && rank < ordBase + ORDCAP;
+                    if (in) order[rank - ordBase] = (uint16_t)e;
+                    inRange += (uint32_t)__popcll(ballot(in));
+                }
+                fAvail = ordBase + inRange;
+                wave_sync();
+            }
+            nb = fAvail - fDone < (uint32_t)EB ? fAvail - fDone : (uint32_t)EB;
+            if ((uint32_t)lane < nb) G.eidx[lane] = order[fDone - ordBase + lane];
+            fDone += nb;
             wave_sync();
-            if ((int)(e % WAVE) == lane) recompute_lane_max(S, ar, lane);
-            if (lane == 0) G.eidx[nb] = e;
-            nb++;
-            wave_sync();
-            if (!forced) break;
         }
         if (nb == 0) {
             PH_ADD(A, S, PH_POP, tpop);
             if (forced) { finalize_read(A, st, result, flags); return true; }
             return false;
         }
+        PH_ADD(A, S, PH_SEL, tpop);
+        PH_T(A, tfe);
         // ---- fetch the batch from the arena in one round trip
         {
             constexpr int NLD = (EB * ELEM_DWORDS + WAVE - 1) / WAVE;
@@ -392,6 +426,7 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<128> &S, Elem 
             }
             wave_sync();
         }
+        PH_ADD(A, S, PH_FETCH, tfe);
         // ---- candidate list: elements in pop order, ascending bit; lane sl owns element sl
         uint32_t nc;
         {
@@ -420,6 +455,9 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<128> &S, Elem 
         PH_ADD(A, S, PH_POP, tpop);
         PH_CNT(A, S, PH_NCAND, nc);
         PH_CNT(A, S, PH_NPOPPED, nb);
+        PH_T(A, tpl);
+        uint32_t lastSlot = NONE;   // element of the last candidate reached, and its lps decision
+        bool lastSkip = false;
         for (uint32_t i0 = 0; i0 < nc;) {
             if (overdue(st, 2)) return true;
             const int k = st.scoreLimit < (uint32_t)(MAX_K - 1) ? (int)st.scoreLimit : MAX_K - 1;
@@ -444,7 +482,9 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<128> &S, Elem 
             const uint32_t ew11 = leader ? G.ecache[sl][11] : 0u;
             for (int g0 = 0; g0 < m;) {
                 const int kNow = (int)(st.scoreLimit < (uint32_t)(MAX_K - 1) ? st.scoreLimit : MAX_K - 1);
-                const bool skip = ((ew11 >> 8) & 0xff) > st.scoreLimit;   // element lps (BaseAligner.cpp:1129)
+                // element lps test, made once when the element's first candidate is reached
+                // (BaseAligner.cpp:1129); candidates of one element are contiguous
+                const bool skip = sl == lastSlot ? lastSkip : ((ew11 >> 8) & 0xff) > st.scoreLimit;
                 const int lim2 = (int)st.scoreLimit - e1 > MAX_K - 1 ? MAX_K - 1 : (int)st.scoreLimit - e1;
                 const bool succ = leader && !skip && P.act && e1 >= 0 && e1 <= kNow && e2 >= 0 && e2 <= lim2;
                 const uint64_t sm = ballot(succ && gq >= g0);
@@ -482,7 +522,13 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<128> &S, Elem 
                     st.nScored += (uint32_t)__popcll(fm);
                     wave_sync();
                 }
-                if (gs >= m) break;
+                if (gs >= m) {
+                    lastSlot = readlaneu(sl, (m - 1) * GS);
+                    lastSkip = readlane(skip ? 1 : 0, (m - 1) * GS) != 0;
+                    break;
+                }
+                lastSlot = readlaneu(sl, gs * GS);
+                lastSkip = false;
                 // ---- the success at group gs: full bookkeeping (BaseAligner.cpp:1227-1384)
                 const int ln = gs * GS;
                 const uint32_t csl = readlaneu(sl, ln), cbit = readlaneu(bit, ln);
@@ -576,6 +622,7 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<128> &S, Elem 
             PH_ADD(A, S, PH_APPLY, tapp);
             i0 += (uint32_t)m;
         }
+        PH_ADD(A, S, PH_PASSLOOP, tpl);
         PH_T(A, twb);
         // ---- write the batch back (scored, prob, bestScore, bestLoc, allScored = 1)
         for (uint32_t idx = lane; idx < nb * 8; idx += WAVE) {

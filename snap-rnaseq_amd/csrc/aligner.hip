@@ -307,6 +307,7 @@ __device__ void align_one(const KArgs &A, Lds<MAXLEN> &S, Elem *ar, uint32_t r) 
     st.rid = r;
     st.abort = 0;
     st.t0 = __builtin_amdgcn_s_memrealtime();
+    st.tick = 32;
     st.nSeedsApplied[0] = st.nSeedsApplied[1] = 0;
     uint32_t flags = 0;
     int result = SNAPGPU_NOT_FOUND;
@@ -384,6 +385,7 @@ __device__ void align_one(const KArgs &A, Lds<MAXLEN> &S, Elem *ar, uint32_t r) 
         // One call site for the scorer (it is large): `force` marks the final scoring
         // pass after the seed loop ends (BaseAligner.cpp:707-723, 879-891).
         const uint32_t seedGuard = (nPossible + 2) * (seedLen + 2) + maxSeeds;
+        PH_T(A, tsl);
         for (uint32_t guard = 0;; guard++) {
             bool force = st.nSeedsApplied[0] + st.nSeedsApplied[1] >= maxSeeds;
             if (guard > seedGuard) {   // each pass consumes a seed position or a wrap
@@ -490,6 +492,7 @@ __device__ void align_one(const KArgs &A, Lds<MAXLEN> &S, Elem *ar, uint32_t r) 
             if (fin || force) break;
             if (overdue(st, 8)) break;
         }
+        PH_ADD(A, S, PH_SEEDLOOP, tsl);
     }
     PH_T(A, tout);
     if (lane == 0) {

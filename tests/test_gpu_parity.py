@@ -106,6 +106,10 @@ PARAM_SETS = [
     dict(explorePopularSeeds=True, maxHitsToConsider=40),
     dict(stopOnFirstHit=True),
     dict(maxK=28, extraSearchDepth=3),
+    # scoreLimit falls below a partly scored element's lowestPossibleScore (BaseAligner.cpp:1129
+    # tests it once per element)
+    dict(maxK=2, extraSearchDepth=0),
+    dict(maxK=4, extraSearchDepth=0, maxSeedsToUse=8),
 ]
 
 
