@@ -56,6 +56,49 @@ def load_pmc_traffic():
     return None
 
 
+def init_distributed():
+    """One process per GPU (torch.distributed.run sets RANK/LOCAL_RANK/WORLD_SIZE); gloo
+    carries only the barrier and the max-over-ranks reduction -- reads are independent,
+    the index is replicated, no data-path collective."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    return world, rank, local, dist
+
+
+def make_workload(snapgpu, genome_bases, reads_per_rank, rank):
+    """The same deterministic genome on every rank; rank r aligns shard r of a
+    world x reads_per_rank batch (its own read-generator seed, so shards are disjoint)."""
+    genome = snapgpu.Genome.synthetic(genome_bases, seed=2121, n_contigs=1, n_repeat_families=200)
+    reads = snapgpu.Reads.synthetic(genome, reads_per_rank, seed=99 + rank)
+    return genome, reads
+
+
+def timed_steps(step, steps, dist, sync):
+    """Barrier + sync on both sides of exactly `steps` steps; returns the max over ranks."""
+    if dist:
+        dist.barrier()
+    sync()
+    t_start = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    t_end = time.perf_counter()
+    if dist:
+        dist.barrier()
+    elapsed = t_end - t_start
+    if dist:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -67,19 +110,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+    world, rank, local, dist = init_distributed()
 
     import snapgpu
     t0 = time.time()
-    genome = snapgpu.Genome.synthetic(args.genome_bases, seed=2121, n_contigs=1, n_repeat_families=200)
-    # reads: rank r takes shard r of a world*reads global batch (distinct seed per shard)
-    reads = snapgpu.Reads.synthetic(genome, args.reads, seed=99 + rank)
+    genome, reads = make_workload(snapgpu, args.genome_bases, args.reads, rank)
     idx = snapgpu.GenomeIndex.build(genome, 20, min(16, os.cpu_count() or 8))
     t_index = time.time() - t0
     aligner = snapgpu.BaseAligner(idx, device=local)
@@ -89,26 +124,14 @@ def main():
         dev.run()
         dev.synchronize()
     kernel_ms = []
-    if dist:
-        dist.barrier()
-    dev.synchronize()
-    t_start = time.perf_counter()
-    for _ in range(args.steps):
+
+    def step():
         dev.run()
         dev.synchronize()
         kernel_ms.append(aligner.timing()["mainKernelMs"])
-    dev.synchronize()
-    t_end = time.perf_counter()
-    if dist:
-        dist.barrier()
-    elapsed = t_end - t_start
-    res = dev.results()
 
-    if dist:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = timed_steps(step, args.steps, dist, dev.synchronize)
+    res = dev.results()
     total_reads = args.reads * world * args.steps
     value = total_reads / elapsed
     ms_per_step = elapsed * 1000.0 / args.steps
@@ -122,7 +145,7 @@ def main():
         counts = {int(k): int(v) for k, v in zip(*np.unique(res["result"], return_counts=True))}
         cpu = None
         parity = None
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:   # CPU baseline: rank 0 at N=1 only
             from oracle_ffi import mismatches, oracle_align
             nthr = max(1, args.cpu_threads)
             c0 = time.perf_counter()
