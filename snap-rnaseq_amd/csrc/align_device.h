@@ -192,10 +192,11 @@ struct GroupLds {
     uint32_t ecache[EB][ELEM_DWORDS];    // popped elements (authoritative while in the batch)
     uint32_t eidx[EB];
     uint16_t cand[CANDCAP];              // slot << 8 | bit
-    int16_t pm[2][4][32];                // LV path per [direction][group][row]: matched-run length
-    int8_t pa[2][4][32];                 //   and action (0 X, 1 D, 2 I); probabilities in apply
-    int16_t pL0[2][4];                   //   exact prefix L[0][0]
-    int8_t plen[2][4];                   //   path length (0: exact match, prob = perfect[patternLen])
+    uint8_t rows8[MAX_K][WAVE];          // LV rows: L + 2 per (row, lane); actions are recomputed
+    int16_t pm[2][128];                  // LV path per [direction][group*2*GS + row]: matched-run length
+    int8_t pa[2][128];                   //   and action (0 X, 1 D, 2 I); probabilities in apply
+    int16_t pL0[2][8];                   //   exact prefix L[0][0] per group
+    int8_t plen[2][8];                   //   path length (0: exact match, prob = perfect[patternLen])
 };
 
 template <int MAXLEN>
@@ -218,7 +219,7 @@ struct Lds {
     uint64_t seedUsed[NB + 1];                      // BaseAligner::seedUsed bit vector
     int16_t btAct[BYTE_PATH ? MAX_K + 1 : 1];       // LV backtrace scratch (byte path)
     int16_t btMatched[BYTE_PATH ? MAX_K + 1 : 1];
-    uint16_t rows[MAX_K][WAVE];                     // LV rows: (L+2) | action<<12
+    uint16_t rows[BYTE_PATH ? MAX_K : 1][WAVE];     // byte-path LV rows: (L+2) | action<<12
     GroupLds grp[BYTE_PATH ? 0 : 1];                // scorer of align_kernel<128>
 };
 

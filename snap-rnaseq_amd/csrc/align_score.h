@@ -73,7 +73,10 @@ __device__ __forceinline__ bool mk_bit(const Mask128 &F, int m) {
 template <int GS>
 __device__ __forceinline__ int from_lower(int v) {
     if constexpr (GS == 16) return __builtin_amdgcn_update_dpp(-2, v, 0x111, 0xf, 0xf, false);   // row_shr:1
-    else {
+    else if constexpr (GS == 8) {
+        const int r = __builtin_amdgcn_update_dpp(-2, v, 0x111, 0xf, 0xf, false);
+        return (lane_id() & 7) == 0 ? -2 : r;
+    } else {
         const int r = __builtin_amdgcn_update_dpp(-2, v, 0x138, 0xf, 0xf, false);               // wave_shr:1
         return (lane_id() & (GS - 1)) == 0 ? -2 : r;
     }
@@ -82,7 +85,10 @@ __device__ __forceinline__ int from_lower(int v) {
 template <int GS>
 __device__ __forceinline__ int from_upper(int v) {
     if constexpr (GS == 16) return __builtin_amdgcn_update_dpp(-2, v, 0x101, 0xf, 0xf, false);   // row_shl:1
-    else {
+    else if constexpr (GS == 8) {
+        const int r = __builtin_amdgcn_update_dpp(-2, v, 0x101, 0xf, 0xf, false);
+        return (lane_id() & 7) == 7 ? -2 : r;
+    } else {
         const int r = __builtin_amdgcn_update_dpp(-2, v, 0x130, 0xf, 0xf, false);               // wave_shl:1
         return (lane_id() & (GS - 1)) == GS - 1 ? -2 : r;
     }
@@ -98,11 +104,12 @@ __device__ __forceinline__ int from_upper(int v) {
 // later, only for candidates the scorer applies (lv_prob).
 template <int DIR, int GS>
 __device__ __forceinline__ int lv_group(GroupLds &G, const Mask128 &M, bool gact, int q0, int patternLen,
-                                        int textLen, int k, int kmaxAll, uint16_t (*rows)[WAVE], int &outE) {
+                                        int textLen, int k, int kmaxAll, int &outE) {
     constexpr int dx = DIR > 0 ? 0 : 1;
     const int lane = lane_id();
     const int li = lane & (GS - 1), gi = lane / GS, c = GS / 2 - 1;
     const int d = DIR > 0 ? li - c : c - li;
+    const int pbase = gi * 2 * GS;                       // this group's path slots
     if (k > MAX_K - 1) k = MAX_K - 1;
     outE = -1;
     bool done = !gact;
@@ -138,7 +145,8 @@ __device__ __forceinline__ int lv_group(GroupLds &G, const Mask128 &M, bool gact
         const int slid = f < endd ? f : endd;
         const int bnew = best < endd ? slid : (mk_bit(M, mpos) ? best : endd);
         const int Ln = active ? bnew : Lp;
-        if (active) rows[e][lane] = (uint16_t)((bnew + 2) | (act << 12));
+        if (active) G.rows8[e][lane] = (uint8_t)(bnew + 2);
+        (void)act;
         const uint64_t hit = ballot(active && Ln == patternLen);
         if (hit) {
             const uint64_t gm = GS == 64 ? hit : (hit >> (gi * GS)) & ((1ull << (GS & 63)) - 1);
@@ -152,18 +160,25 @@ __device__ __forceinline__ int lv_group(GroupLds &G, const Mask128 &M, bool gact
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                // backtrace; the action of a cell is recomputed from the previous row exactly
+                // as the row step chose it (X, then D, then I if strictly greater)
+                auto val = [&](int r, int dd) -> int {   // L[r][dd] as the row step saw it
+                    if (r == 0) return dd == 0 ? L0 : -2;
+                    if (dd > r || dd < -r) return -2;
+                    return (int)G.rows8[r][gi * GS + (DIR > 0 ? c + dd : c - dd)] - 2;
+                };
                 int curD = wd;
                 for (int ce = e; ce >= 1; ce--) {
-                    const int ln = gi * GS + (DIR > 0 ? c + curD : c - curD);
-                    const uint32_t cell = rows[ce][ln];
-                    const int a = (int)(cell >> 12);
-                    const int Lcur = (int)(cell & 0xfff) - 2;
+                    const int Lcur = val(ce, curD);
+                    const int x1 = val(ce - 1, curD) + 1, left = val(ce - 1, curD - 1);
+                    const int right = val(ce - 1, curD + 1) + 1;
+                    const int bxd = left > x1 ? left : x1;
+                    const int a = right > bxd ? 2 : (left > x1 ? 1 : 0);
                     const int src = a == 2 ? curD + 1 : (a == 1 ? curD - 1 : curD);
-                    const int ls = gi * GS + (DIR > 0 ? c + src : c - src);
-                    const int Lsrc = (ce - 1 == 0) ? (src == 0 ? L0 : -2) : ((int)(rows[ce - 1][ls] & 0xfff) - 2);
+                    const int Lsrc = a == 2 ? right - 1 : (a == 1 ? left : x1 - 1);
                     if (li == 0) {
-                        G.pa[dx][gi][ce] = (int8_t)a;
-                        G.pm[dx][gi][ce] = (int16_t)(a == 1 ? Lcur - Lsrc : Lcur - Lsrc - 1);
+                        G.pa[dx][pbase + ce] = (int8_t)a;
+                        G.pm[dx][pbase + ce] = (int16_t)(a == 1 ? Lcur - Lsrc : Lcur - Lsrc - 1);
                     }
                     curD = src;
                 }
@@ -184,16 +199,16 @@ __device__ __forceinline__ int lv_group(GroupLds &G, const Mask128 &M, bool gact
 // factor indel[cnt], X steps one phred factor each at offset L0 + sum of earlier
 // steps' (+-1 + matched).  Factors are fetched in parallel and multiplied in the
 // reference's order (x * 1.0 == x, so steps without a factor multiply by 1.0).
-__device__ __forceinline__ void lv_prob_pair(const DevTables *tab, const GroupLds &G, int g, int n, int s0, int t0,
-                                             const char *qual, double &p1, double &p2, int &net2) {
+__device__ __forceinline__ void lv_prob_pair(const DevTables *tab, const GroupLds &G, int g, int pbase, int n, int s0,
+                                             int t0, const char *qual, double &p1, double &p2, int &net2) {
     const int lane = lane_id();
     const int dx = lane >> 5, j = (lane & 31) + 1;               // step j of direction dx
     const int e = G.plen[dx][g];
     const int L0 = G.pL0[dx][g];
     const bool valid = j <= e;
-    const int a = valid ? G.pa[dx][g][j] : -1;
-    const int pmv = valid ? G.pm[dx][g][j] : 0;
-    const int an = j + 1 <= e ? G.pa[dx][g][j + 1] : -2;
+    const int a = valid ? G.pa[dx][pbase + j] : -1;
+    const int pmv = valid ? G.pm[dx][pbase + j] : 0;
+    const int an = j + 1 <= e ? G.pa[dx][pbase + j + 1] : -2;
     const bool runEnd = valid && (j == e || pmv != 0 || an != a);
     // offset before step j: inclusive scan of delta over the half-wave, minus own delta
     const int delta = valid ? (a == 1 ? -1 : 1) + pmv : 0;
@@ -316,10 +331,10 @@ __device__ __forceinline__ void lv_pass(const KArgs &A, Lds<128> &S, uint32_t i0
     PH_ADD(A, S, PH_STAGE, tst);
     PH_T(A, tf);
     const int t = P.s + (int)A.seedLen;
-    const int rf = lv_group<1, GS>(G, F, P.act, t, (int)n - t, P.glen - t, k, k, S.rows, e1);
+    const int rf = lv_group<1, GS>(G, F, P.act, t, (int)n - t, P.glen - t, k, k, e1);
     PH_ADD(A, S, PH_LVF, tf);
     PH_CNT(A, S, PH_ROWSF, rf);
-    PH_CNT(A, S, GS == 16 ? PH_NPASS16 : (GS == 32 ? PH_NPASS32 : PH_NPASS64), 1);
+    PH_CNT(A, S, GS <= 16 ? PH_NPASS16 : (GS == 32 ? PH_NPASS32 : PH_NPASS64), 1);
     PH_T(A, tr);
     const int k2 = k - e1;
     const bool ract = P.act && e1 >= 0;
@@ -328,7 +343,7 @@ __device__ __forceinline__ void lv_pass(const KArgs &A, Lds<128> &S, uint32_t i0
     if (kmax2 >= 0) {
         // reverse LV: pattern = read[s-1 .. 0], text = genome backwards from loc+s-1 (BaseAligner.cpp:1216-1220)
         const Mask128 R = mk_reverse(F);
-        const int rr = lv_group<-1, GS>(G, R, ract, 127 - (P.s - 1), P.s, P.s + MAX_K, k2, kmax2, S.rows, e2);
+        const int rr = lv_group<-1, GS>(G, R, ract, 127 - (P.s - 1), P.s, P.s + MAX_K, k2, kmax2, e2);
         PH_CNT(A, S, PH_ROWSR, rr);
     }
     PH_ADD(A, S, PH_LVR, tr);
@@ -461,13 +476,14 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<128> &S, Elem 
         for (uint32_t i0 = 0; i0 < nc;) {
             if (overdue(st, 2)) return true;
             const int k = st.scoreLimit < (uint32_t)(MAX_K - 1) ? (int)st.scoreLimit : MAX_K - 1;
-            const int GS = k <= 7 ? 16 : (k <= 15 ? 32 : 64);
+            const int GS = k <= 3 ? 8 : (k <= 7 ? 16 : (k <= 15 ? 32 : 64));
             const int Gn = 64 / GS;
             const int m = (int)(nc - i0) < Gn ? (int)(nc - i0) : Gn;
             PH_CNT(A, S, PH_NPASS, 1);
             PassLane P;
             int e1, e2;
-            if (GS == 16) lv_pass<16>(A, S, i0, m, k, n, P, e1, e2);
+            if (GS == 8) lv_pass<8>(A, S, i0, m, k, n, P, e1, e2);
+            else if (GS == 16) lv_pass<16>(A, S, i0, m, k, n, P, e1, e2);
             else if (GS == 32) lv_pass<32>(A, S, i0, m, k, n, P, e1, e2);
             else lv_pass<64>(A, S, i0, m, k, n, P, e1, e2);
             PH_T(A, tapp);
@@ -496,7 +512,7 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<128> &S, Elem 
                     uint64_t acc = 0;
                     bool first = true;
 #pragma unroll
-                    for (int jg = 0; jg < 4; jg++) {
+                    for (int jg = 0; jg < 8; jg++) {
                         const int lj = jg * GS;
                         if (lj < WAVE && ((fm >> (lj & 63)) & 1)) {
                             const uint32_t slj = readlaneu(sl, lj & 63), bj = readlaneu(bit, lj & 63);
@@ -543,7 +559,7 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<128> &S, Elem 
                 const uint32_t dir = cKey & 1;
                 double q1, q2;
                 int net2;
-                lv_prob_pair(tab, G, gs, (int)n, s0, t0, dir ? S.rcQ : S.fwdQ, q1, q2, net2);
+                lv_prob_pair(tab, G, gs, gs * 2 * GS, (int)n, s0, t0, dir ? S.rcQ : S.fwdQ, q1, q2, net2);
                 const double prob = q1 * q2 * tab->seedProb;
                 const uint32_t ebase = (cKey >> 1) * ELEM;
                 const uint32_t elemLoc = ebase + cbit;

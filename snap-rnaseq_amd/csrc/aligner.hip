@@ -522,7 +522,9 @@ __device__ void align_one(const KArgs &A, Lds<MAXLEN> &S, Elem *ar, uint32_t r) 
 }
 
 template <int MAXLEN>
-__global__ __launch_bounds__(64) void align_kernel(KArgs A) {
+// amdgpu_waves_per_eu(3): keep <= 168 VGPRs (3 waves/SIMD, 12 per CU); a few cold spills
+// are cheaper than dropping to 2 waves/SIMD.
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void align_kernel(KArgs A) {
     __shared__ Lds<MAXLEN> S;
     Elem *ar = A.arena + (uint64_t)blockIdx.x * A.arenaElems;
     const int lane = lane_id();
