@@ -349,6 +349,173 @@ __device__ __forceinline__ void lv_pass(const KArgs &A, Lds<128> &S, uint32_t i0
     PH_ADD(A, S, PH_LVR, tr);
 }
 
+// One LV pass over candidates [i0, i0+m) and their application in the reference's
+// order (BaseAligner.cpp:1129-1384).  Returns true when the read is finished
+// (stopOnFirstHit).  GS is a template parameter so group indexing is shifts and the
+// per-group loops unroll.
+template <int GS>
+__device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<128> &S, Elem *ar, ReadState &st, uint32_t i0, int m,
+                                           int k, uint32_t n, uint32_t nb, uint32_t &lastSlot, bool &lastSkip,
+                                           int *result) {
+    const int lane = lane_id();
+    GroupLds &G = S.grp[0];
+    const DevTables *tab = A.tab;
+    PassLane P;
+    int e1, e2;
+    lv_pass<GS>(A, S, i0, m, k, n, P, e1, e2);
+    PH_T(A, tapp);
+    // ---- apply in order with the limit in force at each candidate.  Group
+    // leaders (lane g*GS) hold candidate g.  A failure only sets its scored bit
+    // and, for an element's first scored candidate, bestLoc/bestScore/prob
+    // (BaseAligner.cpp:1253-1265 with score -1: nothing else changes), so the
+    // failures before the next success are applied together, lane-parallel.
+    const int gq = lane / GS;
+    const bool leader = (lane & (GS - 1)) == 0 && gq < m;
+    const uint32_t sl = P.cw >> 8, bit = P.cw & 0xff;
+    const uint32_t ew11 = leader ? G.ecache[sl][11] : 0u;
+    for (int g0 = 0; g0 < m;) {
+        const int kNow = (int)(st.scoreLimit < (uint32_t)(MAX_K - 1) ? st.scoreLimit : MAX_K - 1);
+        // element lps test, made once when the element's first candidate is reached
+        // (BaseAligner.cpp:1129); candidates of one element are contiguous
+        const bool skip = sl == lastSlot ? lastSkip : ((ew11 >> 8) & 0xff) > st.scoreLimit;
+        const int lim2 = (int)st.scoreLimit - e1 > MAX_K - 1 ? MAX_K - 1 : (int)st.scoreLimit - e1;
+        const bool succ = leader && !skip && P.act && e1 >= 0 && e1 <= kNow && e2 >= 0 && e2 <= lim2;
+        const uint64_t sm = ballot(succ && gq >= g0);
+        const int gs = sm ? (int)__builtin_ctzll(sm) / GS : m;
+        const bool fail = leader && !skip && gq >= g0 && gq < gs;
+        const uint64_t fm = ballot(fail);
+        if (fm) {
+            // per element: OR of the failing bits; the first failing lane of the element writes
+            uint64_t acc = 0;
+            bool first = true;
+#pragma unroll
+            for (int jg = 0; jg < 64 / GS; jg++) {
+                const int lj = jg * GS;
+                if (lj < WAVE && ((fm >> (lj & 63)) & 1)) {
+                    const uint32_t slj = readlaneu(sl, lj & 63), bj = readlaneu(bit, lj & 63);
+                    if (fail && slj == sl) {
+                        acc |= 1ull << bj;
+                        if (jg < gq) first = false;
+                    }
+                }
+            }
+            if (fail && first) {
+                uint32_t *ec = G.ecache[sl];
+                const uint64_t old = ((uint64_t)ec[3] << 32) | ec[2];
+                const uint64_t nw = old | acc;
+                ec[2] = (uint32_t)nw;
+                ec[3] = (uint32_t)(nw >> 32);
+                if (old == 0) {   // first scored candidate of the element: score -1 recorded
+                    ec[9] = (ec[6] >> 1) * ELEM + bit;
+                    ec[8] = FAIL_SCORE;
+                    ec[4] = 0u;
+                    ec[5] = 0u;
+                }
+            }
+            st.nScored += (uint32_t)__popcll(fm);
+            wave_sync();
+        }
+        if (gs >= m) {
+            lastSlot = readlaneu(sl, (m - 1) * GS);
+            lastSkip = readlane(skip ? 1 : 0, (m - 1) * GS) != 0;
+            break;
+        }
+        lastSlot = readlaneu(sl, gs * GS);
+        lastSkip = false;
+        // ---- the success at group gs: full bookkeeping (BaseAligner.cpp:1227-1384)
+        const int ln = gs * GS;
+        const uint32_t csl = readlaneu(sl, ln), cbit = readlaneu(bit, ln);
+        const int r1 = readlane(e1, ln), r2 = readlane(e2, ln);
+        const uint32_t ev = lane < 12 ? G.ecache[csl][lane] : 0u;
+        uint64_t cScored = rl64(ev, 2);
+        const double cProb = rld(ev, 4);
+        const uint32_t cKey = rl(ev, 6), cBest = rl(ev, 8);
+        const uint32_t sc = (uint32_t)(r1 + r2);
+        PH_CNT(A, S, PH_NSUCC, 1);
+        const int s0 = readlane(P.s, ln), t0 = s0 + (int)A.seedLen;
+        const uint32_t dir = cKey & 1;
+        double q1, q2;
+        int net2;
+        lv_prob_pair(tab, G, gs, gs * 2 * GS, (int)n, s0, t0, dir ? S.rcQ : S.fwdQ, q1, q2, net2);
+        const double prob = q1 * q2 * tab->seedProb;
+        const uint32_t ebase = (cKey >> 1) * ELEM;
+        const uint32_t elemLoc = ebase + cbit;
+        const uint32_t loc = elemLoc + (uint32_t)net2;
+        const bool anyNearby0 = cScored != 0;
+        cScored |= 1ull << cbit;
+        st.nScored++;
+        g0 = gs + 1;
+        const bool passA = !(anyNearby0 && (cBest < sc || (cBest == sc && prob <= cProb)));
+        bool take = passA;
+        uint32_t nb2 = NONE;
+        int cs = -1;
+        uint32_t nv = 0;
+        if (take) {
+            const uint32_t nl = elemLoc + (2 * (elemLoc % ELEM / (ELEM / 2)) - 1) * (ELEM / 2);
+            const uint32_t nkey = ((nl / ELEM) << 1) | dir;
+            nb2 = uni(chain_find(S.head, ar, nkey, (uint32_t)A.arenaElems));
+        }
+        if (nb2 != NONE) {
+            // the nearby element may be in this batch: its cache is authoritative
+            const uint64_t inb = ballot((uint32_t)lane < nb && G.eidx[lane < EB ? lane : 0] == nb2);
+            cs = inb ? (int)__builtin_ctzll(inb) : -1;
+            if (cs >= 0) nv = lane < 12 ? G.ecache[cs][lane] : 0u;
+            else nv = lane < 12 ? ((const uint32_t *)(ar + nb2))[lane] : 0u;
+            if (rl64(nv, 2) == 0) nb2 = NONE;   // nearby element not scored yet
+            if (nb2 != NONE) {
+                const uint32_t nbase = (rl(nv, 6) >> 1) * ELEM;
+                const uint32_t nbl = rl(nv, 9);
+                if (!((nbase > ebase && loc - nbl <= (uint32_t)ELEM) || (nbase < ebase && nbl <= (uint32_t)ELEM)))
+                    nb2 = NONE;   // sic: BaseAligner.cpp:1311-1312
+            }
+            if (nb2 != NONE) {
+                const uint32_t nbs = rl(nv, 8);
+                const double np = rld(nv, 4);
+                if (nbs < sc || (nbs == sc && np >= prob)) take = false;
+                else {
+                    st.pAll = st.pAll - np > 0.0 ? st.pAll - np : 0.0;
+                    if (cs >= 0) { if (lane == 4 || lane == 5) G.ecache[cs][lane] = 0u; }
+                    else if (lane == 4 || lane == 5) ((uint32_t *)(ar + nb2))[lane] = 0u;
+                }
+            }
+        }
+        // write the element back (scored always; the rest only when taken)
+        {
+            const uint64_t pb = (uint64_t)__double_as_longlong(prob);
+            uint32_t *ec = G.ecache[csl];
+            if (lane == 2) ec[2] = (uint32_t)cScored;
+            else if (lane == 3) ec[3] = (uint32_t)(cScored >> 32);
+            // bestScoreGenomeLocation is set once the candidate passed the first check (:1266-1268)
+            if (lane == 9 && passA) ec[9] = loc;
+            if (take) {
+                if (lane == 4) ec[4] = (uint32_t)pb;
+                else if (lane == 5) ec[5] = (uint32_t)(pb >> 32);
+                else if (lane == 8) ec[8] = sc;
+            }
+            wave_sync();
+        }
+        if (!take) continue;
+        st.pAll = st.pAll - cProb > 0.0 ? st.pAll - cProb : 0.0;
+        st.pAll += prob;
+        if (st.bestScore > sc || (st.bestScore == sc && prob > st.pBest)) {
+            st.bestScore = sc;
+            st.pBest = prob;
+            st.bestLoc = loc;
+            st.outLoc = loc;
+            st.outScore = (int32_t)sc;
+            st.outDir = dir;
+        }
+        if (A.stopOnFirst && st.bestScore <= A.maxK) {
+            *result = SNAPGPU_MULTIPLE_HITS;
+            st.outMapq = 0;
+            return true;
+        }
+        st.scoreLimit = (st.bestScore < A.maxK ? st.bestScore : A.maxK) + A.extra;
+    }
+    PH_ADD(A, S, PH_APPLY, tapp);
+    return false;
+}
+
 // BaseAligner::score (BaseAligner.cpp:977-1399) over batches of popped elements.
 __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<128> &S, Elem *ar, ReadState &st, bool force,
                                            uint32_t n, int *result, uint32_t *flags) {
@@ -480,162 +647,12 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<128> &S, Elem 
             const int Gn = 64 / GS;
             const int m = (int)(nc - i0) < Gn ? (int)(nc - i0) : Gn;
             PH_CNT(A, S, PH_NPASS, 1);
-            PassLane P;
-            int e1, e2;
-            if (GS == 8) lv_pass<8>(A, S, i0, m, k, n, P, e1, e2);
-            else if (GS == 16) lv_pass<16>(A, S, i0, m, k, n, P, e1, e2);
-            else if (GS == 32) lv_pass<32>(A, S, i0, m, k, n, P, e1, e2);
-            else lv_pass<64>(A, S, i0, m, k, n, P, e1, e2);
-            PH_T(A, tapp);
-            // ---- apply in order with the limit in force at each candidate.  Group
-            // leaders (lane g*GS) hold candidate g.  A failure only sets its scored bit
-            // and, for an element's first scored candidate, bestLoc/bestScore/prob
-            // (BaseAligner.cpp:1253-1265 with score -1: nothing else changes), so the
-            // failures before the next success are applied together, lane-parallel.
-            const int gq = lane / GS;
-            const bool leader = (lane & (GS - 1)) == 0 && gq < m;
-            const uint32_t sl = P.cw >> 8, bit = P.cw & 0xff;
-            const uint32_t ew11 = leader ? G.ecache[sl][11] : 0u;
-            for (int g0 = 0; g0 < m;) {
-                const int kNow = (int)(st.scoreLimit < (uint32_t)(MAX_K - 1) ? st.scoreLimit : MAX_K - 1);
-                // element lps test, made once when the element's first candidate is reached
-                // (BaseAligner.cpp:1129); candidates of one element are contiguous
-                const bool skip = sl == lastSlot ? lastSkip : ((ew11 >> 8) & 0xff) > st.scoreLimit;
-                const int lim2 = (int)st.scoreLimit - e1 > MAX_K - 1 ? MAX_K - 1 : (int)st.scoreLimit - e1;
-                const bool succ = leader && !skip && P.act && e1 >= 0 && e1 <= kNow && e2 >= 0 && e2 <= lim2;
-                const uint64_t sm = ballot(succ && gq >= g0);
-                const int gs = sm ? (int)__builtin_ctzll(sm) / GS : m;
-                const bool fail = leader && !skip && gq >= g0 && gq < gs;
-                const uint64_t fm = ballot(fail);
-                if (fm) {
-                    // per element: OR of the failing bits; the first failing lane of the element writes
-                    uint64_t acc = 0;
-                    bool first = true;
-#pragma unroll
-                    for (int jg = 0; jg < 8; jg++) {
-                        const int lj = jg * GS;
-                        if (lj < WAVE && ((fm >> (lj & 63)) & 1)) {
-                            const uint32_t slj = readlaneu(sl, lj & 63), bj = readlaneu(bit, lj & 63);
-                            if (fail && slj == sl) {
-                                acc |= 1ull << bj;
-                                if (jg < gq) first = false;
-                            }
-                        }
-                    }
-                    if (fail && first) {
-                        uint32_t *ec = G.ecache[sl];
-                        const uint64_t old = ((uint64_t)ec[3] << 32) | ec[2];
-                        const uint64_t nw = old | acc;
-                        ec[2] = (uint32_t)nw;
-                        ec[3] = (uint32_t)(nw >> 32);
-                        if (old == 0) {   // first scored candidate of the element: score -1 recorded
-                            ec[9] = (ec[6] >> 1) * ELEM + bit;
-                            ec[8] = FAIL_SCORE;
-                            ec[4] = 0u;
-                            ec[5] = 0u;
-                        }
-                    }
-                    st.nScored += (uint32_t)__popcll(fm);
-                    wave_sync();
-                }
-                if (gs >= m) {
-                    lastSlot = readlaneu(sl, (m - 1) * GS);
-                    lastSkip = readlane(skip ? 1 : 0, (m - 1) * GS) != 0;
-                    break;
-                }
-                lastSlot = readlaneu(sl, gs * GS);
-                lastSkip = false;
-                // ---- the success at group gs: full bookkeeping (BaseAligner.cpp:1227-1384)
-                const int ln = gs * GS;
-                const uint32_t csl = readlaneu(sl, ln), cbit = readlaneu(bit, ln);
-                const int r1 = readlane(e1, ln), r2 = readlane(e2, ln);
-                const uint32_t ev = lane < 12 ? G.ecache[csl][lane] : 0u;
-                uint64_t cScored = rl64(ev, 2);
-                const double cProb = rld(ev, 4);
-                const uint32_t cKey = rl(ev, 6), cBest = rl(ev, 8);
-                const uint32_t sc = (uint32_t)(r1 + r2);
-                PH_CNT(A, S, PH_NSUCC, 1);
-                const int s0 = readlane(P.s, ln), t0 = s0 + (int)A.seedLen;
-                const uint32_t dir = cKey & 1;
-                double q1, q2;
-                int net2;
-                lv_prob_pair(tab, G, gs, gs * 2 * GS, (int)n, s0, t0, dir ? S.rcQ : S.fwdQ, q1, q2, net2);
-                const double prob = q1 * q2 * tab->seedProb;
-                const uint32_t ebase = (cKey >> 1) * ELEM;
-                const uint32_t elemLoc = ebase + cbit;
-                const uint32_t loc = elemLoc + (uint32_t)net2;
-                const bool anyNearby0 = cScored != 0;
-                cScored |= 1ull << cbit;
-                st.nScored++;
-                g0 = gs + 1;
-                const bool passA = !(anyNearby0 && (cBest < sc || (cBest == sc && prob <= cProb)));
-                bool take = passA;
-                uint32_t nb2 = NONE;
-                int cs = -1;
-                uint32_t nv = 0;
-                if (take) {
-                    const uint32_t nl = elemLoc + (2 * (elemLoc % ELEM / (ELEM / 2)) - 1) * (ELEM / 2);
-                    const uint32_t nkey = ((nl / ELEM) << 1) | dir;
-                    nb2 = uni(chain_find(S.head, ar, nkey, (uint32_t)A.arenaElems));
-                }
-                if (nb2 != NONE) {
-                    // the nearby element may be in this batch: its cache is authoritative
-                    const uint64_t inb = ballot((uint32_t)lane < nb && G.eidx[lane < EB ? lane : 0] == nb2);
-                    cs = inb ? (int)__builtin_ctzll(inb) : -1;
-                    if (cs >= 0) nv = lane < 12 ? G.ecache[cs][lane] : 0u;
-                    else nv = lane < 12 ? ((const uint32_t *)(ar + nb2))[lane] : 0u;
-                    if (rl64(nv, 2) == 0) nb2 = NONE;   // nearby element not scored yet
-                    if (nb2 != NONE) {
-                        const uint32_t nbase = (rl(nv, 6) >> 1) * ELEM;
-                        const uint32_t nbl = rl(nv, 9);
-                        if (!((nbase > ebase && loc - nbl <= (uint32_t)ELEM) || (nbase < ebase && nbl <= (uint32_t)ELEM)))
-                            nb2 = NONE;   // sic: BaseAligner.cpp:1311-1312
-                    }
-                    if (nb2 != NONE) {
-                        const uint32_t nbs = rl(nv, 8);
-                        const double np = rld(nv, 4);
-                        if (nbs < sc || (nbs == sc && np >= prob)) take = false;
-                        else {
-                            st.pAll = st.pAll - np > 0.0 ? st.pAll - np : 0.0;
-                            if (cs >= 0) { if (lane == 4 || lane == 5) G.ecache[cs][lane] = 0u; }
-                            else if (lane == 4 || lane == 5) ((uint32_t *)(ar + nb2))[lane] = 0u;
-                        }
-                    }
-                }
-                // write the element back (scored always; the rest only when taken)
-                {
-                    const uint64_t pb = (uint64_t)__double_as_longlong(prob);
-                    uint32_t *ec = G.ecache[csl];
-                    if (lane == 2) ec[2] = (uint32_t)cScored;
-                    else if (lane == 3) ec[3] = (uint32_t)(cScored >> 32);
-                    // bestScoreGenomeLocation is set once the candidate passed the first check (:1266-1268)
-                    if (lane == 9 && passA) ec[9] = loc;
-                    if (take) {
-                        if (lane == 4) ec[4] = (uint32_t)pb;
-                        else if (lane == 5) ec[5] = (uint32_t)(pb >> 32);
-                        else if (lane == 8) ec[8] = sc;
-                    }
-                    wave_sync();
-                }
-                if (!take) continue;
-                st.pAll = st.pAll - cProb > 0.0 ? st.pAll - cProb : 0.0;
-                st.pAll += prob;
-                if (st.bestScore > sc || (st.bestScore == sc && prob > st.pBest)) {
-                    st.bestScore = sc;
-                    st.pBest = prob;
-                    st.bestLoc = loc;
-                    st.outLoc = loc;
-                    st.outScore = (int32_t)sc;
-                    st.outDir = dir;
-                }
-                if (A.stopOnFirst && st.bestScore <= A.maxK) {
-                    *result = SNAPGPU_MULTIPLE_HITS;
-                    st.outMapq = 0;
-                    return true;
-                }
-                st.scoreLimit = (st.bestScore < A.maxK ? st.bestScore : A.maxK) + A.extra;
-            }
-            PH_ADD(A, S, PH_APPLY, tapp);
+            bool fin;
+            if (GS == 8) fin = pass_apply<8>(A, S, ar, st, i0, m, k, n, nb, lastSlot, lastSkip, result);
+            else if (GS == 16) fin = pass_apply<16>(A, S, ar, st, i0, m, k, n, nb, lastSlot, lastSkip, result);
+            else if (GS == 32) fin = pass_apply<32>(A, S, ar, st, i0, m, k, n, nb, lastSlot, lastSkip, result);
+            else fin = pass_apply<64>(A, S, ar, st, i0, m, k, n, nb, lastSlot, lastSkip, result);
+            if (fin) return true;
             i0 += (uint32_t)m;
         }
         PH_ADD(A, S, PH_PASSLOOP, tpl);

@@ -292,7 +292,7 @@ __device__ __forceinline__ void defer_read(const KArgs &A, uint32_t r) {
 
 // ------------------------------------------------------------- AlignRead
 template <int MAXLEN>
-__device__ void align_one(const KArgs &A, Lds<MAXLEN> &S, Elem *ar, uint32_t r) {
+__device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, Elem *ar, uint32_t r) {
     constexpr int NB = MAXLEN / 64;
     const int lane = lane_id();
     PH_T(A, tsetup);
