@@ -40,7 +40,7 @@ constexpr uint32_t NPAD = 100;            // Genome::N_PADDING
 constexpr int NBUCKET_LOG2 = 9;
 constexpr int NBUCKET = 1 << NBUCKET_LOG2;  // element hash buckets (LDS)
 constexpr uint32_t SKCAP = 256;           // selection keys kept in LDS
-constexpr int ELEM_DWORDS = 36;           // meaningful dwords of Elem
+constexpr int ELEM_DWORDS = 36;           // dwords of Elem512 (byte path)
 constexpr int BT = 128;                   // insertion-batch dedupe table (LDS)
 constexpr uint32_t NONE = 0xffffffffu;
 
@@ -53,7 +53,11 @@ struct DevTables {
     double mapqT[72];         // mapqT[q] = 10^(-q/10) (glibc pow): MAPQ thresholds, no device log10
 };
 
-struct Elem {                 // 192 bytes, 64-byte aligned slots in HBM
+// HashTableElement (BaseAligner.h:188-214) in the HBM arena: a 48-byte header of
+// the fields the kernels read and write, then the per-candidate seed offsets.  Reads
+// of <= 128 bases keep u8 offsets (96-B elements); the byte path keeps u16 (144 B).
+template <typename OffT>
+struct ElemT {
     uint64_t used;            // candidatesUsed
     uint64_t scored;          // candidatesScored
     double prob;              // matchProbabilityForBestScore
@@ -63,10 +67,15 @@ struct Elem {                 // 192 bytes, 64-byte aligned slots in HBM
     uint32_t bestLoc;         // bestScoreGenomeLocation
     uint32_t sortkey;         // linked ? weight<<24 | (0xffffff - ts) : 0
     uint8_t weight, lps, allScored, pad;
-    uint16_t seedOffset[ELEM];
-    uint8_t pad2[48];
+    OffT seedOffset[ELEM];
+    static constexpr int DWORDS = (48 + ELEM * (int)sizeof(OffT)) / 4;
 };
-static_assert(sizeof(Elem) == 192, "Elem layout");
+using Elem128 = ElemT<uint8_t>;
+using Elem512 = ElemT<uint16_t>;
+static_assert(sizeof(Elem128) == 96 && sizeof(Elem512) == 144, "Elem layout");
+template <int MAXLEN> struct ElemSel { using type = Elem512; };
+template <> struct ElemSel<128> { using type = Elem128; };
+template <int MAXLEN> using ElemOf = typename ElemSel<MAXLEN>::type;
 
 struct KArgs {
     // index (HBM)
@@ -92,7 +101,7 @@ struct KArgs {
     snapgpu_result_t *out;
     // work queue + arenas
     uint32_t *counter;
-    Elem *arena;
+    void *arena;                 // ElemOf<MAXLEN> per block
     uint64_t arenaElems;         // per-wave capacity
     // genome bit planes {hi, lo, notACGT, 0} per 32 bases, word 0 = position -PACK_GUARD
     const uint4 *gpl;
@@ -189,7 +198,7 @@ constexpr uint32_t ORDCAP = 512;         // forced-mode pop order (u16, overlays
 // Scorer state of align_kernel<128> (align_score.h).
 struct GroupLds {
     uint64_t rpl[2][3][2];               // read[dir] bit planes {hi, lo, notACGT}, positions 0..127
-    uint32_t ecache[EB][ELEM_DWORDS];    // popped elements (authoritative while in the batch)
+    uint32_t ecache[EB][24];             // popped Elem128s (authoritative while in the batch)
     uint32_t eidx[EB];
     uint16_t cand[CANDCAP];              // slot << 8 | bit
     uint8_t rows8[MAX_K][WAVE];          // LV rows: L + 2 per (row, lane); actions are recomputed
@@ -538,7 +547,8 @@ __device__ __forceinline__ bool overdue(ReadState &st, uint32_t site) {
 __device__ __forceinline__ uint32_t elem_hash(uint32_t key) { return (key * 2654435761u) >> (32 - NBUCKET_LOG2); }
 
 // find element with `key`; NONE if absent
-__device__ __forceinline__ uint32_t chain_find(const uint32_t *head, const Elem *ar, uint32_t key, uint32_t cap) {
+template <typename E>
+__device__ __forceinline__ uint32_t chain_find(const uint32_t *head, const E *ar, uint32_t key, uint32_t cap) {
     uint32_t e = head[elem_hash(key)];
     for (uint32_t steps = 0; e != NONE && ar[e].key != key; steps++) {
         if (steps > cap) { diag_report(DIAG_CHAIN, key, e); return NONE; }
@@ -549,18 +559,18 @@ __device__ __forceinline__ uint32_t chain_find(const uint32_t *head, const Elem 
 
 // selection keys: LDS for the first SKCAP elements of a read, HBM beyond
 template <int MAXLEN>
-__device__ __forceinline__ uint32_t sk_get(const Lds<MAXLEN> &S, const Elem *ar, uint32_t e) {
+__device__ __forceinline__ uint32_t sk_get(const Lds<MAXLEN> &S, const ElemOf<MAXLEN> *ar, uint32_t e) {
     return e < SKCAP ? S.sk[e] : ar[e].sortkey;
 }
 template <int MAXLEN>
-__device__ __forceinline__ void sk_set(Lds<MAXLEN> &S, Elem *ar, uint32_t e, uint32_t v) {
+__device__ __forceinline__ void sk_set(Lds<MAXLEN> &S, ElemOf<MAXLEN> *ar, uint32_t e, uint32_t v) {
     if (e < SKCAP) S.sk[e] = v;
     else ar[e].sortkey = v;
 }
 
 // owner-lane recompute of its selection maximum (elements e == lane mod 64)
 template <int MAXLEN>
-__device__ __forceinline__ void recompute_lane_max(Lds<MAXLEN> &S, const Elem *ar, int lane) {
+__device__ __forceinline__ void recompute_lane_max(Lds<MAXLEN> &S, const ElemOf<MAXLEN> *ar, int lane) {
     uint64_t best = 0;
     const uint32_t nElems = S.nElems;
     for (uint32_t e = lane; e < nElems; e += WAVE) {

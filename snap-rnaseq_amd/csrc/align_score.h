@@ -285,7 +285,7 @@ __device__ __forceinline__ void lv_pass(const KArgs &A, Lds<128> &S, uint32_t i0
         P.cw = cw;
         P.loc = (key >> 1) * ELEM + bit;
         P.dir = (int)(key & 1);
-        P.s = (int)((G.ecache[sl][12 + bit / 2] >> (16 * (bit & 1))) & 0xffff);
+        P.s = (int)((G.ecache[sl][12 + bit / 4] >> (8 * (bit & 3))) & 0xff);
         uint32_t glen = n + MAX_K;
         bool ok = substring_ok(A, P.loc, glen);
         if (!ok) {   // BaseAligner.cpp:1163-1185
@@ -354,7 +354,7 @@ __device__ __forceinline__ void lv_pass(const KArgs &A, Lds<128> &S, uint32_t i0
 // (stopOnFirstHit).  GS is a template parameter so group indexing is shifts and the
 // per-group loops unroll.
 template <int GS>
-__device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<128> &S, Elem *ar, ReadState &st, uint32_t i0, int m,
+__device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<128> &S, Elem128 *ar, ReadState &st, uint32_t i0, int m,
                                            int k, uint32_t n, uint32_t nb, uint32_t &lastSlot, bool &lastSkip,
                                            int *result) {
     const int lane = lane_id();
@@ -517,7 +517,7 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<128> &S, Elem *ar
 }
 
 // BaseAligner::score (BaseAligner.cpp:977-1399) over batches of popped elements.
-__device__ __forceinline__ bool score_batched(const KArgs &A, Lds<128> &S, Elem *ar, ReadState &st, bool force,
+__device__ __forceinline__ bool score_batched(const KArgs &A, Lds<128> &S, Elem128 *ar, ReadState &st, bool force,
                                            uint32_t n, int *result, uint32_t *flags) {
     const int lane = lane_id();
     GroupLds &G = S.grp[0];
@@ -593,18 +593,19 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<128> &S, Elem 
         PH_T(A, tfe);
         // ---- fetch the batch from the arena in one round trip
         {
-            constexpr int NLD = (EB * ELEM_DWORDS + WAVE - 1) / WAVE;
-            const uint32_t tot = nb * ELEM_DWORDS;
+            constexpr int ED = Elem128::DWORDS;
+            constexpr int NLD = (EB * ED + WAVE - 1) / WAVE;
+            const uint32_t tot = nb * ED;
             uint32_t v[NLD];
 #pragma unroll
             for (int j = 0; j < NLD; j++) {
                 const uint32_t idx = (uint32_t)(j * WAVE + lane);
-                v[j] = idx < tot ? ((const uint32_t *)(ar + G.eidx[idx / ELEM_DWORDS]))[idx % ELEM_DWORDS] : 0u;
+                v[j] = idx < tot ? ((const uint32_t *)(ar + G.eidx[idx / ED]))[idx % ED] : 0u;
             }
 #pragma unroll
             for (int j = 0; j < NLD; j++) {
                 const uint32_t idx = (uint32_t)(j * WAVE + lane);
-                if (idx < tot) G.ecache[idx / ELEM_DWORDS][idx % ELEM_DWORDS] = v[j];
+                if (idx < tot) G.ecache[idx / ED][idx % ED] = v[j];
             }
             wave_sync();
         }

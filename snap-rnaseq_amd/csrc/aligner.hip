@@ -8,6 +8,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "align_device.h"
@@ -22,7 +23,7 @@ namespace sgk {
 // BaseAligner::score, BaseAligner.cpp:977-1399.  Returns true iff a final
 // result was produced (written into st / *result).
 template <int MAXLEN>
-__device__ __forceinline__ bool score_wave(const KArgs &A, Lds<MAXLEN> &S, Elem *ar, ReadState &st, bool force,
+__device__ __forceinline__ bool score_wave(const KArgs &A, Lds<MAXLEN> &S, Elem512 *ar, ReadState &st, bool force,
                                            uint32_t n, const uint32_t (&rbF)[MAXLEN / 64],
                                            const uint32_t (&rbR)[MAXLEN / 64], int *result, uint32_t *flags) {
     constexpr int NB = MAXLEN / 64;
@@ -199,7 +200,7 @@ __device__ __forceinline__ bool score_wave(const KArgs &A, Lds<MAXLEN> &S, Elem 
 // The per-hit loop of BaseAligner.cpp:829-869 (findCandidate / incrementWeight /
 // allocateNewCandidate) for one seed in one direction.
 template <int MAXLEN>
-__device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem *ar, ReadState &st, uint32_t dir,
+__device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, ElemOf<MAXLEN> *ar, ReadState &st, uint32_t dir,
                                             uint32_t offset, uint32_t lim, const uint32_t *list, uint32_t single,
                                             uint32_t numWeightLists, uint32_t lpsNow) {
     const int lane = lane_id();
@@ -249,7 +250,7 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
                     if (e == NONE) {
                         // allocateNewCandidate (BaseAligner.cpp:1485-1568): tail of weight list 1
                         e = atomicAdd(&S.nElems, 1u);
-                        Elem *ne = ar + e;
+                        auto *ne = ar + e;
                         ne->key = key;
                         ne->scored = 0;
                         ne->lps = (uint8_t)lpsNow;
@@ -271,7 +272,7 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
                             sortkey = (weight << 24) | (0xffffffu - t);
                         }
                     }
-                    ar[e].seedOffset[bit] = (uint16_t)offset;
+                    ar[e].seedOffset[bit] = (std::remove_reference_t<decltype(ar[e].seedOffset[0])>)offset;
                 }
                 ar[e].used = used;
                 ar[e].weight = (uint8_t)weight;
@@ -292,7 +293,7 @@ __device__ __forceinline__ void defer_read(const KArgs &A, uint32_t r) {
 
 // ------------------------------------------------------------- AlignRead
 template <int MAXLEN>
-__device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, Elem *ar, uint32_t r) {
+__device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf<MAXLEN> *ar, uint32_t r) {
     constexpr int NB = MAXLEN / 64;
     const int lane = lane_id();
     PH_T(A, tsetup);
@@ -526,7 +527,7 @@ template <int MAXLEN>
 // are cheaper than dropping to 2 waves/SIMD.
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void align_kernel(KArgs A) {
     __shared__ Lds<MAXLEN> S;
-    Elem *ar = A.arena + (uint64_t)blockIdx.x * A.arenaElems;
+    ElemOf<MAXLEN> *ar = reinterpret_cast<ElemOf<MAXLEN> *>(A.arena) + (uint64_t)blockIdx.x * A.arenaElems;
     const int lane = lane_id();
     const uint32_t total = A.readList ? uni(*A.deferCount) : A.nReads;
     for (;;) {
@@ -675,7 +676,7 @@ struct snapgpu_aligner {
     uint4 *dGPlanes = nullptr;    // genome bit planes (KArgs::gpl)
     const char *dGenome = nullptr;
     DevTables *dTab = nullptr;
-    Elem *dArena = nullptr;
+    void *dArena = nullptr;
     uint64_t arenaElems = 0;
     int grid = 0, grid512 = 0;
     hipEvent_t ev[4] = {};
@@ -808,8 +809,8 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
                                               : (uint32_t)(params->maxSeedCoverage * params->maxReadSize / idx->seedLen);
     a->arenaElems = (uint64_t)(maxSeeds + 2) * params->maxHitsToConsider + 64;
     const uint64_t budget = 24ull << 30;   // HBM for arenas
-    while (a->grid > 64 && (uint64_t)a->grid * a->arenaElems * sizeof(Elem) > budget) a->grid /= 2;
-    if ((e = hipMalloc(&a->dArena, (uint64_t)a->grid * a->arenaElems * sizeof(Elem))) != hipSuccess) return fail("arena", e);
+    while (a->grid > 64 && (uint64_t)a->grid * a->arenaElems * sizeof(Elem512) > budget) a->grid /= 2;
+    if ((e = hipMalloc(&a->dArena, (uint64_t)a->grid * a->arenaElems * sizeof(Elem512))) != hipSuccess) return fail("arena", e);
     int perCU512 = 0;   // pass 2 (deferred reads) reuses the arenas of the first a->grid blocks
     hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU512, (const void *)align_kernel<512>, 64, 0);
     if (perCU512 <= 0) perCU512 = 4;
