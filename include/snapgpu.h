@@ -250,6 +250,7 @@ typedef struct snapgpu_timing {
     double fixupMs;          /* host MAPQ fix-ups */
     uint64_t nSpilled;       /* reads deferred to pass 2 */
     uint64_t nMapqFixed;
+    double lookupKernelMs;   /* pass 0: seed_lookup_kernel (first-round seed lookups) */
 } snapgpu_timing_t;
 int snapgpu_last_timing(snapgpu_aligner_t *a, snapgpu_timing_t *t);
 

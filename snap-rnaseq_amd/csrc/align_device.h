@@ -111,6 +111,7 @@ struct KArgs {
     uint32_t *deferList;         // pass 1 appends read indices here
     uint32_t *deferCount;        // pass 1: atomic append count; pass 2: number of reads
     const uint32_t *readList;    // pass 2: read indices (nullptr in pass 1)
+    const uint4 *seedRecs;       // seed_lookup_kernel records (SeedRec, 8 per read), or nullptr
     unsigned long long *phaseBuf;   // diagnostic (SNAPGPU_PHASES=1): per-block [PH_SLOTS] cycle sums, else null
 };
 

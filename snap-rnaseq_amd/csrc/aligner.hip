@@ -13,6 +13,7 @@
 
 #include "align_device.h"
 #include "align_score.h"
+#include "seed_lookup.h"
 #include "internal.h"
 
 using namespace sgk;
@@ -383,6 +384,12 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
         if (lane <= NB) seedUsed[lane] = 0;
         wave_sync();
         uint32_t next = 0, wrapCount = 0;
+        // first-round lookups resolved by seed_lookup_kernel: lane 4k+f holds field f of record k
+        uint32_t srec = 0, pfIdx = SEEDS_PER_READ;
+        if (MAXLEN == 128 && A.seedRecs && A.maxHits < 0xffffu) {
+            srec = ((const uint32_t *)(A.seedRecs + (uint64_t)r * SEEDS_PER_READ))[lane & 31];
+            pfIdx = 0;
+        }
         // One call site for the scorer (it is large): `force` marks the final scoring
         // pass after the seed loop ends (BaseAligner.cpp:707-723, 879-891).
         const uint32_t seedGuard = (nPossible + 2) * (seedLen + 2) + maxSeeds;
@@ -412,6 +419,21 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
                     seedUsed[next >> 6] = w;
                     wave_sync();
                 }
+                bool found = false, comp = false, pal = false, pre = false;
+                uint32_t v1 = 0, v2 = 0, pcnt = 0;
+                if (pfIdx < (uint32_t)SEEDS_PER_READ) {
+                    const uint32_t meta = readlaneu(srec, 4 * pfIdx);
+                    pre = (meta >> 31) && (meta & 0xff) == next && ((meta >> 16) & 0x7fff) != 0x7fff;
+                    if (pre) {
+                        found = (meta >> 8) & 1; comp = (meta >> 9) & 1; pal = (meta >> 10) & 1;
+                        st.nProbes += (meta >> 16) & 0x7fff;
+                        v1 = readlaneu(srec, 4 * pfIdx + 1);
+                        v2 = readlaneu(srec, 4 * pfIdx + 2);
+                        pcnt = readlaneu(srec, 4 * pfIdx + 3);
+                        pfIdx++;
+                    }
+                }
+                if (!pre) {
                 // Seed::DoesTextRepresentASeed + Seed::Seed (Seed.cpp:28-42, Seed.h:38-51)
                 int v = lane < (int)seedLen ? base_value((uint8_t)S.fwd[next + lane]) : 0;
                 if (ballot(lane < (int)seedLen && v > 3)) continue;
@@ -420,15 +442,14 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
                 const uint64_t f = uni64(or_reduce64(fpart));
                 const uint64_t rcv = uni64(or_reduce64(rpart));
                 // GenomeIndex::lookupSeed + SNAPHashTable::Lookup
-                const bool comp = (int64_t)f > (int64_t)rcv;
+                comp = (int64_t)f > (int64_t)rcv;
+                pal = f == rcv;
                 const uint64_t canon = comp ? rcv : f;
                 const uint32_t table = (uint32_t)(canon >> 32);
                 const uint32_t key = (uint32_t)canon;
                 const uint64_t size = A.tableSize[table];
                 const uint32_t *T = A.slots + 3 * A.tableBase[table];
                 const uint64_t h0 = fmix32(key) % size;
-                bool found = false;
-                uint32_t v1 = 0, v2 = 0;
                 for (uint32_t j0 = 0;; j0 += 8) {
                     uint32_t j = j0 + (lane & 7);
                     uint64_t S_j = j <= 4 ? (uint64_t)j * (j + 1) * (2 * j + 1) / 6 : 30 + (uint64_t)(j - 4);
@@ -448,6 +469,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
                         break;
                     }
                 }
+                }
                 if (overdue(st, 6)) break;
                 // fillInLookedUpResults (GenomeIndex.cpp:1013-1086), both directions
                 uint32_t nH0 = 0, nH1 = 0, sg0 = 0, sg1 = 0;
@@ -455,10 +477,20 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
                 if (found) {
                     uint32_t vf = comp ? v2 : v1, vr = comp ? v1 : v2;
                     if (vf < A.nBases) { nH0 = 1; sg0 = vf; }
-                    else if (vf != UNUSED_SIDE) { uint32_t o = vf - A.nBases; nH0 = uni(A.overflow[o]); ls0 = A.overflow + o + 1; st.nOvf++; }
-                    if (f == rcv) { nH1 = nH0; sg1 = sg0; ls1 = ls0; }   // palindrome (GenomeIndex.cpp:1003-1006)
+                    else if (vf != UNUSED_SIDE) {
+                        uint32_t o = vf - A.nBases;
+                        nH0 = pre ? (pcnt & 0xffff) : uni(A.overflow[o]);
+                        ls0 = A.overflow + o + 1;
+                        st.nOvf++;
+                    }
+                    if (pal) { nH1 = nH0; sg1 = sg0; ls1 = ls0; }   // palindrome (GenomeIndex.cpp:1003-1006)
                     else if (vr < A.nBases) { nH1 = 1; sg1 = vr; }
-                    else if (vr != UNUSED_SIDE) { uint32_t o = vr - A.nBases; nH1 = uni(A.overflow[o]); ls1 = A.overflow + o + 1; st.nOvf++; }
+                    else if (vr != UNUSED_SIDE) {
+                        uint32_t o = vr - A.nBases;
+                        nH1 = pre ? (pcnt >> 16) : uni(A.overflow[o]);
+                        ls1 = A.overflow + o + 1;
+                        st.nOvf++;
+                    }
                 }
                 st.nLookups++;
                 PH_ADD(A, S, PH_LOOKUP, tlk);
@@ -660,6 +692,7 @@ struct snapgpu_device_reads {
     uint32_t *dLengths = nullptr;
     snapgpu_result_t *dOut = nullptr;
     uint32_t *dDefer = nullptr;   // pass 1 -> pass 2 read list
+    SeedRec *dSeeds = nullptr;    // seed_lookup_kernel records, SEEDS_PER_READ per read
     uint64_t n = 0;
     uint32_t maxLen = 0;
     int device = 0;
@@ -844,6 +877,7 @@ snapgpu_device_reads_t *snapgpu_reads_upload(snapgpu_aligner_t *a, const snapgpu
     HIPCHKN(hipMalloc(&d->dLengths, (r->n + 1) * 4));
     HIPCHKN(hipMalloc(&d->dOut, (r->n + 1) * sizeof(snapgpu_result_t)));
     HIPCHKN(hipMalloc(&d->dDefer, (r->n + 1) * sizeof(uint32_t)));
+    HIPCHKN(hipMalloc(&d->dSeeds, (r->n + 8) * SEEDS_PER_READ * sizeof(SeedRec)));
     HIPCHKN(hipMemsetAsync(d->dBases, 0, bytes, a->stream));
     HIPCHKN(hipMemsetAsync(d->dQuals, 0, bytes, a->stream));
     HIPCHKN(hipMemcpyAsync(d->dBases, r->bases, bytes - 64, hipMemcpyHostToDevice, a->stream));
@@ -858,7 +892,7 @@ void snapgpu_device_reads_free(snapgpu_device_reads_t *d) {
     if (!d) return;
     hipSetDevice(d->device);
     hipFree(d->dBases); hipFree(d->dQuals); hipFree(d->dOffsets); hipFree(d->dLengths); hipFree(d->dOut);
-    hipFree(d->dDefer);
+    hipFree(d->dDefer); hipFree(d->dSeeds);
     delete d;
 }
 
@@ -890,6 +924,12 @@ int snapgpu_align_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d) {
     (void)hipGetLastError();   // clear any stale error of an unrelated earlier runtime call
     HIPCHK(hipMemsetAsync(a->dCounter, 0, 64, a->stream));
     HIPCHK(hipMemsetAsync(a->dDiag, 0, sizeof(uint32_t) * 4, a->stream));
+    // pass 0: first-round seed lookups of every read (8 reads per 64-lane block)
+    A.seedRecs = nullptr;
+    HIPCHK(hipEventRecord(a->ev[3], a->stream));
+    hipLaunchKernelGGL(seed_lookup_kernel, dim3((unsigned)((d->n + 7) / 8)), dim3(64), 0, a->stream, A, d->dSeeds);
+    HIPCHK(hipGetLastError());
+    A.seedRecs = reinterpret_cast<const uint4 *>(d->dSeeds);
     HIPCHK(hipEventRecord(a->ev[0], a->stream));
     hipLaunchKernelGGL(align_kernel<128>, dim3(grid), dim3(64), 0, a->stream, A);
     HIPCHK(hipGetLastError());
@@ -898,6 +938,7 @@ int snapgpu_align_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d) {
     KArgs B = A;
     B.counter = a->dCounter + 1;
     B.readList = d->dDefer;
+    B.seedRecs = nullptr;
     int grid2 = a->grid512;
     if ((uint64_t)grid2 > d->n) grid2 = (int)d->n;
     hipLaunchKernelGGL(align_kernel<512>, dim3(grid2), dim3(64), 0, a->stream, B);
@@ -931,6 +972,8 @@ int snapgpu_synchronize(snapgpu_aligner_t *a) {
         a->timing.mainKernelMs = ms;
         HIPCHK(hipEventElapsedTime(&ms, a->ev[1], a->ev[2]));
         a->timing.spillKernelMs = ms;
+        HIPCHK(hipEventElapsedTime(&ms, a->ev[3], a->ev[0]));
+        a->timing.lookupKernelMs = ms;
         uint32_t cnt[4];
         HIPCHK(hipMemcpy(cnt, a->dCounter, sizeof(cnt), hipMemcpyDeviceToHost));
         a->timing.nSpilled = cnt[2];

@@ -1,0 +1,147 @@
+// seed_lookup.h -- first-round seed lookups of every read, resolved up front.
+//
+// In BaseAligner::AlignRead the seed offsets tried first are 0, seedLen, 2*seedLen,
+// ... (a seed containing a non-ACGT base is skipped and the next one starts one base
+// later; BaseAligner.cpp:686-746): they depend only on the read's bases, not on any
+// lookup result.  seed_lookup_kernel resolves GenomeIndex::lookupSeed
+// (GenomeIndex.cpp:971-1086, SNAPHashTable::Lookup HashTable.h:74-105) for those
+// seeds of every read <= 128 bases, one lane per (read, seed): 8 reads per wave,
+// thousands of independent probe chains in flight, so the hash-table gather runs at
+// memory throughput instead of as ~3 dependent HBM round trips inside each read's
+// sequential aligner.  align_kernel<128> consumes the records when its seed loop
+// reaches the same offset and counts probes / overflow lists exactly as before.
+#pragma once
+#include "align_device.h"
+
+namespace sgk {
+
+// 16 bytes per (read, first-round seed k < 8)
+struct SeedRec {
+    uint32_t meta;      // bit31 valid, [7:0] offset, bit8 found, bit9 comp, bit10 palindrome, [30:16] probes
+    uint32_t v1, v2;    // slot values (GenomeIndex.cpp:1004-1010 swaps them when comp)
+    uint32_t cnt;       // overflow counts, u16 each, saturated: [15:0] value1 side, [31:16] value2 side
+};
+constexpr int SEEDS_PER_READ = 8;
+
+// bits [p, p+len) of a 128-bit value (len <= 32)
+__device__ __forceinline__ uint32_t win128(uint64_t lo, uint64_t hi, int p, int len) {
+    uint64_t w;
+    if (p == 0) w = lo;
+    else if (p < 64) w = (lo >> p) | (hi << (64 - p));
+    else w = hi >> (p - 64);
+    return (uint32_t)w & (uint32_t)((1ull << len) - 1);
+}
+// bit i -> bit 2i
+__device__ __forceinline__ uint64_t spread2(uint32_t x32) {
+    uint64_t x = x32;
+    x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
+    x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
+    x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
+    x = (x | (x << 2)) & 0x3333333333333333ull;
+    x = (x | (x << 1)) & 0x5555555555555555ull;
+    return x;
+}
+
+__global__ __launch_bounds__(64) void seed_lookup_kernel(KArgs A, SeedRec *out) {
+    const int lane = lane_id();
+    const uint32_t r = blockIdx.x * 8 + (lane >> 3);
+    const int k = lane & 7;
+    const bool have = r < A.nReads;
+    const uint32_t n = have ? A.lengths[r] : 0;
+    const uint64_t off = have ? A.offsets[r] : 0;
+    const int L = (int)A.seedLen;
+    // 16 bases per lane (read buffer carries >= 64 bytes of slack past the last read)
+    uint64_t chunk = 0;   // [15:0] bit0 of the seed code, [31:16] bit1, [47:32] not-ACGT / past the end
+    {
+        const uint64_t b0 = off + 16 * (uint64_t)k;
+        const uint32_t *src = (const uint32_t *)(A.bases + (b0 & ~3ull));
+        const uint32_t sh = (uint32_t)(b0 & 3) * 8;
+        uint32_t w[5];
+#pragma unroll
+        for (int i = 0; i < 5; i++) w[i] = have && n > 16u * k ? src[i] : 0u;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t d = __builtin_amdgcn_alignbit(w[i + 1], w[i], sh);
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                uint32_t c = (d >> (8 * b)) & 0xff;
+                if (c >= 'a' && c <= 'z') c -= 0x20;   // Read::init upper-cases (Read.h:289-328)
+                const int pos = 16 * k + 4 * i + b;
+                const int v = base_value(c);            // Seed encoding A0 G1 C2 T3 (Tables.cpp:41-48)
+                const bool inv = pos >= (int)n || v > 3;
+                const int bit = 4 * i + b;
+                if (!inv) chunk |= ((uint64_t)(v & 1) << bit) | ((uint64_t)(v >> 1) << (16 + bit));
+                else chunk |= 1ull << (32 + bit);
+            }
+        }
+    }
+    // the read's full 128-position planes in every lane of its group
+    uint64_t P0[2] = {0, 0}, P1[2] = {0, 0}, IV[2] = {0, 0};
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const int src = (lane & ~7) + j;
+        const uint32_t lo = (uint32_t)shfl_idx((int)(uint32_t)chunk, src);
+        const uint32_t hi = (uint32_t)shfl_idx((int)(uint32_t)(chunk >> 32), src);
+        const int wd = j >> 2, s = 16 * (j & 3);
+        P0[wd] |= (uint64_t)(lo & 0xffff) << s;
+        P1[wd] |= (uint64_t)(lo >> 16) << s;
+        IV[wd] |= (uint64_t)(hi & 0xffff) << s;
+    }
+    SeedRec rec = {0u, 0u, 0u, 0u};
+    if (have && n <= 128 && (int)n >= L) {
+        // k-th first-round seed offset
+        const int nPossible = (int)n - L + 1;
+        int p = 0, idx = 0, my = -1;
+        while (p < nPossible) {
+            if (win128(IV[0], IV[1], p, L)) { p++; continue; }   // BaseAligner.cpp:740-744
+            if (idx == k) { my = p; break; }
+            idx++;
+            p += L;
+        }
+        if (my >= 0) {
+            const uint32_t w0 = win128(P0[0], P0[1], my, L), w1 = win128(P1[0], P1[1], my, L);
+            const uint32_t M = (uint32_t)((1ull << L) - 1);
+            // Seed.h:38-51: first base most significant; reverse complement = reverse of code ^ 3
+            const uint32_t r0 = __builtin_bitreverse32(w0) >> (32 - L), r1 = __builtin_bitreverse32(w1) >> (32 - L);
+            const uint64_t f = (spread2(r1) << 1) | spread2(r0);
+            const uint64_t rcv = (spread2(~w1 & M) << 1) | spread2(~w0 & M);
+            const bool comp = (int64_t)f > (int64_t)rcv;
+            const uint64_t canon = comp ? rcv : f;
+            const uint32_t table = (uint32_t)(canon >> 32);
+            const uint32_t key = (uint32_t)canon;
+            const uint64_t size = A.tableSize[table];
+            const uint32_t *T = A.slots + 3 * A.tableBase[table];
+            const uint64_t h0 = fmix32(key) % size;
+            bool found = false;
+            uint32_t v1 = 0, v2 = 0, probes = 0;
+            for (uint32_t j = 0;; j++) {   // SNAPHashTable::Lookup probe order
+                if (j > size + 5) { probes = j; break; }
+                const uint64_t S_j = j <= 4 ? (uint64_t)j * (j + 1) * (2 * j + 1) / 6 : 30 + (uint64_t)(j - 4);
+                const uint64_t pos = (h0 + S_j) % size;
+                const uint32_t kj = T[3 * pos], v1j = T[3 * pos + 1];
+                const bool stop = (j == 0) ? (kj == key && v1j != INVALID) : (kj == key || v1j == INVALID);
+                if (stop) {
+                    probes = j + 1;
+                    if (j == 0 || v1j != INVALID) { found = true; v1 = v1j; v2 = T[3 * pos + 2]; }
+                    break;
+                }
+            }
+            uint32_t cnt = 0;
+            if (found) {   // overflow list lengths (GenomeIndex.cpp:1013-1086)
+                const uint32_t vf = comp ? v2 : v1, vr = comp ? v1 : v2;
+                uint32_t cf = 0, cr = 0;
+                if (vf >= A.nBases && vf != UNUSED_SIDE) cf = A.overflow[vf - A.nBases];
+                if (f != rcv && vr >= A.nBases && vr != UNUSED_SIDE) cr = A.overflow[vr - A.nBases];
+                cnt = (cf < 0xffffu ? cf : 0xffffu) | ((cr < 0xffffu ? cr : 0xffffu) << 16);
+            }
+            rec.meta = 0x80000000u | (uint32_t)my | (found ? 0x100u : 0u) | (comp ? 0x200u : 0u) |
+                       (f == rcv ? 0x400u : 0u) | ((probes < 0x7fffu ? probes : 0x7fffu) << 16);
+            rec.v1 = v1;
+            rec.v2 = v2;
+            rec.cnt = cnt;
+        }
+    }
+    if (have) out[(uint64_t)r * SEEDS_PER_READ + k] = rec;
+}
+
+}  // namespace sgk

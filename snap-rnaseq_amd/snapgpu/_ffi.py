@@ -128,6 +128,7 @@ class Timing(C.Structure):
         ("fixupMs", C.c_double),
         ("nSpilled", C.c_uint64),
         ("nMapqFixed", C.c_uint64),
+        ("lookupKernelMs", C.c_double),
     ]
 
 
