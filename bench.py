@@ -123,12 +123,14 @@ def main():
     for _ in range(args.warmup):
         dev.run()
         dev.synchronize()
-    kernel_ms = []
+    kernel_ms, lookup_ms = [], []
 
     def step():
         dev.run()
         dev.synchronize()
-        kernel_ms.append(aligner.timing()["mainKernelMs"])
+        t = aligner.timing()
+        kernel_ms.append(t["mainKernelMs"])
+        lookup_ms.append(t["lookupKernelMs"])
 
     elapsed = timed_steps(step, args.steps, dist, dev.synchronize)
     res = dev.results()
@@ -142,6 +144,16 @@ def main():
         avg_kernel_s = float(np.mean(kernel_ms)) / 1000.0
         achieved = bytes_launch / avg_kernel_s / 1e9
         traffic = load_pmc_traffic()
+        # seed_lookup_kernel (pass 0): read bytes + offsets/lengths + 8 records of 16 B per read,
+        # then per looked-up seed its table's (size, base), 12 B per probed entry, 4 B per overflow count
+        t = aligner.timing()
+        lk_bytes = int(int(res["nLookups"].size) * (READ_LEN + 12 + 128) + 16 * t["lookupSeeds"] +
+                       12 * t["lookupProbes"] + 4 * t["lookupOverflowReads"])
+        lk_s = float(np.mean(lookup_ms)) / 1000.0
+        lookup = {"kernel": "seed_lookup_kernel", "kernel_ms": lk_s * 1000.0,
+                  "achieved": lk_bytes / lk_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                  "frac": lk_bytes / lk_s / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": lk_bytes,
+                  "seeds": int(t["lookupSeeds"]), "probes": int(t["lookupProbes"])}
         counts = {int(k): int(v) for k, v in zip(*np.unique(res["result"], return_counts=True))}
         cpu = None
         parity = None
@@ -183,6 +195,7 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "align_kernel<128>", "kernel_ms": float(np.mean(kernel_ms)),
                          "algorithmic_bytes_per_launch": bytes_launch},
+            "lookup_roofline": lookup,
             "cpu_baseline": cpu,
             "parity": parity,
         }

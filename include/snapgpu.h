@@ -251,6 +251,9 @@ typedef struct snapgpu_timing {
     uint64_t nSpilled;       /* reads deferred to pass 2 */
     uint64_t nMapqFixed;
     double lookupKernelMs;   /* pass 0: seed_lookup_kernel (first-round seed lookups) */
+    uint64_t lookupSeeds;    /* seeds it looked up */
+    uint64_t lookupProbes;   /* hash-table entries it probed */
+    uint64_t lookupOverflowReads; /* overflow-list counts it read */
 } snapgpu_timing_t;
 int snapgpu_last_timing(snapgpu_aligner_t *a, snapgpu_timing_t *t);
 

@@ -719,6 +719,7 @@ struct snapgpu_aligner {
     bool pendingTiming = false;
     uint32_t *dDiag = nullptr;    // g_diag (watchdog record)
     unsigned long long *dPhase = nullptr;   // [grid][PH_SLOTS] (SNAPGPU_PHASES=1 diagnostics)
+    unsigned long long *dLookupStats = nullptr;   // seed_lookup_kernel: seeds, probes, overflow counts
     double timeoutSec = 0;        // SNAPGPU_TIMEOUT_S
 };
 
@@ -751,7 +752,7 @@ void snapgpu_aligner_free(snapgpu_aligner_t *a) {
     hipSetDevice(a->device);
     hipFree(a->dSlots); hipFree(a->dOverflow); hipFree(a->dPieces); hipFree(a->dCounter);
     hipFree(a->dTableBase); hipFree(a->dTableSize); hipFree(a->dGenomeAlloc); hipFree(a->dTab); hipFree(a->dArena);
-    hipFree(a->dGPlanes); hipFree(a->dPhase);
+    hipFree(a->dGPlanes); hipFree(a->dPhase); hipFree(a->dLookupStats);
     for (auto &e : a->ev) if (e) hipEventDestroy(e);
     if (a->stream) hipStreamDestroy(a->stream);
     delete a;
@@ -831,6 +832,7 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
     if ((e = hipMalloc(&a->dTab, sizeof(DevTables))) != hipSuccess) return fail("tables", e);
     hipMemcpy(a->dTab, &t, sizeof(t), hipMemcpyHostToDevice);
     if ((e = hipMalloc(&a->dCounter, 64)) != hipSuccess) return fail("counter", e);
+    if ((e = hipMalloc(&a->dLookupStats, 1024 * sizeof(unsigned long long))) != hipSuccess) return fail("lookup stats", e);
     // persistent grid: waves resident on the device; element arena per wave
     hipDeviceProp_t prop;
     hipGetDeviceProperties(&prop, device);
@@ -927,7 +929,9 @@ int snapgpu_align_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d) {
     // pass 0: first-round seed lookups of every read (8 reads per 64-lane block)
     A.seedRecs = nullptr;
     HIPCHK(hipEventRecord(a->ev[3], a->stream));
-    hipLaunchKernelGGL(seed_lookup_kernel, dim3((unsigned)((d->n + 7) / 8)), dim3(64), 0, a->stream, A, d->dSeeds);
+    HIPCHK(hipMemsetAsync(a->dLookupStats, 0, 1024 * sizeof(unsigned long long), a->stream));
+    hipLaunchKernelGGL(seed_lookup_kernel, dim3((unsigned)((d->n + 7) / 8)), dim3(64), 0, a->stream, A, d->dSeeds,
+                       a->dLookupStats);
     HIPCHK(hipGetLastError());
     A.seedRecs = reinterpret_cast<const uint4 *>(d->dSeeds);
     HIPCHK(hipEventRecord(a->ev[0], a->stream));
@@ -977,6 +981,14 @@ int snapgpu_synchronize(snapgpu_aligner_t *a) {
         uint32_t cnt[4];
         HIPCHK(hipMemcpy(cnt, a->dCounter, sizeof(cnt), hipMemcpyDeviceToHost));
         a->timing.nSpilled = cnt[2];
+        std::vector<unsigned long long> ls(1024);
+        HIPCHK(hipMemcpy(ls.data(), a->dLookupStats, 1024 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        a->timing.lookupSeeds = a->timing.lookupProbes = a->timing.lookupOverflowReads = 0;
+        for (int i = 0; i < 256; i++) {
+            a->timing.lookupSeeds += ls[4 * i];
+            a->timing.lookupProbes += ls[4 * i + 1];
+            a->timing.lookupOverflowReads += ls[4 * i + 2];
+        }
         a->pendingTiming = false;
         uint32_t diag[4];
         HIPCHK(hipMemcpy(diag, a->dDiag, sizeof(diag), hipMemcpyDeviceToHost));

@@ -42,7 +42,9 @@ __device__ __forceinline__ uint64_t spread2(uint32_t x32) {
     return x;
 }
 
-__global__ __launch_bounds__(64) void seed_lookup_kernel(KArgs A, SeedRec *out) {
+// stats[4*slot + 0..2] += seeds looked up, hash entries probed, overflow counts read (roofline
+// bytes); slot = block % 256
+__global__ __launch_bounds__(64) void seed_lookup_kernel(KArgs A, SeedRec *out, unsigned long long *stats) {
     const int lane = lane_id();
     const uint32_t r = blockIdx.x * 8 + (lane >> 3);
     const int k = lane & 7;
@@ -88,6 +90,7 @@ __global__ __launch_bounds__(64) void seed_lookup_kernel(KArgs A, SeedRec *out) 
         IV[wd] |= (uint64_t)(hi & 0xffff) << s;
     }
     SeedRec rec = {0u, 0u, 0u, 0u};
+    uint32_t nSeed = 0, nProbe = 0, nOvfRead = 0;
     if (have && n <= 128 && (int)n >= L) {
         // k-th first-round seed offset
         const int nPossible = (int)n - L + 1;
@@ -127,11 +130,13 @@ __global__ __launch_bounds__(64) void seed_lookup_kernel(KArgs A, SeedRec *out) 
                 }
             }
             uint32_t cnt = 0;
+            nSeed = 1;
+            nProbe = probes;
             if (found) {   // overflow list lengths (GenomeIndex.cpp:1013-1086)
                 const uint32_t vf = comp ? v2 : v1, vr = comp ? v1 : v2;
                 uint32_t cf = 0, cr = 0;
-                if (vf >= A.nBases && vf != UNUSED_SIDE) cf = A.overflow[vf - A.nBases];
-                if (f != rcv && vr >= A.nBases && vr != UNUSED_SIDE) cr = A.overflow[vr - A.nBases];
+                if (vf >= A.nBases && vf != UNUSED_SIDE) { cf = A.overflow[vf - A.nBases]; nOvfRead++; }
+                if (f != rcv && vr >= A.nBases && vr != UNUSED_SIDE) { cr = A.overflow[vr - A.nBases]; nOvfRead++; }
                 cnt = (cf < 0xffffu ? cf : 0xffffu) | ((cr < 0xffffu ? cr : 0xffffu) << 16);
             }
             rec.meta = 0x80000000u | (uint32_t)my | (found ? 0x100u : 0u) | (comp ? 0x200u : 0u) |
@@ -142,6 +147,21 @@ __global__ __launch_bounds__(64) void seed_lookup_kernel(KArgs A, SeedRec *out) 
         }
     }
     if (have) out[(uint64_t)r * SEEDS_PER_READ + k] = rec;
+    if (stats) {
+        uint64_t v = (uint64_t)nProbe | ((uint64_t)nSeed << 32) | ((uint64_t)nOvfRead << 44);
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t lo = (uint32_t)shfl_idx((int)(uint32_t)v, lane ^ o);
+            const uint32_t hi = (uint32_t)shfl_idx((int)(uint32_t)(v >> 32), lane ^ o);
+            v += ((uint64_t)hi << 32) | lo;
+        }
+        if (lane == 0) {   // 256 slot groups: no single-address atomic hot spot
+            unsigned long long *st = stats + 4 * (blockIdx.x & 255);
+            atomicAdd(st + 0, (unsigned long long)((v >> 32) & 0xfff));
+            atomicAdd(st + 1, (unsigned long long)(v & 0xffffffffull));
+            atomicAdd(st + 2, (unsigned long long)(v >> 44));
+        }
+    }
 }
 
 }  // namespace sgk

@@ -129,6 +129,9 @@ class Timing(C.Structure):
         ("nSpilled", C.c_uint64),
         ("nMapqFixed", C.c_uint64),
         ("lookupKernelMs", C.c_double),
+        ("lookupSeeds", C.c_uint64),
+        ("lookupProbes", C.c_uint64),
+        ("lookupOverflowReads", C.c_uint64),
     ]
 
 
