@@ -232,6 +232,34 @@ void snapgpu_aligner_free(snapgpu_aligner_t *a);
  * buffers: H2D of the reads, the GPU passes, D2H of the records. */
 int snapgpu_align_batch(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, snapgpu_result_t *out);
 
+/* The extended AlignRead (BaseAligner.h:72-86, BaseAligner.cpp:510-938) used by the
+ * paired / transcriptome callers:
+ *  - per-read search window: searchRadius != 0 restricts hits to genome locations
+ *    within searchRadius of searchLocation, in searchDirection only (windowed
+ *    GenomeIndex::lookupSeed, GenomeIndex.cpp:1013-1086, and BaseAligner.cpp:781-853);
+ *  - multi-hit export (fillHitsFound, BaseAligner.cpp:940-975, recording at :1255-1261):
+ *    up to maxHitsToGet hits with edit distance in [best, best+3] per read, written to
+ *    multiHits[i * maxHitsToGet ..], their count to multiHitsFound[i].
+ * search may be NULL (no window for any read); maxHitsToGet 0 disables multi-hit
+ * export (multiHitsFound / multiHits may then be NULL); at most
+ * SNAPGPU_MAX_MULTI_HITS_TO_GET (BaseAligner.h:149). */
+#define SNAPGPU_MAX_MULTI_HITS_TO_GET 512
+typedef struct snapgpu_search {
+    uint32_t searchRadius;
+    uint32_t searchLocation;
+    uint32_t searchDirection;   /* SNAPGPU_FORWARD / SNAPGPU_RC */
+    uint32_t reserved;
+} snapgpu_search_t;
+typedef struct snapgpu_multi_hit {
+    uint32_t location;
+    uint8_t  direction;         /* multiHitRCs */
+    uint8_t  score;             /* multiHitScores */
+    uint16_t reserved;
+} snapgpu_multi_hit_t;
+int snapgpu_align_batch_ex(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, const snapgpu_search_t *search,
+                           uint32_t maxHitsToGet, snapgpu_result_t *out, int32_t *multiHitsFound,
+                           snapgpu_multi_hit_t *multiHits);
+
 /* Device-resident variant: reads are uploaded once with snapgpu_reads_upload;
  * snapgpu_align_resident runs only the GPU passes (inputs already in HBM, output
  * left in HBM); snapgpu_results_download copies the records back. */

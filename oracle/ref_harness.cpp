@@ -13,6 +13,7 @@
 //   align  <indexDir> <reads.fq> [maxHits maxK numSeeds extraSearchDepth]
 //          -> one TSV line per read:
 //             i result loc dir score mapq lookups scored popularSkipped pAll_hex pBest_hex
+//   alignx <indexDir> <reads.fq> <search.tsv> <maxHitsToGet> [...] -> align columns + multi hits
 //   lv     <calls.tsv>   lines: dir k text pattern quals   -> e netIndel prob_hex
 //   lookup <indexDir> <seeds.txt>  one seed string per line -> nF nRC sumF sumRC firstF firstRC
 #define private public          // read-only access to BaseAligner's private scoring state
@@ -69,6 +70,58 @@ static int mode_align(int argc, char **argv) {
     return 0;
 }
 
+// alignx <indexDir> <reads.fq> <search.tsv> <maxHitsToGet> [maxHits maxK numSeeds extra]
+//   search.tsv: one "radius location direction" line per read.  The richer AlignRead
+//   overload (BaseAligner.h:73-86): windowed search + multi-hit export.  Output = the
+//   align columns + nFound + "loc:dir:score,..." (or "-").
+static int mode_alignx(int argc, char **argv) {
+    if (argc < 6) { fprintf(stderr, "alignx <indexDir> <reads.fq> <search.tsv> <maxHitsToGet> [...]\n"); return 2; }
+    int maxGet = atoi(argv[5]);
+    unsigned maxHits = argc > 6 ? atoi(argv[6]) : 300;
+    unsigned maxK = argc > 7 ? atoi(argv[7]) : 14;
+    unsigned numSeeds = argc > 8 ? atoi(argv[8]) : 25;
+    unsigned extra = argc > 9 ? atoi(argv[9]) : 2;
+    initializeLVProbabilitiesToPhredPlus33();
+    GenomeIndex *idx = GenomeIndex::loadFromDirectory(argv[2]);
+    if (!idx) { fprintf(stderr, "cannot load index %s\n", argv[2]); return 1; }
+    BigAllocator *al = new BigAllocator(BaseAligner::getBigAllocatorReservation(
+        true, maxHits, MAX_READ_LENGTH, idx->getSeedLength(), numSeeds, 0));
+    BaseAligner *ba = new (al) BaseAligner(idx, maxHits, maxK, MAX_READ_LENGTH, numSeeds, 0, extra,
+                                           NULL, NULL, NULL, al);
+    std::ifstream in(argv[3]), sin(argv[4]);
+    std::string id, bases, plus, quals;
+    unsigned i = 0;
+    char b1[64], b2[64];
+    std::vector<unsigned> mLoc(maxGet > 0 ? maxGet : 1);
+    std::vector<int> mScore(mLoc.size());
+    bool *mRC = new bool[mLoc.size()];
+    while (std::getline(in, id) && std::getline(in, bases) && std::getline(in, plus) && std::getline(in, quals)) {
+        unsigned radius = 0, sloc = 0; int sdir = 0;
+        sin >> radius >> sloc >> sdir;
+        std::string b = bases + std::string(16, '\0');
+        std::string q = quals + std::string(16, '\0');
+        Read r;
+        r.init(id.c_str() + 1, (unsigned)id.size() - 1, b.c_str(), q.c_str(), (unsigned)bases.size());
+        unsigned loc = 0; Direction dir = 0; int score = 0, mapq = 0, found = -7;
+        _int64 l0 = ba->getNHashTableLookups(), s0 = ba->getLocationsScored();
+        ba->popularSeedsSkipped = 0;
+        ba->probabilityOfAllCandidates = 0; ba->probabilityOfBestCandidate = 0;
+        AlignmentResult res = ba->AlignRead(&r, &loc, &dir, &score, &mapq, radius, sloc, (Direction)sdir, maxGet,
+                                            &found, &mLoc[0], mRC, &mScore[0]);
+        hexd(ba->probabilityOfAllCandidates, b1);
+        hexd(ba->probabilityOfBestCandidate, b2);
+        printf("%u\t%d\t%u\t%d\t%d\t%d\t%lld\t%lld\t%u\t%s\t%s\t%d\t", i, (int)res, loc, dir, score, mapq,
+               (long long)(ba->getNHashTableLookups() - l0), (long long)(ba->getLocationsScored() - s0),
+               ba->popularSeedsSkipped, b1, b2, found);
+        if (found <= 0) printf("-");
+        for (int j = 0; j < found; j++) printf("%s%u:%d:%d", j ? "," : "", mLoc[j], (int)mRC[j], mScore[j]);
+        printf("\n");
+        i++;
+    }
+    delete[] mRC;
+    return 0;
+}
+
 static int mode_lv(int argc, char **argv) {
     if (argc < 3) { fprintf(stderr, "lv <calls.tsv>\n"); return 2; }
     initializeLVProbabilitiesToPhredPlus33();
@@ -120,6 +173,7 @@ int main(int argc, char **argv) {
     if (argc < 2) { fprintf(stderr, "usage: ref_harness align|lv|lookup ...\n"); return 2; }
     std::string m = argv[1];
     if (m == "align") return mode_align(argc, argv);
+    if (m == "alignx") return mode_alignx(argc, argv);
     if (m == "lv") return mode_lv(argc, argv);
     if (m == "lookup") return mode_lookup(argc, argv);
     fprintf(stderr, "unknown mode %s\n", argv[1]);

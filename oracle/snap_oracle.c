@@ -261,6 +261,11 @@ typedef struct {
     unsigned bestScore, bestLoc, scoreLimit, popular;
     double pAll, pBest;
     snapgpu_result_t *out;
+    /* multi-hit recording (BaseAligner.h:149-152) */
+    unsigned maxHitsToGet;
+    unsigned hitCount[MAX_K];
+    uint32_t *hitLoc;                 /* [MAX_K][maxHitsToGet] */
+    uint8_t *hitRC;
 } Oracle;
 
 static inline int base_value(char c) {   /* Tables.cpp:41-48 */
@@ -414,6 +419,12 @@ static int score(Oracle *o, int force, unsigned readLen, int *result) {
                         }
                     }
                 }
+                /* BaseAligner.cpp:1255-1261 */
+                if (o->maxHitsToGet > 0 && sc != 0xffffffffu && sc < MAX_K && o->hitCount[sc] < o->maxHitsToGet) {
+                    o->hitLoc[sc * o->maxHitsToGet + o->hitCount[sc]] = loc;
+                    o->hitRC[sc * o->maxHitsToGet + o->hitCount[sc]] = (uint8_t)el->dir;
+                    o->hitCount[sc]++;
+                }
                 out->nLocationsScored++;
                 if (anyNearby) {
                     if (el->bestScore < sc || (el->bestScore == sc && prob <= el->prob)) continue;
@@ -479,8 +490,51 @@ static unsigned wrapped_next_seed(unsigned seedLen, unsigned wrapCount) {
     return kWrap[seedLen - 16][wrapCount];
 }
 
-/* BaseAligner::AlignRead, BaseAligner.cpp:510-938 (searchRadius == 0, maxHitsToGet == 0) */
-static void align_read(Oracle *o, const char *bases, const char *quals, unsigned readLen, snapgpu_result_t *out) {
+/* BaseAligner::fillHitsFound, BaseAligner.cpp:940-975 */
+static void fill_hits(Oracle *o, int32_t *found, snapgpu_multi_hit_t *mh) {
+    if (o->maxHitsToGet == 0) return;
+    *found = 0;
+    unsigned first = 0;
+    while (first < MAX_K && o->hitCount[first] == 0) first++;
+    for (unsigned dist = first; dist < first + 4 && dist < MAX_K; dist++)
+        for (unsigned i = 0; i < o->hitCount[dist]; i++) {
+            mh[*found].location = o->hitLoc[dist * o->maxHitsToGet + i];
+            mh[*found].direction = o->hitRC[dist * o->maxHitsToGet + i];
+            mh[*found].score = (uint8_t)dist;
+            mh[*found].reserved = 0;
+            *found += 1;
+            if ((unsigned)*found == o->maxHitsToGet) return;
+        }
+}
+
+/* GenomeIndex::fillInLookedUpResults, GenomeIndex.cpp:1013-1086: the hits of one
+ * side in [minLoc, maxLoc] (overflow lists are sorted descending). */
+static void fill_side(const snapgpu_index_view_t *ix, uint32_t v, uint32_t minLoc, uint32_t maxLoc, uint32_t *single,
+                      unsigned *nHits, const uint32_t **hits, uint32_t *nOvf) {
+    if (v < ix->nBases) {
+        *single = v;
+        *nHits = (v >= minLoc && v <= maxLoc) ? 1 : 0;
+        *hits = single;
+    } else if (v == 0xfffffffeu) {
+        *nHits = 0;
+    } else {
+        const uint32_t off = v - ix->nBases;
+        const uint32_t cnt = ix->overflow[off];
+        const uint32_t *all = ix->overflow + off + 1;
+        (*nOvf)++;
+        if (minLoc == 0 && maxLoc == INVALID_LOC) { *nHits = cnt; *hits = all; return; }
+        unsigned lo = 0, hi = cnt;   /* first index with all[i] <= maxLoc */
+        while (lo < hi) { unsigned m = (lo + hi) / 2; if (all[m] <= maxLoc) hi = m; else lo = m + 1; }
+        unsigned end = lo;
+        while (end < cnt && all[end] >= minLoc) end++;
+        *nHits = end - lo;
+        *hits = all + lo;
+    }
+}
+
+/* BaseAligner::AlignRead, BaseAligner.cpp:510-938 */
+static void align_read(Oracle *o, const char *bases, const char *quals, unsigned readLen, snapgpu_result_t *out,
+                       const snapgpu_search_t *search, int32_t *multiFound, snapgpu_multi_hit_t *multiHits) {
     const snapgpu_index_view_t *ix = o->ix;
     const unsigned seedLen = ix->seedLen;
     memset(out, 0, sizeof(*out));
@@ -492,6 +546,14 @@ static void align_read(Oracle *o, const char *bases, const char *quals, unsigned
     out->score = (int)UNUSED_SCORE;
     o->popular = 0;
     o->pAll = o->pBest = 0;
+    if (o->maxHitsToGet > 0) { memset(o->hitCount, 0, sizeof(o->hitCount)); *multiFound = 0; }
+    /* search window, BaseAligner.cpp:596-602 */
+    const uint32_t radius = search ? search->searchRadius : 0;
+    uint32_t minLocation = 0, maxLocation = INVALID_LOC;
+    if (radius != 0) {
+        minLocation = search->searchLocation > radius ? search->searchLocation - radius : 0;
+        maxLocation = search->searchLocation < INVALID_LOC - radius ? search->searchLocation + radius : INVALID_LOC;
+    }
     if (readLen > o->p.maxReadSize) { out->flags |= SNAPGPU_FLAG_READ_TOO_LONG; out->result = SNAPGPU_NOT_FOUND; return; }
     if ((int)readLen < (int)seedLen) { out->result = SNAPGPU_NOT_FOUND; return; }
     /* Read::init upper-cases (Read.h:303-325); RC / reversed copies (BaseAligner.cpp:636-650) */
@@ -545,7 +607,9 @@ static void align_read(Oracle *o, const char *bases, const char *quals, unsigned
             r |= (uint64_t)(v ^ 3) << (i * 2);
         }
         if (!valid) continue;
-        /* GenomeIndex::lookupSeed, GenomeIndex.cpp:971-1011 */
+        /* GenomeIndex::lookupSeed, GenomeIndex.cpp:971-1011, windowed as BaseAligner.cpp:781-783 */
+        const uint32_t minSeedLoc = minLocation < readLen ? 0 : minLocation - readLen;
+        const uint32_t maxSeedLoc = maxLocation > INVALID_LOC - readLen ? INVALID_LOC : maxLocation + readLen;
         unsigned nHits[2] = {0, 0};
         const uint32_t *hits[2] = {NULL, NULL};
         uint32_t singleton[2];
@@ -556,19 +620,14 @@ static void align_read(Oracle *o, const char *bases, const char *quals, unsigned
             for (int side = 0; side < 2; side++) {
                 uint32_t v = (side == 0) == !comp ? e[0] : e[1];   /* fwd: value1 unless complemented */
                 if (side == 1 && f == r) { nHits[1] = nHits[0]; hits[1] = hits[0]; break; }
-                if (v < ix->nBases) { singleton[side] = v; nHits[side] = 1; hits[side] = &singleton[side]; }
-                else if (v == 0xfffffffeu) nHits[side] = 0;
-                else {
-                    uint32_t off = v - ix->nBases;
-                    nHits[side] = ix->overflow[off];
-                    hits[side] = ix->overflow + off + 1;
-                    out->nOverflowLists++;
-                }
+                fill_side(ix, v, minSeedLoc, maxSeedLoc, &singleton[side], &nHits[side], &hits[side],
+                          &out->nOverflowLists);
             }
         }
         out->nLookups++;
         int applied = 0;
         for (int dir = 0; dir < 2; dir++) {
+            if (radius != 0 && (uint32_t)dir != search->searchDirection) continue;   /* BaseAligner.cpp:804-809 */
             if (nHits[dir] > o->p.maxHitsToConsider && !o->p.explorePopularSeeds) {
                 out->nHitsIgnored++;
                 o->popular++;
@@ -586,7 +645,7 @@ static void align_read(Oracle *o, const char *bases, const char *quals, unsigned
                     }
                     uint32_t h = hits[dir][i];
                     uint32_t loc = h - offset;
-                    if (h < offset) continue;
+                    if (loc < minLocation || loc > maxLocation || h < offset) continue;   /* BaseAligner.cpp:849-853 */
                     Elem *el = find_elem(o, loc, dir);
                     unsigned bit = loc % ELEM_SIZE;
                     if (el) {
@@ -619,9 +678,10 @@ static void align_read(Oracle *o, const char *bases, const char *quals, unsigned
             }
         }
         next += seedLen;
-        if (applied && score(o, 0, readLen, &result)) goto finish;
+        if (applied && score(o, 0, readLen, &result)) { fill_hits(o, multiFound, multiHits); goto finish; }
     }
     score(o, 1, readLen, &result);
+    fill_hits(o, multiFound, multiHits);   /* (not on the wrap-count exit above, BaseAligner.cpp:697-719) */
 finish:
     out->result = (uint8_t)result;
     out->popularSeedsSkipped = (uint16_t)o->popular;
@@ -629,7 +689,7 @@ finish:
     out->probabilityOfBestCandidate = o->pBest;
 }
 
-static Oracle *oracle_new(const snapgpu_index_view_t *ix, const snapgpu_aligner_params_t *p) {
+static Oracle *oracle_new(const snapgpu_index_view_t *ix, const snapgpu_aligner_params_t *p, unsigned maxHitsToGet) {
     pthread_once(&g_once, init_tables);
     Oracle *o = (Oracle *)calloc(1, sizeof(Oracle));
     o->ix = ix;
@@ -646,11 +706,16 @@ static Oracle *oracle_new(const snapgpu_index_view_t *ix, const snapgpu_aligner_
     o->mapMask = m - 1;
     o->lists = (Elem *)calloc(o->numWeightLists + 1, sizeof(Elem));
     for (unsigned i = 0; i <= o->numWeightLists; i++) o->lists[i].wnext = o->lists[i].wprev = &o->lists[i];
+    o->maxHitsToGet = maxHitsToGet;
+    if (maxHitsToGet) {
+        o->hitLoc = (uint32_t *)calloc((size_t)MAX_K * maxHitsToGet, sizeof(uint32_t));
+        o->hitRC = (uint8_t *)calloc((size_t)MAX_K * maxHitsToGet, 1);
+    }
     return o;
 }
 
 static void oracle_delete(Oracle *o) {
-    free(o->pool); free(o->map); free(o->lists); free(o);
+    free(o->pool); free(o->map); free(o->lists); free(o->hitLoc); free(o->hitRC); free(o);
 }
 
 typedef struct {
@@ -662,17 +727,23 @@ typedef struct {
     uint64_t n;
     snapgpu_result_t *out;
     volatile uint64_t *cursor;
+    const snapgpu_search_t *search;
+    unsigned maxHitsToGet;
+    int32_t *multiFound;
+    snapgpu_multi_hit_t *multiHits;
 } Job;
 
 static void *worker(void *arg) {
     Job *j = (Job *)arg;
-    Oracle *o = oracle_new(j->ix, j->p);
+    Oracle *o = oracle_new(j->ix, j->p, j->maxHitsToGet);
     for (;;) {
         uint64_t b = __atomic_fetch_add(j->cursor, 64, __ATOMIC_RELAXED);
         if (b >= j->n) break;
         uint64_t e = b + 64 < j->n ? b + 64 : j->n;
         for (uint64_t i = b; i < e; i++)
-            align_read(o, j->bases + j->offsets[i], j->quals + j->offsets[i], j->lengths[i], &j->out[i]);
+            align_read(o, j->bases + j->offsets[i], j->quals + j->offsets[i], j->lengths[i], &j->out[i],
+                       j->search ? &j->search[i] : NULL, j->multiFound ? &j->multiFound[i] : NULL,
+                       j->multiHits ? j->multiHits + i * j->maxHitsToGet : NULL);
     }
     oracle_delete(o);
     return NULL;
@@ -680,16 +751,24 @@ static void *worker(void *arg) {
 
 /* Align a batch of reads on `nThreads` host threads (one private aligner each,
  * as ParallelTask gives each thread its own BaseAligner, ParallelTask.h:127-137). */
-int oracle_align_batch(const snapgpu_index_view_t *ix, const snapgpu_aligner_params_t *p,
-                       const char *bases, const char *quals, const uint64_t *offsets, const uint32_t *lengths,
-                       uint64_t n, snapgpu_result_t *out, int nThreads) {
+int oracle_align_batch_ex(const snapgpu_index_view_t *ix, const snapgpu_aligner_params_t *p,
+                          const char *bases, const char *quals, const uint64_t *offsets, const uint32_t *lengths,
+                          uint64_t n, const snapgpu_search_t *search, unsigned maxHitsToGet, snapgpu_result_t *out,
+                          int32_t *multiFound, snapgpu_multi_hit_t *multiHits, int nThreads) {
     if (ix->seedLen < 16 || ix->seedLen > 25) return -1;
+    if (maxHitsToGet && (!multiFound || !multiHits)) return -1;
     if (nThreads < 1) nThreads = 1;
     volatile uint64_t cursor = 0;
-    Job job = {ix, p, bases, quals, offsets, lengths, n, out, &cursor};
+    Job job = {ix, p, bases, quals, offsets, lengths, n, out, &cursor, search, maxHitsToGet, multiFound, multiHits};
     pthread_t *th = (pthread_t *)calloc((size_t)nThreads, sizeof(pthread_t));
     for (int t = 0; t < nThreads; t++) pthread_create(&th[t], NULL, worker, &job);
     for (int t = 0; t < nThreads; t++) pthread_join(th[t], NULL);
     free(th);
     return 0;
+}
+
+int oracle_align_batch(const snapgpu_index_view_t *ix, const snapgpu_aligner_params_t *p,
+                       const char *bases, const char *quals, const uint64_t *offsets, const uint32_t *lengths,
+                       uint64_t n, snapgpu_result_t *out, int nThreads) {
+    return oracle_align_batch_ex(ix, p, bases, quals, offsets, lengths, n, NULL, 0, out, NULL, NULL, nThreads);
 }

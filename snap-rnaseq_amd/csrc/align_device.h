@@ -113,6 +113,13 @@ struct KArgs {
     const uint32_t *readList;    // pass 2: read indices (nullptr in pass 1)
     const uint4 *seedRecs;       // seed_lookup_kernel records (SeedRec, 8 per read), or nullptr
     unsigned long long *phaseBuf;   // diagnostic (SNAPGPU_PHASES=1): per-block [PH_SLOTS] cycle sums, else null
+    // windowed search + multi-hit export (snapgpu_align_batch_ex; BaseAligner.h:73-86)
+    const snapgpu_search_t *search;     // per read, or nullptr (= unconstrained)
+    uint32_t maxHitsToGet;              // 0: no multi-hit recording
+    uint32_t hitStride;                 // u32 per block in hitScratch
+    uint32_t *hitScratch;               // per block: hitCount[MAX_K], then {loc, dir}[MAX_K][maxHitsToGet]
+    int32_t *multiFound;                // per read
+    snapgpu_multi_hit_t *multiHits;     // [nReads][maxHitsToGet]
 };
 
 // ------------------------------------------------------------ wave helpers
@@ -464,6 +471,69 @@ __device__ __forceinline__ int next_piece_after(const KArgs &A, uint32_t loc) { 
         else hi = m - 1;
     }
     return -1;
+}
+
+// ------------------------------------- multi-hit export / windowed lookups
+// BaseAligner.cpp:1255-1261: remember a scored hit (score != -1) while fewer than
+// maxHitsToGet are held at that distance.  The scratch is per block; lane 0 owns it.
+template <bool EXT>
+__device__ __forceinline__ void record_hit(const KArgs &A, uint32_t loc, uint32_t dir, uint32_t sc) {
+    if (!EXT || A.maxHitsToGet == 0 || sc >= (uint32_t)MAX_K) return;
+    if (lane_id() == 0) {
+        uint32_t *cnt = A.hitScratch + (uint64_t)blockIdx.x * A.hitStride;
+        const uint32_t c = cnt[sc];
+        if (c < A.maxHitsToGet) {
+            uint32_t *h = cnt + MAX_K + 2 * (sc * A.maxHitsToGet + c);
+            h[0] = loc;
+            h[1] = dir;
+            cnt[sc] = c + 1;
+        }
+    }
+}
+
+// BaseAligner::fillHitsFound (BaseAligner.cpp:940-975) from the block's scratch, lane 0
+__device__ __forceinline__ void fill_hits(const KArgs &A, uint32_t r, bool fill) {
+    if (lane_id() != 0) return;
+    int32_t found = 0;
+    if (fill) {
+        const uint32_t *cnt = A.hitScratch + (uint64_t)blockIdx.x * A.hitStride;
+        snapgpu_multi_hit_t *out = A.multiHits + (uint64_t)r * A.maxHitsToGet;
+        int first = 0;
+        while (first < MAX_K && cnt[first] == 0) first++;
+        for (int d = first; d < first + 4 && d < MAX_K; d++) {
+            const uint32_t c = cnt[d];
+            bool full = false;
+            for (uint32_t i = 0; i < c; i++) {
+                const uint32_t *h = cnt + MAX_K + 2 * (d * A.maxHitsToGet + i);
+                snapgpu_multi_hit_t m;
+                m.location = h[0];
+                m.direction = (uint8_t)h[1];
+                m.score = (uint8_t)d;
+                m.reserved = 0;
+                out[found++] = m;
+                if ((uint32_t)found == A.maxHitsToGet) { full = true; break; }
+            }
+            if (full) break;
+        }
+    }
+    A.multiFound[r] = found;
+}
+
+// Number of leading entries > x of a list sorted in descending order (the overflow
+// hit lists, GenomeIndex.cpp:1057-1075): 64-way search, each round shrinks the
+// candidate range 64-fold.  Wave-uniform.
+__device__ __forceinline__ uint32_t count_above_desc(const uint32_t *L, uint32_t cnt, uint32_t x) {
+    uint32_t lo = 0, hi = cnt;
+    while (lo < hi) {
+        const uint32_t step = (hi - lo + 63) / 64;
+        const uint32_t pos = lo + (uint32_t)lane_id() * step;
+        const uint32_t t = (uint32_t)__popcll(ballot(pos < hi && L[pos] > x));
+        if (t == 0) break;
+        const uint32_t nlo = lo + (t - 1) * step + 1;
+        hi = hi < lo + t * step ? hi : lo + t * step;
+        lo = nlo;
+    }
+    return lo;
 }
 
 // ------------------------------------------------------- phase diagnostics

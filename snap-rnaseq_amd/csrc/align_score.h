@@ -353,7 +353,7 @@ __device__ __forceinline__ void lv_pass(const KArgs &A, Lds<128> &S, uint32_t i0
 // order (BaseAligner.cpp:1129-1384).  Returns true when the read is finished
 // (stopOnFirstHit).  GS is a template parameter so group indexing is shifts and the
 // per-group loops unroll.
-template <int GS>
+template <int GS, bool EXT>
 __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<128> &S, Elem128 *ar, ReadState &st, uint32_t i0, int m,
                                            int k, uint32_t n, uint32_t nb, uint32_t &lastSlot, bool &lastSkip,
                                            int *result) {
@@ -443,6 +443,7 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<128> &S, Elem128 
         const uint32_t loc = elemLoc + (uint32_t)net2;
         const bool anyNearby0 = cScored != 0;
         cScored |= 1ull << cbit;
+        record_hit<EXT>(A, loc, dir, sc);
         st.nScored++;
         g0 = gs + 1;
         const bool passA = !(anyNearby0 && (cBest < sc || (cBest == sc && prob <= cProb)));
@@ -517,6 +518,7 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<128> &S, Elem128 
 }
 
 // BaseAligner::score (BaseAligner.cpp:977-1399) over batches of popped elements.
+template <bool EXT>
 __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<128> &S, Elem128 *ar, ReadState &st, bool force,
                                            uint32_t n, int *result, uint32_t *flags) {
     const int lane = lane_id();
@@ -649,10 +651,10 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<128> &S, Elem1
             const int m = (int)(nc - i0) < Gn ? (int)(nc - i0) : Gn;
             PH_CNT(A, S, PH_NPASS, 1);
             bool fin;
-            if (GS == 8) fin = pass_apply<8>(A, S, ar, st, i0, m, k, n, nb, lastSlot, lastSkip, result);
-            else if (GS == 16) fin = pass_apply<16>(A, S, ar, st, i0, m, k, n, nb, lastSlot, lastSkip, result);
-            else if (GS == 32) fin = pass_apply<32>(A, S, ar, st, i0, m, k, n, nb, lastSlot, lastSkip, result);
-            else fin = pass_apply<64>(A, S, ar, st, i0, m, k, n, nb, lastSlot, lastSkip, result);
+            if (GS == 8) fin = pass_apply<8, EXT>(A, S, ar, st, i0, m, k, n, nb, lastSlot, lastSkip, result);
+            else if (GS == 16) fin = pass_apply<16, EXT>(A, S, ar, st, i0, m, k, n, nb, lastSlot, lastSkip, result);
+            else if (GS == 32) fin = pass_apply<32, EXT>(A, S, ar, st, i0, m, k, n, nb, lastSlot, lastSkip, result);
+            else fin = pass_apply<64, EXT>(A, S, ar, st, i0, m, k, n, nb, lastSlot, lastSkip, result);
             if (fin) return true;
             i0 += (uint32_t)m;
         }

@@ -23,7 +23,7 @@ namespace sgk {
 // ------------------------------------------------------------------ score()
 // BaseAligner::score, BaseAligner.cpp:977-1399.  Returns true iff a final
 // result was produced (written into st / *result).
-template <int MAXLEN>
+template <int MAXLEN, bool EXT>
 __device__ __forceinline__ bool score_wave(const KArgs &A, Lds<MAXLEN> &S, Elem512 *ar, ReadState &st, bool force,
                                            uint32_t n, const uint32_t (&rbF)[MAXLEN / 64],
                                            const uint32_t (&rbR)[MAXLEN / 64], int *result, uint32_t *flags) {
@@ -127,6 +127,7 @@ __device__ __forceinline__ bool score_wave(const KArgs &A, Lds<MAXLEN> &S, Elem5
                         }
                     }
                 }
+                if (sc != FAIL_SCORE) record_hit<EXT>(A, loc, dir, sc);
                 st.nScored++;
                 if (anyNearby) {
                     if (ebest < sc || (ebest == sc && prob <= eprob)) continue;
@@ -200,10 +201,11 @@ __device__ __forceinline__ bool score_wave(const KArgs &A, Lds<MAXLEN> &S, Elem5
 // ------------------------------------------------------------ hit insertion
 // The per-hit loop of BaseAligner.cpp:829-869 (findCandidate / incrementWeight /
 // allocateNewCandidate) for one seed in one direction.
-template <int MAXLEN>
+template <int MAXLEN, bool EXT>
 __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, ElemOf<MAXLEN> *ar, ReadState &st, uint32_t dir,
                                             uint32_t offset, uint32_t lim, const uint32_t *list, uint32_t single,
-                                            uint32_t numWeightLists, uint32_t lpsNow) {
+                                            uint32_t numWeightLists, uint32_t lpsNow, uint32_t minLoc,
+                                            uint32_t maxLoc) {
     const int lane = lane_id();
     const bool allowAlloc = lpsNow <= st.scoreLimit;
     for (uint32_t b0 = 0; b0 < lim; b0 += WAVE) {
@@ -211,8 +213,9 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
         uint32_t i = b0 + lane;
         bool valid = i < lim;
         uint32_t h = valid ? (list ? list[i] : single) : 0;
-        valid = valid && h >= offset;
         uint32_t loc = h - offset;
+        valid = valid && h >= offset;
+        if constexpr (EXT) valid = valid && loc >= minLoc && loc <= maxLoc;   // BaseAligner.cpp:849-853
         uint32_t key = ((loc / ELEM) << 1) | dir;
         S.scrLoc[lane] = loc;
         uint32_t slot = 0;
@@ -293,7 +296,8 @@ __device__ __forceinline__ void defer_read(const KArgs &A, uint32_t r) {
 }
 
 // ------------------------------------------------------------- AlignRead
-template <int MAXLEN>
+// EXT: windowed search / multi-hit export compiled in (snapgpu_align_batch_ex)
+template <int MAXLEN, bool EXT>
 __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf<MAXLEN> *ar, uint32_t r) {
     constexpr int NB = MAXLEN / 64;
     const int lane = lane_id();
@@ -319,6 +323,19 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
     if constexpr (MAXLEN == 128) {
         if (n > 128) { defer_read(A, r); return; }
     }
+    // search window (BaseAligner.cpp:596-602); multiHitsFound = 0 up front (:586-590)
+    uint32_t radius = 0, sDir = 0, minLoc = 0, maxLoc = INVALID;
+    if (EXT && A.search) {
+        radius = uni(A.search[r].searchRadius);
+        if (radius) {
+            const uint32_t sLoc = uni(A.search[r].searchLocation);
+            sDir = uni(A.search[r].searchDirection);
+            minLoc = sLoc > radius ? sLoc - radius : 0;
+            maxLoc = sLoc < INVALID - radius ? sLoc + radius : INVALID;
+        }
+    }
+    bool fillHits = false;
+    if (EXT && A.maxHitsToGet && lane < MAX_K) A.hitScratch[(uint64_t)blockIdx.x * A.hitStride + lane] = 0;
     if (n > A.maxReadSize || n > (uint32_t)MAXLEN) { flags |= SNAPGPU_FLAG_READ_TOO_LONG; run = false; }
     else if (n < seedLen) run = false;
     uint32_t rbF[NB], rbR[NB];
@@ -384,9 +401,14 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
         if (lane <= NB) seedUsed[lane] = 0;
         wave_sync();
         uint32_t next = 0, wrapCount = 0;
+        bool wrapForced = false;
+        // BaseAligner.cpp:749-751
+        const uint32_t minSeedLoc = minLoc < n ? 0 : minLoc - n;
+        const uint32_t maxSeedLoc = maxLoc > INVALID - n ? INVALID : maxLoc + n;
+        const bool windowed = EXT && minSeedLoc != 0 || maxSeedLoc != INVALID;
         // first-round lookups resolved by seed_lookup_kernel: lane 4k+f holds field f of record k
         uint32_t srec = 0, pfIdx = SEEDS_PER_READ;
-        if (MAXLEN == 128 && A.seedRecs && A.maxHits < 0xffffu) {
+        if (MAXLEN == 128 && A.seedRecs && A.maxHits < 0xffffu && radius == 0) {
             srec = ((const uint32_t *)(A.seedRecs + (uint64_t)r * SEEDS_PER_READ))[lane & 31];
             pfIdx = 0;
         }
@@ -403,7 +425,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
             if (overdue(st, 3)) break;
             if (!force && next >= nPossible) {
                 wrapCount++;
-                if (wrapCount >= seedLen) force = true;
+                if (wrapCount >= seedLen) { force = true; wrapForced = true; }
                 else {
                     next = A.tab->wrap[wrapCount];
                     st.mostSeeds[0] = st.mostSeeds[1] = wrapCount + 1;
@@ -491,6 +513,20 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
                         ls1 = A.overflow + o + 1;
                         st.nOvf++;
                     }
+                    if (windowed) {   // the hits within [minSeedLoc, maxSeedLoc] (GenomeIndex.cpp:1029-1078)
+                        for (int sd = 0; sd < 2; sd++) {
+                            uint32_t &nh = sd ? nH1 : nH0;
+                            const uint32_t *&ls = sd ? ls1 : ls0;
+                            const uint32_t sg = sd ? sg1 : sg0;
+                            if (sd && pal) { nH1 = nH0; ls1 = ls0; break; }
+                            if (!ls) { if (nh && (sg < minSeedLoc || sg > maxSeedLoc)) nh = 0; continue; }
+                            const uint32_t lo = uni(count_above_desc(ls, nh, maxSeedLoc));
+                            uint32_t end = minSeedLoc ? uni(count_above_desc(ls, nh, minSeedLoc - 1)) : nh;
+                            if (end < lo) end = lo;
+                            nh = end - lo;
+                            ls += lo;
+                        }
+                    }
                 }
                 st.nLookups++;
                 PH_ADD(A, S, PH_LOOKUP, tlk);
@@ -498,6 +534,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
     #pragma unroll
                 for (uint32_t dir = 0; dir < 2; dir++) {
                     const uint32_t nh = dir ? nH1 : nH0;
+                    if (EXT && radius && dir != sDir) continue;   // BaseAligner.cpp:781-786
                     if (nh > A.maxHits && !A.explore) {
                         st.nHitsIgnored++;
                         st.popular++;
@@ -506,8 +543,8 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
                         uint32_t lim = nh < A.maxHits ? nh : A.maxHits;
                         st.nHitWords += lim;
                         PH_T(A, tins);
-                        insert_hits<MAXLEN>(A, S, ar, st, dir, offset, lim, dir ? ls1 : ls0, dir ? sg1 : sg0,
-                                            numWeightLists, dir ? st.lps[1] : st.lps[0]);
+                        insert_hits<MAXLEN, EXT>(A, S, ar, st, dir, offset, lim, dir ? ls1 : ls0, dir ? sg1 : sg0,
+                                            numWeightLists, dir ? st.lps[1] : st.lps[0], minLoc, maxLoc);
                         PH_ADD(A, S, PH_INSERT, tins);
                         if (dir) st.nSeedsApplied[1]++; else st.nSeedsApplied[0]++;
                         applied = true;
@@ -519,10 +556,10 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
             if (overdue(st, 7)) break;
             PH_T(A, tsc);
             bool fin;
-            if constexpr (Lds<MAXLEN>::BYTE_PATH) fin = score_wave<MAXLEN>(A, S, ar, st, force, n, rbF, rbR, &result, &flags);
-            else fin = score_batched(A, S, ar, st, force, n, &result, &flags);
+            if constexpr (Lds<MAXLEN>::BYTE_PATH) fin = score_wave<MAXLEN, EXT>(A, S, ar, st, force, n, rbF, rbR, &result, &flags);
+            else fin = score_batched<EXT>(A, S, ar, st, force, n, &result, &flags);
             PH_ADD(A, S, PH_SCORE, tsc);
-            if (fin || force) break;
+            if (fin || force) { fillHits = !wrapForced; break; }
             if (overdue(st, 8)) break;
         }
         PH_ADD(A, S, PH_SEEDLOOP, tsl);
@@ -550,11 +587,12 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
         o.probabilityOfBestCandidate = st.pBest;
         A.out[r] = o;
     }
+    if constexpr (EXT) { if (A.maxHitsToGet) fill_hits(A, r, run && fillHits); }
     wave_sync();
     PH_ADD(A, S, PH_OUT, tout);
 }
 
-template <int MAXLEN>
+template <int MAXLEN, bool EXT>
 // amdgpu_waves_per_eu(3): keep <= 168 VGPRs (3 waves/SIMD, 12 per CU); a few cold spills
 // are cheaper than dropping to 2 waves/SIMD.
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void align_kernel(KArgs A) {
@@ -569,7 +607,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void al
         if (i >= total) break;
         const uint32_t r = A.readList ? uni(A.readList[i]) : i;
         if (__hip_atomic_load(&g_diag[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;   // watchdog: drain
-        align_one<MAXLEN>(A, S, ar, r);
+        align_one<MAXLEN, EXT>(A, S, ar, r);
     }
 }
 
@@ -837,7 +875,7 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
     hipDeviceProp_t prop;
     hipGetDeviceProperties(&prop, device);
     int perCU = 0;
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, (const void *)align_kernel<128>, 64, 0);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, (const void *)align_kernel<128, false>, 64, 0);
     if (perCU <= 0) perCU = 8;
     a->grid = prop.multiProcessorCount * perCU;
     uint32_t maxSeeds = params->maxSeedsToUse ? params->maxSeedsToUse
@@ -847,7 +885,7 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
     while (a->grid > 64 && (uint64_t)a->grid * a->arenaElems * sizeof(Elem512) > budget) a->grid /= 2;
     if ((e = hipMalloc(&a->dArena, (uint64_t)a->grid * a->arenaElems * sizeof(Elem512))) != hipSuccess) return fail("arena", e);
     int perCU512 = 0;   // pass 2 (deferred reads) reuses the arenas of the first a->grid blocks
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU512, (const void *)align_kernel<512>, 64, 0);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU512, (const void *)align_kernel<512, false>, 64, 0);
     if (perCU512 <= 0) perCU512 = 4;
     a->grid512 = prop.multiProcessorCount * perCU512;
     if (a->grid512 > a->grid) a->grid512 = a->grid;
@@ -898,7 +936,20 @@ void snapgpu_device_reads_free(snapgpu_device_reads_t *d) {
     delete d;
 }
 
-int snapgpu_align_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d) {
+// Extension arguments of snapgpu_align_batch_ex (device pointers; all null for the plain path)
+struct AlignExt {
+    const snapgpu_search_t *search = nullptr;
+    uint32_t maxHitsToGet = 0;
+    uint32_t *hitScratch = nullptr;
+    int32_t *multiFound = nullptr;
+    snapgpu_multi_hit_t *multiHits = nullptr;
+};
+
+static int launch_passes(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, const AlignExt &x);
+
+int snapgpu_align_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d) { return launch_passes(a, d, AlignExt()); }
+
+static int launch_passes(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, const AlignExt &x) {
     if (!a || !d) return SNAPGPU_EINVAL;
     HIPCHK(hipSetDevice(a->device));
     if (d->n == 0) return SNAPGPU_OK;
@@ -921,6 +972,8 @@ int snapgpu_align_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d) {
     A.counter = a->dCounter; A.arena = a->dArena; A.arenaElems = a->arenaElems;
     // dCounter: [0] pass-1 work counter, [1] pass-2 work counter, [2] deferred-read count
     A.deferList = d->dDefer; A.deferCount = a->dCounter + 2; A.readList = nullptr;
+    A.search = x.search; A.maxHitsToGet = x.maxHitsToGet; A.hitStride = MAX_K * (1 + 2 * x.maxHitsToGet);
+    A.hitScratch = x.hitScratch; A.multiFound = x.multiFound; A.multiHits = x.multiHits;
     int grid = a->grid;
     if ((uint64_t)grid > d->n) grid = (int)d->n;
     (void)hipGetLastError();   // clear any stale error of an unrelated earlier runtime call
@@ -935,7 +988,9 @@ int snapgpu_align_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d) {
     HIPCHK(hipGetLastError());
     A.seedRecs = reinterpret_cast<const uint4 *>(d->dSeeds);
     HIPCHK(hipEventRecord(a->ev[0], a->stream));
-    hipLaunchKernelGGL(align_kernel<128>, dim3(grid), dim3(64), 0, a->stream, A);
+    const bool ext = x.search || x.maxHitsToGet;
+    if (ext) hipLaunchKernelGGL((align_kernel<128, true>), dim3(grid), dim3(64), 0, a->stream, A);
+    else hipLaunchKernelGGL((align_kernel<128, false>), dim3(grid), dim3(64), 0, a->stream, A);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(a->ev[1], a->stream));
     // pass 2: reads longer than 128 bases or needing the byte-compare LV
@@ -945,7 +1000,8 @@ int snapgpu_align_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d) {
     B.seedRecs = nullptr;
     int grid2 = a->grid512;
     if ((uint64_t)grid2 > d->n) grid2 = (int)d->n;
-    hipLaunchKernelGGL(align_kernel<512>, dim3(grid2), dim3(64), 0, a->stream, B);
+    if (ext) hipLaunchKernelGGL((align_kernel<512, true>), dim3(grid2), dim3(64), 0, a->stream, B);
+    else hipLaunchKernelGGL((align_kernel<512, false>), dim3(grid2), dim3(64), 0, a->stream, B);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(a->ev[2], a->stream));
     a->lastReads = d;
@@ -1038,6 +1094,67 @@ int snapgpu_align_batch(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, snap
     if (!rc) rc = snapgpu_results_download(a, d, out);
     snapgpu_device_reads_free(d);
     a->lastReads = nullptr;
+    return rc;
+}
+
+int snapgpu_align_batch_ex(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, const snapgpu_search_t *search,
+                           uint32_t maxHitsToGet, snapgpu_result_t *out, int32_t *multiHitsFound,
+                           snapgpu_multi_hit_t *multiHits) {
+    if (!a || !reads || !out) return SNAPGPU_EINVAL;
+    if (maxHitsToGet > SNAPGPU_MAX_MULTI_HITS_TO_GET || (maxHitsToGet && (!multiHitsFound || !multiHits))) {
+        snapgpu::setError("align_batch_ex: maxHitsToGet must be <= 512 and come with multiHitsFound/multiHits");
+        return SNAPGPU_EINVAL;
+    }
+    if (search)
+        for (uint64_t i = 0; i < reads->n; i++)
+            if (search[i].searchRadius && search[i].searchDirection > 1) {
+                snapgpu::setError("align_batch_ex: searchDirection must be 0 (FORWARD) or 1 (RC)");
+                return SNAPGPU_EINVAL;
+            }
+    if (reads->n == 0) return SNAPGPU_OK;
+    snapgpu_device_reads_t *d = snapgpu_reads_upload(a, reads);
+    if (!d) return SNAPGPU_EDEVICE;
+    AlignExt x;
+    void *dSearch = nullptr, *dScratch = nullptr, *dFound = nullptr, *dHits = nullptr;
+    auto cleanup = [&]() {
+        hipFree(dSearch); hipFree(dScratch); hipFree(dFound); hipFree(dHits);
+        snapgpu_device_reads_free(d);
+        a->lastReads = nullptr;
+    };
+    hipError_t e = hipSuccess;
+    const uint64_t n = reads->n;
+    if (search) {
+        if ((e = hipMalloc(&dSearch, n * sizeof(snapgpu_search_t))) == hipSuccess)
+            e = hipMemcpyAsync(dSearch, search, n * sizeof(snapgpu_search_t), hipMemcpyHostToDevice, a->stream);
+        x.search = (const snapgpu_search_t *)dSearch;
+    }
+    if (e == hipSuccess && maxHitsToGet) {
+        const uint64_t blocks = (uint64_t)(a->grid > a->grid512 ? a->grid : a->grid512);
+        const uint64_t stride = (uint64_t)MAX_K * (1 + 2 * maxHitsToGet);
+        if ((e = hipMalloc(&dScratch, blocks * stride * 4)) == hipSuccess &&
+            (e = hipMalloc(&dFound, n * sizeof(int32_t))) == hipSuccess)
+            e = hipMalloc(&dHits, n * maxHitsToGet * sizeof(snapgpu_multi_hit_t));
+        x.maxHitsToGet = maxHitsToGet;
+        x.hitScratch = (uint32_t *)dScratch;
+        x.multiFound = (int32_t *)dFound;
+        x.multiHits = (snapgpu_multi_hit_t *)dHits;
+    }
+    if (e != hipSuccess) {
+        snapgpu::setError(std::string("align_batch_ex: ") + hipGetErrorString(e));
+        cleanup();
+        return SNAPGPU_EDEVICE;
+    }
+    int rc = launch_passes(a, d, x);
+    if (!rc) rc = snapgpu_results_download(a, d, out);
+    if (!rc && maxHitsToGet) {
+        if ((e = hipMemcpy(multiHitsFound, dFound, n * sizeof(int32_t), hipMemcpyDeviceToHost)) == hipSuccess)
+            e = hipMemcpy(multiHits, dHits, n * maxHitsToGet * sizeof(snapgpu_multi_hit_t), hipMemcpyDeviceToHost);
+        if (e != hipSuccess) {
+            snapgpu::setError(std::string("align_batch_ex download: ") + hipGetErrorString(e));
+            rc = SNAPGPU_EDEVICE;
+        }
+    }
+    cleanup();
     return rc;
 }
 

@@ -31,6 +31,26 @@ RESULT_DTYPE = np.dtype([
 ])
 assert RESULT_DTYPE.itemsize == C.sizeof(_ffi.Result)
 
+# snapgpu_search_t / snapgpu_multi_hit_t (include/snapgpu.h)
+SEARCH_DTYPE = np.dtype([("searchRadius", "<u4"), ("searchLocation", "<u4"), ("searchDirection", "<u4"),
+                         ("reserved", "<u4")])
+MULTI_HIT_DTYPE = np.dtype([("location", "<u4"), ("direction", "u1"), ("score", "u1"), ("reserved", "<u2")])
+MAX_MULTI_HITS_TO_GET = 512   # BaseAligner.h:149
+
+
+def search_array(search, n):
+    """None, a SEARCH_DTYPE array, or an (n, 3) array-like of (radius, location, direction)."""
+    if search is None:
+        return None
+    s = np.asarray(search)
+    if s.dtype != SEARCH_DTYPE:
+        a = np.asarray(search, dtype=np.uint64).reshape(-1, 3)
+        s = np.zeros(len(a), dtype=SEARCH_DTYPE)
+        s["searchRadius"], s["searchLocation"], s["searchDirection"] = a[:, 0], a[:, 1], a[:, 2]
+    if len(s) != n:
+        raise ValueError(f"search has {len(s)} entries for {n} reads")
+    return np.ascontiguousarray(s)
+
 
 class SnapGpuError(RuntimeError):
     pass
@@ -255,6 +275,21 @@ class BaseAligner:
             _check(lib().snapgpu_align_batch(self._h, reads._p, out.ctypes.data_as(C.POINTER(_ffi.Result))),
                    "align_batch")
         return out[:n]
+
+    def AlignReadsEx(self, reads, search=None, maxHitsToGet=0):
+        """Batched form of the richer AlignRead (BaseAligner.h:73-86): per-read search
+        windows (see search_array) and up to maxHitsToGet multi-hits per read.
+        -> (results, multiHitsFound int32[n], multiHits MULTI_HIT_DTYPE[n, maxHitsToGet])."""
+        n = reads.n
+        out = np.zeros(max(1, n), dtype=RESULT_DTYPE)
+        found = np.zeros(max(1, n), dtype=np.int32)
+        hits = np.zeros((max(1, n), max(1, maxHitsToGet)), dtype=MULTI_HIT_DTYPE)
+        srch = search_array(search, n)
+        if n:
+            _check(lib().snapgpu_align_batch_ex(self._h, reads._p, None if srch is None else srch.ctypes.data,
+                                                maxHitsToGet, out.ctypes.data, found.ctypes.data,
+                                                hits.ctypes.data), "align_batch_ex")
+        return out[:n], found[:n], hits[:n, :maxHitsToGet]
 
     def AlignRead(self, bases, quals=None):
         """-> (AlignmentResult, genomeLocation, direction, score, mapq) for one read."""

@@ -8,7 +8,8 @@ BaseAligner / LandauVishkin / GenomeIndex::lookupSeed (driven by
 oracle/ref_harness.cpp).  Everything written here is data: FASTA/FASTQ inputs and
 TSV/JSON expected outputs.
 
-    python3 tests/golden/make_golden.py
+    python3 tests/golden/make_golden.py                  # everything
+    python3 tests/golden/make_golden.py --only-multihit  # windowed search / multi-hit runs only
 """
 import hashlib
 import json
@@ -26,7 +27,8 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 import snapgpu  # noqa: E402
 from readsets import edge_reads  # noqa: E402
-from golden_common import PARAM_SETS, C1, C2, ref_tsv_to_canonical, digest  # noqa: E402
+from golden_common import (PARAM_SETS, C1, C2, MULTIHIT_RUNS, ref_tsv_to_canonical, ref_tsvx_to_canonical,  # noqa: E402
+                           digest)
 
 REF_BIN = os.path.join(ROOT, "oracle", "_ref")
 SNAP = os.path.join(REF_BIN, "snap-rna")
@@ -76,8 +78,61 @@ def small_genome_fasta(path):
         f.writelines(out)
 
 
+def search_windows(n, default_tsv, n_bases, seed=23):
+    """Per-read (radius, location, direction) for the windowed AlignRead: unconstrained,
+    windows around the reference's own unconstrained answer (same and opposite
+    direction), random windows, and saturating ones (BaseAligner.cpp:596-602)."""
+    rng = random.Random(seed)
+    best = []
+    for line in open(default_tsv):
+        x = line.split("\t")
+        best.append((int(x[2]), int(x[3])))
+    rows = []
+    for i in range(n):
+        loc, d = best[i]
+        kind = rng.randrange(6)
+        if kind == 0 or (kind in (1, 2) and loc == 0xFFFFFFFF):
+            rows.append((0, 0, 0))
+        elif kind in (1, 2):
+            rad = rng.choice([1, 30, 200, 5000])
+            c = max(0, loc + rng.randint(-rad, rad))
+            rows.append((rad, c, d if kind == 1 else 1 - d))
+        elif kind == 3:
+            rows.append((rng.choice([1000, 50000]), rng.randrange(n_bases), rng.randrange(2)))
+        elif kind == 4:
+            rows.append((rng.choice([0xFFFFFFF0, 4000000000]), rng.randrange(n_bases), rng.randrange(2)))
+        else:
+            rows.append((rng.choice([100, 3000]), rng.randrange(200), rng.randrange(2)))
+    return rows
+
+
+def multihit_fixtures(work):
+    """Windowed search + multi-hit export (BaseAligner.h:73-86) on the small genome."""
+    fa = os.path.join(HERE, "small.fa")
+    idxdir = os.path.join(work, "small_idx_mh")
+    ref_index(fa, idxdir)
+    g = snapgpu.Genome.from_fasta(fa, 500)
+    fq = os.path.join(HERE, "small_reads.fq")
+    n = sum(1 for _ in open(fq)) // 4
+    rows = search_windows(n, os.path.join(HERE, "expected_small_default.tsv"), g.n_bases)
+    sp = os.path.join(HERE, "small_search.tsv")
+    with open(sp, "w") as f:
+        f.writelines(f"{a}\t{b}\t{c}\n" for a, b, c in rows)
+    for name, (maxget, pset) in MULTIHIT_RUNS.items():
+        params = PARAM_SETS[pset]
+        args = [str(params[k]) for k in ("maxHits", "maxK", "numSeeds", "extra")]
+        out = run([HARNESS, "alignx", idxdir, fq, sp, str(maxget)] + args)
+        with open(os.path.join(HERE, f"expected_small_{name}.tsv"), "w") as f:
+            f.write(ref_tsvx_to_canonical(out))
+
+
 def main():
     work = tempfile.mkdtemp(prefix="golden_")
+    if "--only-multihit" in sys.argv:
+        multihit_fixtures(work)
+        shutil.rmtree(work, ignore_errors=True)
+        print("multi-hit fixtures written to", HERE)
+        return
     meta = {"generator": "tests/golden/make_golden.py", "reference": "oracle/_ref (andrewmagis/snap-rna SNAPLib)"}
 
     # 1. small genome + edge/synthetic reads, several parameter sets
@@ -94,6 +149,8 @@ def main():
     for name, params in PARAM_SETS.items():
         with open(os.path.join(HERE, f"expected_small_{name}.tsv"), "w") as f:
             f.write(ref_align(idxdir, fq, params))
+
+    multihit_fixtures(work)
 
     # 2. lookupSeed golden: seeds from the genome, their RCs, mutated and random seeds
     rng = random.Random(9)

@@ -37,5 +37,18 @@ def ref_tsv_to_canonical(text):
     return "\n".join(out) + "\n"
 
 
+def ref_tsvx_to_canonical(text):
+    """ref_harness alignx output -> canonical lines (align columns as above + nFound + hits)."""
+    out = []
+    for line in text.splitlines():
+        x = line.split("\t")
+        out.append(ref_tsv_to_canonical("\t".join(x[:11])).rstrip("\n") + "\t" + "\t".join(x[11:13]))
+    return "\n".join(out) + "\n"
+
+
+# multi-hit / windowed-search fixture runs: name -> (maxHitsToGet, PARAM_SETS key)
+MULTIHIT_RUNS = {"mh8": (8, "default"), "mh1": (1, "k5"), "mh64": (64, "h16")}
+
+
 def digest(text):
     return hashlib.sha256(text.encode()).hexdigest()

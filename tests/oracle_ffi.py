@@ -25,6 +25,10 @@ def oracle_lib():
                                          C.POINTER(C.c_uint64), C.POINTER(C.c_uint32), C.c_uint64,
                                          C.c_void_p, C.c_int]
         o.oracle_align_batch.restype = C.c_int
+        o.oracle_align_batch_ex.argtypes = [C.POINTER(F.IndexView), C.POINTER(F.AlignerParams), C.c_void_p,
+                                            C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32), C.c_uint64,
+                                            C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        o.oracle_align_batch_ex.restype = C.c_int
         o.oracle_lv.argtypes = [C.c_int, C.c_char_p, C.c_int, C.c_char_p, C.c_char_p, C.c_int, C.c_int,
                                 C.POINTER(C.c_double), C.POINTER(C.c_int)]
         o.oracle_lv.restype = C.c_int
@@ -46,6 +50,36 @@ def oracle_align(index, reads, params, n_threads=8):
                                          out.ctypes.data, n_threads)
     assert rc == 0
     return out[:n]
+
+
+def oracle_align_ex(index, reads, params, search=None, max_hits_to_get=0, n_threads=8):
+    """The richer AlignRead (BaseAligner.h:73-86): per-read search windows (an (n, 3)
+    array of radius, location, direction, or None) and multi-hit export.
+    -> (results, multiHitsFound int32[n], multiHits MULTI_HIT_DTYPE[n, max_hits_to_get])."""
+    import snapgpu
+    v = index.view()
+    n = reads.n
+    out = np.zeros(max(1, n), dtype=snapgpu.RESULT_DTYPE)
+    found = np.zeros(max(1, n), dtype=np.int32)
+    hits = np.zeros((max(1, n), max(1, max_hits_to_get)), dtype=snapgpu.MULTI_HIT_DTYPE)
+    srch = snapgpu.search_array(search, n)
+    r = reads._p.contents
+    rc = oracle_lib().oracle_align_batch_ex(C.byref(v), C.byref(params), r.bases, r.quals, r.offsets, r.lengths, n,
+                                            None if srch is None else srch.ctypes.data, max_hits_to_get,
+                                            out.ctypes.data, found.ctypes.data, hits.ctypes.data, n_threads)
+    assert rc == 0
+    return out[:n], found[:n], hits[:n, :max_hits_to_get]
+
+
+def canonical_tsv_ex(res, found, hits):
+    """canonical_tsv + nFound + "loc:dir:score,..." (the ref_harness alignx form)."""
+    base = canonical_tsv(res).splitlines()
+    lines = []
+    for i, b in enumerate(base):
+        f = int(found[i])
+        h = ",".join(f"{int(x['location'])}:{int(x['direction'])}:{int(x['score'])}" for x in hits[i, :max(f, 0)])
+        lines.append(f"{b}\t{f}\t{h or '-'}")
+    return "\n".join(lines) + "\n"
 
 
 def oracle_lv(direction, text, pattern, quals, k):
