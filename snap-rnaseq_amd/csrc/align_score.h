@@ -48,49 +48,45 @@ __device__ __forceinline__ uint32_t ffbl(uint32_t x) {
     asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
     return r;
 }
-// first set position >= m0, m0 in [0, 128]; 128 if none.  Branch-free.
-__device__ __forceinline__ int mk_first(const Mask128 &F, int m0) {
-    const uint64_t S = ~0ull << (m0 & 63);
-    const bool low = m0 < 64;
-    const uint64_t a = F.lo & (low ? S : 0ull);
-    const uint64_t b = F.hi & (low ? ~0ull : S);
-    // OR-ing the word base keeps ffbl's 0xffffffff "none" sentinel
-    uint32_t r = ffbl((uint32_t)a);
-    const uint32_t p1 = ffbl((uint32_t)(a >> 32)) | 32u, p2 = ffbl((uint32_t)b) | 64u, p3 = ffbl((uint32_t)(b >> 32)) | 96u;
-    r = p1 < r ? p1 : r;
-    r = p2 < r ? p2 : r;
-    r = p3 < r ? p3 : r;
-    r = r < 128u ? r : 128u;
-    return m0 >= 128 ? m0 : (int)r;
+// 64 + first set bit of F.hi (128 if none): the "not in the lower word" answer of mk_first
+__device__ __forceinline__ int mk_hi_first(const Mask128 &F) {
+    const uint32_t a = ffbl((uint32_t)F.hi), b = ffbl((uint32_t)(F.hi >> 32)) | 32u;
+    const uint32_t r = a < b ? a : b;
+    return r < 64u ? 64 + (int)r : 128;
 }
-__device__ __forceinline__ bool mk_bit(const Mask128 &F, int m) {
-    const uint64_t w = m < 64 ? F.lo : F.hi;
-    return m >= 128 || ((w >> (m & 63)) & 1) != 0;
+// first set position >= m0, m0 in [0, 128]; 128 if none (hf = mk_hi_first(F)).  Branch-free:
+// one 64-bit shift of the word holding m0 (OR-ing 32 keeps ffbl's 0xffffffff "none").
+__device__ __forceinline__ int mk_first(const Mask128 &F, int hf, int m0) {
+    const bool hw = m0 >= 64;
+    const uint64_t x = (hw ? F.hi : F.lo) >> (m0 & 63);
+    const uint32_t a = ffbl((uint32_t)x), b = ffbl((uint32_t)(x >> 32)) | 32u;
+    const int v = x != 0 ? m0 + (int)(a < b ? a : b) : (hw ? 128 : hf);
+    return v < 128 ? v : 128;
 }
 
 // ------------------------------------------------------------ group shifts
 // lane i <- lane i-1 of its group (-2 at the group start), DPP only
 template <int GS>
-__device__ __forceinline__ int from_lower(int v) {
+__device__ __forceinline__ int from_lower(int v, bool gfirst) {
     if constexpr (GS == 16) return __builtin_amdgcn_update_dpp(-2, v, 0x111, 0xf, 0xf, false);   // row_shr:1
     else if constexpr (GS == 8) {
         const int r = __builtin_amdgcn_update_dpp(-2, v, 0x111, 0xf, 0xf, false);
-        return (lane_id() & 7) == 0 ? -2 : r;
+        return gfirst ? -2 : r;
     } else {
         const int r = __builtin_amdgcn_update_dpp(-2, v, 0x138, 0xf, 0xf, false);               // wave_shr:1
-        return (lane_id() & (GS - 1)) == 0 ? -2 : r;
+        return gfirst ? -2 : r;
     }
 }
 // lane i <- lane i+1 of its group (-2 at the group end)
 template <int GS>
-__device__ __forceinline__ int from_upper(int v) {
+__device__ __forceinline__ int from_upper(int v, bool glast) {
     if constexpr (GS == 16) return __builtin_amdgcn_update_dpp(-2, v, 0x101, 0xf, 0xf, false);   // row_shl:1
     else if constexpr (GS == 8) {
         const int r = __builtin_amdgcn_update_dpp(-2, v, 0x101, 0xf, 0xf, false);
-        return (lane_id() & 7) == 7 ? -2 : r;
+        return glast ? -2 : r;
     } else {
         const int r = __builtin_amdgcn_update_dpp(-2, v, 0x130, 0xf, 0xf, false);               // wave_shl:1
-        return (lane_id() & (GS - 1)) == GS - 1 ? -2 : r;
+        return glast ? -2 : r;
     }
 }
 
@@ -108,13 +104,15 @@ __device__ __forceinline__ int lv_group(GroupLds &G, const Mask128 &M, bool gact
     constexpr int dx = DIR > 0 ? 0 : 1;
     const int lane = lane_id();
     const int li = lane & (GS - 1), gi = lane / GS, c = GS / 2 - 1;
+    const bool gfirst = li == 0, glast = li == GS - 1;   // group boundaries of the row shifts
     const int d = DIR > 0 ? li - c : c - li;
     const int pbase = gi * 2 * GS;                       // this group's path slots
     if (k > MAX_K - 1) k = MAX_K - 1;
     outE = -1;
     bool done = !gact;
     const int end0 = patternLen < textLen ? patternLen : textLen;
-    const int fm = mk_first(M, q0) - q0;
+    const int hf = mk_hi_first(M);
+    const int fm = mk_first(M, hf, q0) - q0;
     const int v0 = fm < end0 ? fm : end0;
     const int L0 = shfl_idx(v0, gi * GS + c);           // exact prefix on diagonal 0
     if (!done && L0 == end0) {                          // LandauVishkin.h:290-305
@@ -130,7 +128,7 @@ __device__ __forceinline__ int lv_group(GroupLds &G, const Mask128 &M, bool gact
         done = done || e > k;                           // limit reached: -1
         if (ballot(!done) == 0) break;
         rowsRun = e;
-        const int lower = from_lower<GS>(Lp), upper = from_upper<GS>(Lp);
+        const int lower = from_lower<GS>(Lp, gfirst), upper = from_upper<GS>(Lp, glast);
         const int left = DIR > 0 ? lower : upper;       // L[e-1][d-1]
         const int right = (DIR > 0 ? upper : lower) + 1;   // L[e-1][d+1] + 1
         const int x1 = Lp + 1;
@@ -141,9 +139,11 @@ __device__ __forceinline__ int lv_group(GroupLds &G, const Mask128 &M, bool gact
         const bool active = !done && d <= e && d >= -e;
         // slide along the diagonal (LandauVishkin.h:325-354)
         const int mpos = q0 + best;
-        const int f = mk_first(M, mpos < 128 ? mpos : 128) - q0;
+        const int mposc = mpos < 128 ? mpos : 128;
+        const int fa = mk_first(M, hf, mposc);             // fa == mposc <=> mismatch at mpos (or past 127)
+        const int f = fa - q0;
         const int slid = f < endd ? f : endd;
-        const int bnew = best < endd ? slid : (mk_bit(M, mpos) ? best : endd);
+        const int bnew = best < endd ? slid : (fa == mposc ? best : endd);
         const int Ln = active ? bnew : Lp;
         if (active) G.rows8[e][lane] = (uint8_t)(bnew + 2);
         (void)act;
@@ -385,32 +385,18 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<128> &S, Elem128 
         const bool fail = leader && !skip && gq >= g0 && gq < gs;
         const uint64_t fm = ballot(fail);
         if (fm) {
-            // per element: OR of the failing bits; the first failing lane of the element writes
-            uint64_t acc = 0;
-            bool first = true;
-#pragma unroll
-            for (int jg = 0; jg < 64 / GS; jg++) {
-                const int lj = jg * GS;
-                if (lj < WAVE && ((fm >> (lj & 63)) & 1)) {
-                    const uint32_t slj = readlaneu(sl, lj & 63), bj = readlaneu(bit, lj & 63);
-                    if (fail && slj == sl) {
-                        acc |= 1ull << bj;
-                        if (jg < gq) first = false;
-                    }
-                }
-            }
-            if (fail && first) {
-                uint32_t *ec = G.ecache[sl];
-                const uint64_t old = ((uint64_t)ec[3] << 32) | ec[2];
-                const uint64_t nw = old | acc;
-                ec[2] = (uint32_t)nw;
-                ec[3] = (uint32_t)(nw >> 32);
-                if (old == 0) {   // first scored candidate of the element: score -1 recorded
-                    ec[9] = (ec[6] >> 1) * ELEM + bit;
-                    ec[8] = FAIL_SCORE;
-                    ec[4] = 0u;
-                    ec[5] = 0u;
-                }
+            // An element's candidates are contiguous in the list: its first failing
+            // candidate of this step records score -1 if nothing of the element was scored
+            // before; every failing candidate ORs its bit into candidatesScored (ds_or_b64).
+            const uint32_t prevSl = (uint32_t)shfl_idx((int)sl, lane >= GS ? lane - GS : lane);
+            uint32_t *ec = G.ecache[sl];
+            const bool was0 = fail && (gq == g0 || prevSl != sl) && (ec[2] | ec[3]) == 0;
+            if (fail) atomicOr(reinterpret_cast<unsigned long long *>(ec + 2), 1ull << bit);
+            if (was0) {
+                ec[9] = (ec[6] >> 1) * ELEM + bit;
+                ec[8] = FAIL_SCORE;
+                ec[4] = 0u;
+                ec[5] = 0u;
             }
             st.nScored += (uint32_t)__popcll(fm);
             wave_sync();

@@ -469,13 +469,14 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
                 const uint64_t canon = comp ? rcv : f;
                 const uint32_t table = (uint32_t)(canon >> 32);
                 const uint32_t key = (uint32_t)canon;
-                const uint64_t size = A.tableSize[table];
+                const uint32_t size = (uint32_t)A.tableSize[table];   // < 2^31 (snapgpu_aligner_create)
                 const uint32_t *T = A.slots + 3 * A.tableBase[table];
-                const uint64_t h0 = fmix32(key) % size;
+                const uint32_t h0 = fmix32(key) % size;
                 for (uint32_t j0 = 0;; j0 += 8) {
                     uint32_t j = j0 + (lane & 7);
-                    uint64_t S_j = j <= 4 ? (uint64_t)j * (j + 1) * (2 * j + 1) / 6 : 30 + (uint64_t)(j - 4);
-                    uint64_t pos = (h0 + S_j) % size;
+                    const uint32_t S_j = j <= 4 ? j * (j + 1) * (2 * j + 1) / 6 : 30 + (j - 4);
+                    uint64_t pos = h0 + S_j;
+                    if (pos >= size) pos %= size;
                     uint32_t kj = 0, v1j = INVALID, v2j = 0;
                     bool beyond = j > size + 5;
                     if (lane < 8 && !beyond) { kj = T[3 * pos]; v1j = T[3 * pos + 1]; v2j = T[3 * pos + 2]; }
@@ -860,6 +861,12 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
         (e = hipMemcpy(a->dOverflow, idx->overflow.data(), idx->overflow.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return fail("ovf", e);
     if ((e = hipMalloc(&a->dTableBase, idx->nTables * 8)) != hipSuccess) return fail("tb", e);
     if ((e = hipMalloc(&a->dTableSize, idx->nTables * 8)) != hipSuccess) return fail("ts", e);
+    for (uint32_t t = 0; t < idx->nTables; t++)   // the kernels hash with 32-bit modulo
+        if (idx->tableSize[t] == 0 || idx->tableSize[t] >= (1ull << 31)) {
+            snapgpu::setError("hash table size must be in [1, 2^31)");
+            snapgpu_aligner_free(a);
+            return nullptr;
+        }
     hipMemcpy(a->dTableBase, idx->tableBase.data(), idx->nTables * 8, hipMemcpyHostToDevice);
     hipMemcpy(a->dTableSize, idx->tableSize.data(), idx->nTables * 8, hipMemcpyHostToDevice);
     size_t np = idx->genome->pieceOffsets.size();

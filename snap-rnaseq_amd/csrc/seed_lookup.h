@@ -112,15 +112,16 @@ __global__ __launch_bounds__(64) void seed_lookup_kernel(KArgs A, SeedRec *out, 
             const uint64_t canon = comp ? rcv : f;
             const uint32_t table = (uint32_t)(canon >> 32);
             const uint32_t key = (uint32_t)canon;
-            const uint64_t size = A.tableSize[table];
+            const uint32_t size = (uint32_t)A.tableSize[table];   // < 2^31 (snapgpu_aligner_create)
             const uint32_t *T = A.slots + 3 * A.tableBase[table];
-            const uint64_t h0 = fmix32(key) % size;
+            const uint32_t h0 = fmix32(key) % size;
             bool found = false;
             uint32_t v1 = 0, v2 = 0, probes = 0;
             for (uint32_t j = 0;; j++) {   // SNAPHashTable::Lookup probe order
                 if (j > size + 5) { probes = j; break; }
-                const uint64_t S_j = j <= 4 ? (uint64_t)j * (j + 1) * (2 * j + 1) / 6 : 30 + (uint64_t)(j - 4);
-                const uint64_t pos = (h0 + S_j) % size;
+                const uint32_t S_j = j <= 4 ? j * (j + 1) * (2 * j + 1) / 6 : 30 + (j - 4);
+                uint64_t pos = h0 + S_j;
+                if (pos >= size) pos %= size;
                 const uint32_t kj = T[3 * pos], v1j = T[3 * pos + 1];
                 const bool stop = (j == 0) ? (kj == key && v1j != INVALID) : (kj == key || v1j == INVALID);
                 if (stop) {
