@@ -233,6 +233,8 @@ struct Lds {
     uint32_t nElems;
     uint32_t pad_[3];
     alignas(16) uint32_t sk[SKCAP];                 // selection keys of elements < SKCAP
+    uint32_t ekey[SKCAP];                           // element key / hash-chain link of elements < SKCAP
+    uint16_t enext[SKCAP];                          //   (0xffff = end of chain)
     uint64_t seedUsed[NB + 1];                      // BaseAligner::seedUsed bit vector
     int16_t btAct[BYTE_PATH ? MAX_K + 1 : 1];       // LV backtrace scratch (byte path)
     int16_t btMatched[BYTE_PATH ? MAX_K + 1 : 1];
@@ -617,13 +619,22 @@ __device__ __forceinline__ bool overdue(ReadState &st, uint32_t site) {
 
 __device__ __forceinline__ uint32_t elem_hash(uint32_t key) { return (key * 2654435761u) >> (32 - NBUCKET_LOG2); }
 
-// find element with `key`; NONE if absent
-template <typename E>
-__device__ __forceinline__ uint32_t chain_find(const uint32_t *head, const E *ar, uint32_t key, uint32_t cap) {
-    uint32_t e = head[elem_hash(key)];
-    for (uint32_t steps = 0; e != NONE && ar[e].key != key; steps++) {
+// find element with `key`; NONE if absent.  Elements < SKCAP keep (key, next) in LDS
+// (next always points to an older, smaller index), so most walks never touch HBM.
+template <int MAXLEN>
+__device__ __forceinline__ uint32_t chain_find(const Lds<MAXLEN> &S, const ElemOf<MAXLEN> *ar, uint32_t key,
+                                               uint32_t cap) {
+    uint32_t e = S.head[elem_hash(key)];
+    for (uint32_t steps = 0; e != NONE; steps++) {
         if (steps > cap) { diag_report(DIAG_CHAIN, key, e); return NONE; }
-        e = ar[e].next;
+        if (e < SKCAP) {
+            if (S.ekey[e] == key) break;
+            const uint32_t nx = S.enext[e];
+            e = nx == 0xffffu ? NONE : nx;
+        } else {
+            if (ar[e].key == key) break;
+            e = ar[e].next;
+        }
     }
     return e;
 }

@@ -440,7 +440,7 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<128> &S, Elem128 
         if (take) {
             const uint32_t nl = elemLoc + (2 * (elemLoc % ELEM / (ELEM / 2)) - 1) * (ELEM / 2);
             const uint32_t nkey = ((nl / ELEM) << 1) | dir;
-            nb2 = uni(chain_find(S.head, ar, nkey, (uint32_t)A.arenaElems));
+            nb2 = uni(chain_find(S, ar, nkey, (uint32_t)A.arenaElems));
         }
         if (nb2 != NONE) {
             // the nearby element may be in this batch: its cache is authoritative

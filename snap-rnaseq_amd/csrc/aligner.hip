@@ -137,7 +137,7 @@ __device__ __forceinline__ bool score_wave(const KArgs &A, Lds<MAXLEN> &S, Elem5
                 if (sc != FAIL_SCORE) {
                     uint32_t nl = elemLoc + (2 * (elemLoc % ELEM / (ELEM / 2)) - 1) * (ELEM / 2);
                     uint32_t nkey = ((nl / ELEM) << 1) | dir;
-                    nb = uni(chain_find(S.head, ar, nkey, (uint32_t)A.arenaElems));
+                    nb = uni(chain_find(S, ar, nkey, (uint32_t)A.arenaElems));
                 }
                 if (nb != NONE) {
                     const uint32_t *nw = (const uint32_t *)(ar + nb);
@@ -238,7 +238,7 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
         if (leader) {
             S.btKey[slot] = NONE;
             S.btMask[slot] = 0;
-            uint32_t e = chain_find(S.head, ar, key, (uint32_t)A.arenaElems);
+            uint32_t e = chain_find(S, ar, key, (uint32_t)A.arenaElems);
             if (e != NONE || allowAlloc) {
                 uint64_t used = 0;
                 uint32_t weight = 0, allScored = 0, sortkey = 0;
@@ -261,7 +261,9 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
                         ne->bestScore = UNUSED_SCORE;
                         ne->bestLoc = 0;
                         ne->prob = 0;
-                        ne->next = atomicExch(&S.head[elem_hash(key)], e);
+                        const uint32_t old = atomicExch(&S.head[elem_hash(key)], e);
+                        if (e < SKCAP) { S.ekey[e] = key; S.enext[e] = (uint16_t)(old == NONE ? 0xffffu : old); }
+                        else ne->next = old;
                         used = 1ull << bit;
                         weight = 1;
                         allScored = 0;
