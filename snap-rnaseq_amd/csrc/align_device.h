@@ -52,6 +52,10 @@ struct DevTables {
     uint32_t wrap[32];        // GetWrappedNextSeedToTest order (SeedSequencer.h)
     double mapqT[72];         // mapqT[q] = 10^(-q/10) (glibc pow): MAPQ thresholds, no device log10
 };
+// The seedLen-independent tables (indel, phred, perfect, mapqT), one copy per device, set
+// once by the host: a global's address is a constant the compiler rematerializes, where a
+// table pointer argument is one more SGPR pair to keep live (and spill) in the scorer.
+__device__ DevTables g_tab;
 
 // HashTableElement (BaseAligner.h:188-214) in the HBM arena: a 48-byte header of
 // the fields the kernels read and write, then the per-candidate seed offsets.  Reads
@@ -340,7 +344,7 @@ __device__ __forceinline__ LvOut lv_wave(const Bitmap<NB> &F, int p0, int patter
     }
     if (L0 == end0) {
         int result = patternLen > end0 ? patternLen - end0 : 0;
-        r.prob = tab->perfect[patternLen];
+        r.prob = g_tab.perfect[patternLen];
         r.score = result > k ? -1 : result;
         return r;
     }
@@ -403,21 +407,21 @@ __device__ __forceinline__ LvOut lv_wave(const Bitmap<NB> &F, int p0, int patter
                 int a = unii(btAct[ce]);
                 int cnt = 1;
                 while (ce + 1 <= e && unii(btMatched[ce]) == 0 && unii(btAct[ce + 1]) == a) { cnt++; ce++; }
-                if (a == 2) { p *= tab->indel[cnt]; offset += cnt; net += cnt; }
-                else if (a == 1) { p *= tab->indel[cnt]; offset -= cnt; net -= cnt; }
+                if (a == 2) { p *= g_tab.indel[cnt]; offset += cnt; net += cnt; }
+                else if (a == 1) { p *= g_tab.indel[cnt]; offset -= cnt; net -= cnt; }
                 else {
                     for (int q = 0; q < cnt; q++) {
                         int qi = offset < 0 ? 0 : offset;
                         if (qi > patternLen - 1) qi = patternLen - 1;
                         uint32_t qc = uni((uint8_t)qual[p0 + DIR * qi]);
-                        p *= tab->phred[qc];
+                        p *= g_tab.phred[qc];
                         offset++;
                     }
                 }
                 offset += unii(btMatched[ce]);
                 ce++;
             }
-            p *= tab->perfect[patternLen - e];
+            p *= g_tab.perfect[patternLen - e];
             r.score = e;
             r.prob = p;
             r.netIndel = net;
@@ -567,10 +571,10 @@ __device__ __forceinline__ int mapq_dev(const DevTables *tab, double pAll, doubl
         int lo = 0, hi = 69;                 // largest q in [0, 69] with x <= T[q] (T[0] = 1 >= x)
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
-            if (x <= tab->mapqT[mid]) lo = mid; else hi = mid - 1;
+            if (x <= g_tab.mapqT[mid]) lo = mid; else hi = mid - 1;
         }
         mq = lo;
-        const double t0 = tab->mapqT[lo], t1 = tab->mapqT[lo + 1];
+        const double t0 = g_tab.mapqT[lo], t1 = g_tab.mapqT[lo + 1];
         if (fabs(x - t0) <= 1e-9 * t0 || fabs(x - t1) <= 1e-9 * t1) *flags |= SNAPGPU_FLAG_MAPQ_FIXED;
     }
     int pen = (int)popular - 10;
@@ -593,17 +597,22 @@ __device__ __forceinline__ void diag_report(uint32_t code, uint32_t a, uint32_t 
 
 struct ReadState {
     uint32_t lps[2], mostSeeds[2], nSeedsApplied[2];
-    uint32_t bestScore, bestLoc, scoreLimit, popular;
+    uint32_t bestScore, bestLoc, scoreLimit;
     double pAll, pBest;
     uint32_t outLoc, outDir;
     int32_t outScore, outMapq;
     uint32_t ts;                 // running hit counter (FIFO timestamps)
-    uint32_t nLookups, nScored, nHitsIgnored, nProbes, nHitWords, nOvf, nElems;
+    uint32_t statv;              // per-read counters, one per lane (SV_*): a VGPR instead of 6 SGPRs
     uint32_t rid;                // read index (watchdog reports)
     uint32_t abort;              // watchdog tripped: finish the read now
     uint32_t tick;               // overdue(): calls left until the next clock read
     uint64_t t0;                 // s_memrealtime at read start
 };
+
+// per-read statistics: lane SV_x of ReadState::statv
+enum : int { SV_LOOKUPS = 0, SV_SCORED = 1, SV_POPULAR = 2, SV_PROBES = 3, SV_HITWORDS = 4, SV_OVF = 5 };
+__device__ __forceinline__ void sv_add(ReadState &st, int lane, int idx, uint32_t v) { st.statv += lane == idx ? v : 0u; }
+__device__ __forceinline__ uint32_t sv_get(const ReadState &st, int idx) { return readlaneu(st.statv, idx); }
 
 // time watchdog: true (once reported) when the read has overrun its deadline.  The
 // clock (an SMEM round trip) is read on every 32nd call only.

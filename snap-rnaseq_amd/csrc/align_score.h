@@ -230,9 +230,9 @@ __device__ __forceinline__ void lv_prob_pair(const DevTables *tab, const GroupLd
     if (qi > patternLen - 1) qi = patternLen - 1;
     const int DIR = dx ? -1 : 1;
     double f = 1.0;
-    if (valid && a == 0) f = tab->phred[(uint8_t)qual[p0 + DIR * qi]];
-    else if (runEnd) f = tab->indel[cnt];
-    const double perf = lane == 0 || lane == 32 ? tab->perfect[patternLen - e] : 1.0;
+    if (valid && a == 0) f = g_tab.phred[(uint8_t)qual[p0 + DIR * qi]];
+    else if (runEnd) f = g_tab.indel[cnt];
+    const double perf = lane == 0 || lane == 32 ? g_tab.perfect[patternLen - e] : 1.0;
     const int e1 = G.plen[0][g], e2 = G.plen[1][g];
     double q = 1.0;
     for (int i = 0; i < e1; i++) q *= readlaned(f, i);
@@ -249,7 +249,7 @@ __device__ __forceinline__ void finalize_read(const KArgs &A, ReadState &st, int
     st.outScore = (int32_t)st.bestScore;
     if (st.bestScore <= A.maxK) {
         st.outLoc = st.bestLoc;
-        const int mq = mapq_dev(A.tab, st.pAll, st.pBest, st.bestScore, st.popular, flags);
+        const int mq = mapq_dev(A.tab, st.pAll, st.pBest, st.bestScore, sv_get(st, SV_POPULAR), flags);
         st.outMapq = mq;
         *result = mq >= 10 ? SNAPGPU_SINGLE_HIT : SNAPGPU_MULTIPLE_HITS;
     } else {
@@ -398,7 +398,7 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<128> &S, Elem128 
                 ec[4] = 0u;
                 ec[5] = 0u;
             }
-            st.nScored += (uint32_t)__popcll(fm);
+            sv_add(st, lane, SV_SCORED, (uint32_t)__popcll(fm));
             wave_sync();
         }
         if (gs >= m) {
@@ -430,7 +430,7 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<128> &S, Elem128 
         const bool anyNearby0 = cScored != 0;
         cScored |= 1ull << cbit;
         record_hit<EXT>(A, loc, dir, sc);
-        st.nScored++;
+        sv_add(st, lane, SV_SCORED, 1);
         g0 = gs + 1;
         const bool passA = !(anyNearby0 && (cBest < sc || (cBest == sc && prob <= cProb)));
         bool take = passA;

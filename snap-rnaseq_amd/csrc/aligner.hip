@@ -45,7 +45,7 @@ __device__ __forceinline__ bool score_wave(const KArgs &A, Lds<MAXLEN> &S, Elem5
                 st.outScore = (int32_t)st.bestScore;
                 if (st.bestScore <= A.maxK) {
                     st.outLoc = st.bestLoc;
-                    const int mq = mapq_dev(A.tab, st.pAll, st.pBest, st.bestScore, st.popular, flags);
+                    const int mq = mapq_dev(A.tab, st.pAll, st.pBest, st.bestScore, sv_get(st, SV_POPULAR), flags);
                     st.outMapq = mq;
                     *result = mq >= 10 ? SNAPGPU_SINGLE_HIT : SNAPGPU_MULTIPLE_HITS;
                 } else {
@@ -128,7 +128,7 @@ __device__ __forceinline__ bool score_wave(const KArgs &A, Lds<MAXLEN> &S, Elem5
                     }
                 }
                 if (sc != FAIL_SCORE) record_hit<EXT>(A, loc, dir, sc);
-                st.nScored++;
+                sv_add(st, lane, SV_SCORED, 1);
                 if (anyNearby) {
                     if (ebest < sc || (ebest == sc && prob <= eprob)) continue;
                 }
@@ -309,8 +309,8 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
     const uint32_t seedLen = A.seedLen;
     ReadState st;
     st.outLoc = INVALID; st.outDir = 0; st.outScore = (int32_t)UNUSED_SCORE; st.outMapq = 0;
-    st.popular = 0; st.pAll = 0; st.pBest = 0;
-    st.nLookups = st.nScored = st.nHitsIgnored = st.nProbes = st.nHitWords = st.nOvf = 0;
+    st.pAll = 0; st.pBest = 0;
+    st.statv = 0;
     st.ts = 0;
     st.rid = r;
     st.abort = 0;
@@ -450,7 +450,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
                     pre = (meta >> 31) && (meta & 0xff) == next && ((meta >> 16) & 0x7fff) != 0x7fff;
                     if (pre) {
                         found = (meta >> 8) & 1; comp = (meta >> 9) & 1; pal = (meta >> 10) & 1;
-                        st.nProbes += (meta >> 16) & 0x7fff;
+                        sv_add(st, lane, SV_PROBES, (meta >> 16) & 0x7fff);
                         v1 = readlaneu(srec, 4 * pfIdx + 1);
                         v2 = readlaneu(srec, 4 * pfIdx + 2);
                         pcnt = readlaneu(srec, 4 * pfIdx + 3);
@@ -488,7 +488,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
                         int jl = __builtin_ctzll(m);
                         uint32_t jj = j0 + jl;
                         bool bey = readlane(beyond ? 1 : 0, jl);
-                        st.nProbes += bey ? jj : jj + 1;
+                        sv_add(st, lane, SV_PROBES, bey ? jj : jj + 1);
                         uint32_t kv1 = readlaneu(v1j, jl);
                         if (!bey && (jj == 0 || kv1 != INVALID)) { found = true; v1 = kv1; v2 = readlaneu(v2j, jl); }
                         break;
@@ -506,7 +506,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
                         uint32_t o = vf - A.nBases;
                         nH0 = pre ? (pcnt & 0xffff) : uni(A.overflow[o]);
                         ls0 = A.overflow + o + 1;
-                        st.nOvf++;
+                        sv_add(st, lane, SV_OVF, 1);
                     }
                     if (pal) { nH1 = nH0; sg1 = sg0; ls1 = ls0; }   // palindrome (GenomeIndex.cpp:1003-1006)
                     else if (vr < A.nBases) { nH1 = 1; sg1 = vr; }
@@ -514,7 +514,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
                         uint32_t o = vr - A.nBases;
                         nH1 = pre ? (pcnt >> 16) : uni(A.overflow[o]);
                         ls1 = A.overflow + o + 1;
-                        st.nOvf++;
+                        sv_add(st, lane, SV_OVF, 1);
                     }
                     if (windowed) {   // the hits within [minSeedLoc, maxSeedLoc] (GenomeIndex.cpp:1029-1078)
                         for (int sd = 0; sd < 2; sd++) {
@@ -531,7 +531,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
                         }
                     }
                 }
-                st.nLookups++;
+                sv_add(st, lane, SV_LOOKUPS, 1);
                 PH_ADD(A, S, PH_LOOKUP, tlk);
                 bool applied = false;
     #pragma unroll
@@ -539,12 +539,11 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
                     const uint32_t nh = dir ? nH1 : nH0;
                     if (EXT && radius && dir != sDir) continue;   // BaseAligner.cpp:781-786
                     if (nh > A.maxHits && !A.explore) {
-                        st.nHitsIgnored++;
-                        st.popular++;
+                        sv_add(st, lane, SV_POPULAR, 1);   // popularSeedsSkipped == nHitsIgnored per read
                     } else {
                         uint32_t offset = dir == 0 ? next : n - seedLen - next;
                         uint32_t lim = nh < A.maxHits ? nh : A.maxHits;
-                        st.nHitWords += lim;
+                        sv_add(st, lane, SV_HITWORDS, lim);
                         PH_T(A, tins);
                         insert_hits<MAXLEN, EXT>(A, S, ar, st, dir, offset, lim, dir ? ls1 : ls0, dir ? sg1 : sg0,
                                             numWeightLists, dir ? st.lps[1] : st.lps[0], minLoc, maxLoc);
@@ -568,6 +567,9 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
         PH_ADD(A, S, PH_SEEDLOOP, tsl);
     }
     PH_T(A, tout);
+    const uint32_t svLookups = sv_get(st, SV_LOOKUPS), svScored = sv_get(st, SV_SCORED);
+    const uint32_t svPopular = sv_get(st, SV_POPULAR), svProbes = sv_get(st, SV_PROBES);
+    const uint32_t svHitWords = sv_get(st, SV_HITWORDS), svOvf = sv_get(st, SV_OVF);
     if (lane == 0) {
         snapgpu_result_t o;
         o.location = st.outLoc;
@@ -577,13 +579,13 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
         o.direction = (uint8_t)st.outDir;
         o.flags = (uint8_t)flags;
         o.reserved = 0;
-        o.nLookups = st.nLookups;
-        o.nLocationsScored = st.nScored;
-        o.popularSeedsSkipped = (uint16_t)st.popular;
-        o.nHitsIgnored = (uint16_t)st.nHitsIgnored;
-        o.nProbes = st.nProbes;
-        o.nHitWords = st.nHitWords;
-        o.nOverflowLists = st.nOvf;
+        o.nLookups = svLookups;
+        o.nLocationsScored = svScored;
+        o.popularSeedsSkipped = (uint16_t)svPopular;
+        o.nHitsIgnored = (uint16_t)svPopular;
+        o.nProbes = svProbes;
+        o.nHitWords = svHitWords;
+        o.nOverflowLists = svOvf;
         o.nElements = run ? S.nElems : 0;
         o.reserved2 = 0;
         o.probabilityOfAllCandidates = st.pAll;
@@ -708,6 +710,20 @@ void fillTables(DevTables &t, uint32_t seedLen) {
         for (int i = 0; i < 25; i++) t.wrap[i] = kWrap[seedLen - 16][i];
 }
 
+// g_tab (align_device.h) on the current device, once per device per process
+hipError_t ensureDeviceTables(int device) {
+    static std::mutex mu;
+    static bool done[64] = {};
+    std::lock_guard<std::mutex> lk(mu);
+    if (device < 0 || device >= 64) return hipErrorInvalidDevice;
+    if (done[device]) return hipSuccess;
+    DevTables t;
+    fillTables(t, 20);   // the seedLen-dependent fields (seedProb, wrap) are read from KArgs::tab
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_tab), &t, sizeof(t), 0, hipMemcpyHostToDevice);
+    if (e == hipSuccess) done[device] = true;
+    return e;
+}
+
 uint32_t packedCode(char c) {   // 2-bit code of the packed genome (4 = not ACGT)
     return c == 'A' ? 0u : c == 'C' ? 1u : c == 'G' ? 2u : c == 'T' ? 3u : 4u;
 }
@@ -824,6 +840,7 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
     if ((e = hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking)) != hipSuccess) return fail("stream", e);
     for (auto &ev : a->ev) if ((e = hipEventCreate(&ev)) != hipSuccess) return fail("event", e);
     if ((e = hipGetSymbolAddress((void **)&a->dDiag, HIP_SYMBOL(g_diag))) != hipSuccess) return fail("g_diag", e);
+    if ((e = ensureDeviceTables(device)) != hipSuccess) return fail("device tables", e);
     // index upload: genome with guards, tables, overflow, pieces
     const uint32_t nBases = idx->genome->nBases;
     size_t gbytes = kDevGuard + nBases + kDevGuard;
@@ -1201,6 +1218,7 @@ int snapgpu_lv_batch(int device, int direction, uint32_t n, const char *texts, c
     int ndev = snapgpu_device_count();
     if (ndev <= 0 || device >= ndev) { snapgpu::setError("no such HIP device"); return SNAPGPU_EDEVICE; }
     HIPCHK(hipSetDevice(device));
+    HIPCHK(ensureDeviceTables(device));
     std::vector<LvTask> tasks(n);
     std::vector<char> rbuf, qbuf, gbuf;
     const int PADG = 512;
