@@ -12,7 +12,7 @@ import os
 import shutil
 import sys
 
-KERNEL = "align_kernel<128>"
+KERNEL = "align_kernel<128, false>"
 
 
 def per_launch(path):
