@@ -37,9 +37,10 @@ constexpr uint32_t UNUSED_SCORE = 0xffffu;
 constexpr uint32_t FAIL_SCORE = 0xffffffffu;
 constexpr int ELEM = 48;                  // hashTableElementSize == maxMergeDist
 constexpr uint32_t NPAD = 100;            // Genome::N_PADDING
-constexpr int NBUCKET_LOG2 = 9;
+constexpr int NBUCKET_LOG2 = 8;
 constexpr int NBUCKET = 1 << NBUCKET_LOG2;  // element hash buckets (LDS)
 constexpr uint32_t SKCAP = 256;           // selection keys kept in LDS
+constexpr uint32_t MIRCAP = 128;          // elements whose key / chain link are mirrored in LDS
 constexpr int ELEM_DWORDS = 36;           // dwords of Elem512 (byte path)
 constexpr int BT = 128;                   // insertion-batch dedupe table (LDS)
 constexpr uint32_t NONE = 0xffffffffu;
@@ -205,7 +206,7 @@ __device__ __forceinline__ uint32_t complement_of(uint32_t c) {   // BaseAligner
 constexpr int64_t PACK_GUARD = 1024;     // bit-plane word 0 = genome position -1024
 constexpr int EB = 8;                    // elements popped per batch (forced mode)
 constexpr int CANDCAP = EB * ELEM;       // candidate list capacity
-constexpr uint32_t ORDCAP = 512;         // forced-mode pop order (u16, overlays Lds::btMask)
+constexpr uint32_t ORDCAP = 256;         // forced-mode pop order (u16)
 
 // Scorer state of align_kernel<128> (align_score.h).
 struct GroupLds {
@@ -213,7 +214,6 @@ struct GroupLds {
     uint32_t ecache[EB][24];             // popped Elem128s (authoritative while in the batch)
     uint32_t eidx[EB];
     uint16_t cand[CANDCAP];              // slot << 8 | bit
-    uint8_t rows8[MAX_K][WAVE];          // LV rows: L + 2 per (row, lane); actions are recomputed
     int16_t pm[2][128];                  // LV path per [direction][group*2*GS + row]: matched-run length
     int8_t pa[2][128];                   //   and action (0 X, 1 D, 2 I); probabilities in apply
     int16_t pL0[2][8];                   //   exact prefix L[0][0] per group
@@ -230,15 +230,25 @@ struct Lds {
     char rcQ[MAXLEN + 64];
     uint32_t win[BYTE_PATH ? (MAXLEN + 192) / 4 : 1];   // genome window [g-64, g+n+64+64)
     uint32_t head[NBUCKET];                         // element hash chains
-    uint32_t btKey[BT];
-    uint64_t btMask[BT];
+    // hit insertion and scoring never overlap in time: their scratch shares LDS (the
+    // insertion table is cleared again after every score call that used it)
+    union {
+        struct {
+            uint32_t btKey[BT];
+            uint64_t btMask[BT];
+            uint32_t scrLoc[WAVE];                  // batch scratch: hit location per lane
+        } ins;
+        struct {
+            uint8_t rows8[BYTE_PATH ? 1 : MAX_K][WAVE];   // LV rows (L + 2 per row, lane); actions recomputed
+            uint16_t order[ORDCAP];                 // forced-mode pop order
+        } sc;
+    } u;
     uint64_t laneMax[WAVE];                         // per-owner-lane max (sortkey<<32 | idx)
-    uint32_t scrLoc[WAVE];                          // batch scratch: hit location per lane
     uint32_t nElems;
     uint32_t pad_[3];
     alignas(16) uint32_t sk[SKCAP];                 // selection keys of elements < SKCAP
-    uint32_t ekey[SKCAP];                           // element key / hash-chain link of elements < SKCAP
-    uint16_t enext[SKCAP];                          //   (0xffff = end of chain)
+    uint32_t ekey[MIRCAP];                          // element key / hash-chain link of elements < MIRCAP
+    uint16_t enext[MIRCAP];                         //   (0xffff = end of chain)
     uint64_t seedUsed[NB + 1];                      // BaseAligner::seedUsed bit vector
     int16_t btAct[BYTE_PATH ? MAX_K + 1 : 1];       // LV backtrace scratch (byte path)
     int16_t btMatched[BYTE_PATH ? MAX_K + 1 : 1];
@@ -628,7 +638,7 @@ __device__ __forceinline__ bool overdue(ReadState &st, uint32_t site) {
 
 __device__ __forceinline__ uint32_t elem_hash(uint32_t key) { return (key * 2654435761u) >> (32 - NBUCKET_LOG2); }
 
-// find element with `key`; NONE if absent.  Elements < SKCAP keep (key, next) in LDS
+// find element with `key`; NONE if absent.  Elements < MIRCAP keep (key, next) in LDS
 // (next always points to an older, smaller index), so most walks never touch HBM.
 template <int MAXLEN>
 __device__ __forceinline__ uint32_t chain_find(const Lds<MAXLEN> &S, const ElemOf<MAXLEN> *ar, uint32_t key,
@@ -636,7 +646,7 @@ __device__ __forceinline__ uint32_t chain_find(const Lds<MAXLEN> &S, const ElemO
     uint32_t e = S.head[elem_hash(key)];
     for (uint32_t steps = 0; e != NONE; steps++) {
         if (steps > cap) { diag_report(DIAG_CHAIN, key, e); return NONE; }
-        if (e < SKCAP) {
+        if (e < MIRCAP) {
             if (S.ekey[e] == key) break;
             const uint32_t nx = S.enext[e];
             e = nx == 0xffffu ? NONE : nx;

@@ -99,7 +99,7 @@ __device__ __forceinline__ int from_upper(int v, bool glast) {
 // 376-431) in G.pa / G.pm / G.pL0 / G.plen[dx]; the match probability is formed
 // later, only for candidates the scorer applies (lv_prob).
 template <int DIR, int GS>
-__device__ __forceinline__ int lv_group(GroupLds &G, const Mask128 &M, bool gact, int q0, int patternLen,
+__device__ __forceinline__ int lv_group(GroupLds &G, uint8_t (*rows8)[WAVE], const Mask128 &M, bool gact, int q0, int patternLen,
                                         int textLen, int k, int kmaxAll, int &outE) {
     constexpr int dx = DIR > 0 ? 0 : 1;
     const int lane = lane_id();
@@ -145,7 +145,7 @@ __device__ __forceinline__ int lv_group(GroupLds &G, const Mask128 &M, bool gact
         const int slid = f < endd ? f : endd;
         const int bnew = best < endd ? slid : (fa == mposc ? best : endd);
         const int Ln = active ? bnew : Lp;
-        if (active) G.rows8[e][lane] = (uint8_t)(bnew + 2);
+        if (active) rows8[e][lane] = (uint8_t)(bnew + 2);
         (void)act;
         const uint64_t hit = ballot(active && Ln == patternLen);
         if (hit) {
@@ -165,7 +165,7 @@ __device__ __forceinline__ int lv_group(GroupLds &G, const Mask128 &M, bool gact
                 auto val = [&](int r, int dd) -> int {   // L[r][dd] as the row step saw it
                     if (r == 0) return dd == 0 ? L0 : -2;
                     if (dd > r || dd < -r) return -2;
-                    return (int)G.rows8[r][gi * GS + (DIR > 0 ? c + dd : c - dd)] - 2;
+                    return (int)rows8[r][gi * GS + (DIR > 0 ? c + dd : c - dd)] - 2;
                 };
                 int curD = wd;
                 for (int ce = e; ce >= 1; ce--) {
@@ -331,7 +331,7 @@ __device__ __forceinline__ void lv_pass(const KArgs &A, Lds<128> &S, uint32_t i0
     PH_ADD(A, S, PH_STAGE, tst);
     PH_T(A, tf);
     const int t = P.s + (int)A.seedLen;
-    const int rf = lv_group<1, GS>(G, F, P.act, t, (int)n - t, P.glen - t, k, k, e1);
+    const int rf = lv_group<1, GS>(G, S.u.sc.rows8, F, P.act, t, (int)n - t, P.glen - t, k, k, e1);
     PH_ADD(A, S, PH_LVF, tf);
     PH_CNT(A, S, PH_ROWSF, rf);
     PH_CNT(A, S, GS <= 16 ? PH_NPASS16 : (GS == 32 ? PH_NPASS32 : PH_NPASS64), 1);
@@ -343,7 +343,7 @@ __device__ __forceinline__ void lv_pass(const KArgs &A, Lds<128> &S, uint32_t i0
     if (kmax2 >= 0) {
         // reverse LV: pattern = read[s-1 .. 0], text = genome backwards from loc+s-1 (BaseAligner.cpp:1216-1220)
         const Mask128 R = mk_reverse(F);
-        const int rr = lv_group<-1, GS>(G, R, ract, 127 - (P.s - 1), P.s, P.s + MAX_K, k2, kmax2, e2);
+        const int rr = lv_group<-1, GS>(G, S.u.sc.rows8, R, ract, 127 - (P.s - 1), P.s, P.s + MAX_K, k2, kmax2, e2);
         PH_CNT(A, S, PH_ROWSR, rr);
     }
     PH_ADD(A, S, PH_LVR, tr);
@@ -522,7 +522,7 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<128> &S, Elem1
     // Forced mode pops every linked element in descending sort-key order and the read
     // ends with it, so the order is computed once (ranks, ORDCAP at a time) and the
     // elements are not unlinked one by one.
-    uint16_t *order = reinterpret_cast<uint16_t *>(S.btMask);   // insertion scratch is idle now
+    uint16_t *order = S.u.sc.order;
     uint32_t fDone = 0, fAvail = 0, ordBase = 0;
     for (uint32_t guard = 0;; guard++) {
         if (guard > (uint32_t)A.arenaElems) {   // every batch unlinks >= 1 element

@@ -217,12 +217,12 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
         valid = valid && h >= offset;
         if constexpr (EXT) valid = valid && loc >= minLoc && loc <= maxLoc;   // BaseAligner.cpp:849-853
         uint32_t key = ((loc / ELEM) << 1) | dir;
-        S.scrLoc[lane] = loc;
+        S.u.ins.scrLoc[lane] = loc;
         uint32_t slot = 0;
         if (valid) {
             uint32_t s = (key * 2654435761u) >> 25;
             for (int probe = 0;; probe++) {
-                uint32_t old = atomicCAS(&S.btKey[s], NONE, key);
+                uint32_t old = atomicCAS(&S.u.ins.btKey[s], NONE, key);
                 if (old == NONE || old == key) break;
                 if (probe >= BT) { diag_report(DIAG_BATCH_TABLE, st.rid, key); valid = false; break; }
                 s = (s + 1) & (BT - 1);
@@ -230,14 +230,14 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
             slot = s;
         }
         wave_sync();
-        if (valid) atomicOr((unsigned long long *)&S.btMask[slot], 1ull << lane);
+        if (valid) atomicOr((unsigned long long *)&S.u.ins.btMask[slot], 1ull << lane);
         wave_sync();
-        uint64_t grp = valid ? S.btMask[slot] : 0;
+        uint64_t grp = valid ? S.u.ins.btMask[slot] : 0;
         bool leader = valid && (__builtin_ctzll(grp) == lane);
         wave_sync();
         if (leader) {
-            S.btKey[slot] = NONE;
-            S.btMask[slot] = 0;
+            S.u.ins.btKey[slot] = NONE;
+            S.u.ins.btMask[slot] = 0;
             uint32_t e = chain_find(S, ar, key, (uint32_t)A.arenaElems);
             if (e != NONE || allowAlloc) {
                 uint64_t used = 0;
@@ -249,7 +249,7 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
                 while (m) {
                     int j = __builtin_ctzll(m);
                     m &= m - 1;
-                    uint32_t bit = S.scrLoc[j] % ELEM;
+                    uint32_t bit = S.u.ins.scrLoc[j] % ELEM;
                     uint32_t t = st.ts + b0 + j;
                     if (e == NONE) {
                         // allocateNewCandidate (BaseAligner.cpp:1485-1568): tail of weight list 1
@@ -262,7 +262,7 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
                         ne->bestLoc = 0;
                         ne->prob = 0;
                         const uint32_t old = atomicExch(&S.head[elem_hash(key)], e);
-                        if (e < SKCAP) { S.ekey[e] = key; S.enext[e] = (uint16_t)(old == NONE ? 0xffffu : old); }
+                        if (e < MIRCAP) { S.ekey[e] = key; S.enext[e] = (uint16_t)(old == NONE ? 0xffffu : old); }
                         else ne->next = old;
                         used = 1ull << bit;
                         weight = 1;
@@ -368,7 +368,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
             if (A.hasIupac && other) { defer_read(A, r); return; }
         }
         for (int i = lane; i < NBUCKET; i += WAVE) S.head[i] = NONE;
-        for (int i = lane; i < BT; i += WAVE) { S.btKey[i] = NONE; S.btMask[i] = 0; }
+        for (int i = lane; i < BT; i += WAVE) { S.u.ins.btKey[i] = NONE; S.u.ins.btMask[i] = 0; }
         S.laneMax[lane] = 0;
         if (lane == 0) S.nElems = 0;
         wave_sync();
@@ -559,7 +559,13 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
             PH_T(A, tsc);
             bool fin;
             if constexpr (Lds<MAXLEN>::BYTE_PATH) fin = score_wave<MAXLEN, EXT>(A, S, ar, st, force, n, rbF, rbR, &result, &flags);
-            else fin = score_batched<EXT>(A, S, ar, st, force, n, &result, &flags);
+            else {
+                fin = score_batched<EXT>(A, S, ar, st, force, n, &result, &flags);
+                if (!fin && !force) {   // the scorer's LV rows overlay the insertion table
+                    for (int i = lane; i < BT; i += WAVE) { S.u.ins.btKey[i] = NONE; S.u.ins.btMask[i] = 0; }
+                    wave_sync();
+                }
+            }
             PH_ADD(A, S, PH_SCORE, tsc);
             if (fin || force) { fillHits = !wrapForced; break; }
             if (overdue(st, 8)) break;
@@ -600,7 +606,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
 template <int MAXLEN, bool EXT>
 // amdgpu_waves_per_eu(3): keep <= 168 VGPRs (3 waves/SIMD, 12 per CU); a few cold spills
 // are cheaper than dropping to 2 waves/SIMD.
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void align_kernel(KArgs A) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MAXLEN == 128 ? 4 : 3))) void align_kernel(KArgs A) {
     __shared__ Lds<MAXLEN> S;
     ElemOf<MAXLEN> *ar = reinterpret_cast<ElemOf<MAXLEN> *>(A.arena) + (uint64_t)blockIdx.x * A.arenaElems;
     const int lane = lane_id();
