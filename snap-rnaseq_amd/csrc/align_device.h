@@ -40,7 +40,7 @@ constexpr uint32_t NPAD = 100;            // Genome::N_PADDING
 constexpr int NBUCKET_LOG2 = 8;
 constexpr int NBUCKET = 1 << NBUCKET_LOG2;  // element hash buckets (LDS)
 constexpr uint32_t SKCAP = 256;           // selection keys kept in LDS
-constexpr uint32_t MIRCAP = 128;          // elements whose key / chain link are mirrored in LDS
+constexpr uint32_t MIRCAP = 256;          // elements whose key / chain link are mirrored in LDS
 constexpr int ELEM_DWORDS = 36;           // dwords of Elem512 (byte path)
 constexpr int BT = 128;                   // insertion-batch dedupe table (LDS)
 constexpr uint32_t NONE = 0xffffffffu;

@@ -200,19 +200,29 @@ __device__ __forceinline__ bool score_wave(const KArgs &A, Lds<MAXLEN> &S, Elem5
 
 // ------------------------------------------------------------ hit insertion
 // The per-hit loop of BaseAligner.cpp:829-869 (findCandidate / incrementWeight /
-// allocateNewCandidate) for one seed in one direction.
+// allocateNewCandidate) for one seed, both directions in one pass: the forward hits
+// [0, lim0) then the reverse-complement hits [lim0, lim0 + lim1), the order and
+// timestamps of applying the directions one after the other (their elements never
+// coincide: the direction is part of the element key).
 template <int MAXLEN, bool EXT>
-__device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, ElemOf<MAXLEN> *ar, ReadState &st, uint32_t dir,
-                                            uint32_t offset, uint32_t lim, const uint32_t *list, uint32_t single,
-                                            uint32_t numWeightLists, uint32_t lpsNow, uint32_t minLoc,
+__device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, ElemOf<MAXLEN> *ar, ReadState &st,
+                                            uint32_t lim0, uint32_t lim1, uint32_t off0, uint32_t off1,
+                                            const uint32_t *list0, const uint32_t *list1, uint32_t single0,
+                                            uint32_t single1, uint32_t numWeightLists, uint32_t minLoc,
                                             uint32_t maxLoc) {
     const int lane = lane_id();
-    const bool allowAlloc = lpsNow <= st.scoreLimit;
+    const uint32_t lim = lim0 + lim1;
     for (uint32_t b0 = 0; b0 < lim; b0 += WAVE) {
         if (overdue(st, 5)) break;
-        uint32_t i = b0 + lane;
+        const uint32_t i = b0 + lane;
+        const uint32_t dir = i >= lim0 ? 1u : 0u;
+        const uint32_t ii = dir ? i - lim0 : i;
+        const uint32_t *list = dir ? list1 : list0;
+        const uint32_t offset = dir ? off1 : off0;
+        const uint32_t lpsNow = dir ? st.lps[1] : st.lps[0];
+        const bool allowAlloc = lpsNow <= st.scoreLimit;
         bool valid = i < lim;
-        uint32_t h = valid ? (list ? list[i] : single) : 0;
+        uint32_t h = valid ? (list ? list[ii] : (dir ? single1 : single0)) : 0;
         uint32_t loc = h - offset;
         valid = valid && h >= offset;
         if constexpr (EXT) valid = valid && loc >= minLoc && loc <= maxLoc;   // BaseAligner.cpp:849-853
@@ -534,23 +544,30 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
                 sv_add(st, lane, SV_LOOKUPS, 1);
                 PH_ADD(A, S, PH_LOOKUP, tlk);
                 bool applied = false;
-    #pragma unroll
+                uint32_t lims[2] = {0, 0};
+#pragma unroll
                 for (uint32_t dir = 0; dir < 2; dir++) {
                     const uint32_t nh = dir ? nH1 : nH0;
                     if (EXT && radius && dir != sDir) continue;   // BaseAligner.cpp:781-786
                     if (nh > A.maxHits && !A.explore) {
                         sv_add(st, lane, SV_POPULAR, 1);   // popularSeedsSkipped == nHitsIgnored per read
                     } else {
-                        uint32_t offset = dir == 0 ? next : n - seedLen - next;
-                        uint32_t lim = nh < A.maxHits ? nh : A.maxHits;
-                        sv_add(st, lane, SV_HITWORDS, lim);
-                        PH_T(A, tins);
-                        insert_hits<MAXLEN, EXT>(A, S, ar, st, dir, offset, lim, dir ? ls1 : ls0, dir ? sg1 : sg0,
-                                            numWeightLists, dir ? st.lps[1] : st.lps[0], minLoc, maxLoc);
-                        PH_ADD(A, S, PH_INSERT, tins);
-                        if (dir) st.nSeedsApplied[1]++; else st.nSeedsApplied[0]++;
+                        lims[dir] = nh < A.maxHits ? nh : A.maxHits;
+                        sv_add(st, lane, SV_HITWORDS, lims[dir]);
                         applied = true;
                     }
+                }
+                if (applied) {
+                    PH_T(A, tins);
+                    insert_hits<MAXLEN, EXT>(A, S, ar, st, lims[0], lims[1], next, n - seedLen - next, ls0, ls1, sg0,
+                                             sg1, numWeightLists, minLoc, maxLoc);
+                    PH_ADD(A, S, PH_INSERT, tins);
+                }
+#pragma unroll
+                for (uint32_t dir = 0; dir < 2; dir++) {   // nSeedsApplied (after both directions' hits)
+                    const uint32_t nh = dir ? nH1 : nH0;
+                    if (EXT && radius && dir != sDir) continue;
+                    if (!(nh > A.maxHits && !A.explore)) st.nSeedsApplied[dir]++;
                 }
                 next += seedLen;
                 if (!applied) continue;
