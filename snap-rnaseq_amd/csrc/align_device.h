@@ -674,6 +674,7 @@ template <int MAXLEN>
 __device__ __forceinline__ void recompute_lane_max(Lds<MAXLEN> &S, const ElemOf<MAXLEN> *ar, int lane) {
     uint64_t best = 0;
     const uint32_t nElems = S.nElems;
+#pragma unroll 1
     for (uint32_t e = lane; e < nElems; e += WAVE) {
         uint32_t k = sk_get(S, ar, e);
         uint64_t v = ((uint64_t)k << 32) | e;
