@@ -106,3 +106,18 @@ def test_aligner_fails_loudly_without_gpu():
     idx = snapgpu.GenomeIndex.build(g, 20, 1)
     with pytest.raises(snapgpu.SnapGpuError):
         snapgpu.BaseAligner(idx)
+
+
+def test_plain_c_caller(tmp_path):
+    """tests/c/abi_smoke.c: the header compiles as C99 (-Wall -Wextra -pedantic) and a C
+    program linked against the library runs the host-side entry points."""
+    import subprocess
+    exe = tmp_path / "abi_smoke"
+    libdir = os.path.dirname(_ffi.LIB_PATH)
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Wextra", "-pedantic", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "c", "abi_smoke.c"), "-o", str(exe), "-L", libdir, "-lsnapgpu",
+                    "-Wl,-rpath," + libdir], check=True)
+    env = dict(os.environ)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, env=env, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "ok 1" in out.stdout
