@@ -186,6 +186,24 @@ __device__ __forceinline__ uint64_t wave_reduce64(uint64_t v) {
 }
 // uniform results (SGPR)
 __device__ __forceinline__ uint64_t max_reduce64(uint64_t v) { return wave_reduce64<true>(v); }
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_max32(uint32_t v) {
+    const uint32_t w = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
+    return w > v ? w : v;
+}
+__device__ __forceinline__ uint32_t max_reduce32(uint32_t v) {
+    v = dpp_max32<0xB1>(v);
+    v = dpp_max32<0x4E>(v);
+    v = dpp_max32<0x141>(v);
+    v = dpp_max32<0x140>(v);
+    uint32_t m = 0;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const uint32_t x = readlaneu(v, 16 * r);
+        m = x > m ? x : m;
+    }
+    return m;
+}
 __device__ __forceinline__ uint64_t or_reduce64(uint64_t v) { return wave_reduce64<false>(v); }
 
 __device__ __forceinline__ uint32_t fmix32(uint32_t k) {   // HashTable.h:60-72

@@ -109,7 +109,7 @@ __device__ __forceinline__ int lv_group(GroupLds &G, uint8_t (*rows8)[WAVE], con
     const int pbase = gi * 2 * GS;                       // this group's path slots
     if (k > MAX_K - 1) k = MAX_K - 1;
     outE = -1;
-    bool done = !gact;
+    uint32_t done = gact ? 0u : 1u;   // a VGPR flag: ballot(done == 0) is one v_cmp
     const int end0 = patternLen < textLen ? patternLen : textLen;
     const int hf = mk_hi_first(M);
     const int fm = mk_first(M, hf, q0) - q0;
@@ -119,14 +119,14 @@ __device__ __forceinline__ int lv_group(GroupLds &G, uint8_t (*rows8)[WAVE], con
         const int result = patternLen > end0 ? patternLen - end0 : 0;
         outE = result > k ? -1 : result;
         if (li == 0) { G.plen[dx][gi] = 0; G.pL0[dx][gi] = (int16_t)L0; }
-        done = true;
+        done = 1u;
     }
     int Lp = (li == c) ? L0 : -2;
     const int endd = patternLen < textLen - d ? patternLen : textLen - d;
     int rowsRun = 0;
     for (int e = 1; e <= kmaxAll; e++) {
-        done = done || e > k;                           // limit reached: -1
-        if (ballot(!done) == 0) break;
+        done = e > k ? 1u : done;                       // limit reached: -1
+        if (ballot(done == 0u) == 0) break;
         rowsRun = e;
         const int lower = from_lower<GS>(Lp, gfirst), upper = from_upper<GS>(Lp, glast);
         const int left = DIR > 0 ? lower : upper;       // L[e-1][d-1]
@@ -184,7 +184,7 @@ __device__ __forceinline__ int lv_group(GroupLds &G, uint8_t (*rows8)[WAVE], con
                 }
                 if (li == 0) { G.plen[dx][gi] = (int8_t)e; G.pL0[dx][gi] = (int16_t)L0; }
                 outE = e;
-                done = true;
+                done = 1u;
             }
         }
         Lp = Ln;
@@ -534,9 +534,12 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<128> &S, Elem1
         // ---- pop in weight-list order (head of the highest list first); LDS only
         uint32_t nb = 0;
         if (!forced) {
-            const uint64_t sel = max_reduce64(S.laneMax[lane]);
-            if (sel != 0) {
-                const uint32_t e = (uint32_t)sel;
+            // sort keys are unique: reduce the 32-bit keys, then take the owner lane's index
+            const uint64_t lm = S.laneMax[lane];
+            const uint32_t kmax = max_reduce32((uint32_t)(lm >> 32));
+            if (kmax != 0) {
+                const int owner = (int)__builtin_ctzll(ballot((uint32_t)(lm >> 32) == kmax));
+                const uint32_t e = readlaneu((uint32_t)lm, owner);
                 sk_set(S, ar, e, 0);                       // unlink (BaseAligner.cpp:1391-1394)
                 wave_sync();
                 if ((int)(e % WAVE) == lane) recompute_lane_max(S, ar, lane);
