@@ -65,28 +65,28 @@ __device__ __forceinline__ int mk_first(const Mask128 &F, int hf, int m0) {
 }
 
 // ------------------------------------------------------------ group shifts
-// lane i <- lane i-1 of its group (-2 at the group start), DPP only
+// Biased shifts (value + 2, so the "-2" of a missing neighbour is 0): bound_ctrl makes
+// DPP write 0 where the source lane is outside the row, no old-value moves needed.
 template <int GS>
-__device__ __forceinline__ int from_lower(int v, bool gfirst) {
-    if constexpr (GS == 16) return __builtin_amdgcn_update_dpp(-2, v, 0x111, 0xf, 0xf, false);   // row_shr:1
+__device__ __forceinline__ int from_lower_b(int v, bool gfirst) {
+    if constexpr (GS == 16) return __builtin_amdgcn_mov_dpp(v, 0x111, 0xf, 0xf, true);   // row_shr:1
     else if constexpr (GS == 8) {
-        const int r = __builtin_amdgcn_update_dpp(-2, v, 0x111, 0xf, 0xf, false);
-        return gfirst ? -2 : r;
+        const int r = __builtin_amdgcn_mov_dpp(v, 0x111, 0xf, 0xf, true);
+        return gfirst ? 0 : r;
     } else {
-        const int r = __builtin_amdgcn_update_dpp(-2, v, 0x138, 0xf, 0xf, false);               // wave_shr:1
-        return gfirst ? -2 : r;
+        const int r = __builtin_amdgcn_mov_dpp(v, 0x138, 0xf, 0xf, true);                 // wave_shr:1
+        return gfirst ? 0 : r;
     }
 }
-// lane i <- lane i+1 of its group (-2 at the group end)
 template <int GS>
-__device__ __forceinline__ int from_upper(int v, bool glast) {
-    if constexpr (GS == 16) return __builtin_amdgcn_update_dpp(-2, v, 0x101, 0xf, 0xf, false);   // row_shl:1
+__device__ __forceinline__ int from_upper_b(int v, bool glast) {
+    if constexpr (GS == 16) return __builtin_amdgcn_mov_dpp(v, 0x101, 0xf, 0xf, true);   // row_shl:1
     else if constexpr (GS == 8) {
-        const int r = __builtin_amdgcn_update_dpp(-2, v, 0x101, 0xf, 0xf, false);
-        return glast ? -2 : r;
+        const int r = __builtin_amdgcn_mov_dpp(v, 0x101, 0xf, 0xf, true);
+        return glast ? 0 : r;
     } else {
-        const int r = __builtin_amdgcn_update_dpp(-2, v, 0x130, 0xf, 0xf, false);               // wave_shl:1
-        return glast ? -2 : r;
+        const int r = __builtin_amdgcn_mov_dpp(v, 0x130, 0xf, 0xf, true);                 // wave_shl:1
+        return glast ? 0 : r;
     }
 }
 
@@ -121,33 +121,33 @@ __device__ __forceinline__ int lv_group(GroupLds &G, uint8_t (*rows8)[WAVE], con
         if (li == 0) { G.plen[dx][gi] = 0; G.pL0[dx][gi] = (int16_t)L0; }
         done = 1u;
     }
-    int Lp = (li == c) ? L0 : -2;
+    // the row loop keeps B = L + 2 (B = 0 for "no value")
+    int Bp = (li == c) ? L0 + 2 : 0;
     const int endd = patternLen < textLen - d ? patternLen : textLen - d;
+    const int enddB = endd + 2, patB = patternLen + 2, q0m2 = q0 - 2;
     int rowsRun = 0;
     for (int e = 1; e <= kmaxAll; e++) {
         done = e > k ? 1u : done;                       // limit reached: -1
         if (ballot(done == 0u) == 0) break;
         rowsRun = e;
-        const int lower = from_lower<GS>(Lp, gfirst), upper = from_upper<GS>(Lp, glast);
-        const int left = DIR > 0 ? lower : upper;       // L[e-1][d-1]
-        const int right = (DIR > 0 ? upper : lower) + 1;   // L[e-1][d+1] + 1
-        const int x1 = Lp + 1;
-        // X, then D if strictly greater, then I if strictly greater
-        const int bxd = left > x1 ? left : x1;
-        const int act = right > bxd ? 2 : (left > x1 ? 1 : 0);
-        const int best = right > bxd ? right : bxd;
+        const int lowerB = from_lower_b<GS>(Bp, gfirst), upperB = from_upper_b<GS>(Bp, glast);
+        const int leftB = DIR > 0 ? lowerB : upperB;    // L[e-1][d-1] + 2
+        const int rightB = (DIR > 0 ? upperB : lowerB) + 1;   // L[e-1][d+1] + 1 + 2
+        const int x1B = Bp + 1;
+        // X, then D if strictly greater, then I if strictly greater (only the value is needed here)
+        const int bxdB = leftB > x1B ? leftB : x1B;
+        const int bestB = rightB > bxdB ? rightB : bxdB;
         const bool active = !done && d <= e && d >= -e;
         // slide along the diagonal (LandauVishkin.h:325-354)
-        const int mpos = q0 + best;
+        const int mpos = q0m2 + bestB;
         const int mposc = mpos < 128 ? mpos : 128;
         const int fa = mk_first(M, hf, mposc);             // fa == mposc <=> mismatch at mpos (or past 127)
-        const int f = fa - q0;
-        const int slid = f < endd ? f : endd;
-        const int bnew = best < endd ? slid : (fa == mposc ? best : endd);
-        const int Ln = active ? bnew : Lp;
-        if (active) rows8[e][lane] = (uint8_t)(bnew + 2);
-        (void)act;
-        const uint64_t hit = ballot(active && Ln == patternLen);
+        const int fB = fa - q0m2;
+        const int slidB = fB < enddB ? fB : enddB;
+        const int bnewB = bestB < enddB ? slidB : (fa == mposc ? bestB : enddB);
+        const int LnB = active ? bnewB : Bp;
+        if (active) rows8[e][lane] = (uint8_t)bnewB;
+        const uint64_t hit = ballot(active && LnB == patB);
         if (hit) {
             const uint64_t gm = GS == 64 ? hit : (hit >> (gi * GS)) & ((1ull << (GS & 63)) - 1);
             if (gm != 0) {
@@ -187,7 +187,7 @@ __device__ __forceinline__ int lv_group(GroupLds &G, uint8_t (*rows8)[WAVE], con
                 done = 1u;
             }
         }
-        Lp = Ln;
+        Bp = LnB;
     }
     return rowsRun;
 }
