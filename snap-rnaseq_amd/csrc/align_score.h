@@ -161,17 +161,36 @@ __device__ __forceinline__ int lv_group(GroupLds &G, uint8_t (*rows8)[WAVE], con
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 // backtrace; the action of a cell is recomputed from the previous row exactly
-                // as the row step chose it (X, then D, then I if strictly greater)
-                auto val = [&](int r, int dd) -> int {   // L[r][dd] as the row step saw it
-                    if (r == 0) return dd == 0 ? L0 : -2;
-                    if (dd > r || dd < -r) return -2;
-                    return (int)rows8[r][gi * GS + (DIR > 0 ? c + dd : c - dd)] - 2;
-                };
+                // as the row step chose it (X, then D, then I if strictly greater).  L of the
+                // current cell is carried (patternLen at the hit); the three cells of row
+                // ce-1 around it are adjacent bytes of the row, read with one ds_read2_b32.
                 int curD = wd;
+                int Lcur = patternLen;
                 for (int ce = e; ce >= 1; ce--) {
-                    const int Lcur = val(ce, curD);
-                    const int x1 = val(ce - 1, curD) + 1, left = val(ce - 1, curD - 1);
-                    const int right = val(ce - 1, curD + 1) + 1;
+                    const int r = ce - 1;
+                    int vm, v0, vp;   // L[r][curD-1], L[r][curD], L[r][curD+1] as the row step saw them
+                    if (r == 0) {
+                        vm = curD == 1 ? L0 : -2;
+                        v0 = curD == 0 ? L0 : -2;
+                        vp = curD == -1 ? L0 : -2;
+                    } else {
+                        const int i0 = gi * GS + (DIR > 0 ? c + curD - 1 : c - curD - 1);   // lowest byte
+                        const uint8_t *rp = &rows8[r][0] + i0;
+                        const uint32_t *p4 = reinterpret_cast<const uint32_t *>(
+                            reinterpret_cast<uintptr_t>(rp) & ~(uintptr_t)3);   // ds_read2_b32
+                        const uint64_t w = ((uint64_t)p4[1] << 32) | p4[0];
+                        const uint32_t sh = 8u * (uint32_t)(reinterpret_cast<uintptr_t>(rp) & 3);
+                        const int b0 = (int)((w >> sh) & 0xff) - 2, b1 = (int)((w >> (sh + 8)) & 0xff) - 2;
+                        const int b2 = (int)((w >> (sh + 16)) & 0xff) - 2;
+                        vm = DIR > 0 ? b0 : b2;
+                        v0 = b1;
+                        vp = DIR > 0 ? b2 : b0;
+                        if (curD - 1 < -r || curD - 1 > r) vm = -2;
+                        if (curD < -r || curD > r) v0 = -2;
+                        if (curD + 1 < -r || curD + 1 > r) vp = -2;
+                    }
+                    const int x1 = v0 + 1, left = vm;
+                    const int right = vp + 1;
                     const int bxd = left > x1 ? left : x1;
                     const int a = right > bxd ? 2 : (left > x1 ? 1 : 0);
                     const int src = a == 2 ? curD + 1 : (a == 1 ? curD - 1 : curD);
@@ -181,6 +200,7 @@ __device__ __forceinline__ int lv_group(GroupLds &G, uint8_t (*rows8)[WAVE], con
                         G.pm[dx][pbase + ce] = (int16_t)(a == 1 ? Lcur - Lsrc : Lcur - Lsrc - 1);
                     }
                     curD = src;
+                    Lcur = Lsrc;
                 }
                 if (li == 0) { G.plen[dx][gi] = (int8_t)e; G.pL0[dx][gi] = (int16_t)L0; }
                 outE = e;
@@ -338,7 +358,7 @@ __device__ __forceinline__ void lv_pass(const KArgs &A, Lds<128> &S, uint32_t i0
     PH_T(A, tr);
     const int k2 = k - e1;
     const bool ract = P.act && e1 >= 0;
-    const int kmax2 = (int)max_reduce64((uint64_t)(uint32_t)(ract ? k2 + 1 : 0)) - 1;   // largest reverse limit
+    const int kmax2 = (int)max_reduce32(ract ? (uint32_t)(k2 + 1) : 0u) - 1;   // largest reverse limit
     e2 = -1;
     if (kmax2 >= 0) {
         // reverse LV: pattern = read[s-1 .. 0], text = genome backwards from loc+s-1 (BaseAligner.cpp:1216-1220)

@@ -417,7 +417,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
         // BaseAligner.cpp:749-751
         const uint32_t minSeedLoc = minLoc < n ? 0 : minLoc - n;
         const uint32_t maxSeedLoc = maxLoc > INVALID - n ? INVALID : maxLoc + n;
-        const bool windowed = EXT && minSeedLoc != 0 || maxSeedLoc != INVALID;
+        const bool windowed = EXT && (minSeedLoc != 0 || maxSeedLoc != INVALID);
         // first-round lookups resolved by seed_lookup_kernel: lane 4k+f holds field f of record k
         uint32_t srec = 0, pfIdx = SEEDS_PER_READ;
         if (MAXLEN == 128 && A.seedRecs && A.maxHits < 0xffffu && radius == 0) {
