@@ -315,6 +315,43 @@ int snapgpu_lv_batch(int device, int direction, uint32_t n,
                      const uint32_t *patLen, const int32_t *k,
                      int32_t *outScore, int32_t *outNetIndel, double *outProb);
 
+/* ------------------------------------------------- CIGAR / SAM records */
+/* The SAM writer's per-read work, on the GPU:
+ * LandauVishkinWithCigar::computeEditDistance (LandauVishkin.cpp:252-535) as
+ * SAMFormat::computeCigarString (SAM.cpp:1162-1230) calls it -- text = the genome
+ * substring at the location with the read's length, k = MAX_K - 1, the read
+ * upper-cased and, for RC, reverse-complemented (getSAMData, SAM.cpp:866-883).
+ * Per read out: editDistance (the NM tag; -1 when the reference prints "*": no
+ * location, no substring (Genome::getSubstring NULL) or no alignment within k),
+ * nOps, and ops[i * SNAPGPU_CIGAR_MAX_OPS ..] as BAM ops (count << 4 | code, code
+ * index into "MIDNSHP=X"; useM != 0 is the `-M` form: '=' and 'X' merged into 'M').
+ * Reads longer than 512 bases are rejected (SNAPGPU_EINVAL). */
+#define SNAPGPU_CIGAR_MAX_OPS 64
+
+/* Explicit (location, direction) per read; location 0xffffffff => "*". */
+int snapgpu_cigar_batch(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, const uint32_t *locations,
+                        const uint8_t *directions, int useM, int32_t *editDistance, uint32_t *nOps, uint32_t *ops);
+/* Device-resident: the CIGARs of the records the last snapgpu_align_resident left
+ * in HBM for these reads, with writeRead's rules (SAM.cpp:1007-1048, 855-883): a
+ * NotFound record keeps its location for the CIGAR but uses the forward read. */
+int snapgpu_cigar_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, int useM);
+int snapgpu_cigar_download(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, int32_t *editDistance, uint32_t *nOps,
+                           uint32_t *ops);
+/* cigar_kernel time of the last snapgpu_cigar_resident / snapgpu_cigar_batch (HIP events). */
+int snapgpu_cigar_last_ms(snapgpu_aligner_t *a, double *ms);
+
+/* One SAM line per read, as SAMFormat::writeRead (SAM.cpp:1007-1155) writes it for a
+ * single-end genome alignment: QNAME (read id up to the first space), FLAG, RNAME,
+ * POS, MAPQ (clamped to [0, 70]; 0 when unmapped), CIGAR, "*", 0, 0, SEQ and QUAL
+ * (reverse-complemented / reversed for RC), RG:Z:<readGroup> (omitted when NULL),
+ * PG:Z:SNAP, NM:i:<editDistance>.  ids[idOffsets[i] .. +idLengths[i]) is read i's
+ * id.  Writes at most `cap` bytes to out and the size needed to *used; returns
+ * SNAPGPU_EINVAL (nothing usable written) when cap is too small. */
+int snapgpu_sam_format(const snapgpu_index_t *idx, const snapgpu_reads_t *reads, const char *ids,
+                       const uint64_t *idOffsets, const uint32_t *idLengths, const snapgpu_result_t *results,
+                       const int32_t *editDistance, const uint32_t *nOps, const uint32_t *ops,
+                       const char *readGroup, char *out, uint64_t cap, uint64_t *used);
+
 /* MAPQ (mapq.h:32-65) as the host computes it; exported for tests. */
 int snapgpu_compute_mapq(double pAll, double pBest, int score, int popularSeedsSkipped);
 

@@ -16,6 +16,13 @@
 //   alignx <indexDir> <reads.fq> <search.tsv> <maxHitsToGet> [...] -> align columns + multi hits
 //   lv     <calls.tsv>   lines: dir k text pattern quals   -> e netIndel prob_hex
 //   lookup <indexDir> <seeds.txt>  one seed string per line -> nF nRC sumF sumRC firstF firstRC
+//   sam    <indexDir> <reads.fq> [maxHits maxK numSeeds extra]
+//          -> per read: AlignRead, then the reference's own SAM writer
+//             (FileFormat::SAM[useM]->writeRead, SAM.cpp:1007-1155) for useM = 0 and 1:
+//             two SAM lines per read
+//   cigar  <indexDir> <calls.tsv>  lines: loc dir useM read
+//          -> ed cigar   (SAMFormat::computeCigarString, SAM.cpp:1162-1230, restated
+//             around the reference's LandauVishkinWithCigar with zeroed slack bytes)
 #define private public          // read-only access to BaseAligner's private scoring state
 #include "stdafx.h"
 #include "BaseAligner.h"
@@ -25,6 +32,9 @@
 #include "Read.h"
 #include "Seed.h"
 #include "BigAlloc.h"
+#include "FileFormat.h"
+#include "Genome.h"
+#include "Tables.h"
 #include <string>
 #include <vector>
 #include <fstream>
@@ -169,6 +179,69 @@ static int mode_lookup(int argc, char **argv) {
     return 0;
 }
 
+static int mode_sam(int argc, char **argv) {
+    if (argc < 4) { fprintf(stderr, "sam <indexDir> <reads.fq> [maxHits maxK numSeeds extra]\n"); return 2; }
+    unsigned maxHits = argc > 4 ? atoi(argv[4]) : 300;
+    unsigned maxK = argc > 5 ? atoi(argv[5]) : 14;
+    unsigned numSeeds = argc > 6 ? atoi(argv[6]) : 25;
+    unsigned extra = argc > 7 ? atoi(argv[7]) : 2;
+    initializeLVProbabilitiesToPhredPlus33();
+    GenomeIndex *idx = GenomeIndex::loadFromDirectory(argv[2]);
+    if (!idx) { fprintf(stderr, "cannot load index %s\n", argv[2]); return 1; }
+    BigAllocator *al = new BigAllocator(BaseAligner::getBigAllocatorReservation(
+        true, maxHits, MAX_READ_LENGTH, idx->getSeedLength(), numSeeds, 0));
+    BaseAligner *ba = new (al) BaseAligner(idx, maxHits, maxK, MAX_READ_LENGTH, numSeeds, 0, extra,
+                                           NULL, NULL, NULL, al);
+    LandauVishkinWithCigar lvc;
+    std::ifstream in(argv[3]);
+    std::string id, bases, plus, quals;
+    std::vector<char> buf(1 << 16);
+    while (std::getline(in, id) && std::getline(in, bases) && std::getline(in, plus) && std::getline(in, quals)) {
+        std::string b = bases + std::string(16, '\0');
+        std::string q = quals + std::string(16, '\0');
+        Read r;
+        r.init(id.c_str() + 1, (unsigned)id.size() - 1, b.c_str(), q.c_str(), (unsigned)bases.size());
+        r.setReadGroup("FASTQ");      // FASTQ.cpp:252 with AlignerOptions.cpp:65's default
+        unsigned loc = 0; Direction dir = 0; int score = 0, mapq = 0;
+        AlignmentResult res = ba->AlignRead(&r, &loc, &dir, &score, &mapq);
+        for (int useM = 0; useM < 2; useM++) {
+            size_t used = 0;
+            if (!FileFormat::SAM[useM]->writeRead(idx->getGenome(), NULL, NULL, &lvc, &buf[0], buf.size(), &used, 0,
+                                                  &r, res, mapq, loc, dir)) { fprintf(stderr, "writeRead failed\n"); return 1; }
+            fwrite(&buf[0], 1, used, stdout);
+        }
+    }
+    return 0;
+}
+
+static int mode_cigar(int argc, char **argv) {
+    if (argc < 4) { fprintf(stderr, "cigar <indexDir> <calls.tsv>\n"); return 2; }
+    GenomeIndex *idx = GenomeIndex::loadFromDirectory(argv[2]);
+    if (!idx) return 1;
+    const Genome *g = idx->getGenome();
+    LandauVishkinWithCigar lvc;
+    std::ifstream in(argv[3]);
+    unsigned loc; int useM; int dirv; std::string read;
+    char cig[MAX_READ_LENGTH * 2];
+    while (in >> loc >> dirv >> useM >> read) {
+        // getSAMData (SAM.cpp:866-883): Read::init upper-cases, RC = reversed COMPLEMENT[]
+        Read r;
+        r.init("x", 1, read.c_str(), read.c_str(), (unsigned)read.size());
+        std::string p(read.size() + 16, '\0');
+        for (size_t i = 0; i < read.size(); i++) {
+            if (dirv) p[read.size() - 1 - i] = COMPLEMENT[(unsigned char)r.getData()[i]];
+            else p[i] = r.getData()[i];
+        }
+        std::vector<unsigned> tokens;
+        const char *ref = g->getSubstring(loc, (unsigned)read.size());
+        if (ref == NULL) { printf("-3\t*\n"); continue; }
+        int ed = lvc.computeEditDistance(ref, (int)read.size(), p.c_str(), (int)read.size(), MAX_K - 1,
+                                         cig, sizeof(cig), useM != 0, tokens);
+        printf("%d\t%s\n", ed, ed >= 0 ? cig : "*");
+    }
+    return 0;
+}
+
 int main(int argc, char **argv) {
     if (argc < 2) { fprintf(stderr, "usage: ref_harness align|lv|lookup ...\n"); return 2; }
     std::string m = argv[1];
@@ -176,6 +249,8 @@ int main(int argc, char **argv) {
     if (m == "alignx") return mode_alignx(argc, argv);
     if (m == "lv") return mode_lv(argc, argv);
     if (m == "lookup") return mode_lookup(argc, argv);
+    if (m == "sam") return mode_sam(argc, argv);
+    if (m == "cigar") return mode_cigar(argc, argv);
     fprintf(stderr, "unknown mode %s\n", argv[1]);
     return 2;
 }

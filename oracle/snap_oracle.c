@@ -772,3 +772,98 @@ int oracle_align_batch(const snapgpu_index_view_t *ix, const snapgpu_aligner_par
                        uint64_t n, snapgpu_result_t *out, int nThreads) {
     return oracle_align_batch_ex(ix, p, bases, quals, offsets, lengths, n, NULL, 0, out, NULL, NULL, nThreads);
 }
+
+/* ------------------------------------------------------------------ CIGAR */
+/* LandauVishkinWithCigar::computeEditDistance (LandauVishkin.cpp:252-535) as
+ * SAMFormat::computeCigarString (SAM.cpp:1162-1230) calls it: text = the genome
+ * substring at `loc` of the read's length, k = MAX_K - 1, COMPACT format.  Ops are
+ * written as BAM ops (count << 4 | code, code index into "MIDNSHP=X"); `pattern`
+ * must carry >= 8 bytes of zero slack (the reference compares 8 bytes at a time).
+ * Returns the edit distance (NM), or -1 for "*" (no substring, or no alignment
+ * within k).  A serial restatement: explicit L/A tables, diagonals visited in the
+ * reference's order 0, -1, +1, -2, +2, ... */
+static void cig_put(uint32_t *ops, int *n, int count, char c) {   /* writeCigar, LandauVishkin.cpp:27-93 */
+    if (count <= 0) return;
+    int code = c == 'M' ? 0 : c == 'I' ? 1 : c == 'D' ? 2 : c == '=' ? 7 : 8;
+    ops[(*n)++] = ((uint32_t)count << 4) | (uint32_t)code;
+}
+
+int oracle_cigar(const snapgpu_index_view_t *v, uint32_t loc, const char *pattern, int len, int useM,
+                 uint32_t *ops, int *nOps) {
+    *nOps = 0;
+    const char *text = get_substring(v, loc, (uint32_t)len);
+    if (!text) return -1;
+    const int k = MAX_K - 1;
+    int L[MAX_K + 1][2 * MAX_K + 1];
+    char A[MAX_K + 1][2 * MAX_K + 1];
+    for (int i = 0; i <= MAX_K; i++)
+        for (int j = 0; j <= 2 * MAX_K; j++) L[i][j] = -2;
+    const int end = len;                       /* min(patternLen, textLen) */
+    int m0 = 0;
+    while (m0 < end && pattern[m0] == text[m0]) m0++;
+    L[0][MAX_K] = m0;
+    if (m0 == end) {
+        cig_put(ops, nOps, len, useM ? 'M' : '=');
+        return 0;
+    }
+    for (int e = 1; e <= k; e++) {
+        for (int d = 0; d != -(e + 1); d = (d >= 0 ? -(d + 1) : -d)) {
+            int best = L[e - 1][MAX_K + d] + 1;
+            char a = 'X';
+            int left = L[e - 1][MAX_K + d - 1];
+            if (left > best) { best = left; a = 'D'; }
+            int right = L[e - 1][MAX_K + d + 1] + 1;
+            if (right > best) { best = right; a = 'I'; }
+            A[e][MAX_K + d] = a;
+            if (pattern[best] == text[d + best]) {
+                int endd = len < len - d ? len : len - d;
+                int m = best;
+                while (m < endd && pattern[m] == text[d + m]) m++;
+                best = m < endd ? m : endd;
+            }
+            L[e][MAX_K + d] = best;
+            if (best != len) continue;
+            /* done at (e, d): straight alignment with e mismatches? (LandauVishkin.cpp:341-393) */
+            int straight = 0;
+            for (int i = 0; i < end; i++) straight += pattern[i] != text[i];
+            if (straight == e) {
+                if (useM) { cig_put(ops, nOps, len, 'M'); return e; }
+                int streak = 0, matching = pattern[0] == text[0];
+                for (int i = 0; i < end; i++) {
+                    int nm = pattern[i] == text[i];
+                    if (nm != matching) { cig_put(ops, nOps, i - streak, matching ? '=' : 'X'); matching = nm; streak = i; }
+                }
+                if (len > streak) cig_put(ops, nOps, len - streak, matching ? '=' : 'X');
+                return e;
+            }
+            /* backtrace (LandauVishkin.cpp:420-440) and emission (:442-520) */
+            char act[MAX_K + 1]; int matched[MAX_K + 1];
+            int curD = d;
+            for (int ce = e; ce >= 1; ce--) {
+                act[ce] = A[ce][MAX_K + curD];
+                int pd = act[ce] == 'I' ? curD + 1 : act[ce] == 'D' ? curD - 1 : curD;
+                matched[ce] = L[ce][MAX_K + curD] - L[ce - 1][MAX_K + pd] - (act[ce] == 'D' ? 0 : 1);
+                curD = pd;
+            }
+            int accM = 0;
+            if (useM) accM = L[0][MAX_K];
+            else if (L[0][MAX_K] > 0) cig_put(ops, nOps, L[0][MAX_K], '=');
+            for (int ce = 1; ce <= e; ce++) {
+                char a2 = act[ce];
+                int cnt = 1;
+                while (ce + 1 <= e && matched[ce] == 0 && act[ce + 1] == a2) { cnt++; ce++; }
+                if (useM) {
+                    if (a2 == 'X') accM += cnt;
+                    else { if (accM) { cig_put(ops, nOps, accM, 'M'); accM = 0; } cig_put(ops, nOps, cnt, a2); }
+                } else cig_put(ops, nOps, cnt, a2);
+                if (matched[ce] > 0) {
+                    if (useM) accM += matched[ce];
+                    else cig_put(ops, nOps, matched[ce], '=');
+                }
+            }
+            if (useM && accM) cig_put(ops, nOps, accM, 'M');
+            return e;
+        }
+    }
+    return -1;
+}

@@ -477,7 +477,8 @@ __device__ __forceinline__ int stage_window(Lds<MAXLEN> &S, const char *genome, 
 }
 
 // Genome::getSubstring (Genome.h:78-148): is [offset, offset+len) servable?
-__device__ __forceinline__ bool substring_ok(const KArgs &A, uint32_t offset, uint32_t len) {
+template <class G>   // KArgs, CigarArgs: anything with nBases, padding, pieces, nPieces
+__device__ __forceinline__ bool substring_ok(const G &A, uint32_t offset, uint32_t len) {
     if (offset > A.nBases || (uint64_t)offset + len > (uint64_t)A.nBases + NPAD) return false;
     if (len <= A.padding) return true;
     if (A.nPieces > 100) {

@@ -14,6 +14,7 @@
 #include "align_device.h"
 #include "align_score.h"
 #include "seed_lookup.h"
+#include "cigar.h"
 #include "internal.h"
 
 using namespace sgk;
@@ -773,6 +774,8 @@ struct snapgpu_device_reads {
     snapgpu_result_t *dOut = nullptr;
     uint32_t *dDefer = nullptr;   // pass 1 -> pass 2 read list
     SeedRec *dSeeds = nullptr;    // seed_lookup_kernel records, SEEDS_PER_READ per read
+    int32_t *dCigEd = nullptr;    // cigar_kernel outputs (allocated by the first snapgpu_cigar_resident)
+    uint32_t *dCigN = nullptr, *dCigOps = nullptr;
     uint64_t n = 0;
     uint32_t maxLen = 0;
     int device = 0;
@@ -801,6 +804,8 @@ struct snapgpu_aligner {
     unsigned long long *dPhase = nullptr;   // [grid][PH_SLOTS] (SNAPGPU_PHASES=1 diagnostics)
     unsigned long long *dLookupStats = nullptr;   // seed_lookup_kernel: seeds, probes, overflow counts
     double timeoutSec = 0;        // SNAPGPU_TIMEOUT_S
+    hipEvent_t cev[2] = {};       // cigar_kernel timing
+    int cigarGrid = 0;
 };
 
 static const size_t kDevGuard = 1024;
@@ -834,6 +839,7 @@ void snapgpu_aligner_free(snapgpu_aligner_t *a) {
     hipFree(a->dTableBase); hipFree(a->dTableSize); hipFree(a->dGenomeAlloc); hipFree(a->dTab); hipFree(a->dArena);
     hipFree(a->dGPlanes); hipFree(a->dPhase); hipFree(a->dLookupStats);
     for (auto &e : a->ev) if (e) hipEventDestroy(e);
+    for (auto &e : a->cev) if (e) hipEventDestroy(e);
     if (a->stream) hipStreamDestroy(a->stream);
     delete a;
 }
@@ -862,6 +868,7 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
     if ((e = hipSetDevice(device)) != hipSuccess) return fail("hipSetDevice", e);
     if ((e = hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking)) != hipSuccess) return fail("stream", e);
     for (auto &ev : a->ev) if ((e = hipEventCreate(&ev)) != hipSuccess) return fail("event", e);
+    for (auto &ev : a->cev) if ((e = hipEventCreate(&ev)) != hipSuccess) return fail("event", e);
     if ((e = hipGetSymbolAddress((void **)&a->dDiag, HIP_SYMBOL(g_diag))) != hipSuccess) return fail("g_diag", e);
     if ((e = ensureDeviceTables(device)) != hipSuccess) return fail("device tables", e);
     // index upload: genome with guards, tables, overflow, pieces
@@ -982,6 +989,7 @@ void snapgpu_device_reads_free(snapgpu_device_reads_t *d) {
     hipSetDevice(d->device);
     hipFree(d->dBases); hipFree(d->dQuals); hipFree(d->dOffsets); hipFree(d->dLengths); hipFree(d->dOut);
     hipFree(d->dDefer); hipFree(d->dSeeds);
+    hipFree(d->dCigEd); hipFree(d->dCigN); hipFree(d->dCigOps);
     delete d;
 }
 
@@ -1296,6 +1304,101 @@ int snapgpu_lv_batch(int device, int direction, uint32_t n, const char *texts, c
     hipMemcpy(outProb, dP, n * 8, hipMemcpyDeviceToHost);
     hipFree(dT); hipFree(dR); hipFree(dQ); hipFree(dG); hipFree(dTab); hipFree(dS); hipFree(dN); hipFree(dP);
     return SNAPGPU_OK;
+}
+
+// ------------------------------------------------------ CIGAR / SAM records
+static CigarArgs cigar_args(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, int useM) {
+    CigarArgs C;
+    memset(&C, 0, sizeof(C));
+    const snapgpu_index_t *idx = a->idx;
+    C.genome = a->dGenome; C.pieces = a->dPieces; C.nPieces = (int32_t)idx->genome->pieceOffsets.size();
+    C.nBases = idx->genome->nBases; C.padding = idx->genome->chromosomePadding;
+    C.bases = d->dBases; C.offsets = d->dOffsets; C.lengths = d->dLengths; C.nReads = (uint32_t)d->n;
+    C.useM = useM ? 1 : 0;
+    return C;
+}
+
+static int cigar_launch(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, CigarArgs C) {
+    if (d->maxLen > (uint32_t)CIG_MAXLEN) { snapgpu::setError("cigar: read longer than 512 bases"); return SNAPGPU_EINVAL; }
+    if (d->n > 0xffffffffull) { snapgpu::setError("batch too large"); return SNAPGPU_EINVAL; }
+    if (!d->dCigEd) {
+        HIPCHK(hipMalloc(&d->dCigEd, (d->n + 1) * 4));
+        HIPCHK(hipMalloc(&d->dCigN, (d->n + 1) * 4));
+        HIPCHK(hipMalloc(&d->dCigOps, (d->n + 1) * CIG_MAX_OPS * 4));
+    }
+    C.outEd = d->dCigEd; C.outNOps = d->dCigN; C.outOps = d->dCigOps;
+    if (!a->cigarGrid) {
+        hipDeviceProp_t prop;
+        HIPCHK(hipGetDeviceProperties(&prop, a->device));
+        int perCU = 0;
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, (const void *)cigar_kernel, 64, 0);
+        a->cigarGrid = prop.multiProcessorCount * (perCU > 0 ? perCU : 8);
+    }
+    int grid = a->cigarGrid;
+    if ((uint64_t)grid > d->n) grid = (int)d->n;
+    if (grid == 0) return SNAPGPU_OK;
+    HIPCHK(hipEventRecord(a->cev[0], a->stream));
+    hipLaunchKernelGGL(cigar_kernel, dim3(grid), dim3(64), 0, a->stream, C);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(a->cev[1], a->stream));
+    return SNAPGPU_OK;
+}
+
+int snapgpu_cigar_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, int useM) {
+    if (!a || !d) return SNAPGPU_EINVAL;
+    HIPCHK(hipSetDevice(a->device));
+    CigarArgs C = cigar_args(a, d, useM);
+    C.records = d->dOut;
+    return cigar_launch(a, d, C);
+}
+
+int snapgpu_cigar_download(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, int32_t *editDistance, uint32_t *nOps,
+                           uint32_t *ops) {
+    if (!a || !d || !editDistance || !nOps || !ops || !d->dCigEd) return SNAPGPU_EINVAL;
+    HIPCHK(hipSetDevice(a->device));
+    HIPCHK(hipStreamSynchronize(a->stream));
+    HIPCHK(hipMemcpy(editDistance, d->dCigEd, d->n * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(nOps, d->dCigN, d->n * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(ops, d->dCigOps, d->n * CIG_MAX_OPS * 4, hipMemcpyDeviceToHost));
+    return SNAPGPU_OK;
+}
+
+int snapgpu_cigar_last_ms(snapgpu_aligner_t *a, double *ms) {
+    if (!a || !ms) return SNAPGPU_EINVAL;
+    HIPCHK(hipSetDevice(a->device));
+    HIPCHK(hipEventSynchronize(a->cev[1]));
+    float f = 0;
+    HIPCHK(hipEventElapsedTime(&f, a->cev[0], a->cev[1]));
+    *ms = f;
+    return SNAPGPU_OK;
+}
+
+int snapgpu_cigar_batch(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, const uint32_t *locations,
+                        const uint8_t *directions, int useM, int32_t *editDistance, uint32_t *nOps, uint32_t *ops) {
+    if (!a || !reads || !locations || !directions || !editDistance || !nOps || !ops) return SNAPGPU_EINVAL;
+    HIPCHK(hipSetDevice(a->device));
+    snapgpu_device_reads_t *d = snapgpu_reads_upload(a, reads);
+    if (!d) return SNAPGPU_EDEVICE;
+    uint32_t *dLoc = nullptr;
+    uint8_t *dDir = nullptr;
+    int rc = SNAPGPU_OK;
+    if (hipMalloc(&dLoc, (reads->n + 1) * 4) != hipSuccess || hipMalloc(&dDir, reads->n + 1) != hipSuccess) {
+        snapgpu::setError("cigar_batch: hipMalloc");
+        rc = SNAPGPU_ENOMEM;
+    }
+    if (!rc && reads->n) {
+        hipMemcpy(dLoc, locations, reads->n * 4, hipMemcpyHostToDevice);
+        hipMemcpy(dDir, directions, reads->n, hipMemcpyHostToDevice);
+        CigarArgs C = cigar_args(a, d, useM);
+        C.locations = dLoc;
+        C.directions = dDir;
+        rc = cigar_launch(a, d, C);
+        if (!rc) rc = snapgpu_cigar_download(a, d, editDistance, nOps, ops);
+    }
+    hipFree(dLoc);
+    hipFree(dDir);
+    snapgpu_device_reads_free(d);
+    return rc;
 }
 
 }  // extern "C"

@@ -1,0 +1,169 @@
+// sam.cpp -- SAM lines of single-end genome alignments, host side.
+//
+// SAMFormat::writeRead (SNAPLib/SAM.cpp:1007-1155) with getSAMData
+// (SAM.cpp:804-975) for a read without mate, without transcriptome and without
+// clipping: the per-read LV-with-CIGAR work comes from the GPU
+// (snapgpu_cigar_resident / snapgpu_cigar_batch); this file only prints.  Lines
+// are formatted in parallel chunks and concatenated in read order.
+#include "internal.h"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <thread>
+
+using namespace snapgpu;
+
+namespace {
+
+const int SAM_UNMAPPED = 0x004;             // SAM.h:40
+const int SAM_REVERSE_COMPLEMENT = 0x010;   // SAM.h:42
+
+inline char upperCase(char c) { return (c >= 'a' && c <= 'z') ? (char)(c - 0x20) : c; }   // Tables.cpp:74-80
+inline char complement(char c) {                                                         // Tables.cpp:22-30
+    switch (c) {
+        case 'A': return 'T';
+        case 'C': return 'G';
+        case 'G': return 'C';
+        case 'T': return 'A';
+        case 'N': return 'N';
+        case 'n': return 'n';
+        default: return 0;
+    }
+}
+
+// Genome::getPieceAtLocation (Genome.cpp:357-374)
+int pieceAt(const Genome &g, uint32_t loc) {
+    int lo = 0, hi = (int)g.pieceOffsets.size() - 1;
+    while (lo <= hi) {
+        int mid = (lo + hi) / 2;
+        if (g.pieceOffsets[mid] <= loc && (mid == (int)g.pieceOffsets.size() - 1 || g.pieceOffsets[mid + 1] > loc))
+            return mid;
+        else if (g.pieceOffsets[mid] <= loc) lo = mid + 1;
+        else hi = mid - 1;
+    }
+    return -1;
+}
+
+struct Job {
+    const Index *idx;
+    const snapgpu_reads_t *reads;
+    const char *ids;
+    const uint64_t *idOffsets;
+    const uint32_t *idLengths;
+    const snapgpu_result_t *res;
+    const int32_t *ed;
+    const uint32_t *nOps;
+    const uint32_t *ops;
+    const char *rg;
+};
+
+void formatOne(const Job &J, uint64_t i, std::string &o) {
+    static const char kOp[] = "MIDNSHP=X";
+    const Genome &g = *J.idx->genome;
+    const snapgpu_result_t &r = J.res[i];
+    const char *bases = J.reads->bases + J.reads->offsets[i];
+    const char *quals = J.reads->quals + J.reads->offsets[i];
+    const uint32_t len = J.reads->lengths[i];
+    // getSAMData: NotFound -> unmapped, unmapped -> forward
+    uint32_t loc = r.location;
+    if (r.result == SNAPGPU_NOT_FOUND) loc = kInvalidLocation;
+    const int rc = loc != kInvalidLocation && r.direction == SNAPGPU_RC;
+    int flags = 0, mapq = 0;
+    const char *pieceName = "*";
+    uint32_t pos = 0;
+    if (loc != kInvalidLocation) {
+        if (rc) flags |= SAM_REVERSE_COMPLEMENT;
+        int p = pieceAt(g, loc);
+        if (p >= 0) {
+            pieceName = g.pieceNames[p].c_str();
+            pos = loc - g.pieceOffsets[p] + 1;
+        }
+        mapq = std::max(0, std::min(70, (int)r.mapq));
+    } else {
+        flags |= SAM_UNMAPPED;
+    }
+    // QNAME: truncated at the first space (SAM.cpp:1080-1086)
+    const char *id = J.ids + J.idOffsets[i];
+    uint32_t qlen = J.idLengths[i];
+    if (const void *sp = memchr(id, ' ', qlen)) qlen = (uint32_t)((const char *)sp - id);
+    char num[64];
+    o.append(id, qlen);
+    snprintf(num, sizeof num, "\t%d\t", flags);
+    o += num;
+    o += pieceName;
+    snprintf(num, sizeof num, "\t%u\t%d\t", pos, mapq);
+    o += num;
+    // CIGAR: computed at writeRead's own location (even for NotFound) -- SAM.cpp:1041-1048
+    const int32_t ed = r.location != kInvalidLocation ? J.ed[i] : -1;
+    if (r.location != kInvalidLocation && ed >= 0) {
+        const uint32_t *op = J.ops + i * SNAPGPU_CIGAR_MAX_OPS;
+        for (uint32_t k = 0; k < J.nOps[i]; k++) {
+            snprintf(num, sizeof num, "%u%c", op[k] >> 4, kOp[op[k] & 15]);
+            o += num;
+        }
+    } else {
+        o += '*';
+    }
+    // SEQ / QUAL are printed with "%.*s" (SAM.cpp:1122-1136): a NUL byte ends them early
+    // (COMPLEMENT[] of a non-ACGTN base is 0; a quality string shorter than the read)
+    o += "\t*\t0\t0\t";
+    const size_t s0 = o.size();
+    o.resize(s0 + len);
+    for (uint32_t k = 0; k < len; k++) o[s0 + k] = rc ? complement(upperCase(bases[len - 1 - k])) : upperCase(bases[k]);
+    o.resize(s0 + strnlen(o.data() + s0, len));
+    o += '\t';
+    const size_t q0 = o.size();
+    o.resize(q0 + len);
+    for (uint32_t k = 0; k < len; k++) o[q0 + k] = rc ? quals[len - 1 - k] : quals[k];
+    o.resize(q0 + strnlen(o.data() + q0, len));
+    if (J.rg) {
+        o += "\tRG:Z:";
+        o += J.rg;
+    }
+    snprintf(num, sizeof num, "\tPG:Z:SNAP\tNM:i:%d\n", ed);
+    o += num;
+}
+
+}  // namespace
+
+extern "C" int snapgpu_sam_format(const snapgpu_index_t *idx, const snapgpu_reads_t *reads, const char *ids,
+                                  const uint64_t *idOffsets, const uint32_t *idLengths,
+                                  const snapgpu_result_t *results, const int32_t *editDistance, const uint32_t *nOps,
+                                  const uint32_t *ops, const char *readGroup, char *out, uint64_t cap,
+                                  uint64_t *used) {
+    if (!idx || !reads || !ids || !idOffsets || !idLengths || !results || !editDistance || !nOps || !ops || !used) {
+        setError("sam_format: null argument");
+        return SNAPGPU_EINVAL;
+    }
+    for (uint64_t i = 0; i < reads->n; i++)
+        if (nOps[i] > SNAPGPU_CIGAR_MAX_OPS) {
+            setError("sam_format: nOps > SNAPGPU_CIGAR_MAX_OPS");
+            return SNAPGPU_EINVAL;
+        }
+    Job J{idx, reads, ids, idOffsets, idLengths, results, editDistance, nOps, ops, readGroup};
+    const uint64_t n = reads->n;
+    unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (n < 4096) nt = 1;
+    std::vector<std::string> parts(nt);
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; t++)
+        th.emplace_back([&, t] {
+            const uint64_t a = n * t / nt, b = n * (t + 1) / nt;
+            parts[t].reserve((b - a) * 320);
+            for (uint64_t i = a; i < b; i++) formatOne(J, i, parts[t]);
+        });
+    for (auto &x : th) x.join();
+    uint64_t total = 0;
+    for (auto &p : parts) total += p.size();
+    *used = total;
+    if (total > cap || (!out && total)) {
+        setError("sam_format: output buffer too small");
+        return SNAPGPU_EINVAL;
+    }
+    for (auto &p : parts) {
+        memcpy(out, p.data(), p.size());
+        out += p.size();
+    }
+    return SNAPGPU_OK;
+}

@@ -298,6 +298,27 @@ class BaseAligner:
         r = self.AlignReads(Reads.from_list([(bases, quals)]))[0]
         return int(r["result"]), int(r["location"]), int(r["direction"]), int(r["score"]), int(r["mapq"])
 
+    def Cigars(self, reads, locations, directions, useM=False):
+        """CIGARs as SAMFormat::computeCigarString computes them (SAM.cpp:1162-1230), on
+        the GPU, for explicit (location, direction) per read (see cigar_inputs for the
+        SAM writer's rules).  -> Cigars(editDistance int32[n], nOps uint32[n],
+        ops uint32[n, 64] BAM ops)."""
+        n = reads.n
+        loc = np.ascontiguousarray(locations, dtype=np.uint32)
+        dr = np.ascontiguousarray(directions, dtype=np.uint8)
+        assert loc.shape == (n,) and dr.shape == (n,)
+        c = Cigars.empty(n)
+        if n:
+            _check(lib().snapgpu_cigar_batch(self._h, reads._p, loc.ctypes.data, dr.ctypes.data, int(useM),
+                                             c.editDistance.ctypes.data, c.nOps.ctypes.data, c.ops.ctypes.data),
+                   "cigar_batch")
+        return c
+
+    def cigar_ms(self):
+        ms = C.c_double()
+        _check(lib().snapgpu_cigar_last_ms(self._h, C.byref(ms)), "cigar_last_ms")
+        return ms.value
+
     # resident path (bench): upload once, time only the GPU passes
     def upload(self, reads):
         return DeviceReads(self, reads)
@@ -369,10 +390,71 @@ class DeviceReads:
                                               out.ctypes.data_as(C.POINTER(_ffi.Result))), "results_download")
         return out[:self.n]
 
+    def run_cigars(self, useM=False):
+        """CIGARs of the records the last run() left in HBM (asynchronous)."""
+        _check(lib().snapgpu_cigar_resident(self.aligner._h, self._h, int(useM)), "cigar_resident")
+
+    def cigars(self):
+        c = Cigars.empty(self.n)
+        _check(lib().snapgpu_cigar_download(self.aligner._h, self._h, c.editDistance.ctypes.data,
+                                            c.nOps.ctypes.data, c.ops.ctypes.data), "cigar_download")
+        return c
+
     def __del__(self):
         if getattr(self, "_h", None):
             lib().snapgpu_device_reads_free(self._h)
             self._h = None
+
+
+CIGAR_OPS = "MIDNSHP=X"   # BAM op codes (SAM spec; BAMAlignment::CigarToCode)
+
+
+class Cigars:
+    """Per-read CIGAR results: editDistance (NM, -1 = "*"), nOps, ops (BAM-encoded)."""
+
+    def __init__(self, editDistance, nOps, ops):
+        self.editDistance, self.nOps, self.ops = editDistance, nOps, ops
+
+    @classmethod
+    def empty(cls, n):
+        return cls(np.full(max(1, n), -1, dtype=np.int32)[:n], np.zeros(max(1, n), dtype=np.uint32)[:n],
+                   np.zeros((max(1, n), _ffi.CIGAR_MAX_OPS), dtype=np.uint32)[:n])
+
+    def string(self, i):
+        """COMPACT_CIGAR_STRING form (LandauVishkin.cpp:49-62), or "*"."""
+        if self.editDistance[i] < 0:
+            return "*"
+        return "".join(f"{int(o) >> 4}{CIGAR_OPS[int(o) & 15]}" for o in self.ops[i, :self.nOps[i]])
+
+
+def cigar_inputs(results):
+    """(locations, directions) the SAM writer computes CIGARs for (SAM.cpp:1007-1048,
+    855-883): writeRead's own location, the forward read unless the read is mapped RC."""
+    loc = np.ascontiguousarray(results["location"], dtype=np.uint32)
+    mapped = (results["result"] != NotFound) & (loc != 0xFFFFFFFF)
+    return loc, np.where(mapped, results["direction"], 0).astype(np.uint8)
+
+
+def sam_format(index, reads, ids, results, cigars, read_group="FASTQ"):
+    """SAM lines (SAMFormat::writeRead, SAM.cpp:1007-1155) of single-end genome
+    alignments -> bytes.  ids: list of read ids (str/bytes)."""
+    n = reads.n
+    idb = [i.encode() if isinstance(i, str) else bytes(i) for i in ids]
+    assert len(idb) == n
+    lens = np.array([len(x) for x in idb], dtype=np.uint32)
+    offs = np.zeros(max(1, n), dtype=np.uint64)
+    if n > 1:
+        offs[1:n] = np.cumsum(lens[:-1], dtype=np.uint64)
+    blob = b"".join(idb) + b"\0"
+    res = np.ascontiguousarray(results, dtype=RESULT_DTYPE)
+    used = C.c_uint64()
+    rg = None if read_group is None else read_group.encode()
+    args = [index._h, reads._p, blob, offs.ctypes.data, lens.ctypes.data, res.ctypes.data,
+            cigars.editDistance.ctypes.data, cigars.nOps.ctypes.data, cigars.ops.ctypes.data, rg]
+    lib().snapgpu_sam_format(*args, None, 0, C.byref(used))
+    buf = C.create_string_buffer(max(1, used.value))
+    _check(lib().snapgpu_sam_format(*args, buf, used.value, C.byref(used)), "sam_format")
+    return buf.raw[:used.value]
 
 
 def lv_batch(direction, tasks, device=0):

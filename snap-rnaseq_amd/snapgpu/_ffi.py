@@ -197,7 +197,17 @@ _PROTOS = [
                                    C.POINTER(C.c_uint32), C.POINTER(C.c_int32), C.POINTER(C.c_int32),
                                    C.POINTER(C.c_int32), C.POINTER(C.c_double)]),
     ("snapgpu_compute_mapq", C.c_int, [C.c_double, C.c_double, C.c_int, C.c_int]),
+    ("snapgpu_cigar_batch", C.c_int, [C.c_void_p, C.POINTER(Reads), C.c_void_p, C.c_void_p, C.c_int, C.c_void_p,
+                                      C.c_void_p, C.c_void_p]),
+    ("snapgpu_cigar_resident", C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
+    ("snapgpu_cigar_download", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("snapgpu_cigar_last_ms", C.c_int, [C.c_void_p, C.POINTER(C.c_double)]),
+    ("snapgpu_sam_format", C.c_int, [C.c_void_p, C.POINTER(Reads), C.c_char_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_char_p, C.c_void_p, C.c_uint64,
+                                     C.POINTER(C.c_uint64)]),
 ]
+
+CIGAR_MAX_OPS = 64   # SNAPGPU_CIGAR_MAX_OPS
 
 EXPORTED_SYMBOLS = [p[0] for p in _PROTOS]
 

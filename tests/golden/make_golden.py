@@ -10,6 +10,7 @@ TSV/JSON expected outputs.
 
     python3 tests/golden/make_golden.py                  # everything
     python3 tests/golden/make_golden.py --only-multihit  # windowed search / multi-hit runs only
+    python3 tests/golden/make_golden.py --only-cigar     # CIGAR calls + SAM records only
 """
 import hashlib
 import json
@@ -126,8 +127,56 @@ def multihit_fixtures(work):
             f.write(ref_tsvx_to_canonical(out))
 
 
+def read_fastq(path):
+    lines = open(path).read().split("\n")
+    return [(lines[i][1:], lines[i + 1], lines[i + 3]) for i in range(0, len(lines) - 3, 4)]
+
+
+def cigar_fixtures(work):
+    """CIGAR / SAM record: the reference's own SAM writer
+    (FileFormat::SAM[useM]->writeRead, SAM.cpp:1007-1155) over BaseAligner's results on
+    the small genome, and LandauVishkinWithCigar as computeCigarString calls it
+    (SAM.cpp:1162-1230) at the aligned location and at perturbed / random locations
+    (large edit distances, indel-heavy backtraces, '*' results, genome ends)."""
+    import gzip
+    fa = os.path.join(HERE, "small.fa")
+    idxdir = os.path.join(work, "small_idx_cig")
+    ref_index(fa, idxdir)
+    g = snapgpu.Genome.from_fasta(fa, 500)
+    fq = os.path.join(HERE, "small_reads.fq")
+    sam = run([HARNESS, "sam", idxdir, fq])
+    with gzip.open(os.path.join(HERE, "expected_small.sam.gz"), "wt", compresslevel=9) as f:
+        f.write(sam)
+    reads = read_fastq(fq)
+    res = [l.split("\t") for l in open(os.path.join(HERE, "expected_small_default.tsv")).read().splitlines()]
+    rng = random.Random(31)
+    nb = g.n_bases
+    rows = []
+    for (rid, b, q), r in zip(reads, res):
+        result, loc, d = int(r[1]), int(r[2]), int(r[3])
+        if loc != 0xFFFFFFFF:
+            rows.append((loc, 0 if result == 0 else d, rng.randrange(2), b))
+            for _ in range(2):
+                dl = rng.choice([rng.randrange(-4, 5), rng.randrange(-35, 36)])
+                pl = max(0, loc + dl)
+                rows.append((pl, d if rng.random() < 0.8 else 1 - d, rng.randrange(2), b))
+        if rng.random() < 0.15:
+            rows.append((rng.choice([0, 1, nb - len(b), nb - len(b) + 1, nb - 50, nb + 99, rng.randrange(nb)]),
+                         rng.randrange(2), rng.randrange(2), b))
+    inp = os.path.join(HERE, "cigar_calls.tsv")
+    with open(inp, "w") as f:
+        f.writelines(f"{a}\t{b}\t{c}\t{d}\n" for a, b, c, d in rows)
+    with open(os.path.join(HERE, "expected_cigar.tsv"), "w") as f:
+        f.write(run([HARNESS, "cigar", idxdir, inp]))
+
+
 def main():
     work = tempfile.mkdtemp(prefix="golden_")
+    if "--only-cigar" in sys.argv:
+        cigar_fixtures(work)
+        shutil.rmtree(work, ignore_errors=True)
+        print("CIGAR / SAM fixtures written to", HERE)
+        return
     if "--only-multihit" in sys.argv:
         multihit_fixtures(work)
         shutil.rmtree(work, ignore_errors=True)
@@ -151,6 +200,7 @@ def main():
             f.write(ref_align(idxdir, fq, params))
 
     multihit_fixtures(work)
+    cigar_fixtures(work)
 
     # 2. lookupSeed golden: seeds from the genome, their RCs, mutated and random seeds
     rng = random.Random(9)

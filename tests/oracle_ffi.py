@@ -32,6 +32,9 @@ def oracle_lib():
         o.oracle_lv.argtypes = [C.c_int, C.c_char_p, C.c_int, C.c_char_p, C.c_char_p, C.c_int, C.c_int,
                                 C.POINTER(C.c_double), C.POINTER(C.c_int)]
         o.oracle_lv.restype = C.c_int
+        o.oracle_cigar.argtypes = [C.POINTER(F.IndexView), C.c_uint32, C.c_char_p, C.c_int, C.c_int,
+                                   C.POINTER(C.c_uint32), C.POINTER(C.c_int)]
+        o.oracle_cigar.restype = C.c_int
         o.oracle_compute_mapq.argtypes = [C.c_double, C.c_double, C.c_int, C.c_int]
         o.oracle_compute_mapq.restype = C.c_int
         _orc = o
@@ -126,3 +129,35 @@ def canonical_tsv(res):
                      f"{r['nLookups']}\t{r['nLocationsScored']}\t{r['popularSeedsSkipped']}\t"
                      f"{int(pa[i]):016x}\t{int(pb[i]):016x}")
     return "\n".join(lines) + "\n"
+
+
+_UPPER = bytes(c - 32 if 97 <= c <= 122 else c for c in range(256))      # Tables.cpp:74-80
+_COMP = bytearray(256)                                                     # Tables.cpp:22-30
+for a, b in zip(b"ACGTNn", b"TGCANn"):
+    _COMP[a] = b
+_COMP = bytes(_COMP)
+
+
+def sam_pattern(read, direction):
+    """The read as getSAMData hands it to computeCigarString (SAM.cpp:866-883)."""
+    r = (read.encode() if isinstance(read, str) else bytes(read)).translate(_UPPER)
+    return r.translate(_COMP)[::-1] if direction else r
+
+
+def oracle_cigars(index, reads_bases, locations, directions, use_m):
+    """CPU restatement of computeCigarString -> list of (editDistance, cigar string)."""
+    import snapgpu
+    v = index.view()
+    ops = (C.c_uint32 * 64)()
+    nops = C.c_int()
+    out = []
+    for b, loc, d in zip(reads_bases, locations, directions):
+        p = sam_pattern(b, d)
+        if int(loc) == 0xFFFFFFFF:
+            out.append((-1, "*"))
+            continue
+        ed = oracle_lib().oracle_cigar(C.byref(v), int(loc), p + b"\0" * 16, len(p), int(use_m), ops,
+                                       C.byref(nops))
+        s = "*" if ed < 0 else "".join(f"{ops[k] >> 4}{snapgpu.CIGAR_OPS[ops[k] & 15]}" for k in range(nops.value))
+        out.append((ed, s))
+    return out
