@@ -163,6 +163,28 @@ def main():
         pcie = {"value": args.reads / p_s, "unit": "reads/s", "ms": p_s * 1000.0,
                 "note": "snapgpu_align_batch on host buffers (H2D reads, GPU passes, D2H records), 1 call, rank 0",
                 "same_results": bool(np.array_equal(hres.view(np.uint8), res.view(np.uint8)))}
+        # SAM records: GPU CIGARs of the resident records
+        # (cigar_kernel, HIP events on the aligner's stream), then the host SAM lines
+        cig_ms = []
+        for _ in range(3):
+            dev.run_cigars()
+            cig_ms.append(aligner.cigar_ms())
+        cig = dev.cigars()
+        mapped = int((cig.editDistance >= 0).sum())
+        # per read: offset + length + record (8 + 4 + 64), the read (100), the genome window
+        # (len + 128), outputs (4 + 4 + 256)
+        cig_bytes = args.reads * (8 + 4 + 64 + READ_LEN + READ_LEN + 128 + 4 + 4 + 256)
+        cig_s = float(np.mean(cig_ms)) / 1000.0
+        ids = [f"read{i}" for i in range(args.reads)]
+        s0 = time.perf_counter()
+        sam = snapgpu.sam_format(idx, reads, ids, res, cig)
+        sam_s = time.perf_counter() - s0
+        sam_rec = {"kernel": "cigar_kernel", "kernel_ms": cig_s * 1000.0, "reads_per_s": args.reads / cig_s,
+                   "with_cigar": mapped, "achieved": cig_bytes / cig_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                   "frac": cig_bytes / cig_s / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": cig_bytes,
+                   "sam_format_reads_per_s": args.reads / sam_s, "sam_bytes": len(sam),
+                   "sam_format_threads": min(16, os.cpu_count() or 1)}
+        del sam
         cpu = None
         parity = None
         if not args.no_cpu_baseline and world == 1:   # CPU baseline: rank 0 at N=1 only
@@ -175,6 +197,12 @@ def main():
                    "sample": f"the rank-0 shard ({args.reads} reads) of the timed workload, oracle/snap_oracle.c "
                              f"(bit-exact C restatement of BaseAligner), {nthr} host threads, {cdt:.2f} s wall"}
             parity = {"reads_compared": len(res), "mismatches": int(len(mismatches(res, cres)))}
+            from oracle_ffi import oracle_cigars   # CIGAR parity on a 20k-read sample
+            ns = min(20000, args.reads)
+            loc, dirs = snapgpu.cigar_inputs(res[:ns])
+            want = oracle_cigars(idx, [reads.get(i)[0] for i in range(ns)], loc, dirs, 0)
+            sam_rec["parity"] = {"reads_compared": ns, "mismatches": sum(
+                1 for i in range(ns) if (int(cig.editDistance[i]), cig.string(i)) != want[i])}
         out = {
             "metric": "aligned reads/sec (100 bp SE, k=20 seed) at 1/2/4/8 GPUs + CPU baseline",
             "value": value,
@@ -207,6 +235,7 @@ def main():
             "cpu_baseline": cpu,
             "pcie_inclusive": pcie,
             "parity": parity,
+            "sam_records": sam_rec,
         }
         print(json.dumps(out), flush=True)
     if dist:
