@@ -545,6 +545,9 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<128> &S, Elem1
     uint16_t *order = S.u.sc.order;
     uint32_t fDone = 0, fAvail = 0, ordBase = 0;
     for (uint32_t guard = 0;; guard++) {
+        // lane id re-read per batch (volatile asm): masks and addresses derived from it are
+        // recomputed in the batch instead of hoisted and kept live, spilled, across the pass loop
+        const int lane = lane_id();
         if (guard > (uint32_t)A.arenaElems) {   // every batch unlinks >= 1 element
             if (lane == 0) diag_report(DIAG_SCORE_LOOP, st.rid, S.nElems);
             st.abort = 1;
