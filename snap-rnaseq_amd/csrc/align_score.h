@@ -394,6 +394,7 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<128> &S, Elem128 
     const uint32_t sl = P.cw >> 8, bit = P.cw & 0xff;
     const uint32_t ew11 = leader ? G.ecache[sl][11] : 0u;
     for (int g0 = 0; g0 < m;) {
+        const int lane = lane_id();   // re-read per step: `lane == c` masks are not hoisted and spilled
         const int kNow = (int)(st.scoreLimit < (uint32_t)(MAX_K - 1) ? st.scoreLimit : MAX_K - 1);
         // element lps test, made once when the element's first candidate is reached
         // (BaseAligner.cpp:1129); candidates of one element are contiguous

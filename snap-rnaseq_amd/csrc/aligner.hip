@@ -430,6 +430,9 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
         const uint32_t seedGuard = (nPossible + 2) * (seedLen + 2) + maxSeeds;
         PH_T(A, tsl);
         for (uint32_t guard = 0;; guard++) {
+            // lane id re-read per seed (volatile asm): lane-derived masks are recomputed here,
+            // not hoisted out of the seed loop and kept live in spilled SGPRs
+            const int lane = lane_id();
             bool force = st.nSeedsApplied[0] + st.nSeedsApplied[1] >= maxSeeds;
             if (guard > seedGuard) {   // each pass consumes a seed position or a wrap
                 if (lane == 0) diag_report(DIAG_SEED_LOOP, r, next);
