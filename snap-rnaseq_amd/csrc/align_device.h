@@ -574,16 +574,23 @@ __device__ __forceinline__ uint32_t count_above_desc(const uint32_t *L, uint32_t
 // ------------------------------------------------------- phase diagnostics
 // With KArgs::phaseBuf set, lane 0 of each wave adds s_memtime deltas per phase (and
 // event counts) to its block's slice with no-return atomics (snapgpu_phase_cycles).
-// Off: one SGPR test per site.
+// Compiled in only with -DSNAPGPU_PHASE_TIMERS=1 (`make PHASE_TIMERS=1`): even switched off
+// at run time, the timestamps held across loops cost SGPR spills in the production kernel.
 enum : int { PH_SETUP = 0, PH_LOOKUP, PH_INSERT, PH_SCORE, PH_POP, PH_DESC, PH_STAGE, PH_LVF, PH_LVR, PH_APPLY,
              PH_WB, PH_OUT, PH_NPASS, PH_NCAND, PH_NREAD, PH_NPASS16, PH_NPASS32, PH_NPASS64, PH_ROWSF, PH_ROWSR,
              PH_NSCORECALL, PH_NFORCED, PH_NPOPPED, PH_NSUCC, PH_PASSLOOP, PH_SEL, PH_FETCH, PH_SEEDLOOP, PH_SLOTS = 32 };
 __device__ __forceinline__ uint64_t clk() { return __builtin_amdgcn_s_memtime(); }
+#if SNAPGPU_PHASE_TIMERS
 #define PH_T(A, v) const uint64_t v = (A).phaseBuf ? sgk::clk() : 0
 #define PH_ADD(A, S, i, v) do { if ((A).phaseBuf && sgk::lane_id() == 0) \
     atomicAdd((A).phaseBuf + blockIdx.x * sgk::PH_SLOTS + (i), (unsigned long long)(sgk::clk() - (v))); } while (0)
 #define PH_CNT(A, S, i, n) do { if ((A).phaseBuf && sgk::lane_id() == 0) \
     atomicAdd((A).phaseBuf + blockIdx.x * sgk::PH_SLOTS + (i), (unsigned long long)(n)); } while (0)
+#else
+#define PH_T(A, v)
+#define PH_ADD(A, S, i, v) do { } while (0)
+#define PH_CNT(A, S, i, n) do { } while (0)
+#endif
 
 // computeMAPQ (mapq.h:32-65) without log10: floor(-10*log10(x)) >= q  <=>  x <= 10^(-q/10).
 // A ratio within 1e-9 (relative) of a threshold is flagged and re-derived on the host

@@ -1232,6 +1232,10 @@ int snapgpu_aligner_get_stats(const snapgpu_aligner_t *a, snapgpu_aligner_stats_
 int snapgpu_phase_cycles(snapgpu_aligner_t *a, uint64_t *out, int reset) {
     if (!a || !out) return SNAPGPU_EINVAL;
     memset(out, 0, PH_SLOTS * sizeof(uint64_t));
+#if !SNAPGPU_PHASE_TIMERS
+    snapgpu::setError("library built without phase timers (make PHASE_TIMERS=1)");
+    return SNAPGPU_EUNSUPPORTED;
+#endif
     if (!a->dPhase) { snapgpu::setError("phase diagnostics off (set SNAPGPU_PHASES=1 before aligner_create)"); return SNAPGPU_EINVAL; }
     HIPCHK(hipSetDevice(a->device));
     HIPCHK(hipStreamSynchronize(a->stream));

@@ -1,7 +1,11 @@
 #!/usr/bin/env python3
 """Diagnostic: per-phase cycle breakdown of align_kernel on the bench workload.
 
-Run on the GPU box: SNAPGPU_PHASES=1 python tools/phase_probe.py [--reads N]
+Needs a library built with the timers compiled in (they cost SGPR spills, so the
+production build leaves them out):
+    MK='s/PHASE_TIMERS ?= 0/PHASE_TIMERS ?= 1/' tools/build_variant.sh phases ""   # -> libsnapgpu_phases.so
+Run on the GPU box:
+    SNAPGPU_LIB=$PWD/snap-rnaseq_amd/snapgpu/libsnapgpu_phases.so SNAPGPU_PHASES=1 python tools/phase_probe.py [--reads N]
 """
 import argparse
 import json
