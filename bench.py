@@ -154,6 +154,15 @@ def main():
                   "achieved": lk_bytes / lk_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                   "frac": lk_bytes / lk_s / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": lk_bytes,
                   "seeds": int(t["lookupSeeds"]), "probes": int(t["lookupProbes"])}
+        # measured random-gather ceiling of the same table (independent 12-B slot loads, no
+        # dependency chain): the bandwidth the lookups' access pattern can reach on this GPU
+        n_g = 1 << 24
+        g_ms = aligner.gather_peak_ms(n_g)
+        lookup["gather_peak"] = {"loads": n_g, "ms": g_ms, "achieved": 12.0 * n_g / (g_ms / 1000.0) / 1e9,
+                                 "unit": "GB/s", "note": "12 B per random slot load, best of 3"}
+        # probes/s of the lookups against slot loads/s of the ceiling: the fraction of the measured
+        # random-access HBM throughput the dependent probe chains sustain
+        lookup["probe_rate_frac_of_gather_peak"] = (t["lookupProbes"] / lk_s) / (n_g / (g_ms / 1000.0))
         counts = {int(k): int(v) for k, v in zip(*np.unique(res["result"], return_counts=True))}
         # host-buffer boundary: snapgpu_align_batch = H2D of the reads +
         # the GPU passes + D2H of the records + host MAPQ fix-ups; reported beside `value`

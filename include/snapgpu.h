@@ -352,6 +352,11 @@ int snapgpu_sam_format(const snapgpu_index_t *idx, const snapgpu_reads_t *reads,
                        const int32_t *editDistance, const uint32_t *nOps, const uint32_t *ops,
                        const char *readGroup, char *out, uint64_t cap, uint64_t *used);
 
+/* Roofline calibration (diagnostic, no reference equivalent): time of nLoads independent
+ * 12-byte SNAPHashTable slot loads at hashed positions of this aligner's resident table
+ * (the access pattern of the seed lookups without their dependency chain), best of 3, ms. */
+int snapgpu_gather_peak(snapgpu_aligner_t *a, uint32_t nLoads, double *ms);
+
 /* MAPQ (mapq.h:32-65) as the host computes it; exported for tests. */
 int snapgpu_compute_mapq(double pAll, double pBest, int score, int popularSeedsSkipped);
 

@@ -813,6 +813,24 @@ struct snapgpu_aligner {
 
 static const size_t kDevGuard = 1024;
 
+// Random-gather ceiling of the hash-table memory (roofline calibration for
+// seed_lookup_kernel): one independent 12-byte slot load per lane at a
+// hashed position of the resident SNAPHashTable slots -- the lookup kernel's access
+// pattern without its dependency chain.  The xor of the loaded words goes to `sink` only
+// when it equals the salt (practically never), so the loads cannot be dropped.
+__global__ __launch_bounds__(256) void gather_peak_kernel(const uint32_t *slots, uint32_t nSlots, uint32_t nLoads,
+                                                          uint32_t salt, uint32_t *sink) {
+    const uint32_t i = (blockIdx.x * 256u + threadIdx.x) * 4u;   // 4 independent loads per lane
+    uint32_t x = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++)
+        if (i + j < nLoads) {
+            const uint32_t *p = slots + 3ull * (sgk::fmix32((i + j) ^ salt) % nSlots);
+            x ^= p[0] ^ p[1] ^ p[2];
+        }
+    if (x == salt) sink[0] = x;   // data-dependent: the loads stay
+}
+
 extern "C" {
 
 void snapgpu_aligner_params_default(snapgpu_aligner_params_t *p) {
@@ -1406,6 +1424,28 @@ int snapgpu_cigar_batch(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, cons
     hipFree(dDir);
     snapgpu_device_reads_free(d);
     return rc;
+}
+
+int snapgpu_gather_peak(snapgpu_aligner_t *a, uint32_t nLoads, double *ms) {
+    if (!a || !ms || nLoads == 0) return SNAPGPU_EINVAL;
+    HIPCHK(hipSetDevice(a->device));
+    const uint64_t nSlots = a->idx->slots.size() / 3;
+    if (nSlots == 0 || nSlots >= (1ull << 32)) { snapgpu::setError("gather_peak: slot count"); return SNAPGPU_EINVAL; }
+    const unsigned grid = (nLoads + 1023) / 1024;
+    float best = 0;
+    for (int rep = 0; rep < 3; rep++) {
+        HIPCHK(hipEventRecord(a->cev[0], a->stream));
+        hipLaunchKernelGGL(gather_peak_kernel, dim3(grid), dim3(256), 0, a->stream, a->dSlots, (uint32_t)nSlots, nLoads,
+                           0x5bd1e995u * (rep + 1), a->dCounter);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(a->cev[1], a->stream));
+        HIPCHK(hipEventSynchronize(a->cev[1]));
+        float f = 0;
+        HIPCHK(hipEventElapsedTime(&f, a->cev[0], a->cev[1]));
+        if (rep == 0 || f < best) best = f;
+    }
+    *ms = best;
+    return SNAPGPU_OK;
 }
 
 }  // extern "C"

@@ -314,6 +314,13 @@ class BaseAligner:
                    "cigar_batch")
         return c
 
+    def gather_peak_ms(self, n_loads):
+        """Diagnostic: best-of-3 time (ms) of n_loads independent random 12-byte slot loads
+        from the resident hash table (roofline calibration for the seed lookups)."""
+        ms = C.c_double()
+        _check(lib().snapgpu_gather_peak(self._h, int(n_loads), C.byref(ms)), "gather_peak")
+        return ms.value
+
     def cigar_ms(self):
         ms = C.c_double()
         _check(lib().snapgpu_cigar_last_ms(self._h, C.byref(ms)), "cigar_last_ms")
