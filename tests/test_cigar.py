@@ -176,3 +176,28 @@ def test_gpu_cigar_matches_oracle_c1(gpu_available, small_world):
         bad = [j for j in range(reads.n) if got[j] != want[j]]
         assert not bad, f"{len(bad)} differ, e.g. {[(got[j], want[j]) for j in bad[:2]]}"
         assert sum(1 for e, _ in want if e > 3) > 100     # indel-heavy / large-distance cases exercised
+
+
+@pytest.mark.gpu
+def test_gpu_cigar_edge_cases(gpu_available, small):
+    """Empty batch; zero-length and single-base reads; no location; genome start/end;
+    reads longer than 512 bases rejected; all-N read."""
+    idx, _, _ = small
+    al = snapgpu.BaseAligner(idx)
+    empty = al.Cigars(snapgpu.Reads.from_list([]), [], [])
+    assert len(empty.editDistance) == 0
+    g = snapgpu.Genome.from_fasta(os.path.join(G, "small.fa"), 500)
+    nb = g.n_bases
+    seq = g.bases(600, 120).decode()
+    rows = [("", 600, 0), ("A", 600, 0), (seq, 0xFFFFFFFF, 0), (seq, 0, 0), (seq, nb - 120, 1), (seq, nb + 50, 0),
+            ("N" * 100, 600, 0), (seq, 600, 1), (seq.lower(), 600, 0), (seq[:60] + "ACGT" + seq[60:], 600, 0)]
+    reads = snapgpu.Reads.from_list([(b, "I" * len(b)) for b, _, _ in rows])
+    for use_m in (0, 1):
+        c = al.Cigars(reads, [r[1] for r in rows], [r[2] for r in rows], useM=use_m)
+        want = oracle_cigars(idx, [r[0] for r in rows], [r[1] for r in rows], [r[2] for r in rows], use_m)
+        got = [(int(c.editDistance[j]), c.string(j)) for j in range(len(rows))]
+        assert got == want, [(i, a, b) for i, (a, b) in enumerate(zip(got, want)) if a != b]
+    assert got[2] == (-1, "*") and got[5] == (-1, "*")
+    long_read = snapgpu.Reads.from_list([("A" * 513, "I" * 513)])
+    with pytest.raises(snapgpu.SnapGpuError):
+        al.Cigars(long_read, [600], [0])
