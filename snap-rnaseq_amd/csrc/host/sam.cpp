@@ -45,6 +45,18 @@ int pieceAt(const Genome &g, uint32_t loc) {
     return -1;
 }
 
+// decimal without snprintf (the lines are written at millions per second)
+inline void appendUint(std::string &o, uint64_t v) {
+    char b[24];
+    int k = 0;
+    do { b[k++] = (char)('0' + v % 10); v /= 10; } while (v);
+    while (k) o += b[--k];
+}
+inline void appendInt(std::string &o, int64_t v) {
+    if (v < 0) { o += '-'; appendUint(o, (uint64_t)(-v)); }
+    else appendUint(o, (uint64_t)v);
+}
+
 struct Job {
     const Index *idx;
     const snapgpu_reads_t *reads;
@@ -87,20 +99,23 @@ void formatOne(const Job &J, uint64_t i, std::string &o) {
     const char *id = J.ids + J.idOffsets[i];
     uint32_t qlen = J.idLengths[i];
     if (const void *sp = memchr(id, ' ', qlen)) qlen = (uint32_t)((const char *)sp - id);
-    char num[64];
     o.append(id, qlen);
-    snprintf(num, sizeof num, "\t%d\t", flags);
-    o += num;
+    o += '\t';
+    appendInt(o, flags);
+    o += '\t';
     o += pieceName;
-    snprintf(num, sizeof num, "\t%u\t%d\t", pos, mapq);
-    o += num;
+    o += '\t';
+    appendUint(o, pos);
+    o += '\t';
+    appendInt(o, mapq);
+    o += '\t';
     // CIGAR: computed at writeRead's own location (even for NotFound) -- SAM.cpp:1041-1048
     const int32_t ed = r.location != kInvalidLocation ? J.ed[i] : -1;
     if (r.location != kInvalidLocation && ed >= 0) {
         const uint32_t *op = J.ops + i * SNAPGPU_CIGAR_MAX_OPS;
         for (uint32_t k = 0; k < J.nOps[i]; k++) {
-            snprintf(num, sizeof num, "%u%c", op[k] >> 4, kOp[op[k] & 15]);
-            o += num;
+            appendUint(o, op[k] >> 4);
+            o += kOp[op[k] & 15];
         }
     } else {
         o += '*';
@@ -108,21 +123,26 @@ void formatOne(const Job &J, uint64_t i, std::string &o) {
     // SEQ / QUAL are printed with "%.*s" (SAM.cpp:1122-1136): a NUL byte ends them early
     // (COMPLEMENT[] of a non-ACGTN base is 0; a quality string shorter than the read)
     o += "\t*\t0\t0\t";
-    const size_t s0 = o.size();
-    o.resize(s0 + len);
-    for (uint32_t k = 0; k < len; k++) o[s0 + k] = rc ? complement(upperCase(bases[len - 1 - k])) : upperCase(bases[k]);
-    o.resize(s0 + strnlen(o.data() + s0, len));
+    char sq[2 * 1024];
+    const uint32_t L = len < 1024 ? len : 1024;
+    uint32_t ns = 0, nq = 0;
+    if (rc) {
+        while (ns < L && (sq[ns] = complement(upperCase(bases[len - 1 - ns]))) != 0) ns++;
+        while (nq < L && (sq[1024 + nq] = quals[len - 1 - nq]) != 0) nq++;
+    } else {
+        while (ns < L && (sq[ns] = upperCase(bases[ns])) != 0) ns++;
+        while (nq < L && (sq[1024 + nq] = quals[nq]) != 0) nq++;
+    }
+    o.append(sq, ns);
     o += '\t';
-    const size_t q0 = o.size();
-    o.resize(q0 + len);
-    for (uint32_t k = 0; k < len; k++) o[q0 + k] = rc ? quals[len - 1 - k] : quals[k];
-    o.resize(q0 + strnlen(o.data() + q0, len));
+    o.append(sq + 1024, nq);
     if (J.rg) {
         o += "\tRG:Z:";
         o += J.rg;
     }
-    snprintf(num, sizeof num, "\tPG:Z:SNAP\tNM:i:%d\n", ed);
-    o += num;
+    o += "\tPG:Z:SNAP\tNM:i:";
+    appendInt(o, ed);
+    o += '\n';
 }
 
 }  // namespace
@@ -137,8 +157,8 @@ extern "C" int snapgpu_sam_format(const snapgpu_index_t *idx, const snapgpu_read
         return SNAPGPU_EINVAL;
     }
     for (uint64_t i = 0; i < reads->n; i++)
-        if (nOps[i] > SNAPGPU_CIGAR_MAX_OPS) {
-            setError("sam_format: nOps > SNAPGPU_CIGAR_MAX_OPS");
+        if (nOps[i] > SNAPGPU_CIGAR_MAX_OPS || reads->lengths[i] > 1024) {   // the reference writer: <= 500
+            setError("sam_format: nOps > SNAPGPU_CIGAR_MAX_OPS or read longer than 1024 bases");
             return SNAPGPU_EINVAL;
         }
     Job J{idx, reads, ids, idOffsets, idLengths, results, editDistance, nOps, ops, readGroup};

@@ -458,10 +458,13 @@ def sam_format(index, reads, ids, results, cigars, read_group="FASTQ"):
     rg = None if read_group is None else read_group.encode()
     args = [index._h, reads._p, blob, offs.ctypes.data, lens.ctypes.data, res.ctypes.data,
             cigars.editDistance.ctypes.data, cigars.nOps.ctypes.data, cigars.ops.ctypes.data, rg]
-    lib().snapgpu_sam_format(*args, None, 0, C.byref(used))
-    buf = C.create_string_buffer(max(1, used.value))
-    _check(lib().snapgpu_sam_format(*args, buf, used.value, C.byref(used)), "sam_format")
-    return buf.raw[:used.value]
+    # one formatting pass with a generous buffer; a second only if it was too small
+    cap = int(lens.sum()) + 2 * int(reads._p.contents.totalBytes) + n * 512
+    buf = C.create_string_buffer(max(1, cap))
+    if lib().snapgpu_sam_format(*args, buf, cap, C.byref(used)) != 0:
+        buf = C.create_string_buffer(max(1, used.value))
+        _check(lib().snapgpu_sam_format(*args, buf, used.value, C.byref(used)), "sam_format")
+    return C.string_at(buf, used.value)
 
 
 def lv_batch(direction, tasks, device=0):
