@@ -117,7 +117,9 @@ def main():
     genome, reads = make_workload(snapgpu, args.genome_bases, args.reads, rank)
     idx = snapgpu.GenomeIndex.build(genome, 20, min(16, os.cpu_count() or 8))
     t_index = time.time() - t0
-    aligner = snapgpu.BaseAligner(idx, device=local)
+    t1 = time.time()
+    aligner = snapgpu.BaseAligner(idx, device=local)   # index + genome upload to this GPU's HBM
+    t_upload = time.time() - t1
     dev = aligner.upload(reads)
 
     for _ in range(args.warmup):
@@ -235,6 +237,7 @@ def main():
                             "NotFound": counts.get(0, 0)},
                 "per_read": {k: round(float(v), 2) for k, v in per_read.items()},
                 "index_build_s": round(t_index, 2),
+                "index_upload_s": round(t_upload, 2),
             },
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
