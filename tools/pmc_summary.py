@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise a gpu_prof.sh run (rocprofv3 kernel trace + PMC passes) for the
+"""Summarise a tools/gpu/prof.sh run (rocprofv3 kernel trace + PMC passes) for the
 dominant kernel: per-launch averages of every counter, the kernel-trace duration,
 and the HBM traffic figure bench.py reports (profiles/pmc_traffic.json).
 
