@@ -352,6 +352,12 @@ int snapgpu_sam_format(const snapgpu_index_t *idx, const snapgpu_reads_t *reads,
                        const int32_t *editDistance, const uint32_t *nOps, const uint32_t *ops,
                        const char *readGroup, char *out, uint64_t cap, uint64_t *used);
 
+/* The SAM header as SAMFormat::writeHeader (SAM.cpp:700-800) writes it for a FASTQ input:
+ * @HD (SO:coordinate if sorted), rgLine or "@RG\tID:FASTQ\tSM:sample", @PG with CL:commandLine
+ * and VN:version, one @SQ per genome piece.  Same size / error contract as snapgpu_sam_format. */
+int snapgpu_sam_header(const snapgpu_index_t *idx, int sorted, const char *commandLine, const char *version,
+                       const char *rgLine, char *out, uint64_t cap, uint64_t *used);
+
 /* Roofline calibration (diagnostic, no reference equivalent): time of nLoads independent
  * 12-byte SNAPHashTable slot loads at hashed positions of this aligner's resident table
  * (the access pattern of the seed lookups without their dependency chain), best of 3, ms. */

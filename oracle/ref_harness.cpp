@@ -20,6 +20,9 @@
 //          -> per read: AlignRead, then the reference's own SAM writer
 //             (FileFormat::SAM[useM]->writeRead, SAM.cpp:1007-1155) for useM = 0 and 1:
 //             two SAM lines per read
+//   samheader <indexDir> <sorted 0|1> <version> [args...]
+//          -> SAMFormat::writeHeader (SAM.cpp:700-800) for a FASTQ input (no input header),
+//             default read group, command line = args
 //   cigar  <indexDir> <calls.tsv>  lines: loc dir useM read
 //          -> ed cigar   (SAMFormat::computeCigarString, SAM.cpp:1162-1230, restated
 //             around the reference's LandauVishkinWithCigar with zeroed slack bytes)
@@ -242,6 +245,22 @@ static int mode_cigar(int argc, char **argv) {
     return 0;
 }
 
+static int mode_samheader(int argc, char **argv) {
+    if (argc < 5) { fprintf(stderr, "samheader <indexDir> <sorted> <version> [args...]\n"); return 2; }
+    GenomeIndex *idx = GenomeIndex::loadFromDirectory(argv[2]);
+    if (!idx) return 1;
+    ReaderContext ctx;
+    memset(&ctx, 0, sizeof(ctx));
+    ctx.genome = idx->getGenome();
+    ctx.defaultReadGroup = "FASTQ";
+    std::vector<char> buf(1 << 24);
+    size_t used = 0;
+    if (!FileFormat::SAM[0]->writeHeader(ctx, &buf[0], buf.size(), &used, atoi(argv[3]) != 0, argc - 5,
+                                         (const char **)(argv + 5), argv[4], NULL)) return 1;
+    fwrite(&buf[0], 1, used, stdout);
+    return 0;
+}
+
 int main(int argc, char **argv) {
     if (argc < 2) { fprintf(stderr, "usage: ref_harness align|lv|lookup ...\n"); return 2; }
     std::string m = argv[1];
@@ -251,6 +270,7 @@ int main(int argc, char **argv) {
     if (m == "lookup") return mode_lookup(argc, argv);
     if (m == "sam") return mode_sam(argc, argv);
     if (m == "cigar") return mode_cigar(argc, argv);
+    if (m == "samheader") return mode_samheader(argc, argv);
     fprintf(stderr, "unknown mode %s\n", argv[1]);
     return 2;
 }

@@ -187,3 +187,40 @@ extern "C" int snapgpu_sam_format(const snapgpu_index_t *idx, const snapgpu_read
     }
     return SNAPGPU_OK;
 }
+
+// SAMFormat::writeHeader (SAM.cpp:700-800) for an input without its own header (FASTQ):
+// @HD, the read-group line, @PG, then one @SQ per genome piece with LN = piece span - 500
+// (the reference subtracts a fixed 500, whatever the padding; unsigned arithmetic kept).
+extern "C" int snapgpu_sam_header(const snapgpu_index_t *idx, int sorted, const char *commandLine,
+                                  const char *version, const char *rgLine, char *out, uint64_t cap, uint64_t *used) {
+    if (!idx || !commandLine || !version || !used) {
+        setError("sam_header: null argument");
+        return SNAPGPU_EINVAL;
+    }
+    const Genome &g = *idx->genome;
+    std::string o = "@HD\tVN:1.4\tSO:";
+    o += sorted ? "coordinate" : "unsorted";
+    o += '\n';
+    o += rgLine ? rgLine : "@RG\tID:FASTQ\tSM:sample";
+    o += "\n@PG\tID:SNAP\tPN:SNAP\tCL:";
+    o += commandLine;
+    o += "\tVN:";
+    o += version;
+    o += '\n';
+    const size_t np = g.pieceOffsets.size();
+    for (size_t i = 0; i < np; i++) {
+        const uint32_t start = g.pieceOffsets[i], end = i + 1 < np ? g.pieceOffsets[i + 1] : g.nBases;
+        o += "@SQ\tSN:";
+        o += g.pieceNames[i];
+        o += "\tLN:";
+        appendUint(o, (uint32_t)((end - start) - 500u));
+        o += '\n';
+    }
+    *used = o.size();
+    if (o.size() > cap || !out) {
+        setError("sam_header: output buffer too small");
+        return SNAPGPU_EINVAL;
+    }
+    memcpy(out, o.data(), o.size());
+    return SNAPGPU_OK;
+}

@@ -442,6 +442,17 @@ def cigar_inputs(results):
     return loc, np.where(mapped, results["direction"], 0).astype(np.uint8)
 
 
+def sam_header(index, command_line, version, sorted_output=False, rg_line=None):
+    """SAM header (SAMFormat::writeHeader, SAM.cpp:700-800) for a FASTQ input -> bytes."""
+    used = C.c_uint64()
+    args = [index._h, int(sorted_output), command_line.encode(), version.encode(),
+            None if rg_line is None else rg_line.encode()]
+    lib().snapgpu_sam_header(*args, None, 0, C.byref(used))
+    buf = C.create_string_buffer(max(1, used.value))
+    _check(lib().snapgpu_sam_header(*args, buf, used.value, C.byref(used)), "sam_header")
+    return C.string_at(buf, used.value)
+
+
 def sam_format(index, reads, ids, results, cigars, read_group="FASTQ"):
     """SAM lines (SAMFormat::writeRead, SAM.cpp:1007-1155) of single-end genome
     alignments -> bytes.  ids: list of read ids (str/bytes)."""

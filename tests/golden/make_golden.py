@@ -145,8 +145,8 @@ def cigar_fixtures(work):
     g = snapgpu.Genome.from_fasta(fa, 500)
     fq = os.path.join(HERE, "small_reads.fq")
     sam = run([HARNESS, "sam", idxdir, fq])
-    with gzip.open(os.path.join(HERE, "expected_small.sam.gz"), "wt", compresslevel=9) as f:
-        f.write(sam)
+    with open(os.path.join(HERE, "expected_small.sam.gz"), "wb") as f:   # mtime 0: reproducible bytes
+        f.write(gzip.compress(sam.encode(), compresslevel=9, mtime=0))
     reads = read_fastq(fq)
     res = [l.split("\t") for l in open(os.path.join(HERE, "expected_small_default.tsv")).read().splitlines()]
     rng = random.Random(31)
@@ -168,6 +168,11 @@ def cigar_fixtures(work):
         f.writelines(f"{a}\t{b}\t{c}\t{d}\n" for a, b, c, d in rows)
     with open(os.path.join(HERE, "expected_cigar.tsv"), "w") as f:
         f.write(run([HARNESS, "cigar", idxdir, inp]))
+    # SAMFormat::writeHeader (SAM.cpp:700-800), unsorted and sorted
+    for srt in (0, 1):
+        with open(os.path.join(HERE, f"expected_small_header{srt}.sam"), "w") as f:
+            f.write(run([HARNESS, "samheader", idxdir, str(srt), "1.0dev.66", "snap-rna", "single", "idx",
+                         "reads.fq", "-o", "out.sam"]))
 
 
 def main():

@@ -201,3 +201,13 @@ def test_gpu_cigar_edge_cases(gpu_available, small):
     long_read = snapgpu.Reads.from_list([("A" * 513, "I" * 513)])
     with pytest.raises(snapgpu.SnapGpuError):
         al.Cigars(long_read, [600], [0])
+
+
+@pytest.mark.parametrize("sorted_output", [0, 1])
+def test_sam_header_matches_reference(small, sorted_output):
+    """SAMFormat::writeHeader (SAM.cpp:700-800) for a FASTQ input, against the reference's own."""
+    idx, _, _ = small
+    got = snapgpu.sam_header(idx, "snap-rna single idx reads.fq -o out.sam", "1.0dev.66",
+                             sorted_output=bool(sorted_output)).decode()
+    want = open(os.path.join(G, f"expected_small_header{sorted_output}.sam")).read()
+    assert got == want
