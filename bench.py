@@ -46,14 +46,15 @@ def algorithmic_bytes(res):
 
 
 def load_pmc_traffic():
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if present."""
+    """HBM bytes and VALU instructions per launch from the committed rocprofv3 PMC summary."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(p):
         try:
-            return json.load(open(p)).get("bytes_per_launch")
+            d = json.load(open(p))
+            return d.get("bytes_per_launch"), d.get("valu_insts_per_launch")
         except Exception:
-            return None
-    return None
+            return None, None
+    return None, None
 
 
 def init_distributed():
@@ -145,7 +146,16 @@ def main():
         bytes_launch, per_read = algorithmic_bytes(res)
         avg_kernel_s = float(np.mean(kernel_ms)) / 1000.0
         achieved = bytes_launch / avg_kernel_s / 1e9
-        traffic = load_pmc_traffic()
+        traffic, valu = load_pmc_traffic()
+        # the bound that binds: VALU issue.  Wave64 VALU ops take 4 cycles on a
+        # 16-lane SIMD; 4 SIMDs per CU at the 2.4 GHz peak engine clock
+        import snapgpu as _sg
+        n_cu = _sg.device_cu_count(local)
+        valu_issue = None
+        if valu and n_cu:
+            valu_issue = {"valu_insts_per_launch": valu, "simds": 4 * n_cu, "clock_ghz": 2.4,
+                          "pipe_occupancy": valu * 4 / (4 * n_cu * avg_kernel_s * 2.4e9),
+                          "source": "profiles/pmc_traffic.json (SQ_INSTS_VALU of the committed PMC pass)"}
         # seed_lookup_kernel (pass 0): read bytes + offsets/lengths + 8 records of 16 B per read,
         # then per looked-up seed its table's (size, base), 12 B per probed entry, 4 B per overflow count
         t = aligner.timing()
@@ -242,7 +252,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "align_kernel<128, false>", "kernel_ms": float(np.mean(kernel_ms)),
-                         "algorithmic_bytes_per_launch": bytes_launch},
+                         "algorithmic_bytes_per_launch": bytes_launch, "valu_issue": valu_issue},
             "lookup_roofline": lookup,
             "cpu_baseline": cpu,
             "pcie_inclusive": pcie,

@@ -222,6 +222,7 @@ void snapgpu_reads_free(snapgpu_reads_t *r);
 typedef struct snapgpu_aligner snapgpu_aligner_t;
 
 int  snapgpu_device_count(void);
+int  snapgpu_device_cu_count(int device);   /* compute units of a device (0 if none) */
 /* BaseAligner::BaseAligner (BaseAligner.cpp:46-194) + index upload to HBM.  The
  * index must outlive the aligner. */
 snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx,

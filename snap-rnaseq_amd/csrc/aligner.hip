@@ -847,6 +847,12 @@ void snapgpu_aligner_params_default(snapgpu_aligner_params_t *p) {
 
 int snapgpu_compute_mapq(double pAll, double pBest, int score, int popular) { return hostMapq(pAll, pBest, score, popular); }
 
+int snapgpu_device_cu_count(int device) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return 0;
+    return prop.multiProcessorCount;
+}
+
 int snapgpu_device_count(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;

@@ -71,6 +71,10 @@ def _check(value, what):
     return value
 
 
+def device_cu_count(device=0):
+    return lib().snapgpu_device_cu_count(device)
+
+
 def device_count():
     return lib().snapgpu_device_count()
 

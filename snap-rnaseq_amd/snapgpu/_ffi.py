@@ -177,6 +177,7 @@ _PROTOS = [
     ("snapgpu_reads_write_fastq", C.c_int, [C.POINTER(Reads), C.c_char_p]),
     ("snapgpu_reads_free", None, [C.POINTER(Reads)]),
     ("snapgpu_device_count", C.c_int, []),
+    ("snapgpu_device_cu_count", C.c_int, [C.c_int]),
     ("snapgpu_aligner_create", C.c_void_p, [C.c_int, C.c_void_p, C.POINTER(AlignerParams)]),
     ("snapgpu_aligner_free", None, [C.c_void_p]),
     ("snapgpu_align_batch", C.c_int, [C.c_void_p, C.POINTER(Reads), C.POINTER(Result)]),

@@ -59,7 +59,9 @@ def main(src, dst):
     json.dump(out, open(os.path.join(dst, "summary.json"), "w"), indent=1)
     if "hbm_bytes_per_launch" in out:
         json.dump({"bytes_per_launch": out["hbm_bytes_per_launch"]["total"], "source": os.path.join(dst, "summary.json"),
-                   "note": "rocprofv3 FETCH_SIZE+WRITE_SIZE (KiB x 1024) per align_kernel<128> launch, uncorrected"},
+                   "note": "rocprofv3 FETCH_SIZE+WRITE_SIZE (KiB x 1024) per align_kernel<128> launch, uncorrected",
+                   "valu_insts_per_launch": out["counters_per_launch"].get("SQ_INSTS_VALU"),
+                   "kernel_ms": out.get("kernel_trace", {}).get("avg_ms")},
                   open(os.path.join(os.path.dirname(dst.rstrip("/")), "..", "pmc_traffic.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))
 
