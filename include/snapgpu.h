@@ -353,6 +353,19 @@ int snapgpu_sam_format(const snapgpu_index_t *idx, const snapgpu_reads_t *reads,
                        const int32_t *editDistance, const uint32_t *nOps, const uint32_t *ops,
                        const char *readGroup, char *out, uint64_t cap, uint64_t *used);
 
+/* Clipped reads (Read::clip, Read.h:357-404, applied by the FASTQ reader, FASTQ.cpp:250;
+ * clipping = NoClipping 0 / ClipFront 1 / ClipBack 2 / ClipFrontAndBack 3 -- the reference's
+ * default is 3): snapgpu_reads_clip narrows offsets/lengths in place to the clipped read (what
+ * the aligner and the CIGAR kernel see) and returns the front clip and unclipped length per
+ * read; snapgpu_sam_format_clipped then prints the unclipped SEQ/QUAL and the soft clips
+ * ("%uS" before / after the CIGAR, mirrored for RC -- SAM.cpp:866-883, 1212-1226). */
+int snapgpu_reads_clip(snapgpu_reads_t *reads, int clipping, uint32_t *frontClipped, uint32_t *unclippedLength);
+int snapgpu_sam_format_clipped(const snapgpu_index_t *idx, const snapgpu_reads_t *reads, const char *ids,
+                               const uint64_t *idOffsets, const uint32_t *idLengths, const snapgpu_result_t *results,
+                               const int32_t *editDistance, const uint32_t *nOps, const uint32_t *ops,
+                               const char *readGroup, const uint32_t *frontClipped, const uint32_t *unclippedLength,
+                               char *out, uint64_t cap, uint64_t *used);
+
 /* The SAM header as SAMFormat::writeHeader (SAM.cpp:700-800) writes it for a FASTQ input:
  * @HD (SO:coordinate if sorted), rgLine or "@RG\tID:FASTQ\tSM:sample", @PG with CL:commandLine
  * and VN:version, one @SQ per genome piece.  Same size / error contract as snapgpu_sam_format. */

@@ -16,7 +16,7 @@
 //   alignx <indexDir> <reads.fq> <search.tsv> <maxHitsToGet> [...] -> align columns + multi hits
 //   lv     <calls.tsv>   lines: dir k text pattern quals   -> e netIndel prob_hex
 //   lookup <indexDir> <seeds.txt>  one seed string per line -> nF nRC sumF sumRC firstF firstRC
-//   sam    <indexDir> <reads.fq> [maxHits maxK numSeeds extra]
+//   sam    <indexDir> <reads.fq> [maxHits maxK numSeeds extra [clipping]]
 //          -> per read: AlignRead, then the reference's own SAM writer
 //             (FileFormat::SAM[useM]->writeRead, SAM.cpp:1007-1155) for useM = 0 and 1:
 //             two SAM lines per read
@@ -188,6 +188,7 @@ static int mode_sam(int argc, char **argv) {
     unsigned maxK = argc > 5 ? atoi(argv[5]) : 14;
     unsigned numSeeds = argc > 6 ? atoi(argv[6]) : 25;
     unsigned extra = argc > 7 ? atoi(argv[7]) : 2;
+    const int clipping = argc > 8 ? atoi(argv[8]) : 0;   // ReadClippingType (Read.h:85), as FASTQ.cpp:250 applies it
     initializeLVProbabilitiesToPhredPlus33();
     GenomeIndex *idx = GenomeIndex::loadFromDirectory(argv[2]);
     if (!idx) { fprintf(stderr, "cannot load index %s\n", argv[2]); return 1; }
@@ -205,6 +206,7 @@ static int mode_sam(int argc, char **argv) {
         Read r;
         r.init(id.c_str() + 1, (unsigned)id.size() - 1, b.c_str(), q.c_str(), (unsigned)bases.size());
         r.setReadGroup("FASTQ");      // FASTQ.cpp:252 with AlignerOptions.cpp:65's default
+        r.clip((ReadClippingType)clipping);
         unsigned loc = 0; Direction dir = 0; int score = 0, mapq = 0;
         AlignmentResult res = ba->AlignRead(&r, &loc, &dir, &score, &mapq);
         for (int useM = 0; useM < 2; useM++) {

@@ -68,15 +68,21 @@ struct Job {
     const uint32_t *nOps;
     const uint32_t *ops;
     const char *rg;
+    const uint32_t *front;       // Read::getFrontClippedLength per read, or null (unclipped)
+    const uint32_t *unclipped;   // Read::getUnclippedLength per read, or null
 };
 
 void formatOne(const Job &J, uint64_t i, std::string &o) {
     static const char kOp[] = "MIDNSHP=X";
     const Genome &g = *J.idx->genome;
     const snapgpu_result_t &r = J.res[i];
-    const char *bases = J.reads->bases + J.reads->offsets[i];
-    const char *quals = J.reads->quals + J.reads->offsets[i];
-    const uint32_t len = J.reads->lengths[i];
+    // SEQ / QUAL are the unclipped read (getSAMData, SAM.cpp:866-883); offsets/lengths are the
+    // clipped read the aligner saw (Read::clip, Read.h:357-404)
+    const uint32_t front = J.front ? J.front[i] : 0u;
+    const uint32_t clippedLen = J.reads->lengths[i];
+    const uint32_t len = J.unclipped ? J.unclipped[i] : clippedLen;
+    const char *bases = J.reads->bases + J.reads->offsets[i] - front;
+    const char *quals = J.reads->quals + J.reads->offsets[i] - front;
     // getSAMData: NotFound -> unmapped, unmapped -> forward
     uint32_t loc = r.location;
     if (r.result == SNAPGPU_NOT_FOUND) loc = kInvalidLocation;
@@ -112,11 +118,17 @@ void formatOne(const Job &J, uint64_t i, std::string &o) {
     // CIGAR: computed at writeRead's own location (even for NotFound) -- SAM.cpp:1041-1048
     const int32_t ed = r.location != kInvalidLocation ? J.ed[i] : -1;
     if (r.location != kInvalidLocation && ed >= 0) {
+        // soft clips around the CIGAR (computeCigarString, SAM.cpp:1212-1226); for RC the
+        // clipped-before count is the read's back clip (getSAMData, SAM.cpp:870-872)
+        const uint32_t back = len - clippedLen - front;
+        const uint32_t before = rc ? back : front, after = rc ? front : back;
+        if (before) { appendUint(o, before); o += 'S'; }
         const uint32_t *op = J.ops + i * SNAPGPU_CIGAR_MAX_OPS;
         for (uint32_t k = 0; k < J.nOps[i]; k++) {
             appendUint(o, op[k] >> 4);
             o += kOp[op[k] & 15];
         }
+        if (after) { appendUint(o, after); o += 'S'; }
     } else {
         o += '*';
     }
@@ -147,21 +159,25 @@ void formatOne(const Job &J, uint64_t i, std::string &o) {
 
 }  // namespace
 
-extern "C" int snapgpu_sam_format(const snapgpu_index_t *idx, const snapgpu_reads_t *reads, const char *ids,
-                                  const uint64_t *idOffsets, const uint32_t *idLengths,
-                                  const snapgpu_result_t *results, const int32_t *editDistance, const uint32_t *nOps,
-                                  const uint32_t *ops, const char *readGroup, char *out, uint64_t cap,
-                                  uint64_t *used) {
+extern "C" int snapgpu_sam_format_clipped(const snapgpu_index_t *idx, const snapgpu_reads_t *reads, const char *ids,
+                                          const uint64_t *idOffsets, const uint32_t *idLengths,
+                                          const snapgpu_result_t *results, const int32_t *editDistance,
+                                          const uint32_t *nOps, const uint32_t *ops, const char *readGroup,
+                                          const uint32_t *frontClipped, const uint32_t *unclippedLength, char *out,
+                                          uint64_t cap, uint64_t *used) {
     if (!idx || !reads || !ids || !idOffsets || !idLengths || !results || !editDistance || !nOps || !ops || !used) {
         setError("sam_format: null argument");
         return SNAPGPU_EINVAL;
     }
     for (uint64_t i = 0; i < reads->n; i++)
-        if (nOps[i] > SNAPGPU_CIGAR_MAX_OPS || reads->lengths[i] > 1024) {   // the reference writer: <= 500
-            setError("sam_format: nOps > SNAPGPU_CIGAR_MAX_OPS or read longer than 1024 bases");
+        if (nOps[i] > SNAPGPU_CIGAR_MAX_OPS || (unclippedLength ? unclippedLength[i] : reads->lengths[i]) > 1024 ||
+            (unclippedLength && (!frontClipped || unclippedLength[i] < reads->lengths[i] + frontClipped[i] ||
+                                 reads->offsets[i] < frontClipped[i]))) {   // the reference writer: <= 500
+            setError("sam_format: nOps > SNAPGPU_CIGAR_MAX_OPS, read longer than 1024 bases or bad clip arrays");
             return SNAPGPU_EINVAL;
         }
-    Job J{idx, reads, ids, idOffsets, idLengths, results, editDistance, nOps, ops, readGroup};
+    Job J{idx, reads, ids, idOffsets, idLengths, results, editDistance, nOps, ops, readGroup,
+          unclippedLength ? frontClipped : nullptr, unclippedLength};
     const uint64_t n = reads->n;
     unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     if (n < 4096) nt = 1;
@@ -184,6 +200,41 @@ extern "C" int snapgpu_sam_format(const snapgpu_index_t *idx, const snapgpu_read
     for (auto &p : parts) {
         memcpy(out, p.data(), p.size());
         out += p.size();
+    }
+    return SNAPGPU_OK;
+}
+
+extern "C" int snapgpu_sam_format(const snapgpu_index_t *idx, const snapgpu_reads_t *reads, const char *ids,
+                                  const uint64_t *idOffsets, const uint32_t *idLengths,
+                                  const snapgpu_result_t *results, const int32_t *editDistance, const uint32_t *nOps,
+                                  const uint32_t *ops, const char *readGroup, char *out, uint64_t cap,
+                                  uint64_t *used) {
+    return snapgpu_sam_format_clipped(idx, reads, ids, idOffsets, idLengths, results, editDistance, nOps, ops,
+                                      readGroup, nullptr, nullptr, out, cap, used);
+}
+
+// Read::clip (Read.h:357-404) on every read of a batch, in place: offsets/lengths become the
+// clipped read; frontClipped / unclippedLength receive what the SAM writer needs.
+extern "C" int snapgpu_reads_clip(snapgpu_reads_t *r, int clipping, uint32_t *frontClipped,
+                                  uint32_t *unclippedLength) {
+    if (!r || !frontClipped || !unclippedLength || clipping < 0 || clipping > 3) {
+        setError("reads_clip: bad argument");
+        return SNAPGPU_EINVAL;
+    }
+    for (uint64_t i = 0; i < r->n; i++) {
+        const char *q = r->quals + r->offsets[i];
+        const uint32_t full = r->lengths[i];
+        uint32_t len = full, front = 0;
+        if (clipping == 2 || clipping == 3)   // ClipBack / ClipFrontAndBack
+            while (len > 0 && q[len - 1] == '#') len--;
+        if (clipping == 1 || clipping == 3)   // ClipFront / ClipFrontAndBack
+            while (front < len && q[front] == '#') front++;
+        if (len - front < 50) { len = full; front = 0; }   // "just use all of it" (Read.h:394-397)
+        else len -= front;
+        frontClipped[i] = front;
+        unclippedLength[i] = full;
+        r->offsets[i] += front;
+        r->lengths[i] = len;
     }
     return SNAPGPU_OK;
 }

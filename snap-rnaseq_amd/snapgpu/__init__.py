@@ -237,6 +237,16 @@ class Reads:
         d = np.ctypeslib.as_array(r.truthDirection, shape=(n,)).copy()
         return loc, d
 
+    def clip(self, clipping=3):
+        """Read::clip (Read.h:357-404) on every read, in place (the FASTQ reader's step,
+        FASTQ.cpp:250; 0 none, 1 front, 2 back, 3 front and back = the reference default).
+        -> (frontClipped, unclippedLength) uint32 arrays for sam_format(clip=...)."""
+        n = self.n
+        front = np.zeros(max(1, n), dtype=np.uint32)
+        full = np.zeros(max(1, n), dtype=np.uint32)
+        _check(lib().snapgpu_reads_clip(self._p, int(clipping), front.ctypes.data, full.ctypes.data), "reads_clip")
+        return front[:n], full[:n]
+
     def write_fastq(self, path):
         _check(lib().snapgpu_reads_write_fastq(self._p, str(path).encode()), "write_fastq")
 
@@ -457,9 +467,10 @@ def sam_header(index, command_line, version, sorted_output=False, rg_line=None):
     return C.string_at(buf, used.value)
 
 
-def sam_format(index, reads, ids, results, cigars, read_group="FASTQ"):
+def sam_format(index, reads, ids, results, cigars, read_group="FASTQ", clip=None):
     """SAM lines (SAMFormat::writeRead, SAM.cpp:1007-1155) of single-end genome
-    alignments -> bytes.  ids: list of read ids (str/bytes)."""
+    alignments -> bytes.  ids: list of read ids (str/bytes); clip: the (frontClipped,
+    unclippedLength) pair Reads.clip returned, or None for unclipped reads."""
     n = reads.n
     idb = [i.encode() if isinstance(i, str) else bytes(i) for i in ids]
     assert len(idb) == n
@@ -473,12 +484,19 @@ def sam_format(index, reads, ids, results, cigars, read_group="FASTQ"):
     rg = None if read_group is None else read_group.encode()
     args = [index._h, reads._p, blob, offs.ctypes.data, lens.ctypes.data, res.ctypes.data,
             cigars.editDistance.ctypes.data, cigars.nOps.ctypes.data, cigars.ops.ctypes.data, rg]
+    fn = lib().snapgpu_sam_format
+    if clip is not None:
+        front = np.ascontiguousarray(clip[0], dtype=np.uint32)
+        full = np.ascontiguousarray(clip[1], dtype=np.uint32)
+        assert front.shape == (n,) and full.shape == (n,)
+        args += [front.ctypes.data, full.ctypes.data]
+        fn = lib().snapgpu_sam_format_clipped
     # one formatting pass with a generous buffer; a second only if it was too small
     cap = int(lens.sum()) + 2 * int(reads._p.contents.totalBytes) + n * 512
     buf = C.create_string_buffer(max(1, cap))
-    if lib().snapgpu_sam_format(*args, buf, cap, C.byref(used)) != 0:
+    if fn(*args, buf, cap, C.byref(used)) != 0:
         buf = C.create_string_buffer(max(1, used.value))
-        _check(lib().snapgpu_sam_format(*args, buf, used.value, C.byref(used)), "sam_format")
+        _check(fn(*args, buf, used.value, C.byref(used)), "sam_format")
     return C.string_at(buf, used.value)
 
 

@@ -203,6 +203,10 @@ _PROTOS = [
     ("snapgpu_cigar_resident", C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
     ("snapgpu_cigar_download", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     ("snapgpu_cigar_last_ms", C.c_int, [C.c_void_p, C.POINTER(C.c_double)]),
+    ("snapgpu_reads_clip", C.c_int, [C.POINTER(Reads), C.c_int, C.c_void_p, C.c_void_p]),
+    ("snapgpu_sam_format_clipped", C.c_int, [C.c_void_p, C.POINTER(Reads), C.c_char_p, C.c_void_p, C.c_void_p,
+                                             C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_char_p, C.c_void_p,
+                                             C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]),
     ("snapgpu_sam_header", C.c_int, [C.c_void_p, C.c_int, C.c_char_p, C.c_char_p, C.c_char_p, C.c_void_p,
                                      C.c_uint64, C.POINTER(C.c_uint64)]),
     ("snapgpu_gather_peak", C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_double)]),

@@ -147,6 +147,11 @@ def cigar_fixtures(work):
     sam = run([HARNESS, "sam", idxdir, fq])
     with open(os.path.join(HERE, "expected_small.sam.gz"), "wb") as f:   # mtime 0: reproducible bytes
         f.write(gzip.compress(sam.encode(), compresslevel=9, mtime=0))
+    # the reference FASTQ reader's default clipping (ClipFrontAndBack, AlignerOptions.cpp:48,
+    # FASTQ.cpp:250): the clipped reads are aligned, the SAM line carries S ops + unclipped SEQ
+    sam3 = run([HARNESS, "sam", idxdir, fq, "300", "14", "25", "2", "3"])
+    with open(os.path.join(HERE, "expected_small_clipped.sam.gz"), "wb") as f:
+        f.write(gzip.compress(sam3.encode(), compresslevel=9, mtime=0))
     reads = read_fastq(fq)
     res = [l.split("\t") for l in open(os.path.join(HERE, "expected_small_default.tsv")).read().splitlines()]
     rng = random.Random(31)

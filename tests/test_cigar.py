@@ -211,3 +211,45 @@ def test_sam_header_matches_reference(small, sorted_output):
                              sorted_output=bool(sorted_output)).decode()
     want = open(os.path.join(G, f"expected_small_header{sorted_output}.sam")).read()
     assert got == want
+
+
+def _clipped_reads():
+    reads = snapgpu.Reads.from_fastq(os.path.join(G, "small_reads.fq"))
+    clip = reads.clip(3)   # ClipFrontAndBack, the reference FASTQ reader's default
+    return reads, clip
+
+
+def _clipped_lines(use_m):
+    return gzip.open(os.path.join(G, "expected_small_clipped.sam.gz"), "rt").read().splitlines()[use_m::2]
+
+
+@pytest.mark.parametrize("use_m", [0, 1])
+def test_clipped_sam_matches_reference_cpu(small, use_m):
+    """Read::clip + soft clips: oracle AlignRead and CIGARs of the clipped reads, host SAM
+    lines with the unclipped SEQ/QUAL, against the reference (clipping = ClipFrontAndBack)."""
+    idx, fq, _ = small
+    reads, clip = _clipped_reads()
+    assert sum(1 for i in range(reads.n) if int(clip[1][i]) != len(reads.get(i)[0])) > 20   # clipping exercised
+    res = oracle_align(idx, reads, snapgpu.default_params())
+    loc, dirs = snapgpu.cigar_inputs(res)
+    cig = _cigars_from_pairs(oracle_cigars(idx, [reads.get(i)[0] for i in range(reads.n)], loc, dirs, use_m))
+    got = snapgpu.sam_format(idx, reads, [i for i, _, _ in fq], res, cig, clip=clip).decode().splitlines()
+    want = _clipped_lines(use_m)
+    bad = [(a, b) for a, b in zip(got, want) if a != b]
+    assert len(got) == len(want) and not bad, f"{len(bad)} differ: {bad[:2]}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("use_m", [0, 1])
+def test_gpu_clipped_sam_matches_reference(gpu_available, small, use_m):
+    idx, fq, _ = small
+    reads, clip = _clipped_reads()
+    al = snapgpu.BaseAligner(idx)
+    dev = al.upload(reads)
+    dev.run()
+    dev.run_cigars(useM=use_m)
+    res, cig = dev.results(), dev.cigars()
+    got = snapgpu.sam_format(idx, reads, [i for i, _, _ in fq], res, cig, clip=clip).decode().splitlines()
+    want = _clipped_lines(use_m)
+    bad = [(a, b) for a, b in zip(got, want) if a != b]
+    assert len(got) == len(want) and not bad, f"{len(bad)} differ: {bad[:2]}"
