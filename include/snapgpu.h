@@ -50,7 +50,8 @@ enum { SNAPGPU_FORWARD = 0, SNAPGPU_RC = 1 };
 /* per-read flags in snapgpu_result_t.flags */
 #define SNAPGPU_FLAG_READ_TOO_LONG  0x01u  /* reference: soft_exit(1), BaseAligner.cpp:609-613 */
 #define SNAPGPU_FLAG_MAPQ_FIXED     0x02u  /* MAPQ re-derived on host with libm log10 (boundary case) */
-#define SNAPGPU_FLAG_SPILLED        0x04u  /* candidate set exceeded the LDS arena; re-run in HBM arena */
+#define SNAPGPU_FLAG_DEFERRED       0x04u  /* aligned by the byte-compare pass (read > 128 bases, or IUPAC
+                                              codes in both read and genome): align_kernel<512> */
 #define SNAPGPU_FLAG_TOO_MANY_NS    0x08u  /* countOfNs > maxK (BaseAligner.cpp:652-655) */
 
 /*
@@ -140,12 +141,24 @@ typedef struct snapgpu_index snapgpu_index_t;
  * (as it does between two reference builds), the lookup results do not.
  * Takes ownership of `genome`.  nThreads <= 0 => hardware concurrency. */
 snapgpu_index_t *snapgpu_index_build(snapgpu_genome_t *genome, int seedLen, int nThreads);
+/* As snapgpu_index_build with the table-size slack of `snap-rna index -h` (GenomeIndex.cpp:208,
+ * default 0.3; <= 0 => 0.3): table i gets (nBases * (1 + slack) / nTables) * bias_i slots with the
+ * exact bias of ComputeBiasTable (GenomeIndex.cpp:1109-1243, 294-346), at least 100 -- the
+ * reference's load factor and probe chains. */
+snapgpu_index_t *snapgpu_index_build_ex(snapgpu_genome_t *genome, int seedLen, int nThreads, double slack);
 /* GenomeIndex::loadFromDirectory (GenomeIndex.cpp:844-963), reference on-disk format. */
 snapgpu_index_t *snapgpu_index_load(const char *directory);
 /* Write the reference on-disk format (GenomeIndex.cpp:646-710, Genome.cpp:125-158,
  * HashTable.cpp:180-215) so the reference `snap-rna` can load our index. */
 int  snapgpu_index_save(const snapgpu_index_t *idx, const char *directory);
 void snapgpu_index_free(snapgpu_index_t *idx);
+/* Multi-rank jobs (no reference equivalent: the reference is one process): build the index
+ * once per node, write it as one flat file (e.g. under /dev/shm) with snapgpu_index_share, and
+ * map it read-only in every rank with snapgpu_index_attach (no private copy of the tables). */
+int snapgpu_index_share(const snapgpu_index_t *idx, const char *path);
+snapgpu_index_t *snapgpu_index_attach(const char *path);
+/* The genome an index owns (valid while the index lives). */
+const snapgpu_genome_t *snapgpu_index_genome(const snapgpu_index_t *idx);
 
 typedef struct snapgpu_index_info {
     uint32_t nBases;
@@ -194,6 +207,19 @@ typedef struct snapgpu_reads {
     uint32_t *lengths;
     uint32_t *truthLocation;   /* generator ground truth (genome offset of read start), or NULL */
     uint8_t  *truthDirection;
+    /* Read::clip state (Read.h:357-404), kept by snapgpu_reads_clip: the front clip and the
+     * unclipped length of every read (NULL until the first clip), and the clipping applied. */
+    uint32_t *frontClipped;
+    uint32_t *unclippedLength;
+    int32_t   clipping;        /* ReadClippingType last applied (0 = NoClipping) */
+    uint32_t  nUploads;        /* device uploads of this batch; clipping is refused after the first */
+    /* Read::getId (Read.h:289-328): id i = ids[idOffsets[i] .. +idLengths[i]) (FASTQ header
+     * without '@'), or NULL when the batch carries no ids. */
+    char     *ids;
+    uint64_t *idOffsets;
+    uint32_t *idLengths;
+    uint32_t  hostFlags;       /* library-internal (bit 0: bases/quals in pinned host memory) */
+    uint32_t  reserved_;
 } snapgpu_reads_t;
 
 /* wgsim-like simulator: uniform start, 50/50 strand,
@@ -271,8 +297,9 @@ int  snapgpu_align_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d);
 int  snapgpu_results_download(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, snapgpu_result_t *out);
 int  snapgpu_synchronize(snapgpu_aligner_t *a);
 
-/* Timing of the dominant kernel (HIP events on the aligner's own stream), in ms,
- * for the last snapgpu_align_resident / snapgpu_align_batch call. */
+/* Timing of the dominant kernel (HIP events on the stream it ran on), in ms, for the last
+ * snapgpu_align_resident / snapgpu_align_batch call.  snapgpu_align_batch pipelines its reads
+ * in chunks over two streams: the kernel figures are then sums over its nLaunches chunks. */
 typedef struct snapgpu_timing {
     double mainKernelMs;     /* pass 1: align_kernel<128> (reads <= 128 bases, bit-plane LV) */
     double spillKernelMs;    /* pass 2: align_kernel<512> over the reads pass 1 deferred */
@@ -283,6 +310,10 @@ typedef struct snapgpu_timing {
     uint64_t lookupSeeds;    /* seeds it looked up */
     uint64_t lookupProbes;   /* hash-table entries it probed */
     uint64_t lookupOverflowReads; /* overflow-list counts it read */
+    uint64_t nLaunches;      /* pass sets the figures above sum over (chunks of snapgpu_align_batch) */
+    double wallMs;           /* snapgpu_align_batch: host reads in -> records out, whole call */
+    double mainKernelBusyMs; /* union of the pass-1 launch intervals (launches of the two lanes overlap) */
+    double lookupKernelBusyMs;/* union of the pass-0 launch intervals */
 } snapgpu_timing_t;
 int snapgpu_last_timing(snapgpu_aligner_t *a, snapgpu_timing_t *t);
 
@@ -297,6 +328,10 @@ typedef struct snapgpu_aligner_stats {
 } snapgpu_aligner_stats_t;
 int snapgpu_aligner_get_stats(const snapgpu_aligner_t *a, snapgpu_aligner_stats_t *s);
 int snapgpu_aligner_max_k(const snapgpu_aligner_t *a);           /* getMaxK() */
+/* Whether the pass sets of the aligner's two streams may run concurrently (default 1; the
+ * environment variable SNAPGPU_OVERLAP sets the initial value).  0 serialises the kernels
+ * (copies and host work still overlap them): each launch's duration is then its own. */
+int snapgpu_aligner_set_overlap(snapgpu_aligner_t *a, int overlap);
 /* Diagnostic (no reference equivalent): with SNAPGPU_PHASES=1 in the environment at
  * snapgpu_aligner_create, align_kernel<128> sums shader cycles per phase and event
  * counts into out32[0..31] (order: snapgpu.BaseAligner.PHASES); reset != 0 zeroes them. */
@@ -376,6 +411,15 @@ int snapgpu_sam_header(const snapgpu_index_t *idx, int sorted, const char *comma
  * 12-byte SNAPHashTable slot loads at hashed positions of this aligner's resident table
  * (the access pattern of the seed lookups without their dependency chain), best of 3, ms. */
 int snapgpu_gather_peak(snapgpu_aligner_t *a, uint32_t nLoads, double *ms);
+
+/* HBM streaming-copy ceiling (diagnostic): best-of-3 time (ms) of copy_peak_kernel reading
+ * `bytes` and writing `bytes` with 16-byte vector accesses. */
+int snapgpu_copy_peak(snapgpu_aligner_t *a, uint64_t bytes, double *ms);
+
+/* Self-test of the device-timeout path (diagnostic, needs no GPU): a wait that times out must
+ * fail with SNAPGPU_EDEVICE, mark the aligner failed, and free no device buffer afterwards.
+ * Returns 0 when the path behaves. */
+int snapgpu_selftest_timeout_path(void);
 
 /* MAPQ (mapq.h:32-65) as the host computes it; exported for tests. */
 int snapgpu_compute_mapq(double pAll, double pBest, int score, int popularSeedsSkipped);

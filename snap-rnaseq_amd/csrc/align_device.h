@@ -623,7 +623,8 @@ __device__ __forceinline__ int mapq_dev(const DevTables *tab, double pAll, doubl
 // Device watchdog: loops whose bound rests on data-structure invariants carry an
 // iteration cap; tripping one records (code, read, detail) here, ends the read and
 // makes the host call fail instead of hanging the GPU.
-enum : uint32_t { DIAG_SEED_LOOP = 1, DIAG_SCORE_LOOP = 2, DIAG_CHAIN = 3, DIAG_BATCH_TABLE = 4, DIAG_OVERDUE = 16 };
+enum : uint32_t { DIAG_SEED_LOOP = 1, DIAG_SCORE_LOOP = 2, DIAG_CHAIN = 3, DIAG_BATCH_TABLE = 4, DIAG_ARENA = 5,
+                  DIAG_OVERDUE = 16 };
 // A read that runs longer than this (100 MHz s_memrealtime ticks, 2 s) is abandoned.
 constexpr uint64_t READ_DEADLINE_TICKS = 200000000ull;
 __device__ uint32_t g_diag[4];

@@ -5,6 +5,8 @@
 #include <chrono>
 #include <cmath>
 #include <cstring>
+#include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -246,6 +248,7 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
         uint64_t grp = valid ? S.u.ins.btMask[slot] : 0;
         bool leader = valid && (__builtin_ctzll(grp) == lane);
         wave_sync();
+        bool overflow = false;   // element arena exhausted (cannot happen at (maxSeeds+2)*maxHits; guarded)
         if (leader) {
             S.u.ins.btKey[slot] = NONE;
             S.u.ins.btMask[slot] = 0;
@@ -265,6 +268,11 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
                     if (e == NONE) {
                         // allocateNewCandidate (BaseAligner.cpp:1485-1568): tail of weight list 1
                         e = atomicAdd(&S.nElems, 1u);
+                        if (e >= (uint32_t)A.arenaElems) {
+                            diag_report(DIAG_ARENA, st.rid, e);
+                            overflow = true;
+                            break;
+                        }
                         auto *ne = ar + e;
                         ne->key = key;
                         ne->scored = 0;
@@ -291,13 +299,17 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
                     }
                     ar[e].seedOffset[bit] = (std::remove_reference_t<decltype(ar[e].seedOffset[0])>)offset;
                 }
-                ar[e].used = used;
-                ar[e].weight = (uint8_t)weight;
-                ar[e].allScored = (uint8_t)allScored;
-                sk_set(S, ar, e, sortkey);
-                if (sortkey) atomicMax((unsigned long long *)&S.laneMax[e % WAVE], ((uint64_t)sortkey << 32) | e);
+                if (overflow) e = NONE;
+                if (e != NONE) {
+                    ar[e].used = used;
+                    ar[e].weight = (uint8_t)weight;
+                    ar[e].allScored = (uint8_t)allScored;
+                    sk_set(S, ar, e, sortkey);
+                    if (sortkey) atomicMax((unsigned long long *)&S.laneMax[e % WAVE], ((uint64_t)sortkey << 32) | e);
+                }
             }
         }
+        if (ballot(overflow)) st.abort = 1;   // the watchdog record makes the host call fail
         wave_sync();
     }
     st.ts += lim;
@@ -328,7 +340,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
     st.t0 = __builtin_amdgcn_s_memrealtime();
     st.tick = 32;
     st.nSeedsApplied[0] = st.nSeedsApplied[1] = 0;
-    uint32_t flags = 0;
+    uint32_t flags = MAXLEN > 128 ? SNAPGPU_FLAG_DEFERRED : 0u;   // pass 2 aligns only deferred reads
     int result = SNAPGPU_NOT_FOUND;
     const uint32_t maxSeeds = A.maxSeedsCmd ? A.maxSeedsCmd : (uint32_t)(int)(A.seedCoverage * n / seedLen);
     const uint32_t numWeightLists = maxSeeds + 1;
@@ -770,7 +782,41 @@ int hostMapq(double pAll, double pBest, int score, int popular) {   // mapq.h:32
 
 }  // namespace
 
+// One execution lane = one HIP stream with everything a pass set needs to run beside the
+// other lane: its own element arenas (persistent waves index them by blockIdx), work
+// counters, lookup statistics and timing events.  Lane 0 serves the resident API
+// (snapgpu_reads_upload / snapgpu_align_resident); snapgpu_align_batch alternates chunks
+// over both lanes so one chunk's copies and host tail overlap the other chunk's kernels,
+// and the second lane's kernel fills the first one's tail.
+struct ExecLane {
+    hipStream_t stream = nullptr;
+    void *arena = nullptr;
+    uint32_t *counter = nullptr;               // [0] pass-1 work, [1] pass-2 work, [2] deferred count
+    unsigned long long *lookupStats = nullptr; // seed_lookup_kernel: [256][4] seeds, probes, overflow counts (per call)
+    hipEvent_t done = nullptr;                 // chunk records back in host memory
+    // chunk buffers of the pipelined snapgpu_align_batch (grown on demand)
+    uint64_t capReads = 0, capBytes = 0;
+    char *dBases = nullptr, *dQuals = nullptr;
+    uint64_t *dOffsets = nullptr;
+    uint32_t *dLengths = nullptr, *dDefer = nullptr;
+    snapgpu_result_t *dOut = nullptr;
+    SeedRec *dSeeds = nullptr;
+    uint64_t *hOffsets = nullptr;               // pinned staging
+    uint32_t *hLengths = nullptr;
+    snapgpu_result_t *hOut = nullptr;
+    unsigned long long *hLookupStats = nullptr; // pinned copy of lookupStats
+    bool pending = false;
+    uint64_t chunkBegin = 0, chunkN = 0, chunkEv = 0;
+};
+
+// Timing events of one pass set (one chunk) and the pinned copy of its work counters.
+struct EvSet {
+    hipEvent_t e[4] = {};   // 3: before pass 0, 0: before pass 1, 1: after pass 1, 2: after pass 2
+    uint32_t *hCounter = nullptr;
+};
+
 struct snapgpu_device_reads {
+    snapgpu_aligner_t *owner = nullptr;
     char *dBases = nullptr, *dQuals = nullptr;
     uint64_t *dOffsets = nullptr;
     uint32_t *dLengths = nullptr;
@@ -786,32 +832,44 @@ struct snapgpu_device_reads {
 
 struct snapgpu_aligner {
     int device = 0;
-    hipStream_t stream = nullptr;
     const snapgpu_index_t *idx = nullptr;
     snapgpu_aligner_params_t p{};
-    uint32_t *dSlots = nullptr, *dOverflow = nullptr, *dPieces = nullptr, *dCounter = nullptr;
+    uint32_t *dSlots = nullptr, *dOverflow = nullptr, *dPieces = nullptr;
     uint64_t *dTableBase = nullptr, *dTableSize = nullptr;
     char *dGenomeAlloc = nullptr;
     uint4 *dGPlanes = nullptr;    // genome bit planes (KArgs::gpl)
     const char *dGenome = nullptr;
     DevTables *dTab = nullptr;
-    void *dArena = nullptr;
+    ExecLane lane[2];
+    std::vector<EvSet> evs;       // one per pass set of the current call (grown on demand)
+    uint64_t nEvUsed = 0;
+    // Pass sets of the two lanes run concurrently: the second lane's waves fill the tail of the
+    // first one's persistent kernel (the last, heavy reads of a launch).  SNAPGPU_OVERLAP=0 runs
+    // them one after the other (copies and host tails still overlap).  With overlap, launch
+    // durations overlap too: snapgpu_timing_t also carries the union of the launch intervals.
+    bool overlapKernels = true;
     uint64_t arenaElems = 0;
     int grid = 0, grid512 = 0;
-    hipEvent_t ev[4] = {};
+    uint64_t chunkReads = 262144; // snapgpu_align_batch chunk (SNAPGPU_CHUNK_READS)
     snapgpu_timing_t timing{};
     snapgpu_aligner_stats_t stats{};
     snapgpu_device_reads_t *lastReads = nullptr;
     bool pendingTiming = false;
     uint32_t *dDiag = nullptr;    // g_diag (watchdog record)
     unsigned long long *dPhase = nullptr;   // [grid][PH_SLOTS] (SNAPGPU_PHASES=1 diagnostics)
-    unsigned long long *dLookupStats = nullptr;   // seed_lookup_kernel: seeds, probes, overflow counts
     double timeoutSec = 0;        // SNAPGPU_TIMEOUT_S
+    // A wait that timed out leaves kernels running on buffers this aligner owns: from then on
+    // nothing is freed or reused (hipFree would block on the running kernel, a reuse could
+    // fault it); every call fails and the process is expected to exit.
+    bool failed = false;
+    hipError_t (*eventQuery)(hipEvent_t) = hipEventQuery;   // test hook (snapgpu_selftest_timeout_path)
     hipEvent_t cev[2] = {};       // cigar_kernel timing
     int cigarGrid = 0;
+    hipStream_t stream() const { return lane[0].stream; }
 };
 
 static const size_t kDevGuard = 1024;
+static std::atomic<uint64_t> g_devFrees{0};   // hipFree calls made by devFree (selftest)
 
 // Random-gather ceiling of the hash-table memory (roofline calibration for
 // seed_lookup_kernel): one independent 12-byte slot load per lane at a
@@ -830,6 +888,158 @@ __global__ __launch_bounds__(256) void gather_peak_kernel(const uint32_t *slots,
         }
     if (x == salt) sink[0] = x;   // data-dependent: the loads stay
 }
+
+// Streaming-copy ceiling of this GPU's HBM (roofline peak calibration, BASELINE.md:47-50):
+// 16-byte vector loads and stores, grid-stride, nWords uint4 read and written.
+__global__ __launch_bounds__(256) void copy_peak_kernel(const uint4 *__restrict__ src, uint4 *__restrict__ dst,
+                                                        uint64_t nWords) {
+    // four independent 16-B loads in flight per lane, then four stores (nWords % 1024 == 0)
+    const uint64_t stride = (uint64_t)gridDim.x * 1024u;
+    for (uint64_t i = (uint64_t)blockIdx.x * 1024u + threadIdx.x; i < nWords; i += stride) {
+        uint4 v[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) v[j] = src[i + 256 * j];
+#pragma unroll
+        for (int j = 0; j < 4; j++) dst[i + 256 * j] = v[j];
+    }
+}
+
+// Genome bit planes {hi, lo, notACGT, 0} for 32 bases per uint4 (KArgs::gpl), built on the
+// device from the uploaded genome bytes: word w covers device-genome bytes [32w, 32w + 32)
+// of the guarded copy (position -kDevGuard at byte 0); bytes past `span` are not ACGT.
+__global__ __launch_bounds__(256) void pack_planes_kernel(const char *g, uint64_t span, uint64_t nWords, uint4 *out) {
+    const uint64_t w = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (w >= nWords) return;
+    uint32_t hi = 0, lo = 0, nm = 0;
+    const uint64_t b0 = w * 32;
+#pragma unroll 4
+    for (int i = 0; i < 32; i++) {
+        const uint64_t p = b0 + (uint64_t)i;
+        const uint32_t c = p < span ? (uint8_t)g[p] : 0u;
+        const uint32_t v = sgk::packed_code(c), bit = 1u << i;
+        if (v > 3) nm |= bit;
+        else { if (v & 2) hi |= bit; if (v & 1) lo |= bit; }
+    }
+    out[w] = make_uint4(hi, lo, nm, 0u);
+}
+
+// ------------------------------------------------------------------ host helpers
+namespace {
+
+std::atomic<int> g_hostDevices{-2};   // HIP devices visible to hostAlloc (-2: not probed yet)
+
+// Every device free goes through here: after a timeout the aligner's buffers may still be
+// in use by a running kernel, so they are left alone (see snapgpu_aligner::failed).
+void devFree(const snapgpu_aligner_t *a, void *p) {
+    if (!p || (a && a->failed)) return;
+    g_devFrees++;
+    hipFree(p);
+}
+
+void hostPinnedFree(void *p) { if (p) hipHostFree(p); }
+
+// Wait for an event, honouring SNAPGPU_TIMEOUT_S: on expiry the aligner is marked failed.
+int waitEvent(snapgpu_aligner_t *a, hipEvent_t ev) {
+    if (a->failed) { snapgpu::setError("aligner failed earlier (device timeout): no further work accepted"); return SNAPGPU_EDEVICE; }
+    if (a->timeoutSec > 0) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (;;) {
+            const hipError_t q = a->eventQuery(ev);
+            if (q == hipSuccess) break;
+            if (q != hipErrorNotReady) HIPCHK(q);
+            if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > a->timeoutSec) {
+                a->failed = true;
+                snapgpu::setError("align kernel did not finish within SNAPGPU_TIMEOUT_S; the aligner is unusable "
+                                  "and its device buffers are not released (exit the process)");
+                return SNAPGPU_EDEVICE;
+            }
+            std::this_thread::sleep_for(std::chrono::microseconds(200));
+        }
+    }
+    HIPCHK(hipEventSynchronize(ev));
+    return SNAPGPU_OK;
+}
+
+// Wait for everything queued on a lane's stream (an event recorded now, then waitEvent).
+int waitLane(snapgpu_aligner_t *a, ExecLane &L) {
+    if (a->failed) return waitEvent(a, nullptr);
+    HIPCHK(hipEventRecord(L.done, L.stream));
+    return waitEvent(a, L.done);
+}
+
+// Host -> device copy of a large pageable buffer through two pinned staging buffers: host
+// threads fill one while the DMA engine drains the other (the index tables, up to tens of
+// GB for a human-sized genome; a plain pageable hipMemcpy runs far below PCIe speed).
+int uploadLarge(hipStream_t s, void *dst, const void *src, uint64_t bytes) {
+    if (bytes == 0) return SNAPGPU_OK;
+    if (bytes < (64ull << 20)) {
+        HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+        HIPCHK(hipStreamSynchronize(s));
+        return SNAPGPU_OK;
+    }
+    const uint64_t CH = 256ull << 20;
+    void *stg[2] = {nullptr, nullptr};
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    int rc = SNAPGPU_OK;
+    auto fail = [&](hipError_t e) {
+        snapgpu::setError(std::string("uploadLarge: ") + hipGetErrorString(e));
+        rc = SNAPGPU_EDEVICE;
+    };
+    hipError_t e;
+    for (int i = 0; i < 2 && rc == SNAPGPU_OK; i++) {
+        if ((e = hipHostMalloc(&stg[i], CH, hipHostMallocDefault)) != hipSuccess) fail(e);
+        else if ((e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming)) != hipSuccess) fail(e);
+    }
+    const unsigned nt = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    for (uint64_t off = 0, k = 0; off < bytes && rc == SNAPGPU_OK; off += CH, k++) {
+        const int b = (int)(k & 1);
+        const uint64_t len = std::min(CH, bytes - off);
+        if (k >= 2 && (e = hipEventSynchronize(ev[b])) != hipSuccess) { fail(e); break; }
+        std::vector<std::thread> th;
+        for (unsigned t = 0; t < nt; t++)
+            th.emplace_back([&, t] {
+                const uint64_t a0 = len * t / nt, a1 = len * (t + 1) / nt;
+                memcpy((char *)stg[b] + a0, (const char *)src + off + a0, a1 - a0);
+            });
+        for (auto &x : th) x.join();
+        if ((e = hipMemcpyAsync((char *)dst + off, stg[b], len, hipMemcpyHostToDevice, s)) != hipSuccess) { fail(e); break; }
+        if ((e = hipEventRecord(ev[b], s)) != hipSuccess) { fail(e); break; }
+    }
+    if ((e = hipStreamSynchronize(s)) != hipSuccess && rc == SNAPGPU_OK) fail(e);
+    for (int i = 0; i < 2; i++) {
+        if (stg[i]) hipHostFree(stg[i]);
+        if (ev[i]) hipEventDestroy(ev[i]);
+    }
+    return rc;
+}
+
+}  // namespace
+
+namespace snapgpu {
+void *hostAlloc(size_t bytes, bool *pinned) {
+    *pinned = false;
+    int nd = g_hostDevices.load();
+    if (nd == -2) {
+        if (hipGetDeviceCount(&nd) != hipSuccess) nd = 0;
+        g_hostDevices = nd;
+    }
+    // batches of >= 1 MB that a GPU will copy from live in page-locked memory
+    if (nd > 0 && bytes >= (1u << 20)) {
+        void *p = nullptr;
+        if (hipHostMalloc(&p, bytes, hipHostMallocPortable) == hipSuccess && p) {
+            memset(p, 0, bytes);
+            *pinned = true;
+            return p;
+        }
+    }
+    return calloc(bytes, 1);
+}
+void hostFree(void *p, bool pinned) {
+    if (!p) return;
+    if (pinned) hipHostFree(p);
+    else free(p);
+}
+}  // namespace snapgpu
 
 extern "C" {
 
@@ -859,15 +1069,41 @@ int snapgpu_device_count(void) {
     return n;
 }
 
+static void freeLaneChunkBuffers(snapgpu_aligner_t *a, ExecLane &L) {
+    devFree(a, L.dBases); devFree(a, L.dQuals); devFree(a, L.dOffsets); devFree(a, L.dLengths);
+    devFree(a, L.dDefer); devFree(a, L.dOut); devFree(a, L.dSeeds);
+    L.dBases = L.dQuals = nullptr; L.dOffsets = nullptr; L.dLengths = L.dDefer = nullptr; L.dOut = nullptr;
+    L.dSeeds = nullptr;
+    if (!a->failed) {
+        hostPinnedFree(L.hOffsets); hostPinnedFree(L.hLengths); hostPinnedFree(L.hOut);
+    }
+    L.hOffsets = nullptr; L.hLengths = nullptr; L.hOut = nullptr;
+    L.capReads = L.capBytes = 0;
+}
+
 void snapgpu_aligner_free(snapgpu_aligner_t *a) {
     if (!a) return;
+    if (a->failed) {   // kernels may still run on these buffers: leave them (the process must exit)
+        delete a;
+        return;
+    }
     hipSetDevice(a->device);
-    hipFree(a->dSlots); hipFree(a->dOverflow); hipFree(a->dPieces); hipFree(a->dCounter);
-    hipFree(a->dTableBase); hipFree(a->dTableSize); hipFree(a->dGenomeAlloc); hipFree(a->dTab); hipFree(a->dArena);
-    hipFree(a->dGPlanes); hipFree(a->dPhase); hipFree(a->dLookupStats);
-    for (auto &e : a->ev) if (e) hipEventDestroy(e);
+    for (auto &L : a->lane) if (L.stream) hipStreamSynchronize(L.stream);
+    devFree(a, a->dSlots); devFree(a, a->dOverflow); devFree(a, a->dPieces);
+    devFree(a, a->dTableBase); devFree(a, a->dTableSize); devFree(a, a->dGenomeAlloc); devFree(a, a->dTab);
+    devFree(a, a->dGPlanes); devFree(a, a->dPhase);
+    for (auto &L : a->lane) {
+        freeLaneChunkBuffers(a, L);
+        devFree(a, L.arena); devFree(a, L.counter); devFree(a, L.lookupStats);
+        hostPinnedFree(L.hLookupStats);
+        if (L.done) hipEventDestroy(L.done);
+        if (L.stream) hipStreamDestroy(L.stream);
+    }
+    for (auto &v : a->evs) {
+        for (auto &e : v.e) if (e) hipEventDestroy(e);
+        hostPinnedFree(v.hCounter);
+    }
     for (auto &e : a->cev) if (e) hipEventDestroy(e);
-    if (a->stream) hipStreamDestroy(a->stream);
     delete a;
 }
 
@@ -886,6 +1122,8 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
     a->idx = idx;
     a->p = *params;
     if (const char *t = getenv("SNAPGPU_TIMEOUT_S")) a->timeoutSec = atof(t);
+    if (const char *t = getenv("SNAPGPU_CHUNK_READS"); t && atoll(t) > 0) a->chunkReads = (uint64_t)atoll(t);
+    if (const char *t = getenv("SNAPGPU_OVERLAP")) a->overlapKernels = atoi(t) != 0;
     auto fail = [&](const char *what, hipError_t e) {
         snapgpu::setError(std::string(what) + ": " + hipGetErrorString(e));
         snapgpu_aligner_free(a);
@@ -893,22 +1131,24 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
     };
     hipError_t e;
     if ((e = hipSetDevice(device)) != hipSuccess) return fail("hipSetDevice", e);
-    if ((e = hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking)) != hipSuccess) return fail("stream", e);
-    for (auto &ev : a->ev) if ((e = hipEventCreate(&ev)) != hipSuccess) return fail("event", e);
+    for (auto &L : a->lane) {
+        if ((e = hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking)) != hipSuccess) return fail("stream", e);
+        if ((e = hipEventCreateWithFlags(&L.done, hipEventDisableTiming)) != hipSuccess) return fail("event", e);
+        if ((e = hipMalloc(&L.counter, 64)) != hipSuccess) return fail("counter", e);
+        if ((e = hipMalloc(&L.lookupStats, 1024 * sizeof(unsigned long long))) != hipSuccess) return fail("lookup stats", e);
+        if ((e = hipHostMalloc(&L.hLookupStats, 1024 * sizeof(unsigned long long), hipHostMallocDefault)) != hipSuccess)
+            return fail("pinned lookup stats", e);
+    }
     for (auto &ev : a->cev) if ((e = hipEventCreate(&ev)) != hipSuccess) return fail("event", e);
     if ((e = hipGetSymbolAddress((void **)&a->dDiag, HIP_SYMBOL(g_diag))) != hipSuccess) return fail("g_diag", e);
     if ((e = ensureDeviceTables(device)) != hipSuccess) return fail("device tables", e);
+    hipStream_t s0 = a->stream();
     // index upload: genome with guards, tables, overflow, pieces
     const uint32_t nBases = idx->genome->nBases;
-    size_t gbytes = kDevGuard + nBases + kDevGuard;
+    const size_t gbytes = kDevGuard + nBases + kDevGuard;
     if ((e = hipMalloc(&a->dGenomeAlloc, gbytes)) != hipSuccess) return fail("hipMalloc genome", e);
-    {
-        std::vector<char> pad(kDevGuard, 'n');
-        hipMemcpy(a->dGenomeAlloc, pad.data(), kDevGuard, hipMemcpyHostToDevice);
-        hipMemcpy(a->dGenomeAlloc + kDevGuard, idx->genome->bases(), nBases, hipMemcpyHostToDevice);
-        if ((e = hipMemcpy(a->dGenomeAlloc + kDevGuard + nBases, pad.data(), kDevGuard, hipMemcpyHostToDevice)) != hipSuccess)
-            return fail("genome upload", e);
-    }
+    if ((e = hipMemsetAsync(a->dGenomeAlloc, 'n', gbytes, s0)) != hipSuccess) return fail("genome guard", e);
+    if (uploadLarge(s0, a->dGenomeAlloc + kDevGuard, idx->genome->bases(), nBases)) { snapgpu_aligner_free(a); return nullptr; }
     a->dGenome = a->dGenomeAlloc + kDevGuard;
     {
         // genome bit planes {hi, lo, notACGT, 0}, 32 bases per uint4, covering genome
@@ -916,25 +1156,15 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
         // align_kernel<128> are built from these with funnel shifts (align_score.h).
         const uint64_t span = (uint64_t)nBases + 2 * kDevGuard;
         const uint64_t nw = (span + 31) / 32 + 8;
-        std::vector<uint32_t> pl(nw * 4, 0);
-        const char *b = idx->genome->bases();
-        for (uint64_t i = 0; i < span; i++) {
-            const int64_t p = (int64_t)i - (int64_t)kDevGuard;
-            const char c = (p >= 0 && p < (int64_t)nBases) ? b[p] : 'n';
-            const uint32_t v = packedCode(c), bit = 1u << (i & 31);
-            uint32_t *w = &pl[(i >> 5) * 4];
-            if (v > 3) w[2] |= bit;
-            else { if (v & 2) w[0] |= bit; if (v & 1) w[1] |= bit; }
-        }
-        for (uint64_t i = span; i < nw * 32; i++) pl[(i >> 5) * 4 + 2] |= 1u << (i & 31);
         if ((e = hipMalloc(&a->dGPlanes, nw * 16)) != hipSuccess) return fail("hipMalloc planes", e);
-        if ((e = hipMemcpy(a->dGPlanes, pl.data(), nw * 16, hipMemcpyHostToDevice)) != hipSuccess) return fail("planes", e);
+        hipLaunchKernelGGL(pack_planes_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s0, a->dGenomeAlloc,
+                           span, nw, a->dGPlanes);
+        if ((e = hipGetLastError()) != hipSuccess) return fail("pack_planes_kernel", e);
     }
     if ((e = hipMalloc(&a->dSlots, idx->slots.size() * 4)) != hipSuccess) return fail("hipMalloc slots", e);
-    if ((e = hipMemcpy(a->dSlots, idx->slots.data(), idx->slots.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return fail("slots", e);
+    if (uploadLarge(s0, a->dSlots, idx->slots.data(), idx->slots.size() * 4)) { snapgpu_aligner_free(a); return nullptr; }
     if ((e = hipMalloc(&a->dOverflow, idx->overflow.size() * 4 + 16)) != hipSuccess) return fail("hipMalloc ovf", e);
-    if (!idx->overflow.empty() &&
-        (e = hipMemcpy(a->dOverflow, idx->overflow.data(), idx->overflow.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return fail("ovf", e);
+    if (uploadLarge(s0, a->dOverflow, idx->overflow.data(), idx->overflow.size() * 4)) { snapgpu_aligner_free(a); return nullptr; }
     if ((e = hipMalloc(&a->dTableBase, idx->nTables * 8)) != hipSuccess) return fail("tb", e);
     if ((e = hipMalloc(&a->dTableSize, idx->nTables * 8)) != hipSuccess) return fail("ts", e);
     for (uint32_t t = 0; t < idx->nTables; t++)   // the kernels hash with 32-bit modulo
@@ -943,18 +1173,17 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
             snapgpu_aligner_free(a);
             return nullptr;
         }
-    hipMemcpy(a->dTableBase, idx->tableBase.data(), idx->nTables * 8, hipMemcpyHostToDevice);
-    hipMemcpy(a->dTableSize, idx->tableSize.data(), idx->nTables * 8, hipMemcpyHostToDevice);
+    if ((e = hipMemcpy(a->dTableBase, idx->tableBase.data(), idx->nTables * 8, hipMemcpyHostToDevice)) != hipSuccess) return fail("tb", e);
+    if ((e = hipMemcpy(a->dTableSize, idx->tableSize.data(), idx->nTables * 8, hipMemcpyHostToDevice)) != hipSuccess) return fail("ts", e);
     size_t np = idx->genome->pieceOffsets.size();
     if ((e = hipMalloc(&a->dPieces, np * 4 + 16)) != hipSuccess) return fail("pieces", e);
-    if (np) hipMemcpy(a->dPieces, idx->genome->pieceOffsets.data(), np * 4, hipMemcpyHostToDevice);
+    if (np && (e = hipMemcpy(a->dPieces, idx->genome->pieceOffsets.data(), np * 4, hipMemcpyHostToDevice)) != hipSuccess)
+        return fail("pieces", e);
     DevTables t;
     fillTables(t, idx->seedLen);
     if ((e = hipMalloc(&a->dTab, sizeof(DevTables))) != hipSuccess) return fail("tables", e);
-    hipMemcpy(a->dTab, &t, sizeof(t), hipMemcpyHostToDevice);
-    if ((e = hipMalloc(&a->dCounter, 64)) != hipSuccess) return fail("counter", e);
-    if ((e = hipMalloc(&a->dLookupStats, 1024 * sizeof(unsigned long long))) != hipSuccess) return fail("lookup stats", e);
-    // persistent grid: waves resident on the device; element arena per wave
+    if ((e = hipMemcpy(a->dTab, &t, sizeof(t), hipMemcpyHostToDevice)) != hipSuccess) return fail("tables", e);
+    // persistent grid: waves resident on the device; element arena per wave and lane
     hipDeviceProp_t prop;
     hipGetDeviceProperties(&prop, device);
     int perCU = 0;
@@ -964,9 +1193,10 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
     uint32_t maxSeeds = params->maxSeedsToUse ? params->maxSeedsToUse
                                               : (uint32_t)(params->maxSeedCoverage * params->maxReadSize / idx->seedLen);
     a->arenaElems = (uint64_t)(maxSeeds + 2) * params->maxHitsToConsider + 64;
-    const uint64_t budget = 24ull << 30;   // HBM for arenas
+    const uint64_t budget = 24ull << 30;   // HBM for the arenas of one lane
     while (a->grid > 64 && (uint64_t)a->grid * a->arenaElems * sizeof(Elem512) > budget) a->grid /= 2;
-    if ((e = hipMalloc(&a->dArena, (uint64_t)a->grid * a->arenaElems * sizeof(Elem512))) != hipSuccess) return fail("arena", e);
+    for (auto &L : a->lane)
+        if ((e = hipMalloc(&L.arena, (uint64_t)a->grid * a->arenaElems * sizeof(Elem512))) != hipSuccess) return fail("arena", e);
     int perCU512 = 0;   // pass 2 (deferred reads) reuses the arenas of the first a->grid blocks
     hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU512, (const void *)align_kernel<512, false>, 64, 0);
     if (perCU512 <= 0) perCU512 = 4;
@@ -983,10 +1213,13 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
 
 snapgpu_device_reads_t *snapgpu_reads_upload(snapgpu_aligner_t *a, const snapgpu_reads_t *r) {
     if (!a || !r) { snapgpu::setError("reads_upload: null"); return nullptr; }
+    if (a->failed) { snapgpu::setError("aligner failed earlier (device timeout)"); return nullptr; }
     HIPCHKN(hipSetDevice(a->device));
     auto *d = new snapgpu_device_reads_t();
+    d->owner = a;
     d->n = r->n;
     d->device = a->device;
+    const_cast<snapgpu_reads_t *>(r)->nUploads++;   // clipping is refused from now on
     uint64_t bytes = 0;
     for (uint64_t i = 0; i < r->n; i++) {
         uint64_t endb = r->offsets[i] + r->lengths[i];
@@ -994,6 +1227,7 @@ snapgpu_device_reads_t *snapgpu_reads_upload(snapgpu_aligner_t *a, const snapgpu
         if (r->lengths[i] > d->maxLen) d->maxLen = r->lengths[i];
     }
     bytes += 64;
+    hipStream_t s = a->stream();
     HIPCHKN(hipMalloc(&d->dBases, bytes));
     HIPCHKN(hipMalloc(&d->dQuals, bytes));
     HIPCHKN(hipMalloc(&d->dOffsets, (r->n + 1) * 8));
@@ -1001,22 +1235,23 @@ snapgpu_device_reads_t *snapgpu_reads_upload(snapgpu_aligner_t *a, const snapgpu
     HIPCHKN(hipMalloc(&d->dOut, (r->n + 1) * sizeof(snapgpu_result_t)));
     HIPCHKN(hipMalloc(&d->dDefer, (r->n + 1) * sizeof(uint32_t)));
     HIPCHKN(hipMalloc(&d->dSeeds, (r->n + 8) * SEEDS_PER_READ * sizeof(SeedRec)));
-    HIPCHKN(hipMemsetAsync(d->dBases, 0, bytes, a->stream));
-    HIPCHKN(hipMemsetAsync(d->dQuals, 0, bytes, a->stream));
-    HIPCHKN(hipMemcpyAsync(d->dBases, r->bases, bytes - 64, hipMemcpyHostToDevice, a->stream));
-    HIPCHKN(hipMemcpyAsync(d->dQuals, r->quals, bytes - 64, hipMemcpyHostToDevice, a->stream));
-    HIPCHKN(hipMemcpyAsync(d->dOffsets, r->offsets, r->n * 8, hipMemcpyHostToDevice, a->stream));
-    HIPCHKN(hipMemcpyAsync(d->dLengths, r->lengths, r->n * 4, hipMemcpyHostToDevice, a->stream));
-    HIPCHKN(hipStreamSynchronize(a->stream));
+    HIPCHKN(hipMemsetAsync(d->dBases, 0, bytes, s));
+    HIPCHKN(hipMemsetAsync(d->dQuals, 0, bytes, s));
+    HIPCHKN(hipMemcpyAsync(d->dBases, r->bases, bytes - 64, hipMemcpyHostToDevice, s));
+    HIPCHKN(hipMemcpyAsync(d->dQuals, r->quals, bytes - 64, hipMemcpyHostToDevice, s));
+    HIPCHKN(hipMemcpyAsync(d->dOffsets, r->offsets, r->n * 8, hipMemcpyHostToDevice, s));
+    HIPCHKN(hipMemcpyAsync(d->dLengths, r->lengths, r->n * 4, hipMemcpyHostToDevice, s));
+    HIPCHKN(hipStreamSynchronize(s));
     return d;
 }
 
 void snapgpu_device_reads_free(snapgpu_device_reads_t *d) {
     if (!d) return;
-    hipSetDevice(d->device);
-    hipFree(d->dBases); hipFree(d->dQuals); hipFree(d->dOffsets); hipFree(d->dLengths); hipFree(d->dOut);
-    hipFree(d->dDefer); hipFree(d->dSeeds);
-    hipFree(d->dCigEd); hipFree(d->dCigN); hipFree(d->dCigOps);
+    const snapgpu_aligner_t *a = d->owner;
+    if (!(a && a->failed)) hipSetDevice(d->device);
+    devFree(a, d->dBases); devFree(a, d->dQuals); devFree(a, d->dOffsets); devFree(a, d->dLengths);
+    devFree(a, d->dOut); devFree(a, d->dDefer); devFree(a, d->dSeeds);
+    devFree(a, d->dCigEd); devFree(a, d->dCigN); devFree(a, d->dCigOps);
     delete d;
 }
 
@@ -1029,15 +1264,24 @@ struct AlignExt {
     snapgpu_multi_hit_t *multiHits = nullptr;
 };
 
-static int launch_passes(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, const AlignExt &x);
+// The device buffers one pass set reads and writes.
+struct PassIO {
+    const char *bases, *quals;
+    const uint64_t *offsets;
+    const uint32_t *lengths;
+    uint64_t n;
+    snapgpu_result_t *out;
+    uint32_t *defer;
+    SeedRec *seeds;
+};
 
-int snapgpu_align_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d) { return launch_passes(a, d, AlignExt()); }
-
-static int launch_passes(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, const AlignExt &x) {
-    if (!a || !d) return SNAPGPU_EINVAL;
-    HIPCHK(hipSetDevice(a->device));
-    if (d->n == 0) return SNAPGPU_OK;
-    if (d->n > 0xffffffffull) { snapgpu::setError("batch too large"); return SNAPGPU_EINVAL; }
+// Queue pass 0 (seed lookups), pass 1 (align_kernel<128>) and pass 2 (align_kernel<512> over
+// the deferred reads) on lane `li`, with HIP events around each.
+static int launch_passes(snapgpu_aligner_t *a, int li, const PassIO &io, const AlignExt &x, EvSet &ev,
+                         const EvSet *prev) {
+    ExecLane &L = a->lane[li];
+    if (io.n == 0) return SNAPGPU_OK;
+    if (io.n > 0xffffffffull) { snapgpu::setError("batch too large"); return SNAPGPU_EINVAL; }
     KArgs A;
     memset(&A, 0, sizeof(A));
     const snapgpu_index_t *idx = a->idx;
@@ -1051,108 +1295,189 @@ static int launch_passes(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, const 
     A.maxSeedsCmd = a->p.maxSeedsToUse; A.seedCoverage = a->p.maxSeedCoverage; A.extra = a->p.extraSearchDepth;
     A.explore = a->p.explorePopularSeeds; A.stopOnFirst = a->p.stopOnFirstHit; A.kRows = 31;
     A.tab = a->dTab;
-    A.bases = d->dBases; A.quals = d->dQuals; A.offsets = d->dOffsets; A.lengths = d->dLengths;
-    A.nReads = (uint32_t)d->n; A.out = d->dOut;
-    A.counter = a->dCounter; A.arena = a->dArena; A.arenaElems = a->arenaElems;
-    // dCounter: [0] pass-1 work counter, [1] pass-2 work counter, [2] deferred-read count
-    A.deferList = d->dDefer; A.deferCount = a->dCounter + 2; A.readList = nullptr;
+    A.bases = io.bases; A.quals = io.quals; A.offsets = io.offsets; A.lengths = io.lengths;
+    A.nReads = (uint32_t)io.n; A.out = io.out;
+    A.counter = L.counter; A.arena = L.arena; A.arenaElems = a->arenaElems;
+    A.deferList = io.defer; A.deferCount = L.counter + 2; A.readList = nullptr;
     A.search = x.search; A.maxHitsToGet = x.maxHitsToGet; A.hitStride = MAX_K * (1 + 2 * x.maxHitsToGet);
     A.hitScratch = x.hitScratch; A.multiFound = x.multiFound; A.multiHits = x.multiHits;
     int grid = a->grid;
-    if ((uint64_t)grid > d->n) grid = (int)d->n;
+    if ((uint64_t)grid > io.n) grid = (int)io.n;
     (void)hipGetLastError();   // clear any stale error of an unrelated earlier runtime call
-    HIPCHK(hipMemsetAsync(a->dCounter, 0, 64, a->stream));
-    HIPCHK(hipMemsetAsync(a->dDiag, 0, sizeof(uint32_t) * 4, a->stream));
+    if (prev && !a->overlapKernels) HIPCHK(hipStreamWaitEvent(L.stream, prev->e[2], 0));
+    HIPCHK(hipMemsetAsync(L.counter, 0, 64, L.stream));
     // pass 0: first-round seed lookups of every read (8 reads per 64-lane block)
     A.seedRecs = nullptr;
-    HIPCHK(hipEventRecord(a->ev[3], a->stream));
-    HIPCHK(hipMemsetAsync(a->dLookupStats, 0, 1024 * sizeof(unsigned long long), a->stream));
-    hipLaunchKernelGGL(seed_lookup_kernel, dim3((unsigned)((d->n + 7) / 8)), dim3(64), 0, a->stream, A, d->dSeeds,
-                       a->dLookupStats);
+    HIPCHK(hipEventRecord(ev.e[3], L.stream));
+    hipLaunchKernelGGL(seed_lookup_kernel, dim3((unsigned)((io.n + 7) / 8)), dim3(64), 0, L.stream, A, io.seeds,
+                       L.lookupStats);
     HIPCHK(hipGetLastError());
-    A.seedRecs = reinterpret_cast<const uint4 *>(d->dSeeds);
-    HIPCHK(hipEventRecord(a->ev[0], a->stream));
+    A.seedRecs = reinterpret_cast<const uint4 *>(io.seeds);
+    HIPCHK(hipEventRecord(ev.e[0], L.stream));
     const bool ext = x.search || x.maxHitsToGet;
-    if (ext) hipLaunchKernelGGL((align_kernel<128, true>), dim3(grid), dim3(64), 0, a->stream, A);
-    else hipLaunchKernelGGL((align_kernel<128, false>), dim3(grid), dim3(64), 0, a->stream, A);
+    if (ext) hipLaunchKernelGGL((align_kernel<128, true>), dim3(grid), dim3(64), 0, L.stream, A);
+    else hipLaunchKernelGGL((align_kernel<128, false>), dim3(grid), dim3(64), 0, L.stream, A);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(a->ev[1], a->stream));
+    HIPCHK(hipEventRecord(ev.e[1], L.stream));
     // pass 2: reads longer than 128 bases or needing the byte-compare LV
     KArgs B = A;
-    B.counter = a->dCounter + 1;
-    B.readList = d->dDefer;
+    B.counter = L.counter + 1;
+    B.readList = io.defer;
     B.seedRecs = nullptr;
     int grid2 = a->grid512;
-    if ((uint64_t)grid2 > d->n) grid2 = (int)d->n;
-    if (ext) hipLaunchKernelGGL((align_kernel<512, true>), dim3(grid2), dim3(64), 0, a->stream, B);
-    else hipLaunchKernelGGL((align_kernel<512, false>), dim3(grid2), dim3(64), 0, a->stream, B);
+    if ((uint64_t)grid2 > io.n) grid2 = (int)io.n;
+    if (ext) hipLaunchKernelGGL((align_kernel<512, true>), dim3(grid2), dim3(64), 0, L.stream, B);
+    else hipLaunchKernelGGL((align_kernel<512, false>), dim3(grid2), dim3(64), 0, L.stream, B);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(a->ev[2], a->stream));
+    HIPCHK(hipEventRecord(ev.e[2], L.stream));
+    HIPCHK(hipMemcpyAsync(ev.hCounter, L.counter, 16, hipMemcpyDeviceToHost, L.stream));
+    return SNAPGPU_OK;
+}
+
+// The event set of the next pass set of the current call (created on first use).
+static EvSet *nextEvSet(snapgpu_aligner_t *a) {
+    if (a->nEvUsed == a->evs.size()) {
+        EvSet v;
+        for (auto &e : v.e)
+            if (hipEventCreate(&e) != hipSuccess) { snapgpu::setError("hipEventCreate"); return nullptr; }
+        if (hipHostMalloc(&v.hCounter, 64, hipHostMallocDefault) != hipSuccess) { snapgpu::setError("pinned counter"); return nullptr; }
+        a->evs.push_back(v);
+    }
+    return &a->evs[a->nEvUsed++];
+}
+
+// Start of a call: lookup statistics accumulate over all its pass sets.
+static int beginCall(snapgpu_aligner_t *a) {
+    a->nEvUsed = 0;
+    a->timing = snapgpu_timing_t{};
+    for (auto &L : a->lane) HIPCHK(hipMemsetAsync(L.lookupStats, 0, 1024 * sizeof(unsigned long long), L.stream));
+    HIPCHK(hipMemsetAsync(a->dDiag, 0, sizeof(uint32_t) * 4, a->lane[0].stream));
+    // the other lane's first kernels must not start before the watchdog record is cleared
+    HIPCHK(hipStreamSynchronize(a->lane[0].stream));
+    return SNAPGPU_OK;
+}
+
+// Union of the [e[from], e[to]] intervals of the call's pass sets (they overlap across lanes), ms.
+static double busyUnion(snapgpu_aligner_t *a, int from, int to) {
+    std::vector<std::pair<float, float>> iv;
+    const hipEvent_t ref = a->evs[0].e[3];
+    for (uint64_t i = 0; i < a->nEvUsed; i++) {
+        float b = 0, e = 0;
+        if (hipEventElapsedTime(&b, ref, a->evs[i].e[from]) != hipSuccess ||
+            hipEventElapsedTime(&e, ref, a->evs[i].e[to]) != hipSuccess) return -1;
+        iv.emplace_back(b, e);
+    }
+    std::sort(iv.begin(), iv.end());
+    double total = 0, cs = -1e30, ce = -1e30;
+    for (auto &x : iv) {
+        if (x.first > ce) { if (ce > cs) total += ce - cs; cs = x.first; ce = x.second; }
+        else if (x.second > ce) ce = x.second;
+    }
+    if (ce > cs) total += ce - cs;
+    return total;
+}
+
+static void accountBusy(snapgpu_aligner_t *a) {
+    if (a->nEvUsed == 0) return;
+    a->timing.mainKernelBusyMs = busyUnion(a, 0, 1);
+    a->timing.lookupKernelBusyMs = busyUnion(a, 3, 0);
+}
+
+// Kernel times and counters of one finished pass set into a->timing.
+static int accountEvSet(snapgpu_aligner_t *a, const EvSet &v) {
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, v.e[0], v.e[1]));
+    a->timing.mainKernelMs += ms;
+    HIPCHK(hipEventElapsedTime(&ms, v.e[1], v.e[2]));
+    a->timing.spillKernelMs += ms;
+    HIPCHK(hipEventElapsedTime(&ms, v.e[3], v.e[0]));
+    a->timing.lookupKernelMs += ms;
+    a->timing.nLaunches++;
+    a->timing.nSpilled += v.hCounter[2];
+    return SNAPGPU_OK;
+}
+
+// Device-resident reads: the same chunk-sized pass sets as snapgpu_align_batch, alternating
+// over the two lanes, on sub-ranges of the resident buffers (no copies).  The extended path
+// (windowed search / multi-hit scratch per block) runs as one pass set on lane 0.
+static int launch_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, const AlignExt &x) {
+    if (!a || !d) return SNAPGPU_EINVAL;
+    if (a->failed) { snapgpu::setError("aligner failed earlier (device timeout)"); return SNAPGPU_EDEVICE; }
+    HIPCHK(hipSetDevice(a->device));
+    int rc = beginCall(a);
+    if (rc) return rc;
+    const bool ext = x.search || x.maxHitsToGet;
+    const uint64_t n = d->n;
+    const uint64_t nChunks = ext || n == 0 ? 1 : (n + a->chunkReads - 1) / a->chunkReads;
+    const uint64_t per = (n + nChunks - 1) / nChunks;
+    for (uint64_t c = 0; c < nChunks; c++) {
+        const uint64_t b = c * per, m = std::min(n, b + per) - b;
+        EvSet *ev = nextEvSet(a);
+        if (!ev) return SNAPGPU_EDEVICE;
+        PassIO io{d->dBases, d->dQuals, d->dOffsets + b, d->dLengths + b, m, d->dOut + b, d->dDefer + b,
+                  d->dSeeds + b * SEEDS_PER_READ};
+        if ((rc = launch_passes(a, (int)(c & 1), io, x, *ev, c ? &a->evs[a->nEvUsed - 2] : nullptr))) return rc;
+    }
     a->lastReads = d;
-    a->pendingTiming = true;
+    a->pendingTiming = n > 0;
+    return SNAPGPU_OK;
+}
+
+int snapgpu_align_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d) { return launch_resident(a, d, AlignExt()); }
+
+// sum of the per-slot lookup statistics of a lane (host copy)
+static void addLookupStats(snapgpu_timing_t &t, const unsigned long long *ls) {
+    for (int i = 0; i < 256; i++) {
+        t.lookupSeeds += ls[4 * i];
+        t.lookupProbes += ls[4 * i + 1];
+        t.lookupOverflowReads += ls[4 * i + 2];
+    }
+}
+
+static int checkWatchdog(snapgpu_aligner_t *a) {
+    uint32_t diag[4];
+    HIPCHK(hipMemcpy(diag, a->dDiag, sizeof(diag), hipMemcpyDeviceToHost));
+    if (diag[0]) {
+        char msg[160];
+        snprintf(msg, sizeof msg, "device watchdog tripped: code %u read %u detail %u", diag[0], diag[1], diag[2]);
+        snapgpu::setError(msg);
+        return SNAPGPU_EDEVICE;
+    }
     return SNAPGPU_OK;
 }
 
 int snapgpu_synchronize(snapgpu_aligner_t *a) {
     if (!a) return SNAPGPU_EINVAL;
+    if (a->failed) { snapgpu::setError("aligner failed earlier (device timeout)"); return SNAPGPU_EDEVICE; }
     HIPCHK(hipSetDevice(a->device));
-    if (a->timeoutSec > 0) {   // SNAPGPU_TIMEOUT_S: fail the call instead of waiting forever
-        const auto t0 = std::chrono::steady_clock::now();
-        for (;;) {
-            hipError_t q = hipStreamQuery(a->stream);
-            if (q == hipSuccess) break;
-            if (q != hipErrorNotReady) HIPCHK(q);
-            if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > a->timeoutSec) {
-                snapgpu::setError("align kernel did not finish within SNAPGPU_TIMEOUT_S");
-                return SNAPGPU_EDEVICE;
-            }
-            std::this_thread::sleep_for(std::chrono::microseconds(200));
-        }
+    for (auto &L : a->lane) {
+        const int rc = waitLane(a, L);
+        if (rc) return rc;
     }
-    HIPCHK(hipStreamSynchronize(a->stream));
     if (a->pendingTiming) {
-        float ms = 0;
-        HIPCHK(hipEventElapsedTime(&ms, a->ev[0], a->ev[1]));
-        a->timing.mainKernelMs = ms;
-        HIPCHK(hipEventElapsedTime(&ms, a->ev[1], a->ev[2]));
-        a->timing.spillKernelMs = ms;
-        HIPCHK(hipEventElapsedTime(&ms, a->ev[3], a->ev[0]));
-        a->timing.lookupKernelMs = ms;
-        uint32_t cnt[4];
-        HIPCHK(hipMemcpy(cnt, a->dCounter, sizeof(cnt), hipMemcpyDeviceToHost));
-        a->timing.nSpilled = cnt[2];
+        a->timing = snapgpu_timing_t{};
+        for (uint64_t i = 0; i < a->nEvUsed; i++) {
+            const int rc = accountEvSet(a, a->evs[i]);
+            if (rc) return rc;
+        }
+        accountBusy(a);
         std::vector<unsigned long long> ls(1024);
-        HIPCHK(hipMemcpy(ls.data(), a->dLookupStats, 1024 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-        a->timing.lookupSeeds = a->timing.lookupProbes = a->timing.lookupOverflowReads = 0;
-        for (int i = 0; i < 256; i++) {
-            a->timing.lookupSeeds += ls[4 * i];
-            a->timing.lookupProbes += ls[4 * i + 1];
-            a->timing.lookupOverflowReads += ls[4 * i + 2];
+        for (auto &L : a->lane) {
+            HIPCHK(hipMemcpy(ls.data(), L.lookupStats, 1024 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+            addLookupStats(a->timing, ls.data());
         }
         a->pendingTiming = false;
-        uint32_t diag[4];
-        HIPCHK(hipMemcpy(diag, a->dDiag, sizeof(diag), hipMemcpyDeviceToHost));
-        if (diag[0]) {
-            char msg[160];
-            snprintf(msg, sizeof msg, "device watchdog tripped: code %u read %u detail %u", diag[0], diag[1], diag[2]);
-            snapgpu::setError(msg);
-            return SNAPGPU_EDEVICE;
-        }
+        const int rc = checkWatchdog(a);
+        if (rc) return rc;
     }
     return SNAPGPU_OK;
 }
 
-int snapgpu_results_download(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, snapgpu_result_t *out) {
-    if (!a || !d || !out) return SNAPGPU_EINVAL;
-    HIPCHK(hipSetDevice(a->device));
-    int rc = snapgpu_synchronize(a);   // before the copy: a pageable-destination copy blocks
-    if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(out, d->dOut, d->n * sizeof(snapgpu_result_t), hipMemcpyDeviceToHost, a->stream));
-    HIPCHK(hipStreamSynchronize(a->stream));
-    // host MAPQ fix-ups (ratio within 1e-9 of a threshold 10^(-q/10), mapq_dev)
-    auto t0 = std::chrono::steady_clock::now();
+// Records -> caller: MAPQ fix-ups (ratio within 1e-9 of a threshold 10^(-q/10), mapq_dev,
+// re-derived with glibc log10) and the aligner statistics, over out[0, n).
+static void finishRecords(snapgpu_aligner_t *a, snapgpu_result_t *out, uint64_t n) {
     uint64_t fixed = 0;
-    for (uint64_t i = 0; i < d->n; i++) {
+    for (uint64_t i = 0; i < n; i++) {
         snapgpu_result_t &o = out[i];
         if (o.flags & SNAPGPU_FLAG_MAPQ_FIXED) {
             o.mapq = hostMapq(o.probabilityOfAllCandidates, o.probabilityOfBestCandidate, o.score, o.popularSeedsSkipped);
@@ -1165,19 +1490,169 @@ int snapgpu_results_download(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, sn
         a->stats.nReadsIgnoredBecauseOfTooManyNs += (o.flags & SNAPGPU_FLAG_TOO_MANY_NS) ? 1 : 0;
         a->stats.nReads++;
     }
-    a->timing.nMapqFixed = fixed;
+    a->timing.nMapqFixed += fixed;
+}
+
+int snapgpu_results_download(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, snapgpu_result_t *out) {
+    if (!a || !d || !out) return SNAPGPU_EINVAL;
+    HIPCHK(hipSetDevice(a->device));
+    int rc = snapgpu_synchronize(a);   // before the copy: a pageable-destination copy blocks
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(out, d->dOut, d->n * sizeof(snapgpu_result_t), hipMemcpyDeviceToHost, a->stream()));
+    HIPCHK(hipStreamSynchronize(a->stream()));
+    auto t0 = std::chrono::steady_clock::now();
+    a->timing.nMapqFixed = 0;
+    finishRecords(a, out, d->n);
     a->timing.fixupMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return SNAPGPU_OK;
 }
 
+// (Re)allocate a lane's chunk buffers for `reads` reads spanning `bytes` read bytes.
+static int ensureLaneCapacity(snapgpu_aligner_t *a, ExecLane &L, uint64_t reads, uint64_t bytes) {
+    if (reads <= L.capReads && bytes <= L.capBytes) return SNAPGPU_OK;
+    int rc = waitLane(a, L);
+    if (rc) return rc;
+    freeLaneChunkBuffers(a, L);
+    reads = std::max<uint64_t>(reads, 1024);
+    const uint64_t cb = bytes + 512;   // zero slack past the last read: over-reading loads stay inside
+    HIPCHK(hipMalloc(&L.dBases, cb));
+    HIPCHK(hipMalloc(&L.dQuals, cb));
+    HIPCHK(hipMemset(L.dBases, 0, cb));
+    HIPCHK(hipMemset(L.dQuals, 0, cb));
+    HIPCHK(hipMalloc(&L.dOffsets, (reads + 1) * 8));
+    HIPCHK(hipMalloc(&L.dLengths, (reads + 1) * 4));
+    HIPCHK(hipMalloc(&L.dDefer, (reads + 1) * 4));
+    HIPCHK(hipMalloc(&L.dOut, (reads + 1) * sizeof(snapgpu_result_t)));
+    HIPCHK(hipMalloc(&L.dSeeds, (reads + 8) * SEEDS_PER_READ * sizeof(SeedRec)));
+    HIPCHK(hipHostMalloc(&L.hOffsets, (reads + 1) * 8, hipHostMallocDefault));
+    HIPCHK(hipHostMalloc(&L.hLengths, (reads + 1) * 4, hipHostMallocDefault));
+    HIPCHK(hipHostMalloc(&L.hOut, (reads + 1) * sizeof(snapgpu_result_t), hipHostMallocDefault));
+    L.capReads = reads;
+    L.capBytes = bytes;
+    return SNAPGPU_OK;
+}
+
+// The host tail of one chunk: wait for its records, account its kernel times, then MAPQ
+// fix-ups, statistics and the copy into the caller's array (host threads, while the GPU
+// already runs the next chunks).
+static int finishChunk(snapgpu_aligner_t *a, ExecLane &L, snapgpu_result_t *out) {
+    if (!L.pending) return SNAPGPU_OK;
+    L.pending = false;
+    int rc = waitEvent(a, L.done);
+    if (rc) return rc;
+    if ((rc = accountEvSet(a, a->evs[L.chunkEv]))) return rc;
+    const auto t0 = std::chrono::steady_clock::now();
+    const uint64_t n = L.chunkN;
+    snapgpu_result_t *dst = out + L.chunkBegin;
+    const unsigned nt = n >= 65536 ? std::max(1u, std::min(4u, std::thread::hardware_concurrency())) : 1u;
+    std::vector<snapgpu_aligner_stats_t> st(nt, snapgpu_aligner_stats_t{});
+    std::vector<uint64_t> fixed(nt, 0);
+    auto work = [&](unsigned t) {
+        const uint64_t b = n * t / nt, e = n * (t + 1) / nt;
+        memcpy(dst + b, L.hOut + b, (e - b) * sizeof(snapgpu_result_t));
+        for (uint64_t i = b; i < e; i++) {
+            snapgpu_result_t &o = dst[i];
+            if (o.flags & SNAPGPU_FLAG_MAPQ_FIXED) {
+                o.mapq = hostMapq(o.probabilityOfAllCandidates, o.probabilityOfBestCandidate, o.score, o.popularSeedsSkipped);
+                o.result = o.mapq >= 10 ? SNAPGPU_SINGLE_HIT : SNAPGPU_MULTIPLE_HITS;
+                fixed[t]++;
+            }
+            st[t].nHashTableLookups += o.nLookups;
+            st[t].nLocationsScored += o.nLocationsScored;
+            st[t].nHitsIgnoredBecauseOfTooHighPopularity += o.nHitsIgnored;
+            st[t].nReadsIgnoredBecauseOfTooManyNs += (o.flags & SNAPGPU_FLAG_TOO_MANY_NS) ? 1 : 0;
+        }
+    };
+    if (nt == 1) work(0);
+    else {
+        std::vector<std::thread> th;
+        for (unsigned t = 0; t < nt; t++) th.emplace_back(work, t);
+        for (auto &x : th) x.join();
+    }
+    for (unsigned t = 0; t < nt; t++) {
+        a->stats.nHashTableLookups += st[t].nHashTableLookups;
+        a->stats.nLocationsScored += st[t].nLocationsScored;
+        a->stats.nHitsIgnoredBecauseOfTooHighPopularity += st[t].nHitsIgnoredBecauseOfTooHighPopularity;
+        a->stats.nReadsIgnoredBecauseOfTooManyNs += st[t].nReadsIgnoredBecauseOfTooManyNs;
+        a->timing.nMapqFixed += fixed[t];
+    }
+    a->stats.nReads += n;
+    a->timing.fixupMs += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return SNAPGPU_OK;
+}
+
+// Batched BaseAligner::AlignRead over host buffers (SURVEY.md 8(d) d1 boundary): the reads are
+// cut into chunks that alternate over the two execution lanes -- H2D of the chunk's bytes,
+// offsets and lengths, the three passes, D2H of its records into pinned staging -- and the
+// host tail of chunk c-2 runs while chunks c-1 and c are on the GPU.
 int snapgpu_align_batch(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, snapgpu_result_t *out) {
     if (!a || !reads || !out) return SNAPGPU_EINVAL;
-    snapgpu_device_reads_t *d = snapgpu_reads_upload(a, reads);
-    if (!d) return SNAPGPU_EDEVICE;
-    int rc = snapgpu_align_resident(a, d);
-    if (!rc) rc = snapgpu_results_download(a, d, out);
-    snapgpu_device_reads_free(d);
+    if (a->failed) { snapgpu::setError("aligner failed earlier (device timeout)"); return SNAPGPU_EDEVICE; }
+    HIPCHK(hipSetDevice(a->device));
+    const auto w0 = std::chrono::steady_clock::now();
+    const uint64_t n = reads->n;
+    a->timing = snapgpu_timing_t{};
+    if (n == 0) return SNAPGPU_OK;
+    const uint64_t nChunks = (n + a->chunkReads - 1) / a->chunkReads;
+    const uint64_t per = (n + nChunks - 1) / nChunks;
+    // byte span of every chunk (reads are normally contiguous; any layout is accepted)
+    std::vector<uint64_t> lo(nChunks, ~0ull), hi(nChunks, 0);
+    uint64_t maxSpan = 0;
+    for (uint64_t c = 0; c < nChunks; c++) {
+        for (uint64_t i = c * per; i < std::min(n, (c + 1) * per); i++) {
+            lo[c] = std::min(lo[c], reads->offsets[i]);
+            hi[c] = std::max(hi[c], reads->offsets[i] + reads->lengths[i]);
+        }
+        if (hi[c] < lo[c]) lo[c] = hi[c] = 0;
+        maxSpan = std::max(maxSpan, hi[c] - lo[c]);
+    }
+    const uint64_t hostEnd = reads->totalBytes + 64;   // allocated and zeroed past the last read
+    for (auto &L : a->lane) {
+        const int rc = ensureLaneCapacity(a, L, std::min(per, n), maxSpan + 64);
+        if (rc) return rc;
+    }
+    int rc = beginCall(a);
+    if (rc) return rc;
+    for (uint64_t c = 0; c < nChunks && rc == SNAPGPU_OK; c++) {
+        ExecLane &L = a->lane[c & 1];
+        if ((rc = finishChunk(a, L, out))) break;   // chunk c-2: its buffers are free again
+        const uint64_t b = c * per, m = std::min(n, b + per) - b;
+        for (uint64_t i = 0; i < m; i++) {
+            L.hOffsets[i] = reads->offsets[b + i] - lo[c];
+            L.hLengths[i] = reads->lengths[b + i];
+        }
+        const uint64_t span = std::min(hi[c] + 64, std::max(hostEnd, hi[c])) - lo[c];
+        hipStream_t s = L.stream;
+        HIPCHK(hipMemcpyAsync(L.dBases, reads->bases + lo[c], span, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(L.dQuals, reads->quals + lo[c], span, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(L.dOffsets, L.hOffsets, m * 8, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(L.dLengths, L.hLengths, m * 4, hipMemcpyHostToDevice, s));
+        PassIO io{L.dBases, L.dQuals, L.dOffsets, L.dLengths, m, L.dOut, L.dDefer, L.dSeeds};
+        EvSet *ev = nextEvSet(a);
+        if (!ev) { rc = SNAPGPU_EDEVICE; break; }
+        if ((rc = launch_passes(a, (int)(c & 1), io, AlignExt(), *ev, c ? &a->evs[a->nEvUsed - 2] : nullptr))) break;
+        HIPCHK(hipMemcpyAsync(L.hOut, L.dOut, m * sizeof(snapgpu_result_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipEventRecord(L.done, s));
+        L.pending = true;
+        L.chunkBegin = b;
+        L.chunkN = m;
+        L.chunkEv = a->nEvUsed - 1;
+    }
+    // the older pending chunk first (chunk nChunks-2 is on lane (nChunks-2)&1)
+    for (uint64_t k = 0; k < 2 && rc == SNAPGPU_OK; k++) rc = finishChunk(a, a->lane[(nChunks + k) & 1], out);
+    if (rc) {   // leave no chunk in flight on these buffers (unless a timeout made that impossible)
+        for (auto &L : a->lane) { L.pending = false; if (!a->failed) waitLane(a, L); }
+        return rc;
+    }
+    accountBusy(a);
+    for (auto &L : a->lane) {   // lookup statistics of the whole call
+        HIPCHK(hipMemcpy(L.hLookupStats, L.lookupStats, 1024 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        addLookupStats(a->timing, L.hLookupStats);
+    }
+    rc = checkWatchdog(a);
     a->lastReads = nullptr;
+    a->pendingTiming = false;
+    a->timing.wallMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
     return rc;
 }
 
@@ -1201,7 +1676,7 @@ int snapgpu_align_batch_ex(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, c
     AlignExt x;
     void *dSearch = nullptr, *dScratch = nullptr, *dFound = nullptr, *dHits = nullptr;
     auto cleanup = [&]() {
-        hipFree(dSearch); hipFree(dScratch); hipFree(dFound); hipFree(dHits);
+        devFree(a, dSearch); devFree(a, dScratch); devFree(a, dFound); devFree(a, dHits);
         snapgpu_device_reads_free(d);
         a->lastReads = nullptr;
     };
@@ -1209,7 +1684,7 @@ int snapgpu_align_batch_ex(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, c
     const uint64_t n = reads->n;
     if (search) {
         if ((e = hipMalloc(&dSearch, n * sizeof(snapgpu_search_t))) == hipSuccess)
-            e = hipMemcpyAsync(dSearch, search, n * sizeof(snapgpu_search_t), hipMemcpyHostToDevice, a->stream);
+            e = hipMemcpyAsync(dSearch, search, n * sizeof(snapgpu_search_t), hipMemcpyHostToDevice, a->stream());
         x.search = (const snapgpu_search_t *)dSearch;
     }
     if (e == hipSuccess && maxHitsToGet) {
@@ -1228,7 +1703,7 @@ int snapgpu_align_batch_ex(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, c
         cleanup();
         return SNAPGPU_EDEVICE;
     }
-    int rc = launch_passes(a, d, x);
+    int rc = launch_resident(a, d, x);
     if (!rc) rc = snapgpu_results_download(a, d, out);
     if (!rc && maxHitsToGet) {
         if ((e = hipMemcpy(multiHitsFound, dFound, n * sizeof(int32_t), hipMemcpyDeviceToHost)) == hipSuccess)
@@ -1240,6 +1715,26 @@ int snapgpu_align_batch_ex(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, c
     }
     cleanup();
     return rc;
+}
+
+// Diagnostic self-test of the timeout path (no GPU needed): an aligner whose event never
+// completes must fail the wait with SNAPGPU_EDEVICE, mark itself failed, and from then on
+// free nothing (a freed buffer could still be in use by the kernel that never finished).
+int snapgpu_selftest_timeout_path(void) {
+    snapgpu_aligner_t fake;
+    fake.timeoutSec = 0.02;
+    fake.eventQuery = [](hipEvent_t) { return hipErrorNotReady; };
+    hipEvent_t never = reinterpret_cast<hipEvent_t>(0x10);
+    if (waitEvent(&fake, never) != SNAPGPU_EDEVICE || !fake.failed) return 1;
+    if (waitEvent(&fake, never) != SNAPGPU_EDEVICE) return 2;   // stays failed
+    auto *d = new snapgpu_device_reads_t();
+    d->owner = &fake;
+    d->dBases = reinterpret_cast<char *>(0x1000);   // never dereferenced or freed
+    d->dOut = reinterpret_cast<snapgpu_result_t *>(0x2000);
+    const uint64_t before = g_devFrees.load();
+    snapgpu_device_reads_free(d);
+    if (g_devFrees.load() != before) return 3;
+    return 0;
 }
 
 int snapgpu_last_timing(snapgpu_aligner_t *a, snapgpu_timing_t *t) {
@@ -1262,11 +1757,16 @@ int snapgpu_phase_cycles(snapgpu_aligner_t *a, uint64_t *out, int reset) {
 #endif
     if (!a->dPhase) { snapgpu::setError("phase diagnostics off (set SNAPGPU_PHASES=1 before aligner_create)"); return SNAPGPU_EINVAL; }
     HIPCHK(hipSetDevice(a->device));
-    HIPCHK(hipStreamSynchronize(a->stream));
+    HIPCHK(hipStreamSynchronize(a->stream()));
     std::vector<uint64_t> buf((size_t)a->grid * PH_SLOTS);
     HIPCHK(hipMemcpy(buf.data(), a->dPhase, buf.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
     for (size_t i = 0; i < buf.size(); i++) out[i % PH_SLOTS] += buf[i];
     if (reset) HIPCHK(hipMemset(a->dPhase, 0, buf.size() * sizeof(uint64_t)));
+    return SNAPGPU_OK;
+}
+int snapgpu_aligner_set_overlap(snapgpu_aligner_t *a, int overlap) {
+    if (!a) return SNAPGPU_EINVAL;
+    a->overlapKernels = overlap != 0;
     return SNAPGPU_OK;
 }
 int snapgpu_aligner_max_k(const snapgpu_aligner_t *a) { return a ? (int)a->p.maxK : -1; }
@@ -1368,16 +1868,20 @@ static int cigar_launch(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, CigarAr
     int grid = a->cigarGrid;
     if ((uint64_t)grid > d->n) grid = (int)d->n;
     if (grid == 0) return SNAPGPU_OK;
-    HIPCHK(hipEventRecord(a->cev[0], a->stream));
-    hipLaunchKernelGGL(cigar_kernel, dim3(grid), dim3(64), 0, a->stream, C);
+    HIPCHK(hipEventRecord(a->cev[0], a->stream()));
+    hipLaunchKernelGGL(cigar_kernel, dim3(grid), dim3(64), 0, a->stream(), C);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(a->cev[1], a->stream));
+    HIPCHK(hipEventRecord(a->cev[1], a->stream()));
     return SNAPGPU_OK;
 }
 
 int snapgpu_cigar_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, int useM) {
     if (!a || !d) return SNAPGPU_EINVAL;
     HIPCHK(hipSetDevice(a->device));
+    if (a->failed) { snapgpu::setError("aligner failed earlier (device timeout)"); return SNAPGPU_EDEVICE; }
+    // the records may come from pass sets on both lanes: lane 0 waits for lane 1
+    HIPCHK(hipEventRecord(a->lane[1].done, a->lane[1].stream));
+    HIPCHK(hipStreamWaitEvent(a->lane[0].stream, a->lane[1].done, 0));
     CigarArgs C = cigar_args(a, d, useM);
     C.records = d->dOut;
     return cigar_launch(a, d, C);
@@ -1387,7 +1891,7 @@ int snapgpu_cigar_download(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, int3
                            uint32_t *ops) {
     if (!a || !d || !editDistance || !nOps || !ops || !d->dCigEd) return SNAPGPU_EINVAL;
     HIPCHK(hipSetDevice(a->device));
-    HIPCHK(hipStreamSynchronize(a->stream));
+    HIPCHK(hipStreamSynchronize(a->stream()));
     HIPCHK(hipMemcpy(editDistance, d->dCigEd, d->n * 4, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(nOps, d->dCigN, d->n * 4, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(ops, d->dCigOps, d->n * CIG_MAX_OPS * 4, hipMemcpyDeviceToHost));
@@ -1440,11 +1944,11 @@ int snapgpu_gather_peak(snapgpu_aligner_t *a, uint32_t nLoads, double *ms) {
     const unsigned grid = (nLoads + 1023) / 1024;
     float best = 0;
     for (int rep = 0; rep < 3; rep++) {
-        HIPCHK(hipEventRecord(a->cev[0], a->stream));
-        hipLaunchKernelGGL(gather_peak_kernel, dim3(grid), dim3(256), 0, a->stream, a->dSlots, (uint32_t)nSlots, nLoads,
-                           0x5bd1e995u * (rep + 1), a->dCounter);
+        HIPCHK(hipEventRecord(a->cev[0], a->stream()));
+        hipLaunchKernelGGL(gather_peak_kernel, dim3(grid), dim3(256), 0, a->stream(), a->dSlots, (uint32_t)nSlots, nLoads,
+                           0x5bd1e995u * (rep + 1), a->lane[0].counter + 8);
         HIPCHK(hipGetLastError());
-        HIPCHK(hipEventRecord(a->cev[1], a->stream));
+        HIPCHK(hipEventRecord(a->cev[1], a->stream()));
         HIPCHK(hipEventSynchronize(a->cev[1]));
         float f = 0;
         HIPCHK(hipEventElapsedTime(&f, a->cev[0], a->cev[1]));
@@ -1452,6 +1956,36 @@ int snapgpu_gather_peak(snapgpu_aligner_t *a, uint32_t nLoads, double *ms) {
     }
     *ms = best;
     return SNAPGPU_OK;
+}
+
+// Streaming-copy ceiling (copy_peak_kernel): best of 3 over `bytes` read + `bytes` written.
+int snapgpu_copy_peak(snapgpu_aligner_t *a, uint64_t bytes, double *ms) {
+    if (!a || !ms || bytes < 4096) return SNAPGPU_EINVAL;
+    if (a->failed) return SNAPGPU_EDEVICE;
+    HIPCHK(hipSetDevice(a->device));
+    const uint64_t nw = bytes / 16 / 1024 * 1024;
+    void *src = nullptr, *dst = nullptr;
+    HIPCHK(hipMalloc(&src, nw * 16));
+    if (hipMalloc(&dst, nw * 16) != hipSuccess) { devFree(a, src); snapgpu::setError("copy_peak: hipMalloc"); return SNAPGPU_ENOMEM; }
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, a->device));
+    const unsigned grid = (unsigned)prop.multiProcessorCount * 16;
+    float best = 0;
+    int rc = SNAPGPU_OK;
+    HIPCHK(hipMemsetAsync(src, 1, nw * 16, a->stream()));
+    for (int rep = 0; rep < 4 && rc == SNAPGPU_OK; rep++) {   // first run warms up
+        hipEventRecord(a->cev[0], a->stream());
+        hipLaunchKernelGGL(copy_peak_kernel, dim3(grid), dim3(256), 0, a->stream(), (const uint4 *)src, (uint4 *)dst, nw);
+        hipEventRecord(a->cev[1], a->stream());
+        if (hipEventSynchronize(a->cev[1]) != hipSuccess) { rc = SNAPGPU_EDEVICE; break; }
+        float f = 0;
+        hipEventElapsedTime(&f, a->cev[0], a->cev[1]);
+        if (rep == 1 || (rep > 1 && f < best)) best = f;
+    }
+    devFree(a, src);
+    devFree(a, dst);
+    *ms = best;
+    return rc;
 }
 
 }  // extern "C"

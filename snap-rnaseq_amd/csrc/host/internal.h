@@ -2,6 +2,7 @@
 #pragma once
 #include "snapgpu.h"
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -18,14 +19,21 @@ constexpr unsigned kQuadraticChainingDepth = 5;      // HashTable.h:115
 
 void setError(const std::string &msg);
 
+// Host buffers the GPU copies from (read bases/qualities): page-locked when a HIP device is
+// present, so the aligner's chunked H2D copies run asynchronously at PCIe speed; plain
+// zeroed heap memory otherwise (build container).  *pinned says which one hostFree must undo.
+void *hostAlloc(size_t bytes, bool *pinned);
+void hostFree(void *p, bool pinned);
+
 struct Genome {
-    std::vector<char> buf;          // guard + bases + guard
+    std::vector<char> buf;          // guard + bases + guard (built or loaded genomes)
+    const char *ext = nullptr;      // or: the same layout in a mapped shared index (snapgpu_index_attach)
     uint32_t nBases = 0;
     uint32_t chromosomePadding = 500;
     std::vector<uint32_t> pieceOffsets;
     std::vector<std::string> pieceNames;
-    const char *bases() const { return buf.data() + kGenomeGuard; }
-    char *bases() { return buf.data() + kGenomeGuard; }
+    const char *bases() const { return (ext ? ext : buf.data()) + kGenomeGuard; }
+    char *bases() { return const_cast<char *>(ext ? ext : buf.data()) + kGenomeGuard; }   // writable only when built
     // Append a contig the way ReadFASTAGenome does (FASTA.cpp:93-120): padding,
     // then the (already upper-cased, N->n) sequence.
     void reserve(uint64_t n);
@@ -35,17 +43,35 @@ struct Genome {
     void finish();                  // trailing padding + guards
 };
 
+// A read-only array that is either owned (heap, uninitialised until written) or a view into
+// a mapped file (a shared index attached by another rank).
+template <class T>
+struct Table {
+    std::unique_ptr<T[]> owned;
+    const T *ptr = nullptr;
+    uint64_t count = 0;
+    void allocate(uint64_t n) { owned.reset(new T[n ? n : 1]); ptr = owned.get(); count = n; }
+    void view(const T *p, uint64_t n) { owned.reset(); ptr = p; count = n; }
+    T *mut() { return owned.get(); }
+    const T *data() const { return ptr; }
+    uint64_t size() const { return count; }
+    bool empty() const { return count == 0; }
+    const T &operator[](uint64_t i) const { return ptr[i]; }
+};
+
 struct Index {
     Genome *genome = nullptr;       // owned
     uint32_t seedLen = 20;
     uint32_t nTables = 0;
-    std::vector<uint32_t> slots;    // 3 words per slot: key, value1, value2
+    Table<uint32_t> slots;          // 3 words per slot: key, value1, value2
     std::vector<uint64_t> tableBase;
     std::vector<uint64_t> tableSize;
     std::vector<uint64_t> tableUsed;
-    std::vector<uint32_t> overflow;
+    Table<uint32_t> overflow;
     bool hasIupac = false;
-    ~Index() { delete genome; }
+    void *mapBase = nullptr;        // snapgpu_index_attach: the mapped shared file
+    uint64_t mapLen = 0;
+    ~Index();
 };
 
 // SNAPHashTable::hash (HashTable.h:60-72): MurmurHash3 fmix32.

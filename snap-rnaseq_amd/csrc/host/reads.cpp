@@ -14,8 +14,10 @@ snapgpu_reads_t *allocReads(uint64_t n, uint64_t totalBytes, bool truth) {
     auto *r = new snapgpu_reads_t();
     r->n = n;
     r->totalBytes = totalBytes;
-    r->bases = new char[totalBytes + 64]();
-    r->quals = new char[totalBytes + 64]();
+    bool pb = false, pq = false;
+    r->bases = (char *)hostAlloc(totalBytes + 64, &pb);
+    r->quals = (char *)hostAlloc(totalBytes + 64, &pq);
+    r->hostFlags = (pb ? 1u : 0u) | (pq ? 2u : 0u);
     r->offsets = new uint64_t[n + 1]();
     r->lengths = new uint32_t[n + 1]();
     r->truthLocation = truth ? new uint32_t[n + 1]() : nullptr;
@@ -134,9 +136,11 @@ snapgpu_reads_t *snapgpu_reads_from_arrays(uint64_t n, const char *bases, const 
 }
 
 snapgpu_reads_t *snapgpu_reads_from_fastq(const char *path) {
+    // FASTQReader::getNextRead (FASTQ.cpp:196-253): 4-line records, id = header line without
+    // '@' (trailing CR/LF removed), bases, '+' line, qualities.
     FILE *f = fopen(path, "r");
     if (!f) { setError(std::string("cannot open ") + path); return nullptr; }
-    std::vector<std::string> b, q;
+    std::vector<std::string> b, q, ids;
     std::string lines[4];
     char buf[1 << 16];
     int k = 0;
@@ -144,19 +148,37 @@ snapgpu_reads_t *snapgpu_reads_from_fastq(const char *path) {
         std::string s(buf);
         while (!s.empty() && (s.back() == '\n' || s.back() == '\r')) s.pop_back();
         lines[k++] = s;
-        if (k == 4) { b.push_back(lines[1]); q.push_back(lines[3]); k = 0; }
+        if (k == 4) {
+            if (lines[0].empty() || lines[0][0] != '@') {
+                fclose(f);
+                setError(std::string("FASTQ record without '@' header in ") + path);
+                return nullptr;
+            }
+            ids.push_back(lines[0].substr(1));
+            b.push_back(lines[1]);
+            q.push_back(lines[3]);
+            k = 0;
+        }
     }
     fclose(f);
-    uint64_t total = 0;
+    uint64_t total = 0, idTotal = 0;
     for (auto &s : b) total += s.size();
+    for (auto &s : ids) idTotal += s.size();
     snapgpu_reads_t *r = allocReads(b.size(), total, false);
-    uint64_t o = 0;
+    r->ids = new char[idTotal + 1]();
+    r->idOffsets = new uint64_t[b.size() + 1]();
+    r->idLengths = new uint32_t[b.size() + 1]();
+    uint64_t o = 0, io = 0;
     for (size_t i = 0; i < b.size(); i++) {
         memcpy(r->bases + o, b[i].data(), b[i].size());
         memcpy(r->quals + o, q[i].data(), std::min(q[i].size(), b[i].size()));
         r->offsets[i] = o;
         r->lengths[i] = (uint32_t)b[i].size();
         o += b[i].size();
+        memcpy(r->ids + io, ids[i].data(), ids[i].size());
+        r->idOffsets[i] = io;
+        r->idLengths[i] = (uint32_t)ids[i].size();
+        io += ids[i].size();
     }
     return r;
 }
@@ -165,8 +187,13 @@ int snapgpu_reads_write_fastq(const snapgpu_reads_t *r, const char *path) {
     FILE *f = fopen(path, "w");
     if (!f) { setError(std::string("cannot write ") + path); return SNAPGPU_EIO; }
     for (uint64_t i = 0; i < r->n; i++) {
-        fprintf(f, "@read%llu", (unsigned long long)i);
-        if (r->truthLocation) fprintf(f, "_%u_%u", r->truthLocation[i], (unsigned)r->truthDirection[i]);
+        if (r->ids) {
+            fputc('@', f);
+            fwrite(r->ids + r->idOffsets[i], 1, r->idLengths[i], f);
+        } else {
+            fprintf(f, "@read%llu", (unsigned long long)i);
+            if (r->truthLocation) fprintf(f, "_%u_%u", r->truthLocation[i], (unsigned)r->truthDirection[i]);
+        }
         fputc('\n', f);
         fwrite(r->bases + r->offsets[i], 1, r->lengths[i], f);
         fputs("\n+\n", f);
@@ -180,8 +207,12 @@ int snapgpu_reads_write_fastq(const snapgpu_reads_t *r, const char *path) {
 
 void snapgpu_reads_free(snapgpu_reads_t *r) {
     if (!r) return;
-    delete[] r->bases; delete[] r->quals; delete[] r->offsets; delete[] r->lengths;
+    hostFree(r->bases, r->hostFlags & 1u);
+    hostFree(r->quals, r->hostFlags & 2u);
+    delete[] r->offsets; delete[] r->lengths;
     delete[] r->truthLocation; delete[] r->truthDirection;
+    delete[] r->frontClipped; delete[] r->unclippedLength;
+    delete[] r->ids; delete[] r->idOffsets; delete[] r->idLengths;
     delete r;
 }
 

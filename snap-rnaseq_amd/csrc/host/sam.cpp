@@ -176,6 +176,16 @@ extern "C" int snapgpu_sam_format_clipped(const snapgpu_index_t *idx, const snap
             setError("sam_format: nOps > SNAPGPU_CIGAR_MAX_OPS, read longer than 1024 bases or bad clip arrays");
             return SNAPGPU_EINVAL;
         }
+    if (reads->frontClipped && unclippedLength)   // caller arrays must describe the batch's clip state
+        for (uint64_t i = 0; i < reads->n; i++)
+            if (frontClipped[i] != reads->frontClipped[i] || unclippedLength[i] != reads->unclippedLength[i]) {
+                setError("sam_format: clip arrays differ from the batch's clip state (snapgpu_reads_clip)");
+                return SNAPGPU_EINVAL;
+            }
+    if (!unclippedLength && reads->frontClipped) {   // the batch knows its own clips
+        frontClipped = reads->frontClipped;
+        unclippedLength = reads->unclippedLength;
+    }
     Job J{idx, reads, ids, idOffsets, idLengths, results, editDistance, nOps, ops, readGroup,
           unclippedLength ? frontClipped : nullptr, unclippedLength};
     const uint64_t n = reads->n;
@@ -214,28 +224,48 @@ extern "C" int snapgpu_sam_format(const snapgpu_index_t *idx, const snapgpu_read
 }
 
 // Read::clip (Read.h:357-404) on every read of a batch, in place: offsets/lengths become the
-// clipped read; frontClipped / unclippedLength receive what the SAM writer needs.
+// clipped read; frontClipped / unclippedLength receive what the SAM writer needs (and are kept
+// in the batch).  As Read::clip: a no-op when the batch is already in that state, otherwise the
+// read is restored to its unclipped extent first, so clip(3) twice or clip(3) then clip(0) give
+// the reference's reads.  Refused once the batch has been uploaded (the device copy would keep
+// the old extents while the SAM writer prints the new clips).
 extern "C" int snapgpu_reads_clip(snapgpu_reads_t *r, int clipping, uint32_t *frontClipped,
                                   uint32_t *unclippedLength) {
-    if (!r || !frontClipped || !unclippedLength || clipping < 0 || clipping > 3) {
+    if (!r || clipping < 0 || clipping > 3) {
         setError("reads_clip: bad argument");
         return SNAPGPU_EINVAL;
     }
-    for (uint64_t i = 0; i < r->n; i++) {
-        const char *q = r->quals + r->offsets[i];
-        const uint32_t full = r->lengths[i];
-        uint32_t len = full, front = 0;
-        if (clipping == 2 || clipping == 3)   // ClipBack / ClipFrontAndBack
-            while (len > 0 && q[len - 1] == '#') len--;
-        if (clipping == 1 || clipping == 3)   // ClipFront / ClipFrontAndBack
-            while (front < len && q[front] == '#') front++;
-        if (len - front < 50) { len = full; front = 0; }   // "just use all of it" (Read.h:394-397)
-        else len -= front;
-        frontClipped[i] = front;
-        unclippedLength[i] = full;
-        r->offsets[i] += front;
-        r->lengths[i] = len;
+    if (r->nUploads) {
+        setError("reads_clip: the batch was already uploaded to a device; clip before uploading");
+        return SNAPGPU_EINVAL;
     }
+    if (!r->frontClipped) {   // first clip: remember the unclipped extents
+        r->frontClipped = new uint32_t[r->n + 1]();
+        r->unclippedLength = new uint32_t[r->n + 1]();
+        for (uint64_t i = 0; i < r->n; i++) r->unclippedLength[i] = r->lengths[i];
+        r->clipping = 0;
+    }
+    if (clipping != r->clipping) {
+        for (uint64_t i = 0; i < r->n; i++) {
+            // revert to unclipped (Read.h:369-372)
+            r->offsets[i] -= r->frontClipped[i];
+            const uint32_t full = r->unclippedLength[i];
+            const char *q = r->quals + r->offsets[i];
+            uint32_t len = full, front = 0;
+            if (clipping == 2 || clipping == 3)   // ClipBack / ClipFrontAndBack
+                while (len > 0 && q[len - 1] == '#') len--;
+            if (clipping == 1 || clipping == 3)   // ClipFront / ClipFrontAndBack
+                while (front < len && q[front] == '#') front++;
+            if (len - front < 50) { len = full; front = 0; }   // "just use all of it" (Read.h:393-397)
+            else len -= front;
+            r->frontClipped[i] = front;
+            r->offsets[i] += front;
+            r->lengths[i] = len;
+        }
+        r->clipping = clipping;
+    }
+    if (frontClipped) memcpy(frontClipped, r->frontClipped, r->n * sizeof(uint32_t));
+    if (unclippedLength) memcpy(unclippedLength, r->unclippedLength, r->n * sizeof(uint32_t));
     return SNAPGPU_OK;
 }
 

@@ -20,6 +20,7 @@ UnusedScoreValue = 0xFFFF                                           # BaseAligne
 
 FLAG_READ_TOO_LONG = 0x01
 FLAG_MAPQ_FIXED = 0x02
+FLAG_DEFERRED = 0x04
 FLAG_TOO_MANY_NS = 0x08
 
 RESULT_DTYPE = np.dtype([
@@ -56,7 +57,7 @@ class SnapGpuError(RuntimeError):
     pass
 
 
-_PTR_CALLS = ("genome_from_fasta", "genome_synthetic", "index_build", "index_load", "reads_synthetic",
+_PTR_CALLS = ("genome_from_fasta", "genome_synthetic", "index_build", "index_load", "index_attach", "reads_synthetic",
               "reads_from_fastq", "reads_from_arrays", "aligner_create", "reads_upload")
 
 
@@ -130,14 +131,29 @@ class GenomeIndex:
         self._h = handle
 
     @classmethod
-    def build(cls, genome, seed_len=20, n_threads=0):
+    def build(cls, genome, seed_len=20, n_threads=0, slack=0.3):
+        """GenomeIndex::BuildIndexToDirectory semantics with the reference's table sizing
+        (slack as `snap-rna index -h`); takes ownership of the genome."""
         h = genome._h
         genome._h = None          # ownership moves to the index
-        return cls(_check(lib().snapgpu_index_build(h, seed_len, n_threads), "index_build"))
+        return cls(_check(lib().snapgpu_index_build_ex(h, seed_len, n_threads, float(slack)), "index_build"))
 
     @classmethod
     def load(cls, directory):
         return cls(_check(lib().snapgpu_index_load(str(directory).encode()), "index_load"))
+
+    def share(self, path):
+        """Write the flat shared form (one file, e.g. under /dev/shm) for snapgpu_index_attach."""
+        _check(lib().snapgpu_index_share(self._h, str(path).encode()), "index_share")
+
+    @classmethod
+    def attach(cls, path):
+        """Map a shared index read-only (no private copy of the tables)."""
+        return cls(_check(lib().snapgpu_index_attach(str(path).encode()), "index_attach"))
+
+    def genome_handle(self):
+        """The owned genome (a raw handle for Reads.synthetic; valid while the index lives)."""
+        return lib().snapgpu_index_genome(self._h)
 
     def save(self, directory):
         _check(lib().snapgpu_index_save(self._h, str(directory).encode()), "index_save")
@@ -216,6 +232,16 @@ class Reads:
         l = (C.c_uint32 * max(1, n))(*lens)
         return cls(_check(lib().snapgpu_reads_from_arrays(n, bytes(bases), bytes(quals), o, l), "reads_from_arrays"))
 
+    def slice(self, start, count):
+        """A copy of reads [start, start + count) as a new batch."""
+        r = self._p.contents
+        count = max(0, min(count, r.n - start))
+        offs = C.cast(C.addressof(r.offsets.contents) + 8 * start, C.POINTER(C.c_uint64))
+        lens = C.cast(C.addressof(r.lengths.contents) + 4 * start, C.POINTER(C.c_uint32))
+        return Reads(_check(lib().snapgpu_reads_from_arrays(count, C.cast(r.bases, C.c_char_p),
+                                                            C.cast(r.quals, C.c_char_p), offs, lens),
+                            "reads_from_arrays"))
+
     @property
     def n(self):
         return self._p.contents.n
@@ -227,6 +253,13 @@ class Reads:
         r = self._p.contents
         o, l = r.offsets[i], r.lengths[i]
         return C.string_at(r.bases + o, l), C.string_at(r.quals + o, l)
+
+    def ids(self):
+        """Read ids (FASTQ header without '@'), or None when the batch has none."""
+        r = self._p.contents
+        if not r.ids:
+            return None
+        return [C.string_at(r.ids + r.idOffsets[i], r.idLengths[i]) for i in range(r.n)]
 
     def truth(self):
         r = self._p.contents
@@ -281,10 +314,14 @@ class BaseAligner:
                                          stopOnFirstHit=int(stopOnFirstHit))
         self._h = _check(lib().snapgpu_aligner_create(device, index._h, C.byref(self.params)), "aligner_create")
 
-    def AlignReads(self, reads):
-        """Batched AlignRead -> numpy structured array of RESULT_DTYPE."""
+    def AlignReads(self, reads, out=None):
+        """Batched AlignRead -> numpy structured array of RESULT_DTYPE (written into `out`
+        when given: a caller streaming batches reuses one record buffer)."""
         n = reads.n
-        out = np.zeros(max(1, n), dtype=RESULT_DTYPE)
+        if out is None:
+            out = np.zeros(max(1, n), dtype=RESULT_DTYPE)
+        elif out.dtype != RESULT_DTYPE or len(out) < n or not out.flags.c_contiguous:
+            raise ValueError("out must be a C-contiguous RESULT_DTYPE array of at least reads.n records")
         if n:
             _check(lib().snapgpu_align_batch(self._h, reads._p, out.ctypes.data_as(C.POINTER(_ffi.Result))),
                    "align_batch")
@@ -333,6 +370,16 @@ class BaseAligner:
         from the resident hash table (roofline calibration for the seed lookups)."""
         ms = C.c_double()
         _check(lib().snapgpu_gather_peak(self._h, int(n_loads), C.byref(ms)), "gather_peak")
+        return ms.value
+
+    def set_overlap(self, overlap):
+        """Let the pass sets of the two streams run concurrently (default) or one after the other."""
+        _check(lib().snapgpu_aligner_set_overlap(self._h, int(bool(overlap))), "set_overlap")
+
+    def copy_peak_ms(self, nbytes):
+        """Diagnostic: best-of-3 time (ms) of a streaming copy of nbytes (read nbytes + write nbytes)."""
+        ms = C.c_double()
+        _check(lib().snapgpu_copy_peak(self._h, int(nbytes), C.byref(ms)), "copy_peak")
         return ms.value
 
     def cigar_ms(self):

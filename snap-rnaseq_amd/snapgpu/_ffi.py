@@ -86,6 +86,15 @@ class Reads(C.Structure):
         ("lengths", C.POINTER(C.c_uint32)),
         ("truthLocation", C.POINTER(C.c_uint32)),
         ("truthDirection", C.POINTER(C.c_uint8)),
+        ("frontClipped", C.POINTER(C.c_uint32)),
+        ("unclippedLength", C.POINTER(C.c_uint32)),
+        ("clipping", C.c_int32),
+        ("nUploads", C.c_uint32),
+        ("ids", C.c_void_p),
+        ("idOffsets", C.POINTER(C.c_uint64)),
+        ("idLengths", C.POINTER(C.c_uint32)),
+        ("hostFlags", C.c_uint32),
+        ("reserved_", C.c_uint32),
     ]
 
 
@@ -132,6 +141,10 @@ class Timing(C.Structure):
         ("lookupSeeds", C.c_uint64),
         ("lookupProbes", C.c_uint64),
         ("lookupOverflowReads", C.c_uint64),
+        ("nLaunches", C.c_uint64),
+        ("wallMs", C.c_double),
+        ("mainKernelBusyMs", C.c_double),
+        ("lookupKernelBusyMs", C.c_double),
     ]
 
 
@@ -163,7 +176,11 @@ _PROTOS = [
     ("snapgpu_genome_piece_offset", C.c_uint32, [C.c_void_p, C.c_int]),
     ("snapgpu_genome_piece_name", C.c_char_p, [C.c_void_p, C.c_int]),
     ("snapgpu_index_build", C.c_void_p, [C.c_void_p, C.c_int, C.c_int]),
+    ("snapgpu_index_build_ex", C.c_void_p, [C.c_void_p, C.c_int, C.c_int, C.c_double]),
     ("snapgpu_index_load", C.c_void_p, [C.c_char_p]),
+    ("snapgpu_index_share", C.c_int, [C.c_void_p, C.c_char_p]),
+    ("snapgpu_index_attach", C.c_void_p, [C.c_char_p]),
+    ("snapgpu_index_genome", C.c_void_p, [C.c_void_p]),
     ("snapgpu_index_save", C.c_int, [C.c_void_p, C.c_char_p]),
     ("snapgpu_index_free", None, [C.c_void_p]),
     ("snapgpu_index_get_info", C.c_int, [C.c_void_p, C.POINTER(IndexInfo)]),
@@ -191,6 +208,7 @@ _PROTOS = [
     ("snapgpu_last_timing", C.c_int, [C.c_void_p, C.POINTER(Timing)]),
     ("snapgpu_aligner_get_stats", C.c_int, [C.c_void_p, C.POINTER(AlignerStats)]),
     ("snapgpu_aligner_max_k", C.c_int, [C.c_void_p]),
+    ("snapgpu_aligner_set_overlap", C.c_int, [C.c_void_p, C.c_int]),
     ("snapgpu_phase_cycles", C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]),
     ("snapgpu_aligner_name", C.c_char_p, [C.c_void_p]),
     ("snapgpu_lv_batch", C.c_int, [C.c_int, C.c_int, C.c_uint32, C.c_char_p, C.POINTER(C.c_uint64),
@@ -210,6 +228,8 @@ _PROTOS = [
     ("snapgpu_sam_header", C.c_int, [C.c_void_p, C.c_int, C.c_char_p, C.c_char_p, C.c_char_p, C.c_void_p,
                                      C.c_uint64, C.POINTER(C.c_uint64)]),
     ("snapgpu_gather_peak", C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_double)]),
+    ("snapgpu_copy_peak", C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_double)]),
+    ("snapgpu_selftest_timeout_path", C.c_int, []),
     ("snapgpu_sam_format", C.c_int, [C.c_void_p, C.POINTER(Reads), C.c_char_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                      C.c_void_p, C.c_void_p, C.c_void_p, C.c_char_p, C.c_void_p, C.c_uint64,
                                      C.POINTER(C.c_uint64)]),

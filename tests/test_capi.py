@@ -121,3 +121,74 @@ def test_plain_c_caller(tmp_path):
     out = subprocess.run([str(exe)], capture_output=True, text=True, env=env, timeout=120)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "ok 1" in out.stdout
+
+
+def _clip_reads():
+    """Reads with '#' runs at both ends (clipped), one whose clip would leave < 50 bases
+    (kept whole, Read.h:393-397) and one without '#'."""
+    q1 = "###" + "I" * 90 + "#####"
+    q2 = "#" * 30 + "I" * 40 + "#" * 30
+    q3 = "I" * 100
+    seq = "ACGT" * 25
+    return snapgpu.Reads.from_list([(seq[:len(q1)], q1), (seq, q2), (seq, q3)])
+
+
+def test_clip_is_idempotent_and_reversible():
+    """Read::clip (Read.h:357-404): same state -> no-op; a new state re-clips from the
+    unclipped read; clip(0) restores it (a second clip used to re-clip the
+    clipped extents)."""
+    r = _clip_reads()
+    raw = [r.get(i) for i in range(r.n)]
+    f1, u1 = r.clip(3)
+    after1 = [r.get(i) for i in range(r.n)]
+    assert list(f1) == [3, 0, 0] and list(u1) == [98, 100, 100]
+    assert after1[0][0] == raw[0][0][3:93] and after1[1] == raw[1] and after1[2] == raw[2]
+    f2, u2 = r.clip(3)                       # same state: nothing changes
+    assert list(f2) == list(f1) and list(u2) == list(u1)
+    assert [r.get(i) for i in range(r.n)] == after1
+    f3, _ = r.clip(2)                        # ClipBack only, from the unclipped read
+    assert list(f3) == [0, 0, 0] and r.get(0)[0] == raw[0][0][:93]
+    f4, u4 = r.clip(0)                       # back to the unclipped read
+    assert list(f4) == [0, 0, 0] and list(u4) == [98, 100, 100]
+    assert [r.get(i) for i in range(r.n)] == raw
+
+
+def test_clip_refused_after_upload():
+    """A batch already on a device keeps its extents there: clipping is refused."""
+    r = _clip_reads()
+    r._p.contents.nUploads = 1             # what snapgpu_reads_upload records
+    with pytest.raises(snapgpu.SnapGpuError):
+        r.clip(3)
+
+
+def test_sam_format_rejects_foreign_clip_arrays():
+    g = snapgpu.Genome.synthetic(100_000, seed=1)
+    idx = snapgpu.GenomeIndex.build(g, 20, 1)
+    r = _clip_reads()
+    front, full = r.clip(3)
+    res = np.zeros(r.n, dtype=snapgpu.RESULT_DTYPE)
+    res["location"] = 0xFFFFFFFF
+    cig = snapgpu.Cigars.empty(r.n)
+    ok = snapgpu.sam_format(idx, r, ["a", "b", "c"], res, cig, clip=(front, full))
+    assert ok.count(b"\n") == 3
+    assert snapgpu.sam_format(idx, r, ["a", "b", "c"], res, cig) == ok   # the batch knows its clips
+    bad = front.copy()
+    bad[0] += 1
+    with pytest.raises(snapgpu.SnapGpuError):
+        snapgpu.sam_format(idx, r, ["a", "b", "c"], res, cig, clip=(bad, full))
+
+
+def test_fastq_ids_roundtrip(tmp_path):
+    fq = tmp_path / "r.fq"
+    fq.write_text("@r1 extra words\nACGTACGT\n+\nIIIIIIII\n@r2\nGGGG\n+\n####\n")
+    r = snapgpu.Reads.from_fastq(fq)
+    assert r.n == 2 and r.get(1) == (b"GGGG", b"####")
+    assert r.ids() == [b"r1 extra words", b"r2"]
+    r.write_fastq(tmp_path / "o.fq")
+    assert (tmp_path / "o.fq").read_text() == fq.read_text()
+
+
+def test_timeout_path_frees_nothing():
+    """after a device wait times out the aligner is failed and no device buffer is
+    freed (a hipFree would block on, or a reuse fault, the still-running kernel)."""
+    assert _ffi.lib().snapgpu_selftest_timeout_path() == 0

@@ -1,16 +1,15 @@
-"""N>1 orchestration of bench.py on CPU: two ranks over gloo (127.0.0.1), each
-generating its own read shard against the shared deterministic genome, a barrier-
-bracketed timed region and the max-over-ranks reduction.  The aligner itself needs a
-GPU; the per-rank compute here is the oracle on the rank's shard, and the check is
-that sharding + reduction behave as the driver's N-GPU bench expects (SURVEY 8(e):
-reads shard with no data-path collective)."""
+"""N>1 orchestration of bench.py on CPU: two ranks over gloo (127.0.0.1).  Rank 0 builds the
+index once and shares it through /dev/shm; rank 1 maps it (no second build); each rank
+generates its own read shard; the timed region is barrier-bracketed and reports the max over
+ranks.  The aligner itself needs a GPU; the per-rank compute here is the oracle on the rank's
+shard, and the checks are that index sharing, sharding and the reduction behave as the
+driver's N-GPU bench expects (reads shard with no data-path collective)."""
 import hashlib
 import os
 import socket
 import sys
 import time
 
-import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -30,10 +29,12 @@ def _rank_main(rank, world, port, q):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import bench
     import snapgpu
+    from snapgpu import shared_index
     from oracle_ffi import oracle_align
     w, r, local, dist = bench.init_distributed()
-    genome, reads = bench.make_workload(snapgpu, 300_000, 400, r)
-    idx = snapgpu.GenomeIndex.build(genome, 20, 2)
+    gen = dict(seed=2121, n_contigs=2, n_repeat_families=40)
+    idx, info = shared_index.build_once(snapgpu, 300_000, gen, 20, 2, r, w, dist)
+    reads = snapgpu.Reads.synthetic(idx.genome_handle(), 400, seed=99 + r)
     res = {}
 
     def step():
@@ -41,15 +42,23 @@ def _rank_main(rank, world, port, q):
         time.sleep(0.05 * (r + 1))          # rank 1 is the slow one
 
     elapsed = bench.timed_steps(step, 2, dist, lambda: None)
-    gdig = hashlib.sha256(snapgpu.Genome.synthetic(300_000, seed=2121, n_contigs=1,
-                                                   n_repeat_families=200).bases(0, 300_000)).hexdigest()
+    ii = idx.info()
+    v = idx.view()
+    import ctypes as C
+    gdig = hashlib.sha256(C.string_at(v.slots, 12 * ii["totalHashSlots"]) +
+                          C.string_at(v.genome, ii["nBases"])).hexdigest()
     rdig = hashlib.sha256(bytes(reads.get(0)[0]) + bytes(reads.get(399)[0])).hexdigest()
     single = int((res["out"]["result"] == snapgpu.SingleHit).sum())
+    path = info["shared_file"]
+    dist.barrier()
+    shared_index.cleanup(r, w)
+    dist.barrier()
+    gone = not os.path.exists(path)
     dist.destroy_process_group()
-    q.put((r, w, elapsed, gdig, rdig, single))
+    q.put((r, w, elapsed, gdig, rdig, single, info["built_by_this_rank"], gone))
 
 
-def test_two_rank_sharding_and_max_reduction():
+def test_two_rank_index_built_once_sharding_and_max_reduction():
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -69,9 +78,43 @@ def test_two_rank_sharding_and_max_reduction():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (r0, w0, e0, g0, d0, s0), (r1, w1, e1, g1, d1, s1) = out
+    (r0, w0, e0, g0, d0, s0, b0, x0), (r1, w1, e1, g1, d1, s1, b1, x1) = out
     assert (r0, r1, w0, w1) == (0, 1, 2, 2)
     assert e0 == e1 >= 2 * 0.1                 # every rank reports the slowest rank's time
-    assert g0 == g1                            # replicated genome/index
+    assert (b0, b1) == (True, False)           # the index is built exactly once (rank 0)
+    assert g0 == g1                            # rank 1 maps the very same tables and genome
+    assert x0 and x1                           # the shared file is removed at the end
     assert d0 != d1                            # disjoint read shards
     assert s0 > 300 and s1 > 300               # each shard aligns (oracle stand-in for the GPU)
+
+
+def test_shared_index_roundtrip(tmp_path):
+    """snapgpu_index_share / snapgpu_index_attach: identical info, tables, genome and lookups."""
+    import ctypes as C
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "snap-rnaseq_amd"))
+    import snapgpu
+    g = snapgpu.Genome.synthetic(200_000, seed=5, n_contigs=3, n_repeat_families=20)
+    idx = snapgpu.GenomeIndex.build(g, 20, 2)
+    idx.share(tmp_path / "idx.bin")
+    at = snapgpu.GenomeIndex.attach(tmp_path / "idx.bin")
+    i1, i2 = idx.info(), at.info()
+    assert i1 == i2
+    v1, v2 = idx.view(), at.view()
+    assert C.string_at(v1.slots, 12 * i1["totalHashSlots"]) == C.string_at(v2.slots, 12 * i2["totalHashSlots"])
+    assert C.string_at(v1.overflow, 4 * i1["overflowTableSize"]) == C.string_at(v2.overflow, 4 * i2["overflowTableSize"])
+    assert C.string_at(v1.genome - 256, i1["nBases"] + 512) == C.string_at(v2.genome - 256, i2["nBases"] + 512)
+    gen1 = snapgpu.Genome(idx.genome_handle())
+    gen2 = snapgpu.Genome(at.genome_handle())
+    try:
+        assert [p for p in gen1.pieces] == [p for p in gen2.pieces]
+    finally:
+        gen1._h = gen2._h = None   # borrowed handles: the indexes own the genomes
+    rng = np.random.default_rng(1)
+    for p in rng.integers(1000, i1["nBases"] - 1000, 200):
+        s = idx.genome_bases(int(p), 20).decode()
+        if set(s) <= set("ACGT"):
+            assert idx.lookupSeed(s) == at.lookupSeed(s)
+    with pytest.raises(snapgpu.SnapGpuError):
+        (tmp_path / "bad.bin").write_bytes(b"x" * 8192)
+        snapgpu.GenomeIndex.attach(tmp_path / "bad.bin")

@@ -1,13 +1,17 @@
 #!/bin/bash
-# rocprofv3 passes for the bench workload: kernel trace + stats, then PMC passes
-# (FETCH_SIZE; SQ wave-state; instruction mix), each in its own run.
+# rocprofv3 evidence for the bench workload, each pass in its own run:
+#   kt   kernel trace + stats of the bench command itself (same command as the bench line)
+#   pmc* FETCH_SIZE / WRITE_SIZE / SQ wave state / SQ instruction mix (one counter group per run)
+# then tools/pmc_summary.py folds them into profiles/<tag>/summary.json + profiles/pmc_traffic.json.
+#   gpurun -- bash tools/gpu/prof.sh <tag> [bench args...]
 export TMPDIR=/tmp
-OUT=gpurun_out/prof_${1:-r01}
+TAG=${1:-r02}; shift
+OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o run --output-format csv -- $B > $OUT/kt.log 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc1 -o run --output-format csv -- $B > $OUT/pmc1.log 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc1w -o run --output-format csv -- $B > $OUT/pmc1w.log 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d $OUT/pmc2 -o run --output-format csv -- $B > $OUT/pmc2.log 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_INSTS_BRANCH -d $OUT/pmc3 -o run --output-format csv -- $B > $OUT/pmc3.log 2>&1 || exit $?
-echo PROF_DONE
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o run --output-format csv -- python3 bench.py "$@" > $OUT/bench_kt.json 2> $OUT/kt.log || exit $?
+B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline $*"
+timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc1 -o run --output-format csv -- $B > $OUT/pmc1.log 2>&1 || exit $?
+timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc1w -o run --output-format csv -- $B > $OUT/pmc1w.log 2>&1 || exit $?
+timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d $OUT/pmc2 -o run --output-format csv -- $B > $OUT/pmc2.log 2>&1 || exit $?
+timeout -s KILL 180 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_THREAD_CYCLES_VALU -d $OUT/pmc3 -o run --output-format csv -- $B > $OUT/pmc3.log 2>&1 || exit $?
+python3 tools/pmc_summary.py $OUT profiles/$TAG && echo PROF_DONE
