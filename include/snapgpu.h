@@ -351,6 +351,16 @@ int snapgpu_lv_batch(int device, int direction, uint32_t n,
                      const uint32_t *patLen, const int32_t *k,
                      int32_t *outScore, int32_t *outNetIndel, double *outProb);
 
+/* The same calls through the production bit-plane LV of align_kernel<128> (lv_group /
+ * lv_prob_pair in align_score.h) instead of the byte-compare engine: unit parity for the LV
+ * that scores every read of <= 128 bases.  Patterns of 1..127 bases; netIndel is reported
+ * for direction -1 only (the aligner uses only the reverse call's, BaseAligner.cpp:1232). */
+int snapgpu_lv_group_batch(int device, int direction, uint32_t n,
+                           const char *texts, const uint64_t *textOff, const uint32_t *textLen,
+                           const char *patterns, const char *quals, const uint64_t *patOff,
+                           const uint32_t *patLen, const int32_t *k,
+                           int32_t *outScore, int32_t *outNetIndel, double *outProb);
+
 /* ------------------------------------------------- CIGAR / SAM records */
 /* The SAM writer's per-read work, on the GPU:
  * LandauVishkinWithCigar::computeEditDistance (LandauVishkin.cpp:252-535) as

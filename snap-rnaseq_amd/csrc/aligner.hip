@@ -687,6 +687,92 @@ __global__ __launch_bounds__(64) void lv_kernel(const LvTask *tasks, const char 
     if (lane == 0) { outScore[blockIdx.x] = r.score; outNet[blockIdx.x] = r.netIndel; outProb[blockIdx.x] = r.prob; }
 }
 
+// Unit-test kernel of the production bit-plane LV (align_score.h): one task per wave, group 0
+// of lv_group<DIR, GS> (GS chosen from k as score_batched does) on the mismatch mask a pass
+// would build, then lv_prob_pair for the match probability.  The task's text and pattern are
+// mapped onto a virtual read and genome window exactly as lv_pass sees them:
+//   forward: read = pattern, genome[loc + y] = text[y]; pattern index i = read position i;
+//   reverse: read[m] = pattern[pl-1-m], genome[loc + y] = text[tl - pl + y], and the reverse LV
+//            runs on the bit-reversed mask with q0 = 127 - (pl - 1), as lv_pass calls it.
+struct LvgTask {
+    uint64_t pOff, tOff;   // pattern/quals offset, text offset
+    int32_t pl, tl, k, dir;
+};
+
+template <int GS, int DIR>
+__device__ __forceinline__ void lvg_run(Lds<128> &S, const LvgTask &T, const char *pats, const char *texts,
+                                        int32_t *outScore, int32_t *outNet, double *outProb) {
+    GroupLds &G = S.grp[0];
+    const int lane = lane_id();
+    const int li = lane & (GS - 1), gi = lane / GS, c = GS / 2 - 1;
+    const bool act = gi == 0;
+    const int pl = T.pl, tl = T.tl;
+    // F_x[m] = read[m] != genome[loc + x + m], x = li - c; mismatch past the read or the text
+    Mask128 F;
+    uint32_t f[4] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+    if (act) {
+        const int x = li - c;
+        for (int m = 0; m < 128; m++) {
+            bool mm = true;
+            if (m < pl) {
+                const char r = DIR > 0 ? pats[T.pOff + m] : pats[T.pOff + pl - 1 - m];
+                const int y = DIR > 0 ? x + m : tl - pl + x + m;
+                if (y >= 0 && y < tl) {
+                    const char g = texts[T.tOff + y];
+                    const uint32_t rc = packed_code((uint8_t)r), gc = packed_code((uint8_t)g);
+                    mm = rc > 3 || gc > 3 || rc != gc;
+                }
+            }
+            if (!mm) f[m >> 5] &= ~(1u << (m & 31));
+        }
+    }
+    F.lo = ((uint64_t)f[1] << 32) | f[0];
+    F.hi = ((uint64_t)f[3] << 32) | f[2];
+    int e = -1;
+    if (DIR > 0) lv_group<1, GS>(G, S.u.sc.rows8, F, act, 0, pl, tl, T.k, T.k, e);
+    else lv_group<-1, GS>(G, S.u.sc.rows8, mk_reverse(F), act, 127 - (pl - 1), pl, tl, T.k, T.k, e);
+    e = readlane(e, 0);
+    wave_sync();
+    double p1 = 1.0, p2 = 1.0;
+    int net2 = 0;
+    if (e >= 0) {
+        if (lane == 0) G.plen[DIR > 0 ? 1 : 0][0] = 0;   // only this direction's path
+        wave_sync();
+        // forward: patternLen = n - t0 = pl (t0 = 0); reverse: patternLen = s0 = pl (t0 = n)
+        lv_prob_pair(nullptr, G, 0, 0, pl, DIR > 0 ? 0 : pl, DIR > 0 ? 0 : pl, S.fwdQ, p1, p2, net2);
+    }
+    if (lane == 0) {
+        outScore[blockIdx.x] = e;
+        outNet[blockIdx.x] = DIR > 0 ? 0 : net2;
+        outProb[blockIdx.x] = e >= 0 ? (DIR > 0 ? p1 : p2) : 1.0;
+    }
+}
+
+__global__ __launch_bounds__(64) void lv_group_kernel(const LvgTask *tasks, const char *pats, const char *quals,
+                                                      const char *texts, int32_t *outScore, int32_t *outNet,
+                                                      double *outProb) {
+    __shared__ Lds<128> S;
+    const int lane = lane_id();
+    const LvgTask T = tasks[blockIdx.x];
+    // qualities in read coordinates (reverse: read[m] = pattern[pl-1-m])
+    for (int m = lane; m < 128 + 64; m += WAVE)
+        S.fwdQ[m] = m < T.pl ? (T.dir > 0 ? quals[T.pOff + m] : quals[T.pOff + T.pl - 1 - m]) : 0;
+    wave_sync();
+    const int k = T.k < MAX_K - 1 ? T.k : MAX_K - 1;
+    const int GS = k <= 3 ? 8 : (k <= 7 ? 16 : (k <= 15 ? 32 : 64));   // score_batched's choice
+    if (T.dir > 0) {
+        if (GS == 8) lvg_run<8, 1>(S, T, pats, texts, outScore, outNet, outProb);
+        else if (GS == 16) lvg_run<16, 1>(S, T, pats, texts, outScore, outNet, outProb);
+        else if (GS == 32) lvg_run<32, 1>(S, T, pats, texts, outScore, outNet, outProb);
+        else lvg_run<64, 1>(S, T, pats, texts, outScore, outNet, outProb);
+    } else {
+        if (GS == 8) lvg_run<8, -1>(S, T, pats, texts, outScore, outNet, outProb);
+        else if (GS == 16) lvg_run<16, -1>(S, T, pats, texts, outScore, outNet, outProb);
+        else if (GS == 32) lvg_run<32, -1>(S, T, pats, texts, outScore, outNet, outProb);
+        else lvg_run<64, -1>(S, T, pats, texts, outScore, outNet, outProb);
+    }
+}
+
 }  // namespace sgk
 
 // ======================================================================= host
@@ -1835,6 +1921,56 @@ int snapgpu_lv_batch(int device, int direction, uint32_t n, const char *texts, c
     hipMemcpy(outProb, dP, n * 8, hipMemcpyDeviceToHost);
     hipFree(dT); hipFree(dR); hipFree(dQ); hipFree(dG); hipFree(dTab); hipFree(dS); hipFree(dN); hipFree(dP);
     return SNAPGPU_OK;
+}
+
+// The production bit-plane LV (lv_group + lv_prob_pair) on explicit tasks: unit parity for
+// LandauVishkin<dir>::computeEditDistance as align_kernel<128> runs it (patterns <= 127 bases).
+int snapgpu_lv_group_batch(int device, int direction, uint32_t n, const char *texts, const uint64_t *textOff,
+                           const uint32_t *textLen, const char *patterns, const char *quals, const uint64_t *patOff,
+                           const uint32_t *patLen, const int32_t *k, int32_t *outScore, int32_t *outNetIndel,
+                           double *outProb) {
+    if (n == 0) return SNAPGPU_OK;
+    int ndev = snapgpu_device_count();
+    if (ndev <= 0 || device >= ndev) { snapgpu::setError("no such HIP device"); return SNAPGPU_EDEVICE; }
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(ensureDeviceTables(device));
+    std::vector<LvgTask> tasks(n);
+    uint64_t pBytes = 0, tBytes = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        if (patLen[i] == 0 || patLen[i] > 127 || k[i] < 0) {
+            snapgpu::setError("lv_group_batch: pattern length must be 1..127 and k >= 0");
+            return SNAPGPU_EINVAL;
+        }
+        pBytes = std::max<uint64_t>(pBytes, patOff[i] + patLen[i]);
+        tBytes = std::max<uint64_t>(tBytes, textOff[i] + textLen[i]);
+        tasks[i] = LvgTask{patOff[i], textOff[i], (int32_t)patLen[i], (int32_t)textLen[i], k[i], direction > 0 ? 1 : -1};
+    }
+    LvgTask *dT = nullptr; char *dP = nullptr, *dQ = nullptr, *dX = nullptr;
+    int32_t *dS = nullptr, *dN = nullptr; double *dPr = nullptr;
+    int rc = SNAPGPU_OK;
+    if (hipMalloc(&dT, n * sizeof(LvgTask)) != hipSuccess || hipMalloc(&dP, pBytes + 64) != hipSuccess ||
+        hipMalloc(&dQ, pBytes + 64) != hipSuccess || hipMalloc(&dX, tBytes + 64) != hipSuccess ||
+        hipMalloc(&dS, n * 4) != hipSuccess || hipMalloc(&dN, n * 4) != hipSuccess || hipMalloc(&dPr, n * 8) != hipSuccess) {
+        snapgpu::setError("lv_group_batch: hipMalloc");
+        rc = SNAPGPU_ENOMEM;
+    }
+    if (!rc) {
+        hipMemcpy(dT, tasks.data(), n * sizeof(LvgTask), hipMemcpyHostToDevice);
+        hipMemcpy(dP, patterns, pBytes, hipMemcpyHostToDevice);
+        hipMemcpy(dQ, quals, pBytes, hipMemcpyHostToDevice);
+        hipMemcpy(dX, texts, tBytes, hipMemcpyHostToDevice);
+        hipLaunchKernelGGL(lv_group_kernel, dim3(n), dim3(64), 0, 0, dT, dP, dQ, dX, dS, dN, dPr);
+        if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+            snapgpu::setError("lv_group_kernel failed");
+            rc = SNAPGPU_EDEVICE;
+        } else {
+            hipMemcpy(outScore, dS, n * 4, hipMemcpyDeviceToHost);
+            hipMemcpy(outNetIndel, dN, n * 4, hipMemcpyDeviceToHost);
+            hipMemcpy(outProb, dPr, n * 8, hipMemcpyDeviceToHost);
+        }
+    }
+    hipFree(dT); hipFree(dP); hipFree(dQ); hipFree(dX); hipFree(dS); hipFree(dN); hipFree(dPr);
+    return rc;
 }
 
 // ------------------------------------------------------ CIGAR / SAM records

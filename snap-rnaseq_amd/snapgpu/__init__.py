@@ -547,10 +547,12 @@ def sam_format(index, reads, ids, results, cigars, read_group="FASTQ", clip=None
     return C.string_at(buf, used.value)
 
 
-def lv_batch(direction, tasks, device=0):
+def lv_batch(direction, tasks, device=0, engine="byte"):
     """LandauVishkin<direction>::computeEditDistance on the GPU.
 
-    tasks: list of (text, pattern, quals, k) (str/bytes).  -> list of (score, netIndel, prob)."""
+    tasks: list of (text, pattern, quals, k) (str/bytes).  -> list of (score, netIndel, prob).
+    engine "byte": the byte-compare LV of align_kernel<512>; "bitplane": the production LV of
+    align_kernel<128> (patterns of 1..127 bases)."""
     n = len(tasks)
     texts, pats, quals = bytearray(), bytearray(), bytearray()
     toff, tlen, poff, plen, ks = [], [], [], [], []
@@ -564,8 +566,9 @@ def lv_batch(direction, tasks, device=0):
     texts += b"\0" * 16; pats += b"\0" * 16; quals += b"\0" * 16
     A64, A32, AI = C.c_uint64 * n, C.c_uint32 * n, C.c_int32 * n
     os_, on, op = AI(), AI(), (C.c_double * n)()
-    _check(lib().snapgpu_lv_batch(device, direction, n, bytes(texts), A64(*toff), A32(*tlen), bytes(pats),
-                                  bytes(quals), A64(*poff), A32(*plen), AI(*ks), os_, on, op), "lv_batch")
+    fn = lib().snapgpu_lv_batch if engine == "byte" else lib().snapgpu_lv_group_batch
+    _check(fn(device, direction, n, bytes(texts), A64(*toff), A32(*tlen), bytes(pats),
+              bytes(quals), A64(*poff), A32(*plen), AI(*ks), os_, on, op), "lv_batch")
     return [(os_[i], on[i], op[i]) for i in range(n)]
 
 

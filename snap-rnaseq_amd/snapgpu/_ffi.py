@@ -215,6 +215,10 @@ _PROTOS = [
                                    C.POINTER(C.c_uint32), C.c_char_p, C.c_char_p, C.POINTER(C.c_uint64),
                                    C.POINTER(C.c_uint32), C.POINTER(C.c_int32), C.POINTER(C.c_int32),
                                    C.POINTER(C.c_int32), C.POINTER(C.c_double)]),
+    ("snapgpu_lv_group_batch", C.c_int, [C.c_int, C.c_int, C.c_uint32, C.c_char_p, C.POINTER(C.c_uint64),
+                                         C.POINTER(C.c_uint32), C.c_char_p, C.c_char_p, C.POINTER(C.c_uint64),
+                                         C.POINTER(C.c_uint32), C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                         C.POINTER(C.c_int32), C.POINTER(C.c_double)]),
     ("snapgpu_compute_mapq", C.c_int, [C.c_double, C.c_double, C.c_int, C.c_int]),
     ("snapgpu_cigar_batch", C.c_int, [C.c_void_p, C.POINTER(Reads), C.c_void_p, C.c_void_p, C.c_int, C.c_void_p,
                                       C.c_void_p, C.c_void_p]),

@@ -11,6 +11,7 @@ TSV/JSON expected outputs.
     python3 tests/golden/make_golden.py                  # everything
     python3 tests/golden/make_golden.py --only-multihit  # windowed search / multi-hit runs only
     python3 tests/golden/make_golden.py --only-cigar     # CIGAR calls + SAM records only
+    python3 tests/golden/make_golden.py --only-refindex  # reference-built index + seedLen fixtures
 """
 import hashlib
 import json
@@ -180,8 +181,49 @@ def cigar_fixtures(work):
                          "reads.fq", "-o", "out.sam"]))
 
 
+SEED_LENS = (16, 22, 25)
+
+
+def refindex_fixtures(work):
+    """(1) The reference's own on-disk index of small.fa (`snap-rna index`, seed 20, slack 0.3),
+    committed as a gzipped tar: the exact input GenomeIndex::loadFromDirectory
+    (GenomeIndex.cpp:845-963) and our snapgpu_index_load read.  (2) The reference's AlignRead
+    outputs at seed lengths 16, 22 and 25 (`snap-rna index -s N`): these pin the
+    GetWrappedNextSeedToTest tables of SeedSequencer.h:28-287 and the 1 / 4096 / 262144-table
+    layouts."""
+    import tarfile
+    import io
+    import gzip
+    fa = os.path.join(HERE, "small.fa")
+    fq = os.path.join(HERE, "small_reads.fq")
+    idxdir = os.path.join(work, "small_ref_idx")
+    ref_index(fa, idxdir)
+    buf = io.BytesIO()
+    with tarfile.open(fileobj=buf, mode="w") as t:
+        for fn in sorted(os.listdir(idxdir)):
+            info = t.gettarinfo(os.path.join(idxdir, fn), arcname=fn)
+            info.mtime = 0
+            info.uid = info.gid = 0
+            info.uname = info.gname = ""
+            with open(os.path.join(idxdir, fn), "rb") as f:
+                t.addfile(info, f)
+    with open(os.path.join(HERE, "small_ref_index.tar.gz"), "wb") as f:
+        f.write(gzip.compress(buf.getvalue(), compresslevel=9, mtime=0))
+    for L in SEED_LENS:
+        d = os.path.join(work, f"small_idx_s{L}")
+        shutil.rmtree(d, ignore_errors=True)
+        run([SNAP, "index", fa, d, "-s", str(L)])
+        with open(os.path.join(HERE, f"expected_small_seed{L}.tsv"), "w") as f:
+            f.write(ref_align(d, fq, PARAM_SETS["default"]))
+
+
 def main():
     work = tempfile.mkdtemp(prefix="golden_")
+    if "--only-refindex" in sys.argv:
+        refindex_fixtures(work)
+        shutil.rmtree(work, ignore_errors=True)
+        print("reference index + seedLen fixtures written to", HERE)
+        return
     if "--only-cigar" in sys.argv:
         cigar_fixtures(work)
         shutil.rmtree(work, ignore_errors=True)
@@ -211,6 +253,7 @@ def main():
 
     multihit_fixtures(work)
     cigar_fixtures(work)
+    refindex_fixtures(work)
 
     # 2. lookupSeed golden: seeds from the genome, their RCs, mutated and random seeds
     rng = random.Random(9)
