@@ -417,6 +417,64 @@ int snapgpu_sam_format_clipped(const snapgpu_index_t *idx, const snapgpu_reads_t
 int snapgpu_sam_header(const snapgpu_index_t *idx, int sorted, const char *commandLine, const char *version,
                        const char *rgLine, char *out, uint64_t cap, uint64_t *used);
 
+/* --------------------------------------------- RNA annotation (GTF) */
+/* GTFReader (SNAPLib/GTFReader.cpp): exon lines of a GTF/GFF3 file -> transcripts, each an
+ * exon list sorted by start with an intron feature between consecutive exons (Load :1245,
+ * Parse :1302, GTFTranscript::Process :972). */
+typedef struct snapgpu_gtf snapgpu_gtf_t;
+snapgpu_gtf_t *snapgpu_gtf_load(const char *path);
+void snapgpu_gtf_free(snapgpu_gtf_t *gtf);
+int snapgpu_gtf_counts(const snapgpu_gtf_t *gtf, uint32_t *nFeatures, uint32_t *nTranscripts, uint32_t *nGenes);
+/* GTFReader::BuildTranscriptome (GTFReader.cpp:1840-1867): the FASTA `snap-rna transcriptome`
+ * indexes -- every transcript (id order) as the genome bytes of its exon/intron list. */
+int snapgpu_gtf_write_transcriptome(const snapgpu_gtf_t *gtf, const snapgpu_genome_t *genome, const char *fastaPath);
+/* GTFTranscript::GenomicPosition (GTFReader.cpp:1075-1105): 1-based transcript position ->
+ * 1-based genomic position (0 when the span runs past the transcript). */
+int snapgpu_gtf_genomic_position(const snapgpu_gtf_t *gtf, const char *transcriptId, uint32_t pos, uint32_t span,
+                                 uint32_t *genomicPos);
+/* LandauVishkinWithCigar::insertSpliceJunctions (LandauVishkin.cpp:119-250): the CIGAR of a
+ * transcriptome alignment at 1-based transcript position `pos`, given as (count, op) tokens,
+ * with 'N' runs inserted at the transcript's junctions.  NUL-terminated string out. */
+int snapgpu_gtf_splice_cigar(const snapgpu_gtf_t *gtf, const char *transcriptId, uint32_t pos, uint32_t nTokens,
+                             const uint32_t *counts, const char *ops, char *out, uint64_t cap, uint64_t *used);
+
+/* ----------------------------------- single-end product path (f1) */
+/* SingleAlignerContext::runIterationThread (SNAPLib/SingleAligner.cpp:141-320) batched on the
+ * GPU: per read Read::clip, the quality / length / N pre-filter (:247-257), the transcriptome
+ * and genome BaseAligner::AlignRead (two aligners, :270-276), AlignmentFilter::AddAlignment /
+ * FilterSingle (AlignmentFilter.cpp:140-300) and SAMFormat::writeRead (SAM.cpp:978-1153:
+ * GPU CIGARs, transcriptome records with insertSpliceJunctions) -- the SAM file `snap-rna single
+ * <genome> <transcriptome> <gtf> <reads>` writes.  Not built: the contamination database (-x),
+ * BAM / sorted output and the per-gene read-count files written after the run. */
+typedef struct snapgpu_single_options {
+    int32_t  clipping;               /* ReadClippingType, default 3 = ClipFrontAndBack (AlignerOptions.cpp:48) */
+    uint32_t confDiff;               /* -c, default 2 */
+    uint32_t maxDist;                /* -d, default 14 (the filter's maxDist) */
+    float    minPercentAbovePhred;   /* -fp, default 90 */
+    uint32_t minPhred;               /* -fm, default 20 */
+    uint32_t phredOffset;            /* -fo, default 33 */
+    uint32_t useM;                   /* -M */
+    uint32_t reserved;
+    const char *readGroup;           /* default "FASTQ" (AlignerOptions.cpp:65) */
+    const char *commandLine;         /* @PG CL: */
+    const char *version;             /* @PG VN: */
+} snapgpu_single_options_t;
+void snapgpu_single_options_default(snapgpu_single_options_t *o);
+
+typedef struct snapgpu_single_stats {   /* AlignerStats (AlignerStats.h:40-69) */
+    uint64_t totalReads, usefulReads, singleHits, multiHits, notFound, transcriptomeRecords;
+    double alignMs, cigarMs, filterMs, writeMs, wallMs;
+} snapgpu_single_stats_t;
+
+/* reads: a FASTQ batch with ids (snapgpu_reads_from_fastq), clipped here.  samPath receives
+ * the header and one line per read in input order. */
+int snapgpu_single_align(snapgpu_aligner_t *genomeAligner, snapgpu_aligner_t *transcriptomeAligner,
+                         const snapgpu_gtf_t *gtf, snapgpu_reads_t *reads, const snapgpu_single_options_t *opt,
+                         const char *samPath, snapgpu_single_stats_t *stats);
+/* The index an aligner was created over (BaseAligner's GenomeIndex; getGenome for the SAM writer). */
+const snapgpu_index_t *snapgpu_aligner_index(const snapgpu_aligner_t *a);
+int snapgpu_aligner_get_params(const snapgpu_aligner_t *a, snapgpu_aligner_params_t *p);
+
 /* Roofline calibration (diagnostic, no reference equivalent): time of nLoads independent
  * 12-byte SNAPHashTable slot loads at hashed positions of this aligner's resident table
  * (the access pattern of the seed lookups without their dependency chain), best of 3, ms. */

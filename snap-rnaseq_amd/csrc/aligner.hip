@@ -1850,6 +1850,12 @@ int snapgpu_phase_cycles(snapgpu_aligner_t *a, uint64_t *out, int reset) {
     if (reset) HIPCHK(hipMemset(a->dPhase, 0, buf.size() * sizeof(uint64_t)));
     return SNAPGPU_OK;
 }
+const snapgpu_index_t *snapgpu_aligner_index(const snapgpu_aligner_t *a) { return a ? a->idx : nullptr; }
+int snapgpu_aligner_get_params(const snapgpu_aligner_t *a, snapgpu_aligner_params_t *p) {
+    if (!a || !p) return SNAPGPU_EINVAL;
+    *p = a->p;
+    return SNAPGPU_OK;
+}
 int snapgpu_aligner_set_overlap(snapgpu_aligner_t *a, int overlap) {
     if (!a) return SNAPGPU_EINVAL;
     a->overlapKernels = overlap != 0;

@@ -99,6 +99,24 @@ inline int baseValue(char c) {
 // (HashTable.h:74-105).  Returns pointer to value1 or nullptr; adds probes.
 const uint32_t *lookupSlot(const Index &idx, uint32_t table, uint32_t key, uint32_t *nProbes);
 
+// One SAM line of a read without mate (SAMFormat::writeRead, SAM.cpp:1007-1155; sam.cpp).
+struct SamLine {
+    const char *id = nullptr;
+    uint32_t idLen = 0;
+    const char *bases = nullptr, *quals = nullptr;   // the unclipped read
+    uint32_t fullLen = 0, front = 0, clippedLen = 0;  // unclipped length, front clip, clipped length
+    int result = 0;                                   // AlignmentResult written
+    uint32_t loc = kInvalidLocation;                  // writeRead's genomeLocation
+    int dir = 0;
+    int mapq = 0;
+    int32_t ed = -1;                                  // NM (the CIGAR's edit distance), -1 = "*"
+    const uint32_t *ops = nullptr;                    // BAM ops of the CIGAR, or
+    uint32_t nOps = 0;
+    const std::string *cigar = nullptr;               // a complete CIGAR (transcriptome records)
+    const char *rg = nullptr;
+};
+void samAppendLine(std::string &o, const Genome &g, const SamLine &L);
+
 // xoshiro256** seeded with splitmix64: deterministic on every host.
 struct Rng {
     uint64_t s[4];

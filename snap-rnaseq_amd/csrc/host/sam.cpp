@@ -73,20 +73,40 @@ struct Job {
 };
 
 void formatOne(const Job &J, uint64_t i, std::string &o) {
-    static const char kOp[] = "MIDNSHP=X";
-    const Genome &g = *J.idx->genome;
     const snapgpu_result_t &r = J.res[i];
+    SamLine L;
+    L.id = J.ids + J.idOffsets[i];
+    L.idLen = J.idLengths[i];
     // SEQ / QUAL are the unclipped read (getSAMData, SAM.cpp:866-883); offsets/lengths are the
     // clipped read the aligner saw (Read::clip, Read.h:357-404)
-    const uint32_t front = J.front ? J.front[i] : 0u;
-    const uint32_t clippedLen = J.reads->lengths[i];
-    const uint32_t len = J.unclipped ? J.unclipped[i] : clippedLen;
-    const char *bases = J.reads->bases + J.reads->offsets[i] - front;
-    const char *quals = J.reads->quals + J.reads->offsets[i] - front;
+    L.front = J.front ? J.front[i] : 0u;
+    L.clippedLen = J.reads->lengths[i];
+    L.fullLen = J.unclipped ? J.unclipped[i] : L.clippedLen;
+    L.bases = J.reads->bases + J.reads->offsets[i] - L.front;
+    L.quals = J.reads->quals + J.reads->offsets[i] - L.front;
+    L.result = r.result;
+    L.loc = r.location;
+    L.dir = r.direction;
+    L.mapq = r.mapq;
+    L.ed = J.ed[i];
+    L.ops = J.ops + i * SNAPGPU_CIGAR_MAX_OPS;
+    L.nOps = J.nOps[i];
+    L.rg = J.rg;
+    samAppendLine(o, *J.idx->genome, L);
+}
+
+}  // namespace
+
+namespace snapgpu {
+
+// One SAMFormat::writeRead line (SAM.cpp:1007-1155 with getSAMData, :804-975) for a read
+// without mate.
+void samAppendLine(std::string &o, const Genome &g, const SamLine &L) {
+    static const char kOp[] = "MIDNSHP=X";
     // getSAMData: NotFound -> unmapped, unmapped -> forward
-    uint32_t loc = r.location;
-    if (r.result == SNAPGPU_NOT_FOUND) loc = kInvalidLocation;
-    const int rc = loc != kInvalidLocation && r.direction == SNAPGPU_RC;
+    uint32_t loc = L.loc;
+    if (L.result == SNAPGPU_NOT_FOUND) loc = kInvalidLocation;
+    const int rc = loc != kInvalidLocation && L.dir == SNAPGPU_RC;
     int flags = 0, mapq = 0;
     const char *pieceName = "*";
     uint32_t pos = 0;
@@ -97,15 +117,14 @@ void formatOne(const Job &J, uint64_t i, std::string &o) {
             pieceName = g.pieceNames[p].c_str();
             pos = loc - g.pieceOffsets[p] + 1;
         }
-        mapq = std::max(0, std::min(70, (int)r.mapq));
+        mapq = std::max(0, std::min(70, L.mapq));
     } else {
         flags |= SAM_UNMAPPED;
     }
     // QNAME: truncated at the first space (SAM.cpp:1080-1086)
-    const char *id = J.ids + J.idOffsets[i];
-    uint32_t qlen = J.idLengths[i];
-    if (const void *sp = memchr(id, ' ', qlen)) qlen = (uint32_t)((const char *)sp - id);
-    o.append(id, qlen);
+    uint32_t qlen = L.idLen;
+    if (const void *sp = memchr(L.id, ' ', qlen)) qlen = (uint32_t)((const char *)sp - L.id);
+    o.append(L.id, qlen);
     o += '\t';
     appendInt(o, flags);
     o += '\t';
@@ -115,18 +134,19 @@ void formatOne(const Job &J, uint64_t i, std::string &o) {
     o += '\t';
     appendInt(o, mapq);
     o += '\t';
-    // CIGAR: computed at writeRead's own location (even for NotFound) -- SAM.cpp:1041-1048
-    const int32_t ed = r.location != kInvalidLocation ? J.ed[i] : -1;
-    if (r.location != kInvalidLocation && ed >= 0) {
+    // CIGAR: computed at writeRead's own location (even for NotFound) -- SAM.cpp:1041-1066
+    const int32_t ed = L.loc != kInvalidLocation ? L.ed : -1;
+    if (L.loc != kInvalidLocation && L.cigar) {
+        o += *L.cigar;   // transcriptome record: insertSpliceJunctions output (may be empty)
+    } else if (L.loc != kInvalidLocation && ed >= 0) {
         // soft clips around the CIGAR (computeCigarString, SAM.cpp:1212-1226); for RC the
         // clipped-before count is the read's back clip (getSAMData, SAM.cpp:870-872)
-        const uint32_t back = len - clippedLen - front;
-        const uint32_t before = rc ? back : front, after = rc ? front : back;
+        const uint32_t back = L.fullLen - L.clippedLen - L.front;
+        const uint32_t before = rc ? back : L.front, after = rc ? L.front : back;
         if (before) { appendUint(o, before); o += 'S'; }
-        const uint32_t *op = J.ops + i * SNAPGPU_CIGAR_MAX_OPS;
-        for (uint32_t k = 0; k < J.nOps[i]; k++) {
-            appendUint(o, op[k] >> 4);
-            o += kOp[op[k] & 15];
+        for (uint32_t k = 0; k < L.nOps; k++) {
+            appendUint(o, L.ops[k] >> 4);
+            o += kOp[L.ops[k] & 15];
         }
         if (after) { appendUint(o, after); o += 'S'; }
     } else {
@@ -136,27 +156,31 @@ void formatOne(const Job &J, uint64_t i, std::string &o) {
     // (COMPLEMENT[] of a non-ACGTN base is 0; a quality string shorter than the read)
     o += "\t*\t0\t0\t";
     char sq[2 * 1024];
-    const uint32_t L = len < 1024 ? len : 1024;
+    const uint32_t len = L.fullLen;
+    const uint32_t n = len < 1024 ? len : 1024;
     uint32_t ns = 0, nq = 0;
     if (rc) {
-        while (ns < L && (sq[ns] = complement(upperCase(bases[len - 1 - ns]))) != 0) ns++;
-        while (nq < L && (sq[1024 + nq] = quals[len - 1 - nq]) != 0) nq++;
+        while (ns < n && (sq[ns] = complement(upperCase(L.bases[len - 1 - ns]))) != 0) ns++;
+        while (nq < n && (sq[1024 + nq] = L.quals[len - 1 - nq]) != 0) nq++;
     } else {
-        while (ns < L && (sq[ns] = upperCase(bases[ns])) != 0) ns++;
-        while (nq < L && (sq[1024 + nq] = quals[nq]) != 0) nq++;
+        while (ns < n && (sq[ns] = upperCase(L.bases[ns])) != 0) ns++;
+        while (nq < n && (sq[1024 + nq] = L.quals[nq]) != 0) nq++;
     }
     o.append(sq, ns);
     o += '\t';
     o.append(sq + 1024, nq);
-    if (J.rg) {
+    if (L.rg) {
         o += "\tRG:Z:";
-        o += J.rg;
+        o += L.rg;
     }
     o += "\tPG:Z:SNAP\tNM:i:";
     appendInt(o, ed);
     o += '\n';
 }
 
+}  // namespace snapgpu
+
+namespace {
 }  // namespace
 
 extern "C" int snapgpu_sam_format_clipped(const snapgpu_index_t *idx, const snapgpu_reads_t *reads, const char *ids,

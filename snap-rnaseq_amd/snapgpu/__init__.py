@@ -57,7 +57,8 @@ class SnapGpuError(RuntimeError):
     pass
 
 
-_PTR_CALLS = ("genome_from_fasta", "genome_synthetic", "index_build", "index_load", "index_attach", "reads_synthetic",
+_PTR_CALLS = ("genome_from_fasta", "genome_synthetic", "index_build", "index_load", "index_attach", "gtf_load",
+              "reads_synthetic",
               "reads_from_fastq", "reads_from_arrays", "aligner_create", "reads_upload")
 
 
@@ -574,3 +575,64 @@ def lv_batch(direction, tasks, device=0, engine="byte"):
 
 def compute_mapq(pAll, pBest, score, popularSeedsSkipped):
     return lib().snapgpu_compute_mapq(pAll, pBest, score, popularSeedsSkipped)
+
+
+class Gtf:
+    """Genome annotation (SNAPLib/GTFReader: exon lines -> transcripts with introns)."""
+
+    def __init__(self, handle):
+        self._h = handle
+
+    @classmethod
+    def load(cls, path):
+        return cls(_check(lib().snapgpu_gtf_load(str(path).encode()), "gtf_load"))
+
+    def counts(self):
+        a, b, c = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        _check(lib().snapgpu_gtf_counts(self._h, C.byref(a), C.byref(b), C.byref(c)), "gtf_counts")
+        return {"features": a.value, "transcripts": b.value, "genes": c.value}
+
+    def write_transcriptome(self, genome, path):
+        """GTFReader::BuildTranscriptome: the transcriptome FASTA `snap-rna transcriptome` indexes.
+        genome: a Genome or a raw genome handle (GenomeIndex.genome_handle())."""
+        g = genome._h if isinstance(genome, Genome) else genome
+        _check(lib().snapgpu_gtf_write_transcriptome(self._h, g, str(path).encode()), "gtf_write_transcriptome")
+
+    def genomic_position(self, transcript_id, pos, span):
+        out = C.c_uint32()
+        _check(lib().snapgpu_gtf_genomic_position(self._h, transcript_id.encode(), pos, span, C.byref(out)),
+               "gtf_genomic_position")
+        return out.value
+
+    def splice_cigar(self, transcript_id, pos, tokens):
+        """insertSpliceJunctions over [(count, op), ...] -> CIGAR string."""
+        counts = (C.c_uint32 * max(1, len(tokens)))(*[int(c) for c, _ in tokens])
+        ops = "".join(o for _, o in tokens).encode()
+        used = C.c_uint64()
+        buf = C.create_string_buffer(4096)
+        _check(lib().snapgpu_gtf_splice_cigar(self._h, transcript_id.encode(), pos, len(tokens), counts, ops, buf,
+                                              4096, C.byref(used)), "gtf_splice_cigar")
+        return buf.value.decode()
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().snapgpu_gtf_free(self._h)
+            self._h = None
+
+
+def single_options(**kw):
+    o = _ffi.SingleOptions()
+    lib().snapgpu_single_options_default(C.byref(o))
+    for k, v in kw.items():
+        setattr(o, k, v.encode() if isinstance(v, str) else v)
+    return o
+
+
+def single_align(genome_aligner, transcriptome_aligner, gtf, reads, sam_path, **options):
+    """`snap-rna single` (SingleAligner.cpp:141-320) over a FASTQ batch, both AlignRead calls and
+    the CIGARs on the GPU; writes sam_path.  options: SingleOptions fields.  -> stats dict."""
+    o = single_options(**options)
+    st = _ffi.SingleStats()
+    _check(lib().snapgpu_single_align(genome_aligner._h, transcriptome_aligner._h, gtf._h, reads._p, C.byref(o),
+                                      str(sam_path).encode(), C.byref(st)), "single_align")
+    return {f: getattr(st, f) for f, _ in st._fields_}

@@ -148,6 +148,28 @@ class Timing(C.Structure):
     ]
 
 
+class SingleOptions(C.Structure):
+    _fields_ = [
+        ("clipping", C.c_int32),
+        ("confDiff", C.c_uint32),
+        ("maxDist", C.c_uint32),
+        ("minPercentAbovePhred", C.c_float),
+        ("minPhred", C.c_uint32),
+        ("phredOffset", C.c_uint32),
+        ("useM", C.c_uint32),
+        ("reserved", C.c_uint32),
+        ("readGroup", C.c_char_p),
+        ("commandLine", C.c_char_p),
+        ("version", C.c_char_p),
+    ]
+
+
+class SingleStats(C.Structure):
+    _fields_ = [(f, C.c_uint64) for f in ("totalReads", "usefulReads", "singleHits", "multiHits", "notFound",
+                                          "transcriptomeRecords")] + \
+               [(f, C.c_double) for f in ("alignMs", "cigarMs", "filterMs", "writeMs", "wallMs")]
+
+
 class AlignerStats(C.Structure):
     _fields_ = [
         ("nHashTableLookups", C.c_int64),
@@ -237,6 +259,22 @@ _PROTOS = [
     ("snapgpu_sam_format", C.c_int, [C.c_void_p, C.POINTER(Reads), C.c_char_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                      C.c_void_p, C.c_void_p, C.c_void_p, C.c_char_p, C.c_void_p, C.c_uint64,
                                      C.POINTER(C.c_uint64)]),
+]
+
+_PROTOS += [
+    ("snapgpu_gtf_load", C.c_void_p, [C.c_char_p]),
+    ("snapgpu_gtf_free", None, [C.c_void_p]),
+    ("snapgpu_gtf_counts", C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+    ("snapgpu_gtf_write_transcriptome", C.c_int, [C.c_void_p, C.c_void_p, C.c_char_p]),
+    ("snapgpu_gtf_genomic_position", C.c_int, [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32,
+                                               C.POINTER(C.c_uint32)]),
+    ("snapgpu_gtf_splice_cigar", C.c_int, [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_char_p,
+                                           C.c_char_p, C.c_uint64, C.POINTER(C.c_uint64)]),
+    ("snapgpu_single_options_default", None, [C.POINTER(SingleOptions)]),
+    ("snapgpu_single_align", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(Reads), C.POINTER(SingleOptions),
+                                       C.c_char_p, C.POINTER(SingleStats)]),
+    ("snapgpu_aligner_index", C.c_void_p, [C.c_void_p]),
+    ("snapgpu_aligner_get_params", C.c_int, [C.c_void_p, C.POINTER(AlignerParams)]),
 ]
 
 CIGAR_MAX_OPS = 64   # SNAPGPU_CIGAR_MAX_OPS

@@ -12,6 +12,7 @@ TSV/JSON expected outputs.
     python3 tests/golden/make_golden.py --only-multihit  # windowed search / multi-hit runs only
     python3 tests/golden/make_golden.py --only-cigar     # CIGAR calls + SAM records only
     python3 tests/golden/make_golden.py --only-refindex  # reference-built index + seedLen fixtures
+    python3 tests/golden/make_golden.py --only-single    # `snap-rna single` end-to-end SAM fixtures
 """
 import hashlib
 import json
@@ -217,8 +218,123 @@ def refindex_fixtures(work):
             f.write(ref_align(d, fq, PARAM_SETS["default"]))
 
 
+def small_gtf(path, seqs, rng):
+    """Genes on small.fa: 2-5 exons, alternative transcripts that skip exons (shared exons and
+    introns), an exon abutting the next (zero-length intron), a transcript on a chromosome the
+    genome lacks (skipped by BuildTranscriptome), and non-exon lines (ignored by Parse)."""
+    lines = ["#!genome-build synthetic", "#!annotation for tests/golden/small.fa"]
+    chrs = list(seqs)
+    for g in range(12):
+        c = chrs[g % len(chrs)]
+        L = len(seqs[c])
+        p = rng.randrange(2000, L - 30000)
+        exons = []
+        for e in range(rng.randrange(2, 6)):
+            ln = rng.randrange(60, 400)
+            exons.append((p, p + ln - 1))
+            p += ln + (0 if (g == 3 and e == 0) else rng.randrange(150, 2500))
+        lines.append(f'{c}\tsrc\tgene\t{exons[0][0]}\t{exons[-1][1]}\t.\t+\t.\tgene_id "G{g}"; gene_name "GENE{g}";')
+        for t in range(rng.randrange(1, 4)):
+            use = exons if t == 0 else [x for k, x in enumerate(exons) if k == 0 or k == len(exons) - 1 or rng.random() < 0.5]
+            for a, b in use:
+                lines.append(f'{c}\tsrc\texon\t{a}\t{b}\t.\t{"+-"[g % 2]}\t.\tgene_id "G{g}"; transcript_id "T{g}.{t}"; '
+                             f'gene_name "GENE{g}"; transcript_name "GENE{g}-{t}";')
+    lines.append('chrUn\tsrc\texon\t100\t400\t.\t+\t.\tgene_id "GX"; transcript_id "TX.0";')
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    return lines
+
+
+def single_reads(path, seqs, gtf_lines, rng):
+    """Reads for the end-to-end run: from transcript pre-mRNA spans (the transcriptome the
+    reference builds) around exon/intron boundaries, from anywhere in the genome, both strands;
+    '#' runs at the ends (clipping), low-quality reads, N-rich reads, short reads, random reads."""
+    comp = str.maketrans("ACGTN", "TGCAN")
+    ex = [l.split("\t") for l in gtf_lines if "\texon\t" in l and not l.startswith("chrUn")]
+    reads = []
+    for i in range(1200):
+        u = rng.random()
+        if u < 0.55:
+            f = rng.choice(ex)
+            c, a, b = f[0], int(f[3]), int(f[4])
+            pos = rng.randrange(max(0, a - 160), b + 60) - 1
+        elif u < 0.95:
+            c = rng.choice(list(seqs))
+            pos = rng.randrange(0, len(seqs[c]) - 200)
+        else:
+            c, pos = None, 0
+        L = rng.choice([100, 100, 100, 101, 120, 75, 60, 45])
+        s = "".join(rng.choice("ACGT") for _ in range(L)) if c is None else seqs[c][pos:pos + L]
+        s = list(s)
+        for _ in range(rng.choice([0, 0, 1, 2, 3, 6])):
+            s[rng.randrange(len(s))] = rng.choice("ACGT")
+        if rng.random() < 0.05:
+            j = rng.randrange(5, len(s) - 5)
+            s = s[:j] + s[j + rng.randrange(1, 4):] if rng.random() < 0.5 else s[:j] + list("ACG"[:rng.randrange(1, 4)]) + s[j:]
+        s = "".join(s)
+        if rng.random() < 0.5:
+            s = s.translate(comp)[::-1]
+        q = ["I"] * len(s)
+        r = rng.random()
+        if r < 0.08:
+            q = [rng.choice("#%+5") for _ in s]
+        elif r < 0.25:
+            for j in range(rng.randrange(1, 12)):
+                q[-1 - j] = "#"
+            for j in range(rng.randrange(0, 5)):
+                q[j] = "#"
+        elif r < 0.3:
+            q = [rng.choice("I?5") for _ in s]
+        if rng.random() < 0.03:
+            s = "".join("N" if rng.random() < 0.25 else ch for ch in s)
+        reads.append((f"sr{i} len={len(s)}", s, "".join(q)))
+    with open(path, "w") as f:
+        for n, s, q in reads:
+            f.write(f"@{n}\n{s}\n+\n{q}\n")
+
+
+def single_fixtures(work):
+    """`snap-rna single <genome> <transcriptome> <gtf> <reads> -t 1 -o out.sam` (the product
+    path, SingleAligner.cpp:141-320), default options and -M; plus the reference's
+    transcriptome FASTA (GTFReader::BuildTranscriptome) for the same GTF."""
+    import gzip
+    rng = random.Random(41)
+    fa = os.path.join(HERE, "small.fa")
+    seqs, name = {}, None
+    for line in open(fa):
+        line = line.strip()
+        if line.startswith(">"):
+            name = line[1:].split()[0]
+            seqs[name] = []
+        else:
+            seqs[name].append(line.upper())
+    seqs = {k: "".join(v) for k, v in seqs.items()}
+    gtf = os.path.join(HERE, "small.gtf")
+    lines = small_gtf(gtf, seqs, rng)
+    fq = os.path.join(HERE, "single_reads.fq")
+    single_reads(fq, seqs, lines, rng)
+    gidx = os.path.join(work, "gidx")
+    ref_index(fa, gidx)
+    twd = os.path.join(work, "tx")
+    os.makedirs(twd, exist_ok=True)
+    run([SNAP, "transcriptome", gtf, fa, "tidx", "-O1000"], cwd=twd)
+    with open(os.path.join(twd, "transcriptome.fa"), "rb") as src, \
+            open(os.path.join(HERE, "expected_transcriptome.fa.gz"), "wb") as dst:
+        dst.write(gzip.compress(src.read(), compresslevel=9, mtime=0))
+    for tag, extra in (("", []), ("_M", ["-M"])):
+        out = os.path.join(work, f"out{tag}.sam")
+        run([SNAP, "single", gidx, os.path.join(twd, "tidx"), gtf, fq, "-t", "1", "-o", out] + extra, cwd=work)
+        with open(out, "rb") as src, open(os.path.join(HERE, f"expected_single{tag}.sam.gz"), "wb") as dst:
+            dst.write(gzip.compress(src.read(), compresslevel=9, mtime=0))
+
+
 def main():
     work = tempfile.mkdtemp(prefix="golden_")
+    if "--only-single" in sys.argv:
+        single_fixtures(work)
+        shutil.rmtree(work, ignore_errors=True)
+        print("single-end product path fixtures written to", HERE)
+        return
     if "--only-refindex" in sys.argv:
         refindex_fixtures(work)
         shutil.rmtree(work, ignore_errors=True)
@@ -254,6 +370,7 @@ def main():
     multihit_fixtures(work)
     cigar_fixtures(work)
     refindex_fixtures(work)
+    single_fixtures(work)
 
     # 2. lookupSeed golden: seeds from the genome, their RCs, mutated and random seeds
     rng = random.Random(9)

@@ -1,0 +1,75 @@
+"""The single-end RNA product path: `snap-rna single` rebuilt on the GPU.
+
+Fixtures (tests/golden/make_golden.py --only-single) are the reference CLI's own outputs on
+tests/golden/small.fa + small.gtf + single_reads.fq: the transcriptome FASTA of
+`snap-rna transcriptome` and the SAM files of `snap-rna single ... -t 1` (default and -M).
+Our run builds both indexes itself (the GPU box has no reference), loads the GTF, and must
+write the same SAM bytes (the @PG line differs only in the command line it echoes)."""
+import gzip
+import os
+
+import pytest
+
+import snapgpu
+
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def test_gtf_model():
+    gtf = snapgpu.Gtf.load(os.path.join(G, "small.gtf"))
+    c = gtf.counts()
+    assert c["transcripts"] >= 20 and c["genes"] == 13 and c["features"] > c["transcripts"]
+    # GenomicPosition: exon coordinates only, 0 past the transcript end
+    first = [l.split("\t") for l in open(os.path.join(G, "small.gtf")) if '"T0.0"' in l]
+    a, b = int(first[0][3]), int(first[0][4])
+    assert gtf.genomic_position("T0.0", 1, 100) == a
+    assert gtf.genomic_position("T0.0", 10, 0) == a + 9
+    assert gtf.genomic_position("T0.0", 10**7, 100) == 0
+    ln = b - a + 1
+    # a match run across exon 1's end gets the intron as an N run (insertSpliceJunctions)
+    nxt = int(first[1][3])
+    cig = gtf.splice_cigar("T0.0", ln - 9, [(100, "=")])
+    assert cig == f"10={nxt - b - 1}N90="
+    assert gtf.splice_cigar("T0.0", 1, [(3, "S"), (50, "="), (2, "I"), (45, "=")]) == "3S50=2I45="
+
+
+def test_transcriptome_fasta_matches_reference(tmp_path):
+    gtf = snapgpu.Gtf.load(os.path.join(G, "small.gtf"))
+    g = snapgpu.Genome.from_fasta(os.path.join(G, "small.fa"), 500)
+    out = tmp_path / "transcriptome.fa"
+    gtf.write_transcriptome(g, out)
+    assert out.read_bytes() == gzip.open(os.path.join(G, "expected_transcriptome.fa.gz")).read()
+
+
+def _indexes(tmp_path):
+    gtf = snapgpu.Gtf.load(os.path.join(G, "small.gtf"))
+    gidx = snapgpu.GenomeIndex.build(snapgpu.Genome.from_fasta(os.path.join(G, "small.fa"), 500), 20, 4)
+    tfa = tmp_path / "transcriptome.fa"
+    gtf.write_transcriptome(gidx.genome_handle(), tfa)
+    tidx = snapgpu.GenomeIndex.build(snapgpu.Genome.from_fasta(tfa, 500), 20, 4)
+    return gtf, gidx, tidx
+
+
+def _records(text):
+    lines = text.splitlines()
+    return [l for l in lines if not l.startswith("@PG")]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("use_m,fixture", [(0, "expected_single.sam.gz"), (1, "expected_single_M.sam.gz")])
+def test_single_end_product_path_matches_reference(gpu_available, tmp_path, use_m, fixture):
+    gtf, gidx, tidx = _indexes(tmp_path)
+    ga = snapgpu.BaseAligner(gidx)
+    ta = snapgpu.BaseAligner(tidx)
+    reads = snapgpu.Reads.from_fastq(os.path.join(G, "single_reads.fq"))
+    out = tmp_path / "out.sam"
+    st = snapgpu.single_align(ga, ta, gtf, reads, out, useM=use_m, version="0.1alpha", commandLine="x")
+    got = out.read_text()
+    want = gzip.open(os.path.join(G, fixture), "rt").read()
+    g, w = _records(got), _records(want)
+    assert len(g) == len(w)
+    bad = [(a, b) for a, b in zip(g, w) if a != b]
+    assert not bad, f"{len(bad)} lines differ, first: {bad[:2]}"
+    assert st["totalReads"] == reads.n and 0 < st["usefulReads"] < reads.n
+    assert st["transcriptomeRecords"] > 50
+    assert "N" in "".join(l.split("\t")[5] for l in g if not l.startswith("@"))   # junctions exercised
