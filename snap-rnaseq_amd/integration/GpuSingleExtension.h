@@ -1,0 +1,69 @@
+// GpuSingleExtension.h -- the drop-in for SNAPLib: what a SNAPLib maintainer adds to run
+// `snap-rna single` on MI355X GPUs.  Written against the reference's own
+// headers (SNAPLib/AlignerContext.h, Aligner.h, Read.h, AlignmentFilter.h) in the reference's
+// dialect (C++98); tests/test_integration_build.py compiles and links it with the reference's
+// objects in the build container.
+//
+//  * GpuBaseAligner : Aligner -- BaseAligner::AlignRead (BaseAligner.cpp:196-200) one read at a
+//    time through snapgpu_align_batch, for any existing caller of Aligner*.
+//  * GpuSingleExtension : AlignerExtension -- the hook SingleAlignerContext::runIterationThread
+//    calls first (SingleAligner.cpp:150-153, AlignerContext.h:157): the thread's reads are taken
+//    in batches, both AlignRead calls of every read run as two GPU batches, and the unchanged
+//    host tail (the reference's AlignmentFilter, ReadWriter, stats) runs per read in input order.
+#pragma once
+
+#include "stdafx.h"
+#include "Aligner.h"
+#include "AlignerContext.h"
+#include "AlignerOptions.h"
+#include "Read.h"
+#include "snapgpu.h"
+
+class GpuBaseAligner : public Aligner {
+public:
+    // The index is the reference's on-disk index directory (snapgpu_index_load reads it).
+    GpuBaseAligner(const char *indexDir, int device, unsigned maxHits, unsigned maxK, unsigned maxReadSize,
+                   unsigned numSeeds, double seedCoverage, unsigned extraSearchDepth, bool explorePopular,
+                   bool stopOnFirst);
+    virtual ~GpuBaseAligner();
+
+    virtual AlignmentResult AlignRead(Read *read, unsigned *genomeLocation, Direction *hitDirection,
+                                      int *finalScore = NULL, int *mapq = NULL);
+    virtual _int64 getNHashTableLookups() const;
+    virtual _int64 getLocationsScored() const;
+    virtual _int64 getNHitsIgnoredBecauseOfTooHighPopularity() const;
+    virtual _int64 getNReadsIgnoredBecauseOfTooManyNs() const;
+    virtual _int64 getNIndelsMerged() const;
+    virtual void addIgnoredReads(_int64 newlyIgnoredReads);
+    virtual const char *getRCTranslationTable() const;
+    virtual int getMaxK() const;
+    virtual const char *getName() const;
+
+private:
+    snapgpu_aligner_stats_t stats() const;
+    snapgpu_index_t *idx;
+    snapgpu_aligner_t *gpu;
+    _int64 ignoredReads;
+};
+
+class GpuSingleExtension : public AlignerExtension {
+public:
+    // batchReads: reads per GPU batch; device -1 = one GPU per thread, round robin
+    GpuSingleExtension(unsigned batchReads = 1u << 20, int device = -1);
+    virtual ~GpuSingleExtension();
+
+    virtual void initialize();                 // loads both indexes once (AlignerContext.cpp:104)
+    virtual AlignerExtension *copy();          // per-thread copy (AlignerContext.cpp:141)
+    virtual void beginThread();                // GPU aligners of this thread
+    virtual void finishThread();
+    virtual bool runIterationThread(ReadSupplier *supplier, AlignerContext *ctx);
+
+private:
+    struct Shared;                             // indexes loaded once, shared by the thread copies
+    GpuSingleExtension(Shared *shared, unsigned batchReads, int device);
+    Shared *shared;
+    bool owner;
+    unsigned batchReads;
+    int device;
+    snapgpu_aligner_t *g, *t;                  // genome and transcriptome aligners of this thread
+};
