@@ -156,6 +156,8 @@ def main():
     ap.add_argument("--reads", type=int, default=None, help="reads per GPU (default: the workload's)")
     ap.add_argument("--genome-bases", type=int, default=None)
     ap.add_argument("--resident-steps", type=int, default=5)
+    ap.add_argument("--mode", choices=("stream", "sync"), default="stream",
+                    help="stream: submit every step, wait once (a streaming caller); sync: one blocking call per step")
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="reads timed on the CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip ceilings, CIGAR/SAM and parity legs")
@@ -187,21 +189,44 @@ def main():
     out = np.zeros(wl["reads"], dtype=snapgpu.RESULT_DTYPE)
     log(rank, f"{wl['reads']} reads generated")
 
+    outs = [out, np.zeros(wl["reads"], dtype=snapgpu.RESULT_DTYPE)]
     for _ in range(args.warmup):
         aligner.AlignReads(reads, out=out)
     kernel_ms, lookup_ms, launches, fix_ms, busy_ms, lk_busy_ms = [], [], [], [], [], []
 
-    def step():
-        aligner.AlignReads(reads, out=out)
-        t = aligner.timing()
-        kernel_ms.append(t["mainKernelMs"])
-        lookup_ms.append(t["lookupKernelMs"])
-        launches.append(t["nLaunches"])
-        fix_ms.append(t["fixupMs"])
-        busy_ms.append(t["mainKernelBusyMs"])
-        lk_busy_ms.append(t["lookupKernelBusyMs"])
+    def record(t, k):
+        kernel_ms.append(t["mainKernelMs"] / k)
+        lookup_ms.append(t["lookupKernelMs"] / k)
+        launches.append(t["nLaunches"] / k)
+        fix_ms.append(t["fixupMs"] / k)
+        busy_ms.append(t["mainKernelBusyMs"] / k)
+        lk_busy_ms.append(t["lookupKernelBusyMs"] / k)
 
-    elapsed = timed_steps(step, args.steps, dist, lambda: None)
+    if args.mode == "stream":
+        # a streaming caller: batch k+1 is submitted while batch k's last chunks are on the GPU
+        # (snapgpu_align_batch_submit), records land in alternating host arrays, one wait at the end
+        n_sub = [0]
+
+        def step():
+            aligner.submit(reads, outs[n_sub[0] & 1])
+            n_sub[0] += 1
+
+        def sync():
+            aligner.wait()
+            if n_sub[0]:
+                record(aligner.timing(), n_sub[0])
+                n_sub[0] = 0
+    else:
+        def step():
+            aligner.AlignReads(reads, out=out)
+            record(aligner.timing(), 1)
+
+        def sync():
+            pass
+
+    elapsed = timed_steps(step, args.steps, dist, sync)
+    if args.mode == "stream":
+        assert np.array_equal(outs[0].view(np.uint8), outs[1].view(np.uint8))
     log(rank, f"timed {args.steps} steps: {elapsed:.3f}s")
     res = out
     total_reads = wl["reads"] * world * args.steps
@@ -367,7 +392,11 @@ def main():
                 "extraSearchDepth": 2,
                 "parallelism": f"reads sharded over {world} GPU(s), index built once per node and replicated",
                 "boundary": "host reads in (pinned) -> host records out: H2D, passes, D2H, MAPQ fix-ups "
-                            "(snapgpu_align_batch, chunks pipelined over 2 HIP streams)",
+                            "(chunks pipelined over 2 HIP streams; " + (
+                                "mode stream: snapgpu_align_batch_submit per step, one snapgpu_align_batch_wait, "
+                                "records alternate between two host arrays)" if args.mode == "stream" else
+                                "mode sync: one blocking snapgpu_align_batch per step)"),
+                "mode": args.mode,
                 "results": {"SingleHit": counts.get(1, 0), "MultipleHits": counts.get(2, 0),
                             "NotFound": counts.get(0, 0)},
                 "per_read": {k: round(float(v), 2) for k, v in per_read.items()},

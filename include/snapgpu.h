@@ -259,6 +259,14 @@ void snapgpu_aligner_free(snapgpu_aligner_t *a);
  * buffers: H2D of the reads, the GPU passes, D2H of the records. */
 int snapgpu_align_batch(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, snapgpu_result_t *out);
 
+/* Streaming form of snapgpu_align_batch for callers that keep several batches in flight (the
+ * GpuSingleExtension pattern): submit returns once the batch is queued (its last chunks still
+ * on the GPU; earlier batches' chunks are finished as their streams are reused); wait drains
+ * everything submitted.  reads and out must stay valid, and out untouched, until the wait.
+ * snapgpu_last_timing then covers every batch since the previous wait. */
+int snapgpu_align_batch_submit(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, snapgpu_result_t *out);
+int snapgpu_align_batch_wait(snapgpu_aligner_t *a);
+
 /* The extended AlignRead (BaseAligner.h:72-86, BaseAligner.cpp:510-938) used by the
  * paired / transcriptome callers:
  *  - per-read search window: searchRadius != 0 restricts hits to genome locations

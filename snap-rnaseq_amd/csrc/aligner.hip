@@ -893,6 +893,7 @@ struct ExecLane {
     unsigned long long *hLookupStats = nullptr; // pinned copy of lookupStats
     bool pending = false;
     uint64_t chunkBegin = 0, chunkN = 0, chunkEv = 0;
+    snapgpu_result_t *chunkOut = nullptr;       // the caller's record array of the pending chunk
 };
 
 // Timing events of one pass set (one chunk) and the pinned copy of its work counters.
@@ -934,6 +935,11 @@ struct snapgpu_aligner {
     // them one after the other (copies and host tails still overlap).  With overlap, launch
     // durations overlap too: snapgpu_timing_t also carries the union of the launch intervals.
     bool overlapKernels = true;
+    // snapgpu_align_batch_submit: chunks of consecutive batches stream through the lanes until
+    // snapgpu_align_batch_wait; timing and statistics cover that whole stream
+    bool streamOpen = false;
+    uint64_t nextLane = 0;
+    std::chrono::steady_clock::time_point streamStart;
     uint64_t arenaElems = 0;
     int grid = 0, grid512 = 0;
     uint64_t chunkReads = 262144; // snapgpu_align_batch chunk (SNAPGPU_CHUNK_READS)
@@ -1486,11 +1492,15 @@ static int accountEvSet(snapgpu_aligner_t *a, const EvSet &v) {
 // Device-resident reads: the same chunk-sized pass sets as snapgpu_align_batch, alternating
 // over the two lanes, on sub-ranges of the resident buffers (no copies).  The extended path
 // (windowed search / multi-hit scratch per block) runs as one pass set on lane 0.
+int snapgpu_align_batch_wait(snapgpu_aligner_t *a);
+
 static int launch_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, const AlignExt &x) {
     if (!a || !d) return SNAPGPU_EINVAL;
     if (a->failed) { snapgpu::setError("aligner failed earlier (device timeout)"); return SNAPGPU_EDEVICE; }
     HIPCHK(hipSetDevice(a->device));
-    int rc = beginCall(a);
+    int rc = snapgpu_align_batch_wait(a);   // no submitted batch may still use the lanes
+    if (rc) return rc;
+    rc = beginCall(a);
     if (rc) return rc;
     const bool ext = x.search || x.maxHitsToGet;
     const uint64_t n = d->n;
@@ -1621,8 +1631,9 @@ static int ensureLaneCapacity(snapgpu_aligner_t *a, ExecLane &L, uint64_t reads,
 // The host tail of one chunk: wait for its records, account its kernel times, then MAPQ
 // fix-ups, statistics and the copy into the caller's array (host threads, while the GPU
 // already runs the next chunks).
-static int finishChunk(snapgpu_aligner_t *a, ExecLane &L, snapgpu_result_t *out) {
+static int finishChunk(snapgpu_aligner_t *a, ExecLane &L) {
     if (!L.pending) return SNAPGPU_OK;
+    snapgpu_result_t *out = L.chunkOut;
     L.pending = false;
     int rc = waitEvent(a, L.done);
     if (rc) return rc;
@@ -1670,14 +1681,21 @@ static int finishChunk(snapgpu_aligner_t *a, ExecLane &L, snapgpu_result_t *out)
 // Batched BaseAligner::AlignRead over host buffers (SURVEY.md 8(d) d1 boundary): the reads are
 // cut into chunks that alternate over the two execution lanes -- H2D of the chunk's bytes,
 // offsets and lengths, the three passes, D2H of its records into pinned staging -- and the
-// host tail of chunk c-2 runs while chunks c-1 and c are on the GPU.
-int snapgpu_align_batch(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, snapgpu_result_t *out) {
+// host tail of chunk c-2 runs while chunks c-1 and c are on the GPU.  Submitting returns with
+// the last two chunks in flight; the next submit continues the same pipeline (its first chunks
+// overlap this batch's last kernels) and snapgpu_align_batch_wait drains it.
+int snapgpu_align_batch_submit(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, snapgpu_result_t *out) {
     if (!a || !reads || !out) return SNAPGPU_EINVAL;
     if (a->failed) { snapgpu::setError("aligner failed earlier (device timeout)"); return SNAPGPU_EDEVICE; }
     HIPCHK(hipSetDevice(a->device));
-    const auto w0 = std::chrono::steady_clock::now();
+    int rc = SNAPGPU_OK;
+    if (!a->streamOpen) {
+        if (a->pendingTiming && (rc = snapgpu_synchronize(a))) return rc;   // a resident run still queued
+        if ((rc = beginCall(a))) return rc;
+        a->streamOpen = true;
+        a->streamStart = std::chrono::steady_clock::now();
+    }
     const uint64_t n = reads->n;
-    a->timing = snapgpu_timing_t{};
     if (n == 0) return SNAPGPU_OK;
     const uint64_t nChunks = (n + a->chunkReads - 1) / a->chunkReads;
     const uint64_t per = (n + nChunks - 1) / nChunks;
@@ -1693,15 +1711,14 @@ int snapgpu_align_batch(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, snap
         maxSpan = std::max(maxSpan, hi[c] - lo[c]);
     }
     const uint64_t hostEnd = reads->totalBytes + 64;   // allocated and zeroed past the last read
-    for (auto &L : a->lane) {
-        const int rc = ensureLaneCapacity(a, L, std::min(per, n), maxSpan + 64);
-        if (rc) return rc;
-    }
-    int rc = beginCall(a);
-    if (rc) return rc;
+    for (auto &L : a->lane)
+        if (std::min(per, n) > L.capReads || maxSpan + 64 > L.capBytes) {   // grow: its pending chunk first
+            if ((rc = finishChunk(a, L)) || (rc = ensureLaneCapacity(a, L, std::min(per, n), maxSpan + 64))) return rc;
+        }
     for (uint64_t c = 0; c < nChunks && rc == SNAPGPU_OK; c++) {
-        ExecLane &L = a->lane[c & 1];
-        if ((rc = finishChunk(a, L, out))) break;   // chunk c-2: its buffers are free again
+        const int li = (int)(a->nextLane++ & 1);
+        ExecLane &L = a->lane[li];
+        if ((rc = finishChunk(a, L))) break;   // the lane's previous chunk: its buffers are free again
         const uint64_t b = c * per, m = std::min(n, b + per) - b;
         for (uint64_t i = 0; i < m; i++) {
             L.hOffsets[i] = reads->offsets[b + i] - lo[c];
@@ -1716,30 +1733,52 @@ int snapgpu_align_batch(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, snap
         PassIO io{L.dBases, L.dQuals, L.dOffsets, L.dLengths, m, L.dOut, L.dDefer, L.dSeeds};
         EvSet *ev = nextEvSet(a);
         if (!ev) { rc = SNAPGPU_EDEVICE; break; }
-        if ((rc = launch_passes(a, (int)(c & 1), io, AlignExt(), *ev, c ? &a->evs[a->nEvUsed - 2] : nullptr))) break;
+        if ((rc = launch_passes(a, li, io, AlignExt(), *ev, a->nEvUsed >= 2 ? &a->evs[a->nEvUsed - 2] : nullptr))) break;
         HIPCHK(hipMemcpyAsync(L.hOut, L.dOut, m * sizeof(snapgpu_result_t), hipMemcpyDeviceToHost, s));
         HIPCHK(hipEventRecord(L.done, s));
         L.pending = true;
         L.chunkBegin = b;
         L.chunkN = m;
         L.chunkEv = a->nEvUsed - 1;
+        L.chunkOut = out;
     }
-    // the older pending chunk first (chunk nChunks-2 is on lane (nChunks-2)&1)
-    for (uint64_t k = 0; k < 2 && rc == SNAPGPU_OK; k++) rc = finishChunk(a, a->lane[(nChunks + k) & 1], out);
     if (rc) {   // leave no chunk in flight on these buffers (unless a timeout made that impossible)
+        for (auto &L : a->lane) { L.pending = false; if (!a->failed) waitLane(a, L); }
+        a->streamOpen = false;
+    }
+    return rc;
+}
+
+int snapgpu_align_batch_wait(snapgpu_aligner_t *a) {
+    if (!a) return SNAPGPU_EINVAL;
+    if (!a->streamOpen) return a->failed ? SNAPGPU_EDEVICE : SNAPGPU_OK;
+    HIPCHK(hipSetDevice(a->device));
+    int rc = SNAPGPU_OK;
+    // the older pending chunk first: the next chunk would go to lane nextLane & 1
+    for (uint64_t k = 0; k < 2 && rc == SNAPGPU_OK; k++) rc = finishChunk(a, a->lane[(a->nextLane + k) & 1]);
+    a->streamOpen = false;
+    if (rc) {
         for (auto &L : a->lane) { L.pending = false; if (!a->failed) waitLane(a, L); }
         return rc;
     }
     accountBusy(a);
-    for (auto &L : a->lane) {   // lookup statistics of the whole call
+    for (auto &L : a->lane) {   // lookup statistics of the whole stream
         HIPCHK(hipMemcpy(L.hLookupStats, L.lookupStats, 1024 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
         addLookupStats(a->timing, L.hLookupStats);
     }
     rc = checkWatchdog(a);
     a->lastReads = nullptr;
     a->pendingTiming = false;
-    a->timing.wallMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
+    a->timing.wallMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a->streamStart).count();
     return rc;
+}
+
+int snapgpu_align_batch(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, snapgpu_result_t *out) {
+    if (!a || !reads || !out) return SNAPGPU_EINVAL;
+    int rc = snapgpu_align_batch_wait(a);   // a stream the caller left open
+    if (rc) return rc;
+    if ((rc = snapgpu_align_batch_submit(a, reads, out))) return rc;
+    return snapgpu_align_batch_wait(a);
 }
 
 int snapgpu_align_batch_ex(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, const snapgpu_search_t *search,

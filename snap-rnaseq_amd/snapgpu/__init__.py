@@ -328,6 +328,19 @@ class BaseAligner:
                    "align_batch")
         return out[:n]
 
+    def submit(self, reads, out):
+        """Queue a batch (snapgpu_align_batch_submit); `reads` and `out` stay owned by the caller
+        and must not change until wait()."""
+        if out.dtype != RESULT_DTYPE or len(out) < reads.n or not out.flags.c_contiguous:
+            raise ValueError("out must be a C-contiguous RESULT_DTYPE array of at least reads.n records")
+        if reads.n:
+            _check(lib().snapgpu_align_batch_submit(self._h, reads._p, out.ctypes.data_as(C.POINTER(_ffi.Result))),
+                   "align_batch_submit")
+
+    def wait(self):
+        """Finish every submitted batch (snapgpu_align_batch_wait)."""
+        _check(lib().snapgpu_align_batch_wait(self._h), "align_batch_wait")
+
     def AlignReadsEx(self, reads, search=None, maxHitsToGet=0):
         """Batched form of the richer AlignRead (BaseAligner.h:73-86): per-read search
         windows (see search_array) and up to maxHitsToGet multi-hits per read.

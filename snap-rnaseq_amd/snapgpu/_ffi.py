@@ -220,6 +220,8 @@ _PROTOS = [
     ("snapgpu_aligner_create", C.c_void_p, [C.c_int, C.c_void_p, C.POINTER(AlignerParams)]),
     ("snapgpu_aligner_free", None, [C.c_void_p]),
     ("snapgpu_align_batch", C.c_int, [C.c_void_p, C.POINTER(Reads), C.POINTER(Result)]),
+    ("snapgpu_align_batch_submit", C.c_int, [C.c_void_p, C.POINTER(Reads), C.POINTER(Result)]),
+    ("snapgpu_align_batch_wait", C.c_int, [C.c_void_p]),
     ("snapgpu_align_batch_ex", C.c_int, [C.c_void_p, C.POINTER(Reads), C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
                                          C.c_void_p]),
     ("snapgpu_reads_upload", C.c_void_p, [C.c_void_p, C.POINTER(Reads)]),

@@ -130,3 +130,31 @@ def test_getters_aggregate(gpu_available, small_world):
     assert al.getNHashTableLookups() == int(res["nLookups"].sum())
     assert al.getLocationsScored() == int(res["nLocationsScored"].sum())
     assert al.getMaxK() == 14
+
+
+def test_stream_submit_wait(gpu_available, small_world, monkeypatch):
+    """snapgpu_align_batch_submit / _wait: batches of different sizes (several chunks, one
+    read, a one-chunk batch) stream through the two lanes before one wait; every record equals
+    the blocking call's, and a resident run closes an open stream first."""
+    idx, reads = small_world["index"], small_world["reads"]
+    monkeypatch.setenv("SNAPGPU_CHUNK_READS", "700")   # several chunks per batch, lanes alternate across batches
+    al = snapgpu.BaseAligner(idx)
+    want = al.AlignReads(reads)
+    cuts = [(0, 2500), (2500, 1), (2501, 600), (3101, reads.n - 3101)]
+    parts = [reads.slice(s, c) for s, c in cuts]
+    outs = [np.zeros(p.n, dtype=snapgpu.RESULT_DTYPE) for p in parts]
+    for p, o in zip(parts, outs):
+        al.submit(p, o)
+    al.wait()
+    got = np.concatenate(outs)
+    assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
+    t = al.timing()
+    assert t["nLaunches"] == 4 + 1 + 1 + 2   # every chunk of the whole stream (700 reads a chunk)
+    # submit, then a resident run without an explicit wait
+    o2 = np.zeros(parts[0].n, dtype=snapgpu.RESULT_DTYPE)
+    al.submit(parts[0], o2)
+    dev = al.upload(parts[2])
+    dev.run()
+    assert np.array_equal(dev.results().view(np.uint8), want[2501:3101].view(np.uint8))
+    assert np.array_equal(o2.view(np.uint8), want[:2500].view(np.uint8))
+    al.wait()   # nothing left: a no-op
