@@ -257,7 +257,9 @@ struct Lds {
             uint32_t scrLoc[WAVE];                  // batch scratch: hit location per lane
         } ins;
         struct {
-            uint8_t rows8[BYTE_PATH ? 1 : MAX_K][WAVE];   // LV rows (L + 2 per row, lane); actions recomputed
+            // LV rows (L + 2 per row, lane; actions recomputed); between passes, the staged
+            // selection keys of the forced-mode ranking
+            alignas(16) uint8_t rows8[BYTE_PATH ? 1 : MAX_K][WAVE];
             uint16_t order[ORDCAP];                 // forced-mode pop order
         } sc;
     } u;
@@ -578,7 +580,8 @@ __device__ __forceinline__ uint32_t count_above_desc(const uint32_t *L, uint32_t
 // at run time, the timestamps held across loops cost SGPR spills in the production kernel.
 enum : int { PH_SETUP = 0, PH_LOOKUP, PH_INSERT, PH_SCORE, PH_POP, PH_DESC, PH_STAGE, PH_LVF, PH_LVR, PH_APPLY,
              PH_WB, PH_OUT, PH_NPASS, PH_NCAND, PH_NREAD, PH_NPASS16, PH_NPASS32, PH_NPASS64, PH_ROWSF, PH_ROWSR,
-             PH_NSCORECALL, PH_NFORCED, PH_NPOPPED, PH_NSUCC, PH_PASSLOOP, PH_SEL, PH_FETCH, PH_SEEDLOOP, PH_SLOTS = 32 };
+             PH_NSCORECALL, PH_NFORCED, PH_NPOPPED, PH_NSUCC, PH_PASSLOOP, PH_SEL, PH_FETCH, PH_SEEDLOOP, PH_NBATCH,
+             PH_RANK, PH_NELEMSF, PH_CANDL, PH_SLOTS = 32 };
 __device__ __forceinline__ uint64_t clk() { return __builtin_amdgcn_s_memtime(); }
 #if SNAPGPU_PHASE_TIMERS
 #define PH_T(A, v) const uint64_t v = (A).phaseBuf ? sgk::clk() : 0
@@ -696,18 +699,22 @@ __device__ __forceinline__ void sk_set(Lds<MAXLEN> &S, ElemOf<MAXLEN> *ar, uint3
     else ar[e].sortkey = v;
 }
 
-// owner-lane recompute of its selection maximum (elements e == lane mod 64)
+// recompute of `owner`'s selection maximum (elements e == owner mod 64), the whole wave
+// scanning that lane's elements 64 at a time
 template <int MAXLEN>
-__device__ __forceinline__ void recompute_lane_max(Lds<MAXLEN> &S, const ElemOf<MAXLEN> *ar, int lane) {
+__device__ __forceinline__ void recompute_lane_max(Lds<MAXLEN> &S, const ElemOf<MAXLEN> *ar, int owner) {
+    const int lane = lane_id();
     uint64_t best = 0;
     const uint32_t nElems = S.nElems;
 #pragma unroll 1
-    for (uint32_t e = lane; e < nElems; e += WAVE) {
-        uint32_t k = sk_get(S, ar, e);
-        uint64_t v = ((uint64_t)k << 32) | e;
+    for (uint32_t b = (uint32_t)owner; b < nElems; b += WAVE * WAVE) {
+        const uint32_t e = b + WAVE * (uint32_t)lane;
+        const uint32_t k = e < nElems ? sk_get(S, ar, e) : 0u;
+        const uint64_t v = ((uint64_t)k << 32) | e;
         if (k && v > best) best = v;
     }
-    S.laneMax[lane] = best;
+    best = max_reduce64(best);
+    if (lane == owner) S.laneMax[owner] = best;
 }
 
 // uniform field extraction from a cooperatively loaded element (lane i = dword i)

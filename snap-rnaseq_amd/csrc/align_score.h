@@ -545,6 +545,7 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<128> &S, Elem1
     // elements are not unlinked one by one.
     uint16_t *order = S.u.sc.order;
     uint32_t fDone = 0, fAvail = 0, ordBase = 0;
+    bool fMore = true;   // a ranking window came back full: elements of lower rank may remain
     for (uint32_t guard = 0;; guard++) {
         // lane id re-read per batch (volatile asm): masks and addresses derived from it are
         // recomputed in the batch instead of hoisted and kept live, spilled, across the pass loop
@@ -566,33 +567,51 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<128> &S, Elem1
                 const uint32_t e = readlaneu((uint32_t)lm, owner);
                 sk_set(S, ar, e, 0);                       // unlink (BaseAligner.cpp:1391-1394)
                 wave_sync();
-                if ((int)(e % WAVE) == lane) recompute_lane_max(S, ar, lane);
+                recompute_lane_max(S, ar, owner);
                 if (lane == 0) G.eidx[0] = e;
                 nb = 1;
                 wave_sync();
             }
         } else {
-            if (fDone == fAvail) {
-                // rank[e] = number of linked elements with a larger key (keys are unique)
+            if (fDone == fAvail && fMore) {
+                PH_T(A, trk);
+                PH_CNT(A, S, PH_NELEMSF, fDone == 0 ? S.nElems : 0);
+                // rank[e] = number of linked elements with a larger key (keys are unique).  The
+                // keys of elements >= SKCAP are staged from the arena into LDS a block at a time
+                // (the LV rows are idle here), so every lane compares against broadcast LDS reads.
                 ordBase = fDone;
                 const uint32_t nE = S.nElems;
+                const uint32_t nL = nE < SKCAP ? nE : SKCAP;
+                uint32_t *stage = reinterpret_cast<uint32_t *>(&S.u.sc.rows8[0][0]);
                 uint32_t inRange = 0;
                 for (uint32_t e0 = 0; e0 < nE; e0 += WAVE) {
                     const uint32_t e = e0 + lane;
                     const uint32_t ke = e < nE ? sk_get(S, ar, e) : 0u;
                     uint32_t rank = 0;
                     uint32_t f = 0;
-                    for (; f + 4 <= nE && f + 4 <= SKCAP; f += 4) {
+                    for (; f + 4 <= nL; f += 4) {
                         const uint4 k4 = *reinterpret_cast<const uint4 *>(&S.sk[f]);
                         rank += (k4.x > ke) + (k4.y > ke) + (k4.z > ke) + (k4.w > ke);
                     }
-                    for (; f < nE; f++) rank += sk_get(S, ar, f) > ke;
+                    for (; f < nL; f++) rank += S.sk[f] > ke;
+                    for (uint32_t b0 = SKCAP; b0 < nE; b0 += SKCAP) {
+                        const uint32_t nk = nE - b0 < SKCAP ? nE - b0 : SKCAP;
+                        wave_sync();
+                        for (uint32_t j = lane; j < ((nk + 3) & ~3u); j += WAVE) stage[j] = j < nk ? ar[b0 + j].sortkey : 0u;
+                        wave_sync();
+                        for (uint32_t g = 0; g < nk; g += 4) {
+                            const uint4 k4 = *reinterpret_cast<const uint4 *>(&stage[g]);
+                            rank += (k4.x > ke) + (k4.y > ke) + (k4.z > ke) + (k4.w > ke);
+                        }
+                    }
                     const bool in = ke != 0 && rank >= ordBase && rank < ordBase + ORDCAP;
                     if (in) order[rank - ordBase] = (uint16_t)e;
                     inRange += (uint32_t)__popcll(ballot(in));
                 }
                 fAvail = ordBase + inRange;
+                fMore = inRange == ORDCAP;
                 wave_sync();
+                PH_ADD(A, S, PH_RANK, trk);
             }
             nb = fAvail - fDone < (uint32_t)EB ? fAvail - fDone : (uint32_t)EB;
             if ((uint32_t)lane < nb) G.eidx[lane] = order[fDone - ordBase + lane];
@@ -626,6 +645,8 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<128> &S, Elem1
         }
         PH_ADD(A, S, PH_FETCH, tfe);
         // ---- candidate list: elements in pop order, ascending bit; lane sl owns element sl
+        PH_CNT(A, S, PH_NBATCH, 1);
+        PH_T(A, tcl);
         uint32_t nc;
         {
             uint64_t pend = 0;
@@ -650,6 +671,7 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<128> &S, Elem1
             }
             wave_sync();
         }
+        PH_ADD(A, S, PH_CANDL, tcl);
         PH_ADD(A, S, PH_POP, tpop);
         PH_CNT(A, S, PH_NCAND, nc);
         PH_CNT(A, S, PH_NPOPPED, nb);

@@ -80,7 +80,8 @@ __device__ __forceinline__ bool score_wave(const KArgs &A, Lds<MAXLEN> &S, Elem5
         // insertion happens while an element is scored, so the next selection is known
         sk_set(S, ar, e, 0);
         wave_sync();
-        if ((int)(e % WAVE) == lane) recompute_lane_max(S, ar, lane);
+        recompute_lane_max(S, ar, (int)(e % WAVE));
+        wave_sync();
         if (((ewl >> 8) & 0xff) <= st.scoreLimit) {
             uint64_t mask = used;
             while (mask) {

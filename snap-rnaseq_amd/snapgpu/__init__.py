@@ -412,7 +412,8 @@ class BaseAligner:
 
     PHASES = ("setup", "lookup", "insert", "score", "pop", "desc", "stage", "lv_fwd", "lv_rev", "apply",
               "writeback", "out", "n_pass", "n_cand", "n_read", "n_pass16", "n_pass32", "n_pass64", "rows_fwd",
-              "rows_rev", "n_score_calls", "n_forced", "n_popped", "n_succ", "passloop", "select", "fetch", "seedloop")
+              "rows_rev", "n_score_calls", "n_forced", "n_popped", "n_succ", "passloop", "select", "fetch", "seedloop",
+              "n_batch", "rank", "n_elems_forced", "candlist")
 
     def phase_cycles(self, reset=True):
         """Diagnostic per-phase shader-cycle sums (needs SNAPGPU_PHASES=1 at construction)."""

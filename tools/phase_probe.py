@@ -35,5 +35,6 @@ tot = sum(ph[k] for k in ("setup", "lookup", "insert", "score", "out"))
 ph["cycles_per_read_total"] = tot
 out = {"kernel_ms": ms, "reads": args.reads, "cycles_per_read": {k: ph[k] / args.reads for k in ph}}
 out["share_of_wave_time"] = {k: round(ph[k] / tot, 4) for k in ("setup", "lookup", "insert", "score", "pop", "desc",
-                                                                 "stage", "lv_fwd", "lv_rev", "apply", "writeback", "out")}
+                                                                 "stage", "lv_fwd", "lv_rev", "apply", "writeback", "out",
+                                                                 "select", "fetch", "passloop", "rank", "candlist")}
 print(json.dumps(out, indent=1))
