@@ -497,6 +497,62 @@ int snapgpu_copy_peak(snapgpu_aligner_t *a, uint64_t bytes, double *ms);
  * Returns 0 when the path behaves. */
 int snapgpu_selftest_timeout_path(void);
 
+/* ------------------------------------------------------------------ paired-end
+ * ChimericPairedEndAligner::align (ChimericPairedEndAligner.cpp:56-126) over
+ * IntersectingPairedEndAligner::align (IntersectingPairedEndAligner.cpp:142-753), constructed as
+ * PairedAligner.cpp:462-482 does.  Defaults = the paired CLI's (AlignerOptions.cpp:73-77,
+ * PairedAligner.cpp:57-58, 231-235, IntersectingPairedEndAligner.h:32-33). */
+typedef struct snapgpu_paired_params {
+    uint32_t maxHits;              /* -h: maxHits of the chimeric single-end fallback, default 16000 */
+    uint32_t maxK;                 /* -d: maxDist, default 15 */
+    uint32_t maxSeedsToUse;        /* -n: default 8 (0 => seedCoverage) */
+    uint32_t extraSearchDepth;     /* default 2 */
+    uint32_t minSpacing;           /* -s min, default 50 */
+    uint32_t maxSpacing;           /* -s max, default 1000 */
+    uint32_t maxBigHits;           /* -H intersectingAlignerMaxHits, default 16000 */
+    uint32_t maxCandidatePoolSize; /* -mcp, default 1000000 */
+    uint32_t maxReadSize;          /* MAX_READ_LENGTH (Read.h:45), default 500 */
+    uint32_t forceSpacing;         /* -f, default 0 */
+    double   seedCoverage;         /* used iff maxSeedsToUse == 0 */
+} snapgpu_paired_params_t;
+
+/* PairedAlignmentResult (PairedEndAligner.h:31-55) plus counters.  Fields an aligner leaves
+ * unwritten keep the pre-state {status NotFound, location 0xffffffff, direction 0, score -1, mapq 0}. */
+typedef struct snapgpu_pair_result {
+    uint32_t location[2];
+    int32_t  score[2];
+    int32_t  mapq[2];
+    uint8_t  status[2];            /* SNAPGPU_NOT_FOUND .. */
+    uint8_t  direction[2];
+    uint8_t  fromAlignTogether;
+    uint8_t  alignedAsPair;
+    uint16_t flags;                /* SNAPGPU_PFLAG_* */
+    uint32_t nLocationsScored;     /* IntersectingPairedEndAligner::getLocationsScored() delta */
+    uint32_t nSingleScored;        /* the fallback BaseAligner's getLocationsScored() delta */
+    uint32_t reserved, reserved2;
+    double   probabilityOfAllPairs;   /* the intersecting aligner's MAPQ inputs (align()'s locals) */
+    double   probabilityOfBestPair;
+} snapgpu_pair_result_t;   /* 64 bytes */
+#define SNAPGPU_PFLAG_POOL_EXHAUSTED 0x01   /* the reference soft_exits ("Ran out of ... pool entries") */
+#define SNAPGPU_PFLAG_READ_TOO_LONG  0x02   /* the reference soft_exits (IntersectingPairedEndAligner.cpp:211-215) */
+#define SNAPGPU_PFLAG_DEFERRED       0x04   /* aligned by the second (large-pool / long-read) pass */
+#define SNAPGPU_PFLAG_MAPQ_FIXED     0x08   /* MAPQ re-derived on the host (threshold case) */
+
+void snapgpu_paired_params_default(snapgpu_paired_params_t *p);
+typedef struct snapgpu_paired_aligner snapgpu_paired_aligner_t;
+/* NULL (and snapgpu_last_error) without a HIP device: there is no CPU fallback. */
+snapgpu_paired_aligner_t *snapgpu_paired_aligner_create(int device, const snapgpu_index_t *idx,
+                                                        const snapgpu_paired_params_t *p);
+void snapgpu_paired_aligner_destroy(snapgpu_paired_aligner_t *pa);
+/* ChimericPairedEndAligner::align for pair i = (reads0[i], reads1[i]), every i, in order. */
+int snapgpu_paired_align_batch(snapgpu_paired_aligner_t *pa, const snapgpu_reads_t *reads0,
+                               const snapgpu_reads_t *reads1, snapgpu_pair_result_t *out);
+/* IntersectingPairedEndAligner::align alone (no single-end fallback), for parity tests. */
+int snapgpu_paired_intersect_batch(snapgpu_paired_aligner_t *pa, const snapgpu_reads_t *reads0,
+                                   const snapgpu_reads_t *reads1, snapgpu_pair_result_t *out);
+/* The single-end BaseAligner the chimeric fallback uses (maxHits, maxK, seeds of the params). */
+snapgpu_aligner_t *snapgpu_paired_aligner_single(snapgpu_paired_aligner_t *pa);
+
 /* MAPQ (mapq.h:32-65) as the host computes it; exported for tests. */
 int snapgpu_compute_mapq(double pAll, double pBest, int score, int popularSeedsSkipped);
 

@@ -23,6 +23,10 @@
 //   samheader <indexDir> <sorted 0|1> <version> [args...]
 //          -> SAMFormat::writeHeader (SAM.cpp:700-800) for a FASTQ input (no input header),
 //             default read group, command line = args
+//   paired <indexDir> <reads0.fq> <reads1.fq> [maxHits maxK numSeeds extra minSpacing maxSpacing maxBigHits]
+//          -> per pair: the IntersectingPairedEndAligner result alone, then the
+//             ChimericPairedEndAligner result, constructed as PairedAligner.cpp:462-482
+//             (paired defaults AlignerOptions.cpp:73-77: maxHits 16000, maxK 15, 8 seeds)
 //   cigar  <indexDir> <calls.tsv>  lines: loc dir useM read
 //          -> ed cigar   (SAMFormat::computeCigarString, SAM.cpp:1162-1230, restated
 //             around the reference's LandauVishkinWithCigar with zeroed slack bytes)
@@ -38,6 +42,8 @@
 #include "FileFormat.h"
 #include "Genome.h"
 #include "Tables.h"
+#include "IntersectingPairedEndAligner.h"
+#include "ChimericPairedEndAligner.h"
 #include <string>
 #include <vector>
 #include <fstream>
@@ -219,6 +225,68 @@ static int mode_sam(int argc, char **argv) {
     return 0;
 }
 
+
+// One line per pair:
+//   i  [intersecting: st0 st1 loc0 loc1 dir0 dir1 sc0 sc1 mq0 mq1 nScored]
+//      [chimeric:     st0 st1 loc0 loc1 dir0 dir1 sc0 sc1 mq0 mq1 fromAlignTogether alignedAsPair nScored]
+// Fields an aligner leaves unwritten keep the pre-state {NotFound, InvalidGenomeLocation, 0, -1, 0}.
+static void pairedPre(PairedAlignmentResult &r) {
+    memset(&r, 0, sizeof(r));
+    for (int k = 0; k < 2; k++) { r.status[k] = NotFound; r.location[k] = 0xffffffffu; r.direction[k] = 0; r.score[k] = -1; r.mapq[k] = 0; }
+}
+static void pairedPrint(const PairedAlignmentResult &r) {
+    printf("\t%d\t%d\t%u\t%u\t%d\t%d\t%d\t%d\t%d\t%d", (int)r.status[0], (int)r.status[1], r.location[0], r.location[1],
+           (int)r.direction[0], (int)r.direction[1], r.score[0], r.score[1], r.mapq[0], r.mapq[1]);
+}
+static int mode_paired(int argc, char **argv) {
+    if (argc < 5) { fprintf(stderr, "paired <indexDir> <reads0.fq> <reads1.fq> [maxHits maxK numSeeds extra minSpacing maxSpacing maxBigHits]\n"); return 2; }
+    unsigned maxHits = argc > 5 ? atoi(argv[5]) : 16000;
+    unsigned maxK = argc > 6 ? atoi(argv[6]) : 15;
+    unsigned numSeeds = argc > 7 ? atoi(argv[7]) : 8;
+    unsigned extra = argc > 8 ? atoi(argv[8]) : 2;
+    unsigned minSpacing = argc > 9 ? atoi(argv[9]) : 50;
+    unsigned maxSpacing = argc > 10 ? atoi(argv[10]) : 1000;
+    unsigned maxBigHits = argc > 11 ? atoi(argv[11]) : DEFAULT_INTERSECTING_ALIGNER_MAX_HITS;
+    const unsigned pool = DEFAULT_MAX_CANDIDATE_POOL_SIZE;
+    initializeLVProbabilitiesToPhredPlus33();
+    GenomeIndex *idx = GenomeIndex::loadFromDirectory(argv[2]);
+    if (!idx) { fprintf(stderr, "cannot load index %s\n", argv[2]); return 1; }
+    const int maxReadSize = MAX_READ_LENGTH;
+    BigAllocator *al = new BigAllocator(IntersectingPairedEndAligner::getBigAllocatorReservation(
+        idx, maxBigHits, maxReadSize, idx->getSeedLength(), numSeeds, 0, maxK, extra, pool));
+    IntersectingPairedEndAligner *ia = new IntersectingPairedEndAligner(idx, maxReadSize, maxHits, maxK, numSeeds, 0,
+                                                                       minSpacing, maxSpacing, maxBigHits, extra, pool, al);
+    ChimericPairedEndAligner *ca = new ChimericPairedEndAligner(idx, maxReadSize, maxHits, maxK, numSeeds, 0, minSpacing,
+                                                               maxSpacing, false, extra, ia);
+    std::ifstream in0(argv[3]), in1(argv[4]);
+    std::string id[2], bases[2], plus[2], quals[2];
+    unsigned i = 0;
+    while (std::getline(in0, id[0]) && std::getline(in0, bases[0]) && std::getline(in0, plus[0]) && std::getline(in0, quals[0]) &&
+           std::getline(in1, id[1]) && std::getline(in1, bases[1]) && std::getline(in1, plus[1]) && std::getline(in1, quals[1])) {
+        std::string b[2], q[2];
+        Read r[2];
+        for (int k = 0; k < 2; k++) {
+            b[k] = bases[k] + std::string(16, '\0');
+            q[k] = quals[k] + std::string(16, '\0');
+            r[k].init(id[k].c_str() + 1, (unsigned)id[k].size() - 1, b[k].c_str(), q[k].c_str(), (unsigned)bases[k].size());
+        }
+        PairedAlignmentResult res;
+        printf("%u", i);
+        pairedPre(res);
+        _int64 s0 = ia->getLocationsScored();
+        ia->align(&r[0], &r[1], &res);
+        pairedPrint(res);
+        printf("\t%lld", (long long)(ia->getLocationsScored() - s0));
+        pairedPre(res);
+        s0 = ca->getLocationsScored();
+        ca->align(&r[0], &r[1], &res);
+        pairedPrint(res);
+        printf("\t%d\t%d\t%lld\n", (int)res.fromAlignTogether, (int)res.alignedAsPair, (long long)(ca->getLocationsScored() - s0));
+        i++;
+    }
+    return 0;
+}
+
 static int mode_cigar(int argc, char **argv) {
     if (argc < 4) { fprintf(stderr, "cigar <indexDir> <calls.tsv>\n"); return 2; }
     GenomeIndex *idx = GenomeIndex::loadFromDirectory(argv[2]);
@@ -272,6 +340,7 @@ int main(int argc, char **argv) {
     if (m == "lookup") return mode_lookup(argc, argv);
     if (m == "sam") return mode_sam(argc, argv);
     if (m == "cigar") return mode_cigar(argc, argv);
+    if (m == "paired") return mode_paired(argc, argv);
     if (m == "samheader") return mode_samheader(argc, argv);
     fprintf(stderr, "unknown mode %s\n", argv[1]);
     return 2;

@@ -867,3 +867,527 @@ int oracle_cigar(const snapgpu_index_view_t *v, uint32_t loc, const char *patter
     }
     return -1;
 }
+
+/* ============================================================== paired-end (f2)
+ * IntersectingPairedEndAligner::align (IntersectingPairedEndAligner.cpp:142-753) and
+ * ChimericPairedEndAligner::align (ChimericPairedEndAligner.cpp:56-126), restated over the
+ * helpers above (lookup, LV, getSubstring, BaseAligner for the chimeric fallback).
+ * The hit sets (HashTableHitSet, :844-1322, the "traditional" binary search of :1219-1263),
+ * the mate / candidate pools and the merge anchors are plain arrays here.  Unsigned
+ * arithmetic is kept where the reference's comparisons depend on it. */
+#define P_MAX_SEEDS 30            /* IntersectingPairedEndAligner.h:93 MAX_MAX_SEEDS */
+#define P_LOOKUP_CAP 64           /* lookups per hit set (seedCoverage mode can ask for more than 30) */
+
+/* isWithin, Util.h:538-541 */
+static inline int is_within(uint32_t a, uint32_t b, uint32_t d) { return (a <= b && a + d >= b) || (a >= b && a <= b + d); }
+static inline uint32_t loc_distance(uint32_t a, uint32_t b) { return a > b ? a - b : b - a; }   /* Genome.cpp:473-479 */
+
+typedef struct {
+    uint32_t seedOffset, nHits, cur, set;
+    const uint32_t *hits;
+    uint32_t single;              /* the singleton a slot value holds (hits points here) */
+} PLookup;
+
+typedef struct {                  /* HashTableHitSet */
+    PLookup lk[P_LOOKUP_CAP];
+    unsigned nLookups, maxMerge;
+    int curSet;
+    unsigned exhausted[P_LOOKUP_CAP], miss[P_LOOKUP_CAP];
+    uint32_t lastReturned;        /* mostRecentLocationReturned */
+} PHitSet;
+
+static void hs_record(PHitSet *h, uint32_t seedOffset, unsigned nHits, const uint32_t *hits, uint32_t single, int begins) {
+    if (begins) { h->curSet++; h->exhausted[h->curSet] = 0; }                 /* :863-867 */
+    if (nHits == 0) { h->exhausted[h->curSet]++; return; }
+    PLookup *l = &h->lk[h->nLookups++];
+    l->cur = 0; l->nHits = nHits; l->seedOffset = seedOffset; l->set = (uint32_t)h->curSet;
+    l->single = single;
+    l->hits = nHits == 1 && hits == NULL ? &l->single : hits;
+    while (l->nHits > 0 && l->hits[l->nHits - 1] < l->seedOffset) l->nHits--;   /* :882-884 */
+}
+
+static unsigned hs_best_possible(PHitSet *h) {   /* computeBestPossibleScoreForCurrentHit, :901-929 */
+    for (int i = 0; i <= h->curSet; i++) h->miss[i] = h->exhausted[i];
+    for (unsigned i = 0; i < h->nLookups; i++) {
+        PLookup *l = &h->lk[i];
+        uint32_t target = h->lastReturned + l->seedOffset;
+        int near = (l->cur != l->nHits && is_within(l->hits[l->cur], target, h->maxMerge)) ||
+                   (l->cur != 0 && is_within(l->hits[l->cur - 1], target, h->maxMerge));
+        if (!near) h->miss[l->set]++;
+    }
+    unsigned best = 0;
+    for (int i = 0; i <= h->curSet; i++) if (h->miss[i] > best) best = h->miss[i];
+    return best;
+}
+
+/* getNextHitLessThanOrEqualTo, the traditional version (:1219-1266) */
+static int hs_next_le(PHitSet *h, uint32_t maxOff, uint32_t *loc, uint32_t *seedOff) {
+    int any = 0;
+    uint32_t bestOff = 0;
+    for (unsigned i = 0; i < h->nLookups; i++) {
+        PLookup *l = &h->lk[i];
+        int lim0 = (int)l->cur, lim1 = (int)l->nHits - 1;
+        uint32_t maxThis = maxOff + l->seedOffset;
+        while (lim0 <= lim1) {
+            unsigned probe = (unsigned)(lim0 + lim1) / 2;
+            if (l->hits[probe] <= maxThis && (probe == 0 || l->hits[probe - 1] > maxThis)) {
+                if (l->hits[probe] - l->seedOffset > bestOff) {
+                    any = 1;
+                    h->lastReturned = *loc = bestOff = l->hits[probe] - l->seedOffset;
+                    *seedOff = l->seedOffset;
+                }
+                l->cur = probe;
+                break;
+            }
+            if (l->hits[probe] > maxThis) lim0 = (int)probe + 1;
+            else lim1 = (int)(probe - 1);
+        }
+        if (lim0 > lim1) l->cur = l->nHits;
+    }
+    return any;
+}
+
+static int hs_first(PHitSet *h, uint32_t *loc, uint32_t *seedOff) {   /* getFirstHit, :1270-1284 */
+    int any = 0;
+    *loc = 0;
+    for (unsigned i = 0; i < h->nLookups; i++) {
+        PLookup *l = &h->lk[i];
+        if (l->nHits > 0 && l->hits[0] - l->seedOffset > *loc) {
+            h->lastReturned = *loc = l->hits[0] - l->seedOffset;
+            *seedOff = l->seedOffset;
+            any = 1;
+        }
+    }
+    return any;
+}
+
+static int hs_next_lower(PHitSet *h, uint32_t *loc, uint32_t *seedOff) {   /* getNextLowerHit, :1286-1322 */
+    uint32_t found = 0;
+    int any = 0;
+    for (unsigned i = 0; i < h->nLookups; i++) {
+        PLookup *l = &h->lk[i];
+        if (l->cur != l->nHits && l->hits[l->cur] - l->seedOffset == h->lastReturned) l->cur++;
+        if (l->cur != l->nHits && found < l->hits[l->cur] - l->seedOffset && l->hits[l->cur] >= l->seedOffset) {
+            *loc = found = l->hits[l->cur] - l->seedOffset;
+            *seedOff = l->seedOffset;
+            any = 1;
+        }
+    }
+    if (any) h->lastReturned = found;
+    return any;
+}
+
+typedef struct {                  /* ScoringMateCandidate, IntersectingPairedEndAligner.h:401-423 */
+    double prob;
+    uint32_t loc, bestPossible, score, scoreLimit, seedOffset;
+    int genomeOffset;
+} PMate;
+typedef struct {                  /* ScoringCandidate, :425-447 (indices instead of pointers) */
+    int next, anchor;
+    uint32_t mateIndex, loc, setPair, seedOffset, bestPossible;
+} PCand;
+typedef struct {                  /* MergeAnchor, :364-393 */
+    double prob;
+    uint32_t moreLoc, fewerLoc;
+    int pairScore;
+} PAnchor;
+
+typedef struct {
+    const snapgpu_index_view_t *ix;
+    snapgpu_paired_params_t p;
+    unsigned maxSeedsCmd, poolSize;
+    PHitSet hs[2][2];
+    PCand *cand; PMate *mate[2]; PAnchor *anchor;
+    int *lists;                   /* scoringCandidates[maxK + extra + 1] */
+    char data[2][2][MAX_READ_LENGTH + 32], qual[2][2][MAX_READ_LENGTH + 32], rev[2][2][MAX_READ_LENGTH + 32];
+    unsigned len[2];
+    uint32_t nScored;
+    Oracle *single;               /* the chimeric fallback's BaseAligner */
+} POracle;
+
+/* scoreLocation, IntersectingPairedEndAligner.cpp:755-841 */
+static void p_score_location(POracle *o, unsigned r, int dir, uint32_t loc, uint32_t seedOffset, uint32_t scoreLimit,
+                             uint32_t *score, double *prob, int *offset) {
+    const snapgpu_index_view_t *ix = o->ix;
+    o->nScored++;
+    const unsigned n = o->len[r];
+    uint32_t gLen = n + MAX_K;
+    const char *data = get_substring(ix, loc, gLen);
+    if (!data) {
+        uint32_t endOffset;
+        if ((uint64_t)loc + n + MAX_K >= ix->nBases) endOffset = ix->nBases;
+        else {   /* getPieceAtLocation(loc + n + MAX_K)->beginningOffset (Genome.cpp:356-374) */
+            uint32_t at = loc + n + MAX_K;
+            int lo = 0, hi = ix->nPieces - 1, pc = -1;
+            while (lo <= hi) {
+                int m = (lo + hi) / 2;
+                if (ix->pieceOffsets[m] <= at && (m == ix->nPieces - 1 || ix->pieceOffsets[m + 1] > at)) { pc = m; break; }
+                else if (ix->pieceOffsets[m] <= at) lo = m + 1;
+                else hi = m - 1;
+            }
+            endOffset = pc >= 0 ? ix->pieceOffsets[pc] : 0;
+        }
+        gLen = endOffset - loc - 1;
+        if (gLen >= n - (uint32_t)MAX_K) data = get_substring(ix, loc, gLen);
+    }
+    if (!data) { *score = 0xffffffffu; *prob = 0; return; }
+    const int seedLen = (int)ix->seedLen, tail = (int)seedOffset + seedLen;
+    double p1 = 0, p2 = 0;
+    int ni;
+    int s1 = oracle_lv(1, data + tail, (int)gLen - tail, o->data[r][dir] + tail, o->qual[r][dir] + tail, (int)n - tail,
+                       (int)scoreLimit, &p1, &ni);
+    if (s1 == -1) *score = 0xffffffffu;
+    else {
+        int limitLeft = (int)scoreLimit - s1;
+        int s2 = oracle_lv(-1, data + seedOffset, (int)seedOffset + MAX_K, o->rev[r][dir] + n - seedOffset,
+                           o->qual[r][!dir] + n - seedOffset, (int)seedOffset, limitLeft, &p2, offset);
+        if (s2 == -1) *score = 0xffffffffu;
+        else {
+            *score = (uint32_t)(s1 + s2);
+            *prob = p1 * p2 * g_seedProb[seedLen];
+        }
+    }
+    if (*score == 0xffffffffu) *prob = 0;
+}
+
+static void pair_pre(snapgpu_pair_result_t *r) {
+    memset(r, 0, sizeof(*r));
+    for (int k = 0; k < 2; k++) { r->location[k] = INVALID_LOC; r->score[k] = -1; }
+}
+
+/* IntersectingPairedEndAligner::align; returns 0, or -1 when the reference would soft_exit */
+static int p_align(POracle *o, const char *b0, const char *q0, unsigned n0, const char *b1, const char *q1, unsigned n1,
+                   snapgpu_pair_result_t *res) {
+    const snapgpu_index_view_t *ix = o->ix;
+    const unsigned seedLen = ix->seedLen;
+    const unsigned maxK = o->p.maxK, extra = o->p.extraSearchDepth;
+    const char *B[2] = {b0, b1}, *Q[2] = {q0, q1};
+    unsigned N[2] = {n0, n1};
+    o->nScored = 0;
+    unsigned maxSeeds = o->maxSeedsCmd ? o->maxSeedsCmd
+                                       : (unsigned)((n0 > n1 ? n0 : n1) * o->p.seedCoverage / seedLen);   /* :150-155 */
+    for (unsigned k = 0; k <= maxK + extra; k++) o->lists[k] = -1;
+    unsigned nCand = 0, nMate[2] = {0, 0}, nAnchor = 0;
+    if (n0 < 50 || n1 < 50) return 0;                                         /* :186-188 */
+    unsigned countOfNs = 0, popular[2] = {0, 0}, nLookups[2] = {0, 0}, total[2][2] = {{0, 0}, {0, 0}};
+    for (unsigned r = 0; r < 2; r++) {
+        o->len[r] = N[r];
+        for (int d = 0; d < 2; d++) {
+            PHitSet *h = &o->hs[r][d];
+            h->nLookups = 0; h->curSet = -1; h->maxMerge = maxK;               /* firstInit(maxSeeds, maxK), init() */
+        }
+        if (N[r] > o->p.maxReadSize) { res->flags |= SNAPGPU_PFLAG_READ_TOO_LONG; return -1; }
+        for (unsigned i = 0; i < N[r]; i++) {
+            char c = B[r][i];
+            if (c >= 'a' && c <= 'z') c = (char)(c - 0x20);                    /* Read::init upper-cases */
+            char cc = c == 'A' ? 'T' : c == 'G' ? 'C' : c == 'C' ? 'G' : c == 'T' ? 'A' : c == 'N' ? 'N' : 0;
+            o->data[r][0][i] = c; o->qual[r][0][i] = Q[r][i];
+            o->data[r][1][N[r] - 1 - i] = cc; o->qual[r][1][N[r] - 1 - i] = Q[r][i];
+            countOfNs += c == 'N';
+        }
+        for (int d = 0; d < 2; d++) {
+            memset(o->data[r][d] + N[r], 0, 32); memset(o->qual[r][d] + N[r], 0, 32);
+            for (unsigned i = 0; i < N[r]; i++) o->rev[r][d][i] = o->data[r][d][N[r] - 1 - i];
+            memset(o->rev[r][d] + N[r], 0, 32);
+        }
+    }
+    if (countOfNs > maxK) return 0;                                            /* :226-228 */
+    /* phase 1: seed lookups (:259-340) */
+    for (unsigned r = 0; r < 2; r++) {
+        unsigned next = 0, wrap = 0, nPossible = N[r] - seedLen + 1;
+        uint8_t used[(MAX_READ_LENGTH + 7) / 8 + 8];
+        memset(used, 0, sizeof(used));
+        int begins[2] = {1, 1};
+        while (nLookups[r] < nPossible && nLookups[r] < maxSeeds && nLookups[r] < P_LOOKUP_CAP) {
+            if (next >= nPossible) {
+                wrap++;
+                begins[0] = begins[1] = 1;
+                if (wrap >= seedLen) break;
+                next = wrapped_next_seed(seedLen, wrap);
+            }
+            while (next < nPossible && (used[next / 8] & (1 << (next % 8)))) next++;
+            if (next >= nPossible) continue;
+            used[next / 8] |= (uint8_t)(1 << (next % 8));
+            uint64_t f = 0, rv = 0;
+            int valid = 1;
+            for (unsigned i = 0; i < seedLen; i++) {
+                int v = base_value(o->data[r][0][next + i]);
+                if (v > 3) { valid = 0; break; }
+                f |= (uint64_t)v << ((seedLen - i - 1) * 2);
+                rv |= (uint64_t)(v ^ 3) << (i * 2);
+            }
+            if (!valid) { next++; continue; }                                   /* :296-302 */
+            unsigned nHits[2] = {0, 0};
+            const uint32_t *hits[2] = {NULL, NULL};
+            uint32_t single[2] = {0, 0};
+            int comp = (int64_t)f > (int64_t)rv;
+            uint64_t canon = comp ? rv : f;
+            uint32_t probes = 0, novf = 0;
+            const uint32_t *e = ht_lookup(ix, (uint32_t)(canon >> 32), (uint32_t)canon, &probes);
+            if (e) {
+                for (int side = 0; side < 2; side++) {
+                    uint32_t v = (side == 0) == !comp ? e[0] : e[1];
+                    if (side == 1 && f == rv) { nHits[1] = nHits[0]; hits[1] = hits[0]; single[1] = single[0]; break; }
+                    fill_side(ix, v, 0, INVALID_LOC, &single[side], &nHits[side], &hits[side], &novf);
+                    if (hits[side] == &single[side]) hits[side] = NULL;             /* the singleton travels by value */
+                }
+            }
+            nLookups[r]++;
+            for (int d = 0; d < 2; d++) {
+                uint32_t offset = d == 0 ? next : N[r] - seedLen - next;
+                if (nHits[d] < o->p.maxBigHits) {
+                    total[r][d] += nHits[d];
+                    hs_record(&o->hs[r][d], offset, nHits[d], hits[d], single[d], begins[d]);
+                    begins[d] = 0;
+                } else popular[r]++;
+            }
+            if ((maxSeeds - nLookups[r] + 1) * seedLen + next < nPossible)        /* :333-338 */
+                next += (nPossible + next) / (maxSeeds - nLookups[r] + 1);
+            else next += seedLen;
+        }
+    }
+    const unsigned more = total[0][0] + total[0][1] > total[1][0] + total[1][1] ? 0 : 1, fewer = 1 - more;   /* :342-343 */
+    static const int spDir[2][2] = {{0, 1}, {1, 0}};                             /* setPairDirection, :351 */
+    /* phase 2: candidates (:357-511) */
+    unsigned maxUsedList = 0;
+    const uint32_t maxSp = o->p.maxSpacing;
+    for (unsigned sp = 0; sp < 2; sp++) {
+        PHitSet *set[2];
+        set[0] = &o->hs[0][sp == 0 ? 0 : 1];
+        set[1] = &o->hs[1][sp == 0 ? 1 : 0];
+        uint32_t fewerLoc, fewerSeed, moreLoc, moreSeed = 0;
+        int outOfMore = 0;
+        if (!hs_first(set[fewer], &fewerLoc, &fewerSeed)) continue;
+        moreLoc = INVALID_LOC;
+        for (;;) {
+            if (moreLoc > fewerLoc + maxSp) {
+                if (!hs_next_le(set[more], fewerLoc + maxSp, &moreLoc, &moreSeed)) break;
+            }
+            if (moreLoc + maxSp < fewerLoc &&
+                (nMate[sp] == 0 || !is_within(o->mate[sp][nMate[sp] - 1].loc, fewerLoc, maxSp))) {
+                if (!hs_next_le(set[fewer], moreLoc + maxSp, &fewerLoc, &fewerSeed)) break;
+                continue;
+            }
+            while (moreLoc + maxSp >= fewerLoc && !outOfMore) {
+                unsigned bps = hs_best_possible(set[more]);
+                if (nMate[sp] >= o->poolSize / 2) { res->flags |= SNAPGPU_PFLAG_POOL_EXHAUSTED; return -1; }
+                PMate *m = &o->mate[sp][nMate[sp]++];
+                m->loc = moreLoc; m->bestPossible = bps; m->seedOffset = moreSeed;
+                m->score = 0xfffffffeu; m->scoreLimit = 0xffffffffu; m->prob = 0; m->genomeOffset = 0;
+                if (!hs_next_lower(set[more], &moreLoc, &moreSeed)) { moreLoc = 0; outOfMore = 1; break; }
+            }
+            unsigned bpsFewer = hs_best_possible(set[fewer]);
+            unsigned lowestMate = maxK + extra;
+            for (int i = (int)nMate[sp] - 1; i >= 0; i--) {
+                if (o->mate[sp][i].loc > fewerLoc + maxSp) break;
+                if (o->mate[sp][i].bestPossible < lowestMate) lowestMate = o->mate[sp][i].bestPossible;
+            }
+            if (lowestMate + bpsFewer <= maxK + extra) {
+                if (nCand >= o->poolSize) { res->flags |= SNAPGPU_PFLAG_POOL_EXHAUSTED; return -1; }
+                unsigned li = lowestMate + bpsFewer;
+                PCand *c = &o->cand[nCand];
+                c->loc = fewerLoc; c->setPair = sp; c->mateIndex = nMate[sp] - 1; c->seedOffset = fewerSeed;
+                c->bestPossible = bpsFewer; c->next = o->lists[li]; c->anchor = -1;
+                o->lists[li] = (int)nCand;
+                nCand++;
+                if (li > maxUsedList) maxUsedList = li;
+            }
+            if (!hs_next_lower(set[fewer], &fewerLoc, &fewerSeed)) break;
+        }
+    }
+    /* phase 3: score and merge (:516-718) */
+    double pBest = 0, pAll = 0;
+    unsigned bestPairScore = 65536, scoreLimit = maxK + extra, list = 0;
+    uint32_t bestLoc[2] = {0, 0}, bestScore[2] = {0, 0};
+    int bestDir[2] = {0, 0};
+    const uint32_t minSp = o->p.minSpacing;
+    while (list <= maxUsedList && list <= scoreLimit) {
+        if (o->lists[list] < 0) { list++; continue; }
+        const int ci = o->lists[list];
+        PCand *c = &o->cand[ci];
+        uint32_t fewerScore;
+        double fewerProb = 0;
+        int fewerOff = 0;
+        p_score_location(o, fewer, spDir[c->setPair][fewer], c->loc, c->seedOffset, scoreLimit, &fewerScore, &fewerProb,
+                         &fewerOff);
+        if (fewerScore != 0xffffffffu) {
+            unsigned mi = c->mateIndex;
+            for (;;) {
+                PMate *m = &o->mate[c->setPair][mi];
+                if (!is_within(m->loc, c->loc, minSp) && m->bestPossible <= scoreLimit - fewerScore) {
+                    if (m->score == 0xfffffffeu || (m->score == 0xffffffffu && m->scoreLimit < scoreLimit - fewerScore)) {
+                        p_score_location(o, more, spDir[c->setPair][more], m->loc, m->seedOffset, scoreLimit - fewerScore,
+                                         &m->score, &m->prob, &m->genomeOffset);
+                        m->scoreLimit = scoreLimit - fewerScore;
+                    }
+                    if (m->score != 0xffffffffu) {
+                        double pairProb = m->prob * fewerProb;
+                        unsigned pairScore = m->score + fewerScore;
+                        int an = c->anchor;
+                        const uint32_t fewerAt = c->loc + (uint32_t)fewerOff, moreAt = m->loc + (uint32_t)m->genomeOffset;
+                        if (an < 0) {   /* :602-626, including the second loop's decrement */
+                            for (int j = ci - 1; j >= 0 && is_within(o->cand[j].loc, fewerAt, 50) &&
+                                                 o->cand[j].setPair == c->setPair; j--)
+                                if (o->cand[j].anchor >= 0) { c->anchor = an = o->cand[j].anchor; break; }
+                            if (an < 0)
+                                for (int j = ci + 1; j >= 0 && j < (int)nCand && is_within(o->cand[j].loc, fewerAt, 50) &&
+                                                     o->cand[j].setPair == c->setPair; j--)
+                                    if (o->cand[j].anchor >= 0) { c->anchor = an = o->cand[j].anchor; break; }
+                        }
+                        int merged;
+                        double oldProb;
+                        if (an < 0) {
+                            if (nAnchor >= o->poolSize) { res->flags |= SNAPGPU_PFLAG_POOL_EXHAUSTED; return -1; }
+                            an = (int)nAnchor++;
+                            PAnchor *a = &o->anchor[an];
+                            a->moreLoc = moreAt; a->fewerLoc = fewerAt; a->prob = pairProb; a->pairScore = (int)pairScore;
+                            merged = 0; oldProb = 0; c->anchor = an;
+                        } else {   /* checkMerge, :1324-1371 */
+                            PAnchor *a = &o->anchor[an];
+                            if (a->moreLoc == INVALID_LOC || !(loc_distance(a->moreLoc, moreAt) < 50 && loc_distance(a->fewerLoc, fewerAt) < 50)) {
+                                a->moreLoc = moreAt; a->fewerLoc = fewerAt; a->prob = pairProb; a->pairScore = (int)pairScore;
+                                oldProb = 0; merged = 0;
+                            } else if ((int)pairScore < a->pairScore || ((int)pairScore == a->pairScore && pairProb > a->prob)) {
+                                oldProb = a->prob; a->prob = pairProb; a->pairScore = (int)pairScore; merged = 0;
+                            } else { merged = 1; oldProb = 0; }
+                        }
+                        if (!merged) {
+                            pAll = pAll - oldProb > 0 ? pAll - oldProb : 0;   /* __max(0, .) */
+                            if (pairScore <= maxK && (pairScore < bestPairScore || (pairScore == bestPairScore && pairProb > pBest))) {
+                                bestPairScore = pairScore;
+                                pBest = pairProb;
+                                bestLoc[fewer] = fewerAt; bestLoc[more] = moreAt;
+                                bestScore[fewer] = fewerScore; bestScore[more] = m->score;
+                                bestDir[fewer] = spDir[c->setPair][fewer]; bestDir[more] = spDir[c->setPair][more];
+                                scoreLimit = bestPairScore + extra;
+                            }
+                            pAll += pairProb;
+                            if (pAll >= 4.9) goto done;
+                        }
+                    }
+                }
+                if (mi == 0 || !is_within(o->mate[c->setPair][mi - 1].loc, c->loc, maxSp)) break;
+                mi--;
+            }
+        }
+        o->lists[list] = c->next;
+    }
+done:
+    res->probabilityOfAllPairs = pAll;
+    res->probabilityOfBestPair = pBest;
+    if (bestPairScore == 65536) {
+        for (int r = 0; r < 2; r++) { res->location[r] = INVALID_LOC; res->mapq[r] = 0; res->score[r] = -1; res->status[r] = SNAPGPU_NOT_FOUND; }
+    } else {
+        for (int r = 0; r < 2; r++) {
+            res->location[r] = bestLoc[r];
+            res->direction[r] = (uint8_t)bestDir[r];
+            res->mapq[r] = oracle_compute_mapq(pAll, pBest, (int)bestScore[r], (int)(popular[0] + popular[1]));
+            res->status[r] = res->mapq[r] > 10 ? SNAPGPU_SINGLE_HIT : SNAPGPU_MULTIPLE_HITS;
+            res->score[r] = (int)bestScore[r];
+        }
+    }
+    return 0;
+}
+
+/* ChimericPairedEndAligner::align (:56-126) */
+static int p_chimeric(POracle *o, const char *b0, const char *q0, unsigned n0, const char *b1, const char *q1, unsigned n1,
+                      snapgpu_pair_result_t *res) {
+    res->status[0] = res->status[1] = SNAPGPU_NOT_FOUND;
+    if (n0 < 50 && n1 < 50) return 0;
+    if (p_align(o, b0, q0, n0, b1, q1, n1, res)) return -1;
+    res->nLocationsScored = o->nScored;
+    res->fromAlignTogether = 1;
+    res->alignedAsPair = 1;
+    if (o->p.forceSpacing) {
+        if (res->status[0] == SNAPGPU_NOT_FOUND) res->fromAlignTogether = 0;
+        return 0;
+    }
+    if (res->status[0] != SNAPGPU_NOT_FOUND && res->status[1] != SNAPGPU_NOT_FOUND) return 0;
+    const char *B[2] = {b0, b1}, *Q[2] = {q0, q1};
+    unsigned N[2] = {n0, n1};
+    for (int r = 0; r < 2; r++) {
+        snapgpu_result_t one;
+        align_read(o->single, B[r], Q[r], N[r], &one, NULL, NULL, NULL);
+        if (one.flags & SNAPGPU_FLAG_READ_TOO_LONG) { res->flags |= SNAPGPU_PFLAG_READ_TOO_LONG; return -1; }
+        res->status[r] = one.result;
+        res->location[r] = one.location;
+        res->direction[r] = one.direction;
+        res->score[r] = one.score;
+        res->mapq[r] = one.mapq / 4;
+        res->nSingleScored += one.nLocationsScored;
+    }
+    res->fromAlignTogether = 0;
+    res->alignedAsPair = 0;
+    return 0;
+}
+
+static snapgpu_aligner_params_t p_single_params(const snapgpu_paired_params_t *p) {
+    snapgpu_aligner_params_t a;
+    memset(&a, 0, sizeof(a));
+    a.maxHitsToConsider = p->maxHits; a.maxK = p->maxK; a.maxReadSize = p->maxReadSize;
+    a.maxSeedsToUse = p->maxSeedsToUse; a.maxSeedCoverage = p->seedCoverage; a.extraSearchDepth = p->extraSearchDepth;
+    return a;
+}
+
+typedef struct {
+    const snapgpu_index_view_t *ix;
+    const snapgpu_paired_params_t *p;
+    const char *b0, *q0, *b1, *q1;
+    const uint64_t *o0, *o1;
+    const uint32_t *l0, *l1;
+    uint64_t n;
+    int chimeric;
+    snapgpu_pair_result_t *out;
+    volatile uint64_t *cursor;
+} PJob;
+
+static void *p_worker(void *arg) {
+    PJob *j = (PJob *)arg;
+    POracle *o = (POracle *)calloc(1, sizeof(POracle));
+    o->ix = j->ix;
+    o->p = *j->p;
+    o->maxSeedsCmd = j->p->maxSeedsToUse < P_MAX_SEEDS ? j->p->maxSeedsToUse : P_MAX_SEEDS;   /* __min(MAX_MAX_SEEDS, .) :47 */
+    unsigned maxSeedsToUse = o->maxSeedsCmd ? o->maxSeedsCmd
+                                            : (unsigned)(j->p->maxReadSize * j->p->seedCoverage / j->ix->seedLen);
+    uint64_t pool = (uint64_t)j->p->maxBigHits * maxSeedsToUse * 2;                         /* :128 */
+    o->poolSize = (unsigned)(pool < j->p->maxCandidatePoolSize ? pool : j->p->maxCandidatePoolSize);
+    o->cand = (PCand *)calloc(o->poolSize + 1, sizeof(PCand));
+    o->mate[0] = (PMate *)calloc(o->poolSize / 2 + 1, sizeof(PMate));
+    o->mate[1] = (PMate *)calloc(o->poolSize / 2 + 1, sizeof(PMate));
+    o->anchor = (PAnchor *)calloc(o->poolSize + 1, sizeof(PAnchor));
+    o->lists = (int *)calloc(j->p->maxK + j->p->extraSearchDepth + 2, sizeof(int));
+    snapgpu_aligner_params_t sp = p_single_params(j->p);
+    if (j->chimeric) o->single = oracle_new(j->ix, &sp, 0);
+    for (;;) {
+        uint64_t b = __atomic_fetch_add(j->cursor, 16, __ATOMIC_RELAXED);
+        if (b >= j->n) break;
+        uint64_t e = b + 16 < j->n ? b + 16 : j->n;
+        for (uint64_t i = b; i < e; i++) {
+            snapgpu_pair_result_t *r = &j->out[i];
+            pair_pre(r);
+            const char *B0 = j->b0 + j->o0[i], *Q0 = j->q0 + j->o0[i], *B1 = j->b1 + j->o1[i], *Q1 = j->q1 + j->o1[i];
+            if (j->chimeric) p_chimeric(o, B0, Q0, j->l0[i], B1, Q1, j->l1[i], r);
+            else { p_align(o, B0, Q0, j->l0[i], B1, Q1, j->l1[i], r); r->nLocationsScored = o->nScored; }
+        }
+    }
+    if (o->single) oracle_delete(o->single);
+    free(o->cand); free(o->mate[0]); free(o->mate[1]); free(o->anchor); free(o->lists); free(o);
+    return NULL;
+}
+
+/* Pairs (reads0[i], reads1[i]); chimeric = 1: ChimericPairedEndAligner::align, 0: the
+ * IntersectingPairedEndAligner alone. */
+int oracle_paired_batch(const snapgpu_index_view_t *ix, const snapgpu_paired_params_t *p, const char *b0, const char *q0,
+                        const uint64_t *o0, const uint32_t *l0, const char *b1, const char *q1, const uint64_t *o1,
+                        const uint32_t *l1, uint64_t n, int chimeric, snapgpu_pair_result_t *out, int nThreads) {
+    if (ix->seedLen < 16 || ix->seedLen > 25) return -1;
+    pthread_once(&g_once, init_tables);
+    if (nThreads < 1) nThreads = 1;
+    volatile uint64_t cursor = 0;
+    PJob job = {ix, p, b0, q0, b1, q1, o0, o1, l0, l1, n, chimeric, out, &cursor};
+    pthread_t *th = (pthread_t *)calloc((size_t)nThreads, sizeof(pthread_t));
+    for (int t = 0; t < nThreads; t++) pthread_create(&th[t], NULL, p_worker, &job);
+    for (int t = 0; t < nThreads; t++) pthread_join(th[t], NULL);
+    free(th);
+    return 0;
+}

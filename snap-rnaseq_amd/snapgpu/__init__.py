@@ -32,6 +32,16 @@ RESULT_DTYPE = np.dtype([
 ])
 assert RESULT_DTYPE.itemsize == C.sizeof(_ffi.Result)
 
+# snapgpu_pair_result_t (include/snapgpu.h): PairedAlignmentResult (PairedEndAligner.h:31-55)
+PAIR_RESULT_DTYPE = np.dtype([
+    ("location", "<u4", (2,)), ("score", "<i4", (2,)), ("mapq", "<i4", (2,)), ("status", "u1", (2,)),
+    ("direction", "u1", (2,)), ("fromAlignTogether", "u1"), ("alignedAsPair", "u1"), ("flags", "<u2"),
+    ("nLocationsScored", "<u4"), ("nSingleScored", "<u4"), ("reserved", "<u4"), ("reserved2", "<u4"),
+    ("probabilityOfAllPairs", "<f8"), ("probabilityOfBestPair", "<f8"),
+])
+assert PAIR_RESULT_DTYPE.itemsize == 64
+PFLAG_POOL_EXHAUSTED, PFLAG_READ_TOO_LONG, PFLAG_DEFERRED, PFLAG_MAPQ_FIXED = 0x01, 0x02, 0x04, 0x08
+
 # snapgpu_search_t / snapgpu_multi_hit_t (include/snapgpu.h)
 SEARCH_DTYPE = np.dtype([("searchRadius", "<u4"), ("searchLocation", "<u4"), ("searchDirection", "<u4"),
                          ("reserved", "<u4")])

@@ -49,6 +49,16 @@ class AlignerParams(C.Structure):
     ]
 
 
+class PairedParams(C.Structure):
+    """snapgpu_paired_params_t (PairedAligner.cpp:462-482 construction arguments)."""
+    _fields_ = [
+        ("maxHits", C.c_uint32), ("maxK", C.c_uint32), ("maxSeedsToUse", C.c_uint32),
+        ("extraSearchDepth", C.c_uint32), ("minSpacing", C.c_uint32), ("maxSpacing", C.c_uint32),
+        ("maxBigHits", C.c_uint32), ("maxCandidatePoolSize", C.c_uint32), ("maxReadSize", C.c_uint32),
+        ("forceSpacing", C.c_uint32), ("seedCoverage", C.c_double),
+    ]
+
+
 class SynthGenomeParams(C.Structure):
     _fields_ = [
         ("seed", C.c_uint64),
@@ -277,6 +287,12 @@ _PROTOS += [
                                        C.c_char_p, C.POINTER(SingleStats)]),
     ("snapgpu_aligner_index", C.c_void_p, [C.c_void_p]),
     ("snapgpu_aligner_get_params", C.c_int, [C.c_void_p, C.POINTER(AlignerParams)]),
+    ("snapgpu_paired_params_default", None, [C.POINTER(PairedParams)]),
+    ("snapgpu_paired_aligner_create", C.c_void_p, [C.c_int, C.c_void_p, C.POINTER(PairedParams)]),
+    ("snapgpu_paired_aligner_destroy", None, [C.c_void_p]),
+    ("snapgpu_paired_align_batch", C.c_int, [C.c_void_p, C.POINTER(Reads), C.POINTER(Reads), C.c_void_p]),
+    ("snapgpu_paired_intersect_batch", C.c_int, [C.c_void_p, C.POINTER(Reads), C.POINTER(Reads), C.c_void_p]),
+    ("snapgpu_paired_aligner_single", C.c_void_p, [C.c_void_p]),
 ]
 
 CIGAR_MAX_OPS = 64   # SNAPGPU_CIGAR_MAX_OPS

@@ -13,6 +13,7 @@ TSV/JSON expected outputs.
     python3 tests/golden/make_golden.py --only-cigar     # CIGAR calls + SAM records only
     python3 tests/golden/make_golden.py --only-refindex  # reference-built index + seedLen fixtures
     python3 tests/golden/make_golden.py --only-single    # `snap-rna single` end-to-end SAM fixtures
+    python3 tests/golden/make_golden.py --only-paired    # Intersecting + Chimeric paired-end aligner runs
 """
 import hashlib
 import json
@@ -30,8 +31,8 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 import snapgpu  # noqa: E402
 from readsets import edge_reads  # noqa: E402
-from golden_common import (PARAM_SETS, C1, C2, MULTIHIT_RUNS, ref_tsv_to_canonical, ref_tsvx_to_canonical,  # noqa: E402
-                           digest)
+from golden_common import (PARAM_SETS, C1, C2, MULTIHIT_RUNS, PAIRED_RUNS, ref_tsv_to_canonical,  # noqa: E402
+                           ref_tsvx_to_canonical, digest)
 
 REF_BIN = os.path.join(ROOT, "oracle", "_ref")
 SNAP = os.path.join(REF_BIN, "snap-rna")
@@ -328,8 +329,119 @@ def single_fixtures(work):
             dst.write(gzip.compress(src.read(), compresslevel=9, mtime=0))
 
 
+def paired_reads(path0, path1, seqs, rng):
+    """Read pairs over small.fa: proper pairs (either mate first, either strand, inserts
+    150-700), with substitutions/indels; overlapping mates (insert < minSpacing); inserts past
+    maxSpacing; chimeric pairs (mates from unrelated places); one or both mates random; short
+    mates (< 50, IntersectingPairedEndAligner.cpp:186 / ChimericPairedEndAligner.cpp:61);
+    N-rich mates (> maxK Ns over the pair, :226); same-orientation mates; 150-base mates."""
+    comp = str.maketrans("ACGTN", "TGCAN")
+    rc = lambda x: x.translate(comp)[::-1]
+    names = list(seqs)
+
+    def mutate(s):
+        s = list(s)
+        for _ in range(rng.choice([0, 0, 0, 1, 2, 3, 5, 8])):
+            s[rng.randrange(len(s))] = rng.choice("ACGT")
+        if rng.random() < 0.08:
+            j = rng.randrange(5, len(s) - 5)
+            s = s[:j] + s[j + rng.randrange(1, 4):] if rng.random() < 0.5 else s[:j] + list("TGA"[:rng.randrange(1, 4)]) + s[j:]
+        return "".join(s)
+
+    def rand_seq(L):
+        return "".join(rng.choice("ACGT") for _ in range(L))
+
+    def frag_pair(L0, L1, ins):
+        c = rng.choice(names)
+        g = seqs[c]
+        pos = rng.randrange(0, max(1, len(g) - ins - 1))
+        f = g[pos:pos + ins]
+        if rng.random() < 0.5:
+            f = rc(f)
+        return f[:L0], rc(f[len(f) - L1:])
+
+    pairs = []
+    for i in range(2400):
+        u = rng.random()
+        L0 = L1 = rng.choice([101, 101, 101, 100, 90, 150, 75, 60])
+        if u < 0.62:
+            a, b = frag_pair(L0, L1, rng.randrange(max(L0, 150), 700))
+        elif u < 0.67:
+            a, b = frag_pair(L0, L1, rng.randrange(L0, L0 + 40))          # mates overlap: within minSpacing
+        elif u < 0.71:
+            a, b = frag_pair(L0, L1, rng.randrange(1050, 4000))           # beyond maxSpacing
+        elif u < 0.79:
+            a, _ = frag_pair(L0, L1, 400)                                  # chimeric
+            _, b = frag_pair(L0, L1, 400)
+        elif u < 0.84:
+            a, b = frag_pair(L0, L1, 400)
+            if rng.random() < 0.5:
+                a = rand_seq(L0)
+            else:
+                b = rand_seq(L1)
+        elif u < 0.86:
+            a, b = rand_seq(L0), rand_seq(L1)
+        elif u < 0.90:
+            a, b = frag_pair(L0, L1, 400)
+            if rng.random() < 0.5:
+                a = a[:rng.randrange(20, 50)]
+            else:
+                b = b[:rng.randrange(20, 50)]
+            if rng.random() < 0.2:
+                a, b = a[:40], b[:45]
+        elif u < 0.93:
+            a, b = frag_pair(L0, L1, 400)
+            a = "".join("N" if rng.random() < 0.12 else ch for ch in a)
+        elif u < 0.96:
+            a, b = frag_pair(L0, L1, 400)
+            b = rc(b)                                                      # same orientation
+        else:
+            a, b = frag_pair(L0, L1, rng.randrange(200, 500))
+            a, b = b, a
+        if rng.random() < 0.5:
+            a, b = b, a
+        a, b = mutate(a) if len(a) > 12 else a, mutate(b) if len(b) > 12 else b
+        qa, qb = ["I"] * len(a), ["I"] * len(b)
+        if rng.random() < 0.1:
+            qa = [rng.choice("#+5?I") for _ in a]
+        pairs.append((a, "".join(qa), b, "".join(qb)))
+    with open(path0, "w") as f0, open(path1, "w") as f1:
+        for i, (a, qa, b, qb) in enumerate(pairs):
+            f0.write(f"@p{i}/1\n{a}\n+\n{qa}\n")
+            f1.write(f"@p{i}/2\n{b}\n+\n{qb}\n")
+
+
+def paired_fixtures(work):
+    """`ref_harness paired`: IntersectingPairedEndAligner::align and ChimericPairedEndAligner::align
+    (constructed as PairedAligner.cpp:462-482) for every pair, under PAIRED_RUNS."""
+    rng = random.Random(61)
+    fa = os.path.join(HERE, "small.fa")
+    seqs, name = {}, None
+    for line in open(fa):
+        line = line.strip()
+        if line.startswith(">"):
+            name = line[1:].split()[0]
+            seqs[name] = []
+        else:
+            seqs[name].append(line.upper())
+    seqs = {k: "".join(v) for k, v in seqs.items()}
+    fq0, fq1 = os.path.join(HERE, "paired_1.fq"), os.path.join(HERE, "paired_2.fq")
+    paired_reads(fq0, fq1, seqs, rng)
+    idx = os.path.join(work, "pidx")
+    ref_index(fa, idx)
+    for name, p in PAIRED_RUNS.items():
+        args = [str(p[k]) for k in ("maxHits", "maxK", "numSeeds", "extra", "minSpacing", "maxSpacing", "maxBigHits")]
+        with open(os.path.join(HERE, f"expected_paired_{name}.tsv"), "w") as f:
+            f.write(run([HARNESS, "paired", idx, fq0, fq1] + args))
+
+
 def main():
     work = tempfile.mkdtemp(prefix="golden_")
+    if "--only-paired" in sys.argv:
+        paired_fixtures(work)
+        shutil.rmtree(work, ignore_errors=True)
+        print("paired-end fixtures written to", HERE)
+        return
     if "--only-single" in sys.argv:
         single_fixtures(work)
         shutil.rmtree(work, ignore_errors=True)
@@ -371,6 +483,7 @@ def main():
     cigar_fixtures(work)
     refindex_fixtures(work)
     single_fixtures(work)
+    paired_fixtures(work)
 
     # 2. lookupSeed golden: seeds from the genome, their RCs, mutated and random seeds
     rng = random.Random(9)

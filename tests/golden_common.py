@@ -49,6 +49,15 @@ def ref_tsvx_to_canonical(text):
 # multi-hit / windowed-search fixture runs: name -> (maxHitsToGet, PARAM_SETS key)
 MULTIHIT_RUNS = {"mh8": (8, "default"), "mh1": (1, "k5"), "mh64": (64, "h16")}
 
+# ref_harness paired runs (PairedAligner.cpp:462-482).  "default" = the paired CLI defaults
+# (AlignerOptions.cpp:73-77, PairedAligner.cpp:57-58,231-235): maxHits 16000, maxDist 15,
+# 8 seeds, extraSearchDepth 2, spacing 50..1000, intersecting maxBigHits 16000.
+PAIRED_RUNS = {
+    "default": dict(maxHits=16000, maxK=15, numSeeds=8, extra=2, minSpacing=50, maxSpacing=1000, maxBigHits=16000),
+    "tight": dict(maxHits=300, maxK=8, numSeeds=4, extra=1, minSpacing=100, maxSpacing=500, maxBigHits=300),
+    "wide": dict(maxHits=2000, maxK=20, numSeeds=12, extra=3, minSpacing=0, maxSpacing=3000, maxBigHits=64),
+}
+
 
 def digest(text):
     return hashlib.sha256(text.encode()).hexdigest()

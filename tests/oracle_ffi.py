@@ -35,6 +35,9 @@ def oracle_lib():
         o.oracle_cigar.argtypes = [C.POINTER(F.IndexView), C.c_uint32, C.c_char_p, C.c_int, C.c_int,
                                    C.POINTER(C.c_uint32), C.POINTER(C.c_int)]
         o.oracle_cigar.restype = C.c_int
+        o.oracle_paired_batch.argtypes = [C.POINTER(F.IndexView), C.POINTER(F.PairedParams)] + [C.c_void_p] * 8 + \
+            [C.c_uint64, C.c_int, C.c_void_p, C.c_int]
+        o.oracle_paired_batch.restype = C.c_int
         o.oracle_compute_mapq.argtypes = [C.c_double, C.c_double, C.c_int, C.c_int]
         o.oracle_compute_mapq.restype = C.c_int
         _orc = o
@@ -53,6 +56,51 @@ def oracle_align(index, reads, params, n_threads=8):
                                          out.ctypes.data, n_threads)
     assert rc == 0
     return out[:n]
+
+
+def oracle_paired(index, reads0, reads1, params, chimeric=True, n_threads=8):
+    """CPU restatement of ChimericPairedEndAligner::align (or IntersectingPairedEndAligner::align
+    alone) for every pair (reads0[i], reads1[i])."""
+    import snapgpu
+    assert reads0.n == reads1.n
+    v = index.view()
+    n = reads0.n
+    out = np.zeros(max(1, n), dtype=snapgpu.PAIR_RESULT_DTYPE)
+    a, b = reads0._p.contents, reads1._p.contents
+    rc = oracle_lib().oracle_paired_batch(C.byref(v), C.byref(params), a.bases, a.quals, C.cast(a.offsets, C.c_void_p),
+                                          C.cast(a.lengths, C.c_void_p), b.bases, b.quals,
+                                          C.cast(b.offsets, C.c_void_p), C.cast(b.lengths, C.c_void_p), n,
+                                          int(chimeric), out.ctypes.data, n_threads)
+    assert rc == 0
+    return out[:n]
+
+
+PAIR_FIELDS = ("status", "location", "direction", "score", "mapq")
+
+
+def paired_tsv_rows(res, chimeric=True):
+    """The ref_harness paired columns of one aligner (canonical text per pair)."""
+    rows = []
+    for r in res:
+        f = [int(r["status"][0]), int(r["status"][1]), int(r["location"][0]), int(r["location"][1]),
+             int(r["direction"][0]), int(r["direction"][1]), int(r["score"][0]), int(r["score"][1]),
+             int(r["mapq"][0]), int(r["mapq"][1])]
+        if chimeric:
+            f += [int(r["fromAlignTogether"]), int(r["alignedAsPair"]), int(r["nLocationsScored"]) + int(r["nSingleScored"])]
+        else:
+            f += [int(r["nLocationsScored"])]
+        rows.append("\t".join(map(str, f)))
+    return rows
+
+
+def ref_paired_rows(path):
+    """Split ref_harness paired output into (intersecting rows, chimeric rows)."""
+    inter, chim = [], []
+    for line in open(path):
+        c = line.rstrip("\n").split("\t")
+        inter.append("\t".join(c[1:12]))
+        chim.append("\t".join(c[12:25]))
+    return inter, chim
 
 
 def oracle_align_ex(index, reads, params, search=None, max_hits_to_get=0, n_threads=8):

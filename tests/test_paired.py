@@ -1,0 +1,74 @@
+"""Paired-end row f2: IntersectingPairedEndAligner + ChimericPairedEndAligner.
+
+Fixtures: tests/golden/paired_{1,2}.fq (2,400 pairs over small.fa: proper pairs either way round,
+overlapping mates, inserts past maxSpacing, chimeric and random mates, short and N-rich mates) and
+expected_paired_<run>.tsv, the reference's own IntersectingPairedEndAligner::align and
+ChimericPairedEndAligner::align outputs (`ref_harness paired`, constructed as
+PairedAligner.cpp:462-482) under the three PAIRED_RUNS of golden_common.py.
+
+* CPU: the C restatement (oracle/snap_oracle.c, paired section) against those fixtures, every
+  field of both aligners, including the locations-scored counters.
+* GPU: snapgpu_paired_intersect_batch / snapgpu_paired_align_batch against the same fixtures and
+  against the restatement (including the MAPQ inputs, bitwise).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import snapgpu
+from snapgpu import _ffi as F
+from golden_common import PAIRED_RUNS
+from oracle_ffi import oracle_paired, paired_tsv_rows, ref_paired_rows
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+G = os.path.join(HERE, "golden")
+
+
+def params_of(run):
+    p = F.PairedParams()
+    for k, v in dict(maxCandidatePoolSize=1000000, maxReadSize=500, forceSpacing=0, seedCoverage=0.0).items():
+        setattr(p, k, v)
+    d = PAIRED_RUNS[run]
+    p.maxHits, p.maxK, p.maxSeedsToUse, p.extraSearchDepth = d["maxHits"], d["maxK"], d["numSeeds"], d["extra"]
+    p.minSpacing, p.maxSpacing, p.maxBigHits = d["minSpacing"], d["maxSpacing"], d["maxBigHits"]
+    return p
+
+
+@pytest.fixture(scope="module")
+def world():
+    idx = snapgpu.GenomeIndex.build(snapgpu.Genome.from_fasta(os.path.join(G, "small.fa"), 500), 20, 4)
+    r0 = snapgpu.Reads.from_fastq(os.path.join(G, "paired_1.fq"))
+    r1 = snapgpu.Reads.from_fastq(os.path.join(G, "paired_2.fq"))
+    assert r0.n == r1.n == 2400
+    return idx, r0, r1
+
+
+def _cmp(got_rows, want_rows):
+    assert len(got_rows) == len(want_rows)
+    bad = [(i, g, w) for i, (g, w) in enumerate(zip(got_rows, want_rows)) if g != w]
+    return bad
+
+
+@pytest.mark.parametrize("run", list(PAIRED_RUNS))
+def test_oracle_paired_matches_reference(world, run):
+    idx, r0, r1 = world
+    p = params_of(run)
+    inter_want, chim_want = ref_paired_rows(os.path.join(G, f"expected_paired_{run}.tsv"))
+    inter = oracle_paired(idx, r0, r1, p, chimeric=False)
+    bad = _cmp(paired_tsv_rows(inter, chimeric=False), inter_want)
+    assert not bad, f"intersecting: {len(bad)} pairs differ, first {bad[:3]}"
+    chim = oracle_paired(idx, r0, r1, p, chimeric=True)
+    bad = _cmp(paired_tsv_rows(chim, chimeric=True), chim_want)
+    assert not bad, f"chimeric: {len(bad)} pairs differ, first {bad[:3]}"
+
+
+def test_oracle_paired_outcome_mix(world):
+    """The fixture exercises every branch the GPU path has to reproduce."""
+    idx, r0, r1 = world
+    inter_want, chim_want = ref_paired_rows(os.path.join(G, "expected_paired_default.tsv"))
+    chim = [row.split("\t") for row in chim_want]
+    together = sum(1 for c in chim if c[10] == "1")
+    fallback = sum(1 for c in chim if c[10] == "0" and c[0] != "0")
+    untouched = sum(1 for c in chim if c[0] == "0" and c[1] == "0" and c[2] == str(0xFFFFFFFF))
+    assert together > 1000 and fallback > 100 and untouched > 10
