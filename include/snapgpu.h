@@ -529,7 +529,8 @@ typedef struct snapgpu_pair_result {
     uint16_t flags;                /* SNAPGPU_PFLAG_* */
     uint32_t nLocationsScored;     /* IntersectingPairedEndAligner::getLocationsScored() delta */
     uint32_t nSingleScored;        /* the fallback BaseAligner's getLocationsScored() delta */
-    uint32_t reserved, reserved2;
+    uint32_t popularSeedsSkipped;  /* both reads' popular seeds (the MAPQ input, :741) */
+    uint32_t reserved;
     double   probabilityOfAllPairs;   /* the intersecting aligner's MAPQ inputs (align()'s locals) */
     double   probabilityOfBestPair;
 } snapgpu_pair_result_t;   /* 64 bytes */
@@ -543,7 +544,7 @@ typedef struct snapgpu_paired_aligner snapgpu_paired_aligner_t;
 /* NULL (and snapgpu_last_error) without a HIP device: there is no CPU fallback. */
 snapgpu_paired_aligner_t *snapgpu_paired_aligner_create(int device, const snapgpu_index_t *idx,
                                                         const snapgpu_paired_params_t *p);
-void snapgpu_paired_aligner_destroy(snapgpu_paired_aligner_t *pa);
+void snapgpu_paired_aligner_free(snapgpu_paired_aligner_t *pa);
 /* ChimericPairedEndAligner::align for pair i = (reads0[i], reads1[i]), every i, in order. */
 int snapgpu_paired_align_batch(snapgpu_paired_aligner_t *pa, const snapgpu_reads_t *reads0,
                                const snapgpu_reads_t *reads1, snapgpu_pair_result_t *out);

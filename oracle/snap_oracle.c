@@ -1275,6 +1275,7 @@ static int p_align(POracle *o, const char *b0, const char *q0, unsigned n0, cons
 done:
     res->probabilityOfAllPairs = pAll;
     res->probabilityOfBestPair = pBest;
+    res->popularSeedsSkipped = popular[0] + popular[1];
     if (bestPairScore == 65536) {
         for (int r = 0; r < 2; r++) { res->location[r] = INVALID_LOC; res->mapq[r] = 0; res->score[r] = -1; res->status[r] = SNAPGPU_NOT_FOUND; }
     } else {

@@ -56,7 +56,7 @@ struct DevTables {
 // The seedLen-independent tables (indel, phred, perfect, mapqT), one copy per device, set
 // once by the host: a global's address is a constant the compiler rematerializes, where a
 // table pointer argument is one more SGPR pair to keep live (and spill) in the scorer.
-__device__ DevTables g_tab;
+static __device__ DevTables g_tab;   // per translation unit (aligner.hip, paired.hip): each sets its own
 
 // HashTableElement (BaseAligner.h:188-214) in the HBM arena: a 48-byte header of
 // the fields the kernels read and write, then the per-candidate seed offsets.  Reads
@@ -630,7 +630,7 @@ enum : uint32_t { DIAG_SEED_LOOP = 1, DIAG_SCORE_LOOP = 2, DIAG_CHAIN = 3, DIAG_
                   DIAG_OVERDUE = 16 };
 // A read that runs longer than this (100 MHz s_memrealtime ticks, 2 s) is abandoned.
 constexpr uint64_t READ_DEADLINE_TICKS = 200000000ull;
-__device__ uint32_t g_diag[4];
+static __device__ uint32_t g_diag[4];
 __device__ __forceinline__ void diag_report(uint32_t code, uint32_t a, uint32_t b) {
     if (atomicCAS(&g_diag[0], 0u, code) == 0u) { g_diag[1] = a; g_diag[2] = b; }
 }

@@ -2171,3 +2171,24 @@ int snapgpu_copy_peak(snapgpu_aligner_t *a, uint64_t bytes, double *ms) {
 }
 
 }  // extern "C"
+
+// ------------------------------------------------- internal hand-off to paired.hip
+// The paired-end aligner (paired.hip) runs over the index one snapgpu_aligner uploaded (the one
+// its chimeric fallback uses): the index, genome and table arguments of its kernels.
+int snapgpu_internal_index_args(const snapgpu_aligner_t *a, sgk::KArgs *A, int *device) {
+    if (!a || !A) return SNAPGPU_EINVAL;
+    memset(A, 0, sizeof(*A));
+    const snapgpu_index_t *idx = a->idx;
+    A->slots = a->dSlots; A->tableBase = a->dTableBase; A->tableSize = a->dTableSize; A->overflow = a->dOverflow;
+    A->genome = a->dGenome; A->pieces = a->dPieces; A->nPieces = (int32_t)idx->genome->pieceOffsets.size();
+    A->gpl = a->dGPlanes; A->hasIupac = idx->hasIupac ? 1u : 0u;
+    A->nBases = idx->genome->nBases; A->seedLen = idx->seedLen; A->nTables = idx->nTables;
+    A->padding = idx->genome->chromosomePadding;
+    A->tab = a->dTab;
+    A->kRows = 31;
+    if (device) *device = a->device;
+    return a->failed ? SNAPGPU_EDEVICE : SNAPGPU_OK;
+}
+
+void snapgpu_internal_fill_tables(sgk::DevTables *t, uint32_t seedLen) { fillTables(*t, seedLen); }
+bool snapgpu_internal_aligner_failed(const snapgpu_aligner_t *a) { return a && a->failed; }

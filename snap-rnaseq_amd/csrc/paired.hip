@@ -1,0 +1,1055 @@
+// paired.hip -- gfx950 paired-end aligner: IntersectingPairedEndAligner::align
+// (SNAPLib/IntersectingPairedEndAligner.cpp:142-753) for a batch of read pairs, one wave per pair,
+// and ChimericPairedEndAligner::align (ChimericPairedEndAligner.cpp:56-126) on the host around it,
+// whose single-end fallback is the GPU BaseAligner of aligner.hip.
+//
+// Per pair the wave runs the reference's three phases with its control flow kept sequential and
+// each step's inner work spread over the lanes:
+//   1. seeds: the seed offsets depend only on the read's bases, so they are chosen first (scalar
+//      SeedSequencer walk); the lookups then run one lane per seed; the hit sets
+//      (HashTableHitSet, :844-899) are assembled in the reference's order afterwards, because
+//      where a disjoint hit set begins depends on which lookups were recorded.
+//   2. intersection (:357-511): the walk over both ends' hit sets is sequential; every hit-set
+//      step (first hit, binary search per lookup, next lower hit, best possible score) is one lane
+//      per lookup plus a wave reduction; mate candidates, scoring candidates and merge anchors live
+//      in a per-wave HBM pool.
+//   3. scoring (:516-718): candidates in best-possible-score order; scoreLocation (:755-841) is
+//      the byte-compare Landau-Vishkin of align_device.h (one lane per diagonal).
+// Pass 1 takes pairs of reads <= 128 bases with pools sized for ordinary pairs; pairs with a longer
+// read, or whose pools overflow, are deferred to pass 2 (reads <= 512, pools of the reference's
+// size on a small grid).  A pair that exceeds the reference's own pool is flagged: the reference
+// exits there (soft_exit, :436-439, :482-485, :634-637).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "align_device.h"
+#include "internal.h"
+
+int snapgpu_internal_index_args(const snapgpu_aligner_t *a, sgk::KArgs *A, int *device);
+void snapgpu_internal_fill_tables(sgk::DevTables *t, uint32_t seedLen);
+bool snapgpu_internal_aligner_failed(const snapgpu_aligner_t *a);
+
+namespace sgk {
+namespace pe {
+
+constexpr int LCAP = 32;                    // lookups per hit set (MAX_MAX_SEEDS = 30, IntersectingPairedEndAligner.h:93)
+constexpr uint32_t UNSCORED = 0xfffffffeu;  // ScoringMateCandidate::score before scoring (-2)
+constexpr int MAX_LISTS = 64;               // scoringCandidates[maxK + extraSearchDepth + 1]
+
+struct PArgs {
+    KArgs X;                                // index, genome, tables (aligner.hip's upload)
+    const char *bases[2], *quals[2];
+    const uint64_t *offsets[2];
+    const uint32_t *lengths[2];
+    uint32_t nPairs;                        // pairs in this launch (pairList entries in pass 2)
+    const uint32_t *pairList;               // pass 2: pair indices; pass 1: nullptr (identity)
+    uint32_t *deferList, *deferCount;       // pass 1 -> pass 2
+    snapgpu_pair_result_t *out;
+    uint32_t *counter;                      // work queue
+    uint32_t maxK, extra, maxSeedsCmd, minSpacing, maxSpacing, maxBigHits, maxReadSize;
+    double seedCoverage;
+    char *pool;                             // per block: candidates, mates[2], anchors
+    uint64_t poolStride;
+    uint32_t candCap, mateCap, anchorCap;   // this pass's pool capacities
+    uint32_t refPool;                       // the reference's scoringCandidatePoolSize (:128)
+    uint32_t maxLen;                        // reads this pass takes (128 or 512)
+};
+
+struct Lookup {                             // HashTableLookup (IntersectingPairedEndAligner.h:101-134)
+    uint32_t seedOffset, nHits, cur, set;
+    uint32_t at;                            // overflow index of hits[0], or the singleton value
+    uint32_t single;
+};
+struct HitSet {                             // HashTableHitSet (IntersectingPairedEndAligner.h:139-194)
+    Lookup lk[LCAP];
+    uint32_t exhausted[LCAP];               // DisjointHitSet::countOfExhaustedHits
+    int32_t curSet;
+    uint32_t nLookups, lastReturned, pad;
+};
+struct Mate {                               // ScoringMateCandidate (:401-423)
+    double prob;
+    uint32_t loc, bestPossible, score, scoreLimit, seedOffset;
+    int32_t genomeOffset;
+};
+struct Cand {                               // ScoringCandidate (:425-447), indices for pointers
+    int32_t next, anchor;
+    uint32_t mateIndex, loc, setPair, seedOffset, bestPossible, pad;
+};
+struct Anchor {                             // MergeAnchor (:364-393)
+    double prob;
+    uint32_t moreLoc, fewerLoc;
+    int32_t pairScore, pad;
+};
+static_assert(sizeof(Mate) == 32 && sizeof(Cand) == 32 && sizeof(Anchor) == 24, "pool layout");
+
+template <int MAXLEN>
+struct PLds {
+    static constexpr int NB = MAXLEN / 64;
+    char rd[2][2][MAXLEN + 64];             // [read][direction] bases, upper-cased, zero slack
+    char rq[2][2][MAXLEN + 64];             // qualities in the same coordinates
+    uint32_t win[(MAXLEN + 192) / 4];       // genome window of scoreLocation
+    uint16_t rows[MAX_K][WAVE];             // lv_wave row history
+    int16_t btAct[MAX_K + 1], btMatched[MAX_K + 1];
+    HitSet hs[2][2];                        // [read][direction]
+    uint32_t miss[LCAP];                    // DisjointHitSet::missCount scratch
+    uint32_t sel[LCAP];                     // chosen seed offsets of one read (bit 31: a wrap preceded it)
+    uint32_t look[LCAP][6];                 // per seed: nHits, at, single for FORWARD and RC
+    uint64_t validBits[NB], usedBits[NB];
+    int32_t lists[MAX_LISTS];
+};
+
+__device__ __forceinline__ bool is_within(uint32_t a, uint32_t b, uint32_t d) {   // Util.h:538-541
+    return (a <= b && a + d >= b) || (a >= b && a <= b + d);
+}
+__device__ __forceinline__ uint32_t loc_distance(uint32_t a, uint32_t b) { return a > b ? a - b : b - a; }
+
+__device__ __forceinline__ uint32_t hit_at(const PArgs &P, const Lookup &l, uint32_t i) {
+    return l.single ? l.at : P.X.overflow[l.at + i];
+}
+
+// --------------------------------------------------------------- hit sets
+// Lane i owns lookup i.  Ties between lookups go to the lowest index, as the reference's
+// in-order scans with strict comparisons do.
+__device__ __forceinline__ uint64_t best_key(bool have, uint32_t v, int lane) {
+    return have ? ((uint64_t)v << 8) | (uint64_t)(255 - lane) : 0ull;
+}
+
+// getFirstHit (:1270-1284)
+template <int MAXLEN>
+__device__ bool hs_first(const PArgs &P, HitSet &h, uint32_t &loc, uint32_t &seedOff) {
+    const int lane = lane_id();
+    bool have = false;
+    uint32_t v = 0;
+    if ((uint32_t)lane < h.nLookups) {
+        const Lookup l = h.lk[lane];
+        if (l.nHits > 0) { v = hit_at(P, l, 0) - l.seedOffset; have = v > 0; }
+    }
+    const uint64_t k = uni64(max_reduce64(best_key(have, v, lane)));
+    loc = 0;
+    if (k == 0) return false;
+    loc = (uint32_t)(k >> 8);
+    seedOff = h.lk[255 - (int)(k & 255)].seedOffset;
+    h.lastReturned = loc;
+    wave_sync();
+    return true;
+}
+
+// getNextHitLessThanOrEqualTo, the version the reference compiles (:1219-1266)
+template <int MAXLEN>
+__device__ bool hs_next_le(const PArgs &P, HitSet &h, uint32_t maxOff, uint32_t &loc, uint32_t &seedOff) {
+    const int lane = lane_id();
+    bool have = false;
+    uint32_t v = 0;
+    if ((uint32_t)lane < h.nLookups) {
+        const Lookup l = h.lk[lane];
+        int lim0 = (int)l.cur, lim1 = (int)l.nHits - 1;
+        const uint32_t maxThis = maxOff + l.seedOffset;
+        uint32_t cur = l.cur;
+        while (lim0 <= lim1) {
+            const uint32_t probe = (uint32_t)(lim0 + lim1) / 2;
+            const uint32_t hp = hit_at(P, l, probe);
+            if (hp <= maxThis && (probe == 0 || hit_at(P, l, probe - 1) > maxThis)) {
+                v = hp - l.seedOffset;
+                have = v > 0;
+                cur = probe;
+                break;
+            }
+            if (hp > maxThis) lim0 = (int)probe + 1;
+            else lim1 = (int)(probe - 1);
+        }
+        if (lim0 > lim1) cur = l.nHits;
+        h.lk[lane].cur = cur;
+    }
+    const uint64_t k = uni64(max_reduce64(best_key(have, v, lane)));
+    wave_sync();
+    if (k == 0) return false;
+    loc = (uint32_t)(k >> 8);
+    seedOff = h.lk[255 - (int)(k & 255)].seedOffset;
+    h.lastReturned = loc;
+    wave_sync();
+    return true;
+}
+
+// getNextLowerHit (:1286-1322)
+template <int MAXLEN>
+__device__ bool hs_next_lower(const PArgs &P, HitSet &h, uint32_t &loc, uint32_t &seedOff) {
+    const int lane = lane_id();
+    bool have = false;
+    uint32_t v = 0;
+    const uint32_t last = h.lastReturned;
+    if ((uint32_t)lane < h.nLookups) {
+        const Lookup l = h.lk[lane];
+        uint32_t cur = l.cur;
+        if (cur != l.nHits && hit_at(P, l, cur) - l.seedOffset == last) cur++;
+        if (cur != l.nHits) {
+            const uint32_t hc = hit_at(P, l, cur);
+            if (hc >= l.seedOffset) { v = hc - l.seedOffset; have = v > 0; }
+        }
+        h.lk[lane].cur = cur;
+    }
+    const uint64_t k = uni64(max_reduce64(best_key(have, v, lane)));
+    wave_sync();
+    if (k == 0) return false;
+    loc = (uint32_t)(k >> 8);
+    seedOff = h.lk[255 - (int)(k & 255)].seedOffset;
+    h.lastReturned = loc;
+    wave_sync();
+    return true;
+}
+
+// computeBestPossibleScoreForCurrentHit (:901-929): the largest miss count of any disjoint hit set
+template <int MAXLEN>
+__device__ uint32_t hs_best_possible(const PArgs &P, PLds<MAXLEN> &S, HitSet &h, uint32_t maxMerge) {
+    const int lane = lane_id();
+    const int nSets = h.curSet + 1;
+    if (lane < nSets) S.miss[lane] = h.exhausted[lane];
+    wave_sync();
+    if ((uint32_t)lane < h.nLookups) {
+        const Lookup l = h.lk[lane];
+        const uint32_t target = h.lastReturned + l.seedOffset;
+        const bool nearCur = l.cur != l.nHits && is_within(hit_at(P, l, l.cur), target, maxMerge);
+        const bool nearPrev = l.cur != 0 && is_within(hit_at(P, l, l.cur - 1), target, maxMerge);
+        if (!(nearCur || nearPrev)) atomicAdd(&S.miss[l.set], 1u);
+    }
+    wave_sync();
+    const uint32_t m = lane < nSets ? S.miss[lane] : 0u;
+    return uni(max_reduce32(m));
+}
+
+// recordLookup (:859-899), uniform: every lane writes the same values
+__device__ __forceinline__ void hs_record(const PArgs &P, HitSet &h, uint32_t seedOffset, uint32_t nHits, uint32_t at,
+                                          uint32_t single, bool begins) {
+    if (begins) { h.curSet = h.curSet + 1; h.exhausted[h.curSet] = 0; }
+    if (nHits == 0) { h.exhausted[h.curSet] = h.exhausted[h.curSet] + 1; wave_sync(); return; }
+    Lookup l;
+    l.cur = 0; l.nHits = nHits; l.seedOffset = seedOffset; l.set = (uint32_t)h.curSet; l.at = at; l.single = single;
+    while (l.nHits > 0 && hit_at(P, l, l.nHits - 1) < l.seedOffset) l.nHits--;   // :882-884
+    h.lk[h.nLookups] = l;
+    h.nLookups = h.nLookups + 1;
+    wave_sync();
+}
+
+// ------------------------------------------------------------ scoreLocation
+// IntersectingPairedEndAligner::scoreLocation (:755-841).  *offset is written only when the
+// reverse LV runs (its netIndel, 0 when it fails), as the reference's genomeLocationOffset.
+template <int MAXLEN>
+__device__ void score_location(const PArgs &P, PLds<MAXLEN> &S, int r, int dir, uint32_t n, uint32_t loc,
+                               uint32_t seedOffset, uint32_t scoreLimit, uint32_t &score, double &prob,
+                               int32_t &offset, uint32_t &nScored) {
+    constexpr int NB = MAXLEN / 64;
+    const KArgs &X = P.X;
+    const int lane = lane_id();
+    nScored++;
+    uint32_t glen = n + MAX_K;
+    bool ok = substring_ok(X, loc, glen);
+    if (!ok) {
+        uint32_t endOffset;
+        if ((uint64_t)loc + n + MAX_K >= X.nBases) endOffset = X.nBases;
+        else {   // getPieceAtLocation(loc + n + MAX_K)->beginningOffset (Genome.cpp:356-374)
+            const uint32_t at = loc + n + MAX_K;
+            int lo = 0, hi = X.nPieces - 1, pc = -1;
+            while (lo <= hi) {
+                const int m = (lo + hi) / 2;
+                if (X.pieces[m] <= at && (m == X.nPieces - 1 || X.pieces[m + 1] > at)) { pc = m; break; }
+                else if (X.pieces[m] <= at) lo = m + 1;
+                else hi = m - 1;
+            }
+            endOffset = pc >= 0 ? X.pieces[pc] : 0u;
+        }
+        glen = endOffset - loc - 1;
+        if (glen >= n - (uint32_t)MAX_K) ok = substring_ok(X, loc, glen);
+    }
+    if (!ok) { score = FAIL_SCORE; prob = 0; return; }
+    // genome bytes [loc - 64, loc + n + 128) into LDS (4-byte aligned start)
+    const int64_t astart = ((int64_t)loc - 64) & ~(int64_t)3;
+    const int nwords = ((int)n + 192 + 4) / 4;
+    const uint32_t *src = (const uint32_t *)(X.genome + astart);
+    for (int i = lane; i < nwords && i < (MAXLEN + 192) / 4; i += WAVE) S.win[i] = src[i];
+    wave_sync();
+    const int w0 = (int)((int64_t)loc - astart);
+    const int kmax = scoreLimit < (uint32_t)(MAX_K - 1) ? (int)scoreLimit : MAX_K - 1;
+    uint32_t rb[NB];
+#pragma unroll
+    for (int b = 0; b < NB; b++) rb[b] = (uint8_t)S.rd[r][dir][b * 64 + lane];
+    Bitmap<NB> F;
+    build_bitmap<NB>(F, rb, rb, false, (const char *)S.win, w0, (int)n, kmax);
+    const char *q = S.rq[r][dir];
+    const int s = (int)seedOffset, t = s + (int)X.seedLen;
+    const LvOut r1 = lv_wave<1, NB>(F, t, (int)n - t, (int)glen - t, (int)scoreLimit, q, S.rows, S.btAct,
+                                    S.btMatched, X.tab);
+    if (r1.score == -1) { score = FAIL_SCORE; prob = 0; return; }
+    const int limitLeft = (int)scoreLimit - r1.score;
+    const LvOut r2 = lv_wave<-1, NB>(F, s - 1, s, s + MAX_K, limitLeft, q, S.rows, S.btAct, S.btMatched, X.tab);
+    offset = r2.netIndel;
+    if (r2.score == -1) { score = FAIL_SCORE; prob = 0; return; }
+    score = (uint32_t)(r1.score + r2.score);
+    prob = r1.prob * r2.prob * X.tab->seedProb;
+}
+
+// ------------------------------------------------------------------ a pair
+struct PairOut {
+    snapgpu_pair_result_t r;
+};
+
+template <int MAXLEN>
+__device__ void write_result(const PArgs &P, uint32_t pi, const snapgpu_pair_result_t &res) {
+    if (lane_id() == 0) P.out[pi] = res;
+}
+
+__device__ __forceinline__ void pre_state(snapgpu_pair_result_t &r) {
+    r.location[0] = r.location[1] = INVALID;
+    r.score[0] = r.score[1] = -1;
+    r.mapq[0] = r.mapq[1] = 0;
+    r.status[0] = r.status[1] = SNAPGPU_NOT_FOUND;
+    r.direction[0] = r.direction[1] = 0;
+    r.fromAlignTogether = 0; r.alignedAsPair = 0; r.flags = 0;
+    r.nLocationsScored = 0; r.nSingleScored = 0; r.popularSeedsSkipped = 0; r.reserved = 0;
+    r.probabilityOfAllPairs = 0; r.probabilityOfBestPair = 0;
+}
+
+template <int MAXLEN>
+__device__ void defer_pair(const PArgs &P, uint32_t pi) {
+    if (!P.deferList) {   // pass 2 never defers (its pools are the reference's); flag instead of losing the pair
+        snapgpu_pair_result_t res;
+        pre_state(res);
+        res.flags = SNAPGPU_PFLAG_POOL_EXHAUSTED;
+        write_result<MAXLEN>(P, pi, res);
+        return;
+    }
+    if (lane_id() == 0) P.deferList[atomicAdd(P.deferCount, 1u)] = pi;
+}
+
+// Phase 1 for read r (IntersectingPairedEndAligner.cpp:259-340): choose the seeds, look them up
+// one lane per seed, then record the hit sets in the reference's order.
+template <int MAXLEN>
+__device__ __forceinline__ void phase1_read(const PArgs &P, PLds<MAXLEN> &S, const int r, const uint32_t nr,
+                                            const uint32_t maxSeeds, uint32_t &totF, uint32_t &totR, uint32_t &popular) {
+    constexpr int NB = MAXLEN / 64;
+    const KArgs &X = P.X;
+    const int lane = lane_id();
+    const uint32_t seedLen = X.seedLen;
+#pragma unroll
+    for (int d = 0; d < 2; d++)
+        if (lane == 0) { S.hs[r][d].nLookups = 0; S.hs[r][d].curSet = -1; S.hs[r][d].lastReturned = 0; }
+    const uint32_t nPossible = nr - seedLen + 1;
+    // Seed::DoesTextRepresentASeed per start position, and a clear seedUsed
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        const uint32_t p = (uint32_t)(b * 64 + lane);
+        bool valid = p < nPossible;
+        for (uint32_t i = 0; valid && i < seedLen; i++) {
+            const char c = S.rd[r][0][p + i];
+            valid = c == 'A' || c == 'C' || c == 'G' || c == 'T';
+        }
+        const uint64_t vb = ballot(valid);
+        if (lane == 0) { S.validBits[b] = vb; S.usedBits[b] = 0; }
+    }
+    wave_sync();
+    // SeedSequencer walk (scalar): offsets do not depend on lookup results
+    uint32_t nSel = 0, next = 0, wrap = 0;
+    bool wrapped = false;
+    for (uint32_t guard = 0; nSel < nPossible && nSel < maxSeeds && guard < 4096; guard++) {
+        if (next >= nPossible) {
+            wrap++;
+            wrapped = true;
+            if (wrap >= seedLen) break;
+            next = X.tab->wrap[wrap];
+        }
+        while (next < nPossible && ((S.usedBits[next >> 6] >> (next & 63)) & 1)) next++;
+        if (next >= nPossible) continue;
+        const uint64_t ub = S.usedBits[next >> 6] | (1ull << (next & 63));
+        wave_sync();
+        S.usedBits[next >> 6] = ub;
+        wave_sync();
+        if (!((S.validBits[next >> 6] >> (next & 63)) & 1)) { next++; continue; }   // :296-302
+        S.sel[nSel] = next | (wrapped ? 0x80000000u : 0u);
+        wrapped = false;
+        nSel++;
+        if ((maxSeeds - nSel + 1) * seedLen + next < nPossible)                      // :333-338
+            next += (nPossible + next) / (maxSeeds - nSel + 1);
+        else next += seedLen;
+    }
+    wave_sync();
+    // the lookups, one lane per seed (GenomeIndex::lookupSeed, GenomeIndex.cpp:971-1086)
+    if ((uint32_t)lane < nSel) {
+        const uint32_t so = S.sel[lane] & 0x7fffffffu;
+        uint64_t f = 0, rv = 0;
+        for (uint32_t i = 0; i < seedLen; i++) {
+            const int v = base_value((uint8_t)S.rd[r][0][so + i]);
+            f |= (uint64_t)v << ((seedLen - i - 1) * 2);
+            rv |= (uint64_t)(v ^ 3) << (i * 2);
+        }
+        const bool comp = (int64_t)f > (int64_t)rv;
+        const uint64_t canon = comp ? rv : f;
+        const uint32_t table = (uint32_t)(canon >> 32), key = (uint32_t)canon;
+        const uint32_t size = (uint32_t)X.tableSize[table];
+        const uint32_t *T = X.slots + 3 * X.tableBase[table];
+        const uint32_t h0 = fmix32(key) % size;
+        bool found = false;
+        uint32_t v1 = 0, v2 = 0;
+        for (uint32_t j = 0;; j++) {   // SNAPHashTable::Lookup probe order (HashTable.h:74-105)
+            if (j > size + 5) break;
+            const uint32_t Sj = j <= 4 ? j * (j + 1) * (2 * j + 1) / 6 : 30 + (j - 4);
+            uint64_t pos = h0 + Sj;
+            if (pos >= size) pos %= size;
+            const uint32_t kj = T[3 * pos], v1j = T[3 * pos + 1];
+            const bool stop = (j == 0) ? (kj == key && v1j != INVALID) : (kj == key || v1j == INVALID);
+            if (stop) {
+                if (j == 0 || v1j != INVALID) { found = true; v1 = v1j; v2 = T[3 * pos + 2]; }
+                break;
+            }
+        }
+        uint32_t nh[2] = {0, 0}, at[2] = {0, 0}, sg[2] = {0, 0};
+        if (found) {
+            for (int side = 0; side < 2; side++) {
+                if (side == 1 && f == rv) { nh[1] = nh[0]; at[1] = at[0]; sg[1] = sg[0]; break; }
+                const uint32_t v = (side == 0) == !comp ? v1 : v2;
+                if (v < X.nBases) { nh[side] = 1; at[side] = v; sg[side] = 1; }
+                else if (v != UNUSED_SIDE) {
+                    const uint32_t o = v - X.nBases;
+                    nh[side] = X.overflow[o];
+                    at[side] = o + 1;
+                }
+            }
+        }
+        S.look[lane][0] = nh[0]; S.look[lane][1] = at[0]; S.look[lane][2] = sg[0];
+        S.look[lane][3] = nh[1]; S.look[lane][4] = at[1]; S.look[lane][5] = sg[1];
+    }
+    wave_sync();
+    // the hit sets in the reference's order (:313-328)
+    bool begins[2] = {true, true};
+    for (uint32_t k = 0; k < nSel; k++) {
+        const uint32_t sk = S.sel[k];
+        if (sk & 0x80000000u) begins[0] = begins[1] = true;
+        const uint32_t so = sk & 0x7fffffffu;
+        for (int d = 0; d < 2; d++) {
+            const uint32_t offset = d == 0 ? so : nr - seedLen - so;
+            const uint32_t nh = S.look[k][3 * d];
+            if (nh < P.maxBigHits) {
+                if (d == 0) totF += nh; else totR += nh;
+                hs_record(P, S.hs[r][d], offset, nh, S.look[k][3 * d + 1], S.look[k][3 * d + 2], begins[d]);
+                begins[d] = false;
+            } else popular++;
+        }
+    }
+    wave_sync();
+}
+
+// Read r of the pair into LDS: Read::init upper-cases; RC data and reversed qualities
+// (:217-224); zero slack.  Returns this lane's count of 'N' (:220).
+template <int MAXLEN>
+__device__ __forceinline__ uint32_t load_read(const PArgs &P, PLds<MAXLEN> &S, const int r, const uint32_t nr,
+                                              const uint64_t offr) {
+    const int lane = lane_id();
+    const char *b = P.bases[r] + offr, *q = P.quals[r] + offr;
+    uint32_t ns = 0;
+    for (int i = lane; i < MAXLEN + 64; i += WAVE) {
+        char c = 0, cq = 0, cc = 0;
+        if ((uint32_t)i < nr) {
+            c = b[i];
+            if (c >= 'a' && c <= 'z') c = (char)(c - 0x20);
+            cq = q[i];
+            cc = c == 'A' ? 'T' : c == 'G' ? 'C' : c == 'C' ? 'G' : c == 'T' ? 'A' : c == 'N' ? 'N' : 0;
+            ns += c == 'N';
+            S.rd[r][1][nr - 1 - i] = cc;
+            S.rq[r][1][nr - 1 - i] = cq;
+        } else {
+            S.rd[r][1][i] = 0;
+            S.rq[r][1][i] = 0;
+        }
+        S.rd[r][0][i] = c;
+        S.rq[r][0][i] = cq;
+    }
+    return ns;
+}
+
+// IntersectingPairedEndAligner::align (:142-753).  Returns after writing out[pi] or deferring.
+// Reads are indexed 0/1; `fewer` / `more` are selects, never array indices (no scratch).
+template <int MAXLEN>
+__device__ void align_pair(const PArgs &P, PLds<MAXLEN> &S, Cand *cand, Mate *mates0, Mate *mates1, Anchor *anchors,
+                           uint32_t pi) {
+    const KArgs &X = P.X;
+    const int lane = lane_id();
+    const uint32_t seedLen = X.seedLen;
+    const uint32_t maxK = P.maxK, extra = P.extra;
+    snapgpu_pair_result_t res;
+    pre_state(res);
+    const uint32_t n0 = P.lengths[0][pi], n1 = P.lengths[1][pi];
+    const uint64_t o0 = P.offsets[0][pi], o1 = P.offsets[1][pi];
+    if (n0 < 50 || n1 < 50) { write_result<MAXLEN>(P, pi, res); return; }         // :186-188
+    if (n0 > P.maxReadSize || n1 > P.maxReadSize) {                                // :211-215 (soft_exit)
+        res.flags |= SNAPGPU_PFLAG_READ_TOO_LONG;
+        write_result<MAXLEN>(P, pi, res);
+        return;
+    }
+    if (n0 > P.maxLen || n1 > P.maxLen) { defer_pair<MAXLEN>(P, pi); return; }
+    uint32_t countNs = load_read<MAXLEN>(P, S, 0, n0, o0) + load_read<MAXLEN>(P, S, 1, n1, o1);
+    wave_sync();
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) countNs += (uint32_t)__shfl_xor((int)countNs, o);
+    countNs = uni(countNs);
+    if (countNs > maxK) { write_result<MAXLEN>(P, pi, res); return; }              // :226-228
+    uint32_t maxSeeds = P.maxSeedsCmd ? P.maxSeedsCmd
+                                      : (uint32_t)((n0 > n1 ? n0 : n1) * P.seedCoverage / seedLen);   // :150-155
+    if (maxSeeds > (uint32_t)LCAP) maxSeeds = LCAP;
+    // ---------------------------------------------------------------- phase 1 (:259-340)
+    uint32_t pop0 = 0, pop1 = 0, t00 = 0, t01 = 0, t10 = 0, t11 = 0;
+    phase1_read<MAXLEN>(P, S, 0, n0, maxSeeds, t00, t01, pop0);
+    phase1_read<MAXLEN>(P, S, 1, n1, maxSeeds, t10, t11, pop1);
+    const uint32_t popularAll = pop0 + pop1;
+    const int more = t00 + t01 > t10 + t11 ? 0 : 1, fewer = 1 - more;            // :342-343
+    const uint32_t nFewer = fewer ? n1 : n0, nMore = fewer ? n0 : n1;
+    // ---------------------------------------------------------------- phase 2 (:357-511)
+    for (int k = lane; k < MAX_LISTS; k += WAVE) S.lists[k] = -1;
+    wave_sync();
+    uint32_t nCand = 0, nAnchor = 0, maxUsedList = 0;
+    const uint32_t maxSp = P.maxSpacing, minSp = P.minSpacing;
+    bool deferIt = false, exhausted = false;
+    for (int sp = 0; sp < 2 && !deferIt && !exhausted; sp++) {
+        // set pair 0 = read0 FORWARD + read1 RC, set pair 1 = read0 RC + read1 FORWARD (:351, :361-367)
+        HitSet &hf = S.hs[fewer][fewer ^ sp];
+        HitSet &hm = S.hs[more][more ^ sp];
+        Mate *ms = sp ? mates1 : mates0;
+        uint32_t nM = 0;
+        uint32_t fewerLoc = 0, fewerSeed = 0, moreLoc, moreSeed = 0;
+        bool outOfMore = false;
+        if (!hs_first<MAXLEN>(P, hf, fewerLoc, fewerSeed)) continue;
+        moreLoc = INVALID;
+        for (;;) {
+            if (moreLoc > fewerLoc + maxSp) {
+                if (!hs_next_le<MAXLEN>(P, hm, fewerLoc + maxSp, moreLoc, moreSeed)) break;
+            }
+            if (moreLoc + maxSp < fewerLoc && (nM == 0 || !is_within(ms[nM - 1].loc, fewerLoc, maxSp))) {
+                if (!hs_next_le<MAXLEN>(P, hf, moreLoc + maxSp, fewerLoc, fewerSeed)) break;
+                continue;
+            }
+            while (moreLoc + maxSp >= fewerLoc && !outOfMore) {
+                const uint32_t bps = hs_best_possible<MAXLEN>(P, S, hm, maxK);
+                if (nM >= P.refPool / 2) { exhausted = true; break; }                   // :436-439
+                if (nM >= P.mateCap) { deferIt = true; break; }
+                Mate m;
+                m.prob = 0; m.loc = moreLoc; m.bestPossible = bps; m.score = UNSCORED; m.scoreLimit = 0xffffffffu;
+                m.seedOffset = moreSeed; m.genomeOffset = 0;
+                ms[nM] = m;
+                nM++;
+                if (!hs_next_lower<MAXLEN>(P, hm, moreLoc, moreSeed)) { moreLoc = 0; outOfMore = true; break; }
+            }
+            if (deferIt || exhausted) break;
+            const uint32_t bpsF = hs_best_possible<MAXLEN>(P, S, hf, maxK);
+            // lowest best possible score of the mates up to maxSpacing above this fewer hit,
+            // 64 mates per step from the lowest up (:469-475)
+            uint32_t lowest = maxK + extra;
+            wave_sync();
+            for (int base = (int)nM - 1; base >= 0; base -= WAVE) {
+                const int i = base - lane;
+                uint32_t ml = 0, mb = 0xffffffffu;
+                if (i >= 0) { ml = ms[i].loc; mb = ms[i].bestPossible; }
+                const uint64_t brk = ballot(i >= 0 && ml > fewerLoc + maxSp);
+                const int first = brk ? (int)__builtin_ctzll(brk) : WAVE;
+                const uint32_t c = (i >= 0 && lane < first) ? mb : 0xffffffffu;
+                const uint32_t mn = ~uni(max_reduce32(~c));
+                if (mn < lowest) lowest = mn;
+                if (brk) break;
+            }
+            if (lowest + bpsF <= maxK + extra) {
+                if (nCand >= P.refPool) { exhausted = true; break; }                    // :482-485
+                if (nCand >= P.candCap) { deferIt = true; break; }
+                const uint32_t li = lowest + bpsF;
+                Cand c;
+                c.next = S.lists[li]; c.anchor = -1; c.mateIndex = nM - 1; c.loc = fewerLoc;
+                c.setPair = (uint32_t)sp; c.seedOffset = fewerSeed; c.bestPossible = bpsF; c.pad = 0;
+                cand[nCand] = c;
+                wave_sync();
+                S.lists[li] = (int32_t)nCand;
+                wave_sync();
+                nCand++;
+                if (li > maxUsedList) maxUsedList = li;
+            }
+            if (!hs_next_lower<MAXLEN>(P, hf, fewerLoc, fewerSeed)) break;
+        }
+    }
+    if (exhausted) { res.flags |= SNAPGPU_PFLAG_POOL_EXHAUSTED; write_result<MAXLEN>(P, pi, res); return; }
+    if (deferIt) { defer_pair<MAXLEN>(P, pi); return; }
+    // ---------------------------------------------------------------- phase 3 (:516-718)
+    double pBest = 0, pAll = 0;
+    uint32_t bestPairScore = 65536, scoreLimit = maxK + extra, list = 0;
+    uint32_t bestLocF = 0, bestLocM = 0, bestScoreF = 0, bestScoreM = 0, bestSp = 0;
+    uint32_t nScored = 0;
+    while (list <= maxUsedList && list <= scoreLimit) {
+        const int ci = S.lists[list];
+        if (ci < 0) { list++; continue; }
+        const Cand c = cand[ci];
+        uint32_t fewerScore = 0;
+        double fewerProb = 0;
+        int32_t fewerOff = 0;
+        // direction of read r in set pair sp: r ^ sp (setPairDirection, :351)
+        score_location<MAXLEN>(P, S, fewer, fewer ^ (int)c.setPair, nFewer, c.loc, c.seedOffset, scoreLimit, fewerScore,
+                               fewerProb, fewerOff, nScored);
+        if (fewerScore != FAIL_SCORE) {
+            Mate *ms = c.setPair ? mates1 : mates0;
+            int32_t anchorOf = c.anchor;
+            uint32_t mi = c.mateIndex;
+            for (;;) {
+                Mate m = ms[mi];
+                if (!is_within(m.loc, c.loc, minSp) && m.bestPossible <= scoreLimit - fewerScore) {
+                    if (m.score == UNSCORED || (m.score == FAIL_SCORE && m.scoreLimit < scoreLimit - fewerScore)) {
+                        score_location<MAXLEN>(P, S, more, more ^ (int)c.setPair, nMore, m.loc, m.seedOffset,
+                                               scoreLimit - fewerScore, m.score, m.prob, m.genomeOffset, nScored);
+                        m.scoreLimit = scoreLimit - fewerScore;
+                        ms[mi] = m;
+                        wave_sync();
+                    }
+                    if (m.score != FAIL_SCORE) {
+                        const double pairProb = m.prob * fewerProb;
+                        const uint32_t pairScore = m.score + fewerScore;
+                        const uint32_t fewerAt = c.loc + (uint32_t)fewerOff, moreAt = m.loc + (uint32_t)m.genomeOffset;
+                        int32_t an = anchorOf;
+                        if (an < 0) {   // :602-626, including the second loop's decrement
+                            for (int j = ci - 1; j >= 0; j--) {
+                                const Cand o = cand[j];
+                                if (!(is_within(o.loc, fewerAt, 50) && o.setPair == c.setPair)) break;
+                                if (o.anchor >= 0) { an = o.anchor; break; }
+                            }
+                            if (an < 0)
+                                for (int j = ci + 1; j >= 0 && j < (int)nCand; j--) {
+                                    const Cand o = cand[j];
+                                    if (!(is_within(o.loc, fewerAt, 50) && o.setPair == c.setPair)) break;
+                                    if (o.anchor >= 0) { an = o.anchor; break; }
+                                }
+                            if (an >= 0) { anchorOf = an; cand[ci].anchor = an; wave_sync(); }
+                        }
+                        bool merged;
+                        double oldProb;
+                        if (an < 0) {
+                            if (nAnchor >= P.refPool) { exhausted = true; break; }               // :634-637
+                            if (nAnchor >= P.anchorCap) { deferIt = true; break; }
+                            an = (int32_t)nAnchor++;
+                            Anchor a;
+                            a.moreLoc = moreAt; a.fewerLoc = fewerAt; a.prob = pairProb; a.pairScore = (int32_t)pairScore; a.pad = 0;
+                            anchors[an] = a;
+                            anchorOf = an;
+                            cand[ci].anchor = an;
+                            wave_sync();
+                            merged = false; oldProb = 0;
+                        } else {   // MergeAnchor::checkMerge (:1324-1371)
+                            Anchor a = anchors[an];
+                            if (a.moreLoc == INVALID ||
+                                !(loc_distance(a.moreLoc, moreAt) < 50 && loc_distance(a.fewerLoc, fewerAt) < 50)) {
+                                a.moreLoc = moreAt; a.fewerLoc = fewerAt; a.prob = pairProb; a.pairScore = (int32_t)pairScore;
+                                oldProb = 0; merged = false;
+                            } else if ((int32_t)pairScore < a.pairScore || ((int32_t)pairScore == a.pairScore && pairProb > a.prob)) {
+                                oldProb = a.prob; a.prob = pairProb; a.pairScore = (int32_t)pairScore; merged = false;
+                            } else { merged = true; oldProb = 0; }
+                            anchors[an] = a;
+                            wave_sync();
+                        }
+                        if (!merged) {
+                            pAll = pAll - oldProb > 0 ? pAll - oldProb : 0;   // __max(0, .)
+                            if (pairScore <= maxK && (pairScore < bestPairScore || (pairScore == bestPairScore && pairProb > pBest))) {
+                                bestPairScore = pairScore;
+                                pBest = pairProb;
+                                bestLocF = fewerAt; bestLocM = moreAt;
+                                bestScoreF = fewerScore; bestScoreM = m.score;
+                                bestSp = c.setPair;
+                                scoreLimit = bestPairScore + extra;
+                            }
+                            pAll += pairProb;
+                            if (pAll >= 4.9) goto doneScoring;
+                        }
+                    }
+                }
+                if (mi == 0 || !is_within(ms[mi - 1].loc, c.loc, maxSp)) break;
+                mi--;
+            }
+            if (deferIt || exhausted) break;
+        }
+        S.lists[list] = c.next;
+        wave_sync();
+    }
+doneScoring:
+    if (exhausted) { res.flags |= SNAPGPU_PFLAG_POOL_EXHAUSTED; write_result<MAXLEN>(P, pi, res); return; }
+    if (deferIt) { defer_pair<MAXLEN>(P, pi); return; }
+    res.nLocationsScored = nScored;
+    res.probabilityOfAllPairs = pAll;
+    res.probabilityOfBestPair = pBest;
+    res.popularSeedsSkipped = popularAll;
+    if (P.pairList) res.flags |= SNAPGPU_PFLAG_DEFERRED;
+    if (bestPairScore == 65536) {
+        res.location[0] = res.location[1] = INVALID;
+        res.mapq[0] = res.mapq[1] = 0;
+        res.score[0] = res.score[1] = -1;
+        res.status[0] = res.status[1] = SNAPGPU_NOT_FOUND;
+    } else {
+        const uint32_t loc0 = fewer == 0 ? bestLocF : bestLocM, loc1 = fewer == 0 ? bestLocM : bestLocF;
+        const uint32_t sc0 = fewer == 0 ? bestScoreF : bestScoreM, sc1 = fewer == 0 ? bestScoreM : bestScoreF;
+        uint32_t fl = 0;
+        const int mq0 = mapq_dev(X.tab, pAll, pBest, sc0, popularAll, &fl);
+        const int mq1 = mapq_dev(X.tab, pAll, pBest, sc1, popularAll, &fl);
+        if (fl & SNAPGPU_FLAG_MAPQ_FIXED) res.flags |= SNAPGPU_PFLAG_MAPQ_FIXED;
+        res.location[0] = loc0; res.location[1] = loc1;
+        res.direction[0] = (uint8_t)(0 ^ bestSp); res.direction[1] = (uint8_t)(1 ^ bestSp);
+        res.mapq[0] = mq0; res.mapq[1] = mq1;
+        res.status[0] = mq0 > 10 ? SNAPGPU_SINGLE_HIT : SNAPGPU_MULTIPLE_HITS;
+        res.status[1] = mq1 > 10 ? SNAPGPU_SINGLE_HIT : SNAPGPU_MULTIPLE_HITS;
+        res.score[0] = (int32_t)sc0; res.score[1] = (int32_t)sc1;
+    }
+    write_result<MAXLEN>(P, pi, res);
+}
+
+template <int MAXLEN>
+__global__ __launch_bounds__(64) void paired_kernel(PArgs P) {
+    __shared__ PLds<MAXLEN> S;
+    char *base = P.pool + (uint64_t)blockIdx.x * P.poolStride;
+    Cand *cand = reinterpret_cast<Cand *>(base);
+    Mate *m0 = reinterpret_cast<Mate *>(base + (uint64_t)P.candCap * sizeof(Cand));
+    Mate *m1 = m0 + P.mateCap;
+    Anchor *an = reinterpret_cast<Anchor *>(m1 + P.mateCap);
+    for (;;) {
+        uint32_t t = 0;
+        if (lane_id() == 0) t = atomicAdd(P.counter, 1u);
+        t = uni(t);
+        if (t >= P.nPairs) break;
+        const uint32_t pi = P.pairList ? P.pairList[t] : t;
+        align_pair<MAXLEN>(P, S, cand, m0, m1, an, pi);
+    }
+}
+
+}  // namespace pe
+}  // namespace sgk
+
+using namespace sgk;
+using namespace sgk::pe;
+
+// ======================================================================= host
+namespace {
+
+#define PCHK(x)                                                                         \
+    do {                                                                                \
+        hipError_t e_ = (x);                                                            \
+        if (e_ != hipSuccess) {                                                         \
+            snapgpu::setError(std::string(#x) + ": " + hipGetErrorString(e_));          \
+            return SNAPGPU_EDEVICE;                                                     \
+        }                                                                               \
+    } while (0)
+
+std::mutex g_tabMu;
+bool g_tabDone[64] = {};
+
+hipError_t ensurePairedTables(int device) {   // this translation unit's g_tab (align_device.h)
+    std::lock_guard<std::mutex> lk(g_tabMu);
+    if (device < 0 || device >= 64) return hipErrorInvalidDevice;
+    if (g_tabDone[device]) return hipSuccess;
+    DevTables t;
+    snapgpu_internal_fill_tables(&t, 20);
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_tab), &t, sizeof(t), 0, hipMemcpyHostToDevice);
+    if (e == hipSuccess) g_tabDone[device] = true;
+    return e;
+}
+
+struct PassPool {
+    char *pool = nullptr;
+    uint64_t stride = 0;
+    int grid = 0;
+    uint32_t candCap = 0, mateCap = 0, anchorCap = 0;
+};
+
+}  // namespace
+
+struct snapgpu_paired_aligner {
+    int device = 0;
+    snapgpu_paired_params_t p{};
+    snapgpu_aligner_t *single = nullptr;   // the chimeric fallback's BaseAligner; owns the index upload
+    KArgs X{};
+    hipStream_t stream = nullptr;
+    PassPool pass[2];
+    uint32_t refPool = 0, maxSeedsCmd = 0;
+    uint32_t *dCounter = nullptr;          // [0] pass 1 queue, [1] pass 2 queue, [2] defer count
+    uint32_t *dDefer = nullptr;
+    snapgpu_pair_result_t *dOut = nullptr;
+    char *dB[2] = {}, *dQ[2] = {};
+    uint64_t *dO[2] = {};
+    uint32_t *dL[2] = {};
+    uint64_t capPairs = 0, capBytes[2] = {0, 0};
+};
+
+static void pfree(void *p) { if (p) (void)hipFree(p); }
+
+static int ensurePairCapacity(snapgpu_paired_aligner_t *pa, uint64_t n, const uint64_t bytes[2]) {
+    if (n > pa->capPairs) {
+        pfree(pa->dOut); pfree(pa->dDefer); pfree(pa->dO[0]); pfree(pa->dO[1]); pfree(pa->dL[0]); pfree(pa->dL[1]);
+        pa->dOut = nullptr; pa->dDefer = nullptr; pa->dO[0] = pa->dO[1] = nullptr; pa->dL[0] = pa->dL[1] = nullptr;
+        pa->capPairs = 0;
+        PCHK(hipMalloc(&pa->dOut, n * sizeof(snapgpu_pair_result_t)));
+        PCHK(hipMalloc(&pa->dDefer, n * 4 + 16));
+        for (int r = 0; r < 2; r++) {
+            PCHK(hipMalloc(&pa->dO[r], n * 8 + 16));
+            PCHK(hipMalloc(&pa->dL[r], n * 4 + 16));
+        }
+        pa->capPairs = n;
+    }
+    for (int r = 0; r < 2; r++)
+        if (bytes[r] + 1024 > pa->capBytes[r]) {
+            pfree(pa->dB[r]); pfree(pa->dQ[r]);
+            pa->dB[r] = pa->dQ[r] = nullptr;
+            pa->capBytes[r] = 0;
+            const uint64_t c = bytes[r] + (bytes[r] >> 3) + 4096;
+            PCHK(hipMalloc(&pa->dB[r], c));
+            PCHK(hipMalloc(&pa->dQ[r], c));
+            PCHK(hipMemset(pa->dB[r], 0, c));
+            PCHK(hipMemset(pa->dQ[r], 0, c));
+            pa->capBytes[r] = c;
+        }
+    return SNAPGPU_OK;
+}
+
+static int allocPass(PassPool &pp, int grid, uint32_t candCap, uint32_t mateCap, uint32_t anchorCap) {
+    pp.grid = grid;
+    pp.candCap = candCap; pp.mateCap = mateCap; pp.anchorCap = anchorCap;
+    pp.stride = ((uint64_t)candCap * sizeof(Cand) + 2ull * mateCap * sizeof(Mate) + (uint64_t)anchorCap * sizeof(Anchor) +
+                 255) & ~255ull;
+    PCHK(hipMalloc(&pp.pool, pp.stride * (uint64_t)grid));
+    return SNAPGPU_OK;
+}
+
+// the intersecting aligner over the whole batch (both passes); records left in pa->dOut
+static int runIntersect(snapgpu_paired_aligner_t *pa, const snapgpu_reads_t *r0, const snapgpu_reads_t *r1,
+                        snapgpu_pair_result_t *out) {
+    const snapgpu_reads_t *R[2] = {r0, r1};
+    const uint64_t n = r0->n;
+    uint64_t bytes[2] = {r0->totalBytes, r1->totalBytes};
+    int rc = ensurePairCapacity(pa, n, bytes);
+    if (rc) return rc;
+    hipStream_t s = pa->stream;
+    for (int r = 0; r < 2; r++) {
+        PCHK(hipMemcpyAsync(pa->dB[r], R[r]->bases, R[r]->totalBytes, hipMemcpyHostToDevice, s));
+        PCHK(hipMemcpyAsync(pa->dQ[r], R[r]->quals, R[r]->totalBytes, hipMemcpyHostToDevice, s));
+        PCHK(hipMemcpyAsync(pa->dO[r], R[r]->offsets, n * 8, hipMemcpyHostToDevice, s));
+        PCHK(hipMemcpyAsync(pa->dL[r], R[r]->lengths, n * 4, hipMemcpyHostToDevice, s));
+    }
+    PCHK(hipMemsetAsync(pa->dCounter, 0, 16, s));
+    PArgs P;
+    memset(&P, 0, sizeof(P));
+    P.X = pa->X;
+    for (int r = 0; r < 2; r++) { P.bases[r] = pa->dB[r]; P.quals[r] = pa->dQ[r]; P.offsets[r] = pa->dO[r]; P.lengths[r] = pa->dL[r]; }
+    P.out = pa->dOut;
+    P.deferList = pa->dDefer; P.deferCount = pa->dCounter + 2;
+    P.maxK = pa->p.maxK; P.extra = pa->p.extraSearchDepth; P.maxSeedsCmd = pa->maxSeedsCmd;
+    P.minSpacing = pa->p.minSpacing; P.maxSpacing = pa->p.maxSpacing; P.maxBigHits = pa->p.maxBigHits;
+    P.maxReadSize = pa->p.maxReadSize; P.seedCoverage = pa->p.seedCoverage;
+    P.refPool = pa->refPool;
+    // pass 1: reads <= 128 bases, pools for ordinary pairs
+    P.nPairs = (uint32_t)n; P.pairList = nullptr; P.counter = pa->dCounter; P.maxLen = 128;
+    P.pool = pa->pass[0].pool; P.poolStride = pa->pass[0].stride;
+    P.candCap = pa->pass[0].candCap; P.mateCap = pa->pass[0].mateCap; P.anchorCap = pa->pass[0].anchorCap;
+    int grid = pa->pass[0].grid;
+    if ((uint64_t)grid > n) grid = (int)n;
+    if (grid > 0) hipLaunchKernelGGL(paired_kernel<128>, dim3(grid), dim3(64), 0, s, P);
+    PCHK(hipGetLastError());
+    uint32_t nDefer = 0;
+    PCHK(hipMemcpyAsync(&nDefer, pa->dCounter + 2, 4, hipMemcpyDeviceToHost, s));
+    PCHK(hipStreamSynchronize(s));
+    if (nDefer) {   // pass 2: long reads and pool overflows, the reference's pool sizes
+        P.nPairs = nDefer; P.pairList = pa->dDefer; P.counter = pa->dCounter + 1; P.maxLen = 512;
+        P.deferList = nullptr;
+        P.pool = pa->pass[1].pool; P.poolStride = pa->pass[1].stride;
+        P.candCap = pa->pass[1].candCap; P.mateCap = pa->pass[1].mateCap; P.anchorCap = pa->pass[1].anchorCap;
+        grid = pa->pass[1].grid;
+        if ((uint32_t)grid > nDefer) grid = (int)nDefer;
+        hipLaunchKernelGGL(paired_kernel<512>, dim3(grid), dim3(64), 0, s, P);
+        PCHK(hipGetLastError());
+    }
+    PCHK(hipMemcpyAsync(out, pa->dOut, n * sizeof(snapgpu_pair_result_t), hipMemcpyDeviceToHost, s));
+    PCHK(hipStreamSynchronize(s));
+    // MAPQ threshold cases re-derived with glibc log10 (as snapgpu_results_download does)
+    for (uint64_t i = 0; i < n; i++) {
+        snapgpu_pair_result_t &r = out[i];
+        if (!(r.flags & SNAPGPU_PFLAG_MAPQ_FIXED)) continue;
+        for (int k = 0; k < 2; k++) {
+            r.mapq[k] = snapgpu_compute_mapq(r.probabilityOfAllPairs, r.probabilityOfBestPair, r.score[k],
+                                             (int)r.popularSeedsSkipped);
+            r.status[k] = r.mapq[k] > 10 ? SNAPGPU_SINGLE_HIT : SNAPGPU_MULTIPLE_HITS;
+        }
+    }
+    for (uint64_t i = 0; i < n; i++)
+        if (out[i].flags & (SNAPGPU_PFLAG_POOL_EXHAUSTED | SNAPGPU_PFLAG_READ_TOO_LONG)) {
+            snapgpu::setError(out[i].flags & SNAPGPU_PFLAG_READ_TOO_LONG
+                                  ? "paired: read longer than maxReadSize (the reference exits, IntersectingPairedEndAligner.cpp:211-215)"
+                                  : "paired: scoring candidate pool exhausted (the reference exits; raise maxCandidatePoolSize)");
+            return SNAPGPU_EINVAL;
+        }
+    return SNAPGPU_OK;
+}
+
+extern "C" {
+
+void snapgpu_paired_params_default(snapgpu_paired_params_t *p) {
+    if (!p) return;
+    memset(p, 0, sizeof(*p));
+    p->maxHits = 16000;                // AlignerOptions.cpp:73-77 (forPairedEnd)
+    p->maxK = 15;
+    p->maxSeedsToUse = 8;
+    p->extraSearchDepth = 2;
+    p->minSpacing = 50;                // PairedAligner.cpp:57-58
+    p->maxSpacing = 1000;
+    p->maxBigHits = 16000;             // DEFAULT_INTERSECTING_ALIGNER_MAX_HITS
+    p->maxCandidatePoolSize = 1000000; // DEFAULT_MAX_CANDIDATE_POOL_SIZE
+    p->maxReadSize = 500;              // MAX_READ_LENGTH
+    p->forceSpacing = 0;
+    p->seedCoverage = 0;
+}
+
+snapgpu_paired_aligner_t *snapgpu_paired_aligner_create(int device, const snapgpu_index_t *idx,
+                                                        const snapgpu_paired_params_t *params) {
+    if (!idx) { snapgpu::setError("paired_aligner_create: null index"); return nullptr; }
+    snapgpu_paired_params_t p;
+    if (params) p = *params; else snapgpu_paired_params_default(&p);
+    if (p.maxK + p.extraSearchDepth + 1 > (uint32_t)MAX_LISTS || p.maxK > (uint32_t)MAX_K - 1) {
+        snapgpu::setError("paired_aligner_create: maxK + extraSearchDepth too large");
+        return nullptr;
+    }
+    if (p.maxReadSize > 512) { snapgpu::setError("paired_aligner_create: maxReadSize > 512"); return nullptr; }
+    snapgpu_aligner_params_t bp;
+    snapgpu_aligner_params_default(&bp);
+    bp.maxHitsToConsider = p.maxHits; bp.maxK = p.maxK; bp.maxReadSize = p.maxReadSize;
+    bp.maxSeedsToUse = p.maxSeedsToUse; bp.maxSeedCoverage = p.seedCoverage; bp.extraSearchDepth = p.extraSearchDepth;
+    snapgpu_aligner_t *single = snapgpu_aligner_create(device, idx, &bp);   // fails loudly without a GPU
+    if (!single) return nullptr;
+    auto *pa = new snapgpu_paired_aligner_t();
+    pa->device = device;
+    pa->p = p;
+    pa->single = single;
+    auto fail = [&](const char *what, hipError_t e) -> snapgpu_paired_aligner_t * {
+        snapgpu::setError(std::string("paired_aligner_create: ") + what + ": " + hipGetErrorString(e));
+        snapgpu_paired_aligner_free(pa);
+        return nullptr;
+    };
+    if (snapgpu_internal_index_args(single, &pa->X, nullptr)) { snapgpu_paired_aligner_free(pa); return nullptr; }
+    hipError_t e;
+    if ((e = hipSetDevice(device)) != hipSuccess) return fail("device", e);
+    if ((e = ensurePairedTables(device)) != hipSuccess) return fail("tables", e);
+    if ((e = hipStreamCreateWithFlags(&pa->stream, hipStreamNonBlocking)) != hipSuccess) return fail("stream", e);
+    if ((e = hipMalloc(&pa->dCounter, 64)) != hipSuccess) return fail("counter", e);
+    // IntersectingPairedEndAligner ctor (:47-57, :128): numSeedsFromCommandLine = min(30, -n)
+    pa->maxSeedsCmd = p.maxSeedsToUse < 30 ? p.maxSeedsToUse : 30;
+    const uint32_t maxSeedsToUse = pa->maxSeedsCmd ? pa->maxSeedsCmd
+                                                   : (uint32_t)(p.maxReadSize * p.seedCoverage / idx->seedLen);
+    const uint64_t pool = (uint64_t)p.maxBigHits * maxSeedsToUse * 2;
+    pa->refPool = (uint32_t)std::min<uint64_t>(pool, p.maxCandidatePoolSize);
+    hipDeviceProp_t prop;
+    if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) return fail("props", e);
+    int perCU = 0;
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, (const void *)paired_kernel<128>, 64, 0);
+    if (perCU <= 0) perCU = 4;
+    uint32_t c1 = std::min<uint32_t>(pa->refPool, 4096);
+    if (const char *t = getenv("SNAPGPU_PAIRED_POOL1"); t && atoi(t) > 1) c1 = std::min<uint32_t>(pa->refPool, (uint32_t)atoi(t));
+    if (allocPass(pa->pass[0], prop.multiProcessorCount * std::min(perCU, 8), c1, std::max<uint32_t>(1, std::min(pa->refPool / 2, c1 / 2)), c1))
+        { snapgpu_paired_aligner_free(pa); return nullptr; }
+    int perCU2 = 0;
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU2, (const void *)paired_kernel<512>, 64, 0);
+    if (perCU2 <= 0) perCU2 = 2;
+    // pass 2 pools hold the reference's whole pool; as many waves as fit in 8 GB
+    const uint64_t stride2 = (uint64_t)pa->refPool * sizeof(Cand) + (uint64_t)pa->refPool * sizeof(Mate) +
+                             (uint64_t)pa->refPool * sizeof(Anchor) + 256;
+    int grid2 = prop.multiProcessorCount * perCU2;
+    while (grid2 > 8 && (uint64_t)grid2 * stride2 > (8ull << 30)) grid2 /= 2;
+    if (allocPass(pa->pass[1], grid2, pa->refPool, std::max<uint32_t>(1, pa->refPool / 2), pa->refPool))
+        { snapgpu_paired_aligner_free(pa); return nullptr; }
+    return pa;
+}
+
+void snapgpu_paired_aligner_free(snapgpu_paired_aligner_t *pa) {
+    if (!pa) return;
+    if (pa->single && snapgpu_internal_aligner_failed(pa->single)) {
+        // a timed-out kernel may still run on these buffers: leak them (see aligner.hip)
+    } else {
+        (void)hipSetDevice(pa->device);
+        if (pa->stream) (void)hipStreamSynchronize(pa->stream);
+        pfree(pa->dCounter); pfree(pa->dDefer); pfree(pa->dOut);
+        for (int r = 0; r < 2; r++) { pfree(pa->dB[r]); pfree(pa->dQ[r]); pfree(pa->dO[r]); pfree(pa->dL[r]); }
+        for (auto &pp : pa->pass) pfree(pp.pool);
+        if (pa->stream) (void)hipStreamDestroy(pa->stream);
+    }
+    if (pa->single) snapgpu_aligner_free(pa->single);
+    delete pa;
+}
+
+snapgpu_aligner_t *snapgpu_paired_aligner_single(snapgpu_paired_aligner_t *pa) { return pa ? pa->single : nullptr; }
+
+int snapgpu_paired_intersect_batch(snapgpu_paired_aligner_t *pa, const snapgpu_reads_t *reads0,
+                                   const snapgpu_reads_t *reads1, snapgpu_pair_result_t *out) {
+    if (!pa || !reads0 || !reads1 || !out) return SNAPGPU_EINVAL;
+    if (reads0->n != reads1->n) { snapgpu::setError("paired: the two read batches differ in length"); return SNAPGPU_EINVAL; }
+    if (reads0->n == 0) return SNAPGPU_OK;
+    if (reads0->n > 0xffffffffull) { snapgpu::setError("paired: batch too large"); return SNAPGPU_EINVAL; }
+    PCHK(hipSetDevice(pa->device));
+    return runIntersect(pa, reads0, reads1, out);
+}
+
+// ChimericPairedEndAligner::align (ChimericPairedEndAligner.cpp:56-126) for every pair: the
+// intersecting aligner on the GPU, then the pairs it left NotFound through the single-end GPU
+// BaseAligner, each end on its own, MAPQ / 4.
+int snapgpu_paired_align_batch(snapgpu_paired_aligner_t *pa, const snapgpu_reads_t *reads0,
+                               const snapgpu_reads_t *reads1, snapgpu_pair_result_t *out) {
+    int rc = snapgpu_paired_intersect_batch(pa, reads0, reads1, out);
+    if (rc) return rc;
+    const uint64_t n = reads0->n;
+    std::vector<uint64_t> fb;   // pairs for the single-end fallback
+    for (uint64_t i = 0; i < n; i++) {
+        snapgpu_pair_result_t &r = out[i];
+        const uint32_t n0 = reads0->lengths[i], n1 = reads1->lengths[i];
+        if (n0 < 50 && n1 < 50) {   // :61-64: status NotFound, nothing else written
+            const uint16_t f = r.flags;
+            memset(&r, 0, sizeof(r));
+            r.location[0] = r.location[1] = 0xffffffffu;
+            r.score[0] = r.score[1] = -1;
+            r.flags = f;
+            continue;
+        }
+        r.fromAlignTogether = 1;
+        r.alignedAsPair = 1;
+        if (pa->p.forceSpacing) {
+            if (r.status[0] == SNAPGPU_NOT_FOUND) r.fromAlignTogether = 0;
+            continue;
+        }
+        if (r.status[0] != SNAPGPU_NOT_FOUND && r.status[1] != SNAPGPU_NOT_FOUND) continue;
+        fb.push_back(i);
+    }
+    if (fb.empty()) return SNAPGPU_OK;
+    const snapgpu_reads_t *R[2] = {reads0, reads1};
+    for (int e = 0; e < 2; e++) {
+        std::vector<uint64_t> o(fb.size());
+        std::vector<uint32_t> l(fb.size());
+        for (size_t j = 0; j < fb.size(); j++) { o[j] = R[e]->offsets[fb[j]]; l[j] = R[e]->lengths[fb[j]]; }
+        snapgpu_reads_t *sub = snapgpu_reads_from_arrays(fb.size(), R[e]->bases, R[e]->quals, o.data(), l.data());
+        if (!sub) return SNAPGPU_ENOMEM;
+        std::vector<snapgpu_result_t> res(fb.size());
+        rc = snapgpu_align_batch(pa->single, sub, res.data());
+        snapgpu_reads_free(sub);
+        if (rc) return rc;
+        for (size_t j = 0; j < fb.size(); j++) {
+            snapgpu_pair_result_t &r = out[fb[j]];
+            const snapgpu_result_t &s = res[j];
+            if (s.flags & SNAPGPU_FLAG_READ_TOO_LONG) {
+                snapgpu::setError("paired: read longer than maxReadSize (the reference exits, BaseAligner.cpp:609-613)");
+                return SNAPGPU_EINVAL;
+            }
+            r.status[e] = s.result;
+            r.location[e] = s.location;
+            r.direction[e] = s.direction;
+            r.score[e] = s.score;
+            r.mapq[e] = s.mapq / 4;   // :118
+            r.nSingleScored += s.nLocationsScored;
+        }
+    }
+    for (uint64_t i : fb) { out[i].fromAlignTogether = 0; out[i].alignedAsPair = 0; }
+    return SNAPGPU_OK;
+}
+
+}  // extern "C"

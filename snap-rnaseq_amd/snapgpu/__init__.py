@@ -36,7 +36,7 @@ assert RESULT_DTYPE.itemsize == C.sizeof(_ffi.Result)
 PAIR_RESULT_DTYPE = np.dtype([
     ("location", "<u4", (2,)), ("score", "<i4", (2,)), ("mapq", "<i4", (2,)), ("status", "u1", (2,)),
     ("direction", "u1", (2,)), ("fromAlignTogether", "u1"), ("alignedAsPair", "u1"), ("flags", "<u2"),
-    ("nLocationsScored", "<u4"), ("nSingleScored", "<u4"), ("reserved", "<u4"), ("reserved2", "<u4"),
+    ("nLocationsScored", "<u4"), ("nSingleScored", "<u4"), ("popularSeedsSkipped", "<u4"), ("reserved", "<u4"),
     ("probabilityOfAllPairs", "<f8"), ("probabilityOfBestPair", "<f8"),
 ])
 assert PAIR_RESULT_DTYPE.itemsize == 64
@@ -69,7 +69,7 @@ class SnapGpuError(RuntimeError):
 
 _PTR_CALLS = ("genome_from_fasta", "genome_synthetic", "index_build", "index_load", "index_attach", "gtf_load",
               "reads_synthetic",
-              "reads_from_fastq", "reads_from_arrays", "aligner_create", "reads_upload")
+              "reads_from_fastq", "reads_from_arrays", "aligner_create", "reads_upload", "paired_aligner_create")
 
 
 def _check(value, what):
@@ -259,6 +259,11 @@ class Reads:
 
     def __len__(self):
         return self.n
+
+    def lengths(self):
+        """Read lengths as a uint32 array (a copy)."""
+        r = self._p.contents
+        return np.ctypeslib.as_array(r.lengths, shape=(r.n,)).copy() if r.n else np.zeros(0, np.uint32)
 
     def get(self, i):
         r = self._p.contents
@@ -461,6 +466,49 @@ class BaseAligner:
     def __del__(self):
         if getattr(self, "_h", None):
             lib().snapgpu_aligner_free(self._h)
+            self._h = None
+
+
+def paired_params(**kw):
+    """snapgpu_paired_params_t with the paired CLI defaults, overridden by kw."""
+    p = _ffi.PairedParams()
+    lib().snapgpu_paired_params_default(C.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+class PairedAligner:
+    """GPU ChimericPairedEndAligner over an IntersectingPairedEndAligner, constructed as
+    PairedAligner.cpp:462-482 does (SNAPLib/ChimericPairedEndAligner.h, IntersectingPairedEndAligner.h).
+    align() is ChimericPairedEndAligner::align for every pair; intersect() the intersecting aligner
+    alone.  Keyword arguments: snapgpu_paired_params_t fields (maxHits, maxK, maxSeedsToUse,
+    extraSearchDepth, minSpacing, maxSpacing, maxBigHits, maxCandidatePoolSize, maxReadSize,
+    forceSpacing, seedCoverage)."""
+
+    def __init__(self, index, device=0, **kw):
+        self.index = index
+        self.params = paired_params(**kw)
+        self._h = _check(lib().snapgpu_paired_aligner_create(device, index._h, C.byref(self.params)),
+                         "paired_aligner_create")
+
+    def _run(self, fn, reads0, reads1, what):
+        if reads0.n != reads1.n:
+            raise ValueError("the two read batches differ in length")
+        out = np.zeros(max(1, reads0.n), dtype=PAIR_RESULT_DTYPE)
+        if reads0.n:
+            _check(fn(self._h, reads0._p, reads1._p, out.ctypes.data), what)
+        return out[:reads0.n]
+
+    def align(self, reads0, reads1):
+        return self._run(lib().snapgpu_paired_align_batch, reads0, reads1, "paired_align_batch")
+
+    def intersect(self, reads0, reads1):
+        return self._run(lib().snapgpu_paired_intersect_batch, reads0, reads1, "paired_intersect_batch")
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().snapgpu_paired_aligner_free(self._h)
             self._h = None
 
 

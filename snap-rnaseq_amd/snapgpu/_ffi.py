@@ -289,7 +289,7 @@ _PROTOS += [
     ("snapgpu_aligner_get_params", C.c_int, [C.c_void_p, C.POINTER(AlignerParams)]),
     ("snapgpu_paired_params_default", None, [C.POINTER(PairedParams)]),
     ("snapgpu_paired_aligner_create", C.c_void_p, [C.c_int, C.c_void_p, C.POINTER(PairedParams)]),
-    ("snapgpu_paired_aligner_destroy", None, [C.c_void_p]),
+    ("snapgpu_paired_aligner_free", None, [C.c_void_p]),
     ("snapgpu_paired_align_batch", C.c_int, [C.c_void_p, C.POINTER(Reads), C.POINTER(Reads), C.c_void_p]),
     ("snapgpu_paired_intersect_batch", C.c_int, [C.c_void_p, C.POINTER(Reads), C.POINTER(Reads), C.c_void_p]),
     ("snapgpu_paired_aligner_single", C.c_void_p, [C.c_void_p]),

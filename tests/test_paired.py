@@ -72,3 +72,68 @@ def test_oracle_paired_outcome_mix(world):
     fallback = sum(1 for c in chim if c[10] == "0" and c[0] != "0")
     untouched = sum(1 for c in chim if c[0] == "0" and c[1] == "0" and c[2] == str(0xFFFFFFFF))
     assert together > 1000 and fallback > 100 and untouched > 10
+
+
+# ------------------------------------------------------------------------- GPU
+def _gpu_aligner(idx, run):
+    d = PAIRED_RUNS[run]
+    return snapgpu.PairedAligner(idx, maxHits=d["maxHits"], maxK=d["maxK"], maxSeedsToUse=d["numSeeds"],
+                                 extraSearchDepth=d["extra"], minSpacing=d["minSpacing"], maxSpacing=d["maxSpacing"],
+                                 maxBigHits=d["maxBigHits"])
+
+
+def _bitwise(a, b, fields):
+    bad = np.zeros(len(a), dtype=bool)
+    for f in fields:
+        x, y = a[f], b[f]
+        if x.dtype.kind == "f":
+            x, y = x.view(np.uint64), y.view(np.uint64)
+        bad |= (x != y).reshape(len(a), -1).any(axis=1)
+    return np.nonzero(bad)[0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("run", list(PAIRED_RUNS))
+def test_gpu_intersecting_matches_reference_and_oracle(gpu_available, world, run):
+    idx, r0, r1 = world
+    pa = _gpu_aligner(idx, run)
+    got = pa.intersect(r0, r1)
+    inter_want, _ = ref_paired_rows(os.path.join(G, f"expected_paired_{run}.tsv"))
+    bad = _cmp(paired_tsv_rows(got, chimeric=False), inter_want)
+    assert not bad, f"{len(bad)} pairs differ from the reference, first {bad[:3]}"
+    cpu = oracle_paired(idx, r0, r1, params_of(run), chimeric=False)
+    bad = _bitwise(got, cpu, ("status", "location", "direction", "score", "mapq", "nLocationsScored",
+                              "popularSeedsSkipped", "probabilityOfAllPairs", "probabilityOfBestPair"))
+    assert len(bad) == 0, f"{len(bad)} pairs differ from the oracle, e.g. {got[bad[0]]} vs {cpu[bad[0]]}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("run", list(PAIRED_RUNS))
+def test_gpu_chimeric_matches_reference(gpu_available, world, run):
+    idx, r0, r1 = world
+    pa = _gpu_aligner(idx, run)
+    got = pa.align(r0, r1)
+    _, chim_want = ref_paired_rows(os.path.join(G, f"expected_paired_{run}.tsv"))
+    bad = _cmp(paired_tsv_rows(got, chimeric=True), chim_want)
+    assert not bad, f"{len(bad)} pairs differ from the reference, first {bad[:3]}"
+
+
+@pytest.mark.gpu
+def test_gpu_paired_pass2_and_pool_paths(gpu_available, world, monkeypatch):
+    """Pass-1 pools of 8 entries (SNAPGPU_PAIRED_POOL1) send every pair with more candidates to
+    pass 2 (the reference's pool sizes); reads > 128 bases always go there.  The records must be
+    the same as with the default pools, and the oracle's."""
+    idx, r0, r1 = world
+    want = _gpu_aligner(idx, "default").intersect(r0, r1)
+    lens = np.maximum(r0.lengths(), r1.lengths())
+    assert np.all((want["flags"][(lens > 128) & (np.minimum(r0.lengths(), r1.lengths()) >= 50)]
+                   & snapgpu.PFLAG_DEFERRED) != 0)
+    monkeypatch.setenv("SNAPGPU_PAIRED_POOL1", "8")
+    got = _gpu_aligner(idx, "default").intersect(r0, r1)
+    nDeferred = int(((got["flags"] & snapgpu.PFLAG_DEFERRED) != 0).sum())
+    assert nDeferred > int(((want["flags"] & snapgpu.PFLAG_DEFERRED) != 0).sum()) + 50
+    fields = ("status", "location", "direction", "score", "mapq", "nLocationsScored", "probabilityOfAllPairs",
+              "probabilityOfBestPair")
+    assert len(_bitwise(got, want, fields)) == 0
+    cpu = oracle_paired(idx, r0, r1, params_of("default"), chimeric=False)
+    assert len(_bitwise(got, cpu, fields)) == 0
