@@ -481,6 +481,7 @@ __device__ void align_pair(const PArgs &P, PLds<MAXLEN> &S, Cand *cand, Mate *ma
     const uint32_t maxK = P.maxK, extra = P.extra;
     snapgpu_pair_result_t res;
     pre_state(res);
+    if (P.pairList) res.flags |= SNAPGPU_PFLAG_DEFERRED;
     const uint32_t n0 = P.lengths[0][pi], n1 = P.lengths[1][pi];
     const uint64_t o0 = P.offsets[0][pi], o1 = P.offsets[1][pi];
     if (n0 < 50 || n1 < 50) { write_result<MAXLEN>(P, pi, res); return; }         // :186-188
@@ -680,7 +681,6 @@ doneScoring:
     res.probabilityOfAllPairs = pAll;
     res.probabilityOfBestPair = pBest;
     res.popularSeedsSkipped = popularAll;
-    if (P.pairList) res.flags |= SNAPGPU_PFLAG_DEFERRED;
     if (bestPairScore == 65536) {
         res.location[0] = res.location[1] = INVALID;
         res.mapq[0] = res.mapq[1] = 0;
