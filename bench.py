@@ -126,6 +126,51 @@ def init_distributed():
     return world, rank, local, dist
 
 
+def paired_leg(args, idx, local, rank, cpus):
+    """SURVEY.md 8(f) f2 (BASELINE configs[3] shape on this workload's genome): wgsim-like
+    2 x 101 bp pairs (insert 500 +- 50) through ChimericPairedEndAligner::align on the GPU
+    (intersecting kernel, then the single-end fallback), host buffers in and out; the C
+    restatement on the job's CPUs beside it, and parity of every record field on a sample."""
+    import snapgpu
+    n = args.paired_pairs
+    r0, r1 = snapgpu.Reads.synthetic_pairs(idx.genome_handle(), n, seed=7 + rank, read_length=101)
+    pa = snapgpu.PairedAligner(idx, device=local)
+    pa.align(r0, r1)
+    ts = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        res = pa.align(r0, r1)
+        ts.append(time.perf_counter() - t0)
+    t0 = time.perf_counter()
+    inter = pa.intersect(r0, r1)
+    t_int = time.perf_counter() - t0
+    dt = float(np.median(ts))
+    together = int(res["fromAlignTogether"].sum())
+    out = {"value": 2 * n / dt, "unit": "reads/s", "pairs_per_s": n / dt, "pairs": n, "ms_per_batch": dt * 1000.0,
+           "intersect_only_ms": t_int * 1000.0, "aligned_together": together, "fallback_pairs": int(n - together),
+           "status_pairs": {int(k): int(v) for k, v in zip(*np.unique(res["status"][:, 0], return_counts=True))},
+           "deferred_to_pass2": int(((inter["flags"] & snapgpu.PFLAG_DEFERRED) != 0).sum()),
+           "params": "paired CLI defaults: maxHits 16000, maxDist 15, 8 seeds, extra 2, spacing 50..1000",
+           "boundary": "host pairs in -> host PairedAlignmentResult out (snapgpu_paired_align_batch)"}
+    if not args.no_cpu_baseline:
+        from oracle_ffi import oracle_paired
+        ns = min(n, 200_000)
+        s0, s1 = r0.slice(0, ns), r1.slice(0, ns)
+        nthr = cpus["usable"]
+        c0 = time.perf_counter()
+        cres = oracle_paired(idx, s0, s1, pa.params, chimeric=True, n_threads=nthr)
+        cdt = time.perf_counter() - c0
+        fields = ("status", "location", "direction", "score", "mapq", "fromAlignTogether", "alignedAsPair",
+                  "nLocationsScored", "nSingleScored")
+        bad = np.zeros(ns, dtype=bool)
+        for f in fields:
+            bad |= (res[f][:ns] != cres[f]).reshape(ns, -1).any(axis=1)
+        out["cpu_baseline"] = {"value": 2 * ns / cdt, "unit": "reads/s", "cores": nthr, "kind": "port",
+                               "sample": f"the first {ns} pairs, oracle/snap_oracle.c paired section, {nthr} threads"}
+        out["parity"] = {"pairs_compared": ns, "mismatches": int(bad.sum()), "fields": list(fields)}
+    return out
+
+
 def timed_steps(step, steps, dist, sync):
     """Barrier + sync on both sides of exactly `steps` steps; returns the max over ranks."""
     if dist:
@@ -156,6 +201,8 @@ def main():
     ap.add_argument("--reads", type=int, default=None, help="reads per GPU (default: the workload's)")
     ap.add_argument("--genome-bases", type=int, default=None)
     ap.add_argument("--resident-steps", type=int, default=5)
+    ap.add_argument("--paired-pairs", type=int, default=500_000,
+                    help="extras.paired: 2 x 101 bp pairs through the GPU ChimericPairedEndAligner (0: skip)")
     ap.add_argument("--mode", choices=("stream", "sync"), default="stream",
                     help="stream: submit every step, wait once (a streaming caller); sync: one blocking call per step")
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="reads timed on the CPU baseline")
@@ -346,6 +393,8 @@ def main():
                                      "frac": cig_bytes / cig_s / 1e9 / HBM_PEAK_GBS,
                                      "sam_format_reads_per_s": wl["reads"] / sam_s, "sam_bytes": len(sam)}
             del sam, dev
+            if args.paired_pairs:
+                extras["paired"] = paired_leg(args, idx, local, rank, cpus)
         log(rank, "extras done")
         cpu = None
         parity = None

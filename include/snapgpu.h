@@ -237,6 +237,9 @@ typedef struct snapgpu_synth_reads_params {
     double   randomReadFraction;/* fraction of reads of pure noise (NotFound) */
 } snapgpu_synth_reads_params_t;
 snapgpu_reads_t *snapgpu_reads_synthetic(const snapgpu_genome_t *g, const snapgpu_synth_reads_params_t *p);
+/* wgsim-like read pairs (nReads pairs, readLength each): insert ~ N(insertMean, insertSd). */
+int snapgpu_reads_synthetic_pairs(const snapgpu_genome_t *g, const snapgpu_synth_reads_params_t *p, uint32_t insertMean,
+                                  uint32_t insertSd, snapgpu_reads_t **reads0, snapgpu_reads_t **reads1);
 snapgpu_reads_t *snapgpu_reads_from_fastq(const char *path);
 /* Build a batch from caller arrays (copies them). */
 snapgpu_reads_t *snapgpu_reads_from_arrays(uint64_t n, const char *bases, const char *quals,

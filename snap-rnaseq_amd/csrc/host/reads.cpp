@@ -5,6 +5,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <vector>
 
 using namespace snapgpu;
 
@@ -117,6 +118,109 @@ snapgpu_reads_t *snapgpu_reads_synthetic(const snapgpu_genome_t *g, const snapgp
         }
     }
     return r;
+}
+
+// wgsim-like pairs: a fragment of length insert ~ N(insertMean, insertSd) (Irwin-Hall, no libm)
+// walked through the mutated haplotype; read 0 = the fragment's first L bases, read 1 = the
+// reverse complement of its last L, the whole fragment from either strand; base errors per read.
+// Truth: fragment start and the strand of read 0.
+int snapgpu_reads_synthetic_pairs(const snapgpu_genome_t *g, const snapgpu_synth_reads_params_t *p, uint32_t insertMean,
+                                  uint32_t insertSd, snapgpu_reads_t **reads0, snapgpu_reads_t **reads1) {
+    if (!g || !p || !reads0 || !reads1 || p->readLength == 0 || g->pieceOffsets.empty() || insertMean < p->readLength) {
+        setError("bad pair params");
+        return SNAPGPU_EINVAL;
+    }
+    const uint32_t L = p->readLength;
+    const uint64_t n = p->nReads;
+    snapgpu_reads_t *R[2] = {allocReads(n, n * (uint64_t)L, true), allocReads(n, n * (uint64_t)L, true)};
+    Rng rng(p->seed);
+    static const char kBases[4] = {'A', 'C', 'G', 'T'};
+    const uint32_t maxIns = insertMean + 6 * insertSd + 1;
+    std::vector<uint64_t> cStart, cLen, cum;
+    uint64_t total = 0;
+    for (size_t i = 0; i < g->pieceOffsets.size(); i++) {
+        uint64_t st = g->pieceOffsets[i];
+        uint64_t e = i + 1 < g->pieceOffsets.size() ? g->pieceOffsets[i + 1] - g->chromosomePadding : g->nBases - g->chromosomePadding;
+        cStart.push_back(st); cLen.push_back(e - st);
+        total += e - st > 2ull * maxIns + 64 ? e - st : 0;
+        cum.push_back(total);
+    }
+    if (total == 0) { setError("contigs too short"); snapgpu_reads_free(R[0]); snapgpu_reads_free(R[1]); return SNAPGPU_EINVAL; }
+    const char *gb = g->bases();
+    std::string frag, t;
+    for (uint64_t i = 0; i < n; i++) {
+        for (int k = 0; k < 2; k++) {
+            R[k]->offsets[i] = i * L;
+            R[k]->lengths[i] = L;
+            memset(R[k]->quals + i * L, (int)p->qualityChar, L);
+        }
+        double z = 0;
+        for (int j = 0; j < 12; j++) z += rng.uniform();
+        int64_t ins = (int64_t)insertMean + (int64_t)((z - 6.0) * (double)insertSd);
+        if (ins < (int64_t)L) ins = L;
+        if (ins > (int64_t)maxIns) ins = maxIns;
+        for (int attempt = 0;; attempt++) {
+            uint64_t x = rng.below(total);
+            size_t c = 0;
+            while (cum[c] <= x) c++;
+            const uint64_t start = cStart[c] + rng.below(cLen[c] - maxIns - 48);
+            frag.clear();
+            uint64_t pos = start;
+            while (frag.size() < (size_t)ins) {
+                char base = gb[pos];
+                if (base == 'n') base = 'N';
+                const double u = rng.uniform();
+                if (u < p->mutationRate) {
+                    if (rng.uniform() < p->indelFraction) {
+                        uint32_t len = 1;
+                        while (rng.uniform() < p->indelExtend && len < 10) len++;
+                        if (rng.next() >> 63) { pos += len; continue; }
+                        frag.push_back(base);
+                        for (uint32_t k = 0; k < len && frag.size() < (size_t)ins; k++) frag.push_back(kBases[rng.next() >> 62]);
+                        pos++;
+                        continue;
+                    }
+                    char nb;
+                    do { nb = kBases[rng.next() >> 62]; } while (nb == base);
+                    frag.push_back(nb);
+                } else frag.push_back(base);
+                pos++;
+            }
+            frag.resize((size_t)ins);
+            uint32_t nN = 0;
+            for (char ch : frag) nN += ch == 'N';
+            if (nN > (uint32_t)ins / 20 && attempt < 16) continue;
+            const bool rc = rng.next() >> 63;
+            if (rc) {
+                t.assign(frag.rbegin(), frag.rend());
+                for (auto &ch : t) ch = complement(ch);
+                frag.swap(t);
+            }
+            std::string m[2];
+            m[0] = frag.substr(0, L);
+            t.assign(frag.rbegin(), frag.rbegin() + L);
+            for (auto &ch : t) ch = complement(ch);
+            m[1] = t;
+            for (int k = 0; k < 2; k++) {
+                char *out = R[k]->bases + i * L;
+                for (uint32_t j = 0; j < L; j++) {
+                    char ch = m[k][j];
+                    if (ch != 'N' && rng.uniform() < p->baseErrorRate) {
+                        char nb;
+                        do { nb = kBases[rng.next() >> 62]; } while (nb == ch);
+                        ch = nb;
+                    }
+                    out[j] = ch;
+                }
+                R[k]->truthLocation[i] = (uint32_t)start;
+                R[k]->truthDirection[i] = (uint8_t)(rc ^ (k == 1));
+            }
+            break;
+        }
+    }
+    *reads0 = R[0];
+    *reads1 = R[1];
+    return SNAPGPU_OK;
 }
 
 snapgpu_reads_t *snapgpu_reads_from_arrays(uint64_t n, const char *bases, const char *quals,

@@ -220,6 +220,21 @@ class Reads:
         return cls(_check(lib().snapgpu_reads_synthetic(g, C.byref(p)), "reads_synthetic"))
 
     @classmethod
+    def synthetic_pairs(cls, genome, n_pairs, seed=99, read_length=101, insert_mean=500, insert_sd=50,
+                        quality_char="2", base_error_rate=0.02, mutation_rate=0.001, indel_fraction=0.15,
+                        indel_extend=0.3):
+        """wgsim-like pairs (snapgpu_reads_synthetic_pairs) -> (reads0, reads1)."""
+        p = _ffi.SynthReadsParams(seed=seed, nReads=n_pairs, readLength=read_length,
+                                  qualityChar=ord(quality_char), baseErrorRate=base_error_rate,
+                                  mutationRate=mutation_rate, indelFraction=indel_fraction,
+                                  indelExtend=indel_extend, randomReadFraction=0.0)
+        g = genome._h if isinstance(genome, Genome) else genome
+        a, b = C.POINTER(_ffi.Reads)(), C.POINTER(_ffi.Reads)()
+        _check(lib().snapgpu_reads_synthetic_pairs(g, C.byref(p), insert_mean, insert_sd, C.byref(a), C.byref(b)),
+               "reads_synthetic_pairs")
+        return cls(a), cls(b)
+
+    @classmethod
     def from_fastq(cls, path):
         return cls(_check(lib().snapgpu_reads_from_fastq(str(path).encode()), "reads_from_fastq"))
 

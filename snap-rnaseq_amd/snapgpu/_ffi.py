@@ -220,6 +220,8 @@ _PROTOS = [
     ("snapgpu_index_lookup", C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(C.c_uint32),
                                        C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.c_uint32]),
     ("snapgpu_reads_synthetic", C.POINTER(Reads), [C.c_void_p, C.POINTER(SynthReadsParams)]),
+    ("snapgpu_reads_synthetic_pairs", C.c_int, [C.c_void_p, C.POINTER(SynthReadsParams), C.c_uint32, C.c_uint32,
+                                                C.POINTER(C.POINTER(Reads)), C.POINTER(C.POINTER(Reads))]),
     ("snapgpu_reads_from_fastq", C.POINTER(Reads), [C.c_char_p]),
     ("snapgpu_reads_from_arrays", C.POINTER(Reads), [C.c_uint64, C.c_char_p, C.c_char_p,
                                                      C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]),
