@@ -21,6 +21,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNELS = {"align": "align_kernel<128, false>", "lookup": "seed_lookup_kernel", "copy": "copy_peak_kernel",
+           "paired": "paired_kernel<128>",
            "gather": "gather_peak_kernel", "cigar": "cigar_kernel", "align512": "align_kernel<512, false>"}
 
 
