@@ -99,8 +99,8 @@ struct PLds {
     int16_t btAct[MAX_K + 1], btMatched[MAX_K + 1];
     HitSet hs[2][2];                        // [read][direction]
     uint32_t miss[LCAP];                    // DisjointHitSet::missCount scratch
-    uint32_t sel[LCAP];                     // chosen seed offsets of one read (bit 31: a wrap preceded it)
-    uint32_t look[LCAP][6];                 // per seed: nHits, at, single for FORWARD and RC
+    uint32_t sel[2][LCAP];                  // chosen seed offsets per read (bit 31: a wrap preceded it)
+    uint32_t look[2][LCAP][8];                 // per seed and direction: nHits, at, single, nHits after the trim
     uint64_t validBits[NB], usedBits[NB];
     int32_t lists[MAX_LISTS];
 };
@@ -224,13 +224,13 @@ __device__ uint32_t hs_best_possible(const PArgs &P, PLds<MAXLEN> &S, HitSet &h,
 }
 
 // recordLookup (:859-899), uniform: every lane writes the same values
-__device__ __forceinline__ void hs_record(const PArgs &P, HitSet &h, uint32_t seedOffset, uint32_t nHits, uint32_t at,
+// (nHits as looked up; trimmed = after the trim of :882-884, done by the lookup lane)
+__device__ __forceinline__ void hs_record(HitSet &h, uint32_t seedOffset, uint32_t nHits, uint32_t trimmed, uint32_t at,
                                           uint32_t single, bool begins) {
     if (begins) { h.curSet = h.curSet + 1; h.exhausted[h.curSet] = 0; }
     if (nHits == 0) { h.exhausted[h.curSet] = h.exhausted[h.curSet] + 1; wave_sync(); return; }
     Lookup l;
-    l.cur = 0; l.nHits = nHits; l.seedOffset = seedOffset; l.set = (uint32_t)h.curSet; l.at = at; l.single = single;
-    while (l.nHits > 0 && hit_at(P, l, l.nHits - 1) < l.seedOffset) l.nHits--;   // :882-884
+    l.cur = 0; l.nHits = trimmed; l.seedOffset = seedOffset; l.set = (uint32_t)h.curSet; l.at = at; l.single = single;
     h.lk[h.nLookups] = l;
     h.nLookups = h.nLookups + 1;
     wave_sync();
@@ -326,11 +326,11 @@ __device__ void defer_pair(const PArgs &P, uint32_t pi) {
     if (lane_id() == 0) P.deferList[atomicAdd(P.deferCount, 1u)] = pi;
 }
 
-// Phase 1 for read r (IntersectingPairedEndAligner.cpp:259-340): choose the seeds, look them up
-// one lane per seed, then record the hit sets in the reference's order.
+// Phase 1 (IntersectingPairedEndAligner.cpp:259-340).  The seed walk of a read depends only on
+// its bases, so both reads' seeds are chosen first, then looked up in one round, one lane per seed.
 template <int MAXLEN>
-__device__ __forceinline__ void phase1_read(const PArgs &P, PLds<MAXLEN> &S, const int r, const uint32_t nr,
-                                            const uint32_t maxSeeds, uint32_t &totF, uint32_t &totR, uint32_t &popular) {
+__device__ __forceinline__ uint32_t choose_seeds(const PArgs &P, PLds<MAXLEN> &S, const int r, const uint32_t nr,
+                                                 const uint32_t maxSeeds) {
     constexpr int NB = MAXLEN / 64;
     const KArgs &X = P.X;
     const int lane = lane_id();
@@ -369,7 +369,7 @@ __device__ __forceinline__ void phase1_read(const PArgs &P, PLds<MAXLEN> &S, con
         S.usedBits[next >> 6] = ub;
         wave_sync();
         if (!((S.validBits[next >> 6] >> (next & 63)) & 1)) { next++; continue; }   // :296-302
-        S.sel[nSel] = next | (wrapped ? 0x80000000u : 0u);
+        S.sel[r][nSel] = next | (wrapped ? 0x80000000u : 0u);
         wrapped = false;
         nSel++;
         if ((maxSeeds - nSel + 1) * seedLen + next < nPossible)                      // :333-338
@@ -377,9 +377,21 @@ __device__ __forceinline__ void phase1_read(const PArgs &P, PLds<MAXLEN> &S, con
         else next += seedLen;
     }
     wave_sync();
-    // the lookups, one lane per seed (GenomeIndex::lookupSeed, GenomeIndex.cpp:971-1086)
-    if ((uint32_t)lane < nSel) {
-        const uint32_t so = S.sel[lane] & 0x7fffffffu;
+    return nSel;
+}
+
+// GenomeIndex::lookupSeed (GenomeIndex.cpp:971-1086) for the chosen seeds of both reads at
+// once: lanes 0-31 take read 0's seeds, lanes 32-63 read 1's.
+template <int MAXLEN>
+__device__ __forceinline__ void lookup_seeds(const PArgs &P, PLds<MAXLEN> &S, const uint32_t n0, const uint32_t n1,
+                                             const uint32_t nSel0, const uint32_t nSel1) {
+    const KArgs &X = P.X;
+    const int lane = lane_id();
+    const uint32_t seedLen = X.seedLen;
+    const int r = lane >> 5, k = lane & 31;
+    const uint32_t nr = r ? n1 : n0;
+    if ((uint32_t)k < (r ? nSel1 : nSel0)) {
+        const uint32_t so = S.sel[r][k] & 0x7fffffffu;
         uint64_t f = 0, rv = 0;
         for (uint32_t i = 0; i < seedLen; i++) {
             const int v = base_value((uint8_t)S.rd[r][0][so + i]);
@@ -419,22 +431,43 @@ __device__ __forceinline__ void phase1_read(const PArgs &P, PLds<MAXLEN> &S, con
                 }
             }
         }
-        S.look[lane][0] = nh[0]; S.look[lane][1] = at[0]; S.look[lane][2] = sg[0];
-        S.look[lane][3] = nh[1]; S.look[lane][4] = at[1]; S.look[lane][5] = sg[1];
-    }
-    wave_sync();
-    // the hit sets in the reference's order (:313-328)
-    bool begins[2] = {true, true};
-    for (uint32_t k = 0; k < nSel; k++) {
-        const uint32_t sk = S.sel[k];
-        if (sk & 0x80000000u) begins[0] = begins[1] = true;
-        const uint32_t so = sk & 0x7fffffffu;
+        // recordLookup's trim of the hits below the seed offset (:882-884), one lane per seed here
+        uint32_t tr[2];
+#pragma unroll
         for (int d = 0; d < 2; d++) {
             const uint32_t offset = d == 0 ? so : nr - seedLen - so;
-            const uint32_t nh = S.look[k][3 * d];
+            Lookup l;
+            l.nHits = nh[d]; l.at = at[d]; l.single = sg[d]; l.seedOffset = offset; l.cur = 0; l.set = 0;
+            if (nh[d] < P.maxBigHits)
+                while (l.nHits > 0 && hit_at(P, l, l.nHits - 1) < offset) l.nHits--;
+            tr[d] = l.nHits;
+        }
+        S.look[r][k][0] = nh[0]; S.look[r][k][1] = at[0]; S.look[r][k][2] = sg[0]; S.look[r][k][3] = tr[0];
+        S.look[r][k][4] = nh[1]; S.look[r][k][5] = at[1]; S.look[r][k][6] = sg[1]; S.look[r][k][7] = tr[1];
+    }
+    wave_sync();
+    wave_sync();
+}
+
+// The hit sets of read r in the reference's order (:313-328): where a disjoint hit set begins
+// depends on which lookups were recorded (a lookup with >= maxBigHits hits is skipped).
+__device__ __forceinline__ void record_hits(const PArgs &P, HitSet (&hs)[2], const uint32_t (&look)[LCAP][8],
+                                            const uint32_t *sel, const uint32_t nSel, const uint32_t nr,
+                                            uint32_t &totF, uint32_t &totR, uint32_t &popular) {
+    const uint32_t seedLen = P.X.seedLen;
+    bool begins[2] = {true, true};
+    for (uint32_t k = 0; k < nSel; k++) {
+        const uint32_t sk = sel[k];
+        if (sk & 0x80000000u) begins[0] = begins[1] = true;
+        const uint32_t so = sk & 0x7fffffffu;
+#pragma unroll
+        for (int d = 0; d < 2; d++) {
+            const uint32_t offset = d == 0 ? so : nr - seedLen - so;
+            const uint32_t nh = look[k][4 * d];
             if (nh < P.maxBigHits) {
                 if (d == 0) totF += nh; else totR += nh;
-                hs_record(P, S.hs[r][d], offset, nh, S.look[k][3 * d + 1], S.look[k][3 * d + 2], begins[d]);
+                hs_record(hs[d], offset, nh, look[k][4 * d + 3], look[k][4 * d + 1], look[k][4 * d + 2],
+                          begins[d]);
                 begins[d] = false;
             } else popular++;
         }
@@ -502,8 +535,11 @@ __device__ void align_pair(const PArgs &P, PLds<MAXLEN> &S, Cand *cand, Mate *ma
     if (maxSeeds > (uint32_t)LCAP) maxSeeds = LCAP;
     // ---------------------------------------------------------------- phase 1 (:259-340)
     uint32_t pop0 = 0, pop1 = 0, t00 = 0, t01 = 0, t10 = 0, t11 = 0;
-    phase1_read<MAXLEN>(P, S, 0, n0, maxSeeds, t00, t01, pop0);
-    phase1_read<MAXLEN>(P, S, 1, n1, maxSeeds, t10, t11, pop1);
+    const uint32_t nSel0 = choose_seeds<MAXLEN>(P, S, 0, n0, maxSeeds);
+    const uint32_t nSel1 = choose_seeds<MAXLEN>(P, S, 1, n1, maxSeeds);
+    lookup_seeds<MAXLEN>(P, S, n0, n1, nSel0, nSel1);
+    record_hits(P, S.hs[0], S.look[0], S.sel[0], nSel0, n0, t00, t01, pop0);
+    record_hits(P, S.hs[1], S.look[1], S.sel[1], nSel1, n1, t10, t11, pop1);
     const uint32_t popularAll = pop0 + pop1;
     const int more = t00 + t01 > t10 + t11 ? 0 : 1, fewer = 1 - more;            // :342-343
     const uint32_t nFewer = fewer ? n1 : n0, nMore = fewer ? n0 : n1;
@@ -949,7 +985,7 @@ snapgpu_paired_aligner_t *snapgpu_paired_aligner_create(int device, const snapgp
     if (perCU <= 0) perCU = 4;
     uint32_t c1 = std::min<uint32_t>(pa->refPool, 4096);
     if (const char *t = getenv("SNAPGPU_PAIRED_POOL1"); t && atoi(t) > 1) c1 = std::min<uint32_t>(pa->refPool, (uint32_t)atoi(t));
-    if (allocPass(pa->pass[0], prop.multiProcessorCount * std::min(perCU, 8), c1, std::max<uint32_t>(1, std::min(pa->refPool / 2, c1 / 2)), c1))
+    if (allocPass(pa->pass[0], prop.multiProcessorCount * perCU, c1, std::max<uint32_t>(1, std::min(pa->refPool / 2, c1 / 2)), c1))
         { snapgpu_paired_aligner_free(pa); return nullptr; }
     int perCU2 = 0;
     hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU2, (const void *)paired_kernel<512>, 64, 0);
