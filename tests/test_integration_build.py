@@ -38,3 +38,22 @@ def test_extension_builds_against_reference_and_fails_loudly_without_gpu(tmp_pat
                        capture_output=True, text=True, timeout=120)
     assert p.returncode != 0
     assert "MI355X aligner" in p.stdout + p.stderr and "no such HIP device" in p.stdout + p.stderr
+
+
+@pytest.mark.reference
+def test_paired_dropin_builds_and_fails_loudly_without_gpu(tmp_path):
+    """GpuPairedEndAligner (a PairedEndAligner, PairedEndAligner.h:60-78) in the same binary:
+    `snap-rna-gpu pairs` must stop at the GPU aligner's construction here, not fall back."""
+    if not os.path.exists(os.path.join(REF, "snap-rna")) or not os.path.isdir("/root/reference/SNAPLib"):
+        pytest.skip("reference build (oracle/_ref) not available: build container only")
+    subprocess.run(["make", "-s", "-f", os.path.join(ROOT, "snap-rnaseq_amd", "integration", "Makefile")], check=True)
+    exe = os.path.join(REF, "integration", "snap-rna-gpu")
+    subprocess.run([os.path.join(REF, "snap-rna"), "index", os.path.join(G, "small.fa"), str(tmp_path / "gidx")],
+                   check=True, capture_output=True)
+    import snapgpu
+    if snapgpu.device_count() > 0:
+        pytest.skip("GPU present: the no-GPU failure path is what this container checks")
+    p = subprocess.run([exe, "pairs", str(tmp_path / "gidx"), os.path.join(G, "paired_1.fq"),
+                        os.path.join(G, "paired_2.fq")], capture_output=True, text=True, timeout=120)
+    assert p.returncode != 0
+    assert "MI355X paired aligner" in p.stdout + p.stderr and "no such HIP device" in p.stdout + p.stderr
