@@ -7,7 +7,7 @@ for i in 1 2; do
   for v in "$@"; do
     k=$((k+1))
     env $v timeout -k 10 120 python bench.py --steps 20 --no-cpu-baseline --no-extras > gpurun_out/abe_${k}_$i.log 2>/dev/null || exit $?
-    env $v timeout -k 10 120 python bench.py --steps 10 --resident-steps 10 --no-cpu-baseline > gpurun_out/abr_${k}_$i.log 2>/dev/null || exit $?
+    env $v timeout -k 10 120 python bench.py --steps 10 --resident-steps 10 --no-cpu-baseline --paired-pairs 0 > gpurun_out/abr_${k}_$i.log 2>/dev/null || exit $?
   done
 done
 python3 - "$@" <<'PY'
