@@ -94,14 +94,22 @@ struct PLds {
     static constexpr int NB = MAXLEN / 64;
     char rd[2][2][MAXLEN + 64];             // [read][direction] bases, upper-cased, zero slack
     char rq[2][2][MAXLEN + 64];             // qualities in the same coordinates
-    uint32_t win[(MAXLEN + 192) / 4];       // genome window of scoreLocation
-    uint16_t rows[MAX_K][WAVE];             // lv_wave row history
-    int16_t btAct[MAX_K + 1], btMatched[MAX_K + 1];
-    HitSet hs[2][2];                        // [read][direction]
+    uint32_t win[MAXLEN == 128 ? 1 : (MAXLEN + 192) / 4];   // <512>: genome window of scoreLocation
+    // phases 1-2 (seeds, hit sets) and phase 3 (scoring) never overlap: their scratch shares LDS
+    union {
+        struct {
+            HitSet hs[2][2];                // [read][direction]
+            uint32_t look[2][LCAP][8];      // per read, seed and direction: nHits, at, single, trimmed nHits
+        } walk;
+        struct {
+            uint16_t rows[MAX_K][WAVE];     // lv_wave row history
+            int16_t btAct[MAX_K + 1], btMatched[MAX_K + 1];
+        } lv;
+    } u;
     uint32_t miss[LCAP];                    // DisjointHitSet::missCount scratch
     uint32_t sel[2][LCAP];                  // chosen seed offsets per read (bit 31: a wrap preceded it)
-    uint32_t look[2][LCAP][8];                 // per seed and direction: nHits, at, single, nHits after the trim
     uint64_t validBits[NB], usedBits[NB];
+    uint64_t rpl[2][2][3][2];               // <128>: read bit planes [read][dir]{hi, lo, notACGT} x 2 words
     int32_t lists[MAX_LISTS];
 };
 
@@ -115,107 +123,130 @@ __device__ __forceinline__ uint32_t hit_at(const PArgs &P, const Lookup &l, uint
 }
 
 // --------------------------------------------------------------- hit sets
-// Lane i owns lookup i.  Ties between lookups go to the lowest index, as the reference's
-// in-order scans with strict comparisons do.
+// The intersection walks two hit sets at a time (the fewer-hits and the more-hits end of one set
+// pair).  Lane i keeps lookup i of each in registers: its cursor (currentHitForIntersection) and
+// the hits at cur - 1, cur and cur + 1, so computeBestPossibleScoreForCurrentHit needs no load and
+// getNextLowerHit's advance uses the prefetched next hit (the load for the one after it is issued
+// then and only waited for at the next advance).  Ties between lookups go to the lowest index,
+// as the reference's in-order scans with strict comparisons do.
+struct LaneLk {
+    uint32_t cur, nHits, so, set, at, single;
+    uint32_t curV, prevV, nextV;   // hits[cur], hits[cur - 1], hits[cur + 1] (when they exist)
+    bool on;                       // lane < nLookups
+};
+struct Walk {                      // one hit set being walked: per-lane lookups + uniform state
+    LaneLk l;
+    uint32_t last;                 // mostRecentLocationReturned
+    uint32_t nLookups;
+    int32_t curSet;
+    const uint32_t *exhausted;     // LDS: DisjointHitSet::countOfExhaustedHits
+};
+
+__device__ __forceinline__ uint32_t lk_hit(const PArgs &P, const LaneLk &l, uint32_t i) {
+    return l.single ? l.at : P.X.overflow[l.at + i];
+}
+
+__device__ __forceinline__ void walk_init(const PArgs &P, const HitSet &h, Walk &w) {
+    const int lane = lane_id();
+    w.nLookups = h.nLookups;
+    w.curSet = h.curSet;
+    w.exhausted = h.exhausted;
+    w.last = 0;
+    LaneLk &l = w.l;
+    l.on = (uint32_t)lane < w.nLookups;
+    const Lookup k = h.lk[l.on ? lane : 0];
+    l.cur = 0; l.nHits = l.on ? k.nHits : 0; l.so = k.seedOffset; l.set = k.set; l.at = k.at; l.single = k.single;
+    l.curV = l.nHits > 0 ? lk_hit(P, l, 0) : 0u;
+    l.nextV = l.nHits > 1 ? lk_hit(P, l, 1) : 0u;
+    l.prevV = 0;
+}
+
 __device__ __forceinline__ uint64_t best_key(bool have, uint32_t v, int lane) {
     return have ? ((uint64_t)v << 8) | (uint64_t)(255 - lane) : 0ull;
 }
-
-// getFirstHit (:1270-1284)
-template <int MAXLEN>
-__device__ bool hs_first(const PArgs &P, HitSet &h, uint32_t &loc, uint32_t &seedOff) {
-    const int lane = lane_id();
-    bool have = false;
-    uint32_t v = 0;
-    if ((uint32_t)lane < h.nLookups) {
-        const Lookup l = h.lk[lane];
-        if (l.nHits > 0) { v = hit_at(P, l, 0) - l.seedOffset; have = v > 0; }
-    }
-    const uint64_t k = uni64(max_reduce64(best_key(have, v, lane)));
-    loc = 0;
+__device__ __forceinline__ bool take_best(Walk &w, uint64_t k, uint32_t &loc, uint32_t &seedOff) {
     if (k == 0) return false;
     loc = (uint32_t)(k >> 8);
-    seedOff = h.lk[255 - (int)(k & 255)].seedOffset;
-    h.lastReturned = loc;
-    wave_sync();
+    seedOff = (uint32_t)__builtin_amdgcn_readlane((int)w.l.so, 255 - (int)(k & 255));
+    w.last = loc;
     return true;
 }
 
-// getNextHitLessThanOrEqualTo, the version the reference compiles (:1219-1266)
-template <int MAXLEN>
-__device__ bool hs_next_le(const PArgs &P, HitSet &h, uint32_t maxOff, uint32_t &loc, uint32_t &seedOff) {
+// getFirstHit (:1270-1284)
+__device__ bool hs_first(Walk &w, uint32_t &loc, uint32_t &seedOff) {
     const int lane = lane_id();
+    const LaneLk &l = w.l;
+    const uint32_t v = l.curV - l.so;
+    const uint64_t k = uni64(max_reduce64(best_key(l.on && l.nHits > 0 && v > 0, v, lane)));
+    loc = 0;
+    return take_best(w, k, loc, seedOff);
+}
+
+// getNextHitLessThanOrEqualTo, the version the reference compiles (:1219-1266)
+__device__ bool hs_next_le(const PArgs &P, Walk &w, uint32_t maxOff, uint32_t &loc, uint32_t &seedOff) {
+    const int lane = lane_id();
+    LaneLk &l = w.l;
     bool have = false;
     uint32_t v = 0;
-    if ((uint32_t)lane < h.nLookups) {
-        const Lookup l = h.lk[lane];
+    if (l.on) {
         int lim0 = (int)l.cur, lim1 = (int)l.nHits - 1;
-        const uint32_t maxThis = maxOff + l.seedOffset;
-        uint32_t cur = l.cur;
+        const uint32_t maxThis = maxOff + l.so;
         while (lim0 <= lim1) {
             const uint32_t probe = (uint32_t)(lim0 + lim1) / 2;
-            const uint32_t hp = hit_at(P, l, probe);
-            if (hp <= maxThis && (probe == 0 || hit_at(P, l, probe - 1) > maxThis)) {
-                v = hp - l.seedOffset;
+            const uint32_t hp = lk_hit(P, l, probe);
+            const uint32_t hq = probe == 0 ? 0u : lk_hit(P, l, probe - 1);
+            if (hp <= maxThis && (probe == 0 || hq > maxThis)) {
+                v = hp - l.so;
                 have = v > 0;
-                cur = probe;
+                l.cur = probe;
+                l.curV = hp;
+                l.prevV = hq;
+                l.nextV = probe + 1 < l.nHits ? lk_hit(P, l, probe + 1) : 0u;
                 break;
             }
             if (hp > maxThis) lim0 = (int)probe + 1;
             else lim1 = (int)(probe - 1);
         }
-        if (lim0 > lim1) cur = l.nHits;
-        h.lk[lane].cur = cur;
+        if (lim0 > lim1 && l.cur != l.nHits) {   // exhausted: hits[cur - 1] is now the last hit
+            l.cur = l.nHits;
+            l.prevV = l.nHits ? lk_hit(P, l, l.nHits - 1) : 0u;
+        }
     }
     const uint64_t k = uni64(max_reduce64(best_key(have, v, lane)));
-    wave_sync();
-    if (k == 0) return false;
-    loc = (uint32_t)(k >> 8);
-    seedOff = h.lk[255 - (int)(k & 255)].seedOffset;
-    h.lastReturned = loc;
-    wave_sync();
-    return true;
+    return take_best(w, k, loc, seedOff);
 }
 
 // getNextLowerHit (:1286-1322)
-template <int MAXLEN>
-__device__ bool hs_next_lower(const PArgs &P, HitSet &h, uint32_t &loc, uint32_t &seedOff) {
+__device__ bool hs_next_lower(const PArgs &P, Walk &w, uint32_t &loc, uint32_t &seedOff) {
     const int lane = lane_id();
+    LaneLk &l = w.l;
     bool have = false;
     uint32_t v = 0;
-    const uint32_t last = h.lastReturned;
-    if ((uint32_t)lane < h.nLookups) {
-        const Lookup l = h.lk[lane];
-        uint32_t cur = l.cur;
-        if (cur != l.nHits && hit_at(P, l, cur) - l.seedOffset == last) cur++;
-        if (cur != l.nHits) {
-            const uint32_t hc = hit_at(P, l, cur);
-            if (hc >= l.seedOffset) { v = hc - l.seedOffset; have = v > 0; }
+    if (l.on) {
+        if (l.cur != l.nHits && l.curV - l.so == w.last) {
+            l.cur++;
+            l.prevV = l.curV;
+            l.curV = l.nextV;
+            l.nextV = l.cur + 1 < l.nHits ? lk_hit(P, l, l.cur + 1) : 0u;
         }
-        h.lk[lane].cur = cur;
+        if (l.cur != l.nHits && l.curV >= l.so) { v = l.curV - l.so; have = v > 0; }
     }
     const uint64_t k = uni64(max_reduce64(best_key(have, v, lane)));
-    wave_sync();
-    if (k == 0) return false;
-    loc = (uint32_t)(k >> 8);
-    seedOff = h.lk[255 - (int)(k & 255)].seedOffset;
-    h.lastReturned = loc;
-    wave_sync();
-    return true;
+    return take_best(w, k, loc, seedOff);
 }
 
 // computeBestPossibleScoreForCurrentHit (:901-929): the largest miss count of any disjoint hit set
 template <int MAXLEN>
-__device__ uint32_t hs_best_possible(const PArgs &P, PLds<MAXLEN> &S, HitSet &h, uint32_t maxMerge) {
+__device__ uint32_t hs_best_possible(PLds<MAXLEN> &S, const Walk &w, uint32_t maxMerge) {
     const int lane = lane_id();
-    const int nSets = h.curSet + 1;
-    if (lane < nSets) S.miss[lane] = h.exhausted[lane];
+    const int nSets = w.curSet + 1;
+    if (lane < nSets) S.miss[lane] = w.exhausted[lane];
     wave_sync();
-    if ((uint32_t)lane < h.nLookups) {
-        const Lookup l = h.lk[lane];
-        const uint32_t target = h.lastReturned + l.seedOffset;
-        const bool nearCur = l.cur != l.nHits && is_within(hit_at(P, l, l.cur), target, maxMerge);
-        const bool nearPrev = l.cur != 0 && is_within(hit_at(P, l, l.cur - 1), target, maxMerge);
+    const LaneLk &l = w.l;
+    if (l.on) {
+        const uint32_t target = w.last + l.so;
+        const bool nearCur = l.cur != l.nHits && is_within(l.curV, target, maxMerge);
+        const bool nearPrev = l.cur != 0 && is_within(l.prevV, target, maxMerge);
         if (!(nearCur || nearPrev)) atomicAdd(&S.miss[l.set], 1u);
     }
     wave_sync();
@@ -267,26 +298,51 @@ __device__ void score_location(const PArgs &P, PLds<MAXLEN> &S, int r, int dir, 
         if (glen >= n - (uint32_t)MAX_K) ok = substring_ok(X, loc, glen);
     }
     if (!ok) { score = FAIL_SCORE; prob = 0; return; }
-    // genome bytes [loc - 64, loc + n + 128) into LDS (4-byte aligned start)
-    const int64_t astart = ((int64_t)loc - 64) & ~(int64_t)3;
-    const int nwords = ((int)n + 192 + 4) / 4;
-    const uint32_t *src = (const uint32_t *)(X.genome + astart);
-    for (int i = lane; i < nwords && i < (MAXLEN + 192) / 4; i += WAVE) S.win[i] = src[i];
-    wave_sync();
-    const int w0 = (int)((int64_t)loc - astart);
-    const int kmax = scoreLimit < (uint32_t)(MAX_K - 1) ? (int)scoreLimit : MAX_K - 1;
-    uint32_t rb[NB];
-#pragma unroll
-    for (int b = 0; b < NB; b++) rb[b] = (uint8_t)S.rd[r][dir][b * 64 + lane];
     Bitmap<NB> F;
-    build_bitmap<NB>(F, rb, rb, false, (const char *)S.win, w0, (int)n, kmax);
+    if constexpr (MAXLEN == 128) {
+        // lane l holds diagonal x = l - 31: F_x[m] = read[m] != genome[loc + x + m] from the genome
+        // and read bit planes (as lv_pass, align_score.h); bytes past the read are not ACGT
+        const int64_t gp = (int64_t)loc + (lane - 31) + PACK_GUARD;
+        const uint4 *src = X.gpl + (gp >> 5);
+        const uint32_t sh = (uint32_t)gp & 31;
+        uint4 w[5];
+#pragma unroll
+        for (int j = 0; j < 5; j++) w[j] = src[j];
+        const uint64_t *rp = &S.rpl[r][dir][0][0];
+        const uint64_t rh0 = rp[0], rh1 = rp[1], rl0 = rp[2], rl1 = rp[3], rm0 = rp[4], rm1 = rp[5];
+        uint32_t f[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t gh = __builtin_amdgcn_alignbit(w[j + 1].x, w[j].x, sh);
+            const uint32_t gl = __builtin_amdgcn_alignbit(w[j + 1].y, w[j].y, sh);
+            const uint32_t gm = __builtin_amdgcn_alignbit(w[j + 1].z, w[j].z, sh);
+            const uint64_t RH = j < 2 ? rh0 : rh1, RL = j < 2 ? rl0 : rl1, RM = j < 2 ? rm0 : rm1;
+            const uint32_t sft = 32 * (j & 1);
+            f[j] = (gh ^ (uint32_t)(RH >> sft)) | (gl ^ (uint32_t)(RL >> sft)) | gm | (uint32_t)(RM >> sft);
+        }
+        F.w[0] = ((uint64_t)f[1] << 32) | f[0];
+        F.w[1] = ((uint64_t)f[3] << 32) | f[2];
+    } else {
+        // genome bytes [loc - 64, loc + n + 128) into LDS (4-byte aligned start), byte compares
+        const int64_t astart = ((int64_t)loc - 64) & ~(int64_t)3;
+        const int nwords = ((int)n + 192 + 4) / 4;
+        const uint32_t *src = (const uint32_t *)(X.genome + astart);
+        for (int i = lane; i < nwords && i < (MAXLEN + 192) / 4; i += WAVE) S.win[i] = src[i];
+        wave_sync();
+        const int w0 = (int)((int64_t)loc - astart);
+        const int kmax = scoreLimit < (uint32_t)(MAX_K - 1) ? (int)scoreLimit : MAX_K - 1;
+        uint32_t rb[NB];
+#pragma unroll
+        for (int b = 0; b < NB; b++) rb[b] = (uint8_t)S.rd[r][dir][b * 64 + lane];
+        build_bitmap<NB>(F, rb, rb, false, (const char *)S.win, w0, (int)n, kmax);
+    }
     const char *q = S.rq[r][dir];
     const int s = (int)seedOffset, t = s + (int)X.seedLen;
-    const LvOut r1 = lv_wave<1, NB>(F, t, (int)n - t, (int)glen - t, (int)scoreLimit, q, S.rows, S.btAct,
-                                    S.btMatched, X.tab);
+    const LvOut r1 = lv_wave<1, NB>(F, t, (int)n - t, (int)glen - t, (int)scoreLimit, q, S.u.lv.rows, S.u.lv.btAct,
+                                    S.u.lv.btMatched, X.tab);
     if (r1.score == -1) { score = FAIL_SCORE; prob = 0; return; }
     const int limitLeft = (int)scoreLimit - r1.score;
-    const LvOut r2 = lv_wave<-1, NB>(F, s - 1, s, s + MAX_K, limitLeft, q, S.rows, S.btAct, S.btMatched, X.tab);
+    const LvOut r2 = lv_wave<-1, NB>(F, s - 1, s, s + MAX_K, limitLeft, q, S.u.lv.rows, S.u.lv.btAct, S.u.lv.btMatched, X.tab);
     offset = r2.netIndel;
     if (r2.score == -1) { score = FAIL_SCORE; prob = 0; return; }
     score = (uint32_t)(r1.score + r2.score);
@@ -337,7 +393,7 @@ __device__ __forceinline__ uint32_t choose_seeds(const PArgs &P, PLds<MAXLEN> &S
     const uint32_t seedLen = X.seedLen;
 #pragma unroll
     for (int d = 0; d < 2; d++)
-        if (lane == 0) { S.hs[r][d].nLookups = 0; S.hs[r][d].curSet = -1; S.hs[r][d].lastReturned = 0; }
+        if (lane == 0) { S.u.walk.hs[r][d].nLookups = 0; S.u.walk.hs[r][d].curSet = -1; S.u.walk.hs[r][d].lastReturned = 0; }
     const uint32_t nPossible = nr - seedLen + 1;
     // Seed::DoesTextRepresentASeed per start position, and a clear seedUsed
 #pragma unroll
@@ -442,8 +498,8 @@ __device__ __forceinline__ void lookup_seeds(const PArgs &P, PLds<MAXLEN> &S, co
                 while (l.nHits > 0 && hit_at(P, l, l.nHits - 1) < offset) l.nHits--;
             tr[d] = l.nHits;
         }
-        S.look[r][k][0] = nh[0]; S.look[r][k][1] = at[0]; S.look[r][k][2] = sg[0]; S.look[r][k][3] = tr[0];
-        S.look[r][k][4] = nh[1]; S.look[r][k][5] = at[1]; S.look[r][k][6] = sg[1]; S.look[r][k][7] = tr[1];
+        S.u.walk.look[r][k][0] = nh[0]; S.u.walk.look[r][k][1] = at[0]; S.u.walk.look[r][k][2] = sg[0]; S.u.walk.look[r][k][3] = tr[0];
+        S.u.walk.look[r][k][4] = nh[1]; S.u.walk.look[r][k][5] = at[1]; S.u.walk.look[r][k][6] = sg[1]; S.u.walk.look[r][k][7] = tr[1];
     }
     wave_sync();
     wave_sync();
@@ -526,6 +582,26 @@ __device__ void align_pair(const PArgs &P, PLds<MAXLEN> &S, Cand *cand, Mate *ma
     if (n0 > P.maxLen || n1 > P.maxLen) { defer_pair<MAXLEN>(P, pi); return; }
     uint32_t countNs = load_read<MAXLEN>(P, S, 0, n0, o0) + load_read<MAXLEN>(P, S, 1, n1, o1);
     wave_sync();
+    if constexpr (MAXLEN == 128) {
+        // read bit planes of both reads and directions; a genome with IUPAC codes and a read with
+        // a non-ACGTN byte need byte compares (an IUPAC code can match itself): pass 2
+        bool other = false;
+#pragma unroll
+        for (int r = 0; r < 2; r++)
+#pragma unroll
+            for (int dr = 0; dr < 2; dr++)
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const uint8_t c = (uint8_t)S.rd[r][dr][h * 64 + lane];
+                    const uint32_t code = packed_code(c);
+                    const uint64_t bh = ballot(code < 4 && (code & 2)), bl = ballot(code < 4 && (code & 1));
+                    const uint64_t bm = ballot(code > 3);
+                    other = other || (c != 0 && code > 3 && c != 'N');
+                    if (lane == 0) { S.rpl[r][dr][0][h] = bh; S.rpl[r][dr][1][h] = bl; S.rpl[r][dr][2][h] = bm; }
+                }
+        wave_sync();
+        if (X.hasIupac && ballot(other)) { defer_pair<MAXLEN>(P, pi); return; }
+    }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) countNs += (uint32_t)__shfl_xor((int)countNs, o);
     countNs = uni(countNs);
@@ -538,8 +614,8 @@ __device__ void align_pair(const PArgs &P, PLds<MAXLEN> &S, Cand *cand, Mate *ma
     const uint32_t nSel0 = choose_seeds<MAXLEN>(P, S, 0, n0, maxSeeds);
     const uint32_t nSel1 = choose_seeds<MAXLEN>(P, S, 1, n1, maxSeeds);
     lookup_seeds<MAXLEN>(P, S, n0, n1, nSel0, nSel1);
-    record_hits(P, S.hs[0], S.look[0], S.sel[0], nSel0, n0, t00, t01, pop0);
-    record_hits(P, S.hs[1], S.look[1], S.sel[1], nSel1, n1, t10, t11, pop1);
+    record_hits(P, S.u.walk.hs[0], S.u.walk.look[0], S.sel[0], nSel0, n0, t00, t01, pop0);
+    record_hits(P, S.u.walk.hs[1], S.u.walk.look[1], S.sel[1], nSel1, n1, t10, t11, pop1);
     const uint32_t popularAll = pop0 + pop1;
     const int more = t00 + t01 > t10 + t11 ? 0 : 1, fewer = 1 - more;            // :342-343
     const uint32_t nFewer = fewer ? n1 : n0, nMore = fewer ? n0 : n1;
@@ -551,24 +627,25 @@ __device__ void align_pair(const PArgs &P, PLds<MAXLEN> &S, Cand *cand, Mate *ma
     bool deferIt = false, exhausted = false;
     for (int sp = 0; sp < 2 && !deferIt && !exhausted; sp++) {
         // set pair 0 = read0 FORWARD + read1 RC, set pair 1 = read0 RC + read1 FORWARD (:351, :361-367)
-        HitSet &hf = S.hs[fewer][fewer ^ sp];
-        HitSet &hm = S.hs[more][more ^ sp];
+        Walk hf, hm;
+        walk_init(P, S.u.walk.hs[fewer][fewer ^ sp], hf);
+        walk_init(P, S.u.walk.hs[more][more ^ sp], hm);
         Mate *ms = sp ? mates1 : mates0;
         uint32_t nM = 0;
         uint32_t fewerLoc = 0, fewerSeed = 0, moreLoc, moreSeed = 0;
         bool outOfMore = false;
-        if (!hs_first<MAXLEN>(P, hf, fewerLoc, fewerSeed)) continue;
+        if (!hs_first(hf, fewerLoc, fewerSeed)) continue;
         moreLoc = INVALID;
         for (;;) {
             if (moreLoc > fewerLoc + maxSp) {
-                if (!hs_next_le<MAXLEN>(P, hm, fewerLoc + maxSp, moreLoc, moreSeed)) break;
+                if (!hs_next_le(P, hm, fewerLoc + maxSp, moreLoc, moreSeed)) break;
             }
             if (moreLoc + maxSp < fewerLoc && (nM == 0 || !is_within(ms[nM - 1].loc, fewerLoc, maxSp))) {
-                if (!hs_next_le<MAXLEN>(P, hf, moreLoc + maxSp, fewerLoc, fewerSeed)) break;
+                if (!hs_next_le(P, hf, moreLoc + maxSp, fewerLoc, fewerSeed)) break;
                 continue;
             }
             while (moreLoc + maxSp >= fewerLoc && !outOfMore) {
-                const uint32_t bps = hs_best_possible<MAXLEN>(P, S, hm, maxK);
+                const uint32_t bps = hs_best_possible<MAXLEN>(S, hm, maxK);
                 if (nM >= P.refPool / 2) { exhausted = true; break; }                   // :436-439
                 if (nM >= P.mateCap) { deferIt = true; break; }
                 Mate m;
@@ -576,10 +653,10 @@ __device__ void align_pair(const PArgs &P, PLds<MAXLEN> &S, Cand *cand, Mate *ma
                 m.seedOffset = moreSeed; m.genomeOffset = 0;
                 ms[nM] = m;
                 nM++;
-                if (!hs_next_lower<MAXLEN>(P, hm, moreLoc, moreSeed)) { moreLoc = 0; outOfMore = true; break; }
+                if (!hs_next_lower(P, hm, moreLoc, moreSeed)) { moreLoc = 0; outOfMore = true; break; }
             }
             if (deferIt || exhausted) break;
-            const uint32_t bpsF = hs_best_possible<MAXLEN>(P, S, hf, maxK);
+            const uint32_t bpsF = hs_best_possible<MAXLEN>(S, hf, maxK);
             // lowest best possible score of the mates up to maxSpacing above this fewer hit,
             // 64 mates per step from the lowest up (:469-475)
             uint32_t lowest = maxK + extra;
@@ -609,7 +686,7 @@ __device__ void align_pair(const PArgs &P, PLds<MAXLEN> &S, Cand *cand, Mate *ma
                 nCand++;
                 if (li > maxUsedList) maxUsedList = li;
             }
-            if (!hs_next_lower<MAXLEN>(P, hf, fewerLoc, fewerSeed)) break;
+            if (!hs_next_lower(P, hf, fewerLoc, fewerSeed)) break;
         }
     }
     if (exhausted) { res.flags |= SNAPGPU_PFLAG_POOL_EXHAUSTED; write_result<MAXLEN>(P, pi, res); return; }
