@@ -84,3 +84,30 @@ def test_c3_shard_parity_and_properties(c3):
     again = dev.results()
     assert np.array_equal(again.view(np.uint8), out.view(np.uint8))
     _log("resident path equal")
+
+
+@pytest.mark.gpu
+def test_c3_paired_shard(c3):
+    """Row f2 at C3 scale (BASELINE configs[3] shape on the 3.1 Gb genome): 250k wgsim-like
+    2 x 101 pairs through ChimericPairedEndAligner on the GPU; every field of a 20k-pair sample
+    against the C restatement, and properties over the whole batch."""
+    from oracle_ffi import oracle_paired
+    idx, al, reads, info = c3
+    r0, r1 = snapgpu.Reads.synthetic_pairs(idx.genome_handle(), 250_000, seed=31, read_length=101)
+    pa = snapgpu.PairedAligner(idx, device=0)
+    res = pa.align(r0, r1)
+    _log("paired shard aligned")
+    ns = 20_000
+    cpu = oracle_paired(idx, r0.slice(0, ns), r1.slice(0, ns), pa.params, chimeric=True, n_threads=16)
+    for f in ("status", "location", "direction", "score", "mapq", "fromAlignTogether", "alignedAsPair",
+              "nLocationsScored", "nSingleScored"):
+        bad = np.nonzero((res[f][:ns] != cpu[f]).reshape(ns, -1).any(axis=1))[0]
+        assert len(bad) == 0, f"{f}: {len(bad)} pairs differ, e.g. {res[bad[0]]} vs {cpu[bad[0]]}"
+    _log("paired oracle sample equal")
+    together = res["fromAlignTogether"] == 1
+    assert together.mean() > 0.9
+    both = together & (res["status"][:, 0] == snapgpu.SingleHit) & (res["status"][:, 1] == snapgpu.SingleHit)
+    loc, _ = r0.truth()
+    near = np.abs(res["location"][:, 0].astype(np.int64) - loc.astype(np.int64)) <= 1200
+    assert near[both].mean() > 0.97
+    assert np.all(res["score"][both] <= pa.params.maxK)
