@@ -62,11 +62,13 @@ struct PArgs {
     uint32_t maxLen;                        // reads this pass takes (128 or 512)
 };
 
-struct Lookup {                             // HashTableLookup (IntersectingPairedEndAligner.h:101-134)
-    uint32_t seedOffset, nHits, cur, set;
+struct Lookup {                             // HashTableLookup (IntersectingPairedEndAligner.h:101-134);
     uint32_t at;                            // overflow index of hits[0], or the singleton value
-    uint32_t single;
+    uint32_t nHits;                         // the cursor lives in registers during the walk (LaneLk)
+    uint16_t seedOffset;
+    uint8_t set, single;
 };
+static_assert(sizeof(Lookup) == 12, "Lookup layout");
 struct HitSet {                             // HashTableHitSet (IntersectingPairedEndAligner.h:139-194)
     Lookup lk[LCAP];
     uint32_t exhausted[LCAP];               // DisjointHitSet::countOfExhaustedHits
@@ -99,7 +101,7 @@ struct PLds {
     union {
         struct {
             HitSet hs[2][2];                // [read][direction]
-            uint32_t look[2][LCAP][8];      // per read, seed and direction: nHits, at, single, trimmed nHits
+            uint32_t look[2][LCAP][6];      // per read, seed, direction: nHits | single << 31, at, trimmed
         } walk;
         struct {
             uint16_t rows[MAX_K][WAVE];     // lv_wave row history
@@ -261,7 +263,7 @@ __device__ __forceinline__ void hs_record(HitSet &h, uint32_t seedOffset, uint32
     if (begins) { h.curSet = h.curSet + 1; h.exhausted[h.curSet] = 0; }
     if (nHits == 0) { h.exhausted[h.curSet] = h.exhausted[h.curSet] + 1; wave_sync(); return; }
     Lookup l;
-    l.cur = 0; l.nHits = trimmed; l.seedOffset = seedOffset; l.set = (uint32_t)h.curSet; l.at = at; l.single = single;
+    l.nHits = trimmed; l.seedOffset = (uint16_t)seedOffset; l.set = (uint8_t)h.curSet; l.at = at; l.single = (uint8_t)single;
     h.lk[h.nLookups] = l;
     h.nLookups = h.nLookups + 1;
     wave_sync();
@@ -492,14 +494,13 @@ __device__ __forceinline__ void lookup_seeds(const PArgs &P, PLds<MAXLEN> &S, co
 #pragma unroll
         for (int d = 0; d < 2; d++) {
             const uint32_t offset = d == 0 ? so : nr - seedLen - so;
-            Lookup l;
-            l.nHits = nh[d]; l.at = at[d]; l.single = sg[d]; l.seedOffset = offset; l.cur = 0; l.set = 0;
+            uint32_t t = nh[d];
             if (nh[d] < P.maxBigHits)
-                while (l.nHits > 0 && hit_at(P, l, l.nHits - 1) < offset) l.nHits--;
-            tr[d] = l.nHits;
+                while (t > 0 && (sg[d] ? at[d] : X.overflow[at[d] + t - 1]) < offset) t--;
+            tr[d] = t;
         }
-        S.u.walk.look[r][k][0] = nh[0]; S.u.walk.look[r][k][1] = at[0]; S.u.walk.look[r][k][2] = sg[0]; S.u.walk.look[r][k][3] = tr[0];
-        S.u.walk.look[r][k][4] = nh[1]; S.u.walk.look[r][k][5] = at[1]; S.u.walk.look[r][k][6] = sg[1]; S.u.walk.look[r][k][7] = tr[1];
+        S.u.walk.look[r][k][0] = nh[0] | (sg[0] << 31); S.u.walk.look[r][k][1] = at[0]; S.u.walk.look[r][k][2] = tr[0];
+        S.u.walk.look[r][k][3] = nh[1] | (sg[1] << 31); S.u.walk.look[r][k][4] = at[1]; S.u.walk.look[r][k][5] = tr[1];
     }
     wave_sync();
     wave_sync();
@@ -507,7 +508,7 @@ __device__ __forceinline__ void lookup_seeds(const PArgs &P, PLds<MAXLEN> &S, co
 
 // The hit sets of read r in the reference's order (:313-328): where a disjoint hit set begins
 // depends on which lookups were recorded (a lookup with >= maxBigHits hits is skipped).
-__device__ __forceinline__ void record_hits(const PArgs &P, HitSet (&hs)[2], const uint32_t (&look)[LCAP][8],
+__device__ __forceinline__ void record_hits(const PArgs &P, HitSet (&hs)[2], const uint32_t (&look)[LCAP][6],
                                             const uint32_t *sel, const uint32_t nSel, const uint32_t nr,
                                             uint32_t &totF, uint32_t &totR, uint32_t &popular) {
     const uint32_t seedLen = P.X.seedLen;
@@ -519,10 +520,10 @@ __device__ __forceinline__ void record_hits(const PArgs &P, HitSet (&hs)[2], con
 #pragma unroll
         for (int d = 0; d < 2; d++) {
             const uint32_t offset = d == 0 ? so : nr - seedLen - so;
-            const uint32_t nh = look[k][4 * d];
+            const uint32_t nh = look[k][3 * d] & 0x7fffffffu;
             if (nh < P.maxBigHits) {
                 if (d == 0) totF += nh; else totR += nh;
-                hs_record(hs[d], offset, nh, look[k][4 * d + 3], look[k][4 * d + 1], look[k][4 * d + 2],
+                hs_record(hs[d], offset, nh, look[k][3 * d + 2], look[k][3 * d + 1], look[k][3 * d] >> 31,
                           begins[d]);
                 begins[d] = false;
             } else popular++;
