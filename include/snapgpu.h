@@ -279,9 +279,13 @@ int snapgpu_align_batch_wait(snapgpu_aligner_t *a);
  *    up to maxHitsToGet hits with edit distance in [best, best+3] per read, written to
  *    multiHits[i * maxHitsToGet ..], their count to multiHitsFound[i].
  * search may be NULL (no window for any read); maxHitsToGet 0 disables multi-hit
- * export (multiHitsFound / multiHits may then be NULL); at most
- * SNAPGPU_MAX_MULTI_HITS_TO_GET (BaseAligner.h:149). */
-#define SNAPGPU_MAX_MULTI_HITS_TO_GET 512
+ * export (multiHitsFound / multiHits may then be NULL); at most SNAPGPU_MAX_MULTI_HITS_TO_GET.
+ * The reference keeps 512 hits per distance (BaseAligner.h:148-151) but counts up to
+ * maxHitsToGet per distance, so above 512 a distance's extra hits overwrite the next
+ * distances' rows; that layout is reproduced (the RNA paired path asks for 1000,
+ * PairedAligner.cpp:584).  maxHitsToGet > 512 needs (maxK + extraSearchDepth) * 512 +
+ * maxHitsToGet <= 31 * 512 (the writes stay inside the reference's table). */
+#define SNAPGPU_MAX_MULTI_HITS_TO_GET 1024
 typedef struct snapgpu_search {
     uint32_t searchRadius;
     uint32_t searchLocation;
@@ -556,6 +560,46 @@ int snapgpu_paired_intersect_batch(snapgpu_paired_aligner_t *pa, const snapgpu_r
                                    const snapgpu_reads_t *reads1, snapgpu_pair_result_t *out);
 /* The single-end BaseAligner the chimeric fallback uses (maxHits, maxK, seeds of the params). */
 snapgpu_aligner_t *snapgpu_paired_aligner_single(snapgpu_paired_aligner_t *pa);
+
+/* ------------------------------------------- RNA seed census
+ * BaseAligner::CharacterizeSeeds (BaseAligner.cpp:206-508) on the GPU: the seeds of AlignRead's
+ * order until numSeeds directions applied (or the wrap runs out), every hit of a side that is
+ * not popular recorded as (read-start location implied by the hit, seed offset).  The
+ * reference returns two std::map<unsigned, std::set<unsigned>> (map = forward, mapRC = RC);
+ * here each map entry is one run record, forward runs first, then RC runs, locations ascending
+ * (the maps' iteration order).  The caller's aligner supplies the index (its HBM upload); the
+ * scan parameters are those of the partial aligner PairedAligner.cpp:518-527 constructs. */
+typedef struct snapgpu_seed_run {
+    uint32_t location;     /* map key */
+    uint16_t minOffset;    /* *set.begin(): smallest seed offset (forward-read coordinates) */
+    uint16_t maxOffset;    /* *set.rbegin() */
+    uint16_t count;        /* set.size() */
+    uint8_t  direction;    /* 0: map, 1: mapRC */
+    uint8_t  reserved;
+} snapgpu_seed_run_t;      /* 12 bytes */
+typedef struct snapgpu_seed_runs {
+    uint64_t n;                 /* reads scanned */
+    uint64_t *start;            /* [n + 1]: read i's runs are runs[start[i] .. start[i + 1]) */
+    uint32_t *nForward;         /* [n]: how many of them are forward (map) runs */
+    uint32_t *flags;            /* [n]: SNAPGPU_FLAG_READ_TOO_LONG (the reference exits), SNAPGPU_FLAG_TOO_MANY_NS */
+    snapgpu_seed_run_t *runs;
+    uint64_t nRuns;
+} snapgpu_seed_runs_t;
+typedef struct snapgpu_charseeds_params {
+    uint32_t maxHits;              /* 300 (PairedAligner.cpp:520) */
+    uint32_t maxK;                 /* the paired maxDist, 15: reads with more Ns are skipped */
+    uint32_t numSeeds;             /* 12 (PairedAligner.cpp:523) */
+    uint32_t maxReadSize;          /* 500 */
+    uint32_t explorePopularSeeds;  /* 0 */
+    uint32_t reserved;
+} snapgpu_charseeds_params_t;
+void snapgpu_charseeds_params_default(snapgpu_charseeds_params_t *p);
+/* readList: indices into reads of the reads to scan (NULL: all, nList ignored).  Needs
+ * (numSeeds + 1) * maxHits <= 4096 and maxReadSize <= 512.  NULL on error (snapgpu_last_error). */
+snapgpu_seed_runs_t *snapgpu_characterize_seeds(snapgpu_aligner_t *a, const snapgpu_reads_t *reads,
+                                                const uint64_t *readList, uint64_t nList,
+                                                const snapgpu_charseeds_params_t *p);
+void snapgpu_seed_runs_free(snapgpu_seed_runs_t *runs);
 
 /* MAPQ (mapq.h:32-65) as the host computes it; exported for tests. */
 int snapgpu_compute_mapq(double pAll, double pBest, int score, int popularSeedsSkipped);

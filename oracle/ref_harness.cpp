@@ -28,6 +28,12 @@
 //             ChimericPairedEndAligner result, constructed as PairedAligner.cpp:462-482
 //             (paired defaults AlignerOptions.cpp:73-77: maxHits 16000, maxK 15, 8 seeds)
 //   cigar  <indexDir> <calls.tsv>  lines: loc dir useM read
+//   charseeds <indexDir> <reads.fq> [maxHits maxK numSeeds extra]
+//          -> BaseAligner::CharacterizeSeeds (BaseAligner.cpp:206-508) per read with the
+//             partial aligner of PairedAligner.cpp:518-527 (maxHits 300, maxK 15, 12 seeds):
+//             "i nF nRC F:loc:min:max:count,... RC:loc:min:max:count,..." (std::map order).
+//             Needs ref_harness_rna (BaseAligner.cpp at -O0: the function falls off its end,
+//             which g++ -O3 compiles into a crash; oracle/Makefile.ref).
 //          -> ed cigar   (SAMFormat::computeCigarString, SAM.cpp:1162-1230, restated
 //             around the reference's LandauVishkinWithCigar with zeroed slack bytes)
 #define private public          // read-only access to BaseAligner's private scoring state
@@ -331,6 +337,48 @@ static int mode_samheader(int argc, char **argv) {
     return 0;
 }
 
+static void dumpSeedMap(const char *tag, seed_map &m) {
+    printf("\t%s", tag);
+    bool first = true;
+    for (seed_map::iterator it = m.begin(); it != m.end(); ++it) {
+        printf("%s%u:%u:%u:%u", first ? ":" : ",", it->first, *it->second.begin(), *it->second.rbegin(),
+               (unsigned)it->second.size());
+        first = false;
+    }
+}
+
+static int mode_charseeds(int argc, char **argv) {
+    if (argc < 4) { fprintf(stderr, "charseeds <indexDir> <reads.fq> [maxHits maxK numSeeds extra]\n"); return 2; }
+    unsigned maxHits = argc > 4 ? atoi(argv[4]) : 300;
+    unsigned maxK = argc > 5 ? atoi(argv[5]) : 15;
+    unsigned numSeeds = argc > 6 ? atoi(argv[6]) : 12;
+    unsigned extra = argc > 7 ? atoi(argv[7]) : 2;
+    initializeLVProbabilitiesToPhredPlus33();
+    GenomeIndex *idx = GenomeIndex::loadFromDirectory(argv[2]);
+    if (!idx) { fprintf(stderr, "cannot load index %s\n", argv[2]); return 1; }
+    // the partial aligner of PairedAligner.cpp:518-527 (own LV objects, no BigAllocator)
+    BaseAligner *ba = new BaseAligner(idx, maxHits, maxK, MAX_READ_LENGTH, numSeeds, 0, extra, NULL, NULL);
+    std::ifstream in(argv[3]);
+    std::string id, bases, plus, quals;
+    unsigned i = 0;
+    while (std::getline(in, id) && std::getline(in, bases) && std::getline(in, plus) && std::getline(in, quals)) {
+        std::string b = bases + std::string(16, '\0');
+        std::string q = quals + std::string(16, '\0');
+        Read r;
+        r.init(id.c_str() + 1, (unsigned)id.size() - 1, b.c_str(), q.c_str(), (unsigned)bases.size());
+        seed_map map, mapRC;
+        unsigned loc = InvalidGenomeLocation; Direction dir = 0; int score = 0, mapq = 0;
+        ba->setReadId(0);
+        ba->CharacterizeSeeds(&r, &loc, &dir, &score, &mapq, 0, 0, FORWARD, map, mapRC);
+        printf("%u\t%u\t%u", i, (unsigned)map.size(), (unsigned)mapRC.size());
+        dumpSeedMap("F", map);
+        dumpSeedMap("RC", mapRC);
+        printf("\n");
+        i++;
+    }
+    return 0;
+}
+
 int main(int argc, char **argv) {
     if (argc < 2) { fprintf(stderr, "usage: ref_harness align|lv|lookup ...\n"); return 2; }
     std::string m = argv[1];
@@ -342,6 +390,7 @@ int main(int argc, char **argv) {
     if (m == "cigar") return mode_cigar(argc, argv);
     if (m == "paired") return mode_paired(argc, argv);
     if (m == "samheader") return mode_samheader(argc, argv);
+    if (m == "charseeds") return mode_charseeds(argc, argv);
     fprintf(stderr, "unknown mode %s\n", argv[1]);
     return 2;
 }

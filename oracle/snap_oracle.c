@@ -264,7 +264,8 @@ typedef struct {
     /* multi-hit recording (BaseAligner.h:149-152) */
     unsigned maxHitsToGet;
     unsigned hitCount[MAX_K];
-    uint32_t *hitLoc;                 /* [MAX_K][maxHitsToGet] */
+    unsigned hitSlot;                 /* distance stride: min(maxHitsToGet, 512) (BaseAligner.h:148-151) */
+    uint32_t *hitLoc;                 /* [MAX_K * hitSlot + extra]: rows alias above 512 as the reference's */
     uint8_t *hitRC;
 } Oracle;
 
@@ -421,8 +422,8 @@ static int score(Oracle *o, int force, unsigned readLen, int *result) {
                 }
                 /* BaseAligner.cpp:1255-1261 */
                 if (o->maxHitsToGet > 0 && sc != 0xffffffffu && sc < MAX_K && o->hitCount[sc] < o->maxHitsToGet) {
-                    o->hitLoc[sc * o->maxHitsToGet + o->hitCount[sc]] = loc;
-                    o->hitRC[sc * o->maxHitsToGet + o->hitCount[sc]] = (uint8_t)el->dir;
+                    o->hitLoc[sc * o->hitSlot + o->hitCount[sc]] = loc;
+                    o->hitRC[sc * o->hitSlot + o->hitCount[sc]] = (uint8_t)el->dir;
                     o->hitCount[sc]++;
                 }
                 out->nLocationsScored++;
@@ -498,8 +499,8 @@ static void fill_hits(Oracle *o, int32_t *found, snapgpu_multi_hit_t *mh) {
     while (first < MAX_K && o->hitCount[first] == 0) first++;
     for (unsigned dist = first; dist < first + 4 && dist < MAX_K; dist++)
         for (unsigned i = 0; i < o->hitCount[dist]; i++) {
-            mh[*found].location = o->hitLoc[dist * o->maxHitsToGet + i];
-            mh[*found].direction = o->hitRC[dist * o->maxHitsToGet + i];
+            mh[*found].location = o->hitLoc[dist * o->hitSlot + i];
+            mh[*found].direction = o->hitRC[dist * o->hitSlot + i];
             mh[*found].score = (uint8_t)dist;
             mh[*found].reserved = 0;
             *found += 1;
@@ -708,8 +709,10 @@ static Oracle *oracle_new(const snapgpu_index_view_t *ix, const snapgpu_aligner_
     for (unsigned i = 0; i <= o->numWeightLists; i++) o->lists[i].wnext = o->lists[i].wprev = &o->lists[i];
     o->maxHitsToGet = maxHitsToGet;
     if (maxHitsToGet) {
-        o->hitLoc = (uint32_t *)calloc((size_t)MAX_K * maxHitsToGet, sizeof(uint32_t));
-        o->hitRC = (uint8_t *)calloc((size_t)MAX_K * maxHitsToGet, 1);
+        o->hitSlot = maxHitsToGet < 512 ? maxHitsToGet : 512;
+        const size_t cells = (size_t)MAX_K * o->hitSlot + (maxHitsToGet > 512 ? maxHitsToGet : 0);
+        o->hitLoc = (uint32_t *)calloc(cells, sizeof(uint32_t));
+        o->hitRC = (uint8_t *)calloc(cells, 1);
     }
     return o;
 }
@@ -1390,5 +1393,108 @@ int oracle_paired_batch(const snapgpu_index_view_t *ix, const snapgpu_paired_par
     for (int t = 0; t < nThreads; t++) pthread_create(&th[t], NULL, p_worker, &job);
     for (int t = 0; t < nThreads; t++) pthread_join(th[t], NULL);
     free(th);
+    return 0;
+}
+
+/* ================================================================ CharacterizeSeeds
+ * BaseAligner::CharacterizeSeeds (BaseAligner.cpp:206-508) as the partial aligner of
+ * PairedAligner.cpp:518-527 runs it: AlignRead's seed order, unwindowed lookups, every hit of a
+ * non-popular side recorded under (direction, hit - offset) with the seed offset `next`.  The
+ * two std::map<unsigned, std::set<unsigned>> are rebuilt as sorted (dir, location, offset)
+ * keys reduced to runs {location, *set.begin(), *set.rbegin(), set.size()} -- map order: map,
+ * then mapRC, locations ascending.  Test infrastructure (pinned to ref_harness_rna charseeds). */
+static int cmp_u64(const void *a, const void *b) {
+    const uint64_t x = *(const uint64_t *)a, y = *(const uint64_t *)b;
+    return x < y ? -1 : x > y;
+}
+
+int oracle_characterize_seeds(const snapgpu_index_view_t *ix, unsigned maxHits, unsigned maxK, unsigned numSeeds,
+                              int explore, const char *bases, const uint64_t *offsets, const uint32_t *lengths,
+                              uint64_t n, uint64_t *start, uint32_t *nForward, snapgpu_seed_run_t *runs, uint64_t cap) {
+    const unsigned seedLen = ix->seedLen;
+    uint64_t *keys = (uint64_t *)malloc(sizeof(uint64_t) * ((size_t)(numSeeds + 2) * maxHits + 64));
+    if (!keys) return -1;
+    uint64_t at = 0;
+    for (uint64_t r = 0; r < n; r++) {
+        start[r] = at;
+        nForward[r] = 0;
+        const unsigned len = lengths[r];
+        const char *b = bases + offsets[r];
+        if (len > 500 || len < seedLen) continue;   /* :272-282 (too long: the reference exits) */
+        char fwd[512 + 32];
+        unsigned nN = 0;
+        for (unsigned i = 0; i < len; i++) {
+            char c = b[i];
+            if (c >= 'a' && c <= 'z') c = (char)(c - 0x20);
+            fwd[i] = c;
+            nN += c == 'N';
+        }
+        if (nN > maxK) continue;   /* :303-306 */
+        uint8_t used[64];
+        memset(used, 0, sizeof(used));
+        unsigned nPossible = len - seedLen + 1, next = 0, wrapCount = 0, applied[2] = {0, 0};
+        size_t nk = 0;
+        while (applied[0] + applied[1] < numSeeds) {   /* :336 */
+            if (next >= nPossible) {
+                wrapCount++;
+                if (wrapCount >= seedLen) break;   /* :348-354 */
+                next = wrapped_next_seed(seedLen, wrapCount);
+            }
+            while (next < nPossible && (used[next / 8] & (1 << (next % 8)))) next++;
+            if (next >= nPossible) continue;
+            used[next / 8] |= (uint8_t)(1 << (next % 8));
+            uint64_t f = 0, rr = 0;
+            int valid = 1;
+            for (unsigned i = 0; i < seedLen; i++) {
+                int v = base_value(fwd[next + i]);
+                if (v > 3) { valid = 0; break; }
+                f |= (uint64_t)v << ((seedLen - i - 1) * 2);
+                rr |= (uint64_t)(v ^ 3) << (i * 2);
+            }
+            if (!valid) continue;   /* :375-377 */
+            unsigned nHits[2] = {0, 0}, nOvf = 0;
+            const uint32_t *hits[2] = {NULL, NULL};
+            uint32_t singleton[2], probes = 0;
+            int comp = (int64_t)f > (int64_t)rr;
+            uint64_t canon = comp ? rr : f;
+            const uint32_t *e = ht_lookup(ix, (uint32_t)(canon >> 32), (uint32_t)canon, &probes);
+            if (e) {
+                for (int side = 0; side < 2; side++) {
+                    uint32_t v = (side == 0) == !comp ? e[0] : e[1];
+                    if (side == 1 && f == rr) { nHits[1] = nHits[0]; hits[1] = hits[0]; break; }
+                    fill_side(ix, v, 0, INVALID_LOC, &singleton[side], &nHits[side], &hits[side], &nOvf);
+                }
+            }
+            for (int dir = 0; dir < 2; dir++) {   /* :393-497 */
+                if (nHits[dir] > maxHits && !explore) continue;
+                const unsigned offset = dir == 0 ? next : len - seedLen - next;
+                const unsigned lim = nHits[dir] < maxHits ? nHits[dir] : maxHits;
+                for (unsigned i = 0; i < lim; i++) {
+                    const uint32_t h = hits[dir][i];
+                    if (h < offset) continue;
+                    keys[nk++] = ((uint64_t)dir << 41) | ((uint64_t)(h - offset) << 9) | next;
+                }
+                applied[dir]++;
+            }
+            next += seedLen;
+        }
+        qsort(keys, nk, sizeof(uint64_t), cmp_u64);
+        for (size_t i = 0; i < nk;) {
+            size_t j = i;
+            while (j + 1 < nk && (keys[j + 1] >> 9) == (keys[i] >> 9)) j++;
+            if (at >= cap) { free(keys); return -2; }
+            snapgpu_seed_run_t *o = &runs[at++];
+            o->location = (uint32_t)(keys[i] >> 9);
+            o->minOffset = (uint16_t)(keys[i] & 511);
+            o->maxOffset = (uint16_t)(keys[j] & 511);
+            o->count = (uint16_t)(j - i + 1);
+            o->direction = (uint8_t)(keys[i] >> 41);
+            o->reserved = 0;
+            if (!o->direction) nForward[r]++;
+            i = j + 1;
+        }
+    }
+    start[n] = at;
+    free(keys);
     return 0;
 }

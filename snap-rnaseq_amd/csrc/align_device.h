@@ -122,7 +122,8 @@ struct KArgs {
     const snapgpu_search_t *search;     // per read, or nullptr (= unconstrained)
     uint32_t maxHitsToGet;              // 0: no multi-hit recording
     uint32_t hitStride;                 // u32 per block in hitScratch
-    uint32_t *hitScratch;               // per block: hitCount[MAX_K], then {loc, dir}[MAX_K][maxHitsToGet]
+    uint32_t hitSlot;                   // distance stride of the hit table: min(maxHitsToGet, 512)
+    uint32_t *hitScratch;               // per block: hitCount[MAX_K], then {loc, dir}[MAX_K * hitSlot (+ maxHitsToGet)]
     int32_t *multiFound;                // per read
     snapgpu_multi_hit_t *multiHits;     // [nReads][maxHitsToGet]
 };
@@ -513,6 +514,11 @@ __device__ __forceinline__ int next_piece_after(const KArgs &A, uint32_t loc) { 
 // ------------------------------------- multi-hit export / windowed lookups
 // BaseAligner.cpp:1255-1261: remember a scored hit (score != -1) while fewer than
 // maxHitsToGet are held at that distance.  The scratch is per block; lane 0 owns it.
+// The reference's table is hitLocations[MAX_K][512] / hitRCs[MAX_K][512] (BaseAligner.h:
+// 148-151) indexed [score][hitCount[score]] with hitCount < maxHitsToGet: for maxHitsToGet >
+// 512 (the RNA paired path asks for 1000, PairedAligner.cpp:584) entries 512.. of a distance
+// land in the next distances' rows.  The flat index score * hitSlot + count keeps exactly
+// that aliasing (hitSlot = 512 then; = maxHitsToGet below, where nothing aliases).
 template <bool EXT>
 __device__ __forceinline__ void record_hit(const KArgs &A, uint32_t loc, uint32_t dir, uint32_t sc) {
     if (!EXT || A.maxHitsToGet == 0 || sc >= (uint32_t)MAX_K) return;
@@ -520,7 +526,7 @@ __device__ __forceinline__ void record_hit(const KArgs &A, uint32_t loc, uint32_
         uint32_t *cnt = A.hitScratch + (uint64_t)blockIdx.x * A.hitStride;
         const uint32_t c = cnt[sc];
         if (c < A.maxHitsToGet) {
-            uint32_t *h = cnt + MAX_K + 2 * (sc * A.maxHitsToGet + c);
+            uint32_t *h = cnt + MAX_K + 2 * (sc * A.hitSlot + c);
             h[0] = loc;
             h[1] = dir;
             cnt[sc] = c + 1;
@@ -541,7 +547,7 @@ __device__ __forceinline__ void fill_hits(const KArgs &A, uint32_t r, bool fill)
             const uint32_t c = cnt[d];
             bool full = false;
             for (uint32_t i = 0; i < c; i++) {
-                const uint32_t *h = cnt + MAX_K + 2 * (d * A.maxHitsToGet + i);
+                const uint32_t *h = cnt + MAX_K + 2 * (d * A.hitSlot + i);
                 snapgpu_multi_hit_t m;
                 m.location = h[0];
                 m.direction = (uint8_t)h[1];

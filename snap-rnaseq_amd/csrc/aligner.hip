@@ -1348,6 +1348,13 @@ void snapgpu_device_reads_free(snapgpu_device_reads_t *d) {
     delete d;
 }
 
+// u32 words per block of the multi-hit scratch: hitCount[MAX_K], then {loc, dir} pairs at flat
+// index score * hitSlot + count (record_hit), count < maxHitsToGet
+static inline uint64_t multiHitStride(uint32_t maxHitsToGet) {
+    const uint64_t slot = maxHitsToGet < 512 ? maxHitsToGet : 512;
+    return (uint64_t)MAX_K + 2 * ((uint64_t)MAX_K * slot + (maxHitsToGet > 512 ? maxHitsToGet : 0));
+}
+
 // Extension arguments of snapgpu_align_batch_ex (device pointers; all null for the plain path)
 struct AlignExt {
     const snapgpu_search_t *search = nullptr;
@@ -1392,7 +1399,9 @@ static int launch_passes(snapgpu_aligner_t *a, int li, const PassIO &io, const A
     A.nReads = (uint32_t)io.n; A.out = io.out;
     A.counter = L.counter; A.arena = L.arena; A.arenaElems = a->arenaElems;
     A.deferList = io.defer; A.deferCount = L.counter + 2; A.readList = nullptr;
-    A.search = x.search; A.maxHitsToGet = x.maxHitsToGet; A.hitStride = MAX_K * (1 + 2 * x.maxHitsToGet);
+    A.search = x.search; A.maxHitsToGet = x.maxHitsToGet;
+    A.hitSlot = x.maxHitsToGet < 512 ? x.maxHitsToGet : 512;
+    A.hitStride = multiHitStride(x.maxHitsToGet);
     A.hitScratch = x.hitScratch; A.multiFound = x.multiFound; A.multiHits = x.multiHits;
     int grid = a->grid;
     if ((uint64_t)grid > io.n) grid = (int)io.n;
@@ -1787,8 +1796,13 @@ int snapgpu_align_batch_ex(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, c
                            snapgpu_multi_hit_t *multiHits) {
     if (!a || !reads || !out) return SNAPGPU_EINVAL;
     if (maxHitsToGet > SNAPGPU_MAX_MULTI_HITS_TO_GET || (maxHitsToGet && (!multiHitsFound || !multiHits))) {
-        snapgpu::setError("align_batch_ex: maxHitsToGet must be <= 512 and come with multiHitsFound/multiHits");
+        snapgpu::setError("align_batch_ex: maxHitsToGet must be <= 1024 and come with multiHitsFound/multiHits");
         return SNAPGPU_EINVAL;
+    }
+    // above 512 the reference's rows alias (record_hit); they must stay inside hitLocations
+    if (maxHitsToGet > 512 && (a->p.maxK + a->p.extraSearchDepth) * 512u + maxHitsToGet > (uint32_t)MAX_K * 512u) {
+        snapgpu::setError("align_batch_ex: maxHitsToGet > 512 needs (maxK + extraSearchDepth) * 512 + maxHitsToGet <= 15872");
+        return SNAPGPU_EUNSUPPORTED;
     }
     if (search)
         for (uint64_t i = 0; i < reads->n; i++)
@@ -1815,7 +1829,7 @@ int snapgpu_align_batch_ex(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, c
     }
     if (e == hipSuccess && maxHitsToGet) {
         const uint64_t blocks = (uint64_t)(a->grid > a->grid512 ? a->grid : a->grid512);
-        const uint64_t stride = (uint64_t)MAX_K * (1 + 2 * maxHitsToGet);
+        const uint64_t stride = multiHitStride(maxHitsToGet);
         if ((e = hipMalloc(&dScratch, blocks * stride * 4)) == hipSuccess &&
             (e = hipMalloc(&dFound, n * sizeof(int32_t))) == hipSuccess)
             e = hipMalloc(&dHits, n * maxHitsToGet * sizeof(snapgpu_multi_hit_t));

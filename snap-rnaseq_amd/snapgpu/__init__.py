@@ -527,6 +527,44 @@ class PairedAligner:
             self._h = None
 
 
+SEED_RUN_DTYPE = np.dtype([("location", "<u4"), ("minOffset", "<u2"), ("maxOffset", "<u2"), ("count", "<u2"),
+                           ("direction", "u1"), ("reserved", "u1")])
+
+
+def charseeds_params(**kw):
+    """snapgpu_charseeds_params_t: the partial aligner of PairedAligner.cpp:518-527 by default."""
+    p = _ffi.CharSeedsParams()
+    lib().snapgpu_charseeds_params_default(C.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def characterize_seeds(aligner, reads, read_list=None, **kw):
+    """BaseAligner::CharacterizeSeeds (BaseAligner.cpp:206-508) on the GPU over `reads` (or the
+    reads at indices read_list), on the index of `aligner`.  -> (start uint64[n+1],
+    nForward uint32[n], flags uint32[n], runs SEED_RUN_DTYPE[...]): read i's map entries are
+    runs[start[i]:start[i+1]], the first nForward[i] of them from `map`, the rest from `mapRC`."""
+    p = charseeds_params(**kw)
+    lst = None if read_list is None else np.ascontiguousarray(read_list, dtype=np.uint64)
+    h = lib().snapgpu_characterize_seeds(aligner._h, reads._p, None if lst is None else lst.ctypes.data,
+                                         0 if lst is None else len(lst), C.byref(p))
+    if not h:
+        raise SnapGpuError(f"characterize_seeds: {last_error()}")
+    try:
+        r = h.contents
+        n = r.n
+        start = np.ctypeslib.as_array(r.start, shape=(n + 1,)).copy()
+        nfwd = np.ctypeslib.as_array(r.nForward, shape=(max(1, n),))[:n].copy()
+        flags = np.ctypeslib.as_array(r.flags, shape=(max(1, n),))[:n].copy()
+        runs = np.zeros(r.nRuns, dtype=SEED_RUN_DTYPE)
+        if r.nRuns:
+            C.memmove(runs.ctypes.data, r.runs, r.nRuns * SEED_RUN_DTYPE.itemsize)
+    finally:
+        lib().snapgpu_seed_runs_free(h)
+    return start, nfwd, flags, runs
+
+
 class DeviceReads:
     def __init__(self, aligner, reads):
         self.aligner = aligner

@@ -180,6 +180,17 @@ class SingleStats(C.Structure):
                [(f, C.c_double) for f in ("alignMs", "cigarMs", "filterMs", "writeMs", "wallMs")]
 
 
+class SeedRuns(C.Structure):
+    """snapgpu_seed_runs_t (BaseAligner::CharacterizeSeeds maps as run records)."""
+    _fields_ = [("n", C.c_uint64), ("start", C.POINTER(C.c_uint64)), ("nForward", C.POINTER(C.c_uint32)),
+                ("flags", C.POINTER(C.c_uint32)), ("runs", C.c_void_p), ("nRuns", C.c_uint64)]
+
+
+class CharSeedsParams(C.Structure):
+    _fields_ = [("maxHits", C.c_uint32), ("maxK", C.c_uint32), ("numSeeds", C.c_uint32), ("maxReadSize", C.c_uint32),
+                ("explorePopularSeeds", C.c_uint32), ("reserved", C.c_uint32)]
+
+
 class AlignerStats(C.Structure):
     _fields_ = [
         ("nHashTableLookups", C.c_int64),
@@ -295,6 +306,10 @@ _PROTOS += [
     ("snapgpu_paired_align_batch", C.c_int, [C.c_void_p, C.POINTER(Reads), C.POINTER(Reads), C.c_void_p]),
     ("snapgpu_paired_intersect_batch", C.c_int, [C.c_void_p, C.POINTER(Reads), C.POINTER(Reads), C.c_void_p]),
     ("snapgpu_paired_aligner_single", C.c_void_p, [C.c_void_p]),
+    ("snapgpu_charseeds_params_default", None, [C.POINTER(CharSeedsParams)]),
+    ("snapgpu_characterize_seeds", C.POINTER(SeedRuns), [C.c_void_p, C.POINTER(Reads), C.c_void_p, C.c_uint64,
+                                                         C.POINTER(CharSeedsParams)]),
+    ("snapgpu_seed_runs_free", None, [C.POINTER(SeedRuns)]),
 ]
 
 CIGAR_MAX_OPS = 64   # SNAPGPU_CIGAR_MAX_OPS

@@ -435,8 +435,88 @@ def paired_fixtures(work):
             f.write(run([HARNESS, "paired", idx, fq0, fq1] + args))
 
 
+HARNESS_RNA = os.path.join(REF_BIN, "ref_harness_rna")
+
+
+def multihit_alias_fixtures(work):
+    """maxHitsToGet 1000 (the RNA paired path's transcriptome call, PairedAligner.cpp:584) on a
+    genome holding one 150-base element 700 times exactly, 700 times with one substitution and
+    400 times with two: more than 512 hits at one distance, so the reference's per-distance rows
+    (hitLocations[MAX_K][512], BaseAligner.h:148-151) overflow into each other.  Paired CLI
+    aligner parameters (maxHits 16000, maxK 15, 8 seeds, extra 2), no search window."""
+    rng = random.Random(77)
+    elem = "".join(rng.choice("ACGT") for _ in range(150))
+    sub = lambda s, i: s[:i] + {"A": "C", "C": "G", "G": "T", "T": "A"}[s[i]] + s[i + 1:]
+    copies = [elem] * 700 + [sub(elem, 75)] * 700 + [sub(sub(elem, 40), 110)] * 400
+    rng.shuffle(copies)
+    seqs = []
+    for c in range(3):
+        parts = ["".join(rng.choice("ACGT") for _ in range(5000))]
+        for k in copies[c * 600:(c + 1) * 600]:
+            parts.append(k if rng.random() < 0.5 else k[::-1].translate(str.maketrans("ACGT", "TGCA")))
+            parts.append("".join(rng.choice("ACGT") for _ in range(rng.randrange(20, 60))))
+        seqs.append("".join(parts))
+    fa = os.path.join(HERE, "repeat.fa")
+    with open(fa, "w") as f:
+        for c, sq in enumerate(seqs):
+            f.write(f">rep{c}\n")
+            f.writelines(sq[i:i + 70] + "\n" for i in range(0, len(sq), 70))
+    rc = lambda x: x[::-1].translate(str.maketrans("ACGT", "TGCA"))
+    reads = []
+    for i in range(24):
+        a = rng.randrange(0, 50)
+        r = elem[a:a + 100]
+        if i % 3 == 1:
+            r = sub(r, 60)
+        if i % 2:
+            r = rc(r)
+        reads.append((r, "I" * len(r)))
+    for i in range(8):   # anchored outside the element as well
+        c = rng.randrange(3)
+        p0 = rng.randrange(0, 4800)
+        r = seqs[c][p0:p0 + 100]
+        reads.append((r, "I" * len(r)))
+    fq = os.path.join(HERE, "repeat_reads.fq")
+    write_fastq(fq, reads)
+    sp = os.path.join(work, "nosearch.tsv")
+    with open(sp, "w") as f:
+        f.writelines("0\t0\t0\n" for _ in reads)
+    idxdir = os.path.join(work, "repeat_idx")
+    run([SNAP, "index", fa, idxdir, "-O1000"])   # a repeat this dense needs the larger overflow space
+    out = run([HARNESS, "alignx", idxdir, fq, sp, "1000", "16000", "15", "8", "2"])
+    with open(os.path.join(HERE, "expected_repeat_mh1000.tsv"), "w") as f:
+        f.write(ref_tsvx_to_canonical(out))
+
+
+def charseeds_fixtures(work):
+    """`ref_harness_rna charseeds`: BaseAligner::CharacterizeSeeds (BaseAligner.cpp:206-508) of
+    the partial aligner (PairedAligner.cpp:518-527: maxHits 300, maxK 15, 12 seeds) over every
+    read of paired_1.fq / paired_2.fq and single_reads.fq, on the reference's index of small.fa,
+    plus a tight variant (maxHits 20, 4 seeds) that makes popular seeds common."""
+    import gzip
+    fa = os.path.join(HERE, "small.fa")
+    idx = os.path.join(work, "csidx")
+    ref_index(fa, idx)
+    for tag, args in (("", []), ("_tight", ["20", "15", "4", "2"])):
+        out = []
+        for fq in ("paired_1.fq", "paired_2.fq", "single_reads.fq"):
+            out.append(run([HARNESS_RNA, "charseeds", idx, os.path.join(HERE, fq)] + args))
+        with open(os.path.join(HERE, f"expected_charseeds{tag}.tsv.gz"), "wb") as f:
+            f.write(gzip.compress("".join(out).encode(), compresslevel=9, mtime=0))
+
+
 def main():
     work = tempfile.mkdtemp(prefix="golden_")
+    if "--only-mh1000" in sys.argv:
+        multihit_alias_fixtures(work)
+        shutil.rmtree(work, ignore_errors=True)
+        print("maxHitsToGet 1000 fixtures written to", HERE)
+        return
+    if "--only-charseeds" in sys.argv:
+        charseeds_fixtures(work)
+        shutil.rmtree(work, ignore_errors=True)
+        print("CharacterizeSeeds fixtures written to", HERE)
+        return
     if "--only-paired" in sys.argv:
         paired_fixtures(work)
         shutil.rmtree(work, ignore_errors=True)

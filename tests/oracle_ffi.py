@@ -38,6 +38,10 @@ def oracle_lib():
         o.oracle_paired_batch.argtypes = [C.POINTER(F.IndexView), C.POINTER(F.PairedParams)] + [C.c_void_p] * 8 + \
             [C.c_uint64, C.c_int, C.c_void_p, C.c_int]
         o.oracle_paired_batch.restype = C.c_int
+        o.oracle_characterize_seeds.argtypes = [C.POINTER(F.IndexView), C.c_uint, C.c_uint, C.c_uint, C.c_int,
+                                                C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
+                                                C.c_void_p, C.c_void_p, C.c_uint64]
+        o.oracle_characterize_seeds.restype = C.c_int
         o.oracle_compute_mapq.argtypes = [C.c_double, C.c_double, C.c_int, C.c_int]
         o.oracle_compute_mapq.restype = C.c_int
         _orc = o
@@ -73,6 +77,50 @@ def oracle_paired(index, reads0, reads1, params, chimeric=True, n_threads=8):
                                           int(chimeric), out.ctypes.data, n_threads)
     assert rc == 0
     return out[:n]
+
+
+def oracle_charseeds(index, reads, maxHits=300, maxK=15, numSeeds=12, explore=0):
+    """CPU restatement of BaseAligner::CharacterizeSeeds -> (start, nForward, runs) as
+    snapgpu.characterize_seeds returns them (flags aside)."""
+    import snapgpu
+    v = index.view()
+    n = reads.n
+    r = reads._p.contents
+    cap = max(1, n) * (numSeeds + 1) * maxHits
+    start = np.zeros(n + 1, dtype=np.uint64)
+    nfwd = np.zeros(max(1, n), dtype=np.uint32)
+    runs = np.zeros(cap, dtype=snapgpu.SEED_RUN_DTYPE)
+    rc = oracle_lib().oracle_characterize_seeds(C.byref(v), maxHits, maxK, numSeeds, explore, r.bases,
+                                                C.cast(r.offsets, C.c_void_p), C.cast(r.lengths, C.c_void_p), n,
+                                                start.ctypes.data, nfwd.ctypes.data, runs.ctypes.data, cap)
+    assert rc == 0
+    return start, nfwd[:n], runs[:int(start[n])]
+
+
+def parse_charseeds(text):
+    """ref_harness_rna charseeds lines -> list per read of (nF, nRC, [(dir, loc, min, max, count), ...])."""
+    out = []
+    for line in text.splitlines():
+        f = line.split("\t")
+        runs = []
+        for d, col in ((0, f[3]), (1, f[4])):
+            body = col.split(":", 1)[1] if ":" in col else ""
+            for item in filter(None, body.split(",")):
+                loc, mn, mx, cnt = (int(x) for x in item.split(":"))
+                runs.append((d, loc, mn, mx, cnt))
+        out.append((int(f[1]), int(f[2]), runs))
+    return out
+
+
+def runs_as_lists(start, nfwd, runs):
+    """(start, nForward, runs) -> the parse_charseeds form, for comparisons."""
+    out = []
+    for i in range(len(start) - 1):
+        rs = runs[int(start[i]):int(start[i + 1])]
+        lst = [(int(x["direction"]), int(x["location"]), int(x["minOffset"]), int(x["maxOffset"]), int(x["count"]))
+               for x in rs]
+        out.append((int(nfwd[i]), len(lst) - int(nfwd[i]), lst))
+    return out
 
 
 PAIR_FIELDS = ("status", "location", "direction", "score", "mapq")

@@ -122,9 +122,42 @@ def test_gpu_multihit_c1_matches_oracle():
 def test_gpu_ex_rejects_bad_arguments(small_index, small_reads):
     al = snapgpu.BaseAligner(small_index)
     with pytest.raises(snapgpu.SnapGpuError):
-        al.AlignReadsEx(small_reads, None, 513)
+        al.AlignReadsEx(small_reads, None, 1025)
     s = np.zeros((small_reads.n, 3), dtype=np.uint64)
     s[:, 0] = 10
     s[:, 2] = 2
     with pytest.raises(snapgpu.SnapGpuError):
         al.AlignReadsEx(small_reads, s, 0)
+
+
+# maxHitsToGet 1000 (PairedAligner.cpp:584) with > 512 hits per distance: the reference's rows
+# hitLocations[MAX_K][512] alias (BaseAligner.h:148-151); fixture from ref_harness alignx on
+# tests/golden/repeat.fa (make_golden.py --only-mh1000), paired CLI aligner parameters
+REPEAT_KW = dict(maxHitsToConsider=16000, maxK=15, maxSeedsToUse=8, extraSearchDepth=2)
+
+
+@pytest.fixture(scope="module")
+def repeat_index():
+    return snapgpu.GenomeIndex.build(snapgpu.Genome.from_fasta(os.path.join(G, "repeat.fa"), 500), 20, 4)
+
+
+def test_oracle_mh1000_aliasing_matches_reference(repeat_index):
+    reads = snapgpu.Reads.from_fastq(os.path.join(G, "repeat_reads.fq"))
+    p = snapgpu.default_params()
+    for k, v in REPEAT_KW.items():
+        setattr(p, k, v)
+    res, found, hits = oracle_align_ex(repeat_index, reads, p, None, 1000, n_threads=4)
+    got = canonical_tsv_ex(res, found, hits)
+    want = open(os.path.join(G, "expected_repeat_mh1000.tsv")).read()
+    assert got == want, _first_diff(got, want)
+    assert (found == 1000).sum() >= 20
+
+
+@pytest.mark.gpu
+def test_gpu_mh1000_aliasing_matches_reference(repeat_index):
+    reads = snapgpu.Reads.from_fastq(os.path.join(G, "repeat_reads.fq"))
+    al = snapgpu.BaseAligner(repeat_index, **REPEAT_KW)
+    res, found, hits = al.AlignReadsEx(reads, None, 1000)
+    got = canonical_tsv_ex(res, found, hits)
+    want = open(os.path.join(G, "expected_repeat_mh1000.tsv")).read()
+    assert got == want, _first_diff(got, want)
