@@ -601,6 +601,69 @@ snapgpu_seed_runs_t *snapgpu_characterize_seeds(snapgpu_aligner_t *a, const snap
                                                 const snapgpu_charseeds_params_t *p);
 void snapgpu_seed_runs_free(snapgpu_seed_runs_t *runs);
 
+/* --------------------------------------- RNA paired-end product path
+ * PairedAlignerContext::runIterationThread (SNAPLib/PairedAligner.cpp:405-689) batched on the
+ * GPU -- what `snap-rna paired <genome> <transcriptome> <gtf> r1.fq r2.fq` computes per pair:
+ * Read::clip, the length / N / quality pre-filter (:555-575), transcriptome AlignRead of each
+ * read with 1000-hit export (:584-614), the genome ChimericPairedEndAligner (:625),
+ * AlignmentFilter::AddAlignment / Filter (AlignmentFilter.cpp:140-214, 302-739) with
+ * FindPartialMatches' CharacterizeSeeds on the GPU (:957-1037), forceSpacing and the MAPQ
+ * halving (:648-663), the SAM pair records (ReadWriter.cpp:133-217, SAM.cpp:804-1153: GPU
+ * CIGARs, insertSpliceJunctions for transcriptome records) and the GTF read counts
+ * (GTFReader::IncrementReadCount, GTFReader.cpp:1409-1611; snapgpu_gtf_write_counts writes
+ * them).  Not built: the contamination database (-x) and GTFReader::AnalyzeReadIntervals
+ * (the interval report UnalignedRead and the *chromosomalPair calls feed). */
+typedef struct snapgpu_rna_paired_options {
+    int32_t  clipping;               /* ReadClippingType, default 3 (AlignerOptions.cpp:48) */
+    uint32_t confDiff;               /* -c, default 2 */
+    uint32_t maxDist;                /* -d, default 15 (filter cut-off and the partial aligner's maxK) */
+    uint32_t minSpacing, maxSpacing; /* -s, default 50 1000 */
+    uint32_t forceSpacing;           /* -fs */
+    float    minPercentAbovePhred;   /* -fp, default 90 */
+    uint32_t minPhred;               /* -fm, default 20 */
+    uint32_t phredOffset;            /* -fo, default 33 */
+    uint32_t useM;                   /* -M */
+    uint32_t maxHitsToGet;           /* transcriptome multi-hits per read, 1000 (PairedAligner.cpp:584) */
+    uint32_t ignoreMismatchedIDs;    /* -I (else mismatched ids fail the call: the reference exits) */
+    const char *readGroup;           /* default "FASTQ" */
+    const char *commandLine;         /* @PG CL: */
+    const char *version;             /* @PG VN: */
+} snapgpu_rna_paired_options_t;
+void snapgpu_rna_paired_options_default(snapgpu_rna_paired_options_t *o);
+
+typedef struct snapgpu_rna_pair_result {   /* PairedAlignmentResult after the filter (PairedEndAligner.h:31-55) */
+    uint32_t location[2];      /* 0xffffffff when NotFound (the SAM writer's view) */
+    uint32_t tlocation[2];     /* transcriptome location of a transcriptome record */
+    int32_t  score[2];
+    int32_t  mapq[2];
+    uint8_t  status[2];
+    uint8_t  direction[2];
+    uint8_t  isTranscriptome[2];
+    uint8_t  fromAlignTogether, alignedAsPair;
+    uint8_t  useful;           /* passed the pre-filter */
+    uint8_t  reserved[7];
+} snapgpu_rna_pair_result_t;   /* 48 bytes */
+
+typedef struct snapgpu_rna_paired_stats {
+    uint64_t totalPairs, usefulPairs, singleHits, multiHits, notFound, transcriptomeRecords;
+    uint64_t partialPairs, partialMatches, seedRuns;   /* FindPartialMatches scans, hits, CharacterizeSeeds runs */
+    double alignMs, filterMs, seedMs, cigarMs, writeMs, wallMs;
+} snapgpu_rna_paired_stats_t;
+
+/* pairedAligner: the genome aligner (snapgpu_paired_aligner_create with the paired CLI defaults);
+ * transcriptomeAligner: a BaseAligner over the transcriptome index (maxHits 16000, maxK 15,
+ * 8 seeds); reads0 / reads1 FASTQ batches with ids, clipped here.  samPath (or NULL) receives the
+ * header and two lines per pair in input order; out (or NULL) one record per pair; the gtf's
+ * read counters are advanced. */
+int snapgpu_rna_paired_align(snapgpu_paired_aligner_t *pairedAligner, snapgpu_aligner_t *transcriptomeAligner,
+                             snapgpu_gtf_t *gtf, snapgpu_reads_t *reads0, snapgpu_reads_t *reads1,
+                             const snapgpu_rna_paired_options_t *opt, const char *samPath,
+                             snapgpu_rna_pair_result_t *out, snapgpu_rna_paired_stats_t *stats);
+/* GTFReader::WriteReadCounts (GTFReader.cpp:1710-1772): <prefix>.{transcript,gene,junction}_{id,name}
+ * .counts.txt from the gtf's read counters; snapgpu_gtf_reset_counts zeroes them. */
+int snapgpu_gtf_write_counts(const snapgpu_gtf_t *gtf, const char *prefix);
+int snapgpu_gtf_reset_counts(snapgpu_gtf_t *gtf);
+
 /* MAPQ (mapq.h:32-65) as the host computes it; exported for tests. */
 int snapgpu_compute_mapq(double pAll, double pBest, int score, int popularSeedsSkipped);
 

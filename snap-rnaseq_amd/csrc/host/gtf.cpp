@@ -14,6 +14,7 @@
 #include "internal.h"
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -28,6 +29,7 @@ struct GtfFeature {
     std::string key, chr, feature, geneId, transcriptId;
     uint32_t start = 0, end = 0;
     int type = 0;   // 1 exon, 2 intron (GTFReader.h:49)
+    uint32_t readCount = 0;   // GTFFeature::read_count (junction counts of introns)
     std::map<std::string, std::string> attributes;
     uint32_t length() const { return end - start + 1; }   // GTFFeature::Length (unsigned)
     bool attr(const std::string &k, std::string &v) const {
@@ -44,16 +46,53 @@ struct GtfFeature {
 };
 
 struct GtfTranscript {
-    std::string chr, geneId, transcriptId;
+    std::string chr, geneId, transcriptId, transcriptName;
     uint32_t start = 0, end = 0;
+    float readCount = 0.f;   // GTFTranscript::read_count (float: 1/n per fragment)
     std::vector<const GtfFeature *> features;   // exon lines, in file order
     std::vector<const GtfFeature *> exons;      // after Process: exons and introns by start
+};
+
+struct GtfGene {                                         // GTFGene (GTFReader.h:276-312)
+    std::string chr, geneId, geneName;
+    uint32_t start = 0, end = 0;
+    uint32_t readCount = 0;
+    std::set<std::string> transcriptIds;
+    std::map<std::string, GtfFeature *> introns;         // GTFGene::features: the introns of its transcripts
+};
+
+// Static interval index over every feature (exons and introns), the reference's feature_tree
+// (IntervalTree.h): sorted by start, implicit balanced tree with the subtree's largest end kept
+// at each node's middle index.  Overlap = closed intervals, as IntervalTree::findOverlapping.
+struct FeatureIndex {
+    std::vector<const GtfFeature *> iv;
+    std::vector<uint32_t> maxEnd;
+    uint32_t build(size_t lo, size_t hi) {
+        if (lo >= hi) return 0;
+        const size_t mid = (lo + hi) / 2;
+        uint32_t m = iv[mid]->end;
+        m = std::max(m, build(lo, mid));
+        m = std::max(m, build(mid + 1, hi));
+        maxEnd[mid] = m;
+        return m;
+    }
+    void query(size_t lo, size_t hi, uint32_t qs, uint32_t qe, std::vector<const GtfFeature *> &out) const {
+        while (lo < hi) {
+            const size_t mid = (lo + hi) / 2;
+            if (maxEnd[mid] < qs) return;
+            query(lo, mid, qs, qe, out);
+            if (iv[mid]->start > qe) return;
+            if (iv[mid]->end >= qs) out.push_back(iv[mid]);
+            lo = mid + 1;
+        }
+    }
 };
 
 struct Gtf {
     std::map<std::string, GtfFeature> features;          // feature_map (keys stable: pointers stay valid)
     std::map<std::string, GtfTranscript> transcripts;    // transcript_map
-    std::map<std::string, std::set<std::string>> genes;  // gene_id -> transcript ids
+    std::map<std::string, GtfGene> genes;                // gene_map
+    FeatureIndex featureIndex;
 };
 
 // GTFFeature::GTFFeature(string line) (GTFReader.cpp:646-713): strtok on '\'' and '\t' for the
@@ -125,6 +164,8 @@ snapgpu_gtf_t *snapgpu_gtf_load(const char *path) {
                 if (tp == g->transcripts.end()) {
                     GtfTranscript t;
                     t.chr = f.chr; t.geneId = f.geneId; t.transcriptId = f.transcriptId;
+                    std::string tn;
+                    t.transcriptName = f.attr("transcript_name", tn) ? tn : f.transcriptId;   // TranscriptName :728-736
                     t.start = f.start; t.end = f.end;
                     t.features.push_back(fe);
                     g->transcripts.insert({f.transcriptId, t});
@@ -133,14 +174,25 @@ snapgpu_gtf_t *snapgpu_gtf_load(const char *path) {
                     tp->second.start = std::min(tp->second.start, f.start);   // UpdateBoundaries
                     tp->second.end = std::max(tp->second.end, f.end);
                 }
-                g->genes[f.geneId].insert(f.transcriptId);
+                auto gp = g->genes.find(f.geneId);
+                if (gp == g->genes.end()) {   // GTFGene(chr, gene_id, start, end, GeneName) of the first exon
+                    GtfGene ge;
+                    ge.chr = f.chr; ge.geneId = f.geneId; ge.geneName = f.geneName();
+                    ge.start = f.start; ge.end = f.end;
+                    ge.transcriptIds.insert(f.transcriptId);
+                    g->genes.insert({f.geneId, ge});
+                } else {
+                    gp->second.transcriptIds.insert(f.transcriptId);
+                    gp->second.start = std::min(gp->second.start, f.start);   // GTFGene::UpdateBoundaries
+                    gp->second.end = std::max(gp->second.end, f.end);
+                }
             }
         }
         std::getline(in, line, '\n');
     }
     // genes in gene_id order, each gene's transcripts in id order: GTFTranscript::Process
     for (auto &gene : g->genes)
-        for (auto &tid : gene.second) {
+        for (auto &tid : gene.second.transcriptIds) {
             GtfTranscript &t = g->transcripts[tid];
             std::sort(t.features.begin(), t.features.end(),
                       [](const GtfFeature *a, const GtfFeature *b) { return a->start < b->start; });
@@ -155,12 +207,19 @@ snapgpu_gtf_t *snapgpu_gtf_load(const char *path) {
                     intron.key = intron.chr + u32s(intron.start) + u32s(intron.end);
                     intron.type = 2;
                     auto ip = g->features.insert({intron.key, intron}).first;   // shared when present
+                    gene.second.introns.insert({intron.key, &ip->second});
                     t.exons.push_back(&ip->second);
                 }
                 t.exons.push_back(cur);
                 prev = cur;
             }
         }
+    // feature_tree over every feature, in feature_map order before the sort (Load :1275-1280)
+    FeatureIndex &fi = g->featureIndex;
+    for (auto &f : g->features) fi.iv.push_back(&f.second);
+    std::stable_sort(fi.iv.begin(), fi.iv.end(), [](const GtfFeature *a, const GtfFeature *b) { return a->start < b->start; });
+    fi.maxEnd.assign(fi.iv.size(), 0);
+    fi.build(0, fi.iv.size());
     return g;
 }
 
@@ -311,6 +370,152 @@ int snapgpu_gtf_splice_cigar(const snapgpu_gtf_t *g, const char *transcriptId, u
     *used = s.size();
     if (!out || s.size() + 1 > cap) { setError("splice_cigar: buffer too small"); return SNAPGPU_EINVAL; }
     memcpy(out, s.c_str(), s.size() + 1);
+    return SNAPGPU_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------ read counts
+// GTFReader's per-run counters (GTFFeature / GTFGene / GTFTranscript::IncrementReadCount) and
+// the six files GTFReader::WriteReadCounts (GTFReader.cpp:1710-1772) writes after a run.  The
+// product paths collect one count event per fragment and apply them in input order: transcript
+// counts are float sums of 1/n, whose rounding depends on that order.
+namespace snapgpu {
+
+const GtfGene *gtfGene(const snapgpu_gtf_t *g, const std::string &geneId) {
+    auto it = g->genes.find(geneId);
+    return it == g->genes.end() ? nullptr : &it->second;
+}
+
+const std::string &gtfTranscriptGene(const GtfTranscript *t) { return t->geneId; }
+
+// GTFGene::CheckBoundary (GTFReader.cpp:890-902), buffer default 1000 (GTFReader.h:290);
+// unsigned arithmetic kept: start - buffer + 1 wraps for genes starting before 1000
+bool gtfGeneCheckBoundary(const GtfGene *ge, const std::string &chr, uint32_t pos, uint32_t buffer) {
+    if (ge->chr != chr) return false;
+    const uint32_t lo = std::max(ge->start - buffer + 1, (uint32_t)1);
+    return pos >= lo && pos <= ge->end + buffer;
+}
+
+// GTFReader::IncrementReadCount(transcript, ...) single-read form (:1388-1407): the gene only
+void gtfCountSingle(snapgpu_gtf_t *g, const std::string &transcriptId) {
+    auto t = g->transcripts.find(transcriptId);
+    if (t == g->transcripts.end()) return;
+    auto ge = g->genes.find(t->second.geneId);
+    if (ge != g->genes.end()) ge->second.readCount++;
+}
+
+// the transcripts whose features cover every segment of one read (:1417-1486)
+static bool readTranscripts(snapgpu_gtf_t *g, const std::string &tid, uint32_t tstart, uint32_t start, uint32_t length,
+                            std::set<std::string> &ids) {
+    auto tp = g->transcripts.find(tid);
+    if (tp == g->transcripts.end()) return false;   // GetTranscript exits
+    const GtfTranscript &t = tp->second;
+    std::vector<std::pair<uint32_t, const GtfFeature *>> js;
+    junctions(&t, tstart, length, js);
+    std::vector<const GtfFeature *> hits;
+    auto segment = [&](uint32_t a, uint32_t b) {
+        hits.clear();
+        g->featureIndex.query(0, g->featureIndex.iv.size(), a, b, hits);
+        if (ids.empty()) {
+            for (const GtfFeature *f : hits)
+                if (f->chr == t.chr) ids.insert(f->transcriptId);
+        } else {
+            std::set<std::string> keep;
+            for (const GtfFeature *f : hits)
+                if (f->chr == t.chr && ids.count(f->transcriptId)) keep.insert(f->transcriptId);
+            ids.swap(keep);
+        }
+    };
+    for (auto &j : js) {
+        const_cast<GtfFeature *>(j.second)->readCount++;   // the junction's splice count
+        const uint32_t len = j.first - tstart;
+        segment(start, start + len - 1);
+        tstart += len;
+        start += len + j.second->length();
+        length -= len;
+    }
+    segment(start, start + length - 1);
+    return true;
+}
+
+// GTFReader::IncrementReadCount(pair form) (:1409-1611)
+bool gtfCountPair(snapgpu_gtf_t *g, const std::string &tid0, uint32_t tstart0, uint32_t start0, uint32_t len0,
+                  const std::string &tid1, uint32_t tstart1, uint32_t start1, uint32_t len1) {
+    std::set<std::string> ids0, ids1;
+    if (tid0.empty()) return true;
+    if (!readTranscripts(g, tid0, tstart0, start0, len0, ids0)) return false;
+    if (tid1.empty()) return true;
+    if (!readTranscripts(g, tid1, tstart1, start1, len1, ids1)) return false;
+    std::set<std::string> fin;
+    for (auto &x : ids0)
+        if (ids1.count(x)) fin.insert(x);
+    if (fin.empty()) return true;
+    std::string geneId;
+    for (auto &x : fin) {
+        auto tp = g->transcripts.find(x);
+        if (tp == g->transcripts.end()) return false;
+        geneId = tp->second.geneId;
+        tp->second.readCount += 1.f / (float)fin.size();
+    }
+    auto ge = g->genes.find(geneId);
+    if (ge == g->genes.end()) return false;
+    ge->second.readCount++;
+    return true;
+}
+
+}  // namespace snapgpu
+
+extern "C" {
+
+int snapgpu_gtf_reset_counts(snapgpu_gtf_t *g) {
+    if (!g) return SNAPGPU_EINVAL;
+    for (auto &f : g->features) f.second.readCount = 0;
+    for (auto &t : g->transcripts) t.second.readCount = 0.f;
+    for (auto &ge : g->genes) ge.second.readCount = 0;
+    return SNAPGPU_OK;
+}
+
+// ostream << double with the default format (precision 6, %g)
+static std::string fmtG(double v) {
+    char b[64];
+    snprintf(b, sizeof(b), "%g", v);
+    return b;
+}
+
+int snapgpu_gtf_write_counts(const snapgpu_gtf_t *g, const char *prefix) {
+    if (!g || !prefix) return SNAPGPU_EINVAL;
+    const std::string p = prefix;
+    std::string tid, tname, gid, gname, jid;
+    for (auto &t : g->transcripts) {   // GTFTranscript::WriteReadCountID / Name: round(float)
+        const std::string c = fmtG(::round((double)t.second.readCount));
+        tid += t.first + '\t' + c + '\n';
+        tname += t.second.transcriptName + '\t' + c + '\n';
+    }
+    std::map<std::string, uint32_t> byName;
+    for (auto &ge : g->genes) {
+        gid += ge.first + '\t' + std::to_string(ge.second.readCount) + '\n';
+        // GTFGene::WriteJunctionCountID (:916-924): count / (gene reads / 1000 + 1), rounded
+        const float expression = (float)(((float)ge.second.readCount / 1000.0) + 1);
+        for (auto &in : ge.second.introns) {
+            const GtfFeature *f = in.second;
+            jid += ge.first + ":" + f->chr + ':' + u32s(f->start) + "-" + u32s(f->end) + '\t' +
+                   fmtG(::round((double)((float)f->readCount / expression))) + '\n';
+        }
+        auto it = byName.find(ge.second.geneName);
+        if (it == byName.end()) byName.insert({ge.second.geneName, ge.second.readCount});
+        else it->second += ge.second.readCount;
+    }
+    for (auto &x : byName) gname += x.first + '\t' + std::to_string(x.second) + '\n';
+    const std::pair<const char *, const std::string *> files[] = {
+        {".transcript_id.counts.txt", &tid}, {".gene_id.counts.txt", &gid}, {".junction_id.counts.txt", &jid},
+        {".transcript_name.counts.txt", &tname}, {".gene_name.counts.txt", &gname}, {".junction_name.counts.txt", nullptr}};
+    for (auto &f : files) {
+        FILE *o = fopen((p + f.first).c_str(), "w");
+        if (!o) { setError("cannot write " + p + f.first); return SNAPGPU_EIO; }
+        bool ok = !f.second || fwrite(f.second->data(), 1, f.second->size(), o) == f.second->size();
+        if (fclose(o) != 0 || !ok) { setError("write failed: " + p + f.first); return SNAPGPU_EIO; }
+    }
     return SNAPGPU_OK;
 }
 

@@ -114,6 +114,13 @@ struct SamLine {
     uint32_t nOps = 0;
     const std::string *cigar = nullptr;               // a complete CIGAR (transcriptome records)
     const char *rg = nullptr;
+    // paired records (getSAMData's hasMate branch, SAM.cpp:914-973; SimpleReadWriter::writePair,
+    // ReadWriter.cpp:133-217)
+    uint32_t qnameLen = 0;                            // writePair's QNAME length ("/1" "/2" dropped), 0 = idLen
+    bool hasMate = false, firstInPair = false;
+    uint32_t mateLoc = kInvalidLocation;              // the mate's location (invalid when NotFound)
+    int mateDir = 0;
+    uint32_t mateFront = 0, mateClippedLen = 0, mateFullLen = 0;
 };
 void samAppendLine(std::string &o, const Genome &g, const SamLine &L);
 

@@ -1,0 +1,679 @@
+// rna_paired.cpp -- the RNA paired-end product path: `snap-rna paired
+// <genome> <transcriptome> <gtf> r1.fq r2.fq` over a batch of pairs.
+//
+// PairedAlignerContext::runIterationThread (SNAPLib/PairedAligner.cpp:405-689) handles one pair
+// at a time: pre-filter, two transcriptome AlignRead calls with multi-hit export (1000 hits), the
+// genome ChimericPairedEndAligner, AlignmentFilter::AddAlignment for every hit,
+// AlignmentFilter::Filter (AlignmentFilter.cpp:302-739) -- which for some pairs re-scans both
+// reads with BaseAligner::CharacterizeSeeds (FindPartialMatches :957-1037) --, the spacing and
+// MAPQ adjustments, writePair (ReadWriter.cpp:133-217) and the GTF read counts.  Here every
+// stage runs over the batch: the three aligners as batched GPU calls, the filter on host
+// threads, the seed census of the reads that need it as one GPU batch (charseeds_kernel), the
+// count events in input order, the CIGARs as GPU batches, the SAM lines on host threads.
+//
+// Not restated: the contamination database (-x) and GTFReader::AnalyzeReadIntervals (the
+// intra/inter-chromosomal interval report fed by UnalignedRead / *chromosomalPair): no SAM
+// record or read count depends on them.
+#include "internal.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace snapgpu {
+struct GtfTranscript;
+struct GtfGene;
+const GtfTranscript *gtfTranscript(const snapgpu_gtf_t *g, const std::string &id);
+const std::string &gtfTranscriptChr(const GtfTranscript *t);
+const std::string &gtfTranscriptGene(const GtfTranscript *t);
+uint32_t gtfGenomicPosition(const GtfTranscript *t, uint32_t pos, uint32_t span);
+bool gtfSpliceCigar(const GtfTranscript *t, uint32_t pos, const std::vector<std::pair<uint32_t, char>> &tokens,
+                    std::string &out);
+const GtfGene *gtfGene(const snapgpu_gtf_t *g, const std::string &geneId);
+bool gtfGeneCheckBoundary(const GtfGene *ge, const std::string &chr, uint32_t pos, uint32_t buffer);
+bool gtfCountPair(snapgpu_gtf_t *g, const std::string &tid0, uint32_t tstart0, uint32_t start0, uint32_t len0,
+                  const std::string &tid1, uint32_t tstart1, uint32_t start1, uint32_t len1);
+}  // namespace snapgpu
+
+using namespace snapgpu;
+
+namespace {
+
+double msSince(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+int pieceAt(const Genome &g, uint32_t loc) {   // Genome::getPieceAtLocation (Genome.cpp:356-374)
+    int lo = 0, hi = (int)g.pieceOffsets.size() - 1;
+    while (lo <= hi) {
+        const int mid = (lo + hi) / 2;
+        if (g.pieceOffsets[mid] <= loc && (mid == (int)g.pieceOffsets.size() - 1 || g.pieceOffsets[mid + 1] > loc))
+            return mid;
+        else if (g.pieceOffsets[mid] <= loc) lo = mid + 1;
+        else hi = mid - 1;
+    }
+    return -1;
+}
+
+template <class F>
+void parallel(uint64_t n, F &&f) {
+    const unsigned nt = n < 2048 ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (nt == 1) { f(0u, (uint64_t)0, n); return; }
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; t++) th.emplace_back([&, t] { f(t, n * t / nt, n * (t + 1) / nt); });
+    for (auto &x : th) x.join();
+}
+
+// Alignment (AlignmentFilter.h:41-70)
+struct Alignment {
+    uint32_t location = 0;
+    int direction = 0;
+    int score = 0, mapq = 0;
+    std::string rname;
+    uint32_t pos = 0, posEnd = 0, posOriginal = 0;
+    bool isTranscriptome = false;
+    std::string transcriptId, geneId;
+};
+typedef std::map<std::string, Alignment> AlignmentMap;   // alignment_map, keyed by rname_pos
+
+// AlignmentPair (AlignmentFilter.cpp:63-98): score unsigned, distance int (unsigned differences)
+struct AlignmentPair {
+    const Alignment *a1, *a2;
+    int distance = 0;
+    uint32_t score = 0;
+    AlignmentPair(const Alignment *x, const Alignment *y) : a1(x), a2(y) {
+        score = (uint32_t)(x->score + y->score);
+        if (x->direction && !y->direction) distance = (int)(x->pos - y->pos);
+        else if (!x->direction && y->direction) distance = (int)(y->pos - x->pos);
+    }
+    bool operator<(const AlignmentPair &r) const { return score < r.score; }
+};
+
+// PairedAlignmentResult (PairedEndAligner.h:31-55) as the filter leaves it
+struct PairOut {
+    int status[2] = {SNAPGPU_NOT_FOUND, SNAPGPU_NOT_FOUND};
+    uint32_t location[2] = {kInvalidLocation, kInvalidLocation}, tlocation[2] = {0, 0};
+    int direction[2] = {0, 0}, score[2] = {0, 0}, mapq[2] = {0, 0};
+    bool isTranscriptome[2] = {false, false};
+    bool fromAlignTogether = false, alignedAsPair = false;
+};
+
+struct Ctx {
+    const Genome *genome, *transcriptome;
+    snapgpu_gtf_t *gtf;
+    std::map<std::string, uint32_t> pieceByName;   // Genome::getOffsetOfPiece
+    const snapgpu_rna_paired_options_t *opt;
+};
+
+struct Err {
+    std::string msg;
+    void set(const std::string &m) { if (msg.empty()) msg = m; }
+};
+
+// AlignmentFilter::AddAlignment + HashAlignment (AlignmentFilter.cpp:113-214).  isMate0 picks
+// map mate0 and the span of read1 (the reference's naming: read0's hits go to mate1).
+void addAlignment(const Ctx &C, AlignmentMap &mate0, AlignmentMap &mate1, uint32_t location, int direction, int score,
+                  int mapq, bool isT, bool isMate0, uint32_t len0, uint32_t len1, Err &err) {
+    if ((uint32_t)score > C.opt->maxDist) return;   // `score > maxDist`, unsigned
+    std::string rname = "*", tid, gid;
+    uint32_t pos = 0, posEnd = 0, posOriginal = 0;
+    const uint32_t span = isMate0 ? len1 : len0;
+    if (location != kInvalidLocation) {
+        const Genome &g = isT ? *C.transcriptome : *C.genome;
+        const int p = pieceAt(g, location);
+        if (p < 0) { err.set("AddAlignment: location before the first piece (the reference dereferences NULL)"); return; }
+        rname = g.pieceNames[p];
+        posOriginal = location - g.pieceOffsets[p] + 1;
+        pos = posOriginal;
+        if (!isT) {
+            posEnd = pos + span - 1;
+        } else {
+            const GtfTranscript *t = gtfTranscript(C.gtf, rname);
+            if (!t) { err.set("No transcript " + rname); return; }   // GTFReader::GetTranscript exits
+            tid = rname;
+            gid = gtfTranscriptGene(t);
+            rname = gtfTranscriptChr(t);
+            posEnd = gtfGenomicPosition(t, pos + span - 1, 0);
+            pos = gtfGenomicPosition(t, pos, span);
+        }
+    }
+    if (pos == 0) return;
+    Alignment a;
+    a.location = location; a.direction = direction; a.score = score; a.mapq = mapq; a.rname = rname;
+    a.pos = pos; a.posEnd = posEnd; a.posOriginal = posOriginal; a.isTranscriptome = isT;
+    a.transcriptId = tid; a.geneId = gid;
+    AlignmentMap &m = isMate0 ? mate0 : mate1;
+    const std::string key = rname + '_' + std::to_string(pos);
+    auto it = m.find(key);
+    if (it == m.end()) m.insert({key, a});
+    else if (a.score < it->second.score) it->second = a;
+    else if (a.score == it->second.score && a.isTranscriptome) it->second = a;
+}
+
+bool checkBoundary(const Ctx &C, const std::string &geneId, const std::string &chr, uint32_t pos, Err &err) {
+    const GtfGene *ge = gtfGene(C.gtf, geneId);
+    if (!ge) { err.set("No gene " + geneId); return false; }   // GTFReader::GetGene exits
+    return gtfGeneCheckBoundary(ge, chr, pos, 1000);
+}
+
+// AlignmentFilter::ProcessPairs (:1061-1180)
+void processPairs(const Ctx &C, PairOut &r, std::vector<AlignmentPair> &pairs, uint32_t &genomeMapq, Err &err) {
+    if (pairs.size() > 1) std::sort(pairs.begin(), pairs.end());
+    const AlignmentPair &p = pairs[0];
+    const Alignment *a[2] = {p.a1, p.a2};
+    for (int k = 0; k < 2; k++) {
+        if (a[k]->isTranscriptome) {
+            r.tlocation[k] = a[k]->location;
+            auto po = C.pieceByName.find(a[k]->rname);
+            if (po == C.pieceByName.end()) { err.set("chromosome " + a[k]->rname + " not in the genome"); return; }
+            r.location[k] = po->second + a[k]->pos - 1;
+        } else {
+            r.tlocation[k] = 0;
+            r.location[k] = a[k]->location;
+        }
+    }
+    if (!a[0]->isTranscriptome && !a[1]->isTranscriptome) genomeMapq = (uint32_t)a[0]->mapq;
+    for (int k = 0; k < 2; k++) {
+        r.direction[k] = a[k]->direction;
+        r.score[k] = a[k]->score;
+        r.isTranscriptome[k] = a[k]->isTranscriptome;
+    }
+    const int m = (int)std::min(70u, genomeMapq);
+    if (pairs.size() == 1 || pairs[1].score - pairs[0].score >= C.opt->confDiff) {
+        r.status[0] = r.status[1] = SNAPGPU_SINGLE_HIT;
+        r.mapq[0] = r.mapq[1] = m;
+    } else {
+        r.status[0] = r.status[1] = SNAPGPU_MULTIPLE_HITS;
+        r.mapq[0] = r.mapq[1] = 1;
+    }
+}
+
+// AlignmentFilter::CheckNoRC (:1039-1059)
+void checkNoRC(PairOut &r, const std::vector<AlignmentPair> &noRc) {
+    for (auto &it : noRc)
+        if (it.a1->rname == it.a2->rname && it.score < (uint32_t)(r.score[0] + r.score[1])) {
+            r.status[0] = r.status[1] = SNAPGPU_MULTIPLE_HITS;
+            r.mapq[0] = r.mapq[1] = 1;
+        }
+}
+
+// what AlignmentFilter::Filter (:302-739) decided for one pair before FindPartialMatches
+struct FilterState {
+    PairOut r;
+    bool needPartial = false;    // FindPartialMatches is due (the result is SingleHit there)
+    bool countPair = false;      // GTFReader::IncrementReadCount (pair form) is due
+    std::string tid0, tid1;
+    uint32_t tstart0 = 0, start0 = 0, len0 = 0, tstart1 = 0, start1 = 0, len1 = 0;
+};
+
+void filterPair(const Ctx &C, AlignmentMap &mate0, AlignmentMap &mate1, uint32_t len0, uint32_t len1, FilterState &S,
+                Err &err) {
+    std::vector<AlignmentPair> noRc, intragene, intra, inter;
+    uint32_t genomeMapq = 70;   // genome_mapq(maxMAPQ)
+    // mate0 / mate1 empty: UnalignedRead (:742-933) only feeds the interval report (not built)
+    for (auto &m0 : mate0)
+        for (auto &m1 : mate1) {
+            const Alignment &x = m0.second, &y = m1.second;
+            if ((x.direction && y.direction) || (!x.direction && !y.direction)) { noRc.emplace_back(&y, &x); continue; }
+            if (x.isTranscriptome && y.isTranscriptome) {
+                if (x.rname != y.rname) inter.emplace_back(&y, &x);
+                else if (checkBoundary(C, x.geneId, y.rname, y.pos, err)) intragene.emplace_back(&y, &x);
+                else if (checkBoundary(C, y.geneId, x.rname, x.pos, err)) intragene.emplace_back(&y, &x);
+                else intra.emplace_back(&y, &x);
+            } else if (x.isTranscriptome) {
+                if (x.rname != y.rname) inter.emplace_back(&y, &x);
+                else if (checkBoundary(C, x.geneId, y.rname, y.pos, err)) intragene.emplace_back(&y, &x);
+                else intra.emplace_back(&y, &x);
+            } else if (y.isTranscriptome) {
+                if (x.rname != y.rname) inter.emplace_back(&y, &x);
+                else if (checkBoundary(C, y.geneId, x.rname, x.pos, err)) intragene.emplace_back(&y, &x);
+                else intra.emplace_back(&y, &x);
+            } else {
+                intragene.emplace_back(&y, &x);
+            }
+        }
+    PairOut &r = S.r;
+    if (!intragene.empty()) {
+        processPairs(C, r, intragene, genomeMapq, err);
+        if (r.status[0] == SNAPGPU_SINGLE_HIT) {
+            const AlignmentPair &p = intragene[0];
+            S.countPair = true;
+            S.tid0 = p.a1->transcriptId; S.tstart0 = p.a1->posOriginal; S.start0 = p.a1->pos; S.len0 = len1;
+            S.tid1 = p.a2->transcriptId; S.tstart1 = p.a2->posOriginal; S.start1 = p.a2->pos; S.len1 = len0;
+        }
+        r.fromAlignTogether = false;
+        r.alignedAsPair = true;
+        return;
+    }
+    if (!intra.empty()) {
+        processPairs(C, r, intra, genomeMapq, err);
+        if (r.status[0] == SNAPGPU_SINGLE_HIT) checkNoRC(r, noRc);
+        if ((uint32_t)intra[0].distance <= C.opt->maxSpacing) return;   // flags left as the chimeric aligner set them
+        S.needPartial = r.status[0] == SNAPGPU_SINGLE_HIT;
+        r.fromAlignTogether = false;
+        r.alignedAsPair = false;
+        return;
+    }
+    if (!inter.empty()) {
+        processPairs(C, r, inter, genomeMapq, err);
+        if (r.status[0] == SNAPGPU_SINGLE_HIT) checkNoRC(r, noRc);
+        S.needPartial = r.status[0] == SNAPGPU_SINGLE_HIT;
+        r.fromAlignTogether = false;
+        r.alignedAsPair = false;
+        return;
+    }
+    if (!noRc.empty()) {
+        processPairs(C, r, noRc, genomeMapq, err);
+        S.needPartial = r.status[0] == SNAPGPU_SINGLE_HIT;
+        r.fromAlignTogether = false;
+        r.alignedAsPair = false;
+        return;
+    }
+    for (int k = 0; k < 2; k++) {
+        r.tlocation[k] = 0; r.status[k] = SNAPGPU_NOT_FOUND; r.location[k] = 0; r.direction[k] = 0;
+        r.score[k] = 0; r.mapq[k] = 0; r.isTranscriptome[k] = false;
+    }
+    r.fromAlignTogether = false;
+    r.alignedAsPair = false;
+}
+
+// FindPartialMatches (:957-1037): any pair of seed-run starts of the two reads on one
+// chromosome closer than maxSpacing (the reference's double loop, as a sorted sweep)
+bool partialMatch(const Ctx &C, const snapgpu_seed_runs_t *R, uint64_t i0, uint64_t i1, uint32_t len0, uint32_t len1,
+                  Err &err) {
+    std::vector<std::pair<int, int>> p[2];   // (piece, 1-based position)
+    const uint64_t ri[2] = {i0, i1};
+    const uint32_t lens[2] = {len0, len1};
+    for (int k = 0; k < 2; k++)
+        for (uint64_t j = R->start[ri[k]]; j < R->start[ri[k] + 1]; j++) {
+            const snapgpu_seed_run_t &run = R->runs[j];
+            const uint32_t loc = run.direction ? run.location + (lens[k] - run.maxOffset) : run.location + run.minOffset;
+            const int pc = pieceAt(*C.genome, loc);
+            if (pc < 0) { err.set("FindPartialMatches: location before the first piece (the reference dereferences NULL)"); return false; }
+            p[k].push_back({pc, (int)(loc - C.genome->pieceOffsets[pc] + 1)});
+        }
+    std::sort(p[1].begin(), p[1].end());
+    for (auto &a : p[0]) {
+        // closest positions of the other read on the same piece
+        auto it = std::lower_bound(p[1].begin(), p[1].end(), a);
+        for (int d = 0; d < 2; d++) {
+            auto b = d == 0 ? it : (it == p[1].begin() ? p[1].end() : it - 1);
+            if (b == p[1].end() || b->first != a.first) continue;
+            if ((uint32_t)std::abs(b->second - a.second) < C.opt->maxSpacing) return true;
+        }
+    }
+    return false;
+}
+
+bool idsMatch(const char *a, uint32_t la, const char *b, uint32_t lb) {   // readIdsMatch (SAM.cpp:53-68)
+    if (la != lb) return false;
+    for (uint32_t i = 0; i < la; i++) {
+        if (a[i] != b[i]) return false;
+        if (a[i] == ' ' || a[i] == '/') return true;
+    }
+    return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+void snapgpu_rna_paired_options_default(snapgpu_rna_paired_options_t *o) {
+    if (!o) return;
+    memset(o, 0, sizeof(*o));
+    o->clipping = 3;              // AlignerOptions.cpp:48
+    o->confDiff = 2;
+    o->maxDist = 15;              // AlignerOptions.cpp:73-77 (paired)
+    o->minSpacing = 50;           // PairedAligner.cpp:57-58
+    o->maxSpacing = 1000;
+    o->minPercentAbovePhred = 90.0f;
+    o->minPhred = 20;
+    o->phredOffset = 33;
+    o->maxHitsToGet = 1000;       // PairedAligner.cpp:584
+    o->readGroup = "FASTQ";
+    o->commandLine = "";
+    o->version = "";
+}
+
+int snapgpu_rna_paired_align(snapgpu_paired_aligner_t *pa, snapgpu_aligner_t *ta, snapgpu_gtf_t *gtf,
+                             snapgpu_reads_t *reads0, snapgpu_reads_t *reads1, const snapgpu_rna_paired_options_t *opt,
+                             const char *samPath, snapgpu_rna_pair_result_t *out, snapgpu_rna_paired_stats_t *stats) {
+    const auto w0 = std::chrono::steady_clock::now();
+    if (!pa || !ta || !gtf || !reads0 || !reads1 || !opt) { setError("rna_paired_align: null argument"); return SNAPGPU_EINVAL; }
+    if (reads0->n != reads1->n) { setError("rna_paired_align: the two read batches differ in length"); return SNAPGPU_EINVAL; }
+    if (!reads0->ids || !reads1->ids) { setError("rna_paired_align: the reads carry no ids (use snapgpu_reads_from_fastq)"); return SNAPGPU_EINVAL; }
+    snapgpu_aligner_t *ga = snapgpu_paired_aligner_single(pa);   // the genome index upload (BaseAligner)
+    const snapgpu_index_t *gi = snapgpu_aligner_index(ga), *ti = snapgpu_aligner_index(ta);
+    if (!gi || !ti) { setError("rna_paired_align: aligner without index"); return SNAPGPU_EINVAL; }
+    snapgpu_rna_paired_stats_t st{};
+    const uint64_t n = reads0->n;
+    st.totalPairs = n;
+    snapgpu_reads_t *R[2] = {reads0, reads1};
+    for (int k = 0; k < 2; k++) {
+        const int rc = snapgpu_reads_clip(R[k], opt->clipping, nullptr, nullptr);   // FASTQReader (FASTQ.cpp:250)
+        if (rc) return rc;
+    }
+    if (!opt->ignoreMismatchedIDs)   // Read::checkIdMatch (Read.cpp:37-49): the reference exits
+        for (uint64_t i = 0; i < n; i++)
+            if (!idsMatch(reads0->ids + reads0->idOffsets[i], reads0->idLengths[i], reads1->ids + reads1->idOffsets[i],
+                          reads1->idLengths[i])) {
+                setError("rna_paired_align: unmatched read IDs at pair " + std::to_string(i) + " (ignoreMismatchedIDs)");
+                return SNAPGPU_EINVAL;
+            }
+    // pre-filter (PairedAligner.cpp:555-575): length / Ns per read, quality of read0 (sic, :564)
+    std::vector<uint8_t> useful(n, 0);
+    parallel(n, [&](unsigned, uint64_t b, uint64_t e) {
+        for (uint64_t i = b; i < e; i++) {
+            bool u[2], q[2];
+            for (int k = 0; k < 2; k++) {
+                const char *d = R[k]->bases + R[k]->offsets[i], *qq = R[k]->quals + R[k]->offsets[i];
+                const uint32_t len = R[k]->lengths[i];
+                unsigned ns = 0, good = 0;
+                for (uint32_t j = 0; j < len; j++) {
+                    ns += d[j] == 'N' || d[j] == 'n';
+                    good += (unsigned)(int)qq[j] - opt->phredOffset >= opt->minPhred;
+                }
+                u[k] = len >= 50 && (int)ns <= (int)opt->maxDist;
+                q[k] = ((float)good / (float)len) * 100.f >= opt->minPercentAbovePhred;
+            }
+            useful[i] = !((!u[0] && !u[1]) || !q[0]);
+        }
+    });
+    std::vector<uint64_t> ui;
+    for (uint64_t i = 0; i < n; i++) if (useful[i]) ui.push_back(i);
+    const uint64_t nu = ui.size();
+    st.usefulPairs = nu;
+    // the useful pairs as batches (views of the clipped reads)
+    snapgpu_reads_t *U[2] = {nullptr, nullptr};
+    std::vector<uint64_t> uo[2];
+    std::vector<uint32_t> ul[2];
+    for (int k = 0; k < 2; k++) {
+        uo[k].resize(nu + 1); ul[k].resize(nu + 1);
+        for (uint64_t j = 0; j < nu; j++) { uo[k][j] = R[k]->offsets[ui[j]]; ul[k][j] = R[k]->lengths[ui[j]]; }
+        U[k] = snapgpu_reads_from_arrays(nu, R[k]->bases, R[k]->quals, uo[k].data(), ul[k].data());
+        if (!U[k]) { snapgpu_reads_free(U[0]); return SNAPGPU_ENOMEM; }
+    }
+    snapgpu_seed_runs_t *runs = nullptr;
+    auto fail = [&](int code) {
+        snapgpu_reads_free(U[0]); snapgpu_reads_free(U[1]);
+        snapgpu_seed_runs_free(runs);
+        return code;
+    };
+    int rc = SNAPGPU_OK;
+    const uint32_t mh = opt->maxHitsToGet;
+    std::vector<snapgpu_result_t> tr[2];
+    std::vector<int32_t> tf[2];
+    std::vector<snapgpu_multi_hit_t> th[2];
+    std::vector<snapgpu_pair_result_t> gr(nu + 1);
+    auto t0 = std::chrono::steady_clock::now();
+    if (nu) {
+        // transcriptomeAligner->AlignRead(read0 / read1, ..., maxHitsToGet 1000, multiHits) (:601-605)
+        for (int k = 0; k < 2; k++) {
+            tr[k].resize(nu); tf[k].resize(nu); th[k].resize(nu * (uint64_t)mh);
+            if ((rc = snapgpu_align_batch_ex(ta, U[k], nullptr, mh, tr[k].data(), tf[k].data(), th[k].data())))
+                return fail(rc);
+        }
+        // g_aligner->align(read0, read1, &result) (:625)
+        if ((rc = snapgpu_paired_align_batch(pa, U[0], U[1], gr.data()))) return fail(rc);
+    }
+    st.alignMs = msSince(t0);
+    // AddAlignment + Filter up to FindPartialMatches, on host threads
+    t0 = std::chrono::steady_clock::now();
+    Ctx C{gi->genome, ti->genome, gtf, {}, opt};
+    for (size_t p = 0; p < gi->genome->pieceNames.size(); p++) C.pieceByName.insert({gi->genome->pieceNames[p], gi->genome->pieceOffsets[p]});
+    std::vector<FilterState> fs(nu + 1);
+    std::vector<Err> errs(16);
+    parallel(nu, [&](unsigned t, uint64_t b, uint64_t e) {
+        AlignmentMap mate0, mate1;
+        for (uint64_t j = b; j < e && errs[t].msg.empty(); j++) {
+            mate0.clear(); mate1.clear();
+            const uint32_t len0 = ul[0][j], len1 = ul[1][j];
+            for (int k = 0; k < 2; k++)
+                for (int32_t h = 0; h < tf[k][j]; h++) {
+                    const snapgpu_multi_hit_t &m = th[k][j * (uint64_t)mh + h];
+                    addAlignment(C, mate0, mate1, m.location, m.direction, m.score, 0, true, k == 1, len0, len1, errs[t]);
+                }
+            const snapgpu_pair_result_t &g = gr[j];
+            addAlignment(C, mate0, mate1, g.location[0], g.direction[0], g.score[0], g.mapq[0], false, false, len0, len1, errs[t]);
+            addAlignment(C, mate0, mate1, g.location[1], g.direction[1], g.score[1], g.mapq[1], false, true, len0, len1, errs[t]);
+            FilterState &S = fs[j];
+            S.r.fromAlignTogether = g.fromAlignTogether;
+            S.r.alignedAsPair = g.alignedAsPair;
+            filterPair(C, mate0, mate1, len0, len1, S, errs[t]);
+        }
+    });
+    for (auto &e : errs) if (!e.msg.empty()) { setError("rna_paired_align: " + e.msg); return fail(SNAPGPU_EFORMAT); }
+    st.filterMs = msSince(t0);
+    // FindPartialMatches: CharacterizeSeeds of both reads of the pairs that need it, one GPU batch
+    t0 = std::chrono::steady_clock::now();
+    std::vector<uint64_t> need;
+    for (uint64_t j = 0; j < nu; j++) if (fs[j].needPartial) need.push_back(j);
+    st.partialPairs = need.size();
+    if (!need.empty()) {
+        // both reads in one batch: read0 of need[i] at 2i, read1 at 2i + 1
+        std::vector<uint64_t> po(2 * need.size() + 1);
+        std::vector<uint32_t> pl(2 * need.size() + 1);
+        std::string bb, qq;
+        for (size_t i = 0; i < need.size(); i++)
+            for (int k = 0; k < 2; k++) {
+                const uint64_t o = uo[k][need[i]];
+                po[2 * i + k] = bb.size();
+                pl[2 * i + k] = ul[k][need[i]];
+                bb.append(R[k]->bases + o, ul[k][need[i]]);
+                qq.append(R[k]->quals + o, ul[k][need[i]]);
+            }
+        snapgpu_reads_t *both = snapgpu_reads_from_arrays(2 * need.size(), bb.data(), qq.data(), po.data(), pl.data());
+        if (!both) return fail(SNAPGPU_ENOMEM);
+        snapgpu_charseeds_params_t cp;
+        snapgpu_charseeds_params_default(&cp);   // the partial aligner: maxHits 300, 12 seeds (:518-527)
+        cp.maxK = opt->maxDist;
+        runs = snapgpu_characterize_seeds(ga, both, nullptr, 0, &cp);
+        snapgpu_reads_free(both);
+        if (!runs) return fail(SNAPGPU_EDEVICE);
+        for (uint64_t i = 0; i < 2 * need.size(); i++)
+            if (runs->flags[i] & SNAPGPU_FLAG_READ_TOO_LONG) {
+                setError("rna_paired_align: read longer than maxReadSize (the reference exits, BaseAligner.cpp:272-275)");
+                return fail(SNAPGPU_EINVAL);
+            }
+        st.seedRuns = runs->nRuns;
+        std::vector<uint8_t> hit(need.size(), 0);
+        parallel(need.size(), [&](unsigned t, uint64_t b, uint64_t e) {
+            for (uint64_t i = b; i < e; i++)
+                hit[i] = partialMatch(C, runs, 2 * i, 2 * i + 1, ul[0][need[i]], ul[1][need[i]], errs[t]);
+        });
+        for (auto &e : errs) if (!e.msg.empty()) { setError("rna_paired_align: " + e.msg); return fail(SNAPGPU_EFORMAT); }
+        for (size_t i = 0; i < need.size(); i++)
+            if (hit[i]) {
+                PairOut &r = fs[need[i]].r;
+                r.status[0] = r.status[1] = SNAPGPU_MULTIPLE_HITS;
+                r.mapq[0] = r.mapq[1] = 1;
+                st.partialMatches++;
+            }
+    }
+    st.seedMs = msSince(t0);
+    // spacing and MAPQ adjustments (PairedAligner.cpp:648-663); read counts in input order
+    for (uint64_t j = 0; j < nu; j++) {
+        PairOut &r = fs[j].r;
+        if (opt->forceSpacing && (r.status[0] == SNAPGPU_SINGLE_HIT) != (r.status[1] == SNAPGPU_SINGLE_HIT)) {
+            r.status[0] = r.status[1] = SNAPGPU_NOT_FOUND;
+            r.location[0] = r.location[1] = kInvalidLocation;
+        }
+        if (r.score[0] + r.score[1] >= 5)
+            for (int k = 0; k < 2; k++) if (r.mapq[k] < 50) r.mapq[k] /= 2;
+        const FilterState &S = fs[j];
+        if (S.countPair &&
+            !gtfCountPair(gtf, S.tid0, S.tstart0, S.start0, S.len0, S.tid1, S.tstart1, S.start1, S.len1)) {
+            setError("rna_paired_align: read count for an unknown transcript or gene");
+            return fail(SNAPGPU_EFORMAT);
+        }
+    }
+    // the pairs' records, in input order; filtered pairs: NotFound, InvalidGenomeLocation
+    std::vector<PairOut> po(n);
+    {
+        std::vector<int64_t> uidx(n, -1);
+        for (uint64_t j = 0; j < nu; j++) uidx[ui[j]] = (int64_t)j;
+        for (uint64_t i = 0; i < n; i++) if (uidx[i] >= 0) po[i] = fs[uidx[i]].r;
+    }
+    // CIGARs on the GPU (writeRead, SAM.cpp:1040-1066): genome records at the location, the
+    // transcriptome records on the transcriptome at tlocation
+    t0 = std::chrono::steady_clock::now();
+    std::vector<int32_t> ged[2], ted[2];
+    std::vector<uint32_t> gn[2], tn[2], gops[2], tops[2];
+    std::vector<uint8_t> isT[2];
+    for (int k = 0; k < 2; k++) {
+        std::vector<uint32_t> gl(n), tl(n);
+        std::vector<uint8_t> gd(n), td(n);
+        isT[k].assign(n, 0);
+        uint64_t nt = 0;
+        for (uint64_t i = 0; i < n; i++) {
+            const PairOut &r = po[i];
+            const uint32_t loc = r.status[k] != SNAPGPU_NOT_FOUND ? r.location[k] : kInvalidLocation;
+            const bool t = loc != kInvalidLocation && r.isTranscriptome[k];
+            isT[k][i] = t;
+            gl[i] = t ? kInvalidLocation : loc;
+            gd[i] = (uint8_t)(loc == kInvalidLocation ? 0 : r.direction[k]);
+            tl[i] = t ? r.tlocation[k] : kInvalidLocation;
+            td[i] = (uint8_t)r.direction[k];
+            nt += t;
+        }
+        st.transcriptomeRecords += nt;
+        ged[k].assign(n + 1, -1); gn[k].assign(n + 1, 0); gops[k].assign((n + 1) * SNAPGPU_CIGAR_MAX_OPS, 0);
+        ted[k].assign(n + 1, -1); tn[k].assign(n + 1, 0); tops[k].assign((n + 1) * SNAPGPU_CIGAR_MAX_OPS, 0);
+        if (n && (rc = snapgpu_cigar_batch(ga, R[k], gl.data(), gd.data(), (int)opt->useM, ged[k].data(), gn[k].data(),
+                                           gops[k].data())))
+            return fail(rc);
+        if (nt && (rc = snapgpu_cigar_batch(ta, R[k], tl.data(), td.data(), (int)opt->useM, ted[k].data(), tn[k].data(),
+                                            tops[k].data())))
+            return fail(rc);
+    }
+    // transcriptome records: computeCigarString's tokens through insertSpliceJunctions
+    std::vector<std::string> splice[2];
+    for (int k = 0; k < 2; k++) {
+        splice[k].assign(n, std::string());
+        parallel(n, [&](unsigned, uint64_t b, uint64_t e) {
+            std::vector<std::pair<uint32_t, char>> tk;
+            static const char kOp[] = "MIDNSHP=X";
+            for (uint64_t i = b; i < e; i++) {
+                if (!isT[k][i]) continue;
+                tk.clear();
+                const PairOut &r = po[i];
+                if (ted[k][i] >= 0) {
+                    const uint32_t full = R[k]->unclippedLength[i], front = R[k]->frontClipped[i];
+                    const uint32_t back = full - R[k]->lengths[i] - front;
+                    const bool rcd = r.direction[k] == SNAPGPU_RC;
+                    const uint32_t before = rcd ? back : front, after = rcd ? front : back;
+                    if (before) tk.push_back({before, 'S'});
+                    for (uint32_t q = 0; q < tn[k][i]; q++) {
+                        const uint32_t op = tops[k][i * SNAPGPU_CIGAR_MAX_OPS + q];
+                        tk.push_back({op >> 4, kOp[op & 15]});
+                    }
+                    if (after) tk.push_back({after, 'S'});
+                }
+                const Genome &tg = *ti->genome;
+                const int p = pieceAt(tg, r.tlocation[k]);
+                const GtfTranscript *t = p >= 0 ? gtfTranscript(gtf, tg.pieceNames[p]) : nullptr;
+                if (t) gtfSpliceCigar(t, r.tlocation[k] - tg.pieceOffsets[p] + 1, tk, splice[k][i]);
+            }
+        });
+    }
+    st.cigarMs = msSince(t0);
+    // writePair (ReadWriter.cpp:133-217): the end at the lower location first
+    t0 = std::chrono::steady_clock::now();
+    const unsigned ntd = n < 2048 ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::string> parts(ntd);
+    std::vector<uint64_t> cnt(3 * ntd, 0);
+    parallel(n, [&](unsigned t, uint64_t b, uint64_t e) {
+        std::string &o = parts[t];
+        o.reserve((e - b) * 640);
+        for (uint64_t i = b; i < e; i++) {
+            const PairOut &r = po[i];
+            uint32_t idLen[2] = {R[0]->idLengths[i], R[1]->idLengths[i]};
+            const char *id[2] = {R[0]->ids + R[0]->idOffsets[i], R[1]->ids + R[1]->idOffsets[i]};
+            if (idLen[0] == idLen[1] && idLen[0] > 2 && id[0][idLen[0] - 2] == '/' && id[1][idLen[0] - 2] == '/') {
+                const char c0 = id[0][idLen[0] - 1], c1 = id[1][idLen[1] - 1];
+                if ((c0 == '1' || c0 == '2') && (c0 == '1' || c1 == '2') && c0 != c1) { idLen[0] -= 2; idLen[1] -= 2; }
+            }
+            uint32_t locs[2];
+            for (int k = 0; k < 2; k++) locs[k] = r.status[k] != SNAPGPU_NOT_FOUND ? r.location[k] : kInvalidLocation;
+            const int first = locs[0] > locs[1], second = 1 - first;
+            for (int w = 0; w < 2; w++) {
+                const int k = w == 0 ? first : second, m = 1 - k;
+                SamLine L;
+                L.id = id[k];
+                L.idLen = R[k]->idLengths[i];
+                L.qnameLen = idLen[k];
+                L.front = R[k]->frontClipped[i];
+                L.clippedLen = R[k]->lengths[i];
+                L.fullLen = R[k]->unclippedLength[i];
+                L.bases = R[k]->bases + R[k]->offsets[i] - L.front;
+                L.quals = R[k]->quals + R[k]->offsets[i] - L.front;
+                L.rg = opt->readGroup;
+                L.result = r.status[k];
+                L.loc = locs[k];
+                L.dir = r.direction[k];
+                L.mapq = r.mapq[k];
+                if (isT[k][i]) {
+                    L.cigar = &splice[k][i];
+                    L.ed = ted[k][i];
+                } else {
+                    L.ed = ged[k][i];
+                    L.ops = gops[k].data() + i * SNAPGPU_CIGAR_MAX_OPS;
+                    L.nOps = gn[k][i];
+                }
+                L.hasMate = true;
+                L.firstInPair = w == 0;
+                L.mateLoc = locs[m];
+                L.mateDir = r.direction[m];
+                L.mateFront = R[m]->frontClipped[i];
+                L.mateClippedLen = R[m]->lengths[i];
+                L.mateFullLen = R[m]->unclippedLength[i];
+                samAppendLine(o, *gi->genome, L);
+                cnt[3 * t + (r.status[k] == SNAPGPU_SINGLE_HIT ? 0 : r.status[k] == SNAPGPU_MULTIPLE_HITS ? 1 : 2)]++;
+            }
+        }
+    });
+    for (unsigned t = 0; t < ntd; t++) { st.singleHits += cnt[3 * t]; st.multiHits += cnt[3 * t + 1]; st.notFound += cnt[3 * t + 2]; }
+    if (samPath) {
+        FILE *f = fopen(samPath, "w");
+        if (!f) { setError(std::string("cannot write ") + samPath); return fail(SNAPGPU_EIO); }
+        uint64_t hlen = 0;
+        snapgpu_sam_header(gi, 0, opt->commandLine ? opt->commandLine : "", opt->version ? opt->version : "", nullptr,
+                           nullptr, 0, &hlen);
+        std::string hdr(hlen, '\0');
+        if ((rc = snapgpu_sam_header(gi, 0, opt->commandLine ? opt->commandLine : "", opt->version ? opt->version : "",
+                                     nullptr, &hdr[0], hlen, &hlen))) { fclose(f); return fail(rc); }
+        bool ok = fwrite(hdr.data(), 1, hdr.size(), f) == hdr.size();
+        for (auto &p : parts) ok = ok && fwrite(p.data(), 1, p.size(), f) == p.size();
+        ok = (fclose(f) == 0) && ok;
+        if (!ok) { setError(std::string("write failed: ") + samPath); return fail(SNAPGPU_EIO); }
+    }
+    if (out)
+        for (uint64_t i = 0; i < n; i++) {
+            const PairOut &r = po[i];
+            snapgpu_rna_pair_result_t &o = out[i];
+            memset(&o, 0, sizeof(o));
+            for (int k = 0; k < 2; k++) {
+                o.status[k] = (uint8_t)r.status[k];
+                o.location[k] = r.status[k] != SNAPGPU_NOT_FOUND ? r.location[k] : kInvalidLocation;
+                o.tlocation[k] = r.tlocation[k];
+                o.direction[k] = (uint8_t)r.direction[k];
+                o.score[k] = r.score[k];
+                o.mapq[k] = r.mapq[k];
+                o.isTranscriptome[k] = r.isTranscriptome[k];
+            }
+            o.fromAlignTogether = r.fromAlignTogether;
+            o.alignedAsPair = r.alignedAsPair;
+            o.useful = useful[i];
+        }
+    st.writeMs = msSince(t0);
+    st.wallMs = msSince(w0);
+    if (stats) *stats = st;
+    return fail(SNAPGPU_OK);
+}
+
+}  // extern "C"

@@ -16,8 +16,14 @@ using namespace snapgpu;
 
 namespace {
 
-const int SAM_UNMAPPED = 0x004;             // SAM.h:40
-const int SAM_REVERSE_COMPLEMENT = 0x010;   // SAM.h:42
+const int SAM_MULTI_SEGMENT = 0x001;        // SAM.h:38-46
+const int SAM_ALL_ALIGNED = 0x002;
+const int SAM_UNMAPPED = 0x004;
+const int SAM_NEXT_UNMAPPED = 0x008;
+const int SAM_REVERSE_COMPLEMENT = 0x010;
+const int SAM_NEXT_REVERSED = 0x020;
+const int SAM_FIRST_SEGMENT = 0x040;
+const int SAM_LAST_SEGMENT = 0x080;
 
 inline char upperCase(char c) { return (c >= 'a' && c <= 'z') ? (char)(c - 0x20) : c; }   // Tables.cpp:74-80
 inline char complement(char c) {                                                         // Tables.cpp:22-30
@@ -109,20 +115,62 @@ void samAppendLine(std::string &o, const Genome &g, const SamLine &L) {
     const int rc = loc != kInvalidLocation && L.dir == SNAPGPU_RC;
     int flags = 0, mapq = 0;
     const char *pieceName = "*";
+    int pieceIdx = -1;
     uint32_t pos = 0;
     if (loc != kInvalidLocation) {
         if (rc) flags |= SAM_REVERSE_COMPLEMENT;
         int p = pieceAt(g, loc);
         if (p >= 0) {
             pieceName = g.pieceNames[p].c_str();
+            pieceIdx = p;
             pos = loc - g.pieceOffsets[p] + 1;
         }
         mapq = std::max(0, std::min(70, L.mapq));
     } else {
         flags |= SAM_UNMAPPED;
     }
+    // mate fields (SAM.cpp:914-973): RNEXT "=" unless both are mapped on different pieces
+    // (the reference compares piece-name pointers), TLEN from the clipped-read extents
+    const char *mateName = "*";
+    uint32_t matePos = 0;
+    int64_t tlen = 0;
+    if (L.hasMate) {
+        flags |= SAM_MULTI_SEGMENT | (L.firstInPair ? SAM_FIRST_SEGMENT : SAM_LAST_SEGMENT);
+        int mateIdx = -1;
+        if (L.mateLoc != kInvalidLocation) {
+            const int mp = pieceAt(g, L.mateLoc);
+            if (mp >= 0) {
+                mateName = g.pieceNames[mp].c_str();
+                mateIdx = mp;
+                matePos = L.mateLoc - g.pieceOffsets[mp] + 1;
+            }
+            if (L.mateDir == SNAPGPU_RC) flags |= SAM_NEXT_REVERSED;
+            if (loc == kInvalidLocation) {   // the unmapped end takes the mate's RNAME / POS
+                pieceName = mateName;
+                pieceIdx = -2;               // a different pointer from mateName below
+                mateName = "=";
+                pos = matePos;
+            }
+        } else {
+            flags |= SAM_NEXT_UNMAPPED;
+            mateName = "=";
+            matePos = pos;
+        }
+        if (loc != kInvalidLocation && L.mateLoc != kInvalidLocation) {
+            flags |= SAM_ALL_ALIGNED;
+            const uint32_t back = L.fullLen - L.clippedLen - L.front;
+            const uint32_t before = rc ? back : L.front, after = rc ? L.front : back;
+            const int64_t myStart = (int64_t)(uint32_t)(loc - before);
+            const int64_t myEnd = (int64_t)(uint32_t)(loc + L.clippedLen + after);
+            const int64_t mBefore = L.mateFront, mAfter = (int64_t)L.mateFullLen - L.mateClippedLen - L.mateFront;
+            const int64_t mateStart = (int64_t)L.mateLoc - (L.mateDir == SNAPGPU_RC ? mAfter : mBefore);
+            const int64_t mateEnd = (int64_t)L.mateLoc + L.mateClippedLen + (L.mateDir == SNAPGPU_FORWARD ? mAfter : mBefore);
+            if (pieceIdx >= 0 && pieceIdx == mateIdx) tlen = myStart < mateStart ? mateEnd - myStart : -(myEnd - mateStart);
+        }
+        if (pieceIdx >= 0 && pieceIdx == mateIdx) mateName = "=";
+    }
     // QNAME: truncated at the first space (SAM.cpp:1080-1086)
-    uint32_t qlen = L.idLen;
+    uint32_t qlen = L.qnameLen ? L.qnameLen : L.idLen;
     if (const void *sp = memchr(L.id, ' ', qlen)) qlen = (uint32_t)((const char *)sp - L.id);
     o.append(L.id, qlen);
     o += '\t';
@@ -154,7 +202,13 @@ void samAppendLine(std::string &o, const Genome &g, const SamLine &L) {
     }
     // SEQ / QUAL are printed with "%.*s" (SAM.cpp:1122-1136): a NUL byte ends them early
     // (COMPLEMENT[] of a non-ACGTN base is 0; a quality string shorter than the read)
-    o += "\t*\t0\t0\t";
+    o += '\t';
+    o += mateName;
+    o += '\t';
+    appendUint(o, matePos);
+    o += '\t';
+    appendInt(o, tlen);
+    o += '\t';
     char sq[2 * 1024];
     const uint32_t len = L.fullLen;
     const uint32_t n = len < 1024 ? len : 1024;

@@ -739,6 +739,13 @@ class Gtf:
                                               4096, C.byref(used)), "gtf_splice_cigar")
         return buf.value.decode()
 
+    def write_counts(self, prefix):
+        """GTFReader::WriteReadCounts: <prefix>.{transcript,gene,junction}_{id,name}.counts.txt."""
+        _check(lib().snapgpu_gtf_write_counts(self._h, str(prefix).encode()), "gtf_write_counts")
+
+    def reset_counts(self):
+        _check(lib().snapgpu_gtf_reset_counts(self._h), "gtf_reset_counts")
+
     def __del__(self):
         if getattr(self, "_h", None):
             lib().snapgpu_gtf_free(self._h)
@@ -761,3 +768,32 @@ def single_align(genome_aligner, transcriptome_aligner, gtf, reads, sam_path, **
     _check(lib().snapgpu_single_align(genome_aligner._h, transcriptome_aligner._h, gtf._h, reads._p, C.byref(o),
                                       str(sam_path).encode(), C.byref(st)), "single_align")
     return {f: getattr(st, f) for f, _ in st._fields_}
+
+
+RNA_PAIR_RESULT_DTYPE = np.dtype([
+    ("location", "<u4", (2,)), ("tlocation", "<u4", (2,)), ("score", "<i4", (2,)), ("mapq", "<i4", (2,)),
+    ("status", "u1", (2,)), ("direction", "u1", (2,)), ("isTranscriptome", "u1", (2,)), ("fromAlignTogether", "u1"),
+    ("alignedAsPair", "u1"), ("useful", "u1"), ("reserved", "u1", (7,)),
+])
+assert RNA_PAIR_RESULT_DTYPE.itemsize == 48
+
+
+def rna_paired_options(**kw):
+    o = _ffi.RnaPairedOptions()
+    lib().snapgpu_rna_paired_options_default(C.byref(o))
+    for k, v in kw.items():
+        setattr(o, k, v.encode() if isinstance(v, str) else v)
+    return o
+
+
+def rna_paired_align(paired_aligner, transcriptome_aligner, gtf, reads0, reads1, sam_path=None, **options):
+    """`snap-rna paired` (PairedAligner.cpp:405-689) over a FASTQ pair batch: the transcriptome and
+    genome aligners, the seed census of FindPartialMatches and the CIGARs on the GPU; writes
+    sam_path (if given) and advances gtf's read counters.  -> (RNA_PAIR_RESULT_DTYPE[n], stats)."""
+    o = rna_paired_options(**options)
+    st = _ffi.RnaPairedStats()
+    out = np.zeros(max(1, reads0.n), dtype=RNA_PAIR_RESULT_DTYPE)
+    _check(lib().snapgpu_rna_paired_align(paired_aligner._h, transcriptome_aligner._h, gtf._h, reads0._p, reads1._p,
+                                          C.byref(o), None if sam_path is None else str(sam_path).encode(),
+                                          out.ctypes.data, C.byref(st)), "rna_paired_align")
+    return out[:reads0.n], {f: getattr(st, f) for f, _ in st._fields_}

@@ -174,6 +174,22 @@ class SingleOptions(C.Structure):
     ]
 
 
+class RnaPairedOptions(C.Structure):
+    _fields_ = [
+        ("clipping", C.c_int32), ("confDiff", C.c_uint32), ("maxDist", C.c_uint32), ("minSpacing", C.c_uint32),
+        ("maxSpacing", C.c_uint32), ("forceSpacing", C.c_uint32), ("minPercentAbovePhred", C.c_float),
+        ("minPhred", C.c_uint32), ("phredOffset", C.c_uint32), ("useM", C.c_uint32), ("maxHitsToGet", C.c_uint32),
+        ("ignoreMismatchedIDs", C.c_uint32), ("readGroup", C.c_char_p), ("commandLine", C.c_char_p),
+        ("version", C.c_char_p),
+    ]
+
+
+class RnaPairedStats(C.Structure):
+    _fields_ = [(f, C.c_uint64) for f in ("totalPairs", "usefulPairs", "singleHits", "multiHits", "notFound",
+                                          "transcriptomeRecords", "partialPairs", "partialMatches", "seedRuns")] + \
+               [(f, C.c_double) for f in ("alignMs", "filterMs", "seedMs", "cigarMs", "writeMs", "wallMs")]
+
+
 class SingleStats(C.Structure):
     _fields_ = [(f, C.c_uint64) for f in ("totalReads", "usefulReads", "singleHits", "multiHits", "notFound",
                                           "transcriptomeRecords")] + \
@@ -307,6 +323,12 @@ _PROTOS += [
     ("snapgpu_paired_intersect_batch", C.c_int, [C.c_void_p, C.POINTER(Reads), C.POINTER(Reads), C.c_void_p]),
     ("snapgpu_paired_aligner_single", C.c_void_p, [C.c_void_p]),
     ("snapgpu_charseeds_params_default", None, [C.POINTER(CharSeedsParams)]),
+    ("snapgpu_rna_paired_options_default", None, [C.POINTER(RnaPairedOptions)]),
+    ("snapgpu_rna_paired_align", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(Reads), C.POINTER(Reads),
+                                           C.POINTER(RnaPairedOptions), C.c_char_p, C.c_void_p,
+                                           C.POINTER(RnaPairedStats)]),
+    ("snapgpu_gtf_write_counts", C.c_int, [C.c_void_p, C.c_char_p]),
+    ("snapgpu_gtf_reset_counts", C.c_int, [C.c_void_p]),
     ("snapgpu_characterize_seeds", C.POINTER(SeedRuns), [C.c_void_p, C.POINTER(Reads), C.c_void_p, C.c_uint64,
                                                          C.POINTER(CharSeedsParams)]),
     ("snapgpu_seed_runs_free", None, [C.POINTER(SeedRuns)]),

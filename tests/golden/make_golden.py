@@ -505,8 +505,199 @@ def charseeds_fixtures(work):
             f.write(gzip.compress("".join(out).encode(), compresslevel=9, mtime=0))
 
 
+RNA_BLOCK = 200
+COUNT_FILES = ("transcript_id", "transcript_name", "gene_id", "gene_name", "junction_id", "junction_name")
+
+
+def rna_paired_reads(path0, path1, seqs, gtf_path, rng):
+    """Read pairs for `snap-rna paired` (PairedAligner.cpp:405-668): mates from spliced mRNAs
+    (crossing exon junctions) and from pre-mRNA spans (the transcriptome the reference indexes),
+    intergenic pairs, chimeras between genes on one chromosome and on two, same-orientation
+    mates, one or both mates random, short / N-rich / low-quality mates, mutated mates."""
+    comp = str.maketrans("ACGTN", "TGCAN")
+    rc = lambda x: x.translate(comp)[::-1]
+    tx = {}
+    for line in open(gtf_path):
+        f = line.rstrip("\n").split("\t")
+        if len(f) < 9 or f[2] != "exon" or f[0] not in seqs:
+            continue
+        tid = f[8].split('transcript_id "')[1].split('"')[0]
+        tx.setdefault(tid, []).append((f[0], int(f[3]), int(f[4])))
+    spliced, premrna = [], []
+    for t, ex in sorted(tx.items()):
+        ex.sort(key=lambda e: e[1])
+        c = ex[0][0]
+        spliced.append((c, "".join(seqs[c][a - 1:b] for _, a, b in ex)))
+        premrna.append((c, seqs[c][ex[0][1] - 1:ex[-1][2]]))
+    names = list(seqs)
+
+    def mutate(s):
+        s = list(s)
+        for _ in range(rng.choice([0, 0, 0, 1, 2, 4])):
+            s[rng.randrange(len(s))] = rng.choice("ACGT")
+        return "".join(s)
+
+    def rand_seq(L):
+        return "".join(rng.choice("ACGT") for _ in range(L))
+
+    def frag(src, L0, L1, ins):
+        ins = max(ins, L0, L1)
+        if len(src) <= ins:
+            ins = len(src)
+        p = rng.randrange(0, len(src) - ins + 1)
+        f = src[p:p + ins]
+        if rng.random() < 0.5:
+            f = rc(f)
+        return f[:L0], rc(f[len(f) - L1:])
+
+    def genomic(L0, L1, ins):
+        c = rng.choice(names)
+        return frag(seqs[c], L0, L1, ins)
+
+    def gene_mate(L, pool=None):
+        c, sq = rng.choice(pool or spliced)
+        a, _ = frag(sq, L, L, L)
+        return c, a
+
+    pairs = []
+    for i in range(3000):
+        u = rng.random()
+        L0 = L1 = rng.choice([101, 101, 100, 100, 90, 75])
+        if u < 0.30:
+            a, b = frag(rng.choice(spliced)[1], L0, L1, rng.randrange(150, 450))
+        elif u < 0.45:
+            a, b = frag(rng.choice(premrna)[1], L0, L1, rng.randrange(150, 600))
+        elif u < 0.55:
+            a, b = genomic(L0, L1, rng.randrange(150, 700))
+        elif u < 0.65:   # chimera within one chromosome (two genes)
+            c0, a = gene_mate(L0)
+            same = [x for x in spliced if x[0] == c0]
+            _, b = gene_mate(L1, same)
+        elif u < 0.73:   # chimera across chromosomes
+            c0, a = gene_mate(L0)
+            other = [x for x in spliced if x[0] != c0] or spliced
+            _, b = gene_mate(L1, other)
+        elif u < 0.78:   # same orientation
+            a, b = frag(rng.choice(spliced + premrna)[1], L0, L1, rng.randrange(150, 400))
+            b = rc(b)
+        elif u < 0.86:   # one mate random
+            a, b = frag(rng.choice(spliced)[1], L0, L1, 300)
+            if rng.random() < 0.5:
+                a = rand_seq(L0)
+            else:
+                b = rand_seq(L1)
+        elif u < 0.89:
+            a, b = rand_seq(L0), rand_seq(L1)
+        elif u < 0.92:   # genomic pair far apart on one chromosome (past maxSpacing)
+            a, b = genomic(L0, L1, rng.randrange(1500, 20000))
+        elif u < 0.95:
+            a, b = frag(rng.choice(spliced)[1], L0, L1, 300)
+            if rng.random() < 0.5:
+                a = a[:rng.randrange(30, 60)]
+            else:
+                a = "".join("N" if rng.random() < 0.2 else ch for ch in a)
+        else:
+            a, b = frag(rng.choice(premrna)[1], L0, L1, rng.randrange(150, 400))
+        if rng.random() < 0.5:
+            a, b = b, a
+        a, b = mutate(a), mutate(b)
+        # small.fa's IUPAC codes: the FASTQ reader takes a record starting with one for garbage
+        # (FASTQ.cpp:241), so mates carry ACGTN only
+        a, b = ("".join(ch if ch in "ACGTN" else "A" for ch in x) for x in (a, b))
+        qa, qb = ["I"] * len(a), ["I"] * len(b)
+        r = rng.random()
+        if r < 0.05:
+            qa = [rng.choice("#+5?I") for _ in a]
+        elif r < 0.15:
+            for j in range(rng.randrange(1, 10)):
+                qb[-1 - j] = "#"
+        pairs.append((a, "".join(qa), b, "".join(qb)))
+    with open(path0, "w") as f0, open(path1, "w") as f1:
+        for i, (a, qa, b, qb) in enumerate(pairs):
+            f0.write(f"@rp{i}/1\n{a}\n+\n{qa}\n")
+            f1.write(f"@rp{i}/2\n{b}\n+\n{qb}\n")
+
+
+def rna_paired_fixtures(work):
+    """`snap-rna paired <genome> <transcriptome> <gtf> r1.fq r2.fq -t 1 -o out.sam` (the RNA
+    paired product path, PairedAligner.cpp:405-689; BaseAligner.cpp at -O0, see
+    oracle/Makefile.ref): the SAM file and the six read-count files GTFReader::WriteReadCounts
+    writes (GTFReader.cpp:1710-1772)."""
+    import gzip
+    rng = random.Random(83)
+    fa = os.path.join(HERE, "small.fa")
+    seqs, name = {}, None
+    for line in open(fa):
+        line = line.strip()
+        if line.startswith(">"):
+            name = line[1:].split()[0]
+            seqs[name] = []
+        else:
+            seqs[name].append(line.upper())
+    seqs = {k: "".join(v) for k, v in seqs.items()}
+    gtf = os.path.join(HERE, "small.gtf")
+    fq0, fq1 = os.path.join(HERE, "rna_1.fq"), os.path.join(HERE, "rna_2.fq")
+    rna_paired_reads(fq0, fq1, seqs, gtf, rng)
+    gidx = os.path.join(work, "gidx")
+    ref_index(fa, gidx)
+    twd = os.path.join(work, "tx")
+    os.makedirs(twd, exist_ok=True)
+    run([SNAP, "transcriptome", gtf, fa, "tidx", "-O1000"], cwd=twd)
+    # The reference segfaults at the end of a run in GTFReader::AnalyzeReadIntervals (the
+    # interval-clustering report, GTFReader.cpp:1774-1838 -- not restated here) once enough
+    # overlapping read-pair intervals accumulate.  So the pairs are aligned in blocks of
+    # RNA_BLOCK (each block is its own `snap-rna paired` run, SAM bodies concatenated, count
+    # files kept per block), and a pair whose block still crashes on its own is left out.
+    recs = [open(x).read().splitlines() for x in (fq0, fq1)]
+    n = len(recs[0]) // 4
+
+    def attempt(idx, d, extra=(), out="try"):
+        for k in range(2):
+            with open(os.path.join(d, f"{out}_{k}.fq"), "w") as f:
+                f.write("".join("\n".join(recs[k][4 * i:4 * i + 4]) + "\n" for i in idx))
+        r = subprocess.run([SNAP, "paired", gidx, os.path.join(twd, "tidx"), gtf, os.path.join(d, f"{out}_0.fq"),
+                            os.path.join(d, f"{out}_1.fq"), "-t", "1", "-o", os.path.join(d, f"{out}.sam")] + list(extra),
+                           capture_output=True, cwd=d)
+        return r.returncode == 0
+
+    drop = []
+    for c in range(0, n, RNA_BLOCK):
+        block = list(range(c, min(n, c + RNA_BLOCK)))
+        if not attempt(block, work):
+            drop += [i for i in block if not attempt([i], work)]
+    keep = [i for i in range(n) if i not in set(drop)]
+    for k, x in enumerate((fq0, fq1)):
+        with open(x, "w") as f:
+            f.write("".join("\n".join(recs[k][4 * i:4 * i + 4]) + "\n" for i in keep))
+    recs = [open(x).read().splitlines() for x in (fq0, fq1)]
+    n = len(recs[0]) // 4
+    if drop:
+        print("pairs left out (the reference crashes in AnalyzeReadIntervals):", drop)
+    for tag, extra in (("", []), ("_M", ["-M"])):
+        body, counts = [], []
+        for bi, c in enumerate(range(0, n, RNA_BLOCK)):
+            assert attempt(range(c, min(n, c + RNA_BLOCK)), work, extra, out=f"blk{tag}")
+            lines = open(os.path.join(work, f"blk{tag}.sam")).read().splitlines(keepends=True)
+            if bi == 0:
+                body += [l for l in lines if l.startswith("@")]
+            body += [l for l in lines if not l.startswith("@")]
+            for cf in COUNT_FILES:
+                counts.append(f"## block {bi} {cf}\n")
+                counts.append(open(os.path.join(work, f"blk{tag}.{cf}.counts.txt")).read())
+        with open(os.path.join(HERE, f"expected_rna_paired{tag}.sam.gz"), "wb") as dst:
+            dst.write(gzip.compress("".join(body).encode(), compresslevel=9, mtime=0))
+        if not tag:
+            with open(os.path.join(HERE, "expected_rna_paired.counts.txt"), "w") as dst:
+                dst.write("".join(counts))
+
+
 def main():
     work = tempfile.mkdtemp(prefix="golden_")
+    if "--only-rna-paired" in sys.argv:
+        rna_paired_fixtures(work)
+        shutil.rmtree(work, ignore_errors=True)
+        print("RNA paired product path fixtures written to", HERE)
+        return
     if "--only-mh1000" in sys.argv:
         multihit_alias_fixtures(work)
         shutil.rmtree(work, ignore_errors=True)

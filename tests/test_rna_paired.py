@@ -1,0 +1,100 @@
+"""The RNA paired-end product path: `snap-rna paired` rebuilt on the GPU.
+
+Fixtures (tests/golden/make_golden.py --only-rna-paired): the reference CLI's own outputs
+(`snap-rna paired <genome> <transcriptome> <gtf> rna_1.fq rna_2.fq -t 1`, BaseAligner.cpp built at
+-O0 -- oracle/Makefile.ref) on tests/golden/small.fa + small.gtf for 2,999 pairs aligned in blocks
+of 200 (the reference crashes at the end of larger runs in GTFReader::AnalyzeReadIntervals, which
+is not restated; one pair whose block crashes alone is left out): the SAM records (default and -M)
+and the six read-count files of every block.  Our run builds both indexes itself, aligns each
+block through snapgpu_rna_paired_align with fresh GTF counters and must write the same SAM
+records and count files byte for byte (the @PG line echoes a different command line)."""
+import gzip
+import os
+
+import numpy as np
+import pytest
+
+import snapgpu
+
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+BLOCK = 200
+COUNT_FILES = ("transcript_id", "transcript_name", "gene_id", "gene_name", "junction_id", "junction_name")
+
+
+def _expected_counts():
+    out, cur = {}, None
+    for line in open(os.path.join(G, "expected_rna_paired.counts.txt")):
+        if line.startswith("## block "):
+            _, _, b, name = line.split()
+            cur = (int(b), name)
+            out[cur] = ""
+        else:
+            out[cur] += line
+    return out
+
+
+def test_count_files_layout_matches_reference(tmp_path):
+    """GTFReader::WriteReadCounts' keys and order (transcripts and genes in id order, each gene's
+    introns by key, gene names merged) from the GTF model alone, with every counter at zero."""
+    gtf = snapgpu.Gtf.load(os.path.join(G, "small.gtf"))
+    gtf.write_counts(tmp_path / "z")
+    want = _expected_counts()
+    for name in COUNT_FILES:
+        got = open(tmp_path / f"z.{name}.counts.txt").read().splitlines()
+        exp = want[(0, name)].splitlines()
+        assert [l.split("\t")[0] for l in got] == [l.split("\t")[0] for l in exp], name
+        assert all(l.endswith("\t0") for l in got), name
+
+
+def _indexes(tmp_path):
+    gtf = snapgpu.Gtf.load(os.path.join(G, "small.gtf"))
+    gidx = snapgpu.GenomeIndex.build(snapgpu.Genome.from_fasta(os.path.join(G, "small.fa"), 500), 20, 4)
+    tfa = tmp_path / "transcriptome.fa"
+    gtf.write_transcriptome(gidx.genome_handle(), tfa)
+    tidx = snapgpu.GenomeIndex.build(snapgpu.Genome.from_fasta(tfa, 500), 20, 4)
+    return gtf, gidx, tidx
+
+
+def _fastq_block(path, b, dst):
+    lines = open(path).read().splitlines()
+    with open(dst, "w") as f:
+        f.write("\n".join(lines[4 * BLOCK * b:4 * BLOCK * (b + 1)]) + "\n")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("use_m,fixture", [(0, "expected_rna_paired.sam.gz"), (1, "expected_rna_paired_M.sam.gz")])
+def test_rna_paired_product_path_matches_reference(gpu_available, tmp_path, use_m, fixture):
+    gtf, gidx, tidx = _indexes(tmp_path)
+    pa = snapgpu.PairedAligner(gidx, device=0)   # paired CLI defaults (maxHits 16000, maxK 15, 8 seeds)
+    ta = snapgpu.BaseAligner(tidx, maxHitsToConsider=16000, maxK=15, maxSeedsToUse=8, extraSearchDepth=2)
+    n = sum(1 for _ in open(os.path.join(G, "rna_1.fq"))) // 4
+    body, counts = [], _expected_counts()
+    totals = dict(partialPairs=0, partialMatches=0, transcriptomeRecords=0, multiHits=0)
+    for b in range((n + BLOCK - 1) // BLOCK):
+        f0, f1 = tmp_path / "b_1.fq", tmp_path / "b_2.fq"
+        _fastq_block(os.path.join(G, "rna_1.fq"), b, f0)
+        _fastq_block(os.path.join(G, "rna_2.fq"), b, f1)
+        r0, r1 = snapgpu.Reads.from_fastq(f0), snapgpu.Reads.from_fastq(f1)
+        gtf.reset_counts()
+        sam = tmp_path / "b.sam"
+        res, st = snapgpu.rna_paired_align(pa, ta, gtf, r0, r1, sam, useM=use_m)
+        for k in totals:
+            totals[k] += st[k]
+        lines = open(sam).read().splitlines(keepends=True)
+        if b == 0:
+            body += [l for l in lines if l.startswith("@") and not l.startswith("@PG")]
+        body += [l for l in lines if not l.startswith("@")]
+        if not use_m:
+            gtf.write_counts(tmp_path / "c")
+            for name in COUNT_FILES:
+                got = open(tmp_path / f"c.{name}.counts.txt").read()
+                assert got == counts[(b, name)], f"block {b} {name}"
+    want = [l for l in gzip.open(os.path.join(G, fixture), "rt").read().splitlines(keepends=True)
+            if not l.startswith("@PG")]
+    got = "".join(body).splitlines(keepends=True)
+    assert len(got) == len(want)
+    bad = [i for i in range(len(want)) if got[i] != want[i]]
+    assert not bad, f"{len(bad)} SAM lines differ, first:\n got  {got[bad[0]]} want {want[bad[0]]}"
+    # the fixture exercises the filter's branches: transcriptome records, FindPartialMatches
+    # scans on the GPU, MultipleHits
+    assert totals["transcriptomeRecords"] > 100 and totals["partialPairs"] > 20 and totals["multiHits"] > 10, totals
