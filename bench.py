@@ -171,6 +171,51 @@ def paired_leg(args, idx, local, rank, cpus):
     return out
 
 
+def rna_leg(args, idx, local, build_threads):
+    """SURVEY.md 8(f) f4 (BASELINE configs[4] shape on this workload's genome): the RNA paired
+    product path (`snap-rna paired`: transcriptome multi-hit + chimeric genome aligners,
+    AlignmentFilter::Filter with the GPU seed census, GPU CIGARs, SAM lines, GTF read counts) on
+    a synthetic GTF (2,000 genes) and 2 x 150 bp pairs, host FASTQ batches in -> SAM lines out."""
+    import shutil
+    import tempfile
+    import snapgpu
+    from rna_synth import synth_rna_workload
+    work = tempfile.mkdtemp(prefix="snapgpu_rna_")
+    try:
+        t0 = time.time()
+        gtf_path, fq0, fq1, info = synth_rna_workload(idx.genome_handle(), work, n_pairs=args.rna_pairs)
+        gtf = snapgpu.Gtf.load(gtf_path)
+        tfa = os.path.join(work, "transcriptome.fa")
+        gtf.write_transcriptome(idx.genome_handle(), tfa)
+        tidx = snapgpu.GenomeIndex.build(snapgpu.Genome.from_fasta(tfa, 500), 20, build_threads)
+        t_prep = time.time() - t0
+        pa = snapgpu.PairedAligner(idx, device=local)
+        ta = snapgpu.BaseAligner(tidx, maxHitsToConsider=16000, maxK=15, maxSeedsToUse=8, extraSearchDepth=2,
+                                 device=local)
+        r0, r1 = snapgpu.Reads.from_fastq(fq0), snapgpu.Reads.from_fastq(fq1)
+        snapgpu.rna_paired_align(pa, ta, gtf, r0, r1)   # warm-up
+        ts, sts = [], []
+        for _ in range(3):
+            gtf.reset_counts()
+            c0 = time.perf_counter()
+            res, st = snapgpu.rna_paired_align(pa, ta, gtf, r0, r1)
+            ts.append(time.perf_counter() - c0)
+            sts.append(st)
+        k = int(np.argsort(ts)[1])
+        dt, st = ts[k], sts[k]
+        n = r0.n
+        return {"value": 2 * n / dt, "unit": "reads/s", "pairs_per_s": n / dt, "pairs": n, "ms_per_batch": dt * 1e3,
+                "read_len": 150, "workload": info, "transcriptome_bases": tidx.info()["nBases"],
+                "stage_ms": {x: round(st[x], 2) for x in ("alignMs", "filterMs", "seedMs", "cigarMs", "writeMs")},
+                "records": {x: st[x] for x in ("singleHits", "multiHits", "notFound", "transcriptomeRecords")},
+                "partial_pairs": st["partialPairs"], "partial_matches": st["partialMatches"],
+                "seed_runs": st["seedRuns"], "prep_s": round(t_prep, 1),
+                "boundary": "host FASTQ batches in -> SAM lines + read counters (snapgpu_rna_paired_align; "
+                            "lines formatted, not written to disk)"}
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
+
+
 def timed_steps(step, steps, dist, sync):
     """Barrier + sync on both sides of exactly `steps` steps; returns the max over ranks."""
     if dist:
@@ -203,6 +248,8 @@ def main():
     ap.add_argument("--resident-steps", type=int, default=5)
     ap.add_argument("--paired-pairs", type=int, default=500_000,
                     help="extras.paired: 2 x 101 bp pairs through the GPU ChimericPairedEndAligner (0: skip)")
+    ap.add_argument("--rna-pairs", type=int, default=100_000,
+                    help="extras.rna_paired: 2 x 150 bp pairs through the RNA paired product path (0: skip)")
     ap.add_argument("--mode", choices=("stream", "sync"), default="stream",
                     help="stream: submit every step, wait once (a streaming caller); sync: one blocking call per step")
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="reads timed on the CPU baseline")
@@ -395,6 +442,8 @@ def main():
             del sam, dev
             if args.paired_pairs:
                 extras["paired"] = paired_leg(args, idx, local, rank, cpus)
+            if args.rna_pairs:
+                extras["rna_paired"] = rna_leg(args, idx, local, build_threads)
         log(rank, "extras done")
         cpu = None
         parity = None

@@ -459,8 +459,9 @@ int snapgpu_gtf_splice_cigar(const snapgpu_gtf_t *gtf, const char *transcriptId,
  * and genome BaseAligner::AlignRead (two aligners, :270-276), AlignmentFilter::AddAlignment /
  * FilterSingle (AlignmentFilter.cpp:140-300) and SAMFormat::writeRead (SAM.cpp:978-1153:
  * GPU CIGARs, transcriptome records with insertSpliceJunctions) -- the SAM file `snap-rna single
- * <genome> <transcriptome> <gtf> <reads>` writes.  Not built: the contamination database (-x),
- * BAM / sorted output and the per-gene read-count files written after the run. */
+ * <genome> <transcriptome> <gtf> <reads>` writes, and the gene read counts FilterSingle records
+ * (snapgpu_gtf_write_counts writes the count files).  Not built: the contamination database (-x),
+ * BAM / sorted output. */
 typedef struct snapgpu_single_options {
     int32_t  clipping;               /* ReadClippingType, default 3 = ClipFrontAndBack (AlignerOptions.cpp:48) */
     uint32_t confDiff;               /* -c, default 2 */
@@ -484,7 +485,7 @@ typedef struct snapgpu_single_stats {   /* AlignerStats (AlignerStats.h:40-69) *
 /* reads: a FASTQ batch with ids (snapgpu_reads_from_fastq), clipped here.  samPath receives
  * the header and one line per read in input order. */
 int snapgpu_single_align(snapgpu_aligner_t *genomeAligner, snapgpu_aligner_t *transcriptomeAligner,
-                         const snapgpu_gtf_t *gtf, snapgpu_reads_t *reads, const snapgpu_single_options_t *opt,
+                         snapgpu_gtf_t *gtf, snapgpu_reads_t *reads, const snapgpu_single_options_t *opt,
                          const char *samPath, snapgpu_single_stats_t *stats);
 /* The index an aligner was created over (BaseAligner's GenomeIndex; getGenome for the SAM writer). */
 const snapgpu_index_t *snapgpu_aligner_index(const snapgpu_aligner_t *a);

@@ -313,7 +313,8 @@ extern "C" int snapgpu_reads_clip(snapgpu_reads_t *r, int clipping, uint32_t *fr
         setError("reads_clip: bad argument");
         return SNAPGPU_EINVAL;
     }
-    if (r->nUploads) {
+    const bool same = r->frontClipped ? clipping == r->clipping : clipping == 0;
+    if (r->nUploads && !same) {   // Read::clip returns early when the state is unchanged (Read.h:361-363)
         setError("reads_clip: the batch was already uploaded to a device; clip before uploading");
         return SNAPGPU_EINVAL;
     }

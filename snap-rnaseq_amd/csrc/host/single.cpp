@@ -25,6 +25,7 @@ const std::string &gtfTranscriptChr(const GtfTranscript *t);
 uint32_t gtfGenomicPosition(const GtfTranscript *t, uint32_t pos, uint32_t span);
 bool gtfSpliceCigar(const GtfTranscript *t, uint32_t pos, const std::vector<std::pair<uint32_t, char>> &tokens,
                     std::string &out);
+void gtfCountSingle(snapgpu_gtf_t *g, const std::string &transcriptId);
 }  // namespace snapgpu
 
 using namespace snapgpu;
@@ -53,13 +54,14 @@ struct Alignment {
     uint32_t location = 0;
     int direction = 0;
     int score = 0;
-    std::string rname;
+    std::string rname, transcriptId;
     uint32_t pos = 0;
     bool isTranscriptome = false;
     bool operator<(const Alignment &r) const { return score < r.score; }   // AlignmentFilter.cpp:55-57
 };
 
 struct FilterOut {
+    const std::string *countTranscript = nullptr;   // GTFReader::IncrementReadCount (:261, :291)
     int result = SNAPGPU_NOT_FOUND;
     uint32_t location = 0, tlocation = 0;
     int direction = 0, score = 0, mapq = 0;
@@ -68,7 +70,7 @@ struct FilterOut {
 
 struct Ctx {
     const Genome *genome, *transcriptome;
-    const snapgpu_gtf_t *gtf;
+    snapgpu_gtf_t *gtf;
     std::map<std::string, uint32_t> pieceByName;   // Genome::getOffsetOfPiece (Genome.cpp:317-345)
     uint32_t maxDist, confDiff;
 };
@@ -79,6 +81,7 @@ int addAlignment(const Ctx &C, std::map<std::string, Alignment> &mate0, uint32_t
     if (score > (int)C.maxDist) return -1;   // `score > maxDist`: unsigned comparison in the reference
     std::string rname = "*";
     uint32_t pos = 0;
+    std::string tid;
     if (location != kInvalidLocation) {
         const Genome &g = isTranscriptome ? *C.transcriptome : *C.genome;
         const int p = pieceAt(g, location);
@@ -88,6 +91,7 @@ int addAlignment(const Ctx &C, std::map<std::string, Alignment> &mate0, uint32_t
         if (isTranscriptome) {
             const GtfTranscript *t = gtfTranscript(C.gtf, rname);
             if (!t) { *err = "No transcript " + rname; return -2; }   // GTFReader::GetTranscript exits
+            tid = rname;
             rname = gtfTranscriptChr(t);
             pos = gtfGenomicPosition(t, pos, readLen);
         }
@@ -96,6 +100,7 @@ int addAlignment(const Ctx &C, std::map<std::string, Alignment> &mate0, uint32_t
     Alignment a;
     a.location = location; a.direction = direction; a.score = score; a.rname = rname; a.pos = pos;
     a.isTranscriptome = isTranscriptome;
+    a.transcriptId = tid;
     const std::string key = rname + '_' + std::to_string(pos);
     auto it = mate0.find(key);
     if (it == mate0.end()) mate0.insert({key, a});
@@ -105,7 +110,8 @@ int addAlignment(const Ctx &C, std::map<std::string, Alignment> &mate0, uint32_t
 }
 
 // AlignmentFilter::FilterSingle (AlignmentFilter.cpp:216-300)
-bool filterSingle(const Ctx &C, const std::map<std::string, Alignment> &mate0, FilterOut &o, std::string *err) {
+bool filterSingle(const Ctx &C, const std::map<std::string, Alignment> &mate0, FilterOut &o, std::string *err,
+                  std::string &countTranscript) {
     std::vector<Alignment> al;
     for (auto &m : mate0)
         if (!(m.second.score > (int)C.maxDist)) al.push_back(m.second);
@@ -127,6 +133,7 @@ bool filterSingle(const Ctx &C, const std::map<std::string, Alignment> &mate0, F
     if (al.size() == 1 || (uint32_t)(al[1].score - al[0].score) >= C.confDiff) {
         o.mapq = 70;   // min(maxMAPQ, genome_mapq), both 70
         o.result = SNAPGPU_SINGLE_HIT;
+        if (a.isTranscriptome) { countTranscript = a.transcriptId; o.countTranscript = &countTranscript; }
     } else {
         o.mapq = 1;
         o.result = SNAPGPU_MULTIPLE_HITS;
@@ -162,7 +169,7 @@ void snapgpu_single_options_default(snapgpu_single_options_t *o) {
     o->version = "";
 }
 
-int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, const snapgpu_gtf_t *gtf,
+int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_gtf_t *gtf,
                          snapgpu_reads_t *reads, const snapgpu_single_options_t *opt, const char *samPath,
                          snapgpu_single_stats_t *stats) {
     const auto w0 = std::chrono::steady_clock::now();
@@ -200,6 +207,7 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, const sna
     if (!ub) return SNAPGPU_ENOMEM;
     std::vector<snapgpu_result_t> tr(nu + 1), gr(nu + 1);
     std::vector<FilterOut> fo(nu + 1);
+    std::vector<std::string> countTid(nu + 1);
     std::vector<int32_t> ged(nu + 1, -1), ted(nu + 1, -1);
     std::vector<uint32_t> gn(nu + 1, 0), tn(nu + 1, 0), gops((nu + 1) * SNAPGPU_CIGAR_MAX_OPS),
         tops((nu + 1) * SNAPGPU_CIGAR_MAX_OPS);
@@ -223,10 +231,12 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, const sna
             // AlignmentFilter (AlignmentFilter.cpp:107-109); AddAlignment uses read1 = the read
             if (addAlignment(C, mate0, tr[j].location, tr[j].direction, tr[j].score, true, ul[j], &errs[t]) == -2) break;
             if (addAlignment(C, mate0, gr[j].location, gr[j].direction, gr[j].score, false, ul[j], &errs[t]) == -2) break;
-            if (!filterSingle(C, mate0, fo[j], &errs[t])) break;
+            if (!filterSingle(C, mate0, fo[j], &errs[t], countTid[j])) break;
         }
     });
     for (auto &e : errs) if (!e.empty()) { setError("single_align: " + e); return fail(SNAPGPU_EFORMAT); }
+    for (uint64_t j = 0; j < nu; j++)   // gene read counts (FilterSingle :260-262, :290-292)
+        if (fo[j].countTranscript) gtfCountSingle(gtf, *fo[j].countTranscript);
     st.filterMs = msSince(t0);
     // CIGARs on the GPU: genome records at the filter's location (NotFound keeps location 0 and
     // the forward read, SAM.cpp:1040-1048), transcriptome records on the transcriptome at tlocation

@@ -327,6 +327,11 @@ def single_fixtures(work):
         run([SNAP, "single", gidx, os.path.join(twd, "tidx"), gtf, fq, "-t", "1", "-o", out] + extra, cwd=work)
         with open(out, "rb") as src, open(os.path.join(HERE, f"expected_single{tag}.sam.gz"), "wb") as dst:
             dst.write(gzip.compress(src.read(), compresslevel=9, mtime=0))
+        if not tag:   # GTFReader::WriteReadCounts after the run (gene counts from FilterSingle)
+            with open(os.path.join(HERE, "expected_single.counts.txt"), "w") as dst:
+                for c in ("transcript_id", "transcript_name", "gene_id", "gene_name", "junction_id", "junction_name"):
+                    dst.write(f"## {c}\n")
+                    dst.write(open(os.path.join(work, f"out.{c}.counts.txt")).read())
 
 
 def paired_reads(path0, path1, seqs, rng):

@@ -73,3 +73,14 @@ def test_single_end_product_path_matches_reference(gpu_available, tmp_path, use_
     assert st["totalReads"] == reads.n and 0 < st["usefulReads"] < reads.n
     assert st["transcriptomeRecords"] > 50
     assert "N" in "".join(l.split("\t")[5] for l in g if not l.startswith("@"))   # junctions exercised
+    if not use_m:   # the gene read counts FilterSingle records, written as GTFReader::WriteReadCounts
+        gtf.write_counts(tmp_path / "out")
+        want, cur = {}, None
+        for line in open(os.path.join(G, "expected_single.counts.txt")):
+            if line.startswith("## "):
+                cur = line[3:].strip()
+                want[cur] = ""
+            else:
+                want[cur] += line
+        for name, text in want.items():
+            assert open(tmp_path / f"out.{name}.counts.txt").read() == text, name
