@@ -277,7 +277,9 @@ int snapgpu_align_batch_wait(snapgpu_aligner_t *a);
  *    GenomeIndex::lookupSeed, GenomeIndex.cpp:1013-1086, and BaseAligner.cpp:781-853);
  *  - multi-hit export (fillHitsFound, BaseAligner.cpp:940-975, recording at :1255-1261):
  *    up to maxHitsToGet hits with edit distance in [best, best+3] per read, written to
- *    multiHits[i * maxHitsToGet ..], their count to multiHitsFound[i].
+ *    multiHits[i * maxHitsToGet ..], their count to multiHitsFound[i]; entries past
+ *    multiHitsFound[i] in a read's row are left untouched (only the found hits are copied
+ *    back, compacted on the device).
  * search may be NULL (no window for any read); maxHitsToGet 0 disables multi-hit
  * export (multiHitsFound / multiHits may then be NULL); at most SNAPGPU_MAX_MULTI_HITS_TO_GET.
  * The reference keeps 512 hits per distance (BaseAligner.h:148-151) but counts up to
@@ -317,9 +319,10 @@ int  snapgpu_synchronize(snapgpu_aligner_t *a);
  * in chunks over two streams: the kernel figures are then sums over its nLaunches chunks. */
 typedef struct snapgpu_timing {
     double mainKernelMs;     /* pass 1: align_kernel<128> (reads <= 128 bases, bit-plane LV) */
-    double spillKernelMs;    /* pass 2: align_kernel<512> over the reads pass 1 deferred */
+    double spillKernelMs;    /* passes 2 + 3: align_kernel<256> over the reads pass 1 deferred
+                                (129..256 bases, bit-plane LV), align_kernel<512> over the rest */
     double fixupMs;          /* host MAPQ fix-ups */
-    uint64_t nSpilled;       /* reads deferred to pass 2 */
+    uint64_t nSpilled;       /* reads deferred by pass 1 */
     uint64_t nMapqFixed;
     double lookupKernelMs;   /* pass 0: seed_lookup_kernel (first-round seed lookups) */
     uint64_t lookupSeeds;    /* seeds it looked up */
@@ -329,6 +332,8 @@ typedef struct snapgpu_timing {
     double wallMs;           /* snapgpu_align_batch: host reads in -> records out, whole call */
     double mainKernelBusyMs; /* union of the pass-1 launch intervals (launches of the two lanes overlap) */
     double lookupKernelBusyMs;/* union of the pass-0 launch intervals */
+    uint64_t nByteReads;     /* reads deferred by pass 2 to the byte-compare pass 3 (> 256 bases,
+                                or IUPAC codes in both read and genome) */
 } snapgpu_timing_t;
 int snapgpu_last_timing(snapgpu_aligner_t *a, snapgpu_timing_t *t);
 
@@ -366,10 +371,12 @@ int snapgpu_lv_batch(int device, int direction, uint32_t n,
                      const uint32_t *patLen, const int32_t *k,
                      int32_t *outScore, int32_t *outNetIndel, double *outProb);
 
-/* The same calls through the production bit-plane LV of align_kernel<128> (lv_group /
+/* The same calls through the production bit-plane LV of align_kernel<128> / <256> (lv_group /
  * lv_prob_pair in align_score.h) instead of the byte-compare engine: unit parity for the LV
- * that scores every read of <= 128 bases.  Patterns of 1..127 bases; netIndel is reported
- * for direction -1 only (the aligner uses only the reverse call's, BaseAligner.cpp:1232). */
+ * that scores every read of <= 256 bases.  Patterns of 1..253 bases: a batch whose patterns
+ * are all <= 127 runs on 128-bit masks (align_kernel<128>), any longer pattern puts the whole
+ * batch on 256-bit masks (align_kernel<256>); netIndel is reported for direction -1 only
+ * (the aligner uses only the reverse call's, BaseAligner.cpp:1232). */
 int snapgpu_lv_group_batch(int device, int direction, uint32_t n,
                            const char *texts, const uint64_t *textOff, const uint32_t *textLen,
                            const char *patterns, const char *quals, const uint64_t *patOff,

@@ -60,7 +60,8 @@ static __device__ DevTables g_tab;   // per translation unit (aligner.hip, paire
 
 // HashTableElement (BaseAligner.h:188-214) in the HBM arena: a 48-byte header of
 // the fields the kernels read and write, then the per-candidate seed offsets.  Reads
-// of <= 128 bases keep u8 offsets (96-B elements); the byte path keeps u16 (144 B).
+// of <= 256 bases (the bit-plane kernels) keep u8 offsets (96-B elements); the byte
+// path keeps u16 (144 B).
 template <typename OffT>
 struct ElemT {
     uint64_t used;            // candidatesUsed
@@ -80,6 +81,7 @@ using Elem512 = ElemT<uint16_t>;
 static_assert(sizeof(Elem128) == 96 && sizeof(Elem512) == 144, "Elem layout");
 template <int MAXLEN> struct ElemSel { using type = Elem512; };
 template <> struct ElemSel<128> { using type = Elem128; };
+template <> struct ElemSel<256> { using type = Elem128; };
 template <int MAXLEN> using ElemOf = typename ElemSel<MAXLEN>::type;
 
 struct KArgs {
@@ -227,9 +229,11 @@ constexpr int EB = 8;                    // elements popped per batch (forced mo
 constexpr int CANDCAP = EB * ELEM;       // candidate list capacity
 constexpr uint32_t ORDCAP = 256;         // forced-mode pop order (u16)
 
-// Scorer state of align_kernel<128> (align_score.h).
-struct GroupLds {
-    uint64_t rpl[2][3][2];               // read[dir] bit planes {hi, lo, notACGT}, positions 0..127
+// Scorer state of the bit-plane kernels align_kernel<128> / <256> (align_score.h); NW =
+// 64-position words of the read masks.
+template <int NW>
+struct GroupLdsT {
+    uint64_t rpl[2][3][NW];              // read[dir] bit planes {hi, lo, notACGT}, positions 0..64*NW-1
     uint32_t ecache[EB][24];             // popped Elem128s (authoritative while in the batch)
     uint32_t eidx[EB];
     uint16_t cand[CANDCAP];              // slot << 8 | bit
@@ -238,11 +242,13 @@ struct GroupLds {
     int16_t pL0[2][8];                   //   exact prefix L[0][0] per group
     int8_t plen[2][8];                   //   path length (0: exact match, prob = perfect[patternLen])
 };
+using GroupLds = GroupLdsT<2>;
 
 template <int MAXLEN>
 struct Lds {
     static constexpr int NB = MAXLEN / 64;          // 64-position blocks
-    static constexpr bool BYTE_PATH = MAXLEN > 128; // byte-compare LV (align_device.h) vs bit planes
+    static constexpr bool BYTE_PATH = MAXLEN > 256; // byte-compare LV (align_device.h) vs bit planes
+    static constexpr int NW = BYTE_PATH ? 1 : NB;   // bit-plane mask words
     char fwd[MAXLEN + 64];                          // read[FORWARD], zero slack
     char rc[MAXLEN + 64];                           // read[RC]
     char fwdQ[MAXLEN + 64];
@@ -274,7 +280,7 @@ struct Lds {
     int16_t btAct[BYTE_PATH ? MAX_K + 1 : 1];       // LV backtrace scratch (byte path)
     int16_t btMatched[BYTE_PATH ? MAX_K + 1 : 1];
     uint16_t rows[BYTE_PATH ? MAX_K : 1][WAVE];     // byte-path LV rows: (L+2) | action<<12
-    GroupLds grp[BYTE_PATH ? 0 : 1];                // scorer of align_kernel<128>
+    GroupLdsT<NW> grp[BYTE_PATH ? 0 : 1];           // scorer of align_kernel<128> / <256>
 };
 
 // ------------------------------------------------------------ LV engine

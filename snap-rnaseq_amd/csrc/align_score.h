@@ -1,4 +1,5 @@
-// align_score.h -- BaseAligner::score (BaseAligner.cpp:977-1399) for align_kernel<128>.
+// align_score.h -- BaseAligner::score (BaseAligner.cpp:977-1399) for the bit-plane kernels
+// align_kernel<128> (reads <= 128 bases) and align_kernel<256> (129..256 bases).
 //
 // Batching.  The reference scores one candidate at a time and scoreLimit shrinks as
 // better hits appear.  Landau-Vishkin with limit k' returns exactly what it returns
@@ -18,7 +19,7 @@
 //
 // One pass scores G = 64/GS candidates, one lane group of GS lanes each (GS = 16
 // for k <= 7, 32 for k <= 15, else 64).  Lane `li` of a group holds diagonal
-// x = li - (GS/2-1) as a 128-bit mismatch mask in registers,
+// x = li - (GS/2-1) as a 64*NW-bit mismatch mask in registers (NW = 2 or 4),
 //   F_x[m] = read[dir][m] != genome[loc + x + m],
 // built from the genome's bit planes (hi, lo, notACGT; 32 bases per dword) with
 // funnel shifts; both the forward and the reverse LV read it.  Byte-exact: a base
@@ -29,17 +30,24 @@
 
 namespace sgk {
 
-// ------------------------------------------------------------ 128-bit masks
-// Bit m of a mask = mismatch at read position m.  The reverse LV scans the read
-// backwards, so it runs on the bit-reversed mask R[m'] = F[127 - m'] and both
-// directions only need "first set bit at or after m0" (positions >= 128 count as
+// ------------------------------------------------------------ read-length masks
+// Bit m of a mask = mismatch at read position m (NW 64-bit words: 128 positions for
+// align_kernel<128>, 256 for align_kernel<256>).  The reverse LV scans the read
+// backwards, so it runs on the bit-reversed mask R[m'] = F[NBITS-1 - m'] and both
+// directions only need "first set bit at or after m0" (positions >= NBITS count as
 // set, which is "before position 0" for R).
-struct Mask128 { uint64_t lo, hi; };
+template <int NW>
+struct MaskW { uint64_t w[NW]; };
+using Mask128 = MaskW<2>;
 
-__device__ __forceinline__ Mask128 mk_reverse(const Mask128 &F) {
-    Mask128 R;
-    R.lo = ((uint64_t)__builtin_bitreverse32((uint32_t)F.hi) << 32) | __builtin_bitreverse32((uint32_t)(F.hi >> 32));
-    R.hi = ((uint64_t)__builtin_bitreverse32((uint32_t)F.lo) << 32) | __builtin_bitreverse32((uint32_t)(F.lo >> 32));
+__device__ __forceinline__ uint64_t brev64(uint64_t x) {
+    return ((uint64_t)__builtin_bitreverse32((uint32_t)x) << 32) | __builtin_bitreverse32((uint32_t)(x >> 32));
+}
+template <int NW>
+__device__ __forceinline__ MaskW<NW> mk_reverse(const MaskW<NW> &F) {
+    MaskW<NW> R;
+#pragma unroll
+    for (int j = 0; j < NW; j++) R.w[j] = brev64(F.w[NW - 1 - j]);
     return R;
 }
 // v_ffbl_b32: index of the lowest set bit, 0xffffffff for 0
@@ -48,20 +56,52 @@ __device__ __forceinline__ uint32_t ffbl(uint32_t x) {
     asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
     return r;
 }
-// 64 + first set bit of F.hi (128 if none): the "not in the lower word" answer of mk_first
-__device__ __forceinline__ int mk_hi_first(const Mask128 &F) {
-    const uint32_t a = ffbl((uint32_t)F.hi), b = ffbl((uint32_t)(F.hi >> 32)) | 32u;
-    const uint32_t r = a < b ? a : b;
-    return r < 64u ? 64 + (int)r : 128;
-}
-// first set position >= m0, m0 in [0, 128]; 128 if none (hf = mk_hi_first(F)).  Branch-free:
-// one 64-bit shift of the word holding m0 (OR-ing 32 keeps ffbl's 0xffffffff "none").
-__device__ __forceinline__ int mk_first(const Mask128 &F, int hf, int m0) {
-    const bool hw = m0 >= 64;
-    const uint64_t x = (hw ? F.hi : F.lo) >> (m0 & 63);
+// lowest set bit of a 64-bit word, >= 64 (not exactly 64) for 0
+__device__ __forceinline__ uint32_t ffb64(uint64_t x) {
     const uint32_t a = ffbl((uint32_t)x), b = ffbl((uint32_t)(x >> 32)) | 32u;
-    const int v = x != 0 ? m0 + (int)(a < b ? a : b) : (hw ? 128 : hf);
-    return v < 128 ? v : 128;
+    return a < b ? a : b;
+}
+// "Not in the word holding m0" answers of mk_first: sfx.s[j] = first set position in words
+// j..NW-1 (NBITS if none), for j = 1..NW-1.
+template <int NW>
+struct MaskSfx { int s[NW]; };
+template <int NW>
+__device__ __forceinline__ MaskSfx<NW> mk_suffix(const MaskW<NW> &F) {
+    MaskSfx<NW> x;
+    int acc = 64 * NW;
+#pragma unroll
+    for (int j = NW - 1; j >= 1; j--) {
+        const uint32_t r = ffb64(F.w[j]);
+        acc = r < 64u ? 64 * j + (int)r : acc;
+        x.s[j] = acc;
+    }
+    x.s[0] = 0;
+    return x;
+}
+// first set position >= m0, m0 in [0, NBITS]; NBITS if none.  Branch-free: one 64-bit shift of
+// the word holding m0 (OR-ing 32 keeps ffbl's 0xffffffff "none").
+template <int NW>
+__device__ __forceinline__ int mk_first(const MaskW<NW> &F, const MaskSfx<NW> &sf, int m0) {
+    constexpr int NBITS = 64 * NW;
+    if constexpr (NW == 2) {
+        const bool hw = m0 >= 64;
+        const uint64_t x = (hw ? F.w[1] : F.w[0]) >> (m0 & 63);
+        const uint32_t a = ffbl((uint32_t)x), b = ffbl((uint32_t)(x >> 32)) | 32u;
+        const int v = x != 0 ? m0 + (int)(a < b ? a : b) : (hw ? NBITS : sf.s[1]);
+        return v < NBITS ? v : NBITS;
+    } else {
+        const int wi = m0 >> 6;
+        uint64_t x = F.w[0];
+        int nxt = sf.s[1];
+#pragma unroll
+        for (int j = 1; j < NW; j++) {
+            x = wi >= j ? F.w[j] : x;
+            nxt = wi >= j ? (j + 1 < NW ? sf.s[j + 1 < NW ? j + 1 : j] : NBITS) : nxt;
+        }
+        x >>= (m0 & 63);
+        const int v = x != 0 ? m0 + (int)ffb64(x) : nxt;
+        return v < NBITS ? v : NBITS;
+    }
 }
 
 // ------------------------------------------------------------ group shifts
@@ -98,9 +138,10 @@ __device__ __forceinline__ int from_upper_b(int v, bool glast) {
 // distance or -1.  A group that succeeds records its backtrace (LandauVishkin.h:
 // 376-431) in G.pa / G.pm / G.pL0 / G.plen[dx]; the match probability is formed
 // later, only for candidates the scorer applies (lv_prob).
-template <int DIR, int GS>
-__device__ __forceinline__ int lv_group(GroupLds &G, uint8_t (*rows8)[WAVE], const Mask128 &M, bool gact, int q0, int patternLen,
-                                        int textLen, int k, int kmaxAll, int &outE) {
+template <int DIR, int GS, int NW>
+__device__ __forceinline__ int lv_group(GroupLdsT<NW> &G, uint8_t (*rows8)[WAVE], const MaskW<NW> &M, bool gact, int q0,
+                                        int patternLen, int textLen, int k, int kmaxAll, int &outE) {
+    constexpr int NBITS = 64 * NW;
     constexpr int dx = DIR > 0 ? 0 : 1;
     const int lane = lane_id();
     const int li = lane & (GS - 1), gi = lane / GS, c = GS / 2 - 1;
@@ -111,7 +152,7 @@ __device__ __forceinline__ int lv_group(GroupLds &G, uint8_t (*rows8)[WAVE], con
     outE = -1;
     uint32_t done = gact ? 0u : 1u;   // a VGPR flag: ballot(done == 0) is one v_cmp
     const int end0 = patternLen < textLen ? patternLen : textLen;
-    const int hf = mk_hi_first(M);
+    const MaskSfx<NW> hf = mk_suffix(M);
     const int fm = mk_first(M, hf, q0) - q0;
     const int v0 = fm < end0 ? fm : end0;
     const int L0 = shfl_idx(v0, gi * GS + c);           // exact prefix on diagonal 0
@@ -140,8 +181,8 @@ __device__ __forceinline__ int lv_group(GroupLds &G, uint8_t (*rows8)[WAVE], con
         const bool active = !done && d <= e && d >= -e;
         // slide along the diagonal (LandauVishkin.h:325-354)
         const int mpos = q0m2 + bestB;
-        const int mposc = mpos < 128 ? mpos : 128;
-        const int fa = mk_first(M, hf, mposc);             // fa == mposc <=> mismatch at mpos (or past 127)
+        const int mposc = mpos < NBITS ? mpos : NBITS;
+        const int fa = mk_first(M, hf, mposc);             // fa == mposc <=> mismatch at mpos (or past NBITS-1)
         const int fB = fa - q0m2;
         const int slidB = fB < enddB ? fB : enddB;
         const int bnewB = bestB < enddB ? slidB : (fa == mposc ? bestB : enddB);
@@ -219,7 +260,8 @@ __device__ __forceinline__ int lv_group(GroupLds &G, uint8_t (*rows8)[WAVE], con
 // factor indel[cnt], X steps one phred factor each at offset L0 + sum of earlier
 // steps' (+-1 + matched).  Factors are fetched in parallel and multiplied in the
 // reference's order (x * 1.0 == x, so steps without a factor multiply by 1.0).
-__device__ __forceinline__ void lv_prob_pair(const DevTables *tab, const GroupLds &G, int g, int pbase, int n, int s0,
+template <int NW>
+__device__ __forceinline__ void lv_prob_pair(const DevTables *tab, const GroupLdsT<NW> &G, int g, int pbase, int n, int s0,
                                              int t0, const char *qual, double &p1, double &p2, int &net2) {
     const int lane = lane_id();
     const int dx = lane >> 5, j = (lane & 31) + 1;               // step j of direction dx
@@ -289,10 +331,11 @@ struct PassLane {
 };
 
 // One speculative pass over up to G = 64/GS candidates [i0, i0+m) of the list.
-template <int GS>
-__device__ __forceinline__ void lv_pass(const KArgs &A, Lds<128> &S, uint32_t i0, int m, int k, uint32_t n,
+template <int GS, int MAXLEN>
+__device__ __forceinline__ void lv_pass(const KArgs &A, Lds<MAXLEN> &S, uint32_t i0, int m, int k, uint32_t n,
                                         PassLane &P, int &e1, int &e2) {
-    GroupLds &G = S.grp[0];
+    constexpr int NW = Lds<MAXLEN>::NW;
+    GroupLdsT<NW> &G = S.grp[0];
     const int lane = lane_id();
     const int gi = lane / GS, li = lane & (GS - 1), c = GS / 2 - 1;
     PH_T(A, tst);
@@ -324,34 +367,36 @@ __device__ __forceinline__ void lv_pass(const KArgs &A, Lds<128> &S, uint32_t i0
         P.glen = (int)glen;
         P.act = ok;
     }
-    // F_x from the genome bit planes: positions loc + x + [0, 128)
-    Mask128 F;
+    // F_x from the genome bit planes: positions loc + x + [0, 64*NW)
+    MaskW<NW> F;
     {
         const int64_t gp = (int64_t)P.loc + (li - c) + PACK_GUARD;
         const uint4 *src = A.gpl + (gp >> 5);
         const uint32_t sh = (uint32_t)gp & 31;
-        uint4 w[5];
+        uint4 w[2 * NW + 1];
 #pragma unroll
-        for (int j = 0; j < 5; j++) w[j] = src[j];
+        for (int j = 0; j < 2 * NW + 1; j++) w[j] = src[j];
         const uint64_t *rp = &G.rpl[P.dir][0][0];
-        const uint64_t rh0 = rp[0], rh1 = rp[1], rl0 = rp[2], rl1 = rp[3], rm0 = rp[4], rm1 = rp[5];
-        uint32_t f[4];
+        uint64_t RHw[NW], RLw[NW], RMw[NW];
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
+        for (int j = 0; j < NW; j++) { RHw[j] = rp[j]; RLw[j] = rp[NW + j]; RMw[j] = rp[2 * NW + j]; }
+        uint32_t f[2 * NW];
+#pragma unroll
+        for (int j = 0; j < 2 * NW; j++) {
             const uint32_t gh = __builtin_amdgcn_alignbit(w[j + 1].x, w[j].x, sh);
             const uint32_t gl = __builtin_amdgcn_alignbit(w[j + 1].y, w[j].y, sh);
             const uint32_t gm = __builtin_amdgcn_alignbit(w[j + 1].z, w[j].z, sh);
-            const uint64_t RH = j < 2 ? rh0 : rh1, RL = j < 2 ? rl0 : rl1, RM = j < 2 ? rm0 : rm1;
+            const uint64_t RH = RHw[j / 2], RL = RLw[j / 2], RM = RMw[j / 2];
             const uint32_t sft = 32 * (j & 1);
             f[j] = (gh ^ (uint32_t)(RH >> sft)) | (gl ^ (uint32_t)(RL >> sft)) | gm | (uint32_t)(RM >> sft);
         }
-        F.lo = ((uint64_t)f[1] << 32) | f[0];
-        F.hi = ((uint64_t)f[3] << 32) | f[2];
+#pragma unroll
+        for (int j = 0; j < NW; j++) F.w[j] = ((uint64_t)f[2 * j + 1] << 32) | f[2 * j];
     }
     PH_ADD(A, S, PH_STAGE, tst);
     PH_T(A, tf);
     const int t = P.s + (int)A.seedLen;
-    const int rf = lv_group<1, GS>(G, S.u.sc.rows8, F, P.act, t, (int)n - t, P.glen - t, k, k, e1);
+    const int rf = lv_group<1, GS, NW>(G, S.u.sc.rows8, F, P.act, t, (int)n - t, P.glen - t, k, k, e1);
     PH_ADD(A, S, PH_LVF, tf);
     PH_CNT(A, S, PH_ROWSF, rf);
     PH_CNT(A, S, GS <= 16 ? PH_NPASS16 : (GS == 32 ? PH_NPASS32 : PH_NPASS64), 1);
@@ -362,8 +407,9 @@ __device__ __forceinline__ void lv_pass(const KArgs &A, Lds<128> &S, uint32_t i0
     e2 = -1;
     if (kmax2 >= 0) {
         // reverse LV: pattern = read[s-1 .. 0], text = genome backwards from loc+s-1 (BaseAligner.cpp:1216-1220)
-        const Mask128 R = mk_reverse(F);
-        const int rr = lv_group<-1, GS>(G, S.u.sc.rows8, R, ract, 127 - (P.s - 1), P.s, P.s + MAX_K, k2, kmax2, e2);
+        const MaskW<NW> R = mk_reverse(F);
+        const int rr = lv_group<-1, GS, NW>(G, S.u.sc.rows8, R, ract, 64 * NW - 1 - (P.s - 1), P.s, P.s + MAX_K, k2,
+                                            kmax2, e2);
         PH_CNT(A, S, PH_ROWSR, rr);
     }
     PH_ADD(A, S, PH_LVR, tr);
@@ -373,16 +419,16 @@ __device__ __forceinline__ void lv_pass(const KArgs &A, Lds<128> &S, uint32_t i0
 // order (BaseAligner.cpp:1129-1384).  Returns true when the read is finished
 // (stopOnFirstHit).  GS is a template parameter so group indexing is shifts and the
 // per-group loops unroll.
-template <int GS, bool EXT>
-__device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<128> &S, Elem128 *ar, ReadState &st, uint32_t i0, int m,
+template <int GS, bool EXT, int MAXLEN>
+__device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem128 *ar, ReadState &st, uint32_t i0, int m,
                                            int k, uint32_t n, uint32_t nb, uint32_t &lastSlot, bool &lastSkip,
                                            int *result) {
     const int lane = lane_id();
-    GroupLds &G = S.grp[0];
+    auto &G = S.grp[0];
     const DevTables *tab = A.tab;
     PassLane P;
     int e1, e2;
-    lv_pass<GS>(A, S, i0, m, k, n, P, e1, e2);
+    lv_pass<GS, MAXLEN>(A, S, i0, m, k, n, P, e1, e2);
     PH_T(A, tapp);
     // ---- apply in order with the limit in force at each candidate.  Group
     // leaders (lane g*GS) hold candidate g.  A failure only sets its scored bit
@@ -525,11 +571,11 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<128> &S, Elem128 
 }
 
 // BaseAligner::score (BaseAligner.cpp:977-1399) over batches of popped elements.
-template <bool EXT>
-__device__ __forceinline__ bool score_batched(const KArgs &A, Lds<128> &S, Elem128 *ar, ReadState &st, bool force,
+template <bool EXT, int MAXLEN>
+__device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, Elem128 *ar, ReadState &st, bool force,
                                            uint32_t n, int *result, uint32_t *flags) {
     const int lane = lane_id();
-    GroupLds &G = S.grp[0];
+    auto &G = S.grp[0];
     const DevTables *tab = A.tab;
     for (int d = 0; d < 2; d++)
         if (st.mostSeeds[d]) {

@@ -341,13 +341,13 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
     st.t0 = __builtin_amdgcn_s_memrealtime();
     st.tick = 32;
     st.nSeedsApplied[0] = st.nSeedsApplied[1] = 0;
-    uint32_t flags = MAXLEN > 128 ? SNAPGPU_FLAG_DEFERRED : 0u;   // pass 2 aligns only deferred reads
+    uint32_t flags = MAXLEN > 128 ? SNAPGPU_FLAG_DEFERRED : 0u;   // passes 2 and 3 align only deferred reads
     int result = SNAPGPU_NOT_FOUND;
     const uint32_t maxSeeds = A.maxSeedsCmd ? A.maxSeedsCmd : (uint32_t)(int)(A.seedCoverage * n / seedLen);
     const uint32_t numWeightLists = maxSeeds + 1;
     bool run = true;
-    if constexpr (MAXLEN == 128) {
-        if (n > 128) { defer_read(A, r); return; }
+    if constexpr (!Lds<MAXLEN>::BYTE_PATH) {   // bit-plane kernels: longer reads go on to the next pass
+        if (n > (uint32_t)MAXLEN) { defer_read(A, r); return; }
     }
     // search window (BaseAligner.cpp:596-602); multiHitsFound = 0 up front (:586-590)
     uint32_t radius = 0, sDir = 0, minLoc = 0, maxLoc = INVALID;
@@ -386,7 +386,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
             nN += __popcll(ballot(i < (int)n && c == 'N'));
             other |= ballot(i < (int)n && c != 'A' && c != 'C' && c != 'G' && c != 'T' && c != 'N') != 0;
         }
-        if constexpr (MAXLEN == 128) {
+        if constexpr (!Lds<MAXLEN>::BYTE_PATH) {
             // bit planes compare bytes exactly unless both the read and the genome hold
             // non-ACGTN bytes (an IUPAC code could then match itself): byte path
             if (A.hasIupac && other) { defer_read(A, r); return; }
@@ -404,7 +404,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
 #pragma unroll
             for (int dr = 0; dr < 2; dr++)
 #pragma unroll
-                for (int h = 0; h < 2; h++) {
+                for (int h = 0; h < NB; h++) {
                     const uint32_t code = packed_code((uint8_t)(dr ? S.rc : S.fwd)[h * 64 + lane]);
                     const uint64_t bh = ballot(code < 4 && (code & 2)), bl = ballot(code < 4 && (code & 1));
                     const uint64_t bm = ballot(code > 3);
@@ -594,7 +594,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
             bool fin;
             if constexpr (Lds<MAXLEN>::BYTE_PATH) fin = score_wave<MAXLEN, EXT>(A, S, ar, st, force, n, rbF, rbR, &result, &flags);
             else {
-                fin = score_batched<EXT>(A, S, ar, st, force, n, &result, &flags);
+                fin = score_batched<EXT, MAXLEN>(A, S, ar, st, force, n, &result, &flags);
                 if (!fin && !force) {   // the scorer's LV rows overlay the insertion table
                     for (int i = lane; i < BT; i += WAVE) { S.u.ins.btKey[i] = NONE; S.u.ins.btMask[i] = 0; }
                     wave_sync();
@@ -640,7 +640,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
 template <int MAXLEN, bool EXT>
 // amdgpu_waves_per_eu(3): keep <= 168 VGPRs (3 waves/SIMD, 12 per CU); a few cold spills
 // are cheaper than dropping to 2 waves/SIMD.
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MAXLEN == 128 ? 4 : 3))) void align_kernel(KArgs A) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MAXLEN <= 256 ? 4 : 3))) void align_kernel(KArgs A) {
     __shared__ Lds<MAXLEN> S;
     ElemOf<MAXLEN> *ar = reinterpret_cast<ElemOf<MAXLEN> *>(A.arena) + (uint64_t)blockIdx.x * A.arenaElems;
     const int lane = lane_id();
@@ -700,20 +700,22 @@ struct LvgTask {
     int32_t pl, tl, k, dir;
 };
 
-template <int GS, int DIR>
-__device__ __forceinline__ void lvg_run(Lds<128> &S, const LvgTask &T, const char *pats, const char *texts,
+template <int GS, int DIR, int NW>
+__device__ __forceinline__ void lvg_run(Lds<64 * NW> &S, const LvgTask &T, const char *pats, const char *texts,
                                         int32_t *outScore, int32_t *outNet, double *outProb) {
-    GroupLds &G = S.grp[0];
+    auto &G = S.grp[0];
     const int lane = lane_id();
     const int li = lane & (GS - 1), gi = lane / GS, c = GS / 2 - 1;
     const bool act = gi == 0;
     const int pl = T.pl, tl = T.tl;
     // F_x[m] = read[m] != genome[loc + x + m], x = li - c; mismatch past the read or the text
-    Mask128 F;
-    uint32_t f[4] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+    MaskW<NW> F;
+    uint32_t f[2 * NW];
+#pragma unroll
+    for (int j = 0; j < 2 * NW; j++) f[j] = 0xffffffffu;
     if (act) {
         const int x = li - c;
-        for (int m = 0; m < 128; m++) {
+        for (int m = 0; m < 64 * NW; m++) {
             bool mm = true;
             if (m < pl) {
                 const char r = DIR > 0 ? pats[T.pOff + m] : pats[T.pOff + pl - 1 - m];
@@ -727,11 +729,11 @@ __device__ __forceinline__ void lvg_run(Lds<128> &S, const LvgTask &T, const cha
             if (!mm) f[m >> 5] &= ~(1u << (m & 31));
         }
     }
-    F.lo = ((uint64_t)f[1] << 32) | f[0];
-    F.hi = ((uint64_t)f[3] << 32) | f[2];
+#pragma unroll
+    for (int j = 0; j < NW; j++) F.w[j] = ((uint64_t)f[2 * j + 1] << 32) | f[2 * j];
     int e = -1;
-    if (DIR > 0) lv_group<1, GS>(G, S.u.sc.rows8, F, act, 0, pl, tl, T.k, T.k, e);
-    else lv_group<-1, GS>(G, S.u.sc.rows8, mk_reverse(F), act, 127 - (pl - 1), pl, tl, T.k, T.k, e);
+    if (DIR > 0) lv_group<1, GS, NW>(G, S.u.sc.rows8, F, act, 0, pl, tl, T.k, T.k, e);
+    else lv_group<-1, GS, NW>(G, S.u.sc.rows8, mk_reverse(F), act, 64 * NW - 1 - (pl - 1), pl, tl, T.k, T.k, e);
     e = readlane(e, 0);
     wave_sync();
     double p1 = 1.0, p2 = 1.0;
@@ -749,28 +751,29 @@ __device__ __forceinline__ void lvg_run(Lds<128> &S, const LvgTask &T, const cha
     }
 }
 
+template <int NW>
 __global__ __launch_bounds__(64) void lv_group_kernel(const LvgTask *tasks, const char *pats, const char *quals,
                                                       const char *texts, int32_t *outScore, int32_t *outNet,
                                                       double *outProb) {
-    __shared__ Lds<128> S;
+    __shared__ Lds<64 * NW> S;
     const int lane = lane_id();
     const LvgTask T = tasks[blockIdx.x];
     // qualities in read coordinates (reverse: read[m] = pattern[pl-1-m])
-    for (int m = lane; m < 128 + 64; m += WAVE)
+    for (int m = lane; m < 64 * NW + 64; m += WAVE)
         S.fwdQ[m] = m < T.pl ? (T.dir > 0 ? quals[T.pOff + m] : quals[T.pOff + T.pl - 1 - m]) : 0;
     wave_sync();
     const int k = T.k < MAX_K - 1 ? T.k : MAX_K - 1;
     const int GS = k <= 3 ? 8 : (k <= 7 ? 16 : (k <= 15 ? 32 : 64));   // score_batched's choice
     if (T.dir > 0) {
-        if (GS == 8) lvg_run<8, 1>(S, T, pats, texts, outScore, outNet, outProb);
-        else if (GS == 16) lvg_run<16, 1>(S, T, pats, texts, outScore, outNet, outProb);
-        else if (GS == 32) lvg_run<32, 1>(S, T, pats, texts, outScore, outNet, outProb);
-        else lvg_run<64, 1>(S, T, pats, texts, outScore, outNet, outProb);
+        if (GS == 8) lvg_run<8, 1, NW>(S, T, pats, texts, outScore, outNet, outProb);
+        else if (GS == 16) lvg_run<16, 1, NW>(S, T, pats, texts, outScore, outNet, outProb);
+        else if (GS == 32) lvg_run<32, 1, NW>(S, T, pats, texts, outScore, outNet, outProb);
+        else lvg_run<64, 1, NW>(S, T, pats, texts, outScore, outNet, outProb);
     } else {
-        if (GS == 8) lvg_run<8, -1>(S, T, pats, texts, outScore, outNet, outProb);
-        else if (GS == 16) lvg_run<16, -1>(S, T, pats, texts, outScore, outNet, outProb);
-        else if (GS == 32) lvg_run<32, -1>(S, T, pats, texts, outScore, outNet, outProb);
-        else lvg_run<64, -1>(S, T, pats, texts, outScore, outNet, outProb);
+        if (GS == 8) lvg_run<8, -1, NW>(S, T, pats, texts, outScore, outNet, outProb);
+        else if (GS == 16) lvg_run<16, -1, NW>(S, T, pats, texts, outScore, outNet, outProb);
+        else if (GS == 32) lvg_run<32, -1, NW>(S, T, pats, texts, outScore, outNet, outProb);
+        else lvg_run<64, -1, NW>(S, T, pats, texts, outScore, outNet, outProb);
     }
 }
 
@@ -942,7 +945,7 @@ struct snapgpu_aligner {
     uint64_t nextLane = 0;
     std::chrono::steady_clock::time_point streamStart;
     uint64_t arenaElems = 0;
-    int grid = 0, grid512 = 0;
+    int grid = 0, grid256 = 0, grid512 = 0;
     uint64_t chunkReads = 262144; // snapgpu_align_batch chunk (SNAPGPU_CHUNK_READS)
     snapgpu_timing_t timing{};
     snapgpu_aligner_stats_t stats{};
@@ -994,6 +997,20 @@ __global__ __launch_bounds__(256) void copy_peak_kernel(const uint4 *__restrict_
         for (int j = 0; j < 4; j++) v[j] = src[i + 256 * j];
 #pragma unroll
         for (int j = 0; j < 4; j++) dst[i + 256 * j] = v[j];
+    }
+}
+
+// Multi-hit download (snapgpu_align_batch_ex): the found hits of every read, rows of
+// maxHitsToGet on the device, packed into one dense array at host-computed offsets so only
+// they cross PCIe (the RNA path asks for 1000 per read and finds a handful).  Wave per read.
+__global__ __launch_bounds__(256) void compact_hits_kernel(const snapgpu_multi_hit_t *__restrict__ src,
+                                                           const int32_t *__restrict__ found,
+                                                           const uint64_t *__restrict__ off, uint64_t n, uint32_t mh,
+                                                           snapgpu_multi_hit_t *__restrict__ dst) {
+    const uint64_t waves = (uint64_t)gridDim.x * 4u;
+    for (uint64_t r = (uint64_t)blockIdx.x * 4u + threadIdx.x / 64u; r < n; r += waves) {
+        const uint32_t c = (uint32_t)found[r];
+        for (uint32_t j = threadIdx.x % 64u; j < c; j += 64u) dst[off[r] + j] = src[r * mh + j];
     }
 }
 
@@ -1290,7 +1307,12 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
     while (a->grid > 64 && (uint64_t)a->grid * a->arenaElems * sizeof(Elem512) > budget) a->grid /= 2;
     for (auto &L : a->lane)
         if ((e = hipMalloc(&L.arena, (uint64_t)a->grid * a->arenaElems * sizeof(Elem512))) != hipSuccess) return fail("arena", e);
-    int perCU512 = 0;   // pass 2 (deferred reads) reuses the arenas of the first a->grid blocks
+    int perCU256 = 0;   // passes 2 and 3 (deferred reads) reuse the arenas of the first a->grid blocks
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU256, (const void *)align_kernel<256, false>, 64, 0);
+    if (perCU256 <= 0) perCU256 = 4;
+    a->grid256 = prop.multiProcessorCount * perCU256;
+    if (a->grid256 > a->grid) a->grid256 = a->grid;
+    int perCU512 = 0;
     hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU512, (const void *)align_kernel<512, false>, 64, 0);
     if (perCU512 <= 0) perCU512 = 4;
     a->grid512 = prop.multiProcessorCount * perCU512;
@@ -1326,7 +1348,7 @@ snapgpu_device_reads_t *snapgpu_reads_upload(snapgpu_aligner_t *a, const snapgpu
     HIPCHKN(hipMalloc(&d->dOffsets, (r->n + 1) * 8));
     HIPCHKN(hipMalloc(&d->dLengths, (r->n + 1) * 4));
     HIPCHKN(hipMalloc(&d->dOut, (r->n + 1) * sizeof(snapgpu_result_t)));
-    HIPCHKN(hipMalloc(&d->dDefer, (r->n + 1) * sizeof(uint32_t)));
+    HIPCHKN(hipMalloc(&d->dDefer, 2 * (r->n + 1) * sizeof(uint32_t)));   // pass-1 and pass-2 defer lists
     HIPCHKN(hipMalloc(&d->dSeeds, (r->n + 8) * SEEDS_PER_READ * sizeof(SeedRec)));
     HIPCHKN(hipMemsetAsync(d->dBases, 0, bytes, s));
     HIPCHKN(hipMemsetAsync(d->dQuals, 0, bytes, s));
@@ -1371,12 +1393,16 @@ struct PassIO {
     const uint32_t *lengths;
     uint64_t n;
     snapgpu_result_t *out;
-    uint32_t *defer;
+    uint32_t *defer;    // pass 1 -> pass 2 read list
+    uint32_t *defer2;   // pass 2 -> pass 3 read list
     SeedRec *seeds;
 };
 
-// Queue pass 0 (seed lookups), pass 1 (align_kernel<128>) and pass 2 (align_kernel<512> over
-// the deferred reads) on lane `li`, with HIP events around each.
+// Queue pass 0 (seed lookups), pass 1 (align_kernel<128>), pass 2 (align_kernel<256> over the
+// reads pass 1 deferred: 129..256 bases, bit planes) and pass 3 (align_kernel<512> over what
+// pass 2 deferred: longer reads and IUPAC-on-both-sides reads, byte compare) on lane `li`, with
+// HIP events around them.  The deferred counts stay on the device (each pass reads its list
+// length from the counter the previous one appended with).
 static int launch_passes(snapgpu_aligner_t *a, int li, const PassIO &io, const AlignExt &x, EvSet &ev,
                          const EvSet *prev) {
     ExecLane &L = a->lane[li];
@@ -1421,10 +1447,22 @@ static int launch_passes(snapgpu_aligner_t *a, int li, const PassIO &io, const A
     else hipLaunchKernelGGL((align_kernel<128, false>), dim3(grid), dim3(64), 0, L.stream, A);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(ev.e[1], L.stream));
-    // pass 2: reads longer than 128 bases or needing the byte-compare LV
+    // pass 2: reads of 129..256 bases (bit planes, 256-bit masks)
+    KArgs M = A;
+    M.counter = L.counter + 3;
+    M.readList = io.defer;
+    M.deferList = io.defer2; M.deferCount = L.counter + 4;
+    M.seedRecs = nullptr;
+    int grid256 = a->grid256;
+    if ((uint64_t)grid256 > io.n) grid256 = (int)io.n;
+    if (ext) hipLaunchKernelGGL((align_kernel<256, true>), dim3(grid256), dim3(64), 0, L.stream, M);
+    else hipLaunchKernelGGL((align_kernel<256, false>), dim3(grid256), dim3(64), 0, L.stream, M);
+    HIPCHK(hipGetLastError());
+    // pass 3: reads longer than 256 bases or needing the byte-compare LV
     KArgs B = A;
     B.counter = L.counter + 1;
-    B.readList = io.defer;
+    B.readList = io.defer2; B.deferCount = L.counter + 4;
+    B.deferList = nullptr;
     B.seedRecs = nullptr;
     int grid2 = a->grid512;
     if ((uint64_t)grid2 > io.n) grid2 = (int)io.n;
@@ -1432,7 +1470,7 @@ static int launch_passes(snapgpu_aligner_t *a, int li, const PassIO &io, const A
     else hipLaunchKernelGGL((align_kernel<512, false>), dim3(grid2), dim3(64), 0, L.stream, B);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(ev.e[2], L.stream));
-    HIPCHK(hipMemcpyAsync(ev.hCounter, L.counter, 16, hipMemcpyDeviceToHost, L.stream));
+    HIPCHK(hipMemcpyAsync(ev.hCounter, L.counter, 32, hipMemcpyDeviceToHost, L.stream));
     return SNAPGPU_OK;
 }
 
@@ -1496,6 +1534,7 @@ static int accountEvSet(snapgpu_aligner_t *a, const EvSet &v) {
     a->timing.lookupKernelMs += ms;
     a->timing.nLaunches++;
     a->timing.nSpilled += v.hCounter[2];
+    a->timing.nByteReads += v.hCounter[4];
     return SNAPGPU_OK;
 }
 
@@ -1521,7 +1560,7 @@ static int launch_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, cons
         EvSet *ev = nextEvSet(a);
         if (!ev) return SNAPGPU_EDEVICE;
         PassIO io{d->dBases, d->dQuals, d->dOffsets + b, d->dLengths + b, m, d->dOut + b, d->dDefer + b,
-                  d->dSeeds + b * SEEDS_PER_READ};
+                  d->dDefer + (n + 1) + b, d->dSeeds + b * SEEDS_PER_READ};
         if ((rc = launch_passes(a, (int)(c & 1), io, x, *ev, c ? &a->evs[a->nEvUsed - 2] : nullptr))) return rc;
     }
     a->lastReads = d;
@@ -1627,7 +1666,7 @@ static int ensureLaneCapacity(snapgpu_aligner_t *a, ExecLane &L, uint64_t reads,
     HIPCHK(hipMemset(L.dQuals, 0, cb));
     HIPCHK(hipMalloc(&L.dOffsets, (reads + 1) * 8));
     HIPCHK(hipMalloc(&L.dLengths, (reads + 1) * 4));
-    HIPCHK(hipMalloc(&L.dDefer, (reads + 1) * 4));
+    HIPCHK(hipMalloc(&L.dDefer, 2 * (reads + 1) * 4));   // pass-1 and pass-2 defer lists
     HIPCHK(hipMalloc(&L.dOut, (reads + 1) * sizeof(snapgpu_result_t)));
     HIPCHK(hipMalloc(&L.dSeeds, (reads + 8) * SEEDS_PER_READ * sizeof(SeedRec)));
     HIPCHK(hipHostMalloc(&L.hOffsets, (reads + 1) * 8, hipHostMallocDefault));
@@ -1740,7 +1779,7 @@ int snapgpu_align_batch_submit(snapgpu_aligner_t *a, const snapgpu_reads_t *read
         HIPCHK(hipMemcpyAsync(L.dQuals, reads->quals + lo[c], span, hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(L.dOffsets, L.hOffsets, m * 8, hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(L.dLengths, L.hLengths, m * 4, hipMemcpyHostToDevice, s));
-        PassIO io{L.dBases, L.dQuals, L.dOffsets, L.dLengths, m, L.dOut, L.dDefer, L.dSeeds};
+        PassIO io{L.dBases, L.dQuals, L.dOffsets, L.dLengths, m, L.dOut, L.dDefer, L.dDefer + (L.capReads + 1), L.dSeeds};
         EvSet *ev = nextEvSet(a);
         if (!ev) { rc = SNAPGPU_EDEVICE; break; }
         if ((rc = launch_passes(a, li, io, AlignExt(), *ev, a->nEvUsed >= 2 ? &a->evs[a->nEvUsed - 2] : nullptr))) break;
@@ -1846,8 +1885,40 @@ int snapgpu_align_batch_ex(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, c
     int rc = launch_resident(a, d, x);
     if (!rc) rc = snapgpu_results_download(a, d, out);
     if (!rc && maxHitsToGet) {
-        if ((e = hipMemcpy(multiHitsFound, dFound, n * sizeof(int32_t), hipMemcpyDeviceToHost)) == hipSuccess)
-            e = hipMemcpy(multiHits, dHits, n * maxHitsToGet * sizeof(snapgpu_multi_hit_t), hipMemcpyDeviceToHost);
+        // only the found hits cross PCIe: counts first, then the hits packed on the device
+        void *dOff = nullptr, *dDense = nullptr;
+        std::vector<uint64_t> off(n + 1, 0);
+        std::vector<snapgpu_multi_hit_t> dense;
+        e = hipMemcpy(multiHitsFound, dFound, n * sizeof(int32_t), hipMemcpyDeviceToHost);
+        if (e == hipSuccess) {
+            for (uint64_t i = 0; i < n; i++) {
+                const int32_t f = multiHitsFound[i];
+                off[i + 1] = off[i] + (uint64_t)(f < 0 ? 0 : (f > (int32_t)maxHitsToGet ? (int32_t)maxHitsToGet : f));
+            }
+            const uint64_t total = off[n];
+            if (total) {
+                dense.resize(total);
+                if ((e = hipMalloc(&dOff, (n + 1) * sizeof(uint64_t))) == hipSuccess &&
+                    (e = hipMalloc(&dDense, total * sizeof(snapgpu_multi_hit_t))) == hipSuccess &&
+                    (e = hipMemcpyAsync(dOff, off.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice,
+                                        a->stream())) == hipSuccess) {
+                    const uint64_t blocks = std::min<uint64_t>((n + 3) / 4, 8192);
+                    hipLaunchKernelGGL(compact_hits_kernel, dim3((unsigned)blocks), dim3(256), 0, a->stream(),
+                                       (const snapgpu_multi_hit_t *)dHits, (const int32_t *)dFound,
+                                       (const uint64_t *)dOff, n, maxHitsToGet, (snapgpu_multi_hit_t *)dDense);
+                    if ((e = hipGetLastError()) == hipSuccess &&
+                        (e = hipMemcpyAsync(dense.data(), dDense, total * sizeof(snapgpu_multi_hit_t),
+                                            hipMemcpyDeviceToHost, a->stream())) == hipSuccess)
+                        e = hipStreamSynchronize(a->stream());
+                }
+                if (e == hipSuccess)
+                    for (uint64_t i = 0; i < n; i++)
+                        if (off[i + 1] > off[i])
+                            memcpy(multiHits + i * maxHitsToGet, dense.data() + off[i],
+                                   (off[i + 1] - off[i]) * sizeof(snapgpu_multi_hit_t));
+            }
+        }
+        devFree(a, dOff); devFree(a, dDense);
         if (e != hipSuccess) {
             snapgpu::setError(std::string("align_batch_ex download: ") + hipGetErrorString(e));
             rc = SNAPGPU_EDEVICE;
@@ -1984,7 +2055,9 @@ int snapgpu_lv_batch(int device, int direction, uint32_t n, const char *texts, c
 }
 
 // The production bit-plane LV (lv_group + lv_prob_pair) on explicit tasks: unit parity for
-// LandauVishkin<dir>::computeEditDistance as align_kernel<128> runs it (patterns <= 127 bases).
+// LandauVishkin<dir>::computeEditDistance as align_kernel<128> runs it (patterns <= 127 bases:
+// 128-bit masks) and as align_kernel<256> runs it (a batch with a longer pattern, <= 253 bases:
+// 256-bit masks).
 int snapgpu_lv_group_batch(int device, int direction, uint32_t n, const char *texts, const uint64_t *textOff,
                            const uint32_t *textLen, const char *patterns, const char *quals, const uint64_t *patOff,
                            const uint32_t *patLen, const int32_t *k, int32_t *outScore, int32_t *outNetIndel,
@@ -1996,11 +2069,13 @@ int snapgpu_lv_group_batch(int device, int direction, uint32_t n, const char *te
     HIPCHK(ensureDeviceTables(device));
     std::vector<LvgTask> tasks(n);
     uint64_t pBytes = 0, tBytes = 0;
+    bool wide = false;
     for (uint32_t i = 0; i < n; i++) {
-        if (patLen[i] == 0 || patLen[i] > 127 || k[i] < 0) {
-            snapgpu::setError("lv_group_batch: pattern length must be 1..127 and k >= 0");
+        if (patLen[i] == 0 || patLen[i] > 253 || k[i] < 0) {
+            snapgpu::setError("lv_group_batch: pattern length must be 1..253 and k >= 0");
             return SNAPGPU_EINVAL;
         }
+        wide |= patLen[i] > 127;
         pBytes = std::max<uint64_t>(pBytes, patOff[i] + patLen[i]);
         tBytes = std::max<uint64_t>(tBytes, textOff[i] + textLen[i]);
         tasks[i] = LvgTask{patOff[i], textOff[i], (int32_t)patLen[i], (int32_t)textLen[i], k[i], direction > 0 ? 1 : -1};
@@ -2019,7 +2094,8 @@ int snapgpu_lv_group_batch(int device, int direction, uint32_t n, const char *te
         hipMemcpy(dP, patterns, pBytes, hipMemcpyHostToDevice);
         hipMemcpy(dQ, quals, pBytes, hipMemcpyHostToDevice);
         hipMemcpy(dX, texts, tBytes, hipMemcpyHostToDevice);
-        hipLaunchKernelGGL(lv_group_kernel, dim3(n), dim3(64), 0, 0, dT, dP, dQ, dX, dS, dN, dPr);
+        if (wide) hipLaunchKernelGGL(lv_group_kernel<4>, dim3(n), dim3(64), 0, 0, dT, dP, dQ, dX, dS, dN, dPr);
+        else hipLaunchKernelGGL(lv_group_kernel<2>, dim3(n), dim3(64), 0, 0, dT, dP, dQ, dX, dS, dN, dPr);
         if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
             snapgpu::setError("lv_group_kernel failed");
             rc = SNAPGPU_EDEVICE;

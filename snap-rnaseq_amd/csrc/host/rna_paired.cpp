@@ -21,6 +21,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <string>
 #include <thread>
 #include <vector>
@@ -408,14 +409,16 @@ int snapgpu_rna_paired_align(snapgpu_paired_aligner_t *pa, snapgpu_aligner_t *ta
     const uint32_t mh = opt->maxHitsToGet;
     std::vector<snapgpu_result_t> tr[2];
     std::vector<int32_t> tf[2];
-    std::vector<snapgpu_multi_hit_t> th[2];
+    // rows of mh hits per read; only the found prefix of a row is written (and read), so the
+    // arrays are left uninitialised (no zero-fill of nu * mh entries)
+    std::unique_ptr<snapgpu_multi_hit_t[]> th[2];
     std::vector<snapgpu_pair_result_t> gr(nu + 1);
     auto t0 = std::chrono::steady_clock::now();
     if (nu) {
         // transcriptomeAligner->AlignRead(read0 / read1, ..., maxHitsToGet 1000, multiHits) (:601-605)
         for (int k = 0; k < 2; k++) {
-            tr[k].resize(nu); tf[k].resize(nu); th[k].resize(nu * (uint64_t)mh);
-            if ((rc = snapgpu_align_batch_ex(ta, U[k], nullptr, mh, tr[k].data(), tf[k].data(), th[k].data())))
+            tr[k].resize(nu); tf[k].resize(nu); th[k].reset(new snapgpu_multi_hit_t[nu * (uint64_t)mh]);
+            if ((rc = snapgpu_align_batch_ex(ta, U[k], nullptr, mh, tr[k].data(), tf[k].data(), th[k].get())))
                 return fail(rc);
         }
         // g_aligner->align(read0, read1, &result) (:625)

@@ -16,9 +16,10 @@
 //   3. scoring (:516-718): candidates in best-possible-score order; scoreLocation (:755-841) is
 //      the byte-compare Landau-Vishkin of align_device.h (one lane per diagonal).
 // Pass 1 takes pairs of reads <= 128 bases with pools sized for ordinary pairs; pairs with a longer
-// read, or whose pools overflow, are deferred to pass 2 (reads <= 512, pools of the reference's
-// size on a small grid).  A pair that exceeds the reference's own pool is flagged: the reference
-// exits there (soft_exit, :436-439, :482-485, :634-637).
+// read, or whose pools overflow, are deferred to pass 2 (reads <= 512, the same pool sizes on the
+// full grid); pass 2's pool overflows go to pass 3 (pools of the reference's size on a small grid:
+// 22 MB per wave at the paired defaults).  A pair that exceeds the reference's own pool is
+// flagged: the reference exits there (soft_exit, :436-439, :482-485, :634-637).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -882,10 +883,11 @@ struct snapgpu_paired_aligner {
     snapgpu_aligner_t *single = nullptr;   // the chimeric fallback's BaseAligner; owns the index upload
     KArgs X{};
     hipStream_t stream = nullptr;
-    PassPool pass[2];
+    PassPool pass[3];                      // [0] pass 1, [1] pass 3 (the reference's pools), [2] pass 2
     uint32_t refPool = 0, maxSeedsCmd = 0;
-    uint32_t *dCounter = nullptr;          // [0] pass 1 queue, [1] pass 2 queue, [2] defer count
-    uint32_t *dDefer = nullptr;
+    uint32_t *dCounter = nullptr;          // [0] pass 1 queue, [1] pass 3 queue, [2] pass-1 defer count,
+                                           // [3] pass 2 queue, [4] pass-2 defer count
+    uint32_t *dDefer = nullptr, *dDefer2 = nullptr;
     snapgpu_pair_result_t *dOut = nullptr;
     char *dB[2] = {}, *dQ[2] = {};
     uint64_t *dO[2] = {};
@@ -897,11 +899,12 @@ static void pfree(void *p) { if (p) (void)hipFree(p); }
 
 static int ensurePairCapacity(snapgpu_paired_aligner_t *pa, uint64_t n, const uint64_t bytes[2]) {
     if (n > pa->capPairs) {
-        pfree(pa->dOut); pfree(pa->dDefer); pfree(pa->dO[0]); pfree(pa->dO[1]); pfree(pa->dL[0]); pfree(pa->dL[1]);
-        pa->dOut = nullptr; pa->dDefer = nullptr; pa->dO[0] = pa->dO[1] = nullptr; pa->dL[0] = pa->dL[1] = nullptr;
+        pfree(pa->dOut); pfree(pa->dDefer); pfree(pa->dDefer2); pfree(pa->dO[0]); pfree(pa->dO[1]); pfree(pa->dL[0]); pfree(pa->dL[1]);
+        pa->dOut = nullptr; pa->dDefer = nullptr; pa->dDefer2 = nullptr; pa->dO[0] = pa->dO[1] = nullptr; pa->dL[0] = pa->dL[1] = nullptr;
         pa->capPairs = 0;
         PCHK(hipMalloc(&pa->dOut, n * sizeof(snapgpu_pair_result_t)));
         PCHK(hipMalloc(&pa->dDefer, n * 4 + 16));
+        PCHK(hipMalloc(&pa->dDefer2, n * 4 + 16));
         for (int r = 0; r < 2; r++) {
             PCHK(hipMalloc(&pa->dO[r], n * 8 + 16));
             PCHK(hipMalloc(&pa->dL[r], n * 4 + 16));
@@ -947,21 +950,24 @@ static int runIntersect(snapgpu_paired_aligner_t *pa, const snapgpu_reads_t *r0,
         PCHK(hipMemcpyAsync(pa->dO[r], R[r]->offsets, n * 8, hipMemcpyHostToDevice, s));
         PCHK(hipMemcpyAsync(pa->dL[r], R[r]->lengths, n * 4, hipMemcpyHostToDevice, s));
     }
-    PCHK(hipMemsetAsync(pa->dCounter, 0, 16, s));
+    PCHK(hipMemsetAsync(pa->dCounter, 0, 32, s));
     PArgs P;
     memset(&P, 0, sizeof(P));
     P.X = pa->X;
     for (int r = 0; r < 2; r++) { P.bases[r] = pa->dB[r]; P.quals[r] = pa->dQ[r]; P.offsets[r] = pa->dO[r]; P.lengths[r] = pa->dL[r]; }
     P.out = pa->dOut;
-    P.deferList = pa->dDefer; P.deferCount = pa->dCounter + 2;
     P.maxK = pa->p.maxK; P.extra = pa->p.extraSearchDepth; P.maxSeedsCmd = pa->maxSeedsCmd;
     P.minSpacing = pa->p.minSpacing; P.maxSpacing = pa->p.maxSpacing; P.maxBigHits = pa->p.maxBigHits;
     P.maxReadSize = pa->p.maxReadSize; P.seedCoverage = pa->p.seedCoverage;
     P.refPool = pa->refPool;
-    // pass 1: reads <= 128 bases, pools for ordinary pairs
+    auto usePool = [&P](const PassPool &pp) {
+        P.pool = pp.pool; P.poolStride = pp.stride;
+        P.candCap = pp.candCap; P.mateCap = pp.mateCap; P.anchorCap = pp.anchorCap;
+    };
+    // pass 1: reads <= 128 bases, pools for ordinary pairs, the full grid
     P.nPairs = (uint32_t)n; P.pairList = nullptr; P.counter = pa->dCounter; P.maxLen = 128;
-    P.pool = pa->pass[0].pool; P.poolStride = pa->pass[0].stride;
-    P.candCap = pa->pass[0].candCap; P.mateCap = pa->pass[0].mateCap; P.anchorCap = pa->pass[0].anchorCap;
+    P.deferList = pa->dDefer; P.deferCount = pa->dCounter + 2;
+    usePool(pa->pass[0]);
     int grid = pa->pass[0].grid;
     if ((uint64_t)grid > n) grid = (int)n;
     if (grid > 0) hipLaunchKernelGGL(paired_kernel<128>, dim3(grid), dim3(64), 0, s, P);
@@ -969,11 +975,21 @@ static int runIntersect(snapgpu_paired_aligner_t *pa, const snapgpu_reads_t *r0,
     uint32_t nDefer = 0;
     PCHK(hipMemcpyAsync(&nDefer, pa->dCounter + 2, 4, hipMemcpyDeviceToHost, s));
     PCHK(hipStreamSynchronize(s));
-    if (nDefer) {   // pass 2: long reads and pool overflows, the reference's pool sizes
-        P.nPairs = nDefer; P.pairList = pa->dDefer; P.counter = pa->dCounter + 1; P.maxLen = 512;
-        P.deferList = nullptr;
-        P.pool = pa->pass[1].pool; P.poolStride = pa->pass[1].stride;
-        P.candCap = pa->pass[1].candCap; P.mateCap = pa->pass[1].mateCap; P.anchorCap = pa->pass[1].anchorCap;
+    if (nDefer) {   // pass 2: reads of 129..512 bases (and pass-1 pool overflows), ordinary pools, full grid
+        P.nPairs = nDefer; P.pairList = pa->dDefer; P.counter = pa->dCounter + 3; P.maxLen = 512;
+        P.deferList = pa->dDefer2; P.deferCount = pa->dCounter + 4;
+        usePool(pa->pass[2]);
+        grid = pa->pass[2].grid;
+        if ((uint32_t)grid > nDefer) grid = (int)nDefer;
+        hipLaunchKernelGGL(paired_kernel<512>, dim3(grid), dim3(64), 0, s, P);
+        PCHK(hipGetLastError());
+        PCHK(hipMemcpyAsync(&nDefer, pa->dCounter + 4, 4, hipMemcpyDeviceToHost, s));
+        PCHK(hipStreamSynchronize(s));
+    }
+    if (nDefer) {   // pass 3: pool overflows, the reference's pool sizes on a small grid
+        P.nPairs = nDefer; P.pairList = pa->dDefer2; P.counter = pa->dCounter + 1; P.maxLen = 512;
+        P.deferList = nullptr; P.deferCount = nullptr;
+        usePool(pa->pass[1]);
         grid = pa->pass[1].grid;
         if ((uint32_t)grid > nDefer) grid = (int)nDefer;
         hipLaunchKernelGGL(paired_kernel<512>, dim3(grid), dim3(64), 0, s, P);
@@ -1075,6 +1091,9 @@ snapgpu_paired_aligner_t *snapgpu_paired_aligner_create(int device, const snapgp
     while (grid2 > 8 && (uint64_t)grid2 * stride2 > (8ull << 30)) grid2 /= 2;
     if (allocPass(pa->pass[1], grid2, pa->refPool, std::max<uint32_t>(1, pa->refPool / 2), pa->refPool))
         { snapgpu_paired_aligner_free(pa); return nullptr; }
+    // pass 2 (reads of 129..512 bases): pass 1's pool sizes on the full <512> grid
+    if (allocPass(pa->pass[2], prop.multiProcessorCount * perCU2, c1, std::max<uint32_t>(1, std::min(pa->refPool / 2, c1 / 2)), c1))
+        { snapgpu_paired_aligner_free(pa); return nullptr; }
     return pa;
 }
 
@@ -1085,7 +1104,7 @@ void snapgpu_paired_aligner_free(snapgpu_paired_aligner_t *pa) {
     } else {
         (void)hipSetDevice(pa->device);
         if (pa->stream) (void)hipStreamSynchronize(pa->stream);
-        pfree(pa->dCounter); pfree(pa->dDefer); pfree(pa->dOut);
+        pfree(pa->dCounter); pfree(pa->dDefer); pfree(pa->dDefer2); pfree(pa->dOut);
         for (int r = 0; r < 2; r++) { pfree(pa->dB[r]); pfree(pa->dQ[r]); pfree(pa->dO[r]); pfree(pa->dL[r]); }
         for (auto &pp : pa->pass) pfree(pp.pool);
         if (pa->stream) (void)hipStreamDestroy(pa->stream);

@@ -155,6 +155,7 @@ class Timing(C.Structure):
         ("wallMs", C.c_double),
         ("mainKernelBusyMs", C.c_double),
         ("lookupKernelBusyMs", C.c_double),
+        ("nByteReads", C.c_uint64),
     ]
 
 

@@ -14,6 +14,7 @@ TSV/JSON expected outputs.
     python3 tests/golden/make_golden.py --only-refindex  # reference-built index + seedLen fixtures
     python3 tests/golden/make_golden.py --only-single    # `snap-rna single` end-to-end SAM fixtures
     python3 tests/golden/make_golden.py --only-paired    # Intersecting + Chimeric paired-end aligner runs
+    python3 tests/golden/make_golden.py --only-long      # 129..256-base reads + long LV vectors (align_kernel<256>)
 """
 import hashlib
 import json
@@ -696,8 +697,73 @@ def rna_paired_fixtures(work):
                 dst.write("".join(counts))
 
 
+def long_fixtures(work):
+    """Reads of 129..256 bases (align_kernel<256>: 256-bit bit-plane masks) on the small genome:
+    synthetic 150 / 250 bp and mixed-length reads with the reference's own AlignRead outputs for
+    three parameter sets, and Landau-Vishkin vectors with patterns of 128..253 bases."""
+    fa = os.path.join(HERE, "small.fa")
+    g = snapgpu.Genome.from_fasta(fa, 500)
+    rd = []
+    for rl, cnt, seed in ((150, 1200, 41), (250, 600, 42), (129, 150, 43), (256, 150, 44)):
+        syn = snapgpu.Reads.synthetic(g, cnt, seed=seed, read_length=rl, random_read_fraction=0.02)
+        rd += [tuple(x.decode() for x in syn.get(i)) for i in range(syn.n)]
+    rng = random.Random(45)
+    syn = snapgpu.Reads.synthetic(g, 400, seed=46, read_length=256, random_read_fraction=0.02)
+    for i in range(syn.n):   # mixed lengths 129..256, some lower-case and N bases
+        b, q = (x.decode() for x in syn.get(i))
+        L = rng.randrange(129, 257)
+        b, q = list(b[:L]), q[:L]
+        for _ in range(rng.randrange(0, 3)):
+            b[rng.randrange(L)] = "N"
+        b = "".join(b)
+        if rng.random() < 0.1:
+            b = b.lower()
+        rd.append((b, q))
+    fq = os.path.join(HERE, "small_long_reads.fq")
+    write_fastq(fq, rd)
+    idxdir = os.path.join(work, "small_idx_long")
+    ref_index(fa, idxdir)
+    for name in ("default", "k20", "s4"):
+        with open(os.path.join(HERE, f"expected_small_long_{name}.tsv"), "w") as f:
+            f.write(ref_align(idxdir, fq, PARAM_SETS[name]))
+    for direction in (1, -1):
+        rows = []
+        for _ in range(400):
+            L = rng.choice([128, 140, 160, 190, 220, 240, 253])
+            t = "".join(rng.choice("ACGT") for _ in range(L + 35))
+            p = list(t[:L] if direction > 0 else t[::-1][:L])
+            for _ in range(rng.randrange(0, 12)):
+                op, i = rng.random(), rng.randrange(len(p))
+                if op < 0.6:
+                    p[i] = rng.choice("ACGTN")
+                elif op < 0.8 and len(p) < 253:
+                    p.insert(i, rng.choice("ACGT"))
+                elif len(p) > 128:
+                    del p[i]
+            p = "".join(p)
+            q = "".join(chr(33 + rng.randrange(0, 45)) for _ in p)
+            k = rng.choice([0, 1, 2, 3, 5, 8, 14, 16, 22, 30])
+            tl = rng.choice([len(t), len(p) + 31])
+            tt = t[:tl] if direction > 0 else t[-tl:]
+            rows.append((direction, k, tt, p, q))
+        inp = os.path.join(work, f"lvl{direction}.tsv")
+        with open(inp, "w") as f:
+            for r in rows:
+                f.write("\t".join(map(str, r)) + "\n")
+        out = run([HARNESS, "lv", inp]).splitlines()
+        with open(os.path.join(HERE, f"lv_long_{'fwd' if direction > 0 else 'rev'}.tsv"), "w") as f:
+            for r, o in zip(rows, out):
+                e, net, prob = o.split("\t")
+                f.write("\t".join(map(str, r)) + f"\t{e}\t{net}\t{float.fromhex(prob).hex()}\n")
+
+
 def main():
     work = tempfile.mkdtemp(prefix="golden_")
+    if "--only-long" in sys.argv:
+        long_fixtures(work)
+        shutil.rmtree(work, ignore_errors=True)
+        print("129..256-base read and LV fixtures written to", HERE)
+        return
     if "--only-rna-paired" in sys.argv:
         rna_paired_fixtures(work)
         shutil.rmtree(work, ignore_errors=True)
