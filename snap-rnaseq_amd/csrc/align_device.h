@@ -113,11 +113,13 @@ struct KArgs {
     // genome bit planes {hi, lo, notACGT, 0} per 32 bases, word 0 = position -PACK_GUARD
     const uint4 *gpl;
     uint32_t hasIupac;
-    // two-pass dispatch: align_kernel<128> defers reads it cannot take (longer than
-    // 128 bases, or IUPAC codes on both sides) to align_kernel<512>
-    uint32_t *deferList;         // pass 1 appends read indices here
-    uint32_t *deferCount;        // pass 1: atomic append count; pass 2: number of reads
-    const uint32_t *readList;    // pass 2: read indices (nullptr in pass 1)
+    // three-pass dispatch: align_kernel<128> defers reads it cannot take (longer than 128
+    // bases, or IUPAC codes on both sides) to align_kernel<256>, which defers reads longer than
+    // 256 bases and the IUPAC ones to align_kernel<512>
+    uint32_t *deferList;         // passes 1 and 2 append the read indices they defer here
+    uint32_t *deferCount;        //   (atomic append count)
+    const uint32_t *readList;    // passes 2 and 3: read indices (nullptr in pass 1)
+    const uint32_t *readCount;   //   and their number (the previous pass's deferCount)
     const uint4 *seedRecs;       // seed_lookup_kernel records (SeedRec, 8 per read), or nullptr
     unsigned long long *phaseBuf;   // diagnostic (SNAPGPU_PHASES=1): per-block [PH_SLOTS] cycle sums, else null
     // windowed search + multi-hit export (snapgpu_align_batch_ex; BaseAligner.h:73-86)

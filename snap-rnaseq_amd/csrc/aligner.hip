@@ -644,7 +644,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MAXLEN <= 25
     __shared__ Lds<MAXLEN> S;
     ElemOf<MAXLEN> *ar = reinterpret_cast<ElemOf<MAXLEN> *>(A.arena) + (uint64_t)blockIdx.x * A.arenaElems;
     const int lane = lane_id();
-    const uint32_t total = A.readList ? uni(*A.deferCount) : A.nReads;
+    const uint32_t total = A.readList ? uni(*A.readCount) : A.nReads;
     for (;;) {
         uint32_t i = 0;
         if (lane == 0) i = atomicAdd(A.counter, 1u);
@@ -1450,7 +1450,7 @@ static int launch_passes(snapgpu_aligner_t *a, int li, const PassIO &io, const A
     // pass 2: reads of 129..256 bases (bit planes, 256-bit masks)
     KArgs M = A;
     M.counter = L.counter + 3;
-    M.readList = io.defer;
+    M.readList = io.defer; M.readCount = L.counter + 2;
     M.deferList = io.defer2; M.deferCount = L.counter + 4;
     M.seedRecs = nullptr;
     int grid256 = a->grid256;
@@ -1461,8 +1461,8 @@ static int launch_passes(snapgpu_aligner_t *a, int li, const PassIO &io, const A
     // pass 3: reads longer than 256 bases or needing the byte-compare LV
     KArgs B = A;
     B.counter = L.counter + 1;
-    B.readList = io.defer2; B.deferCount = L.counter + 4;
-    B.deferList = nullptr;
+    B.readList = io.defer2; B.readCount = L.counter + 4;
+    B.deferList = nullptr; B.deferCount = nullptr;
     B.seedRecs = nullptr;
     int grid2 = a->grid512;
     if ((uint64_t)grid2 > io.n) grid2 = (int)io.n;
