@@ -656,6 +656,8 @@ typedef struct snapgpu_rna_paired_stats {
     uint64_t totalPairs, usefulPairs, singleHits, multiHits, notFound, transcriptomeRecords;
     uint64_t partialPairs, partialMatches, seedRuns;   /* FindPartialMatches scans, hits, CharacterizeSeeds runs */
     double alignMs, filterMs, seedMs, cigarMs, writeMs, wallMs;
+    double prepMs;     /* clipping, ID check, pre-filter, batch views (before alignMs) */
+    double countMs;    /* spacing / MAPQ adjustments and the GTF read counts (after seedMs) */
 } snapgpu_rna_paired_stats_t;
 
 /* pairedAligner: the genome aligner (snapgpu_paired_aligner_create with the paired CLI defaults);

@@ -961,6 +961,9 @@ struct snapgpu_aligner {
     hipError_t (*eventQuery)(hipEvent_t) = hipEventQuery;   // test hook (snapgpu_selftest_timeout_path)
     hipEvent_t cev[2] = {};       // cigar_kernel timing
     int cigarGrid = 0;
+    // snapgpu_align_batch_ex buffers, kept across calls (grow-only): search windows, multi-hit
+    // scratch per block, found counts, hit rows, compaction offsets and the packed hits
+    struct ExBuf { void *p = nullptr; uint64_t cap = 0; } exSearch, exScratch, exFound, exHits, exOff, exDense;
     hipStream_t stream() const { return lane[0].stream; }
 };
 
@@ -1214,6 +1217,7 @@ void snapgpu_aligner_free(snapgpu_aligner_t *a) {
         hostPinnedFree(v.hCounter);
     }
     for (auto &e : a->cev) if (e) hipEventDestroy(e);
+    for (auto *b : {&a->exSearch, &a->exScratch, &a->exFound, &a->exHits, &a->exOff, &a->exDense}) devFree(a, b->p);
     delete a;
 }
 
@@ -1853,25 +1857,37 @@ int snapgpu_align_batch_ex(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, c
     snapgpu_device_reads_t *d = snapgpu_reads_upload(a, reads);
     if (!d) return SNAPGPU_EDEVICE;
     AlignExt x;
-    void *dSearch = nullptr, *dScratch = nullptr, *dFound = nullptr, *dHits = nullptr;
+    // grow-only device buffers of the aligner (hipMalloc / hipFree of the hit rows, ~1 GB for
+    // the RNA path's 1000 hits per read, cost more than the kernels)
+    auto ensure = [a](snapgpu_aligner::ExBuf &b, uint64_t bytes) -> hipError_t {
+        if (bytes <= b.cap) return hipSuccess;
+        devFree(a, b.p);
+        b.p = nullptr;
+        b.cap = 0;
+        const uint64_t want = bytes + bytes / 4 + 256;
+        hipError_t e = hipMalloc(&b.p, want);
+        if (e == hipSuccess) b.cap = want;
+        return e;
+    };
     auto cleanup = [&]() {
-        devFree(a, dSearch); devFree(a, dScratch); devFree(a, dFound); devFree(a, dHits);
         snapgpu_device_reads_free(d);
         a->lastReads = nullptr;
     };
     hipError_t e = hipSuccess;
     const uint64_t n = reads->n;
+    void *dScratch = nullptr, *dFound = nullptr, *dHits = nullptr;
     if (search) {
-        if ((e = hipMalloc(&dSearch, n * sizeof(snapgpu_search_t))) == hipSuccess)
-            e = hipMemcpyAsync(dSearch, search, n * sizeof(snapgpu_search_t), hipMemcpyHostToDevice, a->stream());
-        x.search = (const snapgpu_search_t *)dSearch;
+        if ((e = ensure(a->exSearch, n * sizeof(snapgpu_search_t))) == hipSuccess)
+            e = hipMemcpyAsync(a->exSearch.p, search, n * sizeof(snapgpu_search_t), hipMemcpyHostToDevice, a->stream());
+        x.search = (const snapgpu_search_t *)a->exSearch.p;
     }
     if (e == hipSuccess && maxHitsToGet) {
         const uint64_t blocks = (uint64_t)(a->grid > a->grid512 ? a->grid : a->grid512);
         const uint64_t stride = multiHitStride(maxHitsToGet);
-        if ((e = hipMalloc(&dScratch, blocks * stride * 4)) == hipSuccess &&
-            (e = hipMalloc(&dFound, n * sizeof(int32_t))) == hipSuccess)
-            e = hipMalloc(&dHits, n * maxHitsToGet * sizeof(snapgpu_multi_hit_t));
+        if ((e = ensure(a->exScratch, blocks * stride * 4)) == hipSuccess &&
+            (e = ensure(a->exFound, n * sizeof(int32_t))) == hipSuccess)
+            e = ensure(a->exHits, n * maxHitsToGet * sizeof(snapgpu_multi_hit_t));
+        dScratch = a->exScratch.p; dFound = a->exFound.p; dHits = a->exHits.p;
         x.maxHitsToGet = maxHitsToGet;
         x.hitScratch = (uint32_t *)dScratch;
         x.multiFound = (int32_t *)dFound;
@@ -1888,8 +1904,9 @@ int snapgpu_align_batch_ex(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, c
         // only the found hits cross PCIe: counts first, then the hits packed on the device
         void *dOff = nullptr, *dDense = nullptr;
         std::vector<uint64_t> off(n + 1, 0);
+        e = hipStreamSynchronize(a->stream());
         std::vector<snapgpu_multi_hit_t> dense;
-        e = hipMemcpy(multiHitsFound, dFound, n * sizeof(int32_t), hipMemcpyDeviceToHost);
+        if (e == hipSuccess) e = hipMemcpy(multiHitsFound, dFound, n * sizeof(int32_t), hipMemcpyDeviceToHost);
         if (e == hipSuccess) {
             for (uint64_t i = 0; i < n; i++) {
                 const int32_t f = multiHitsFound[i];
@@ -1898,8 +1915,9 @@ int snapgpu_align_batch_ex(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, c
             const uint64_t total = off[n];
             if (total) {
                 dense.resize(total);
-                if ((e = hipMalloc(&dOff, (n + 1) * sizeof(uint64_t))) == hipSuccess &&
-                    (e = hipMalloc(&dDense, total * sizeof(snapgpu_multi_hit_t))) == hipSuccess &&
+                if ((e = ensure(a->exOff, (n + 1) * sizeof(uint64_t))) == hipSuccess &&
+                    (e = ensure(a->exDense, total * sizeof(snapgpu_multi_hit_t))) == hipSuccess &&
+                    ((dOff = a->exOff.p), (dDense = a->exDense.p), true) &&
                     (e = hipMemcpyAsync(dOff, off.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice,
                                         a->stream())) == hipSuccess) {
                     const uint64_t blocks = std::min<uint64_t>((n + 3) / 4, 8192);
@@ -1918,7 +1936,6 @@ int snapgpu_align_batch_ex(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, c
                                    (off[i + 1] - off[i]) * sizeof(snapgpu_multi_hit_t));
             }
         }
-        devFree(a, dOff); devFree(a, dDense);
         if (e != hipSuccess) {
             snapgpu::setError(std::string("align_batch_ex download: ") + hipGetErrorString(e));
             rc = SNAPGPU_EDEVICE;

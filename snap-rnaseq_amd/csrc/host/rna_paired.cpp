@@ -413,6 +413,7 @@ int snapgpu_rna_paired_align(snapgpu_paired_aligner_t *pa, snapgpu_aligner_t *ta
     // arrays are left uninitialised (no zero-fill of nu * mh entries)
     std::unique_ptr<snapgpu_multi_hit_t[]> th[2];
     std::vector<snapgpu_pair_result_t> gr(nu + 1);
+    st.prepMs = msSince(w0);
     auto t0 = std::chrono::steady_clock::now();
     if (nu) {
         // transcriptomeAligner->AlignRead(read0 / read1, ..., maxHitsToGet 1000, multiHits) (:601-605)
@@ -499,6 +500,7 @@ int snapgpu_rna_paired_align(snapgpu_paired_aligner_t *pa, snapgpu_aligner_t *ta
             }
     }
     st.seedMs = msSince(t0);
+    t0 = std::chrono::steady_clock::now();
     // spacing and MAPQ adjustments (PairedAligner.cpp:648-663); read counts in input order
     for (uint64_t j = 0; j < nu; j++) {
         PairOut &r = fs[j].r;
@@ -522,6 +524,7 @@ int snapgpu_rna_paired_align(snapgpu_paired_aligner_t *pa, snapgpu_aligner_t *ta
         for (uint64_t j = 0; j < nu; j++) uidx[ui[j]] = (int64_t)j;
         for (uint64_t i = 0; i < n; i++) if (uidx[i] >= 0) po[i] = fs[uidx[i]].r;
     }
+    st.countMs = msSince(t0);
     // CIGARs on the GPU (writeRead, SAM.cpp:1040-1066): genome records at the location, the
     // transcriptome records on the transcriptome at tlocation
     t0 = std::chrono::steady_clock::now();

@@ -188,7 +188,8 @@ class RnaPairedOptions(C.Structure):
 class RnaPairedStats(C.Structure):
     _fields_ = [(f, C.c_uint64) for f in ("totalPairs", "usefulPairs", "singleHits", "multiHits", "notFound",
                                           "transcriptomeRecords", "partialPairs", "partialMatches", "seedRuns")] + \
-               [(f, C.c_double) for f in ("alignMs", "filterMs", "seedMs", "cigarMs", "writeMs", "wallMs")]
+               [(f, C.c_double) for f in ("alignMs", "filterMs", "seedMs", "cigarMs", "writeMs", "wallMs", "prepMs",
+                                           "countMs")]
 
 
 class SingleStats(C.Structure):

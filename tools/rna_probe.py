@@ -52,7 +52,8 @@ def main():
         def full():
             gtf.reset_counts()
             _, st = snapgpu.rna_paired_align(pa, ta, gtf, R0, R1)
-            out["stage_ms"] = {k: round(st[k], 1) for k in ("alignMs", "filterMs", "seedMs", "cigarMs", "writeMs")}
+            out["stage_ms"] = {k: round(st[k], 1) for k in ("prepMs", "alignMs", "filterMs", "seedMs", "countMs", "cigarMs",
+                                                                    "writeMs", "wallMs")}
         out["rna_paired_align_ms"] = best(full)
         print(out, flush=True)
     finally:
