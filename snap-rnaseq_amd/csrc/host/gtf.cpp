@@ -21,6 +21,7 @@
 #include <map>
 #include <set>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace snapgpu {
@@ -406,8 +407,8 @@ void gtfCountSingle(snapgpu_gtf_t *g, const std::string &transcriptId) {
 }
 
 // the transcripts whose features cover every segment of one read (:1417-1486)
-static bool readTranscripts(snapgpu_gtf_t *g, const std::string &tid, uint32_t tstart, uint32_t start, uint32_t length,
-                            std::set<std::string> &ids) {
+static bool readTranscripts(const snapgpu_gtf_t *g, const std::string &tid, uint32_t tstart, uint32_t start,
+                            uint32_t length, std::set<std::string> &ids, std::vector<GtfFeature *> &junc) {
     auto tp = g->transcripts.find(tid);
     if (tp == g->transcripts.end()) return false;   // GetTranscript exits
     const GtfTranscript &t = tp->second;
@@ -428,7 +429,7 @@ static bool readTranscripts(snapgpu_gtf_t *g, const std::string &tid, uint32_t t
         }
     };
     for (auto &j : js) {
-        const_cast<GtfFeature *>(j.second)->readCount++;   // the junction's splice count
+        junc.push_back(const_cast<GtfFeature *>(j.second));   // the junction's splice count
         const uint32_t len = j.first - tstart;
         segment(start, start + len - 1);
         tstart += len;
@@ -439,29 +440,72 @@ static bool readTranscripts(snapgpu_gtf_t *g, const std::string &tid, uint32_t t
     return true;
 }
 
-// GTFReader::IncrementReadCount(pair form) (:1409-1611)
+// The counter updates one pair makes (GTFReader::IncrementReadCount, pair form, :1409-1611),
+// found without touching any counter: the junctions its reads cross, the transcripts both reads
+// are compatible with (in id order) and their gene.  bad: an unknown transcript or gene (the
+// reference exits).
+struct GtfPairEvent {
+    std::vector<GtfFeature *> junc;
+    std::vector<GtfTranscript *> tr;
+    GtfGene *gene = nullptr;
+    bool bad = false;
+};
+
+static void pairEvent(const snapgpu_gtf_t *g, const GtfPairQuery &q, GtfPairEvent &ev) {
+    std::set<std::string> ids0, ids1;
+    if (q.tid0->empty()) return;
+    if (!readTranscripts(g, *q.tid0, q.tstart0, q.start0, q.len0, ids0, ev.junc)) { ev.bad = true; return; }
+    if (q.tid1->empty()) return;
+    if (!readTranscripts(g, *q.tid1, q.tstart1, q.start1, q.len1, ids1, ev.junc)) { ev.bad = true; return; }
+    std::string geneId;
+    for (auto &x : ids0) {
+        if (!ids1.count(x)) continue;
+        auto tp = g->transcripts.find(x);
+        if (tp == g->transcripts.end()) { ev.bad = true; return; }
+        ev.tr.push_back(const_cast<GtfTranscript *>(&tp->second));
+        geneId = tp->second.geneId;
+    }
+    if (ev.tr.empty()) return;
+    auto ge = g->genes.find(geneId);
+    if (ge == g->genes.end()) { ev.bad = true; return; }
+    ev.gene = const_cast<GtfGene *>(&ge->second);
+}
+
+static void applyEvent(const GtfPairEvent &ev) {
+    for (GtfFeature *f : ev.junc) f->readCount++;
+    for (GtfTranscript *t : ev.tr) t->readCount += 1.f / (float)ev.tr.size();
+    if (ev.gene) ev.gene->readCount++;
+}
+
+// GTFReader::IncrementReadCount (pair form) for one pair
 bool gtfCountPair(snapgpu_gtf_t *g, const std::string &tid0, uint32_t tstart0, uint32_t start0, uint32_t len0,
                   const std::string &tid1, uint32_t tstart1, uint32_t start1, uint32_t len1) {
-    std::set<std::string> ids0, ids1;
-    if (tid0.empty()) return true;
-    if (!readTranscripts(g, tid0, tstart0, start0, len0, ids0)) return false;
-    if (tid1.empty()) return true;
-    if (!readTranscripts(g, tid1, tstart1, start1, len1, ids1)) return false;
-    std::set<std::string> fin;
-    for (auto &x : ids0)
-        if (ids1.count(x)) fin.insert(x);
-    if (fin.empty()) return true;
-    std::string geneId;
-    for (auto &x : fin) {
-        auto tp = g->transcripts.find(x);
-        if (tp == g->transcripts.end()) return false;
-        geneId = tp->second.geneId;
-        tp->second.readCount += 1.f / (float)fin.size();
-    }
-    auto ge = g->genes.find(geneId);
-    if (ge == g->genes.end()) return false;
-    ge->second.readCount++;
+    GtfPairEvent ev;
+    pairEvent(g, GtfPairQuery{&tid0, tstart0, start0, len0, &tid1, tstart1, start1, len1}, ev);
+    if (ev.bad) return false;
+    applyEvent(ev);
     return true;
+}
+
+// The same for a batch of pairs in input order: the interval queries run on host threads (read
+// only), the counter updates afterwards in pair order, so the float transcript counts add up in
+// the reference's order.  Returns the index of the first pair naming an unknown transcript or
+// gene (the counts of the pairs before it applied), or -1.
+int64_t gtfCountPairs(snapgpu_gtf_t *g, const std::vector<GtfPairQuery> &q) {
+    const uint64_t n = q.size();
+    std::vector<GtfPairEvent> ev(n);
+    const unsigned nt = n < 4096 ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; t++)
+        th.emplace_back([&, t] {
+            for (uint64_t i = n * t / nt; i < n * (t + 1) / nt; i++) pairEvent(g, q[i], ev[i]);
+        });
+    for (auto &x : th) x.join();
+    for (uint64_t i = 0; i < n; i++) {
+        if (ev[i].bad) return (int64_t)i;
+        applyEvent(ev[i]);
+    }
+    return -1;
 }
 
 }  // namespace snapgpu

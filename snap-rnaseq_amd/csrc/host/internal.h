@@ -124,6 +124,14 @@ struct SamLine {
 };
 void samAppendLine(std::string &o, const Genome &g, const SamLine &L);
 
+// One pair's GTFReader::IncrementReadCount (pair form) arguments (gtf.cpp: gtfCountPairs).
+struct GtfPairQuery {
+    const std::string *tid0;
+    uint32_t tstart0, start0, len0;
+    const std::string *tid1;
+    uint32_t tstart1, start1, len1;
+};
+
 // xoshiro256** seeded with splitmix64: deterministic on every host.
 struct Rng {
     uint64_t s[4];

@@ -37,8 +37,7 @@ bool gtfSpliceCigar(const GtfTranscript *t, uint32_t pos, const std::vector<std:
                     std::string &out);
 const GtfGene *gtfGene(const snapgpu_gtf_t *g, const std::string &geneId);
 bool gtfGeneCheckBoundary(const GtfGene *ge, const std::string &chr, uint32_t pos, uint32_t buffer);
-bool gtfCountPair(snapgpu_gtf_t *g, const std::string &tid0, uint32_t tstart0, uint32_t start0, uint32_t len0,
-                  const std::string &tid1, uint32_t tstart1, uint32_t start1, uint32_t len1);
+int64_t gtfCountPairs(snapgpu_gtf_t *g, const std::vector<GtfPairQuery> &q);
 }  // namespace snapgpu
 
 using namespace snapgpu;
@@ -502,6 +501,8 @@ int snapgpu_rna_paired_align(snapgpu_paired_aligner_t *pa, snapgpu_aligner_t *ta
     st.seedMs = msSince(t0);
     t0 = std::chrono::steady_clock::now();
     // spacing and MAPQ adjustments (PairedAligner.cpp:648-663); read counts in input order
+    // (interval queries on host threads, counter updates in pair order: gtfCountPairs)
+    std::vector<GtfPairQuery> cq;
     for (uint64_t j = 0; j < nu; j++) {
         PairOut &r = fs[j].r;
         if (opt->forceSpacing && (r.status[0] == SNAPGPU_SINGLE_HIT) != (r.status[1] == SNAPGPU_SINGLE_HIT)) {
@@ -511,11 +512,11 @@ int snapgpu_rna_paired_align(snapgpu_paired_aligner_t *pa, snapgpu_aligner_t *ta
         if (r.score[0] + r.score[1] >= 5)
             for (int k = 0; k < 2; k++) if (r.mapq[k] < 50) r.mapq[k] /= 2;
         const FilterState &S = fs[j];
-        if (S.countPair &&
-            !gtfCountPair(gtf, S.tid0, S.tstart0, S.start0, S.len0, S.tid1, S.tstart1, S.start1, S.len1)) {
-            setError("rna_paired_align: read count for an unknown transcript or gene");
-            return fail(SNAPGPU_EFORMAT);
-        }
+        if (S.countPair) cq.push_back(GtfPairQuery{&S.tid0, S.tstart0, S.start0, S.len0, &S.tid1, S.tstart1, S.start1, S.len1});
+    }
+    if (gtfCountPairs(gtf, cq) >= 0) {
+        setError("rna_paired_align: read count for an unknown transcript or gene");
+        return fail(SNAPGPU_EFORMAT);
     }
     // the pairs' records, in input order; filtered pairs: NotFound, InvalidGenomeLocation
     std::vector<PairOut> po(n);

@@ -20,10 +20,14 @@ import snapgpu  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--reads", type=int, default=1_000_000)
 ap.add_argument("--genome-bases", type=int, default=46_709_983)
+ap.add_argument("--contigs", type=int, default=1)
+ap.add_argument("--families", type=int, default=200)
 args = ap.parse_args()
-g = snapgpu.Genome.synthetic(args.genome_bases, seed=2121, n_contigs=1, n_repeat_families=200)
+# C2 defaults; C3 (bench --workload c3): --genome-bases 3100000000 --contigs 25 --families 2000
+g = snapgpu.Genome.synthetic(args.genome_bases, seed=2121, n_contigs=args.contigs, n_repeat_families=args.families)
 reads = snapgpu.Reads.synthetic(g, args.reads, seed=99)
 idx = snapgpu.GenomeIndex.build(g, 20, 16)
+del g   # the index keeps its genome
 al = snapgpu.BaseAligner(idx, device=0)
 dev = al.upload(reads)
 dev.run(); dev.synchronize()
