@@ -878,26 +878,37 @@ int hostMapq(double pAll, double pBest, int score, int popular) {   // mapq.h:32
 // (snapgpu_reads_upload / snapgpu_align_resident); snapgpu_align_batch alternates chunks
 // over both lanes so one chunk's copies and host tail overlap the other chunk's kernels,
 // and the second lane's kernel fills the first one's tail.
-struct ExecLane {
-    hipStream_t stream = nullptr;
-    void *arena = nullptr;
-    uint32_t *counter = nullptr;               // [0] pass-1 work, [1] pass-2 work, [2] deferred count
-    unsigned long long *lookupStats = nullptr; // seed_lookup_kernel: [256][4] seeds, probes, overflow counts (per call)
-    hipEvent_t done = nullptr;                 // chunk records back in host memory
-    // chunk buffers of the pipelined snapgpu_align_batch (grown on demand)
-    uint64_t capReads = 0, capBytes = 0;
-    char *dBases = nullptr, *dQuals = nullptr;
+// One chunk's input/output staging of the pipelined snapgpu_align_batch.  Two per lane: the
+// H2D of a lane's next chunk (on the aligner's copy stream) runs while the lane's current chunk
+// is still in its kernels, so the lane's next kernel can start the moment the current one ends.
+struct ChunkSlot {
+    char *dBases = nullptr, *dQuals = nullptr;  // device inputs
     uint64_t *dOffsets = nullptr;
-    uint32_t *dLengths = nullptr, *dDefer = nullptr;
-    snapgpu_result_t *dOut = nullptr;
-    SeedRec *dSeeds = nullptr;
+    uint32_t *dLengths = nullptr;
     uint64_t *hOffsets = nullptr;               // pinned staging
     uint32_t *hLengths = nullptr;
     snapgpu_result_t *hOut = nullptr;
-    unsigned long long *hLookupStats = nullptr; // pinned copy of lookupStats
+    hipEvent_t h2d = nullptr;                   // inputs on the device (copy stream)
+    hipEvent_t done = nullptr;                  // records back in host memory (lane stream)
     bool pending = false;
-    uint64_t chunkBegin = 0, chunkN = 0, chunkEv = 0;
+    uint64_t seq = 0, chunkBegin = 0, chunkN = 0, chunkEv = 0;
     snapgpu_result_t *chunkOut = nullptr;       // the caller's record array of the pending chunk
+};
+
+struct ExecLane {
+    hipStream_t stream = nullptr;
+    void *arena = nullptr;
+    uint32_t *counter = nullptr;               // [0] pass-1 work, [1] pass-3 work, [2] pass-1 defers, [3] pass-2 work, [4] pass-2 defers
+    unsigned long long *lookupStats = nullptr; // seed_lookup_kernel: [256][4] seeds, probes, overflow counts (per call)
+    hipEvent_t done = nullptr;                 // scratch event: waitLane, cross-lane ordering
+    // chunk buffers of the pipelined snapgpu_align_batch (grown on demand)
+    uint64_t capReads = 0, capBytes = 0;
+    uint32_t *dDefer = nullptr;
+    snapgpu_result_t *dOut = nullptr;
+    SeedRec *dSeeds = nullptr;
+    ChunkSlot slot[2];
+    uint32_t nextSlot = 0;
+    unsigned long long *hLookupStats = nullptr; // pinned copy of lookupStats
 };
 
 // Timing events of one pass set (one chunk) and the pinned copy of its work counters.
@@ -943,6 +954,8 @@ struct snapgpu_aligner {
     // snapgpu_align_batch_wait; timing and statistics cover that whole stream
     bool streamOpen = false;
     uint64_t nextLane = 0;
+    uint64_t chunkSeq = 0;        // submission order of pipelined chunks (finished oldest first)
+    hipStream_t copyStream = nullptr;   // H2D of the pipelined chunks
     std::chrono::steady_clock::time_point streamStart;
     uint64_t arenaElems = 0;
     int grid = 0, grid256 = 0, grid512 = 0;
@@ -1183,14 +1196,14 @@ int snapgpu_device_count(void) {
 }
 
 static void freeLaneChunkBuffers(snapgpu_aligner_t *a, ExecLane &L) {
-    devFree(a, L.dBases); devFree(a, L.dQuals); devFree(a, L.dOffsets); devFree(a, L.dLengths);
     devFree(a, L.dDefer); devFree(a, L.dOut); devFree(a, L.dSeeds);
-    L.dBases = L.dQuals = nullptr; L.dOffsets = nullptr; L.dLengths = L.dDefer = nullptr; L.dOut = nullptr;
-    L.dSeeds = nullptr;
-    if (!a->failed) {
-        hostPinnedFree(L.hOffsets); hostPinnedFree(L.hLengths); hostPinnedFree(L.hOut);
+    L.dDefer = nullptr; L.dOut = nullptr; L.dSeeds = nullptr;
+    for (ChunkSlot &S : L.slot) {
+        devFree(a, S.dBases); devFree(a, S.dQuals); devFree(a, S.dOffsets); devFree(a, S.dLengths);
+        S.dBases = S.dQuals = nullptr; S.dOffsets = nullptr; S.dLengths = nullptr;
+        if (!a->failed) { hostPinnedFree(S.hOffsets); hostPinnedFree(S.hLengths); hostPinnedFree(S.hOut); }
+        S.hOffsets = nullptr; S.hLengths = nullptr; S.hOut = nullptr;
     }
-    L.hOffsets = nullptr; L.hLengths = nullptr; L.hOut = nullptr;
     L.capReads = L.capBytes = 0;
 }
 
@@ -1210,8 +1223,13 @@ void snapgpu_aligner_free(snapgpu_aligner_t *a) {
         devFree(a, L.arena); devFree(a, L.counter); devFree(a, L.lookupStats);
         hostPinnedFree(L.hLookupStats);
         if (L.done) hipEventDestroy(L.done);
+        for (ChunkSlot &S : L.slot) {
+            if (S.h2d) hipEventDestroy(S.h2d);
+            if (S.done) hipEventDestroy(S.done);
+        }
         if (L.stream) hipStreamDestroy(L.stream);
     }
+    if (a->copyStream) { hipStreamSynchronize(a->copyStream); hipStreamDestroy(a->copyStream); }
     for (auto &v : a->evs) {
         for (auto &e : v.e) if (e) hipEventDestroy(e);
         hostPinnedFree(v.hCounter);
@@ -1248,11 +1266,16 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
     for (auto &L : a->lane) {
         if ((e = hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking)) != hipSuccess) return fail("stream", e);
         if ((e = hipEventCreateWithFlags(&L.done, hipEventDisableTiming)) != hipSuccess) return fail("event", e);
+        for (ChunkSlot &S : L.slot)
+            if ((e = hipEventCreateWithFlags(&S.h2d, hipEventDisableTiming)) != hipSuccess ||
+                (e = hipEventCreateWithFlags(&S.done, hipEventDisableTiming)) != hipSuccess)
+                return fail("event", e);
         if ((e = hipMalloc(&L.counter, 64)) != hipSuccess) return fail("counter", e);
         if ((e = hipMalloc(&L.lookupStats, 1024 * sizeof(unsigned long long))) != hipSuccess) return fail("lookup stats", e);
         if ((e = hipHostMalloc(&L.hLookupStats, 1024 * sizeof(unsigned long long), hipHostMallocDefault)) != hipSuccess)
             return fail("pinned lookup stats", e);
     }
+    if ((e = hipStreamCreateWithFlags(&a->copyStream, hipStreamNonBlocking)) != hipSuccess) return fail("stream", e);
     for (auto &ev : a->cev) if ((e = hipEventCreate(&ev)) != hipSuccess) return fail("event", e);
     if ((e = hipGetSymbolAddress((void **)&a->dDiag, HIP_SYMBOL(g_diag))) != hipSuccess) return fail("g_diag", e);
     if ((e = ensureDeviceTables(device)) != hipSuccess) return fail("device tables", e);
@@ -1664,18 +1687,20 @@ static int ensureLaneCapacity(snapgpu_aligner_t *a, ExecLane &L, uint64_t reads,
     freeLaneChunkBuffers(a, L);
     reads = std::max<uint64_t>(reads, 1024);
     const uint64_t cb = bytes + 512;   // zero slack past the last read: over-reading loads stay inside
-    HIPCHK(hipMalloc(&L.dBases, cb));
-    HIPCHK(hipMalloc(&L.dQuals, cb));
-    HIPCHK(hipMemset(L.dBases, 0, cb));
-    HIPCHK(hipMemset(L.dQuals, 0, cb));
-    HIPCHK(hipMalloc(&L.dOffsets, (reads + 1) * 8));
-    HIPCHK(hipMalloc(&L.dLengths, (reads + 1) * 4));
+    for (ChunkSlot &S : L.slot) {
+        HIPCHK(hipMalloc(&S.dBases, cb));
+        HIPCHK(hipMalloc(&S.dQuals, cb));
+        HIPCHK(hipMemset(S.dBases, 0, cb));
+        HIPCHK(hipMemset(S.dQuals, 0, cb));
+        HIPCHK(hipMalloc(&S.dOffsets, (reads + 1) * 8));
+        HIPCHK(hipMalloc(&S.dLengths, (reads + 1) * 4));
+        HIPCHK(hipHostMalloc(&S.hOffsets, (reads + 1) * 8, hipHostMallocDefault));
+        HIPCHK(hipHostMalloc(&S.hLengths, (reads + 1) * 4, hipHostMallocDefault));
+        HIPCHK(hipHostMalloc(&S.hOut, (reads + 1) * sizeof(snapgpu_result_t), hipHostMallocDefault));
+    }
     HIPCHK(hipMalloc(&L.dDefer, 2 * (reads + 1) * 4));   // pass-1 and pass-2 defer lists
     HIPCHK(hipMalloc(&L.dOut, (reads + 1) * sizeof(snapgpu_result_t)));
     HIPCHK(hipMalloc(&L.dSeeds, (reads + 8) * SEEDS_PER_READ * sizeof(SeedRec)));
-    HIPCHK(hipHostMalloc(&L.hOffsets, (reads + 1) * 8, hipHostMallocDefault));
-    HIPCHK(hipHostMalloc(&L.hLengths, (reads + 1) * 4, hipHostMallocDefault));
-    HIPCHK(hipHostMalloc(&L.hOut, (reads + 1) * sizeof(snapgpu_result_t), hipHostMallocDefault));
     L.capReads = reads;
     L.capBytes = bytes;
     return SNAPGPU_OK;
@@ -1684,7 +1709,7 @@ static int ensureLaneCapacity(snapgpu_aligner_t *a, ExecLane &L, uint64_t reads,
 // The host tail of one chunk: wait for its records, account its kernel times, then MAPQ
 // fix-ups, statistics and the copy into the caller's array (host threads, while the GPU
 // already runs the next chunks).
-static int finishChunk(snapgpu_aligner_t *a, ExecLane &L) {
+static int finishChunk(snapgpu_aligner_t *a, ChunkSlot &L) {
     if (!L.pending) return SNAPGPU_OK;
     snapgpu_result_t *out = L.chunkOut;
     L.pending = false;
@@ -1731,6 +1756,34 @@ static int finishChunk(snapgpu_aligner_t *a, ExecLane &L) {
     return SNAPGPU_OK;
 }
 
+// The host tail of the oldest pipelined chunk still pending (any lane); false if none.
+static int finishOldest(snapgpu_aligner_t *a, bool *any) {
+    ChunkSlot *o = nullptr;
+    for (auto &L : a->lane)
+        for (ChunkSlot &S : L.slot)
+            if (S.pending && (!o || S.seq < o->seq)) o = &S;
+    *any = o != nullptr;
+    return o ? finishChunk(a, *o) : SNAPGPU_OK;
+}
+
+static int finishAll(snapgpu_aligner_t *a) {
+    for (bool any = true; any;) {
+        const int rc = finishOldest(a, &any);
+        if (rc) return rc;
+    }
+    return SNAPGPU_OK;
+}
+
+// After an error: nothing may stay in flight on the chunk buffers (unless a timeout made that impossible).
+static void abandonChunks(snapgpu_aligner_t *a) {
+    for (auto &L : a->lane) {
+        for (ChunkSlot &S : L.slot) S.pending = false;
+        if (!a->failed) waitLane(a, L);
+    }
+    if (!a->failed && a->copyStream) (void)hipStreamSynchronize(a->copyStream);
+    a->streamOpen = false;
+}
+
 // Batched BaseAligner::AlignRead over host buffers (SURVEY.md 8(d) d1 boundary): the reads are
 // cut into chunks that alternate over the two execution lanes -- H2D of the chunk's bytes,
 // offsets and lengths, the three passes, D2H of its records into pinned staging -- and the
@@ -1764,41 +1817,50 @@ int snapgpu_align_batch_submit(snapgpu_aligner_t *a, const snapgpu_reads_t *read
         maxSpan = std::max(maxSpan, hi[c] - lo[c]);
     }
     const uint64_t hostEnd = reads->totalBytes + 64;   // allocated and zeroed past the last read
-    for (auto &L : a->lane)
-        if (std::min(per, n) > L.capReads || maxSpan + 64 > L.capBytes) {   // grow: its pending chunk first
-            if ((rc = finishChunk(a, L)) || (rc = ensureLaneCapacity(a, L, std::min(per, n), maxSpan + 64))) return rc;
-        }
+    bool grow = false;
+    for (auto &L : a->lane) grow |= std::min(per, n) > L.capReads || maxSpan + 64 > L.capBytes;
+    if (grow) {   // every pending chunk first (their buffers are reallocated)
+        if ((rc = finishAll(a))) { abandonChunks(a); return rc; }
+        for (auto &L : a->lane)
+            if ((rc = ensureLaneCapacity(a, L, std::min(per, n), maxSpan + 64))) { abandonChunks(a); return rc; }
+    }
     for (uint64_t c = 0; c < nChunks && rc == SNAPGPU_OK; c++) {
         const int li = (int)(a->nextLane++ & 1);
         ExecLane &L = a->lane[li];
-        if ((rc = finishChunk(a, L))) break;   // the lane's previous chunk: its buffers are free again
+        ChunkSlot &S = L.slot[L.nextSlot];
+        L.nextSlot ^= 1u;
+        // the chunk that last used this slot (4 chunks back) is finished first, oldest first
+        for (bool any = true; S.pending && any;)
+            if ((rc = finishOldest(a, &any))) break;
+        if (rc) break;
         const uint64_t b = c * per, m = std::min(n, b + per) - b;
         for (uint64_t i = 0; i < m; i++) {
-            L.hOffsets[i] = reads->offsets[b + i] - lo[c];
-            L.hLengths[i] = reads->lengths[b + i];
+            S.hOffsets[i] = reads->offsets[b + i] - lo[c];
+            S.hLengths[i] = reads->lengths[b + i];
         }
         const uint64_t span = std::min(hi[c] + 64, std::max(hostEnd, hi[c])) - lo[c];
-        hipStream_t s = L.stream;
-        HIPCHK(hipMemcpyAsync(L.dBases, reads->bases + lo[c], span, hipMemcpyHostToDevice, s));
-        HIPCHK(hipMemcpyAsync(L.dQuals, reads->quals + lo[c], span, hipMemcpyHostToDevice, s));
-        HIPCHK(hipMemcpyAsync(L.dOffsets, L.hOffsets, m * 8, hipMemcpyHostToDevice, s));
-        HIPCHK(hipMemcpyAsync(L.dLengths, L.hLengths, m * 4, hipMemcpyHostToDevice, s));
-        PassIO io{L.dBases, L.dQuals, L.dOffsets, L.dLengths, m, L.dOut, L.dDefer, L.dDefer + (L.capReads + 1), L.dSeeds};
+        // inputs on the copy stream: they land while the lane's previous chunk is still running
+        hipStream_t cs = a->copyStream, s = L.stream;
+        HIPCHK(hipMemcpyAsync(S.dBases, reads->bases + lo[c], span, hipMemcpyHostToDevice, cs));
+        HIPCHK(hipMemcpyAsync(S.dQuals, reads->quals + lo[c], span, hipMemcpyHostToDevice, cs));
+        HIPCHK(hipMemcpyAsync(S.dOffsets, S.hOffsets, m * 8, hipMemcpyHostToDevice, cs));
+        HIPCHK(hipMemcpyAsync(S.dLengths, S.hLengths, m * 4, hipMemcpyHostToDevice, cs));
+        HIPCHK(hipEventRecord(S.h2d, cs));
+        HIPCHK(hipStreamWaitEvent(s, S.h2d, 0));
+        PassIO io{S.dBases, S.dQuals, S.dOffsets, S.dLengths, m, L.dOut, L.dDefer, L.dDefer + (L.capReads + 1), L.dSeeds};
         EvSet *ev = nextEvSet(a);
         if (!ev) { rc = SNAPGPU_EDEVICE; break; }
         if ((rc = launch_passes(a, li, io, AlignExt(), *ev, a->nEvUsed >= 2 ? &a->evs[a->nEvUsed - 2] : nullptr))) break;
-        HIPCHK(hipMemcpyAsync(L.hOut, L.dOut, m * sizeof(snapgpu_result_t), hipMemcpyDeviceToHost, s));
-        HIPCHK(hipEventRecord(L.done, s));
-        L.pending = true;
-        L.chunkBegin = b;
-        L.chunkN = m;
-        L.chunkEv = a->nEvUsed - 1;
-        L.chunkOut = out;
+        HIPCHK(hipMemcpyAsync(S.hOut, L.dOut, m * sizeof(snapgpu_result_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipEventRecord(S.done, s));
+        S.pending = true;
+        S.seq = a->chunkSeq++;
+        S.chunkBegin = b;
+        S.chunkN = m;
+        S.chunkEv = a->nEvUsed - 1;
+        S.chunkOut = out;
     }
-    if (rc) {   // leave no chunk in flight on these buffers (unless a timeout made that impossible)
-        for (auto &L : a->lane) { L.pending = false; if (!a->failed) waitLane(a, L); }
-        a->streamOpen = false;
-    }
+    if (rc) abandonChunks(a);
     return rc;
 }
 
@@ -1806,12 +1868,10 @@ int snapgpu_align_batch_wait(snapgpu_aligner_t *a) {
     if (!a) return SNAPGPU_EINVAL;
     if (!a->streamOpen) return a->failed ? SNAPGPU_EDEVICE : SNAPGPU_OK;
     HIPCHK(hipSetDevice(a->device));
-    int rc = SNAPGPU_OK;
-    // the older pending chunk first: the next chunk would go to lane nextLane & 1
-    for (uint64_t k = 0; k < 2 && rc == SNAPGPU_OK; k++) rc = finishChunk(a, a->lane[(a->nextLane + k) & 1]);
+    int rc = finishAll(a);   // oldest first
     a->streamOpen = false;
     if (rc) {
-        for (auto &L : a->lane) { L.pending = false; if (!a->failed) waitLane(a, L); }
+        abandonChunks(a);
         return rc;
     }
     accountBusy(a);
