@@ -959,7 +959,11 @@ struct snapgpu_aligner {
     std::chrono::steady_clock::time_point streamStart;
     uint64_t arenaElems = 0;
     int grid = 0, grid256 = 0, grid512 = 0;
-    uint64_t chunkReads = 262144; // snapgpu_align_batch chunk (SNAPGPU_CHUNK_READS)
+    // snapgpu_align_batch chunk (SNAPGPU_CHUNK_READS): a streaming caller's 1M-read batches go
+    // as one chunk each, alternating lanes (fewest persistent-kernel tails; A/B in
+    // profiles/r02/ab/chunk_size_slots.txt); resident runs keep 2^18-read chunks over both lanes
+    uint64_t chunkReads = 1u << 20;
+    uint64_t residentChunk = 1u << 18;
     snapgpu_timing_t timing{};
     snapgpu_aligner_stats_t stats{};
     snapgpu_device_reads_t *lastReads = nullptr;
@@ -1580,7 +1584,7 @@ static int launch_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, cons
     if (rc) return rc;
     const bool ext = x.search || x.maxHitsToGet;
     const uint64_t n = d->n;
-    const uint64_t nChunks = ext || n == 0 ? 1 : (n + a->chunkReads - 1) / a->chunkReads;
+    const uint64_t nChunks = ext || n == 0 ? 1 : (n + a->residentChunk - 1) / a->residentChunk;
     const uint64_t per = (n + nChunks - 1) / nChunks;
     for (uint64_t c = 0; c < nChunks; c++) {
         const uint64_t b = c * per, m = std::min(n, b + per) - b;
@@ -1894,11 +1898,16 @@ int snapgpu_align_batch(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, snap
     return snapgpu_align_batch_wait(a);
 }
 
-int snapgpu_align_batch_ex(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, const snapgpu_search_t *search,
-                           uint32_t maxHitsToGet, snapgpu_result_t *out, int32_t *multiHitsFound,
-                           snapgpu_multi_hit_t *multiHits) {
+// The extended AlignRead over a batch with the multi-hits returned packed: read i's hits are
+// packed[off[i] .. off[i+1]) (off has n + 1 entries).  snapgpu_align_batch_ex scatters them into
+// the caller's rows; the RNA path reads them packed (a row layout of 1000 hits per read would
+// fault in ~8 KB of fresh host pages per read for a handful of hits).
+extern "C++" int snapgpu_internal_align_batch_packed(snapgpu_aligner_t *a, const snapgpu_reads_t *reads,
+                                                     const snapgpu_search_t *search, uint32_t maxHitsToGet,
+                                                     snapgpu_result_t *out, int32_t *multiHitsFound,
+                                                     std::vector<uint64_t> &off, std::vector<snapgpu_multi_hit_t> &dense) {
     if (!a || !reads || !out) return SNAPGPU_EINVAL;
-    if (maxHitsToGet > SNAPGPU_MAX_MULTI_HITS_TO_GET || (maxHitsToGet && (!multiHitsFound || !multiHits))) {
+    if (maxHitsToGet > SNAPGPU_MAX_MULTI_HITS_TO_GET || (maxHitsToGet && !multiHitsFound)) {
         snapgpu::setError("align_batch_ex: maxHitsToGet must be <= 1024 and come with multiHitsFound/multiHits");
         return SNAPGPU_EINVAL;
     }
@@ -1963,9 +1972,9 @@ int snapgpu_align_batch_ex(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, c
     if (!rc && maxHitsToGet) {
         // only the found hits cross PCIe: counts first, then the hits packed on the device
         void *dOff = nullptr, *dDense = nullptr;
-        std::vector<uint64_t> off(n + 1, 0);
+        off.assign(n + 1, 0);
         e = hipStreamSynchronize(a->stream());
-        std::vector<snapgpu_multi_hit_t> dense;
+        dense.clear();
         if (e == hipSuccess) e = hipMemcpy(multiHitsFound, dFound, n * sizeof(int32_t), hipMemcpyDeviceToHost);
         if (e == hipSuccess) {
             for (uint64_t i = 0; i < n; i++) {
@@ -1989,11 +1998,6 @@ int snapgpu_align_batch_ex(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, c
                                             hipMemcpyDeviceToHost, a->stream())) == hipSuccess)
                         e = hipStreamSynchronize(a->stream());
                 }
-                if (e == hipSuccess)
-                    for (uint64_t i = 0; i < n; i++)
-                        if (off[i + 1] > off[i])
-                            memcpy(multiHits + i * maxHitsToGet, dense.data() + off[i],
-                                   (off[i + 1] - off[i]) * sizeof(snapgpu_multi_hit_t));
             }
         }
         if (e != hipSuccess) {
@@ -2003,6 +2007,23 @@ int snapgpu_align_batch_ex(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, c
     }
     cleanup();
     return rc;
+}
+
+int snapgpu_align_batch_ex(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, const snapgpu_search_t *search,
+                           uint32_t maxHitsToGet, snapgpu_result_t *out, int32_t *multiHitsFound,
+                           snapgpu_multi_hit_t *multiHits) {
+    if (maxHitsToGet && (!multiHitsFound || !multiHits)) {
+        snapgpu::setError("align_batch_ex: maxHitsToGet must be <= 1024 and come with multiHitsFound/multiHits");
+        return SNAPGPU_EINVAL;
+    }
+    std::vector<uint64_t> off;
+    std::vector<snapgpu_multi_hit_t> dense;
+    const int rc = snapgpu_internal_align_batch_packed(a, reads, search, maxHitsToGet, out, multiHitsFound, off, dense);
+    if (rc || !maxHitsToGet) return rc;
+    for (uint64_t i = 0; i < reads->n; i++)
+        if (off[i + 1] > off[i])
+            memcpy(multiHits + i * maxHitsToGet, dense.data() + off[i], (off[i + 1] - off[i]) * sizeof(snapgpu_multi_hit_t));
+    return SNAPGPU_OK;
 }
 
 // Diagnostic self-test of the timeout path (no GPU needed): an aligner whose event never

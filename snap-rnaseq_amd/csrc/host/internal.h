@@ -132,6 +132,14 @@ struct GtfPairQuery {
     uint32_t tstart1, start1, len1;
 };
 
+}  // namespace snapgpu
+// aligner.hip: snapgpu_align_batch_ex with the multi-hits packed (read i: dense[off[i] .. off[i+1]))
+int snapgpu_internal_align_batch_packed(snapgpu_aligner_t *a, const snapgpu_reads_t *reads,
+                                        const snapgpu_search_t *search, uint32_t maxHitsToGet,
+                                        snapgpu_result_t *out, int32_t *multiHitsFound, std::vector<uint64_t> &off,
+                                        std::vector<snapgpu_multi_hit_t> &dense);
+namespace snapgpu {
+
 // xoshiro256** seeded with splitmix64: deterministic on every host.
 struct Rng {
     uint64_t s[4];

@@ -408,17 +408,17 @@ int snapgpu_rna_paired_align(snapgpu_paired_aligner_t *pa, snapgpu_aligner_t *ta
     const uint32_t mh = opt->maxHitsToGet;
     std::vector<snapgpu_result_t> tr[2];
     std::vector<int32_t> tf[2];
-    // rows of mh hits per read; only the found prefix of a row is written (and read), so the
-    // arrays are left uninitialised (no zero-fill of nu * mh entries)
-    std::unique_ptr<snapgpu_multi_hit_t[]> th[2];
+    std::vector<uint64_t> thOff[2];              // read j's hits: th[k][thOff[k][j] .. thOff[k][j + 1])
+    std::vector<snapgpu_multi_hit_t> th[2];
     std::vector<snapgpu_pair_result_t> gr(nu + 1);
     st.prepMs = msSince(w0);
     auto t0 = std::chrono::steady_clock::now();
     if (nu) {
         // transcriptomeAligner->AlignRead(read0 / read1, ..., maxHitsToGet 1000, multiHits) (:601-605)
         for (int k = 0; k < 2; k++) {
-            tr[k].resize(nu); tf[k].resize(nu); th[k].reset(new snapgpu_multi_hit_t[nu * (uint64_t)mh]);
-            if ((rc = snapgpu_align_batch_ex(ta, U[k], nullptr, mh, tr[k].data(), tf[k].data(), th[k].get())))
+            tr[k].resize(nu); tf[k].resize(nu);
+            if ((rc = snapgpu_internal_align_batch_packed(ta, U[k], nullptr, mh, tr[k].data(), tf[k].data(), thOff[k],
+                                                          th[k])))
                 return fail(rc);
         }
         // g_aligner->align(read0, read1, &result) (:625)
@@ -437,8 +437,8 @@ int snapgpu_rna_paired_align(snapgpu_paired_aligner_t *pa, snapgpu_aligner_t *ta
             mate0.clear(); mate1.clear();
             const uint32_t len0 = ul[0][j], len1 = ul[1][j];
             for (int k = 0; k < 2; k++)
-                for (int32_t h = 0; h < tf[k][j]; h++) {
-                    const snapgpu_multi_hit_t &m = th[k][j * (uint64_t)mh + h];
+                for (uint64_t h = thOff[k][j]; h < thOff[k][j + 1]; h++) {
+                    const snapgpu_multi_hit_t &m = th[k][h];
                     addAlignment(C, mate0, mate1, m.location, m.direction, m.score, 0, true, k == 1, len0, len1, errs[t]);
                 }
             const snapgpu_pair_result_t &g = gr[j];

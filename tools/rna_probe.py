@@ -42,7 +42,12 @@ def main():
         r1.clip(3)
         out = {"pairs": n}
         out["transcriptome_ex_end0_ms"] = best(lambda: ta.AlignReadsEx(r0, maxHitsToGet=1000))
+        out["transcriptome_ex_timing"] = {k: round(v, 2) if isinstance(v, float) else v for k, v in ta.timing().items()
+                                          if k in ("mainKernelMs", "spillKernelMs", "lookupKernelMs", "nSpilled", "nByteReads")}
+        out["transcriptome_ex0_end0_ms"] = best(lambda: ta.AlignReadsEx(r0, maxHitsToGet=0))
         out["transcriptome_plain_end0_ms"] = best(lambda: ta.AlignReads(r0))
+        out["transcriptome_plain_timing"] = {k: round(v, 2) if isinstance(v, float) else v for k, v in ta.timing().items()
+                                             if k in ("mainKernelMs", "spillKernelMs", "lookupKernelMs", "nSpilled", "nByteReads")}
         out["paired_align_ms"] = best(lambda: pa.align(r0, r1))
         out["paired_intersect_ms"] = best(lambda: pa.intersect(r0, r1))
         ga = snapgpu.BaseAligner(idx, maxHitsToConsider=16000, maxK=15, maxSeedsToUse=8, extraSearchDepth=2)
