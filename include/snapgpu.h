@@ -50,9 +50,11 @@ enum { SNAPGPU_FORWARD = 0, SNAPGPU_RC = 1 };
 /* per-read flags in snapgpu_result_t.flags */
 #define SNAPGPU_FLAG_READ_TOO_LONG  0x01u  /* reference: soft_exit(1), BaseAligner.cpp:609-613 */
 #define SNAPGPU_FLAG_MAPQ_FIXED     0x02u  /* MAPQ re-derived on host with libm log10 (boundary case) */
-#define SNAPGPU_FLAG_DEFERRED       0x04u  /* aligned by the byte-compare pass (read > 128 bases, or IUPAC
-                                              codes in both read and genome): align_kernel<512> */
+#define SNAPGPU_FLAG_DEFERRED       0x04u  /* left pass 1 (read > 128 bases, or IUPAC codes in both read and
+                                              genome): aligned by align_kernel<256> or align_kernel<512> */
 #define SNAPGPU_FLAG_TOO_MANY_NS    0x08u  /* countOfNs > maxK (BaseAligner.cpp:652-655) */
+#define SNAPGPU_FLAG_BYTE_PATH      0x10u  /* aligned by the byte-compare pass 3, align_kernel<512> (read
+                                              > 256 bases, or IUPAC codes in both read and genome) */
 
 /*
  * Result of one AlignRead call (BaseAligner.cpp:510-938).  location / direction /
@@ -551,7 +553,7 @@ typedef struct snapgpu_pair_result {
 } snapgpu_pair_result_t;   /* 64 bytes */
 #define SNAPGPU_PFLAG_POOL_EXHAUSTED 0x01   /* the reference soft_exits ("Ran out of ... pool entries") */
 #define SNAPGPU_PFLAG_READ_TOO_LONG  0x02   /* the reference soft_exits (IntersectingPairedEndAligner.cpp:211-215) */
-#define SNAPGPU_PFLAG_DEFERRED       0x04   /* aligned by the second (large-pool / long-read) pass */
+#define SNAPGPU_PFLAG_DEFERRED       0x04   /* left pass 1: aligned by the long-read pass or the large-pool pass */
 #define SNAPGPU_PFLAG_MAPQ_FIXED     0x08   /* MAPQ re-derived on the host (threshold case) */
 
 void snapgpu_paired_params_default(snapgpu_paired_params_t *p);

@@ -98,6 +98,7 @@ struct KArgs {
     uint32_t maxHits, maxK, maxReadSize, maxSeedsCmd;
     double seedCoverage;
     uint32_t extra, explore, stopOnFirst, kRows;
+    uint32_t radixMin;           // forced mode: radix-sort the pop order of reads with >= this many elements
     const DevTables *tab;
     // reads
     const char *bases;

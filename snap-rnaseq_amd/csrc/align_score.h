@@ -570,6 +570,80 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem1
     return false;
 }
 
+// Forced-mode pop order of a read with many elements: every linked element's (sortkey << 32 |
+// index), sorted ascending by an LSD radix sort (4 passes of 8-bit digits; the keys are unique)
+// in the free tail of the wave's element arena, with an LDS histogram (the idle LV rows).  The
+// pops then read it from the top.  O(n) per pass where the windowed ranks cost O(n^2) per
+// 256-element window.  Returns false (rank path) when the arena tail cannot hold two buffers.
+template <int MAXLEN>
+__device__ __forceinline__ bool forced_sort(const KArgs &A, Lds<MAXLEN> &S, Elem128 *ar, uint32_t nE,
+                                            const uint64_t *&sorted, uint32_t &nLinked) {
+    if (((uint64_t)A.arenaElems - nE) * sizeof(Elem128) < 16ull * nE + 64) return false;
+    uint64_t *bufA = reinterpret_cast<uint64_t *>(ar + nE), *bufB = bufA + nE;
+    uint32_t n = 0;
+    for (uint32_t e0 = 0; e0 < nE; e0 += WAVE) {   // linked elements, compacted in index order
+        const int lane = lane_id();
+        const uint32_t e = e0 + (uint32_t)lane;
+        const uint32_t k = e < nE ? sk_get(S, ar, e) : 0u;
+        const uint64_t m = ballot(k != 0u);
+        if (k) bufA[n + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = ((uint64_t)k << 32) | e;
+        n += (uint32_t)__popcll(m);
+    }
+    wave_sync();
+    uint32_t *hist = reinterpret_cast<uint32_t *>(&S.u.sc.rows8[0][0]);
+    for (int pass = 0; pass < 4; pass++) {
+        const int lane = lane_id();
+        const int sh = 32 + 8 * pass;
+        for (int j = lane; j < 256; j += WAVE) hist[j] = 0u;
+        wave_sync();
+        for (uint32_t i0 = 0; i0 < n; i0 += WAVE) {
+            const uint32_t i = i0 + (uint32_t)lane;
+            if (i < n) atomicAdd(&hist[(uint32_t)(bufA[i] >> sh) & 255u], 1u);
+        }
+        wave_sync();
+        // exclusive prefix over the 256 bins, four per lane
+        const uint32_t h0 = hist[4 * lane], h1 = hist[4 * lane + 1], h2 = hist[4 * lane + 2], h3 = hist[4 * lane + 3];
+        const uint32_t tot = h0 + h1 + h2 + h3;
+        uint32_t incl = tot;
+#pragma unroll
+        for (int o = 1; o < WAVE; o <<= 1) {
+            const uint32_t v = (uint32_t)shfl_idx((int)incl, lane >= o ? lane - o : lane);
+            if (lane >= o) incl += v;
+        }
+        const uint32_t base = incl - tot;
+        wave_sync();
+        hist[4 * lane] = base;
+        hist[4 * lane + 1] = base + h0;
+        hist[4 * lane + 2] = base + h0 + h1;
+        hist[4 * lane + 3] = base + h0 + h1 + h2;
+        wave_sync();
+        // stable scatter: a lane's place among the lanes of its digit from eight ballots
+        for (uint32_t i0 = 0; i0 < n; i0 += WAVE) {
+            const int ln = lane_id();
+            const uint32_t i = i0 + (uint32_t)ln;
+            const bool act = i < n;
+            const uint64_t v = act ? bufA[i] : 0ull;
+            const uint32_t d = (uint32_t)(v >> sh) & 255u;
+            uint64_t peers = ballot(act);
+#pragma unroll
+            for (int b = 0; b < 8; b++) {
+                const uint64_t bb = ballot(act && ((d >> b) & 1u));
+                peers &= ((d >> b) & 1u) ? bb : ~bb;
+            }
+            const uint32_t before = (uint32_t)__popcll(peers & ((1ull << ln) - 1));
+            const uint32_t at = act ? hist[d] : 0u;
+            wave_sync();
+            if (act) bufB[at + before] = v;
+            if (act && before == 0) hist[d] = at + (uint32_t)__popcll(peers);
+            wave_sync();
+        }
+        uint64_t *t = bufA; bufA = bufB; bufB = t;
+    }
+    sorted = bufA;
+    nLinked = n;
+    return true;
+}
+
 // BaseAligner::score (BaseAligner.cpp:977-1399) over batches of popped elements.
 template <bool EXT, int MAXLEN>
 __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, Elem128 *ar, ReadState &st, bool force,
@@ -592,6 +666,7 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, El
     uint16_t *order = S.u.sc.order;
     uint32_t fDone = 0, fAvail = 0, ordBase = 0;
     bool fMore = true;   // a ranking window came back full: elements of lower rank may remain
+    const uint64_t *fSorted = nullptr;   // radix-sorted pop order (reads with >= A.radixMin elements)
     for (uint32_t guard = 0;; guard++) {
         // lane id re-read per batch (volatile asm): masks and addresses derived from it are
         // recomputed in the batch instead of hoisted and kept live, spilled, across the pass loop
@@ -619,6 +694,12 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, El
                 wave_sync();
             }
         } else {
+            if (fDone == 0 && !fSorted && S.nElems >= A.radixMin) {
+                PH_T(A, trs);
+                uint32_t nl = 0;
+                if (forced_sort<MAXLEN>(A, S, ar, S.nElems, fSorted, nl)) { fAvail = nl; fMore = false; }
+                PH_ADD(A, S, PH_RANK, trs);
+            }
             if (fDone == fAvail && fMore) {
                 PH_T(A, trk);
                 PH_CNT(A, S, PH_NELEMSF, fDone == 0 ? S.nElems : 0);
@@ -660,7 +741,9 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, El
                 PH_ADD(A, S, PH_RANK, trk);
             }
             nb = fAvail - fDone < (uint32_t)EB ? fAvail - fDone : (uint32_t)EB;
-            if ((uint32_t)lane < nb) G.eidx[lane] = order[fDone - ordBase + lane];
+            if ((uint32_t)lane < nb)
+                G.eidx[lane] = fSorted ? (uint32_t)fSorted[fAvail - 1 - (fDone + (uint32_t)lane)]
+                                       : (uint32_t)order[fDone - ordBase + lane];
             fDone += nb;
             wave_sync();
         }

@@ -342,6 +342,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
     st.tick = 32;
     st.nSeedsApplied[0] = st.nSeedsApplied[1] = 0;
     uint32_t flags = MAXLEN > 128 ? SNAPGPU_FLAG_DEFERRED : 0u;   // passes 2 and 3 align only deferred reads
+    if constexpr (Lds<MAXLEN>::BYTE_PATH) flags |= SNAPGPU_FLAG_BYTE_PATH;
     int result = SNAPGPU_NOT_FOUND;
     const uint32_t maxSeeds = A.maxSeedsCmd ? A.maxSeedsCmd : (uint32_t)(int)(A.seedCoverage * n / seedLen);
     const uint32_t numWeightLists = maxSeeds + 1;
@@ -964,6 +965,9 @@ struct snapgpu_aligner {
     // profiles/r02/ab/chunk_size_slots.txt); resident runs keep 2^18-read chunks over both lanes
     uint64_t chunkReads = 1u << 20;
     uint64_t residentChunk = 1u << 18;
+    // forced mode: reads with at least this many elements get a radix-sorted pop order instead of
+    // windowed ranks (SNAPGPU_RADIX_MIN; beyond SKCAP the ranks stage keys from HBM per window)
+    uint32_t radixMin = SKCAP + 1;
     snapgpu_timing_t timing{};
     snapgpu_aligner_stats_t stats{};
     snapgpu_device_reads_t *lastReads = nullptr;
@@ -1259,6 +1263,7 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
     a->p = *params;
     if (const char *t = getenv("SNAPGPU_TIMEOUT_S")) a->timeoutSec = atof(t);
     if (const char *t = getenv("SNAPGPU_CHUNK_READS"); t && atoll(t) > 0) a->chunkReads = (uint64_t)atoll(t);
+    if (const char *t = getenv("SNAPGPU_RADIX_MIN"); t && atoll(t) > 0) a->radixMin = (uint32_t)atoll(t);
     if (const char *t = getenv("SNAPGPU_OVERLAP")) a->overlapKernels = atoi(t) != 0;
     auto fail = [&](const char *what, hipError_t e) {
         snapgpu::setError(std::string(what) + ": " + hipGetErrorString(e));
@@ -1451,6 +1456,7 @@ static int launch_passes(snapgpu_aligner_t *a, int li, const PassIO &io, const A
     A.maxHits = a->p.maxHitsToConsider; A.maxK = a->p.maxK; A.maxReadSize = a->p.maxReadSize;
     A.maxSeedsCmd = a->p.maxSeedsToUse; A.seedCoverage = a->p.maxSeedCoverage; A.extra = a->p.extraSearchDepth;
     A.explore = a->p.explorePopularSeeds; A.stopOnFirst = a->p.stopOnFirstHit; A.kRows = 31;
+    A.radixMin = a->radixMin;
     A.tab = a->dTab;
     A.bases = io.bases; A.quals = io.quals; A.offsets = io.offsets; A.lengths = io.lengths;
     A.nReads = (uint32_t)io.n; A.out = io.out;

@@ -21,6 +21,7 @@ UnusedScoreValue = 0xFFFF                                           # BaseAligne
 FLAG_READ_TOO_LONG = 0x01
 FLAG_MAPQ_FIXED = 0x02
 FLAG_DEFERRED = 0x04
+FLAG_BYTE_PATH = 0x10
 FLAG_TOO_MANY_NS = 0x08
 
 RESULT_DTYPE = np.dtype([

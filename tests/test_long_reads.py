@@ -84,6 +84,8 @@ def test_gpu_long_reads_match_reference(gpu_available, small_index, long_reads, 
     iupac = sum(1 for i in range(long_reads.n) if set(long_reads.get(i)[0].upper()) - set(b"ACGTN"))
     assert 0 < iupac < 100
     assert t["nSpilled"] == long_reads.n and t["nByteReads"] == iupac, t
+    assert ((res["flags"] & snapgpu.FLAG_DEFERRED) != 0).all()
+    assert int(((res["flags"] & snapgpu.FLAG_BYTE_PATH) != 0).sum()) == iupac
     bad = _diff(canonical_tsv(res), open(os.path.join(G, f"expected_small_long_{name}.tsv")).read())
     assert not bad, f"{len(bad)} differ, first: {bad[:3]}"
     cpu = oracle_align(small_index, long_reads, al.params, n_threads=4)   # counters too
