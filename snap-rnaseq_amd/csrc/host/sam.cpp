@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstring>
 #include <thread>
+#include <vector>
 
 using namespace snapgpu;
 
@@ -39,6 +40,20 @@ inline char complement(char c) {                                                
 }
 
 // Genome::getPieceAtLocation (Genome.cpp:357-374)
+// upperCase and COMPLEMENT[upperCase(c)] as 256-entry tables (SEQ of forward / RC records)
+struct SeqTables {
+    char up[256], rcUp[256];
+    SeqTables() {
+        for (int c = 0; c < 256; c++) {
+            up[c] = upperCase((char)c);
+            rcUp[c] = complement(upperCase((char)c));
+        }
+    }
+};
+const SeqTables kSeq;
+const char *const kUpper = kSeq.up;
+const char *const kRcUpper = kSeq.rcUp;
+
 int pieceAt(const Genome &g, uint32_t loc) {
     int lo = 0, hi = (int)g.pieceOffsets.size() - 1;
     while (lo <= hi) {
@@ -169,67 +184,92 @@ void samAppendLine(std::string &o, const Genome &g, const SamLine &L) {
         }
         if (pieceIdx >= 0 && pieceIdx == mateIdx) mateName = "=";
     }
-    // QNAME: truncated at the first space (SAM.cpp:1080-1086)
+    // The line is written into a thread-local scratch buffer with raw stores and appended once
+    // (one append per line instead of one per field or digit).
     uint32_t qlen = L.qnameLen ? L.qnameLen : L.idLen;
     if (const void *sp = memchr(L.id, ' ', qlen)) qlen = (uint32_t)((const char *)sp - L.id);
-    o.append(L.id, qlen);
-    o += '\t';
-    appendInt(o, flags);
-    o += '\t';
-    o += pieceName;
-    o += '\t';
-    appendUint(o, pos);
-    o += '\t';
-    appendInt(o, mapq);
-    o += '\t';
+    const size_t pieceLen = strlen(pieceName), mateLen = strlen(mateName), rgLen = L.rg ? strlen(L.rg) : 0;
+    const uint32_t len = L.fullLen;
+    const uint32_t n = len < 1024 ? len : 1024;
+    const size_t bound = qlen + pieceLen + mateLen + rgLen + (L.cigar ? L.cigar->size() : 0) + 12 * (size_t)L.nOps +
+                         2 * (size_t)n + 256;
+    thread_local std::vector<char> scratch;
+    if (scratch.size() < bound) scratch.resize(bound * 2);
+    char *w = scratch.data();
+    auto put = [&w](const char *p, size_t k) { memcpy(w, p, k); w += k; };
+    auto putU = [&w](uint64_t v) {
+        char b[24];
+        int k = 0;
+        do { b[k++] = (char)('0' + v % 10); v /= 10; } while (v);
+        while (k) *w++ = b[--k];
+    };
+    auto putI = [&](int64_t v) {
+        if (v < 0) { *w++ = '-'; putU((uint64_t)(-v)); }
+        else putU((uint64_t)v);
+    };
+    put(L.id, qlen);
+    *w++ = '\t';
+    putI(flags);
+    *w++ = '\t';
+    put(pieceName, pieceLen);
+    *w++ = '\t';
+    putU(pos);
+    *w++ = '\t';
+    putI(mapq);
+    *w++ = '\t';
     // CIGAR: computed at writeRead's own location (even for NotFound) -- SAM.cpp:1041-1066
     const int32_t ed = L.loc != kInvalidLocation ? L.ed : -1;
     if (L.loc != kInvalidLocation && L.cigar) {
-        o += *L.cigar;   // transcriptome record: insertSpliceJunctions output (may be empty)
+        put(L.cigar->data(), L.cigar->size());   // transcriptome record: insertSpliceJunctions output (may be empty)
     } else if (L.loc != kInvalidLocation && ed >= 0) {
         // soft clips around the CIGAR (computeCigarString, SAM.cpp:1212-1226); for RC the
         // clipped-before count is the read's back clip (getSAMData, SAM.cpp:870-872)
         const uint32_t back = L.fullLen - L.clippedLen - L.front;
         const uint32_t before = rc ? back : L.front, after = rc ? L.front : back;
-        if (before) { appendUint(o, before); o += 'S'; }
+        if (before) { putU(before); *w++ = 'S'; }
         for (uint32_t k = 0; k < L.nOps; k++) {
-            appendUint(o, L.ops[k] >> 4);
-            o += kOp[L.ops[k] & 15];
+            putU(L.ops[k] >> 4);
+            *w++ = kOp[L.ops[k] & 15];
         }
-        if (after) { appendUint(o, after); o += 'S'; }
+        if (after) { putU(after); *w++ = 'S'; }
     } else {
-        o += '*';
+        *w++ = '*';
     }
+    *w++ = '\t';
+    put(mateName, mateLen);
+    *w++ = '\t';
+    putU(matePos);
+    *w++ = '\t';
+    putI(tlen);
+    *w++ = '\t';
     // SEQ / QUAL are printed with "%.*s" (SAM.cpp:1122-1136): a NUL byte ends them early
     // (COMPLEMENT[] of a non-ACGTN base is 0; a quality string shorter than the read)
-    o += '\t';
-    o += mateName;
-    o += '\t';
-    appendUint(o, matePos);
-    o += '\t';
-    appendInt(o, tlen);
-    o += '\t';
-    char sq[2 * 1024];
-    const uint32_t len = L.fullLen;
-    const uint32_t n = len < 1024 ? len : 1024;
-    uint32_t ns = 0, nq = 0;
+    const unsigned char *B = reinterpret_cast<const unsigned char *>(L.bases);
     if (rc) {
-        while (ns < n && (sq[ns] = complement(upperCase(L.bases[len - 1 - ns]))) != 0) ns++;
-        while (nq < n && (sq[1024 + nq] = L.quals[len - 1 - nq]) != 0) nq++;
+        for (uint32_t k = 0; k < n; k++) {
+            const char c = kRcUpper[B[len - 1 - k]];
+            if (!c) break;
+            *w++ = c;
+        }
+        *w++ = '\t';
+        for (uint32_t k = 0; k < n && L.quals[len - 1 - k]; k++) *w++ = L.quals[len - 1 - k];
     } else {
-        while (ns < n && (sq[ns] = upperCase(L.bases[ns])) != 0) ns++;
-        while (nq < n && (sq[1024 + nq] = L.quals[nq]) != 0) nq++;
+        for (uint32_t k = 0; k < n; k++) {
+            const char c = kUpper[B[k]];
+            if (!c) break;
+            *w++ = c;
+        }
+        *w++ = '\t';
+        for (uint32_t k = 0; k < n && L.quals[k]; k++) *w++ = L.quals[k];
     }
-    o.append(sq, ns);
-    o += '\t';
-    o.append(sq + 1024, nq);
     if (L.rg) {
-        o += "\tRG:Z:";
-        o += L.rg;
+        put("\tRG:Z:", 6);
+        put(L.rg, rgLen);
     }
-    o += "\tPG:Z:SNAP\tNM:i:";
-    appendInt(o, ed);
-    o += '\n';
+    put("\tPG:Z:SNAP\tNM:i:", 16);
+    putI(ed);
+    *w++ = '\n';
+    o.append(scratch.data(), (size_t)(w - scratch.data()));
 }
 
 }  // namespace snapgpu
@@ -285,10 +325,17 @@ extern "C" int snapgpu_sam_format_clipped(const snapgpu_index_t *idx, const snap
         setError("sam_format: output buffer too small");
         return SNAPGPU_EINVAL;
     }
-    for (auto &p : parts) {
-        memcpy(out, p.data(), p.size());
-        out += p.size();
-    }
+    // each thread copies its own part (the first touch of the caller's pages and ~300 MB of copy
+    // per 1M lines run in parallel, not on one thread after the join)
+    std::vector<uint64_t> at(nt + 1, 0);
+    for (unsigned t = 0; t < nt; t++) at[t + 1] = at[t] + parts[t].size();
+    th.clear();
+    for (unsigned t = 0; t < nt; t++)
+        th.emplace_back([&, t] {
+            memcpy(out + at[t], parts[t].data(), parts[t].size());
+            std::string().swap(parts[t]);
+        });
+    for (auto &x : th) x.join();
     return SNAPGPU_OK;
 }
 
