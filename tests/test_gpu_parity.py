@@ -158,3 +158,21 @@ def test_stream_submit_wait(gpu_available, small_world, monkeypatch):
     assert np.array_equal(dev.results().view(np.uint8), want[2501:3101].view(np.uint8))
     assert np.array_equal(o2.view(np.uint8), want[:2500].view(np.uint8))
     al.wait()   # nothing left: a no-op
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(maxK=20, maxSeedsToUse=40, extraSearchDepth=5),
+                                dict(maxHitsToConsider=16), dict(maxK=2, extraSearchDepth=0)],
+                         ids=["default", "k20", "h16", "k2"])
+def test_forced_radix_order_vs_oracle(gpu_available, small_world, monkeypatch, kw):
+    """Forced-mode pop order from the arena-tail radix sort (score_batched / forced_sort),
+    which production uses for reads with > 256 elements, forced here for every read."""
+    monkeypatch.setenv("SNAPGPU_RADIX_MIN", "1")
+    idx = small_world["index"]
+    reads = snapgpu.Reads.from_list(edge_reads(small_world["genome"]) + [
+        small_world["reads"].get(i) for i in range(3000)])
+    al = snapgpu.BaseAligner(idx, **kw)
+    gpu = al.AlignReads(reads)
+    cpu = oracle_align(idx, reads, al.params)
+    bad = mismatches(gpu, cpu)
+    assert len(bad) == 0, f"{len(bad)} of {len(gpu)} differ\n" + _report(gpu, cpu, reads, bad)
+    assert (gpu["nElements"] >= 8).sum() > 10   # orders of many elements were sorted
