@@ -274,6 +274,10 @@ def main():
     idx, index_info = shared_index.build_once(snapgpu, wl["genome_bases"], gen, 20, build_threads, rank, world, dist)
     t_index = time.time() - t0
     log(rank, f"index ready {index_info}")
+    # one GPU per local rank; more ranks than GPUs (a multi-rank rehearsal on a smaller box) share them
+    ndev = snapgpu.device_count()
+    if ndev > 0:
+        local = local % ndev
     t1 = time.time()
     aligner = snapgpu.BaseAligner(idx, device=local)   # index + genome upload to this GPU's HBM
     t_upload = time.time() - t1

@@ -138,7 +138,9 @@ __device__ __forceinline__ int from_upper_b(int v, bool glast) {
 // distance or -1.  A group that succeeds records its backtrace (LandauVishkin.h:
 // 376-431) in G.pa / G.pm / G.pL0 / G.plen[dx]; the match probability is formed
 // later, only for candidates the scorer applies (lv_prob).
-template <int DIR, int GS, int NW>
+// UNIFORM_K: every lane's limit k equals the row bound kmaxAll (the forward call), so the
+// per-row "limit reached" test is the loop bound.
+template <int DIR, int GS, int NW, bool UNIFORM_K = false>
 __device__ __forceinline__ int lv_group(GroupLdsT<NW> &G, uint8_t (*rows8)[WAVE], const MaskW<NW> &M, bool gact, int q0,
                                         int patternLen, int textLen, int k, int kmaxAll, int &outE) {
     constexpr int NBITS = 64 * NW;
@@ -147,6 +149,7 @@ __device__ __forceinline__ int lv_group(GroupLdsT<NW> &G, uint8_t (*rows8)[WAVE]
     const int li = lane & (GS - 1), gi = lane / GS, c = GS / 2 - 1;
     const bool gfirst = li == 0, glast = li == GS - 1;   // group boundaries of the row shifts
     const int d = DIR > 0 ? li - c : c - li;
+    const int ad = d < 0 ? -d : d;                      // diagonal d is in row e's band iff |d| <= e
     const int pbase = gi * 2 * GS;                       // this group's path slots
     if (k > MAX_K - 1) k = MAX_K - 1;
     outE = -1;
@@ -168,7 +171,7 @@ __device__ __forceinline__ int lv_group(GroupLdsT<NW> &G, uint8_t (*rows8)[WAVE]
     const int enddB = endd + 2, patB = patternLen + 2, q0m2 = q0 - 2;
     int rowsRun = 0;
     for (int e = 1; e <= kmaxAll; e++) {
-        done = e > k ? 1u : done;                       // limit reached: -1
+        if constexpr (!UNIFORM_K) done = e > k ? 1u : done;   // limit reached: -1
         if (ballot(done == 0u) == 0) break;
         rowsRun = e;
         const int lowerB = from_lower_b<GS>(Bp, gfirst), upperB = from_upper_b<GS>(Bp, glast);
@@ -178,7 +181,7 @@ __device__ __forceinline__ int lv_group(GroupLdsT<NW> &G, uint8_t (*rows8)[WAVE]
         // X, then D if strictly greater, then I if strictly greater (only the value is needed here)
         const int bxdB = leftB > x1B ? leftB : x1B;
         const int bestB = rightB > bxdB ? rightB : bxdB;
-        const bool active = !done && d <= e && d >= -e;
+        const bool active = !done && ad <= e;
         // slide along the diagonal (LandauVishkin.h:325-354)
         const int mpos = q0m2 + bestB;
         const int mposc = mpos < NBITS ? mpos : NBITS;
@@ -396,7 +399,7 @@ __device__ __forceinline__ void lv_pass(const KArgs &A, Lds<MAXLEN> &S, uint32_t
     PH_ADD(A, S, PH_STAGE, tst);
     PH_T(A, tf);
     const int t = P.s + (int)A.seedLen;
-    const int rf = lv_group<1, GS, NW>(G, S.u.sc.rows8, F, P.act, t, (int)n - t, P.glen - t, k, k, e1);
+    const int rf = lv_group<1, GS, NW, true>(G, S.u.sc.rows8, F, P.act, t, (int)n - t, P.glen - t, k, k, e1);
     PH_ADD(A, S, PH_LVF, tf);
     PH_CNT(A, S, PH_ROWSF, rf);
     PH_CNT(A, S, GS <= 16 ? PH_NPASS16 : (GS == 32 ? PH_NPASS32 : PH_NPASS64), 1);
