@@ -6,6 +6,8 @@ mkdir -p gpurun_out
 export SNAPGPU_TIMEOUT_S=90
 timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 200 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { tail -20 gpurun_out/gpu_tests.log; exit 1; }
 tail -1 gpurun_out/gpu_tests.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
+tail -1 gpurun_out/smoke.log
 timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || exit $?
 python3 -c "import json; d=json.loads(open('gpurun_out/bench.json').readline()); print('bench', round(d['value']/1e6,3), 'M reads/s')"
 bash tools/gpu/prof.sh ${1:-r02} || exit $?
