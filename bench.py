@@ -70,15 +70,33 @@ def lib_sha256():
     return h.hexdigest()
 
 
-def load_pmc(sha):
+def kernel_source_sha256():
+    """Identity of the device code: the HIP sources and headers, the ABI header and the
+    Makefile's compiler flags (a rebuild from the same sources elsewhere gives other .so bytes --
+    hipcc embeds paths -- but the same kernels)."""
+    import glob
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(ROOT, "snap-rnaseq_amd", "csrc", "*.hip")) +
+                   glob.glob(os.path.join(ROOT, "snap-rnaseq_amd", "csrc", "*.h")))
+    files += [os.path.join(ROOT, "include", "snapgpu.h"), os.path.join(ROOT, "snap-rnaseq_amd", "Makefile")]
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def load_pmc(sha, src_sha):
     """Per-read HBM bytes / VALU instructions of align_kernel<128> from the committed rocprofv3
-    PMC summary (profiles/pmc_traffic.json), only if it was collected on this exact library."""
+    PMC summary (profiles/pmc_traffic.json), only if it was collected on this library or on a
+    build of the same device sources."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
         return None, "no profiles/pmc_traffic.json"
     d = json.load(open(p))
-    if d.get("lib_sha256") != sha:
-        return None, f"profiles/pmc_traffic.json was collected on another build ({str(d.get('lib_sha256'))[:12]})"
+    if d.get("lib_sha256") != sha and d.get("kernel_source_sha256") != src_sha:
+        return None, (f"profiles/pmc_traffic.json was collected on another build (library "
+                      f"{str(d.get('lib_sha256'))[:12]}, kernel sources {str(d.get('kernel_source_sha256'))[:12]})")
     return d, d.get("source")
 
 
@@ -334,6 +352,7 @@ def main():
     result = None
     if rank == 0:
         sha = lib_sha256()
+        src_sha = kernel_source_sha256()
         bytes_all, per_read = algorithmic_bytes(res)
         n_launch = float(np.mean(launches))
         bytes_launch = bytes_all / n_launch
@@ -344,7 +363,7 @@ def main():
         busy_step = float(np.mean(busy_ms))
         kms_launch = busy_step / n_launch
         achieved = bytes_launch / (kms_launch / 1000.0) / 1e9
-        pmc, pmc_src = load_pmc(sha)
+        pmc, pmc_src = load_pmc(sha, src_sha)
         reads_launch = wl["reads"] / n_launch
         traffic = None
         valu_issue = None
@@ -370,7 +389,8 @@ def main():
                     "launches_per_step": n_launch, "reads_per_launch": reads_launch,
                     "algorithmic_bytes_per_launch": bytes_launch, "algorithmic_bytes_per_read": bytes_all / len(res),
                     "binding_resource": "VALU issue (DESIGN.md section 4), not HBM bandwidth",
-                    "valu_issue": valu_issue, "pmc_source": pmc_src, "lib_sha256": sha}
+                    "valu_issue": valu_issue, "pmc_source": pmc_src, "lib_sha256": sha,
+                    "kernel_source_sha256": src_sha}
         counts = {int(k): int(v) for k, v in zip(*np.unique(res["result"], return_counts=True))}
         extras = {}
         if not args.no_extras:

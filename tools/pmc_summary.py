@@ -62,6 +62,7 @@ def main(src, dst):
     bench = json.loads(open(os.path.join(src, "bench_kt.json")).readline())
     reads_per_launch = bench["roofline"]["reads_per_launch"]
     out = {"bench_line": os.path.join(dst, "bench_kt.json"), "lib_sha256": bench["roofline"]["lib_sha256"],
+           "kernel_source_sha256": bench["roofline"].get("kernel_source_sha256"),
            "kernels": {}}
     shutil.copy(os.path.join(src, "bench_kt.json"), os.path.join(dst, "bench_kt.json"))
     ks = os.path.join(src, "kt", "run_kernel_stats.csv")
@@ -111,7 +112,8 @@ def main(src, dst):
         per_read = {x: c[x] / reads_per_launch for x in c}
         a["per_read"] = per_read
         hb = a.get("hbm_bytes_per_dispatch_raw", {})
-        traffic = {"lib_sha256": out["lib_sha256"], "kernel": KERNELS["align"], "reads_per_dispatch": reads_per_launch,
+        traffic = {"lib_sha256": out["lib_sha256"], "kernel_source_sha256": out["kernel_source_sha256"],
+                   "kernel": KERNELS["align"], "reads_per_dispatch": reads_per_launch,
                    "hbm_bytes_per_read": (hb.get("fetch", 0) + hb.get("write", 0)) / reads_per_launch,
                    "fetch_bytes_per_read": hb.get("fetch", 0) / reads_per_launch,
                    "write_bytes_per_read": hb.get("write", 0) / reads_per_launch,
