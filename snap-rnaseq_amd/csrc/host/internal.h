@@ -2,6 +2,7 @@
 #pragma once
 #include "snapgpu.h"
 #include <cstdint>
+#include <cstdio>
 #include <memory>
 #include <string>
 #include <vector>
@@ -123,6 +124,10 @@ struct SamLine {
     uint32_t mateFront = 0, mateClippedLen = 0, mateFullLen = 0;
 };
 void samAppendLine(std::string &o, const Genome &g, const SamLine &L);
+// bam.cpp: BAMFormat::writeRead of a read without mate, the BAM header, a BGZF writer
+bool bamAppendRecord(std::string &o, const Genome &g, const SamLine &L, int32_t nm);
+std::string bamHeader(const Genome &g, const std::string &samText);
+bool bgzfWrite(FILE *f, const char *data, size_t n, bool eof);
 
 // One pair's GTFReader::IncrementReadCount (pair form) arguments (gtf.cpp: gtfCountPairs).
 struct GtfPairQuery {

@@ -294,6 +294,23 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
     const unsigned nt = n < 4096 ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     std::vector<std::string> parts(nt);
     std::vector<uint64_t> cnt(3 * nt, 0);
+    // BAM output when the path ends in ".bam" (AlignerOptions: "SAM or BAM format, depending on the
+    // file extension").  BAMFormat::writeRead sets NM only for a record with a location; the others
+    // repeat the previous record's value -- a serial pass in output order fixes each record's NM.
+    const size_t pl = strlen(samPath);
+    const bool bam = pl >= 4 && strcmp(samPath + pl - 4, ".bam") == 0;
+    std::vector<int32_t> bamNm;
+    if (bam) {
+        bamNm.resize(n);
+        int32_t last = 0;   // before any mapped record the reference writes its stack's leftover
+        for (uint64_t i = 0; i < n; i++) {
+            const int64_t j = uidx[i];
+            if (j >= 0 && fo[j].location != kInvalidLocation)
+                last = (fo[j].result != SNAPGPU_NOT_FOUND && fo[j].isTranscriptome) ? ted[j] : ged[j];
+            bamNm[i] = last;
+        }
+    }
+    std::vector<uint8_t> bamBad(nt, 0);
     parallel(n, [&](unsigned t, uint64_t b, uint64_t e) {
         std::string &o = parts[t];
         o.reserve((e - b) * 320);
@@ -328,9 +345,12 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
                 // updateStats (SingleAligner.cpp:338-365)
                 cnt[3 * t + (f.result == SNAPGPU_SINGLE_HIT ? 0 : f.result == SNAPGPU_MULTIPLE_HITS ? 1 : 2)]++;
             }
-            samAppendLine(o, *gi->genome, L);
+            if (!bam) samAppendLine(o, *gi->genome, L);
+            else if (!bamAppendRecord(o, *gi->genome, L, bamNm[i])) bamBad[t] = 1;
         }
     });
+    for (unsigned t = 0; t < nt; t++)
+        if (bamBad[t]) { setError("single_align: BAM QNAME longer than 254 characters"); return fail(SNAPGPU_EINVAL); }
     for (unsigned t = 0; t < nt; t++) { st.singleHits += cnt[3 * t]; st.multiHits += cnt[3 * t + 1]; st.notFound += cnt[3 * t + 2]; }
     FILE *f = fopen(samPath, "w");
     if (!f) { setError(std::string("cannot write ") + samPath); return fail(SNAPGPU_EIO); }
@@ -340,8 +360,18 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
     std::string hdr(hlen, '\0');
     if ((rc = snapgpu_sam_header(gi, 0, opt->commandLine ? opt->commandLine : "", opt->version ? opt->version : "",
                                  nullptr, &hdr[0], hlen, &hlen))) { fclose(f); return fail(rc); }
-    bool ok = fwrite(hdr.data(), 1, hdr.size(), f) == hdr.size();
-    for (auto &p : parts) ok = ok && fwrite(p.data(), 1, p.size(), f) == p.size();
+    bool ok = true;
+    if (bam) {   // BGZF stream: header, then the records (64 KB blocks), then the EOF block
+        hdr.resize(strnlen(hdr.data(), hdr.size()));
+        const std::string bh = bamHeader(*gi->genome, hdr);
+        ok = bgzfWrite(f, bh.data(), bh.size(), false);
+        std::string all;
+        for (auto &p : parts) all += p;
+        ok = ok && bgzfWrite(f, all.data(), all.size(), true);
+    } else {
+        ok = fwrite(hdr.data(), 1, hdr.size(), f) == hdr.size();
+        for (auto &p : parts) ok = ok && fwrite(p.data(), 1, p.size(), f) == p.size();
+    }
     ok = (fclose(f) == 0) && ok;
     if (!ok) { setError(std::string("write failed: ") + samPath); return fail(SNAPGPU_EIO); }
     st.writeMs = msSince(t0);

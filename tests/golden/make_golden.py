@@ -15,6 +15,7 @@ TSV/JSON expected outputs.
     python3 tests/golden/make_golden.py --only-single    # `snap-rna single` end-to-end SAM fixtures
     python3 tests/golden/make_golden.py --only-paired    # Intersecting + Chimeric paired-end aligner runs
     python3 tests/golden/make_golden.py --only-long      # 129..256-base reads + long LV vectors (align_kernel<256>)
+    python3 tests/golden/make_golden.py --only-bam       # `snap-rna single ... -o out.bam` records (BAMFormat)
 """
 import hashlib
 import json
@@ -757,8 +758,49 @@ def long_fixtures(work):
                 f.write("\t".join(map(str, r)) + f"\t{e}\t{net}\t{float.fromhex(prob).hex()}\n")
 
 
+def bam_fixtures(work):
+    """`snap-rna single <genome> <transcriptome> <gtf> single_reads.fq -t 1 -o out.bam` (BAMFormat::
+    writeHeader / writeRead, Bam.cpp:542-790): the BGZF stream decompressed, split into the header's
+    reference list and the alignment records (the header text echoes the command line)."""
+    import gzip
+    import struct
+    fa = os.path.join(HERE, "small.fa")
+    gtf = os.path.join(HERE, "small.gtf")
+    fq = os.path.join(HERE, "single_reads.fq")
+    gidx = os.path.join(work, "gidx")
+    ref_index(fa, gidx)
+    twd = os.path.join(work, "tx")
+    os.makedirs(twd, exist_ok=True)
+    run([SNAP, "transcriptome", gtf, fa, "tidx", "-O1000"], cwd=twd)
+    for tag, extra in (("", []), ("_M", ["-M"])):
+        out = os.path.join(work, f"out{tag}.bam")
+        run([SNAP, "single", gidx, os.path.join(twd, "tidx"), gtf, fq, "-t", "1", "-o", out] + extra, cwd=work)
+        raw = gzip.decompress(open(out, "rb").read())
+        assert raw[:4] == b"BAM\1"
+        l_text = struct.unpack_from("<i", raw, 4)[0]
+        at = 8 + l_text
+        n_ref = struct.unpack_from("<i", raw, at)[0]
+        at += 4
+        refs = []
+        for _ in range(n_ref):
+            ln = struct.unpack_from("<i", raw, at)[0]
+            name = raw[at + 4:at + 4 + ln - 1].decode()
+            lref = struct.unpack_from("<i", raw, at + 4 + ln)[0]
+            refs.append([name, lref])
+            at += 8 + ln
+        with open(os.path.join(HERE, f"expected_single{tag}.bam.refs.json"), "w") as f:
+            json.dump(refs, f)
+        with open(os.path.join(HERE, f"expected_single{tag}.bam.records.gz"), "wb") as f:
+            f.write(gzip.compress(raw[at:], compresslevel=9, mtime=0))
+
+
 def main():
     work = tempfile.mkdtemp(prefix="golden_")
+    if "--only-bam" in sys.argv:
+        bam_fixtures(work)
+        shutil.rmtree(work, ignore_errors=True)
+        print("BAM fixtures written to", HERE)
+        return
     if "--only-long" in sys.argv:
         long_fixtures(work)
         shutil.rmtree(work, ignore_errors=True)

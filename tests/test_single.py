@@ -84,3 +84,46 @@ def test_single_end_product_path_matches_reference(gpu_available, tmp_path, use_
                 want[cur] += line
         for name, text in want.items():
             assert open(tmp_path / f"out.{name}.counts.txt").read() == text, name
+
+
+def _bam_split(raw):
+    """Decompressed BAM -> (SAM header text, [(name, l_ref)], record bytes)."""
+    import struct
+    assert raw[:4] == b"BAM\1"
+    l_text = struct.unpack_from("<i", raw, 4)[0]
+    text = raw[8:8 + l_text].decode()
+    at = 8 + l_text
+    n_ref = struct.unpack_from("<i", raw, at)[0]
+    at += 4
+    refs = []
+    for _ in range(n_ref):
+        ln = struct.unpack_from("<i", raw, at)[0]
+        refs.append([raw[at + 4:at + 4 + ln - 1].decode(), struct.unpack_from("<i", raw, at + 4 + ln)[0]])
+        at += 8 + ln
+    return text, refs, raw[at:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("use_m,fixture", [(0, "expected_single"), (1, "expected_single_M")])
+def test_single_end_bam_matches_reference(gpu_available, tmp_path, use_m, fixture):
+    """`-o out.bam`: BAMFormat::writeHeader / writeRead (Bam.cpp:542-790) in a BGZF stream; the
+    decompressed records equal the reference's byte for byte (incl. its NM carry-over on unmapped
+    records), the reference list too (the header text echoes the command line)."""
+    import json
+    gtf, gidx, tidx = _indexes(tmp_path)
+    ga = snapgpu.BaseAligner(gidx)
+    ta = snapgpu.BaseAligner(tidx)
+    reads = snapgpu.Reads.from_fastq(os.path.join(G, "single_reads.fq"))
+    out = tmp_path / "out.bam"
+    snapgpu.single_align(ga, ta, gtf, reads, out, useM=use_m, version="0.1alpha", commandLine="x")
+    data = out.read_bytes()
+    assert data[:4] == b"\x1f\x8b\x08\x04" and data[12:14] == b"BC"           # BGZF blocks
+    assert data[-28:] == bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
+    text, refs, recs = _bam_split(gzip.decompress(data))
+    assert text.startswith("@HD") and "@SQ" in text
+    assert refs == json.load(open(os.path.join(G, f"{fixture}.bam.refs.json")))
+    want = gzip.decompress(open(os.path.join(G, f"{fixture}.bam.records.gz"), "rb").read())
+    assert len(recs) == len(want)
+    if recs != want:
+        i = next(k for k in range(len(want)) if recs[k] != want[k])
+        raise AssertionError(f"records differ from byte {i}: got {recs[max(0, i - 40):i + 40]!r} want {want[max(0, i - 40):i + 40]!r}")
