@@ -492,7 +492,8 @@ typedef struct snapgpu_single_stats {   /* AlignerStats (AlignerStats.h:40-69) *
 } snapgpu_single_stats_t;
 
 /* reads: a FASTQ batch with ids (snapgpu_reads_from_fastq), clipped here.  samPath receives
- * the header and one line per read in input order. */
+ * the header and one record per read in input order: SAM text, or BGZF-compressed BAM when the
+ * path ends in ".bam" (BAMFormat::writeHeader / writeRead, Bam.cpp:542-790). */
 int snapgpu_single_align(snapgpu_aligner_t *genomeAligner, snapgpu_aligner_t *transcriptomeAligner,
                          snapgpu_gtf_t *gtf, snapgpu_reads_t *reads, const snapgpu_single_options_t *opt,
                          const char *samPath, snapgpu_single_stats_t *stats);

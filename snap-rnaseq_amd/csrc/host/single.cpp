@@ -305,8 +305,8 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
         int32_t last = 0;   // before any mapped record the reference writes its stack's leftover
         for (uint64_t i = 0; i < n; i++) {
             const int64_t j = uidx[i];
-            if (j >= 0 && fo[j].location != kInvalidLocation)
-                last = (fo[j].result != SNAPGPU_NOT_FOUND && fo[j].isTranscriptome) ? ted[j] : ged[j];
+            if (j >= 0 && fo[j].result != SNAPGPU_NOT_FOUND)
+                last = fo[j].isTranscriptome ? ted[j] : ged[j];
             bamNm[i] = last;
         }
     }
@@ -345,6 +345,8 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
                 // updateStats (SingleAligner.cpp:338-365)
                 cnt[3 * t + (f.result == SNAPGPU_SINGLE_HIT ? 0 : f.result == SNAPGPU_MULTIPLE_HITS ? 1 : 2)]++;
             }
+            if (bam && L.result == SNAPGPU_NOT_FOUND) L.loc = kInvalidLocation;   // BAM: FilterSingle's NotFound
+                                                                               // location 0 gives no CIGAR, bin (-1, 0)
             if (!bam) samAppendLine(o, *gi->genome, L);
             else if (!bamAppendRecord(o, *gi->genome, L, bamNm[i])) bamBad[t] = 1;
         }
