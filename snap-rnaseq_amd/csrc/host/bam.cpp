@@ -121,6 +121,7 @@ bool bamAppendRecord(std::string &o, const Genome &g, const SamLine &L, int32_t 
     const int bin = L.loc != kInvalidLocation ? reg2bin((int)pos - 1, (int)pos - 1 + refLength) : reg2bin(-1, 0);
     const size_t rgLen = L.rg ? strlen(L.rg) : 0;
     const size_t size = 36 + qlen + 1 + 4 * ops.size() + (len + 1) / 2 + len + (L.rg ? 4 + rgLen : 0) + 8 + 7;
+    const size_t start = o.size();
     put<int32_t>(o, (int32_t)(size - 4));                // block_size
     put<int32_t>(o, pieceIdx);                           // refID
     put<int32_t>(o, (int32_t)pos - 1);                   // pos
@@ -159,7 +160,7 @@ bool bamAppendRecord(std::string &o, const Genome &g, const SamLine &L, int32_t 
     o.append("PGZSNAP\0", 8);
     o += "NMi";
     put<int32_t>(o, nm);
-    return true;
+    return o.size() - start == size;   // block_size must describe exactly what was appended
 }
 
 // BAMFormat::writeHeader: magic, the SAM header text, one RefSeq per genome piece with

@@ -352,7 +352,10 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
         }
     });
     for (unsigned t = 0; t < nt; t++)
-        if (bamBad[t]) { setError("single_align: BAM QNAME longer than 254 characters"); return fail(SNAPGPU_EINVAL); }
+        if (bamBad[t]) {
+            setError("single_align: BAM record not written (QNAME longer than 254 characters, Bam.cpp:723-726)");
+            return fail(SNAPGPU_EINVAL);
+        }
     for (unsigned t = 0; t < nt; t++) { st.singleHits += cnt[3 * t]; st.multiHits += cnt[3 * t + 1]; st.notFound += cnt[3 * t + 2]; }
     FILE *f = fopen(samPath, "w");
     if (!f) { setError(std::string("cannot write ") + samPath); return fail(SNAPGPU_EIO); }
