@@ -414,15 +414,27 @@ int snapgpu_rna_paired_align(snapgpu_paired_aligner_t *pa, snapgpu_aligner_t *ta
     st.prepMs = msSince(w0);
     auto t0 = std::chrono::steady_clock::now();
     if (nu) {
+        // g_aligner->align(read0, read1, &result) (:625) on a thread of its own, concurrently with
+        // the transcriptome batches: the two aligners have their own streams and device buffers
+        // (results are per aligner, so the order of the calls does not matter)
+        int grc = SNAPGPU_OK;
+        std::string gerr;
+        auto genomePairs = [&] {
+            grc = snapgpu_paired_align_batch(pa, U[0], U[1], gr.data());
+            if (grc) gerr = snapgpu_last_error();
+        };
+        const bool overlap = ta != ga;
+        std::thread gt;
+        if (overlap) gt = std::thread(genomePairs);
         // transcriptomeAligner->AlignRead(read0 / read1, ..., maxHitsToGet 1000, multiHits) (:601-605)
-        for (int k = 0; k < 2; k++) {
+        for (int k = 0; k < 2 && rc == SNAPGPU_OK; k++) {
             tr[k].resize(nu); tf[k].resize(nu);
-            if ((rc = snapgpu_internal_align_batch_packed(ta, U[k], nullptr, mh, tr[k].data(), tf[k].data(), thOff[k],
-                                                          th[k])))
-                return fail(rc);
+            rc = snapgpu_internal_align_batch_packed(ta, U[k], nullptr, mh, tr[k].data(), tf[k].data(), thOff[k], th[k]);
         }
-        // g_aligner->align(read0, read1, &result) (:625)
-        if ((rc = snapgpu_paired_align_batch(pa, U[0], U[1], gr.data()))) return fail(rc);
+        if (overlap) gt.join();
+        else if (rc == SNAPGPU_OK) genomePairs();
+        if (rc) return fail(rc);
+        if (grc) { setError(gerr); return fail(grc); }
     }
     st.alignMs = msSince(t0);
     // AddAlignment + Filter up to FindPartialMatches, on host threads
