@@ -541,34 +541,68 @@ int snapgpu_rna_paired_align(snapgpu_paired_aligner_t *pa, snapgpu_aligner_t *ta
     // CIGARs on the GPU (writeRead, SAM.cpp:1040-1066): genome records at the location, the
     // transcriptome records on the transcriptome at tlocation
     t0 = std::chrono::steady_clock::now();
-    std::vector<int32_t> ged[2], ted[2];
-    std::vector<uint32_t> gn[2], tn[2], gops[2], tops[2];
+    // Only the records with a location go to the GPU, as compact batches (a read without one has
+    // no CIGAR: edit distance -1, no ops); the genome (ga) and transcriptome (ta) batches run
+    // on two host threads.
+    struct CigarSet {
+        std::vector<int64_t> slot;   // record -> row in ed/nOps/ops, -1: no location
+        std::vector<uint64_t> off;
+        std::vector<uint32_t> len, loc, nOps, ops;
+        std::vector<uint8_t> dir;
+        std::vector<int32_t> ed;
+        int32_t edOf(uint64_t i) const { return slot[i] >= 0 ? ed[slot[i]] : -1; }
+        uint32_t nOpsOf(uint64_t i) const { return slot[i] >= 0 ? nOps[slot[i]] : 0u; }
+        const uint32_t *opsOf(uint64_t i) const {
+            static const uint32_t kNone[1] = {0};
+            return slot[i] >= 0 ? ops.data() + slot[i] * SNAPGPU_CIGAR_MAX_OPS : kNone;
+        }
+        void add(uint64_t i, const snapgpu_reads_t *r, uint32_t l, uint8_t d) {
+            slot[i] = (int64_t)loc.size();
+            off.push_back(r->offsets[i]);
+            len.push_back(r->lengths[i]);
+            loc.push_back(l);
+            dir.push_back(d);
+        }
+        int run(snapgpu_aligner_t *a, const snapgpu_reads_t *r, int useM) {
+            const uint64_t m = loc.size();
+            ed.assign(m + 1, -1);
+            nOps.assign(m + 1, 0);
+            ops.resize((m + 1) * SNAPGPU_CIGAR_MAX_OPS);
+            if (!m) return SNAPGPU_OK;
+            snapgpu_reads_t *v = snapgpu_reads_from_arrays(m, r->bases, r->quals, off.data(), len.data());
+            if (!v) return SNAPGPU_ENOMEM;
+            const int rc = snapgpu_cigar_batch(a, v, loc.data(), dir.data(), useM, ed.data(), nOps.data(), ops.data());
+            snapgpu_reads_free(v);
+            return rc;
+        }
+    };
+    CigarSet gc[2], tc[2];
     std::vector<uint8_t> isT[2];
     for (int k = 0; k < 2; k++) {
-        std::vector<uint32_t> gl(n), tl(n);
-        std::vector<uint8_t> gd(n), td(n);
         isT[k].assign(n, 0);
-        uint64_t nt = 0;
+        gc[k].slot.assign(n, -1);
+        tc[k].slot.assign(n, -1);
         for (uint64_t i = 0; i < n; i++) {
             const PairOut &r = po[i];
             const uint32_t loc = r.status[k] != SNAPGPU_NOT_FOUND ? r.location[k] : kInvalidLocation;
             const bool t = loc != kInvalidLocation && r.isTranscriptome[k];
             isT[k][i] = t;
-            gl[i] = t ? kInvalidLocation : loc;
-            gd[i] = (uint8_t)(loc == kInvalidLocation ? 0 : r.direction[k]);
-            tl[i] = t ? r.tlocation[k] : kInvalidLocation;
-            td[i] = (uint8_t)r.direction[k];
-            nt += t;
+            if (t) tc[k].add(i, R[k], r.tlocation[k], (uint8_t)r.direction[k]);
+            else if (loc != kInvalidLocation) gc[k].add(i, R[k], loc, (uint8_t)r.direction[k]);
         }
-        st.transcriptomeRecords += nt;
-        ged[k].assign(n + 1, -1); gn[k].assign(n + 1, 0); gops[k].assign((n + 1) * SNAPGPU_CIGAR_MAX_OPS, 0);
-        ted[k].assign(n + 1, -1); tn[k].assign(n + 1, 0); tops[k].assign((n + 1) * SNAPGPU_CIGAR_MAX_OPS, 0);
-        if (n && (rc = snapgpu_cigar_batch(ga, R[k], gl.data(), gd.data(), (int)opt->useM, ged[k].data(), gn[k].data(),
-                                           gops[k].data())))
-            return fail(rc);
-        if (nt && (rc = snapgpu_cigar_batch(ta, R[k], tl.data(), td.data(), (int)opt->useM, ted[k].data(), tn[k].data(),
-                                            tops[k].data())))
-            return fail(rc);
+        st.transcriptomeRecords += tc[k].loc.size();
+    }
+    {
+        int grc = SNAPGPU_OK;
+        std::string gerr;
+        std::thread gt([&] {
+            for (int k = 0; k < 2 && grc == SNAPGPU_OK; k++) grc = gc[k].run(ga, R[k], (int)opt->useM);
+            if (grc) gerr = snapgpu_last_error();
+        });
+        for (int k = 0; k < 2 && rc == SNAPGPU_OK; k++) rc = tc[k].run(ta, R[k], (int)opt->useM);
+        gt.join();
+        if (rc) return fail(rc);
+        if (grc) { setError(gerr); return fail(grc); }
     }
     // transcriptome records: computeCigarString's tokens through insertSpliceJunctions
     std::vector<std::string> splice[2];
@@ -581,14 +615,15 @@ int snapgpu_rna_paired_align(snapgpu_paired_aligner_t *pa, snapgpu_aligner_t *ta
                 if (!isT[k][i]) continue;
                 tk.clear();
                 const PairOut &r = po[i];
-                if (ted[k][i] >= 0) {
+                if (tc[k].edOf(i) >= 0) {
                     const uint32_t full = R[k]->unclippedLength[i], front = R[k]->frontClipped[i];
                     const uint32_t back = full - R[k]->lengths[i] - front;
                     const bool rcd = r.direction[k] == SNAPGPU_RC;
                     const uint32_t before = rcd ? back : front, after = rcd ? front : back;
                     if (before) tk.push_back({before, 'S'});
-                    for (uint32_t q = 0; q < tn[k][i]; q++) {
-                        const uint32_t op = tops[k][i * SNAPGPU_CIGAR_MAX_OPS + q];
+                    const uint32_t *tops = tc[k].opsOf(i);
+                    for (uint32_t q = 0; q < tc[k].nOpsOf(i); q++) {
+                        const uint32_t op = tops[q];
                         tk.push_back({op >> 4, kOp[op & 15]});
                     }
                     if (after) tk.push_back({after, 'S'});
@@ -638,11 +673,11 @@ int snapgpu_rna_paired_align(snapgpu_paired_aligner_t *pa, snapgpu_aligner_t *ta
                 L.mapq = r.mapq[k];
                 if (isT[k][i]) {
                     L.cigar = &splice[k][i];
-                    L.ed = ted[k][i];
+                    L.ed = tc[k].edOf(i);
                 } else {
-                    L.ed = ged[k][i];
-                    L.ops = gops[k].data() + i * SNAPGPU_CIGAR_MAX_OPS;
-                    L.nOps = gn[k][i];
+                    L.ed = gc[k].edOf(i);
+                    L.ops = gc[k].opsOf(i);
+                    L.nOps = gc[k].nOpsOf(i);
                 }
                 L.hasMate = true;
                 L.firstInPair = w == 0;
