@@ -16,7 +16,8 @@
 //   3. scoring (:516-718): candidates in best-possible-score order; scoreLocation (:755-841) is
 //      the byte-compare Landau-Vishkin of align_device.h (one lane per diagonal).
 // Pass 1 takes pairs of reads <= 128 bases with pools sized for ordinary pairs; pairs with a longer
-// read, or whose pools overflow, are deferred to pass 2 (reads <= 512, the same pool sizes on the
+// read, or whose pools overflow, are deferred to pass 1b (reads <= 256 on 256-bit planes, the same
+// pools), then to pass 2 (reads <= 512 and IUPAC cases, byte compares, the same pool sizes on the
 // full grid); pass 2's pool overflows go to pass 3 (pools of the reference's size on a small grid:
 // 22 MB per wave at the paired defaults).  A pair that exceeds the reference's own pool is
 // flagged: the reference exits there (soft_exit, :436-439, :482-485, :634-637).
@@ -95,9 +96,10 @@ static_assert(sizeof(Mate) == 32 && sizeof(Cand) == 32 && sizeof(Anchor) == 24, 
 template <int MAXLEN>
 struct PLds {
     static constexpr int NB = MAXLEN / 64;
+    static constexpr int PW = MAXLEN <= 256 ? NB : 2;   // read bit-plane words (<128>, <256>)
     char rd[2][2][MAXLEN + 64];             // [read][direction] bases, upper-cased, zero slack
     char rq[2][2][MAXLEN + 64];             // qualities in the same coordinates
-    uint32_t win[MAXLEN == 128 ? 1 : (MAXLEN + 192) / 4];   // <512>: genome window of scoreLocation
+    uint32_t win[MAXLEN <= 256 ? 1 : (MAXLEN + 192) / 4];   // <512>: genome window of scoreLocation
     // phases 1-2 (seeds, hit sets) and phase 3 (scoring) never overlap: their scratch shares LDS
     union {
         struct {
@@ -112,7 +114,7 @@ struct PLds {
     uint32_t miss[LCAP];                    // DisjointHitSet::missCount scratch
     uint32_t sel[2][LCAP];                  // chosen seed offsets per read (bit 31: a wrap preceded it)
     uint64_t validBits[NB], usedBits[NB];
-    uint64_t rpl[2][2][3][2];               // <128>: read bit planes [read][dir]{hi, lo, notACGT} x 2 words
+    uint64_t rpl[2][2][3][PW];              // <128>/<256>: read bit planes [read][dir]{hi, lo, notACGT} x NB words
     int32_t lists[MAX_LISTS];
 };
 
@@ -302,29 +304,30 @@ __device__ void score_location(const PArgs &P, PLds<MAXLEN> &S, int r, int dir, 
     }
     if (!ok) { score = FAIL_SCORE; prob = 0; return; }
     Bitmap<NB> F;
-    if constexpr (MAXLEN == 128) {
+    if constexpr (MAXLEN <= 256) {
         // lane l holds diagonal x = l - 31: F_x[m] = read[m] != genome[loc + x + m] from the genome
         // and read bit planes (as lv_pass, align_score.h); bytes past the read are not ACGT
         const int64_t gp = (int64_t)loc + (lane - 31) + PACK_GUARD;
         const uint4 *src = X.gpl + (gp >> 5);
         const uint32_t sh = (uint32_t)gp & 31;
-        uint4 w[5];
+        uint4 w[2 * NB + 1];
 #pragma unroll
-        for (int j = 0; j < 5; j++) w[j] = src[j];
-        const uint64_t *rp = &S.rpl[r][dir][0][0];
-        const uint64_t rh0 = rp[0], rh1 = rp[1], rl0 = rp[2], rl1 = rp[3], rm0 = rp[4], rm1 = rp[5];
-        uint32_t f[4];
+        for (int j = 0; j < 2 * NB + 1; j++) w[j] = src[j];
+        const uint64_t(*rp)[PLds<MAXLEN>::PW] = S.rpl[r][dir];
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t gh = __builtin_amdgcn_alignbit(w[j + 1].x, w[j].x, sh);
-            const uint32_t gl = __builtin_amdgcn_alignbit(w[j + 1].y, w[j].y, sh);
-            const uint32_t gm = __builtin_amdgcn_alignbit(w[j + 1].z, w[j].z, sh);
-            const uint64_t RH = j < 2 ? rh0 : rh1, RL = j < 2 ? rl0 : rl1, RM = j < 2 ? rm0 : rm1;
-            const uint32_t sft = 32 * (j & 1);
-            f[j] = (gh ^ (uint32_t)(RH >> sft)) | (gl ^ (uint32_t)(RL >> sft)) | gm | (uint32_t)(RM >> sft);
+        for (int b = 0; b < NB; b++) {
+            uint32_t f[2];
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int j = 2 * b + h;
+                const uint32_t gh = __builtin_amdgcn_alignbit(w[j + 1].x, w[j].x, sh);
+                const uint32_t gl = __builtin_amdgcn_alignbit(w[j + 1].y, w[j].y, sh);
+                const uint32_t gm = __builtin_amdgcn_alignbit(w[j + 1].z, w[j].z, sh);
+                const uint32_t sft = 32 * h;
+                f[h] = (gh ^ (uint32_t)(rp[0][b] >> sft)) | (gl ^ (uint32_t)(rp[1][b] >> sft)) | gm | (uint32_t)(rp[2][b] >> sft);
+            }
+            F.w[b] = ((uint64_t)f[1] << 32) | f[0];
         }
-        F.w[0] = ((uint64_t)f[1] << 32) | f[0];
-        F.w[1] = ((uint64_t)f[3] << 32) | f[2];
     } else {
         // genome bytes [loc - 64, loc + n + 128) into LDS (4-byte aligned start), byte compares
         const int64_t astart = ((int64_t)loc - 64) & ~(int64_t)3;
@@ -584,16 +587,16 @@ __device__ void align_pair(const PArgs &P, PLds<MAXLEN> &S, Cand *cand, Mate *ma
     if (n0 > P.maxLen || n1 > P.maxLen) { defer_pair<MAXLEN>(P, pi); return; }
     uint32_t countNs = load_read<MAXLEN>(P, S, 0, n0, o0) + load_read<MAXLEN>(P, S, 1, n1, o1);
     wave_sync();
-    if constexpr (MAXLEN == 128) {
+    if constexpr (MAXLEN <= 256) {
         // read bit planes of both reads and directions; a genome with IUPAC codes and a read with
-        // a non-ACGTN byte need byte compares (an IUPAC code can match itself): pass 2
+        // a non-ACGTN byte need byte compares (an IUPAC code can match itself): the <512> passes
         bool other = false;
 #pragma unroll
         for (int r = 0; r < 2; r++)
 #pragma unroll
             for (int dr = 0; dr < 2; dr++)
 #pragma unroll
-                for (int h = 0; h < 2; h++) {
+                for (int h = 0; h < PLds<MAXLEN>::NB; h++) {
                     const uint8_t c = (uint8_t)S.rd[r][dr][h * 64 + lane];
                     const uint32_t code = packed_code(c);
                     const uint64_t bh = ballot(code < 4 && (code & 2)), bl = ballot(code < 4 && (code & 1));
@@ -883,10 +886,12 @@ struct snapgpu_paired_aligner {
     snapgpu_aligner_t *single = nullptr;   // the chimeric fallback's BaseAligner; owns the index upload
     KArgs X{};
     hipStream_t stream = nullptr;
-    PassPool pass[3];                      // [0] pass 1, [1] pass 3 (the reference's pools), [2] pass 2
+    PassPool pass[3];                      // [0] passes 1 and 1b, [1] pass 3 (the reference's pools), [2] pass 2
+    int grid256 = 0;                       // pass 1b (<256>) grid: at most pass[0].grid (its pools)
     uint32_t refPool = 0, maxSeedsCmd = 0;
     uint32_t *dCounter = nullptr;          // [0] pass 1 queue, [1] pass 3 queue, [2] pass-1 defer count,
-                                           // [3] pass 2 queue, [4] pass-2 defer count
+                                           // [3] pass 2 queue, [4] pass-2 defer count, [5] pass 1b queue,
+                                           // [6] pass-1b defer count
     uint32_t *dDefer = nullptr, *dDefer2 = nullptr;
     snapgpu_pair_result_t *dOut = nullptr;
     char *dB[2] = {}, *dQ[2] = {};
@@ -975,9 +980,21 @@ static int runIntersect(snapgpu_paired_aligner_t *pa, const snapgpu_reads_t *r0,
     uint32_t nDefer = 0;
     PCHK(hipMemcpyAsync(&nDefer, pa->dCounter + 2, 4, hipMemcpyDeviceToHost, s));
     PCHK(hipStreamSynchronize(s));
-    if (nDefer) {   // pass 2: reads of 129..512 bases (and pass-1 pool overflows), ordinary pools, full grid
-        P.nPairs = nDefer; P.pairList = pa->dDefer; P.counter = pa->dCounter + 3; P.maxLen = 512;
-        P.deferList = pa->dDefer2; P.deferCount = pa->dCounter + 4;
+    if (nDefer) {   // pass 1b: reads of 129..256 bases on the 256-bit planes, pass 1's pools
+        P.nPairs = nDefer; P.pairList = pa->dDefer; P.counter = pa->dCounter + 5; P.maxLen = 256;
+        P.deferList = pa->dDefer2; P.deferCount = pa->dCounter + 6;
+        usePool(pa->pass[0]);
+        grid = pa->grid256;
+        if ((uint32_t)grid > nDefer) grid = (int)nDefer;
+        hipLaunchKernelGGL(paired_kernel<256>, dim3(grid), dim3(64), 0, s, P);
+        PCHK(hipGetLastError());
+        PCHK(hipMemcpyAsync(&nDefer, pa->dCounter + 6, 4, hipMemcpyDeviceToHost, s));
+        PCHK(hipStreamSynchronize(s));
+    }
+    if (nDefer) {   // pass 2: reads of 257..512 bases, IUPAC cases and pool overflows, ordinary pools, full grid
+        // (pass 1b has consumed list 1: it is pass 2's output)
+        P.nPairs = nDefer; P.pairList = pa->dDefer2; P.counter = pa->dCounter + 3; P.maxLen = 512;
+        P.deferList = pa->dDefer; P.deferCount = pa->dCounter + 4;
         usePool(pa->pass[2]);
         grid = pa->pass[2].grid;
         if ((uint32_t)grid > nDefer) grid = (int)nDefer;
@@ -987,7 +1004,7 @@ static int runIntersect(snapgpu_paired_aligner_t *pa, const snapgpu_reads_t *r0,
         PCHK(hipStreamSynchronize(s));
     }
     if (nDefer) {   // pass 3: pool overflows, the reference's pool sizes on a small grid
-        P.nPairs = nDefer; P.pairList = pa->dDefer2; P.counter = pa->dCounter + 1; P.maxLen = 512;
+        P.nPairs = nDefer; P.pairList = pa->dDefer; P.counter = pa->dCounter + 1; P.maxLen = 512;
         P.deferList = nullptr; P.deferCount = nullptr;
         usePool(pa->pass[1]);
         grid = pa->pass[1].grid;
@@ -1081,6 +1098,10 @@ snapgpu_paired_aligner_t *snapgpu_paired_aligner_create(int device, const snapgp
     if (const char *t = getenv("SNAPGPU_PAIRED_POOL1"); t && atoi(t) > 1) c1 = std::min<uint32_t>(pa->refPool, (uint32_t)atoi(t));
     if (allocPass(pa->pass[0], prop.multiProcessorCount * perCU, c1, std::max<uint32_t>(1, std::min(pa->refPool / 2, c1 / 2)), c1))
         { snapgpu_paired_aligner_free(pa); return nullptr; }
+    int perCU256 = 0;
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU256, (const void *)paired_kernel<256>, 64, 0);
+    if (perCU256 <= 0) perCU256 = 2;
+    pa->grid256 = std::min(prop.multiProcessorCount * perCU256, pa->pass[0].grid);
     int perCU2 = 0;
     hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU2, (const void *)paired_kernel<512>, 64, 0);
     if (perCU2 <= 0) perCU2 = 2;
