@@ -1,6 +1,6 @@
 """Stage timing of the RNA paired path (bench extras.rna_paired workload) on one GPU:
 transcriptome AlignReadsEx per end (1000 multi-hits), the chimeric paired aligner, the
-intersecting kernel alone, and the whole snapgpu_rna_paired_align call.
+intersecting kernel alone, the whole snapgpu_rna_paired_align call, and snapgpu_single_align over end 0.
   python tools/rna_probe.py [n_pairs]"""
 import os
 import shutil
@@ -60,6 +60,15 @@ def main():
             out["stage_ms"] = {k: round(st[k], 1) for k in ("prepMs", "alignMs", "filterMs", "seedMs", "countMs", "cigarMs",
                                                                     "writeMs", "wallMs")}
         out["rna_paired_align_ms"] = best(full)
+        # the single-end product path (snap-rna single) over end 0
+        S0 = snapgpu.Reads.from_fastq(fq0)
+        sam = os.path.join(work, "single.sam")
+
+        def single():
+            gtf.reset_counts()
+            st = snapgpu.single_align(ga, ta, gtf, S0, sam)
+            out["single_stage_ms"] = {k: round(v, 1) for k, v in st.items() if k.endswith("Ms")}
+        out["single_align_ms"] = best(single)
         print(out, flush=True)
     finally:
         shutil.rmtree(work, ignore_errors=True)
