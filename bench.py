@@ -130,6 +130,30 @@ def log(rank, msg, t0=[time.time()]):
         print(f"[bench {time.time() - t0[0]:7.1f}s] {msg}", file=sys.stderr, flush=True)
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(args, argv):
+    """`python bench.py --gpus N` (N > 1) without a launcher around it: start N rank processes
+    through torch.distributed.run (one per GPU, 127.0.0.1 rendezvous) and exit with its code --
+    the reference's model is one worker per device over disjoint read ranges
+    (ParallelTask.h:127-137).  Runs before anything here imports snapgpu or touches a GPU; the
+    ranks inherit stdout, so rank 0's JSON line is this process's output.  Returns only when
+    this process is itself a rank (WORLD_SIZE set) or N == 1."""
+    if "WORLD_SIZE" in os.environ or args.gpus <= 1:
+        return
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    print(f"[bench] launching {args.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    sys.exit(subprocess.call(cmd, env=env))
+
+
 def init_distributed():
     """One process per GPU (torch.distributed.run sets RANK/LOCAL_RANK/WORLD_SIZE); gloo
     carries only barriers and the max-over-ranks reduction -- reads are independent, the
@@ -234,8 +258,9 @@ def rna_leg(args, idx, local, build_threads):
         shutil.rmtree(work, ignore_errors=True)
 
 
-def timed_steps(step, steps, dist, sync):
-    """Barrier + sync on both sides of exactly `steps` steps; returns the max over ranks."""
+def timed_steps(step, steps, dist, sync, own=None):
+    """Barrier + sync on both sides of exactly `steps` steps; returns the max over ranks (this
+    rank's own time is appended to `own` when given)."""
     if dist:
         dist.barrier()
     sync()
@@ -247,12 +272,72 @@ def timed_steps(step, steps, dist, sync):
     if dist:
         dist.barrier()
     elapsed = t_end - t_start
+    if own is not None:
+        own.append(elapsed)
     if dist:
         import torch
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     return elapsed
+
+
+def gather_per_rank(dist, world, mine):
+    """Every rank's own figures (reads/s on its shard, its index upload time, ...) on every rank
+    (gloo all_gather_object; not on the data path)."""
+    if not dist:
+        return [mine]
+    got = [None] * world
+    dist.all_gather_object(got, mine)
+    return got
+
+
+def shard_tag(reads):
+    """Short identity of a rank's read shard (its first read's bases)."""
+    return hashlib.sha256(bytes(reads.get(0)[0])).hexdigest()[:16]
+
+
+def standin_main(args, wl, world, rank, local, dist):
+    """--oracle-standin: the launch / sharding / index-sharing / reduction path of an N-rank run
+    with the CPU oracle in place of the GPU aligner, so the CPU suite can check `bench.py --gpus N`
+    end to end (tests/test_multirank.py).  Never a measurement: the line says so."""
+    import snapgpu
+    from snapgpu import shared_index
+    from oracle_ffi import oracle_align
+    gen = dict(seed=2121, n_contigs=wl["n_contigs"], n_repeat_families=wl["families"])
+    idx, index_info = shared_index.build_once(snapgpu, wl["genome_bases"], gen, 20, 2, rank, world, dist)
+    reads = snapgpu.Reads.synthetic(idx.genome_handle(), wl["reads"], seed=99 + rank)
+    params = snapgpu.default_params()
+    box = {}
+
+    def step():
+        box["res"] = oracle_align(idx, reads, params, n_threads=1)
+
+    for _ in range(args.warmup):
+        step()
+    own = []
+    elapsed = timed_steps(step, args.steps, dist, lambda: None, own)
+    per_rank = gather_per_rank(dist, world, {
+        "rank": rank, "device": None, "reads": wl["reads"], "elapsed_s": round(own[0], 4),
+        "reads_per_s": wl["reads"] * args.steps / own[0], "index_built_here": bool(index_info.get("built_by_this_rank")),
+        "shard_first_read": shard_tag(reads),
+        "single_hits": int((box["res"]["result"] == snapgpu.SingleHit).sum())})
+    result = None
+    if rank == 0:
+        result = {"metric": METRIC, "value": wl["reads"] * world * args.steps / elapsed, "unit": "reads/s",
+                  "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                  "ms_per_step": elapsed * 1000.0 / args.steps, "higher_is_better": True, "scaling": "weak",
+                  "vs_baseline": None, "dtype": "u8",
+                  "standin": "oracle (CPU test of the N-rank launch path; NOT a GPU measurement)",
+                  "data": "synthetic", "config": {"workload": args.workload, "genome_bases": wl["genome_bases"],
+                                                  "reads_per_gpu": wl["reads"], "index": index_info,
+                                                  "per_rank": per_rank}}
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist.barrier()
+        shared_index.cleanup(rank, world)
+        dist.destroy_process_group()
+    return result
 
 
 def main():
@@ -273,7 +358,11 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="reads timed on the CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip ceilings, CIGAR/SAM and parity legs")
+    ap.add_argument("--oracle-standin", action="store_true",
+                    help="CPU test of the N-rank launch path only: each rank runs the oracle/ restatement on its "
+                         "shard instead of the GPU aligner; the line is marked `standin` and is not a measurement")
     args = ap.parse_args()
+    self_launch(args, sys.argv[1:])
     wl = dict(WORKLOADS[args.workload])
     if args.reads:
         wl["reads"] = args.reads
@@ -281,6 +370,14 @@ def main():
         wl["genome_bases"] = args.genome_bases
 
     world, rank, local, dist = init_distributed()
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but {world} rank(s) were launched (WORLD_SIZE); refusing to report "
+              f"a {world}-GPU run as {args.gpus}", file=sys.stderr, flush=True)
+        if dist:
+            dist.destroy_process_group()
+        sys.exit(2)
+    if args.oracle_standin:
+        return standin_main(args, wl, world, rank, local, dist)
 
     import snapgpu
     from snapgpu import shared_index
@@ -340,7 +437,8 @@ def main():
         def sync():
             pass
 
-    elapsed = timed_steps(step, args.steps, dist, sync)
+    own = []
+    elapsed = timed_steps(step, args.steps, dist, sync, own)
     if args.mode == "stream":
         assert np.array_equal(outs[0].view(np.uint8), outs[1].view(np.uint8))
     log(rank, f"timed {args.steps} steps: {elapsed:.3f}s")
@@ -348,6 +446,10 @@ def main():
     total_reads = wl["reads"] * world * args.steps
     value = total_reads / elapsed
     ms_per_step = elapsed * 1000.0 / args.steps
+    per_rank = gather_per_rank(dist, world, {
+        "rank": rank, "device": local, "reads": wl["reads"], "elapsed_s": round(own[0], 4),
+        "reads_per_s": wl["reads"] * args.steps / own[0], "index_upload_s": round(t_upload, 2),
+        "index_built_here": bool(index_info.get("built_by_this_rank")), "shard_first_read": shard_tag(reads)})
 
     result = None
     if rank == 0:
@@ -531,6 +633,7 @@ def main():
                 "index_build_s": round(t_index, 2),
                 "index_upload_s": round(t_upload, 2),
                 "index": index_info,
+                "per_rank": per_rank,
             },
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -88,6 +88,46 @@ def test_two_rank_index_built_once_sharding_and_max_reduction():
     assert s0 > 300 and s1 > 300               # each shard aligns (oracle stand-in for the GPU)
 
 
+def _bench_env():
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_PORT", "MASTER_ADDR")}
+    env["OMP_NUM_THREADS"] = "1"
+    return env
+
+
+def test_bench_gpus_2_self_launches_two_ranks():
+    """`python bench.py --gpus 2` with no launcher around it starts two ranks itself
+    (torch.distributed.run, 127.0.0.1) and relays rank 0's line: n_gpus 2, the index built once
+    (the other rank attached it), disjoint shards, both ranks' own figures."""
+    import json
+    import subprocess
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--oracle-standin", "--reads", "300",
+           "--genome-bases", "300000", "--steps", "2", "--warmup", "0"]
+    r = subprocess.run(cmd, capture_output=True, text=True, env=_bench_env(), timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and "standin" in d
+    pr = d["config"]["per_rank"]
+    assert sorted(p["rank"] for p in pr) == [0, 1]
+    assert sum(p["index_built_here"] for p in pr) == 1
+    assert pr[0]["shard_first_read"] != pr[1]["shard_first_read"]
+    assert all(p["single_hits"] > 200 for p in pr)
+    assert d["value"] == pytest.approx(2 * 300 * 2 / (d["ms_per_step"] * 2 / 1000.0), rel=1e-6)
+    assert d["ms_per_step"] * 2 / 1000.0 >= max(p["elapsed_s"] for p in pr) - 1e-3
+
+
+def test_bench_refuses_world_gpus_mismatch():
+    """A run whose rank count differs from --gpus exits non-zero instead of mislabelling n_gpus."""
+    import subprocess
+    env = dict(_bench_env(), WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--oracle-standin",
+                        "--reads", "10", "--genome-bases", "100000"], capture_output=True, text=True, env=env,
+                       timeout=300)
+    assert r.returncode == 2 and "refusing" in r.stderr
+
+
 def test_shared_index_roundtrip(tmp_path):
     """snapgpu_index_share / snapgpu_index_attach: identical info, tables, genome and lookups."""
     import ctypes as C
