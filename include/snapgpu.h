@@ -354,6 +354,11 @@ int snapgpu_aligner_max_k(const snapgpu_aligner_t *a);           /* getMaxK() */
  * environment variable SNAPGPU_OVERLAP sets the initial value).  0 serialises the kernels
  * (copies and host work still overlap them): each launch's duration is then its own. */
 int snapgpu_aligner_set_overlap(snapgpu_aligner_t *a, int overlap);
+/* Test hook (no reference equivalent): the aligner's next calls trip its device watchdog when
+ * the batch's read `read_index` starts (0xffffffff: never), so the call fails with
+ * SNAPGPU_EDEVICE.  Each aligner has its own watchdog record: a trip in one aligner neither
+ * fails nor stops another aligner on the same device. */
+int snapgpu_aligner_debug_trip(snapgpu_aligner_t *a, uint32_t read_index);
 /* Diagnostic (no reference equivalent): with SNAPGPU_PHASES=1 in the environment at
  * snapgpu_aligner_create, align_kernel<128> sums shader cycles per phase and event
  * counts into out32[0..31] (order: snapgpu.BaseAligner.PHASES); reset != 0 zeroes them. */

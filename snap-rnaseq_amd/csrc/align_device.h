@@ -85,6 +85,7 @@ template <> struct ElemSel<256> { using type = Elem128; };
 template <int MAXLEN> using ElemOf = typename ElemSel<MAXLEN>::type;
 
 struct KArgs {
+    uint32_t *diag;              // this aligner's watchdog record {code, read, detail, 0} (diag_report)
     // index (HBM)
     const uint32_t *slots;
     const uint64_t *tableBase;
@@ -98,6 +99,7 @@ struct KArgs {
     uint32_t maxHits, maxK, maxReadSize, maxSeedsCmd;
     double seedCoverage;
     uint32_t extra, explore, stopOnFirst, kRows;
+    uint32_t tripRead;           // test hook: report DIAG_TEST_TRIP when this read starts (0xffffffff: never)
     uint32_t radixMin;           // forced mode: radix-sort the pop order of reads with >= this many elements
     const DevTables *tab;
     // reads
@@ -642,12 +644,14 @@ __device__ __forceinline__ int mapq_dev(const DevTables *tab, double pAll, doubl
 // iteration cap; tripping one records (code, read, detail) here, ends the read and
 // makes the host call fail instead of hanging the GPU.
 enum : uint32_t { DIAG_SEED_LOOP = 1, DIAG_SCORE_LOOP = 2, DIAG_CHAIN = 3, DIAG_BATCH_TABLE = 4, DIAG_ARENA = 5,
-                  DIAG_OVERDUE = 16 };
+                  DIAG_TEST_TRIP = 6, DIAG_OVERDUE = 16 };
 // A read that runs longer than this (100 MHz s_memrealtime ticks, 2 s) is abandoned.
 constexpr uint64_t READ_DEADLINE_TICKS = 200000000ull;
-static __device__ uint32_t g_diag[4];
-__device__ __forceinline__ void diag_report(uint32_t code, uint32_t a, uint32_t b) {
-    if (atomicCAS(&g_diag[0], 0u, code) == 0u) { g_diag[1] = a; g_diag[2] = b; }
+// The record is the aligner's own device allocation (KArgs::diag), so aligners that share a
+// device (the RNA path's transcriptome and genome aligners on two host threads) neither clear
+// nor trip each other's record.
+__device__ __forceinline__ void diag_report(uint32_t *d, uint32_t code, uint32_t a, uint32_t b) {
+    if (atomicCAS(&d[0], 0u, code) == 0u) { d[1] = a; d[2] = b; }
 }
 
 struct ReadState {
@@ -671,12 +675,12 @@ __device__ __forceinline__ uint32_t sv_get(const ReadState &st, int idx) { retur
 
 // time watchdog: true (once reported) when the read has overrun its deadline.  The
 // clock (an SMEM round trip) is read on every 32nd call only.
-__device__ __forceinline__ bool overdue(ReadState &st, uint32_t site) {
+__device__ __forceinline__ bool overdue(const KArgs &A, ReadState &st, uint32_t site) {
     if (st.abort) return true;
     if (--st.tick != 0) return false;
     st.tick = 32;
     if (__builtin_amdgcn_s_memrealtime() - st.t0 < READ_DEADLINE_TICKS) return false;
-    if (lane_id() == 0) diag_report(DIAG_OVERDUE + site, st.rid, (uint32_t)((__builtin_amdgcn_s_memrealtime() - st.t0) >> 10));
+    if (lane_id() == 0) diag_report(A.diag, DIAG_OVERDUE + site, st.rid, (uint32_t)((__builtin_amdgcn_s_memrealtime() - st.t0) >> 10));
     st.abort = 1;
     return true;
 }
@@ -686,11 +690,11 @@ __device__ __forceinline__ uint32_t elem_hash(uint32_t key) { return (key * 2654
 // find element with `key`; NONE if absent.  Elements < MIRCAP keep (key, next) in LDS
 // (next always points to an older, smaller index), so most walks never touch HBM.
 template <int MAXLEN>
-__device__ __forceinline__ uint32_t chain_find(const Lds<MAXLEN> &S, const ElemOf<MAXLEN> *ar, uint32_t key,
+__device__ __forceinline__ uint32_t chain_find(const KArgs &A, const Lds<MAXLEN> &S, const ElemOf<MAXLEN> *ar, uint32_t key,
                                                uint32_t cap) {
     uint32_t e = S.head[elem_hash(key)];
     for (uint32_t steps = 0; e != NONE; steps++) {
-        if (steps > cap) { diag_report(DIAG_CHAIN, key, e); return NONE; }
+        if (steps > cap) { diag_report(A.diag, DIAG_CHAIN, key, e); return NONE; }
         if (e < MIRCAP) {
             if (S.ekey[e] == key) break;
             const uint32_t nx = S.enext[e];

@@ -510,7 +510,7 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem1
         if (take) {
             const uint32_t nl = elemLoc + (2 * (elemLoc % ELEM / (ELEM / 2)) - 1) * (ELEM / 2);
             const uint32_t nkey = ((nl / ELEM) << 1) | dir;
-            nb2 = uni(chain_find(S, ar, nkey, (uint32_t)A.arenaElems));
+            nb2 = uni(chain_find(A, S, ar, nkey, (uint32_t)A.arenaElems));
         }
         if (nb2 != NONE) {
             // the nearby element may be in this batch: its cache is authoritative
@@ -675,10 +675,10 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, El
         // recomputed in the batch instead of hoisted and kept live, spilled, across the pass loop
         const int lane = lane_id();
         if (guard > (uint32_t)A.arenaElems) {   // every batch unlinks >= 1 element
-            if (lane == 0) diag_report(DIAG_SCORE_LOOP, st.rid, S.nElems);
+            if (lane == 0) diag_report(A.diag, DIAG_SCORE_LOOP, st.rid, S.nElems);
             st.abort = 1;
         }
-        if (overdue(st, 1)) return true;
+        if (overdue(A, st, 1)) return true;
         PH_T(A, tpop);
         // ---- pop in weight-list order (head of the highest list first); LDS only
         uint32_t nb = 0;
@@ -811,7 +811,7 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, El
         uint32_t lastSlot = NONE;   // element of the last candidate reached, and its lps decision
         bool lastSkip = false;
         for (uint32_t i0 = 0; i0 < nc;) {
-            if (overdue(st, 2)) return true;
+            if (overdue(A, st, 2)) return true;
             const int k = st.scoreLimit < (uint32_t)(MAX_K - 1) ? (int)st.scoreLimit : MAX_K - 1;
             const int GS = k <= 3 ? 8 : (k <= 7 ? 16 : (k <= 15 ? 32 : 64));
             const int Gn = 64 / GS;

@@ -39,7 +39,7 @@ __device__ __forceinline__ bool score_wave(const KArgs &A, Lds<MAXLEN> &S, Elem5
             if (v > st.lps[d]) st.lps[d] = v;
         }
     do {
-        if (overdue(st, 4)) return true;
+        if (overdue(A, st, 4)) return true;
         // head of the highest non-empty weight list == max sortkey over linked elements
         uint64_t sel = uni64(max_reduce64(S.laneMax[lane]));
         uint32_t minLps = st.lps[0] < st.lps[1] ? st.lps[0] : st.lps[1];
@@ -141,7 +141,7 @@ __device__ __forceinline__ bool score_wave(const KArgs &A, Lds<MAXLEN> &S, Elem5
                 if (sc != FAIL_SCORE) {
                     uint32_t nl = elemLoc + (2 * (elemLoc % ELEM / (ELEM / 2)) - 1) * (ELEM / 2);
                     uint32_t nkey = ((nl / ELEM) << 1) | dir;
-                    nb = uni(chain_find(S, ar, nkey, (uint32_t)A.arenaElems));
+                    nb = uni(chain_find(A, S, ar, nkey, (uint32_t)A.arenaElems));
                 }
                 if (nb != NONE) {
                     const uint32_t *nw = (const uint32_t *)(ar + nb);
@@ -217,7 +217,7 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
     const int lane = lane_id();
     const uint32_t lim = lim0 + lim1;
     for (uint32_t b0 = 0; b0 < lim; b0 += WAVE) {
-        if (overdue(st, 5)) break;
+        if (overdue(A, st, 5)) break;
         const uint32_t i = b0 + lane;
         const uint32_t dir = i >= lim0 ? 1u : 0u;
         const uint32_t ii = dir ? i - lim0 : i;
@@ -238,7 +238,7 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
             for (int probe = 0;; probe++) {
                 uint32_t old = atomicCAS(&S.u.ins.btKey[s], NONE, key);
                 if (old == NONE || old == key) break;
-                if (probe >= BT) { diag_report(DIAG_BATCH_TABLE, st.rid, key); valid = false; break; }
+                if (probe >= BT) { diag_report(A.diag, DIAG_BATCH_TABLE, st.rid, key); valid = false; break; }
                 s = (s + 1) & (BT - 1);
             }
             slot = s;
@@ -253,7 +253,7 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
         if (leader) {
             S.u.ins.btKey[slot] = NONE;
             S.u.ins.btMask[slot] = 0;
-            uint32_t e = chain_find(S, ar, key, (uint32_t)A.arenaElems);
+            uint32_t e = chain_find(A, S, ar, key, (uint32_t)A.arenaElems);
             if (e != NONE || allowAlloc) {
                 uint64_t used = 0;
                 uint32_t weight = 0, allScored = 0, sortkey = 0;
@@ -270,7 +270,7 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
                         // allocateNewCandidate (BaseAligner.cpp:1485-1568): tail of weight list 1
                         e = atomicAdd(&S.nElems, 1u);
                         if (e >= (uint32_t)A.arenaElems) {
-                            diag_report(DIAG_ARENA, st.rid, e);
+                            diag_report(A.diag, DIAG_ARENA, st.rid, e);
                             overflow = true;
                             break;
                         }
@@ -449,10 +449,10 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
             const int lane = lane_id();
             bool force = st.nSeedsApplied[0] + st.nSeedsApplied[1] >= maxSeeds;
             if (guard > seedGuard) {   // each pass consumes a seed position or a wrap
-                if (lane == 0) diag_report(DIAG_SEED_LOOP, r, next);
+                if (lane == 0) diag_report(A.diag, DIAG_SEED_LOOP, r, next);
                 st.abort = 1;
             }
-            if (overdue(st, 3)) break;
+            if (overdue(A, st, 3)) break;
             if (!force && next >= nPossible) {
                 wrapCount++;
                 if (wrapCount >= seedLen) { force = true; wrapForced = true; }
@@ -523,7 +523,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
                     }
                 }
                 }
-                if (overdue(st, 6)) break;
+                if (overdue(A, st, 6)) break;
                 // fillInLookedUpResults (GenomeIndex.cpp:1013-1086), both directions
                 uint32_t nH0 = 0, nH1 = 0, sg0 = 0, sg1 = 0;
                 const uint32_t *ls0 = nullptr, *ls1 = nullptr;
@@ -590,7 +590,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
                 next += seedLen;
                 if (!applied) continue;
             }
-            if (overdue(st, 7)) break;
+            if (overdue(A, st, 7)) break;
             PH_T(A, tsc);
             bool fin;
             if constexpr (Lds<MAXLEN>::BYTE_PATH) fin = score_wave<MAXLEN, EXT>(A, S, ar, st, force, n, rbF, rbR, &result, &flags);
@@ -603,7 +603,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
             }
             PH_ADD(A, S, PH_SCORE, tsc);
             if (fin || force) { fillHits = !wrapForced; break; }
-            if (overdue(st, 8)) break;
+            if (overdue(A, st, 8)) break;
         }
         PH_ADD(A, S, PH_SEEDLOOP, tsl);
     }
@@ -652,7 +652,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MAXLEN <= 25
         i = uni((uint32_t)readlane((int)i, 0));
         if (i >= total) break;
         const uint32_t r = A.readList ? uni(A.readList[i]) : i;
-        if (__hip_atomic_load(&g_diag[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;   // watchdog: drain
+        if (__hip_atomic_load(&A.diag[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;   // watchdog: drain
+        if (r == A.tripRead && lane == 0) diag_report(A.diag, DIAG_TEST_TRIP, r, 0);   // test hook
         align_one<MAXLEN, EXT>(A, S, ar, r);
     }
 }
@@ -793,6 +794,13 @@ std::mutex g_errMu;
             return SNAPGPU_EDEVICE;                                                     \
         }                                                                               \
     } while (0)
+// inside a loop whose exit path cleans up (sets rc and leaves the enclosing loop)
+#define HIPBRK(x)                                                                       \
+    if (hipError_t e_ = (x); e_ != hipSuccess) {                                        \
+        snapgpu::setError(std::string(#x) + ": " + hipGetErrorString(e_));              \
+        rc = SNAPGPU_EDEVICE;                                                           \
+        break;                                                                          \
+    }
 #define HIPCHKN(x)                                                                      \
     do {                                                                                \
         hipError_t e_ = (x);                                                            \
@@ -968,11 +976,12 @@ struct snapgpu_aligner {
     // forced mode: reads with at least this many elements get a radix-sorted pop order instead of
     // windowed ranks (SNAPGPU_RADIX_MIN; beyond SKCAP the ranks stage keys from HBM per window)
     uint32_t radixMin = SKCAP + 1;
+    uint32_t tripRead = 0xffffffffu;   // test hook (snapgpu_aligner_debug_trip): trip the watchdog at this read
     snapgpu_timing_t timing{};
     snapgpu_aligner_stats_t stats{};
     snapgpu_device_reads_t *lastReads = nullptr;
     bool pendingTiming = false;
-    uint32_t *dDiag = nullptr;    // g_diag (watchdog record)
+    uint32_t *dDiag = nullptr;    // this aligner's watchdog record (KArgs::diag)
     unsigned long long *dPhase = nullptr;   // [grid][PH_SLOTS] (SNAPGPU_PHASES=1 diagnostics)
     double timeoutSec = 0;        // SNAPGPU_TIMEOUT_S
     // A wait that timed out leaves kernels running on buffers this aligner owns: from then on
@@ -1225,7 +1234,7 @@ void snapgpu_aligner_free(snapgpu_aligner_t *a) {
     for (auto &L : a->lane) if (L.stream) hipStreamSynchronize(L.stream);
     devFree(a, a->dSlots); devFree(a, a->dOverflow); devFree(a, a->dPieces);
     devFree(a, a->dTableBase); devFree(a, a->dTableSize); devFree(a, a->dGenomeAlloc); devFree(a, a->dTab);
-    devFree(a, a->dGPlanes); devFree(a, a->dPhase);
+    devFree(a, a->dGPlanes); devFree(a, a->dPhase); devFree(a, a->dDiag);
     for (auto &L : a->lane) {
         freeLaneChunkBuffers(a, L);
         devFree(a, L.arena); devFree(a, L.counter); devFree(a, L.lookupStats);
@@ -1286,7 +1295,8 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
     }
     if ((e = hipStreamCreateWithFlags(&a->copyStream, hipStreamNonBlocking)) != hipSuccess) return fail("stream", e);
     for (auto &ev : a->cev) if ((e = hipEventCreate(&ev)) != hipSuccess) return fail("event", e);
-    if ((e = hipGetSymbolAddress((void **)&a->dDiag, HIP_SYMBOL(g_diag))) != hipSuccess) return fail("g_diag", e);
+    if ((e = hipMalloc(&a->dDiag, 4 * sizeof(uint32_t))) != hipSuccess) return fail("watchdog record", e);
+    if ((e = hipMemset(a->dDiag, 0, 4 * sizeof(uint32_t))) != hipSuccess) return fail("watchdog record", e);
     if ((e = ensureDeviceTables(device)) != hipSuccess) return fail("device tables", e);
     hipStream_t s0 = a->stream();
     // index upload: genome with guards, tables, overflow, pieces
@@ -1451,12 +1461,14 @@ static int launch_passes(snapgpu_aligner_t *a, int li, const PassIO &io, const A
     A.genome = a->dGenome; A.pieces = a->dPieces; A.nPieces = (int32_t)idx->genome->pieceOffsets.size();
     A.gpl = a->dGPlanes; A.hasIupac = idx->hasIupac ? 1u : 0u;
     A.phaseBuf = a->dPhase;
+    A.diag = a->dDiag;
     A.nBases = idx->genome->nBases; A.seedLen = idx->seedLen; A.nTables = idx->nTables;
     A.padding = idx->genome->chromosomePadding;
     A.maxHits = a->p.maxHitsToConsider; A.maxK = a->p.maxK; A.maxReadSize = a->p.maxReadSize;
     A.maxSeedsCmd = a->p.maxSeedsToUse; A.seedCoverage = a->p.maxSeedCoverage; A.extra = a->p.extraSearchDepth;
     A.explore = a->p.explorePopularSeeds; A.stopOnFirst = a->p.stopOnFirstHit; A.kRows = 31;
     A.radixMin = a->radixMin;
+    A.tripRead = a->tripRead;
     A.tab = a->dTab;
     A.bases = io.bases; A.quals = io.quals; A.offsets = io.offsets; A.lengths = io.lengths;
     A.nReads = (uint32_t)io.n; A.out = io.out;
@@ -1851,18 +1863,18 @@ int snapgpu_align_batch_submit(snapgpu_aligner_t *a, const snapgpu_reads_t *read
         const uint64_t span = std::min(hi[c] + 64, std::max(hostEnd, hi[c])) - lo[c];
         // inputs on the copy stream: they land while the lane's previous chunk is still running
         hipStream_t cs = a->copyStream, s = L.stream;
-        HIPCHK(hipMemcpyAsync(S.dBases, reads->bases + lo[c], span, hipMemcpyHostToDevice, cs));
-        HIPCHK(hipMemcpyAsync(S.dQuals, reads->quals + lo[c], span, hipMemcpyHostToDevice, cs));
-        HIPCHK(hipMemcpyAsync(S.dOffsets, S.hOffsets, m * 8, hipMemcpyHostToDevice, cs));
-        HIPCHK(hipMemcpyAsync(S.dLengths, S.hLengths, m * 4, hipMemcpyHostToDevice, cs));
-        HIPCHK(hipEventRecord(S.h2d, cs));
-        HIPCHK(hipStreamWaitEvent(s, S.h2d, 0));
+        HIPBRK(hipMemcpyAsync(S.dBases, reads->bases + lo[c], span, hipMemcpyHostToDevice, cs));
+        HIPBRK(hipMemcpyAsync(S.dQuals, reads->quals + lo[c], span, hipMemcpyHostToDevice, cs));
+        HIPBRK(hipMemcpyAsync(S.dOffsets, S.hOffsets, m * 8, hipMemcpyHostToDevice, cs));
+        HIPBRK(hipMemcpyAsync(S.dLengths, S.hLengths, m * 4, hipMemcpyHostToDevice, cs));
+        HIPBRK(hipEventRecord(S.h2d, cs));
+        HIPBRK(hipStreamWaitEvent(s, S.h2d, 0));
         PassIO io{S.dBases, S.dQuals, S.dOffsets, S.dLengths, m, L.dOut, L.dDefer, L.dDefer + (L.capReads + 1), L.dSeeds};
         EvSet *ev = nextEvSet(a);
         if (!ev) { rc = SNAPGPU_EDEVICE; break; }
         if ((rc = launch_passes(a, li, io, AlignExt(), *ev, a->nEvUsed >= 2 ? &a->evs[a->nEvUsed - 2] : nullptr))) break;
-        HIPCHK(hipMemcpyAsync(S.hOut, L.dOut, m * sizeof(snapgpu_result_t), hipMemcpyDeviceToHost, s));
-        HIPCHK(hipEventRecord(S.done, s));
+        HIPBRK(hipMemcpyAsync(S.hOut, L.dOut, m * sizeof(snapgpu_result_t), hipMemcpyDeviceToHost, s));
+        HIPBRK(hipEventRecord(S.done, s));
         S.pending = true;
         S.seq = a->chunkSeq++;
         S.chunkBegin = b;
@@ -2088,6 +2100,11 @@ int snapgpu_aligner_get_params(const snapgpu_aligner_t *a, snapgpu_aligner_param
 int snapgpu_aligner_set_overlap(snapgpu_aligner_t *a, int overlap) {
     if (!a) return SNAPGPU_EINVAL;
     a->overlapKernels = overlap != 0;
+    return SNAPGPU_OK;
+}
+int snapgpu_aligner_debug_trip(snapgpu_aligner_t *a, uint32_t read_index) {
+    if (!a) return SNAPGPU_EINVAL;
+    a->tripRead = read_index;
     return SNAPGPU_OK;
 }
 int snapgpu_aligner_max_k(const snapgpu_aligner_t *a) { return a ? (int)a->p.maxK : -1; }

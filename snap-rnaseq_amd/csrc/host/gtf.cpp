@@ -490,7 +490,7 @@ bool gtfCountPair(snapgpu_gtf_t *g, const std::string &tid0, uint32_t tstart0, u
 // The same for a batch of pairs in input order: the interval queries run on host threads (read
 // only), the counter updates afterwards in pair order, so the float transcript counts add up in
 // the reference's order.  Returns the index of the first pair naming an unknown transcript or
-// gene (the counts of the pairs before it applied), or -1.
+// gene, with no counter touched (every event is checked before any is applied), or -1.
 int64_t gtfCountPairs(snapgpu_gtf_t *g, const std::vector<GtfPairQuery> &q) {
     const uint64_t n = q.size();
     std::vector<GtfPairEvent> ev(n);
@@ -501,10 +501,9 @@ int64_t gtfCountPairs(snapgpu_gtf_t *g, const std::vector<GtfPairQuery> &q) {
             for (uint64_t i = n * t / nt; i < n * (t + 1) / nt; i++) pairEvent(g, q[i], ev[i]);
         });
     for (auto &x : th) x.join();
-    for (uint64_t i = 0; i < n; i++) {
+    for (uint64_t i = 0; i < n; i++)
         if (ev[i].bad) return (int64_t)i;
-        applyEvent(ev[i]);
-    }
+    for (uint64_t i = 0; i < n; i++) applyEvent(ev[i]);
     return -1;
 }
 

@@ -595,12 +595,18 @@ int snapgpu_rna_paired_align(snapgpu_paired_aligner_t *pa, snapgpu_aligner_t *ta
     {
         int grc = SNAPGPU_OK;
         std::string gerr;
-        std::thread gt([&] {
+        auto genomeCigars = [&] {
             for (int k = 0; k < 2 && grc == SNAPGPU_OK; k++) grc = gc[k].run(ga, R[k], (int)opt->useM);
             if (grc) gerr = snapgpu_last_error();
-        });
+        };
+        // one aligner's stream, events and upload state serve one host thread at a time: the two
+        // CIGAR loops overlap only when the transcriptome and genome aligners are distinct
+        const bool overlap = ta != ga;
+        std::thread gt;
+        if (overlap) gt = std::thread(genomeCigars);
         for (int k = 0; k < 2 && rc == SNAPGPU_OK; k++) rc = tc[k].run(ta, R[k], (int)opt->useM);
-        gt.join();
+        if (overlap) gt.join();
+        else if (rc == SNAPGPU_OK) genomeCigars();
         if (rc) return fail(rc);
         if (grc) { setError(gerr); return fail(grc); }
     }

@@ -422,6 +422,10 @@ class BaseAligner:
         """Let the pass sets of the two streams run concurrently (default) or one after the other."""
         _check(lib().snapgpu_aligner_set_overlap(self._h, int(bool(overlap))), "set_overlap")
 
+    def debug_trip(self, read_index=0xffffffff):
+        """Test hook: trip this aligner's device watchdog when read `read_index` of a batch starts."""
+        _check(lib().snapgpu_aligner_debug_trip(self._h, int(read_index)), "debug_trip")
+
     def copy_peak_ms(self, nbytes):
         """Diagnostic: best-of-3 time (ms) of a streaming copy of nbytes (read nbytes + write nbytes)."""
         ms = C.c_double()

@@ -274,6 +274,7 @@ _PROTOS = [
     ("snapgpu_aligner_get_stats", C.c_int, [C.c_void_p, C.POINTER(AlignerStats)]),
     ("snapgpu_aligner_max_k", C.c_int, [C.c_void_p]),
     ("snapgpu_aligner_set_overlap", C.c_int, [C.c_void_p, C.c_int]),
+    ("snapgpu_aligner_debug_trip", C.c_int, [C.c_void_p, C.c_uint32]),
     ("snapgpu_phase_cycles", C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]),
     ("snapgpu_aligner_name", C.c_char_p, [C.c_void_p]),
     ("snapgpu_lv_batch", C.c_int, [C.c_int, C.c_int, C.c_uint32, C.c_char_p, C.POINTER(C.c_uint64),
