@@ -213,6 +213,37 @@ def paired_leg(args, idx, local, rank, cpus):
     return out
 
 
+def rna_parity(args, pa, ta, gtf, r0, r1, work):
+    """One more (untimed) run of the RNA leg writing its SAM file; SHA-256 of its records against
+    the reference CLI's own output on the same workload (tests/golden/golden.json "rna_bench",
+    made by make_golden.py --only-rna-bench: `snap-rna paired` over blocks of these pairs)."""
+    import snapgpu
+    ref = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json"))).get("rna_bench")
+    if not ref:
+        return {"compared": False, "why": "no rna_bench digest in tests/golden/golden.json"}
+    if args.workload != "c2" or args.genome_bases or ref["pairs"] != args.rna_pairs:
+        return {"compared": False, "why": "the reference digest covers the default C2 workload with "
+                                          f"{ref['pairs']} pairs only"}
+    sam = os.path.join(work, "rna_parity.sam")
+    gtf.reset_counts()
+    snapgpu.rna_paired_align(pa, ta, gtf, r0, r1, sam)
+    drop = {f"rp{i}" for i in ref["dropped_pairs"]}
+    h = hashlib.sha256()
+    nrec = 0
+    with open(sam) as f:
+        for line in f:
+            if line.startswith("@") or line.split("\t", 1)[0] in drop:
+                continue
+            h.update(line.encode())
+            nrec += 1
+    os.unlink(sam)
+    return {"compared": True, "records": nrec, "reference_records": ref["records"],
+            "sha256_match": h.hexdigest() == ref["sha256"], "reference_runs": ref["reference_runs"],
+            "dropped_pairs": len(ref["dropped_pairs"]),
+            "what": "SAM records of the whole batch vs the reference CLI (`snap-rna paired -t 1`) on the same "
+                    "pairs, genome, GTF"}
+
+
 def rna_leg(args, idx, local, build_threads):
     """SURVEY.md 8(f) f4 (BASELINE configs[4] shape on this workload's genome): the RNA paired
     product path (`snap-rna paired`: transcriptome multi-hit + chimeric genome aligners,
@@ -246,7 +277,8 @@ def rna_leg(args, idx, local, build_threads):
         k = int(np.argsort(ts)[1])
         dt, st = ts[k], sts[k]
         n = r0.n
-        return {"value": 2 * n / dt, "unit": "reads/s", "pairs_per_s": n / dt, "pairs": n, "ms_per_batch": dt * 1e3,
+        parity = rna_parity(args, pa, ta, gtf, r0, r1, work)
+        return {"parity": parity, "value": 2 * n / dt, "unit": "reads/s", "pairs_per_s": n / dt, "pairs": n, "ms_per_batch": dt * 1e3,
                 "read_len": 150, "workload": info, "transcriptome_bases": tidx.info()["nBases"],
                 "stage_ms": {x: round(st[x], 2) for x in ("alignMs", "filterMs", "seedMs", "cigarMs", "writeMs")},
                 "records": {x: st[x] for x in ("singleHits", "multiHits", "notFound", "transcriptomeRecords")},

@@ -16,6 +16,8 @@ TSV/JSON expected outputs.
     python3 tests/golden/make_golden.py --only-paired    # Intersecting + Chimeric paired-end aligner runs
     python3 tests/golden/make_golden.py --only-long      # 129..256-base reads + long LV vectors (align_kernel<256>)
     python3 tests/golden/make_golden.py --only-bam       # `snap-rna single ... -o out.bam` records (BAMFormat)
+    python3 tests/golden/make_golden.py --only-rna150    # `snap-rna paired` on 2 x 150 pairs (configs[4] length)
+    python3 tests/golden/make_golden.py --only-rna-bench # digest of the reference on bench.py's RNA workload
 """
 import hashlib
 import json
@@ -516,7 +518,7 @@ RNA_BLOCK = 200
 COUNT_FILES = ("transcript_id", "transcript_name", "gene_id", "gene_name", "junction_id", "junction_name")
 
 
-def rna_paired_reads(path0, path1, seqs, gtf_path, rng):
+def rna_paired_reads(path0, path1, seqs, gtf_path, rng, n_pairs=3000, lengths=(101, 101, 100, 100, 90, 75)):
     """Read pairs for `snap-rna paired` (PairedAligner.cpp:405-668): mates from spliced mRNAs
     (crossing exon junctions) and from pre-mRNA spans (the transcriptome the reference indexes),
     intergenic pairs, chimeras between genes on one chromosome and on two, same-orientation
@@ -567,9 +569,9 @@ def rna_paired_reads(path0, path1, seqs, gtf_path, rng):
         return c, a
 
     pairs = []
-    for i in range(3000):
+    for i in range(n_pairs):
         u = rng.random()
-        L0 = L1 = rng.choice([101, 101, 100, 100, 90, 75])
+        L0 = L1 = rng.choice(list(lengths))
         if u < 0.30:
             a, b = frag(rng.choice(spliced)[1], L0, L1, rng.randrange(150, 450))
         elif u < 0.45:
@@ -625,13 +627,22 @@ def rna_paired_reads(path0, path1, seqs, gtf_path, rng):
             f1.write(f"@rp{i}/2\n{b}\n+\n{qb}\n")
 
 
-def rna_paired_fixtures(work):
+RNA_SETS = {
+    # name: (rng seed, pairs, mate lengths, file stem)
+    "": (83, 3000, (101, 101, 100, 100, 90, 75), "rna"),
+    # BASELINE configs[4] read length: 2 x 150 (align_kernel<256>, paired_kernel<256>, 150-b CIGARs)
+    "150": (151, 2000, (150, 150, 150, 150, 149, 140, 120), "rna150"),
+}
+
+
+def rna_paired_fixtures(work, variant=""):
     """`snap-rna paired <genome> <transcriptome> <gtf> r1.fq r2.fq -t 1 -o out.sam` (the RNA
     paired product path, PairedAligner.cpp:405-689; BaseAligner.cpp at -O0, see
     oracle/Makefile.ref): the SAM file and the six read-count files GTFReader::WriteReadCounts
-    writes (GTFReader.cpp:1710-1772)."""
+    writes (GTFReader.cpp:1710-1772).  variant "150": 2 x 150 pairs (configs[4]'s read length)."""
     import gzip
-    rng = random.Random(83)
+    seed, n_pairs, lengths, stem = RNA_SETS[variant]
+    rng = random.Random(seed)
     fa = os.path.join(HERE, "small.fa")
     seqs, name = {}, None
     for line in open(fa):
@@ -643,8 +654,8 @@ def rna_paired_fixtures(work):
             seqs[name].append(line.upper())
     seqs = {k: "".join(v) for k, v in seqs.items()}
     gtf = os.path.join(HERE, "small.gtf")
-    fq0, fq1 = os.path.join(HERE, "rna_1.fq"), os.path.join(HERE, "rna_2.fq")
-    rna_paired_reads(fq0, fq1, seqs, gtf, rng)
+    fq0, fq1 = os.path.join(HERE, f"{stem}_1.fq"), os.path.join(HERE, f"{stem}_2.fq")
+    rna_paired_reads(fq0, fq1, seqs, gtf, rng, n_pairs, lengths)
     gidx = os.path.join(work, "gidx")
     ref_index(fa, gidx)
     twd = os.path.join(work, "tx")
@@ -667,6 +678,8 @@ def rna_paired_fixtures(work):
                            capture_output=True, cwd=d)
         return r.returncode == 0
 
+    if variant:
+        return _rna_blocks_bisect(recs, n, attempt, work, fq0, fq1, stem)
     drop = []
     for c in range(0, n, RNA_BLOCK):
         block = list(range(c, min(n, c + RNA_BLOCK)))
@@ -691,11 +704,152 @@ def rna_paired_fixtures(work):
             for cf in COUNT_FILES:
                 counts.append(f"## block {bi} {cf}\n")
                 counts.append(open(os.path.join(work, f"blk{tag}.{cf}.counts.txt")).read())
-        with open(os.path.join(HERE, f"expected_rna_paired{tag}.sam.gz"), "wb") as dst:
+        with open(os.path.join(HERE, f"expected_{stem}_paired{tag}.sam.gz"), "wb") as dst:
             dst.write(gzip.compress("".join(body).encode(), compresslevel=9, mtime=0))
         if not tag:
-            with open(os.path.join(HERE, "expected_rna_paired.counts.txt"), "w") as dst:
+            with open(os.path.join(HERE, f"expected_{stem}_paired.counts.txt"), "w") as dst:
                 dst.write("".join(counts))
+
+
+def _rna_blocks_bisect(recs, n, attempt, work, fq0, fq1, stem):
+    """Block partition for the RNA fixtures whose every block is a clean `snap-rna paired` run in
+    BOTH modes (default and -M), the very runs whose outputs are kept.  The reference's crash in
+    AnalyzeReadIntervals depends on heap layout (it can come and go with an output file name), so
+    a block is accepted only from its final runs; a failing block is halved, and a single pair
+    that still fails is left out.  The block sizes go to expected_<stem>_blocks.json (the test
+    aligns the same blocks with fresh GTF counters)."""
+    import gzip
+
+    def run_block(idx):
+        got = {}
+        for tag, extra in (("", []), ("_M", ["-M"])):
+            if not attempt(idx, work, extra, out=f"blk{tag}"):
+                return None
+            lines = open(os.path.join(work, f"blk{tag}.sam")).read().splitlines(keepends=True)
+            if sum(1 for l in lines if not l.startswith("@")) != 2 * len(idx):
+                return None
+            cnt = {cf: open(os.path.join(work, f"blk{tag}.{cf}.counts.txt")).read() for cf in COUNT_FILES}
+            got[tag] = (lines, cnt)
+        return got
+
+    blocks, drop = [], []
+
+    def solve(idx):
+        r = run_block(idx)
+        if r is not None:
+            blocks.append((idx, r))
+        elif len(idx) == 1:
+            drop.append(idx[0])
+        else:
+            h = len(idx) // 2
+            solve(idx[:h])
+            solve(idx[h:])
+
+    for c in range(0, n, RNA_BLOCK):
+        solve(list(range(c, min(n, c + RNA_BLOCK))))
+    keep = [i for idx, _ in blocks for i in idx]
+    assert keep == sorted(keep)
+    for k, x in enumerate((fq0, fq1)):
+        with open(x, "w") as f:
+            f.write("".join("\n".join(recs[k][4 * i:4 * i + 4]) + "\n" for i in keep))
+    if drop:
+        print("pairs left out (the reference crashes in AnalyzeReadIntervals):", drop)
+    with open(os.path.join(HERE, f"expected_{stem}_blocks.json"), "w") as f:
+        json.dump({"block_sizes": [len(idx) for idx, _ in blocks], "dropped_pairs": drop,
+                   "note": "blocks of the kept pairs, in order; each block is one reference run"}, f)
+    for tag in ("", "_M"):
+        body, counts = [], []
+        for bi, (idx, r) in enumerate(blocks):
+            lines, cnt = r[tag]
+            if bi == 0:
+                body += [l for l in lines if l.startswith("@")]
+            body += [l for l in lines if not l.startswith("@")]
+            for cf in COUNT_FILES:
+                counts.append(f"## block {bi} {cf}\n")
+                counts.append(cnt[cf])
+        with open(os.path.join(HERE, f"expected_{stem}_paired{tag}.sam.gz"), "wb") as dst:
+            dst.write(gzip.compress("".join(body).encode(), compresslevel=9, mtime=0))
+        if not tag:
+            with open(os.path.join(HERE, f"expected_{stem}_paired.counts.txt"), "w") as dst:
+                dst.write("".join(counts))
+
+
+RNA_BENCH_BLOCK = 2000
+
+
+def rna_bench_digest(work, n_pairs=100_000, jobs=8):
+    """Reference output for bench.py's `extras.rna_paired` workload (BASELINE configs[4] shape on
+    the C2 genome): the C2 synthetic genome written as FASTA and indexed by `snap-rna index`, the
+    2,000-gene synthetic GTF and 100k 2 x 150 pairs of tests/rna_synth.py (deterministic, so the GPU
+    box regenerates the same inputs), the transcriptome built by `snap-rna transcriptome`, and
+    `snap-rna paired ... -t 1` run over blocks of pairs (halved where the reference crashes at the
+    end of a run in AnalyzeReadIntervals; a single pair that still crashes is left out).  Stores
+    SHA-256 of the concatenated SAM records (no header) in golden.json["rna_bench"]."""
+    from concurrent.futures import ThreadPoolExecutor
+    from rna_synth import synth_rna_workload
+    gg = snapgpu.Genome.synthetic(**C2["genome"])
+    gfa = os.path.join(work, "c2.fa")
+    gg.write_fasta(gfa)
+    gtf, fq0, fq1, info = synth_rna_workload(gg._h, work, n_pairs=n_pairs)
+    gidx = os.path.join(work, "gidx")
+    ref_index(gfa, gidx)
+    twd = os.path.join(work, "tx")
+    os.makedirs(twd, exist_ok=True)
+    run([SNAP, "transcriptome", gtf, gfa, "tidx", "-O1000"], cwd=twd)
+    recs = [open(x).read().splitlines() for x in (fq0, fq1)]
+    n = len(recs[0]) // 4
+    assert n == n_pairs
+
+    def attempt(idx):
+        d = tempfile.mkdtemp(dir=work, prefix="blk")
+        try:
+            for k in range(2):
+                with open(os.path.join(d, f"r_{k}.fq"), "w") as f:
+                    f.write("".join("\n".join(recs[k][4 * i:4 * i + 4]) + "\n" for i in idx))
+            r = subprocess.run([SNAP, "paired", gidx, os.path.join(twd, "tidx"), gtf, os.path.join(d, "r_0.fq"),
+                                os.path.join(d, "r_1.fq"), "-t", "1", "-o", os.path.join(d, "out.sam")],
+                               capture_output=True, cwd=d)
+            if r.returncode != 0:
+                return None
+            lines = [l for l in open(os.path.join(d, "out.sam")).read().splitlines(keepends=True)
+                     if not l.startswith("@")]
+            return lines if len(lines) == 2 * len(idx) else None
+        finally:
+            shutil.rmtree(d, ignore_errors=True)
+
+    def solve(idx):
+        got = attempt(idx)
+        if got is not None:
+            return [(idx[0], got)], []
+        if len(idx) == 1:
+            return [], [idx[0]]
+        h = len(idx) // 2
+        a, da = solve(idx[:h])
+        b, db = solve(idx[h:])
+        return a + b, da + db
+
+    with ThreadPoolExecutor(jobs) as ex:
+        parts = list(ex.map(solve, [list(range(c, min(n, c + RNA_BENCH_BLOCK)))
+                                    for c in range(0, n, RNA_BENCH_BLOCK)]))
+    blocks = sorted(b for p, _ in parts for b in p)
+    drop = sorted(x for _, d in parts for x in d)
+    h = hashlib.sha256()
+    nrec = 0
+    for _, lines in blocks:
+        for l in lines:
+            h.update(l.encode())
+            nrec += 1
+    out = {"sha256": h.hexdigest(), "records": nrec, "pairs": n, "dropped_pairs": drop,
+           "reference_runs": len(blocks), "workload": info,
+           "what": "SHA-256 of the SAM records (header lines excluded) of `snap-rna paired <C2 index> "
+                   "<transcriptome> synth.gtf r1 r2 -t 1` over tests/rna_synth.py's 100k 2x150 pairs on the "
+                   "C2 genome, in pair order; dropped pairs excluded"}
+    gj = os.path.join(HERE, "golden.json")
+    meta = json.load(open(gj))
+    meta["rna_bench"] = out
+    with open(gj, "w") as f:
+        json.dump(meta, f, indent=1)
+    return out
 
 
 def long_fixtures(work):
@@ -805,6 +959,16 @@ def main():
         long_fixtures(work)
         shutil.rmtree(work, ignore_errors=True)
         print("129..256-base read and LV fixtures written to", HERE)
+        return
+    if "--only-rna-bench" in sys.argv:
+        n = int(sys.argv[sys.argv.index("--only-rna-bench") + 1]) if len(sys.argv) > 2 else 100_000
+        print(json.dumps({k: v for k, v in rna_bench_digest(work, n).items() if k != "workload"}))
+        shutil.rmtree(work, ignore_errors=True)
+        return
+    if "--only-rna150" in sys.argv:
+        rna_paired_fixtures(work, "150")
+        shutil.rmtree(work, ignore_errors=True)
+        print("2 x 150 RNA paired product path fixtures written to", HERE)
         return
     if "--only-rna-paired" in sys.argv:
         rna_paired_fixtures(work)

@@ -7,7 +7,9 @@ of 200 (the reference crashes at the end of larger runs in GTFReader::AnalyzeRea
 is not restated; one pair whose block crashes alone is left out): the SAM records (default and -M)
 and the six read-count files of every block.  Our run builds both indexes itself, aligns each
 block through snapgpu_rna_paired_align with fresh GTF counters and must write the same SAM
-records and count files byte for byte (the @PG line echoes a different command line)."""
+records and count files byte for byte (the @PG line echoes a different command line).
+The 2 x 150 set (make_golden.py --only-rna150, 2,000 pairs, BASELINE configs[4]'s read length)
+is checked the same way over the block partition its generator recorded."""
 import gzip
 import os
 
@@ -21,9 +23,9 @@ BLOCK = 200
 COUNT_FILES = ("transcript_id", "transcript_name", "gene_id", "gene_name", "junction_id", "junction_name")
 
 
-def _expected_counts():
+def _expected_counts(stem="rna"):
     out, cur = {}, None
-    for line in open(os.path.join(G, "expected_rna_paired.counts.txt")):
+    for line in open(os.path.join(G, f"expected_{stem}_paired.counts.txt")):
         if line.startswith("## block "):
             _, _, b, name = line.split()
             cur = (int(b), name)
@@ -55,25 +57,43 @@ def _indexes(tmp_path):
     return gtf, gidx, tidx
 
 
-def _fastq_block(path, b, dst):
+def _blocks(stem, n):
+    """[start, end) of each reference run's pairs: fixed blocks of 200 (the 2 x 101 set), or the
+    partition make_golden.py recorded (expected_<stem>_blocks.json: blocks halved where the
+    reference's AnalyzeReadIntervals crash came up)."""
+    p = os.path.join(G, f"expected_{stem}_blocks.json")
+    if not os.path.exists(p):
+        return [(c, min(n, c + BLOCK)) for c in range(0, n, BLOCK)]
+    import json
+    sizes = json.load(open(p))["block_sizes"]
+    ends = np.cumsum(sizes)
+    assert ends[-1] == n
+    return list(zip([0] + list(ends[:-1]), ends))
+
+
+def _fastq_block(path, a, b, dst):
     lines = open(path).read().splitlines()
     with open(dst, "w") as f:
-        f.write("\n".join(lines[4 * BLOCK * b:4 * BLOCK * (b + 1)]) + "\n")
+        f.write("\n".join(lines[4 * a:4 * b]) + "\n")
 
 
+# stem: 2 x <=101 pairs (rna_*.fq) and 2 x 150 pairs, BASELINE configs[4]'s read length (rna150_*.fq:
+# 150-b mates through align_kernel<256> multi-hit, paired_kernel<256>, 150-b CIGARs and splices)
 @pytest.mark.gpu
-@pytest.mark.parametrize("use_m,fixture", [(0, "expected_rna_paired.sam.gz"), (1, "expected_rna_paired_M.sam.gz")])
-def test_rna_paired_product_path_matches_reference(gpu_available, tmp_path, use_m, fixture):
+@pytest.mark.parametrize("stem", ["rna", "rna150"])
+@pytest.mark.parametrize("use_m", [0, 1])
+def test_rna_paired_product_path_matches_reference(gpu_available, tmp_path, use_m, stem):
+    fixture = f"expected_{stem}_paired{'_M' if use_m else ''}.sam.gz"
     gtf, gidx, tidx = _indexes(tmp_path)
     pa = snapgpu.PairedAligner(gidx, device=0)   # paired CLI defaults (maxHits 16000, maxK 15, 8 seeds)
     ta = snapgpu.BaseAligner(tidx, maxHitsToConsider=16000, maxK=15, maxSeedsToUse=8, extraSearchDepth=2)
-    n = sum(1 for _ in open(os.path.join(G, "rna_1.fq"))) // 4
-    body, counts = [], _expected_counts()
+    n = sum(1 for _ in open(os.path.join(G, f"{stem}_1.fq"))) // 4
+    body, counts = [], _expected_counts(stem)
     totals = dict(partialPairs=0, partialMatches=0, transcriptomeRecords=0, multiHits=0)
-    for b in range((n + BLOCK - 1) // BLOCK):
+    for b, (a0, a1) in enumerate(_blocks(stem, n)):
         f0, f1 = tmp_path / "b_1.fq", tmp_path / "b_2.fq"
-        _fastq_block(os.path.join(G, "rna_1.fq"), b, f0)
-        _fastq_block(os.path.join(G, "rna_2.fq"), b, f1)
+        _fastq_block(os.path.join(G, f"{stem}_1.fq"), a0, a1, f0)
+        _fastq_block(os.path.join(G, f"{stem}_2.fq"), a0, a1, f1)
         r0, r1 = snapgpu.Reads.from_fastq(f0), snapgpu.Reads.from_fastq(f1)
         gtf.reset_counts()
         sam = tmp_path / "b.sam"
@@ -98,3 +118,6 @@ def test_rna_paired_product_path_matches_reference(gpu_available, tmp_path, use_
     # the fixture exercises the filter's branches: transcriptome records, FindPartialMatches
     # scans on the GPU, MultipleHits
     assert totals["transcriptomeRecords"] > 100 and totals["partialPairs"] > 20 and totals["multiHits"] > 10, totals
+    if stem == "rna150":   # the configs[4] read length really is exercised
+        r0 = snapgpu.Reads.from_fastq(os.path.join(G, "rna150_1.fq"))
+        assert sum(1 for i in range(r0.n) if len(r0.get(i)[0]) == 150) > 0.5 * r0.n
