@@ -359,6 +359,9 @@ int snapgpu_aligner_set_overlap(snapgpu_aligner_t *a, int overlap);
  * SNAPGPU_EDEVICE.  Each aligner has its own watchdog record: a trip in one aligner neither
  * fails nor stops another aligner on the same device. */
 int snapgpu_aligner_debug_trip(snapgpu_aligner_t *a, uint32_t read_index);
+/* SHA-256 of the sources this library was built from (snapgpu/_srcsha.py: csrc, this header, the
+ * Makefile); the Python loader refuses a library whose identity differs from the sources beside it. */
+const char *snapgpu_source_sha256(void);
 /* Diagnostic (no reference equivalent): with SNAPGPU_PHASES=1 in the environment at
  * snapgpu_aligner_create, align_kernel<128> sums shader cycles per phase and event
  * counts into out32[0..31] (order: snapgpu.BaseAligner.PHASES); reset != 0 zeroes them. */

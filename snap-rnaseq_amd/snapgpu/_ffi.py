@@ -275,6 +275,7 @@ _PROTOS = [
     ("snapgpu_aligner_max_k", C.c_int, [C.c_void_p]),
     ("snapgpu_aligner_set_overlap", C.c_int, [C.c_void_p, C.c_int]),
     ("snapgpu_aligner_debug_trip", C.c_int, [C.c_void_p, C.c_uint32]),
+    ("snapgpu_source_sha256", C.c_char_p, []),
     ("snapgpu_phase_cycles", C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]),
     ("snapgpu_aligner_name", C.c_char_p, [C.c_void_p]),
     ("snapgpu_lv_batch", C.c_int, [C.c_int, C.c_int, C.c_uint32, C.c_char_p, C.POINTER(C.c_uint64),
@@ -357,8 +358,32 @@ def lib():
             f = getattr(l, name)
             f.restype = res
             f.argtypes = args
+        check_source_identity(l)
         _lib = l
     return _lib
+
+
+class StaleLibraryError(OSError):
+    pass
+
+
+def check_source_identity(l):
+    """The library embeds the identity of the sources it was built from (_srcsha.py); refuse it
+    when the sources beside it differ (a stale prebuilt .so must not run in their place).
+    SNAPGPU_ALLOW_STALE=1 turns the refusal into a warning (diagnostic builds only)."""
+    from . import _srcsha
+    want = _srcsha.source_sha256()
+    if want is None:
+        return
+    got = l.snapgpu_source_sha256().decode() if hasattr(l, "snapgpu_source_sha256") else None
+    if got != want:
+        msg = (f"{LIB_PATH} was built from other sources (embedded {str(got)[:16]}, sources here "
+               f"{want[:16]}): rebuild with `make -C snap-rnaseq_amd`")
+        if os.environ.get("SNAPGPU_ALLOW_STALE") == "1":
+            import warnings
+            warnings.warn(msg)
+        else:
+            raise StaleLibraryError(msg)
 
 
 def last_error():

@@ -192,3 +192,19 @@ def test_timeout_path_frees_nothing():
     """after a device wait times out the aligner is failed and no device buffer is
     freed (a hipFree would block on, or a reuse fault, the still-running kernel)."""
     assert _ffi.lib().snapgpu_selftest_timeout_path() == 0
+
+
+def test_library_identity_matches_sources():
+    """libsnapgpu.so embeds the identity of the sources it was built from (_srcsha.py) and the
+    loader refuses a library built from other sources (verdict r2: binary provenance)."""
+    import snapgpu._ffi as F
+    from snapgpu import _srcsha
+    assert F.lib().snapgpu_source_sha256().decode() == _srcsha.source_sha256()
+
+    class Stale:
+        @staticmethod
+        def snapgpu_source_sha256():
+            return b"0" * 64
+
+    with pytest.raises(F.StaleLibraryError):
+        F.check_source_identity(Stale())

@@ -1,0 +1,140 @@
+// valu_rates.hip -- issue rate of the instruction kinds align_kernel<128> is made of, on gfx950.
+//
+// Verdict r2 item 3: is the kernel's op mix full-rate (2 cycles per wave64 VALU on a SIMD-32
+// once two or more waves issue, MI355X_MICROARCH.md "Wave scheduling") or do its 64-bit shifts,
+// DPP moves, v_ffbl, v_alignbit, v_readlane run at a lower rate?  Each kernel runs a long
+// unrolled stream of ONE instruction kind over 8 independent registers (no dependency stalls),
+// with W waves per SIMD (block = 4*W waves on one CU), and reports shader cycles (s_memtime) per
+// instruction per SIMD: cycles / (instructions per wave * W).
+//
+//   hipcc --offload-arch=gfx950 -O3 -o /tmp/valu_rates tools/gpu/valu_rates.hip && /tmp/valu_rates
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+#include <vector>
+
+#define CHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); return 1; } } while (0)
+
+constexpr int ITERS = 2048;
+constexpr int PER_ITER = 16;   // instructions of the measured kind per loop iteration
+
+// one instruction kind, 16 per iteration over 8 independent registers
+#define K32(OP)                                                                                   \
+    asm volatile(OP(0) OP(1) OP(2) OP(3) OP(4) OP(5) OP(6) OP(7) OP(0) OP(1) OP(2) OP(3) OP(4) OP(5) \
+                     OP(6) OP(7)                                                                   \
+                 : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7)  \
+                 : "s"(sh)                                                                         \
+                 : "vcc", "v40")
+#define K64(OP)                                                                                   \
+    asm volatile(OP(0) OP(1) OP(2) OP(3) OP(4) OP(5) OP(6) OP(7) OP(0) OP(1) OP(2) OP(3) OP(4) OP(5) \
+                     OP(6) OP(7)                                                                   \
+                 : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(q4), "+v"(q5), "+v"(q6), "+v"(q7)  \
+                 : "s"(sh))
+
+#define OP_ADD(i) "v_add_u32 %" #i ", %" #i ", %8\n"
+#define OP_FFBL(i) "v_ffbl_b32 %" #i ", %" #i "\n"
+#define OP_ALIGN(i) "v_alignbit_b32 %" #i ", %" #i ", %" #i ", %8\n"
+#define OP_DPP(i) "v_mov_b32_dpp %" #i ", %" #i " row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+#define OP_WSHR(i) "v_mov_b32_dpp %" #i ", %" #i " wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+#define OP_MAX3(i) "v_max3_i32 %" #i ", %" #i ", %8, %" #i "\n"
+#define OP_CND(i) "v_cndmask_b32 %" #i ", %" #i ", v40, vcc\n"
+#define OP_SHL64(i) "v_lshlrev_b64 %" #i ", %8, %" #i "\n"
+#define OP_SHR64(i) "v_lshrrev_b64 %" #i ", %8, %" #i "\n"
+#define OP_ADD64(i) "v_lshl_add_u64 %" #i ", %" #i ", 0, %" #i "\n"
+
+enum Kind { ADD, FFBL, ALIGN, DPP_ROW, DPP_WAVE, MAX3, CNDMASK, SHL64, SHR64, ADD64, READLANE, NKIND };
+static const char *kName[NKIND] = {"v_add_u32", "v_ffbl_b32", "v_alignbit_b32", "v_mov_b32_dpp row_shr:1",
+                                   "v_mov_b32_dpp wave_shr:1", "v_max3_i32", "v_cndmask_b32",
+                                   "v_lshlrev_b64", "v_lshrrev_b64", "v_lshl_add_u64",
+                                   "v_readlane_b32 (+ s_add_u32 on the result)"};
+
+template <int KIND>
+__global__ __launch_bounds__(1024) void rate_kernel(uint32_t seed, uint64_t *cyc, uint32_t *sink) {
+    const uint32_t t = threadIdx.x + seed;
+    uint32_t r0 = t, r1 = t ^ 1, r2 = t ^ 2, r3 = t ^ 3, r4 = t ^ 4, r5 = t ^ 5, r6 = t ^ 6, r7 = t ^ 7;
+    uint64_t q0 = t, q1 = t + 1, q2 = t + 2, q3 = t + 3, q4 = t + 4, q5 = t + 5, q6 = t + 6, q7 = t + 7;
+    uint32_t sh = (seed & 7) + 1;
+    uint32_t sacc = 0;
+    __syncthreads();
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+#pragma unroll 1
+    for (int it = 0; it < ITERS; it++) {
+        if constexpr (KIND == ADD) K32(OP_ADD);
+        else if constexpr (KIND == FFBL) K32(OP_FFBL);
+        else if constexpr (KIND == ALIGN) K32(OP_ALIGN);
+        else if constexpr (KIND == DPP_ROW) K32(OP_DPP);
+        else if constexpr (KIND == DPP_WAVE) K32(OP_WSHR);
+        else if constexpr (KIND == MAX3) K32(OP_MAX3);
+        else if constexpr (KIND == CNDMASK) K32(OP_CND);
+        else if constexpr (KIND == SHL64) K64(OP_SHL64);
+        else if constexpr (KIND == SHR64) K64(OP_SHR64);
+        else if constexpr (KIND == ADD64) K64(OP_ADD64);
+        else {
+            // VALU -> SGPR -> SALU: the uniform-value idiom of the aligner (uni(), rl())
+            uint32_t s0, s1, s2, s3;
+            asm volatile(
+                "v_readlane_b32 %0, %4, 0\n v_readlane_b32 %1, %5, 1\n v_readlane_b32 %2, %6, 2\n v_readlane_b32 %3, %7, 3\n"
+                "s_add_u32 %0, %0, %1\n s_add_u32 %2, %2, %3\n"
+                "v_readlane_b32 %1, %4, 4\n v_readlane_b32 %3, %5, 5\n v_readlane_b32 %0, %6, 6\n v_readlane_b32 %2, %7, 7\n"
+                "s_add_u32 %0, %0, %1\n s_add_u32 %2, %2, %3\n"
+                "v_readlane_b32 %1, %4, 8\n v_readlane_b32 %3, %5, 9\n v_readlane_b32 %0, %6, 10\n v_readlane_b32 %2, %7, 11\n"
+                "v_readlane_b32 %1, %4, 12\n v_readlane_b32 %3, %5, 13\n v_readlane_b32 %0, %6, 14\n v_readlane_b32 %2, %7, 15\n"
+                : "=&s"(s0), "=&s"(s1), "=&s"(s2), "=&s"(s3)
+                : "v"(r0), "v"(r1), "v"(r2), "v"(r3)
+                : "scc");
+            sacc += s0 + s1 + s2 + s3;
+        }
+    }
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    if ((threadIdx.x & 63) == 0) cyc[blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64] = t1 - t0;
+    const uint32_t x = r0 ^ r1 ^ r2 ^ r3 ^ r4 ^ r5 ^ r6 ^ r7 ^ (uint32_t)(q0 ^ q1 ^ q2 ^ q3 ^ q4 ^ q5 ^ q6 ^ q7) ^ sacc;
+    if (x == 0x12345678u) sink[0] = x;
+}
+
+template <int KIND>
+static int run(int ncu, int wps, double &cpi_wave, double &cpi_simd) {
+    const int waves = 4 * wps;   // one block per CU, wps waves on each of its 4 SIMDs
+    uint64_t *dc;
+    uint32_t *ds;
+    CHK(hipMalloc(&dc, sizeof(uint64_t) * ncu * waves));
+    CHK(hipMalloc(&ds, 4));
+    hipLaunchKernelGGL(rate_kernel<KIND>, dim3(ncu), dim3(64 * waves), 0, 0, 1u, dc, ds);   // warm
+    CHK(hipDeviceSynchronize());
+    hipLaunchKernelGGL(rate_kernel<KIND>, dim3(ncu), dim3(64 * waves), 0, 0, 2u, dc, ds);
+    CHK(hipDeviceSynchronize());
+    std::vector<uint64_t> c(ncu * waves);
+    CHK(hipMemcpy(c.data(), dc, c.size() * 8, hipMemcpyDeviceToHost));
+    double avg = 0;
+    for (auto v : c) avg += (double)v;
+    avg /= (double)c.size();
+    const double instr = (double)ITERS * (KIND == READLANE ? 16 : PER_ITER);
+    cpi_wave = avg / instr;
+    cpi_simd = avg / (instr * wps);
+    (void)hipFree(dc);
+    (void)hipFree(ds);
+    return 0;
+}
+
+template <int KIND>
+static int row(int ncu) {
+    printf("  {\"instruction\": \"%s\"", kName[KIND]);
+    for (int w : {1, 2, 4, 8}) {
+        double cw, cs;
+        if (run<KIND>(ncu, w, cw, cs)) return 1;
+        printf(", \"w%d\": {\"cycles_per_instr_per_wave\": %.3f, \"cycles_per_instr_per_simd\": %.3f}", w, cw, cs);
+    }
+    printf("}%s\n", KIND + 1 < NKIND ? "," : "");
+    return 0;
+}
+
+int main() {
+    int ncu = 0;
+    CHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+    printf("{\"device_cus\": %d, \"iters\": %d, \"note\": \"shader cycles (s_memtime) per instruction; w = waves per "
+           "SIMD; one instruction kind per stream, 8 independent registers\", \"rates\": [\n", ncu, ITERS);
+    int rc = row<ADD>(ncu) | row<FFBL>(ncu) | row<ALIGN>(ncu) | row<DPP_ROW>(ncu) | row<DPP_WAVE>(ncu) |
+             row<MAX3>(ncu) | row<CNDMASK>(ncu) | row<SHL64>(ncu) | row<SHR64>(ncu) | row<ADD64>(ncu) |
+             row<READLANE>(ncu);
+    printf("]}\n");
+    return rc;
+}
