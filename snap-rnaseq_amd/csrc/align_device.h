@@ -135,6 +135,28 @@ struct KArgs {
     snapgpu_multi_hit_t *multiHits;     // [nReads][maxHitsToGet]
 };
 
+// ------------------------------------------------------------ streaming loads
+// Index, genome-plane and hit-list loads are touched once per use; with SNAPGPU_NT they carry
+// the non-temporal hint so they do not push the element arena (re-read and re-written all
+// through a read) out of L2.
+#ifndef SNAPGPU_NT
+#define SNAPGPU_NT 0
+#endif
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+template <typename T>
+__device__ __forceinline__ T ld_stream(const T *p) {
+    if constexpr (SNAPGPU_NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+__device__ __forceinline__ uint4 ld_stream4(const uint4 *p) {
+    if constexpr (SNAPGPU_NT) {
+        const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t *>(p));
+        return make_uint4(v.x, v.y, v.z, v.w);
+    } else {
+        return *p;
+    }
+}
+
 // ------------------------------------------------------------ wave helpers
 // Lane id through volatile asm: the compiler cannot hoist it (or the per-lane LDS
 // addresses derived from it) out of the persistent loop, which would otherwise keep
@@ -707,28 +729,41 @@ __device__ __forceinline__ uint32_t chain_find(const KArgs &A, const Lds<MAXLEN>
     return e;
 }
 
-// selection keys: LDS for the first SKCAP elements of a read, HBM beyond
+// selection keys: LDS for the first SKCAP elements of a read, HBM beyond.  The bit-plane kernels
+// (96-B Elem128 in a wave region sized for 144-B Elem512) keep the HBM keys in a compact array in
+// that region's free tail, transposed by owner lane -- key of element e at [(e % 64) * W + e / 64],
+// W = ceil(arenaElems / 64) -- so the keys of one owner lane (its elements e == owner mod 64) are
+// contiguous: a selection recompute reads them in one coalesced load, not one line per element.
+// The byte path keeps them in the element (Elem512 fills its region).
 template <int MAXLEN>
-__device__ __forceinline__ uint32_t sk_get(const Lds<MAXLEN> &S, const ElemOf<MAXLEN> *ar, uint32_t e) {
-    return e < SKCAP ? S.sk[e] : ar[e].sortkey;
+__device__ __forceinline__ uint32_t *sk_hbm(const KArgs &A, const ElemOf<MAXLEN> *ar, uint32_t e) {
+    const uint32_t W = (uint32_t)((A.arenaElems + 63) >> 6);
+    return reinterpret_cast<uint32_t *>(const_cast<ElemOf<MAXLEN> *>(ar) + A.arenaElems) + (e & 63u) * W + (e >> 6);
 }
 template <int MAXLEN>
-__device__ __forceinline__ void sk_set(Lds<MAXLEN> &S, ElemOf<MAXLEN> *ar, uint32_t e, uint32_t v) {
+__device__ __forceinline__ uint32_t sk_get(const KArgs &A, const Lds<MAXLEN> &S, const ElemOf<MAXLEN> *ar, uint32_t e) {
+    if (e < SKCAP) return S.sk[e];
+    if constexpr (Lds<MAXLEN>::BYTE_PATH) return ar[e].sortkey;
+    else return *sk_hbm<MAXLEN>(A, ar, e);
+}
+template <int MAXLEN>
+__device__ __forceinline__ void sk_set(const KArgs &A, Lds<MAXLEN> &S, ElemOf<MAXLEN> *ar, uint32_t e, uint32_t v) {
     if (e < SKCAP) S.sk[e] = v;
-    else ar[e].sortkey = v;
+    else if constexpr (Lds<MAXLEN>::BYTE_PATH) ar[e].sortkey = v;
+    else *sk_hbm<MAXLEN>(A, ar, e) = v;
 }
 
 // recompute of `owner`'s selection maximum (elements e == owner mod 64), the whole wave
 // scanning that lane's elements 64 at a time
 template <int MAXLEN>
-__device__ __forceinline__ void recompute_lane_max(Lds<MAXLEN> &S, const ElemOf<MAXLEN> *ar, int owner) {
+__device__ __forceinline__ void recompute_lane_max(const KArgs &A, Lds<MAXLEN> &S, const ElemOf<MAXLEN> *ar, int owner) {
     const int lane = lane_id();
     uint64_t best = 0;
     const uint32_t nElems = S.nElems;
 #pragma unroll 1
     for (uint32_t b = (uint32_t)owner; b < nElems; b += WAVE * WAVE) {
         const uint32_t e = b + WAVE * (uint32_t)lane;
-        const uint32_t k = e < nElems ? sk_get(S, ar, e) : 0u;
+        const uint32_t k = e < nElems ? sk_get(A, S, ar, e) : 0u;
         const uint64_t v = ((uint64_t)k << 32) | e;
         if (k && v > best) best = v;
     }

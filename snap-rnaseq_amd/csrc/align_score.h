@@ -378,7 +378,7 @@ __device__ __forceinline__ void lv_pass(const KArgs &A, Lds<MAXLEN> &S, uint32_t
         const uint32_t sh = (uint32_t)gp & 31;
         uint4 w[2 * NW + 1];
 #pragma unroll
-        for (int j = 0; j < 2 * NW + 1; j++) w[j] = src[j];
+        for (int j = 0; j < 2 * NW + 1; j++) w[j] = ld_stream4(src + j);
         const uint64_t *rp = &G.rpl[P.dir][0][0];
         uint64_t RHw[NW], RLw[NW], RMw[NW];
 #pragma unroll
@@ -587,7 +587,7 @@ __device__ __forceinline__ bool forced_sort(const KArgs &A, Lds<MAXLEN> &S, Elem
     for (uint32_t e0 = 0; e0 < nE; e0 += WAVE) {   // linked elements, compacted in index order
         const int lane = lane_id();
         const uint32_t e = e0 + (uint32_t)lane;
-        const uint32_t k = e < nE ? sk_get(S, ar, e) : 0u;
+        const uint32_t k = e < nE ? sk_get(A, S, ar, e) : 0u;
         const uint64_t m = ballot(k != 0u);
         if (k) bufA[n + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = ((uint64_t)k << 32) | e;
         n += (uint32_t)__popcll(m);
@@ -689,9 +689,9 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, El
             if (kmax != 0) {
                 const int owner = (int)__builtin_ctzll(ballot((uint32_t)(lm >> 32) == kmax));
                 const uint32_t e = readlaneu((uint32_t)lm, owner);
-                sk_set(S, ar, e, 0);                       // unlink (BaseAligner.cpp:1391-1394)
+                sk_set(A, S, ar, e, 0);                       // unlink (BaseAligner.cpp:1391-1394)
                 wave_sync();
-                recompute_lane_max(S, ar, owner);
+                recompute_lane_max(A, S, ar, owner);
                 if (lane == 0) G.eidx[0] = e;
                 nb = 1;
                 wave_sync();
@@ -716,7 +716,7 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, El
                 uint32_t inRange = 0;
                 for (uint32_t e0 = 0; e0 < nE; e0 += WAVE) {
                     const uint32_t e = e0 + lane;
-                    const uint32_t ke = e < nE ? sk_get(S, ar, e) : 0u;
+                    const uint32_t ke = e < nE ? sk_get(A, S, ar, e) : 0u;
                     uint32_t rank = 0;
                     uint32_t f = 0;
                     for (; f + 4 <= nL; f += 4) {
@@ -727,7 +727,7 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, El
                     for (uint32_t b0 = SKCAP; b0 < nE; b0 += SKCAP) {
                         const uint32_t nk = nE - b0 < SKCAP ? nE - b0 : SKCAP;
                         wave_sync();
-                        for (uint32_t j = lane; j < ((nk + 3) & ~3u); j += WAVE) stage[j] = j < nk ? ar[b0 + j].sortkey : 0u;
+                        for (uint32_t j = lane; j < ((nk + 3) & ~3u); j += WAVE) stage[j] = j < nk ? sk_get(A, S, ar, b0 + j) : 0u;
                         wave_sync();
                         for (uint32_t g = 0; g < nk; g += 4) {
                             const uint4 k4 = *reinterpret_cast<const uint4 *>(&stage[g]);

@@ -78,9 +78,9 @@ __device__ __forceinline__ bool score_wave(const KArgs &A, Lds<MAXLEN> &S, Elem5
         const uint32_t ebase = (ekey >> 1) * ELEM;
         // unlink now (allExtantCandidatesScored = true, BaseAligner.cpp:1391-1394): no
         // insertion happens while an element is scored, so the next selection is known
-        sk_set(S, ar, e, 0);
+        sk_set(A, S, ar, e, 0);
         wave_sync();
-        recompute_lane_max(S, ar, (int)(e % WAVE));
+        recompute_lane_max(A, S, ar, (int)(e % WAVE));
         wave_sync();
         if (((ewl >> 8) & 0xff) <= st.scoreLimit) {
             uint64_t mask = used;
@@ -226,7 +226,7 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
         const uint32_t lpsNow = dir ? st.lps[1] : st.lps[0];
         const bool allowAlloc = lpsNow <= st.scoreLimit;
         bool valid = i < lim;
-        uint32_t h = valid ? (list ? list[ii] : (dir ? single1 : single0)) : 0;
+        uint32_t h = valid ? (list ? ld_stream(list + ii) : (dir ? single1 : single0)) : 0;
         uint32_t loc = h - offset;
         valid = valid && h >= offset;
         if constexpr (EXT) valid = valid && loc >= minLoc && loc <= maxLoc;   // BaseAligner.cpp:849-853
@@ -257,8 +257,15 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
             if (e != NONE || allowAlloc) {
                 uint64_t used = 0;
                 uint32_t weight = 0, allScored = 0, sortkey = 0;
+                // header dword 11 = weight | lps << 8 | allScored << 16; a new element's header is
+                // written at the end in three 16-byte stores instead of field by field
+                uint32_t w11 = 0, chainNext = NONE;
+                bool isNew = false;
                 if (e != NONE) {
-                    used = ar[e].used; weight = ar[e].weight; allScored = ar[e].allScored; sortkey = sk_get(S, ar, e);
+                    const uint32_t *eh = reinterpret_cast<const uint32_t *>(ar + e);
+                    used = *reinterpret_cast<const uint64_t *>(eh);
+                    w11 = eh[11];
+                    weight = w11 & 0xff; allScored = (w11 >> 16) & 0xff; sortkey = sk_get(A, S, ar, e);
                 }
                 uint64_t m = grp;
                 while (m) {
@@ -274,16 +281,11 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
                             overflow = true;
                             break;
                         }
-                        auto *ne = ar + e;
-                        ne->key = key;
-                        ne->scored = 0;
-                        ne->lps = (uint8_t)lpsNow;
-                        ne->bestScore = UNUSED_SCORE;
-                        ne->bestLoc = 0;
-                        ne->prob = 0;
+                        isNew = true;
+                        w11 = (lpsNow & 0xffu) << 8;
                         const uint32_t old = atomicExch(&S.head[elem_hash(key)], e);
                         if (e < MIRCAP) { S.ekey[e] = key; S.enext[e] = (uint16_t)(old == NONE ? 0xffffu : old); }
-                        else ne->next = old;
+                        chainNext = old;
                         used = 1ull << bit;
                         weight = 1;
                         allScored = 0;
@@ -302,10 +304,19 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
                 }
                 if (overflow) e = NONE;
                 if (e != NONE) {
-                    ar[e].used = used;
-                    ar[e].weight = (uint8_t)weight;
-                    ar[e].allScored = (uint8_t)allScored;
-                    sk_set(S, ar, e, sortkey);
+                    uint32_t *eh = reinterpret_cast<uint32_t *>(ar + e);
+                    w11 = (w11 & 0xff00ff00u) | (weight & 0xffu) | ((allScored & 0xffu) << 16);
+                    if (isNew) {
+                        // {used, scored = 0}, {prob = 0, key, next}, {bestScore, bestLoc, sortkey, w11}
+                        uint4 *h4 = reinterpret_cast<uint4 *>(eh);
+                        h4[0] = make_uint4((uint32_t)used, (uint32_t)(used >> 32), 0u, 0u);
+                        h4[1] = make_uint4(0u, 0u, key, chainNext);
+                        h4[2] = make_uint4(UNUSED_SCORE, 0u, sortkey, w11);
+                    } else {
+                        *reinterpret_cast<uint64_t *>(eh) = used;
+                        eh[11] = w11;
+                    }
+                    sk_set(A, S, ar, e, sortkey);
                     if (sortkey) atomicMax((unsigned long long *)&S.laneMax[e % WAVE], ((uint64_t)sortkey << 32) | e);
                 }
             }
@@ -509,7 +520,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
                     if (pos >= size) pos %= size;
                     uint32_t kj = 0, v1j = INVALID, v2j = 0;
                     bool beyond = j > size + 5;
-                    if (lane < 8 && !beyond) { kj = T[3 * pos]; v1j = T[3 * pos + 1]; v2j = T[3 * pos + 2]; }
+                    if (lane < 8 && !beyond) { kj = ld_stream(T + 3 * pos); v1j = ld_stream(T + 3 * pos + 1); v2j = ld_stream(T + 3 * pos + 2); }
                     bool stop = (j == 0) ? (kj == key && v1j != INVALID) : (kj == key || v1j == INVALID);
                     uint64_t m = ballot(lane < 8 && (stop || beyond)) & 0xffull;
                     if (m) {
@@ -532,7 +543,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
                     if (vf < A.nBases) { nH0 = 1; sg0 = vf; }
                     else if (vf != UNUSED_SIDE) {
                         uint32_t o = vf - A.nBases;
-                        nH0 = pre ? (pcnt & 0xffff) : uni(A.overflow[o]);
+                        nH0 = pre ? (pcnt & 0xffff) : uni(ld_stream(A.overflow + o));
                         ls0 = A.overflow + o + 1;
                         sv_add(st, lane, SV_OVF, 1);
                     }
@@ -540,7 +551,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
                     else if (vr < A.nBases) { nH1 = 1; sg1 = vr; }
                     else if (vr != UNUSED_SIDE) {
                         uint32_t o = vr - A.nBases;
-                        nH1 = pre ? (pcnt >> 16) : uni(A.overflow[o]);
+                        nH1 = pre ? (pcnt >> 16) : uni(ld_stream(A.overflow + o));
                         ls1 = A.overflow + o + 1;
                         sv_add(st, lane, SV_OVF, 1);
                     }

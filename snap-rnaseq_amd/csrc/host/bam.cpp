@@ -1,4 +1,4 @@
-// bam.cpp -- BAM output of the single-end product path (the rest of it):
+// bam.cpp -- BAM output of the single-end and RNA paired product paths:
 // BAMFormat::writeHeader / writeRead (SNAPLib/Bam.cpp:542-790) over the same per-record fields
 // the SAM writer prints (getSAMData, SAM.cpp:804-975), and a BGZF stream (the reference's
 // GzipWriterFilter with 64 KB blocks, DataWriterSupplier::gzip(true, 0x10000, ...)).
@@ -20,8 +20,14 @@ namespace snapgpu {
 
 namespace {
 
-const int SAM_UNMAPPED = 0x004;            // SAM.h:38-46
+const int SAM_MULTI_SEGMENT = 0x001;       // SAM.h:38-46
+const int SAM_ALL_ALIGNED = 0x002;
+const int SAM_UNMAPPED = 0x004;
+const int SAM_NEXT_UNMAPPED = 0x008;
 const int SAM_REVERSE_COMPLEMENT = 0x010;
+const int SAM_NEXT_REVERSED = 0x020;
+const int SAM_FIRST_SEGMENT = 0x040;
+const int SAM_LAST_SEGMENT = 0x080;
 
 inline char upperCase(char c) { return (c >= 'a' && c <= 'z') ? (char)(c - 0x20) : c; }
 inline char complementOf(char c) {
@@ -75,9 +81,11 @@ void put(std::string &o, T v) { o.append(reinterpret_cast<const char *>(&v), siz
 
 }  // namespace
 
-// One BAMFormat::writeRead record (a read without mate) appended to o.  nm: the NM value the
-// reference writes (the record's own edit distance when it has a location, else the previous
-// record's).  False if the QNAME is too long for BAM (the reference exits, Bam.cpp:723-726).
+// One BAMFormat::writeRead record appended to o (Bam.cpp:596-790): a read without mate, or one end
+// of a pair (L.hasMate: getSAMData's mate branch, SAM.cpp:914-973, with piece indices where the SAM
+// line has names).  nm: the NM value the reference writes (the record's own edit distance when it
+// has a location, else the previous record's).  False if the QNAME is too long for BAM (the
+// reference exits, Bam.cpp:723-726).
 bool bamAppendRecord(std::string &o, const Genome &g, const SamLine &L, int32_t nm) {
     static const char kOp[] = "MIDNSHP=X";
     uint32_t loc = L.loc;
@@ -95,6 +103,39 @@ bool bamAppendRecord(std::string &o, const Genome &g, const SamLine &L, int32_t 
         mapq = std::max(0, std::min(70, L.mapq));
     } else {
         flags |= SAM_UNMAPPED;
+    }
+    int mateIdx = -1;
+    uint32_t matePos = 0;
+    int64_t tlen = 0;
+    if (L.hasMate) {
+        flags |= SAM_MULTI_SEGMENT | (L.firstInPair ? SAM_FIRST_SEGMENT : SAM_LAST_SEGMENT);
+        if (L.mateLoc != kInvalidLocation) {
+            const int mp = pieceAt(g, L.mateLoc);
+            if (mp >= 0) {
+                mateIdx = mp;
+                matePos = L.mateLoc - g.pieceOffsets[mp] + 1;
+            }
+            if (L.mateDir == SNAPGPU_RC) flags |= SAM_NEXT_REVERSED;
+            if (loc == kInvalidLocation) {   // the unmapped end takes the mate's RNAME / POS
+                pieceIdx = mateIdx;
+                pos = matePos;
+            }
+        } else {                             // the mate is unmapped: it points at this end
+            flags |= SAM_NEXT_UNMAPPED;
+            mateIdx = pieceIdx;
+            matePos = pos;
+        }
+        if (loc != kInvalidLocation && L.mateLoc != kInvalidLocation) {
+            flags |= SAM_ALL_ALIGNED;
+            const uint32_t back = L.fullLen - L.clippedLen - L.front;
+            const uint32_t before = rc ? back : L.front, after = rc ? L.front : back;
+            const int64_t myStart = (int64_t)(uint32_t)(loc - before);
+            const int64_t myEnd = (int64_t)(uint32_t)(loc + L.clippedLen + after);
+            const int64_t mBefore = L.mateFront, mAfter = (int64_t)L.mateFullLen - L.mateClippedLen - L.mateFront;
+            const int64_t mateStart = (int64_t)L.mateLoc - (L.mateDir == SNAPGPU_RC ? mAfter : mBefore);
+            const int64_t mateEnd = (int64_t)L.mateLoc + L.mateClippedLen + (L.mateDir == SNAPGPU_FORWARD ? mAfter : mBefore);
+            if (pieceIdx >= 0 && pieceIdx == mateIdx) tlen = myStart < mateStart ? mateEnd - myStart : -(myEnd - mateStart);
+        }
     }
     const uint32_t qlen = L.qnameLen ? L.qnameLen : L.idLen;
     if (qlen > 254) return false;
@@ -118,7 +159,10 @@ bool bamAppendRecord(std::string &o, const Genome &g, const SamLine &L, int32_t 
     const uint32_t len = L.fullLen;
     int refLength = ops.empty() ? (int)len : 0;
     for (uint32_t op : ops) refLength += kRefBase[op & 15] * (int)(op >> 4);
-    const int bin = L.loc != kInvalidLocation ? reg2bin((int)pos - 1, (int)pos - 1 + refLength) : reg2bin(-1, 0);
+    // unmapped: at the mate's position, length 1, or at -1 (Bam.cpp:752-756)
+    const int bin = L.loc != kInvalidLocation ? reg2bin((int)pos - 1, (int)pos - 1 + refLength)
+                  : (L.hasMate && L.mateLoc != kInvalidLocation) ? reg2bin((int)matePos - 1, (int)matePos)
+                                                                  : reg2bin(-1, 0);
     const size_t rgLen = L.rg ? strlen(L.rg) : 0;
     const size_t size = 36 + qlen + 1 + 4 * ops.size() + (len + 1) / 2 + len + (L.rg ? 4 + rgLen : 0) + 8 + 7;
     const size_t start = o.size();
@@ -131,9 +175,9 @@ bool bamAppendRecord(std::string &o, const Genome &g, const SamLine &L, int32_t 
     put<uint16_t>(o, (uint16_t)ops.size());              // n_cigar_op
     put<uint16_t>(o, (uint16_t)flags);
     put<int32_t>(o, (int32_t)len);                       // l_seq
-    put<int32_t>(o, -1);                                 // next_refID (no mate)
-    put<int32_t>(o, -1);                                 // next_pos
-    put<int32_t>(o, 0);                                  // tlen
+    put<int32_t>(o, mateIdx);                            // next_refID (-1 without mate)
+    put<int32_t>(o, (int32_t)matePos - 1);               // next_pos
+    put<int32_t>(o, (int32_t)tlen);                      // tlen
     o.append(L.id, qlen);
     o += '\0';
     for (uint32_t op : ops) put<uint32_t>(o, op);

@@ -647,6 +647,28 @@ int snapgpu_rna_paired_align(snapgpu_paired_aligner_t *pa, snapgpu_aligner_t *ta
     const unsigned ntd = n < 2048 ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     std::vector<std::string> parts(ntd);
     std::vector<uint64_t> cnt(3 * ntd, 0);
+    // BAM when the path ends in ".bam" (BAMFormat::writeRead for both ends, Bam.cpp:596-790).  Its NM
+    // is set only for a record with a location; the others repeat the previous record's value, so a
+    // serial pass in write order (per pair: the end at the lower location first) fixes each NM.
+    const size_t spl = samPath ? strlen(samPath) : 0;
+    const bool bam = spl >= 4 && strcmp(samPath + spl - 4, ".bam") == 0;
+    std::vector<int32_t> bamNm;
+    std::vector<uint8_t> bamBad(ntd, 0);
+    if (bam) {
+        bamNm.resize(2 * n);
+        int32_t last = 0;   // before any mapped record the reference writes its stack's leftover
+        for (uint64_t i = 0; i < n; i++) {
+            const PairOut &r = po[i];
+            uint32_t locs[2];
+            for (int k = 0; k < 2; k++) locs[k] = r.status[k] != SNAPGPU_NOT_FOUND ? r.location[k] : kInvalidLocation;
+            const int first = locs[0] > locs[1];
+            for (int w = 0; w < 2; w++) {
+                const int k = w == 0 ? first : 1 - first;
+                if (locs[k] != kInvalidLocation) last = isT[k][i] ? tc[k].edOf(i) : gc[k].edOf(i);
+                bamNm[2 * i + w] = last;
+            }
+        }
+    }
     parallel(n, [&](unsigned t, uint64_t b, uint64_t e) {
         std::string &o = parts[t];
         o.reserve((e - b) * 640);
@@ -692,11 +714,17 @@ int snapgpu_rna_paired_align(snapgpu_paired_aligner_t *pa, snapgpu_aligner_t *ta
                 L.mateFront = R[m]->frontClipped[i];
                 L.mateClippedLen = R[m]->lengths[i];
                 L.mateFullLen = R[m]->unclippedLength[i];
-                samAppendLine(o, *gi->genome, L);
+                if (!bam) samAppendLine(o, *gi->genome, L);
+                else if (!bamAppendRecord(o, *gi->genome, L, bamNm[2 * i + w])) bamBad[t] = 1;
                 cnt[3 * t + (r.status[k] == SNAPGPU_SINGLE_HIT ? 0 : r.status[k] == SNAPGPU_MULTIPLE_HITS ? 1 : 2)]++;
             }
         }
     });
+    for (unsigned t = 0; t < ntd; t++)
+        if (bamBad[t]) {
+            setError("rna_paired_align: BAM record not written (QNAME longer than 254 characters, Bam.cpp:723-726)");
+            return fail(SNAPGPU_EINVAL);
+        }
     for (unsigned t = 0; t < ntd; t++) { st.singleHits += cnt[3 * t]; st.multiHits += cnt[3 * t + 1]; st.notFound += cnt[3 * t + 2]; }
     if (samPath) {
         FILE *f = fopen(samPath, "w");
@@ -707,8 +735,18 @@ int snapgpu_rna_paired_align(snapgpu_paired_aligner_t *pa, snapgpu_aligner_t *ta
         std::string hdr(hlen, '\0');
         if ((rc = snapgpu_sam_header(gi, 0, opt->commandLine ? opt->commandLine : "", opt->version ? opt->version : "",
                                      nullptr, &hdr[0], hlen, &hlen))) { fclose(f); return fail(rc); }
-        bool ok = fwrite(hdr.data(), 1, hdr.size(), f) == hdr.size();
-        for (auto &p : parts) ok = ok && fwrite(p.data(), 1, p.size(), f) == p.size();
+        bool ok = true;
+        if (bam) {   // BGZF stream: header, then the records (64 KB blocks), then the EOF block
+            hdr.resize(strnlen(hdr.data(), hdr.size()));
+            const std::string bh = bamHeader(*gi->genome, hdr);
+            ok = bgzfWrite(f, bh.data(), bh.size(), false);
+            std::string all;
+            for (auto &p : parts) all += p;
+            ok = ok && bgzfWrite(f, all.data(), all.size(), true);
+        } else {
+            ok = fwrite(hdr.data(), 1, hdr.size(), f) == hdr.size();
+            for (auto &p : parts) ok = ok && fwrite(p.data(), 1, p.size(), f) == p.size();
+        }
         ok = (fclose(f) == 0) && ok;
         if (!ok) { setError(std::string("write failed: ") + samPath); return fail(SNAPGPU_EIO); }
     }

@@ -373,8 +373,8 @@ def check_source_identity(l):
     SNAPGPU_ALLOW_STALE=1 turns the refusal into a warning (diagnostic builds only)."""
     from . import _srcsha
     want = _srcsha.source_sha256()
-    if want is None:
-        return
+    if want is None or os.path.abspath(LIB_PATH) != os.path.join(_HERE, "libsnapgpu.so"):
+        return   # no sources here, or an explicitly chosen variant build (SNAPGPU_LIB, tools/build_variant.sh)
     got = l.snapgpu_source_sha256().decode() if hasattr(l, "snapgpu_source_sha256") else None
     if got != want:
         msg = (f"{LIB_PATH} was built from other sources (embedded {str(got)[:16]}, sources here "

@@ -18,6 +18,7 @@ TSV/JSON expected outputs.
     python3 tests/golden/make_golden.py --only-bam       # `snap-rna single ... -o out.bam` records (BAMFormat)
     python3 tests/golden/make_golden.py --only-rna150    # `snap-rna paired` on 2 x 150 pairs (configs[4] length)
     python3 tests/golden/make_golden.py --only-rna-bench # digest of the reference on bench.py's RNA workload
+    python3 tests/golden/make_golden.py --only-rna-bam   # `snap-rna paired ... -o out.bam` records (both RNA sets)
 """
 import hashlib
 import json
@@ -852,6 +853,78 @@ def rna_bench_digest(work, n_pairs=100_000, jobs=8):
     return out
 
 
+def _bam_unpack(raw):
+    """-> (reference list [[name, l_ref]], record bytes) of a decompressed BAM stream."""
+    import struct
+    assert raw[:4] == b"BAM\1"
+    at = 8 + struct.unpack_from("<i", raw, 4)[0]
+    n_ref = struct.unpack_from("<i", raw, at)[0]
+    at += 4
+    refs = []
+    for _ in range(n_ref):
+        ln = struct.unpack_from("<i", raw, at)[0]
+        refs.append([raw[at + 4:at + 4 + ln - 1].decode(), struct.unpack_from("<i", raw, at + 4 + ln)[0]])
+        at += 8 + ln
+    return refs, raw[at:]
+
+
+def _bam_count(recs):
+    import struct
+    n, at = 0, 0
+    while at < len(recs):
+        at += 4 + struct.unpack_from("<i", recs, at)[0]
+        n += 1
+    return n
+
+
+def rna_bam_fixtures(work):
+    """`snap-rna paired ... -o out.bam` (SimpleReadWriter::writePair -> BAMFormat::writeRead with the
+    mate, ReadWriter.cpp:133-217, Bam.cpp:596-790) over the same blocks as the SAM fixtures of both
+    RNA read sets (2 x <=101 in blocks of 200, 2 x 150 over expected_rna150_blocks.json).  A block
+    whose run exits non-zero is kept when its BGZF stream is complete (EOF block) and holds both
+    records of every pair: the reference writes and closes the BAM before the crash in
+    AnalyzeReadIntervals that comes and goes with heap layout.  Stores the decompressed records of
+    the blocks concatenated and the reference list."""
+    import gzip
+    fa = os.path.join(HERE, "small.fa")
+    gtf = os.path.join(HERE, "small.gtf")
+    gidx = os.path.join(work, "gidx")
+    ref_index(fa, gidx)
+    twd = os.path.join(work, "tx")
+    os.makedirs(twd, exist_ok=True)
+    run([SNAP, "transcriptome", gtf, fa, "tidx", "-O1000"], cwd=twd)
+    eof = bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
+    for stem in ("rna", "rna150"):
+        recs = [open(os.path.join(HERE, f"{stem}_{k}.fq")).read().splitlines() for k in (1, 2)]
+        n = len(recs[0]) // 4
+        bj = os.path.join(HERE, f"expected_{stem}_blocks.json")
+        sizes = json.load(open(bj))["block_sizes"] if os.path.exists(bj) else \
+            [min(RNA_BLOCK, n - c) for c in range(0, n, RNA_BLOCK)]
+        for tag, extra in (("", []), ("_M", ["-M"])):
+            body, refs, at = [], None, 0
+            for sz in sizes:
+                for k in range(2):
+                    with open(os.path.join(work, f"b_{k}.fq"), "w") as f:
+                        f.write("".join("\n".join(recs[k][4 * i:4 * i + 4]) + "\n" for i in range(at, at + sz)))
+                out = os.path.join(work, "b.bam")
+                if os.path.exists(out):
+                    os.unlink(out)
+                subprocess.run([SNAP, "paired", gidx, os.path.join(twd, "tidx"), gtf, os.path.join(work, "b_0.fq"),
+                                os.path.join(work, "b_1.fq"), "-t", "1", "-o", out] + extra, capture_output=True,
+                               cwd=work)
+                data = open(out, "rb").read()
+                assert data.endswith(eof), f"{stem} block at {at}: incomplete BAM"
+                rf, rc_ = _bam_unpack(gzip.decompress(data))
+                assert _bam_count(rc_) == 2 * sz, f"{stem} block at {at}: {_bam_count(rc_)} records"
+                refs = refs or rf
+                body.append(rc_)
+                at += sz
+            with open(os.path.join(HERE, f"expected_{stem}_paired{tag}.bam.records.gz"), "wb") as f:
+                f.write(gzip.compress(b"".join(body), compresslevel=9, mtime=0))
+            with open(os.path.join(HERE, f"expected_{stem}_paired.bam.refs.json"), "w") as f:
+                json.dump(refs, f)
+
+
 def long_fixtures(work):
     """Reads of 129..256 bases (align_kernel<256>: 256-bit bit-plane masks) on the small genome:
     synthetic 150 / 250 bp and mixed-length reads with the reference's own AlignRead outputs for
@@ -964,6 +1037,11 @@ def main():
         n = int(sys.argv[sys.argv.index("--only-rna-bench") + 1]) if len(sys.argv) > 2 else 100_000
         print(json.dumps({k: v for k, v in rna_bench_digest(work, n).items() if k != "workload"}))
         shutil.rmtree(work, ignore_errors=True)
+        return
+    if "--only-rna-bam" in sys.argv:
+        rna_bam_fixtures(work)
+        shutil.rmtree(work, ignore_errors=True)
+        print("RNA paired BAM fixtures written to", HERE)
         return
     if "--only-rna150" in sys.argv:
         rna_paired_fixtures(work, "150")
