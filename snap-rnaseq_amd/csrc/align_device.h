@@ -86,6 +86,7 @@ template <int MAXLEN> using ElemOf = typename ElemSel<MAXLEN>::type;
 
 struct KArgs {
     uint32_t *diag;              // this aligner's watchdog record {code, read, detail, 0} (diag_report)
+    uint32_t *skArr;             // bit-plane kernels: selection keys of elements >= SKCAP (sk_hbm)
     // index (HBM)
     const uint32_t *slots;
     const uint64_t *tableBase;
@@ -730,27 +731,28 @@ __device__ __forceinline__ uint32_t chain_find(const KArgs &A, const Lds<MAXLEN>
 }
 
 // selection keys: LDS for the first SKCAP elements of a read, HBM beyond.  The bit-plane kernels
-// (96-B Elem128 in a wave region sized for 144-B Elem512) keep the HBM keys in a compact array in
-// that region's free tail, transposed by owner lane -- key of element e at [(e % 64) * W + e / 64],
-// W = ceil(arenaElems / 64) -- so the keys of one owner lane (its elements e == owner mod 64) are
-// contiguous: a selection recompute reads them in one coalesced load, not one line per element.
-// The byte path keeps them in the element (Elem512 fills its region).
+// keep the HBM keys in a compact per-wave array (KArgs::skArr: the tail of the lane's arena
+// allocation, which is sized for 144-B Elem512 while these kernels use 96-B Elem128), transposed by
+// owner lane -- key of element e at [(e % 64) * W + e / 64], W = ceil(arenaElems / 64) -- so the
+// keys of one owner lane (its elements e == owner mod 64) are contiguous: a selection recompute
+// reads them in one coalesced load, not one line per element.  The byte path keeps them in the
+// element (Elem512 fills the allocation).
 template <int MAXLEN>
-__device__ __forceinline__ uint32_t *sk_hbm(const KArgs &A, const ElemOf<MAXLEN> *ar, uint32_t e) {
+__device__ __forceinline__ uint32_t *sk_hbm(const KArgs &A, uint32_t e) {
     const uint32_t W = (uint32_t)((A.arenaElems + 63) >> 6);
-    return reinterpret_cast<uint32_t *>(const_cast<ElemOf<MAXLEN> *>(ar) + A.arenaElems) + (e & 63u) * W + (e >> 6);
+    return A.skArr + ((uint64_t)blockIdx.x * 64u + (e & 63u)) * W + (e >> 6);
 }
 template <int MAXLEN>
 __device__ __forceinline__ uint32_t sk_get(const KArgs &A, const Lds<MAXLEN> &S, const ElemOf<MAXLEN> *ar, uint32_t e) {
     if (e < SKCAP) return S.sk[e];
     if constexpr (Lds<MAXLEN>::BYTE_PATH) return ar[e].sortkey;
-    else return *sk_hbm<MAXLEN>(A, ar, e);
+    else return *sk_hbm<MAXLEN>(A, e);
 }
 template <int MAXLEN>
 __device__ __forceinline__ void sk_set(const KArgs &A, Lds<MAXLEN> &S, ElemOf<MAXLEN> *ar, uint32_t e, uint32_t v) {
     if (e < SKCAP) S.sk[e] = v;
     else if constexpr (Lds<MAXLEN>::BYTE_PATH) ar[e].sortkey = v;
-    else *sk_hbm<MAXLEN>(A, ar, e) = v;
+    else *sk_hbm<MAXLEN>(A, e) = v;
 }
 
 // recompute of `owner`'s selection maximum (elements e == owner mod 64), the whole wave

@@ -1484,6 +1484,10 @@ static int launch_passes(snapgpu_aligner_t *a, int li, const PassIO &io, const A
     A.bases = io.bases; A.quals = io.quals; A.offsets = io.offsets; A.lengths = io.lengths;
     A.nReads = (uint32_t)io.n; A.out = io.out;
     A.counter = L.counter; A.arena = L.arena; A.arenaElems = a->arenaElems;
+    // the arena is sized for a->grid Elem512 regions; the bit-plane kernels' Elem128 regions leave
+    // a tail of a->grid * arenaElems * 48 B, which holds their compact selection keys (sk_hbm)
+    A.skArr = reinterpret_cast<uint32_t *>(static_cast<char *>(L.arena) + (uint64_t)a->grid * a->arenaElems * sizeof(Elem128));
+    static_assert(sizeof(Elem512) - sizeof(Elem128) >= 8, "sk tail");
     A.deferList = io.defer; A.deferCount = L.counter + 2; A.readList = nullptr;
     A.search = x.search; A.maxHitsToGet = x.maxHitsToGet;
     A.hitSlot = x.maxHitsToGet < 512 ? x.maxHitsToGet : 512;

@@ -10,3 +10,7 @@ for v in base cur curnt; do
 done
 rm -f /dev/shm/snapgpu_ab_c3.bin
 cat gpurun_out/r03d/c3_ab.log
+# RNA leg (bench extras.rna_paired workload): stage times and the kernel trace of the current build
+export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/r03d/rna_kt -o run --output-format csv -- python3 tools/rna_probe.py > gpurun_out/r03d/rna_probe.txt 2> gpurun_out/r03d/rna_probe.err || { tail -5 gpurun_out/r03d/rna_probe.err; exit 1; }
+tail -3 gpurun_out/r03d/rna_probe.txt
