@@ -62,6 +62,21 @@ def algorithmic_bytes(res):
         P=P / n, H=H / n, V=V / n, S=S / n)
 
 
+def granule_bytes(res):
+    """SURVEY.md 8(d) d3, granule-adjusted: every random access moves whole 64-B lines -- the read's
+    bases and qualities, its record, one line per hash probe, per overflow list its count line plus
+    ceil(4 H / 64) hit lines, and per LV-scored candidate the genome window's lines
+    (64 * ceil((readLen + MAX_K) / 64), the byte genome of the reference's layout)."""
+    P = res["nProbes"].astype(np.int64)
+    H = res["nHitWords"].astype(np.int64)
+    V = res["nOverflowLists"].astype(np.int64)
+    S = res["nLocationsScored"].astype(np.int64)
+    line = 64
+    per_read = (2 * line * -(-READ_LEN // line) + line + line * P + line * (V + (4 * H + line - 1) // line) +
+                line * -(-(READ_LEN + MAX_K) // line) * S)
+    return int(per_read.sum())
+
+
 def lib_sha256():
     import snapgpu._ffi as F
     h = hashlib.sha256()
@@ -538,6 +553,10 @@ def main():
                                    "launches (HIP events); launch_duration_ms = mean of each launch's own "
                                    "interval (what rocprofv3 reports per dispatch; launches of the two "
                                    "streams overlap)",
+                    "granule_adjusted": {"bytes_per_read": granule_bytes(res) / len(res),
+                                         "achieved": granule_bytes(res) / n_launch / (kms_launch / 1000.0) / 1e9,
+                                         "frac": granule_bytes(res) / n_launch / (kms_launch / 1000.0) / 1e9 / HBM_PEAK_GBS,
+                                         "note": "64-B lines per random access (SURVEY 8(d) d3)"},
                     "launches_per_step": n_launch, "reads_per_launch": reads_launch,
                     "algorithmic_bytes_per_launch": bytes_launch, "algorithmic_bytes_per_read": bytes_all / len(res),
                     "binding_resource": "VALU issue (DESIGN.md section 4), not HBM bandwidth",
@@ -581,7 +600,12 @@ def main():
                       "achieved": lk_bytes / lk_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                       "frac": lk_bytes / lk_s / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": lk_bytes,
                       "seeds_per_launch": t["lookupSeeds"] / t["nLaunches"],
-                      "probes_per_launch": t["lookupProbes"] / t["nLaunches"]}
+                      "probes_per_launch": t["lookupProbes"] / t["nLaunches"],
+                      # the probes the align kernel makes itself (seeds past the first round, reads the
+                      # pass-0 records do not cover): the records' per-read total minus pass 0's
+                      "in_kernel_probes_per_read": float(res["nProbes"].astype(np.int64).sum() - t["lookupProbes"]) /
+                                                   len(res),
+                      "pass0_probes_per_read": t["lookupProbes"] / len(res)}
             # measured ceilings: random 12-B slot gathers from the resident table (>= 2^28 loads) and a
             # streaming copy (4 GiB read + 4 GiB written)
             n_g = 1 << 28

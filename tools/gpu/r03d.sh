@@ -1,10 +1,11 @@
 #!/bin/bash
 # round 3: PMC traffic of the variants on C2, then C3 A/B (index built once, shared) with record digests
 mkdir -p gpurun_out/r03d
-bash tools/gpu/pmcx.sh r03d cur base curnt || exit 1
+timeout -k 10 120 ./tools/gpu/valu_rates > gpurun_out/r03d/valu_rates.json 2>&1 || { cat gpurun_out/r03d/valu_rates.json; exit 1; }
+bash tools/gpu/pmcx.sh r03d cur base || exit 1
 timeout -k 10 300 python tools/ab_c3.py build > gpurun_out/r03d/c3_build.log 2>&1 || { tail -5 gpurun_out/r03d/c3_build.log; exit 1; }
 L=$PWD/snap-rnaseq_amd/snapgpu
-for v in base cur curnt; do
+for v in base cur; do
   if [ $v = cur ]; then lib=$L/libsnapgpu.so; else lib=$L/libsnapgpu_$v.so; fi
   SNAPGPU_LIB=$lib timeout -k 10 200 python tools/ab_c3.py run /dev/shm/snapgpu_ab_c3.bin 1000000 >> gpurun_out/r03d/c3_ab.log 2>&1 || { tail -5 gpurun_out/r03d/c3_ab.log; rm -f /dev/shm/snapgpu_ab_c3.bin; exit 1; }
 done

@@ -24,7 +24,7 @@ constexpr int PER_ITER = 16;   // instructions of the measured kind per loop ite
                      OP(6) OP(7)                                                                   \
                  : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7)  \
                  : "s"(sh)                                                                         \
-                 : "vcc", "v40")
+                 : "vcc", "v40", "s40", "s41")
 #define K64(OP)                                                                                   \
     asm volatile(OP(0) OP(1) OP(2) OP(3) OP(4) OP(5) OP(6) OP(7) OP(0) OP(1) OP(2) OP(3) OP(4) OP(5) \
                      OP(6) OP(7)                                                                   \
@@ -38,13 +38,17 @@ constexpr int PER_ITER = 16;   // instructions of the measured kind per loop ite
 #define OP_WSHR(i) "v_mov_b32_dpp %" #i ", %" #i " wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
 #define OP_MAX3(i) "v_max3_i32 %" #i ", %" #i ", %8, %" #i "\n"
 #define OP_CND(i) "v_cndmask_b32 %" #i ", %" #i ", v40, vcc\n"
+#define OP_CNDS(i) "v_cndmask_b32_e64 %" #i ", %" #i ", v40, s[40:41]\n"
+#define OP_CMPCND(i) "v_cmp_gt_u32_e64 s[40:41], %" #i ", v40\n v_cndmask_b32_e64 %" #i ", %" #i ", v40, s[40:41]\n"
 #define OP_SHL64(i) "v_lshlrev_b64 %" #i ", %8, %" #i "\n"
 #define OP_SHR64(i) "v_lshrrev_b64 %" #i ", %8, %" #i "\n"
 #define OP_ADD64(i) "v_lshl_add_u64 %" #i ", %" #i ", 0, %" #i "\n"
 
-enum Kind { ADD, FFBL, ALIGN, DPP_ROW, DPP_WAVE, MAX3, CNDMASK, SHL64, SHR64, ADD64, READLANE, NKIND };
+enum Kind { ADD, FFBL, ALIGN, DPP_ROW, DPP_WAVE, MAX3, CNDMASK, CNDMASK_S, CMP_CND, SHL64, SHR64, ADD64, READLANE,
+            NKIND };
 static const char *kName[NKIND] = {"v_add_u32", "v_ffbl_b32", "v_alignbit_b32", "v_mov_b32_dpp row_shr:1",
-                                   "v_mov_b32_dpp wave_shr:1", "v_max3_i32", "v_cndmask_b32",
+                                   "v_mov_b32_dpp wave_shr:1", "v_max3_i32", "v_cndmask_b32 (vcc)",
+                                   "v_cndmask_b32_e64 (SGPR-pair mask)", "v_cmp_gt_u32_e64 + v_cndmask_b32_e64 (pair)",
                                    "v_lshlrev_b64", "v_lshrrev_b64", "v_lshl_add_u64",
                                    "v_readlane_b32 (+ s_add_u32 on the result)"};
 
@@ -55,6 +59,7 @@ __global__ __launch_bounds__(1024) void rate_kernel(uint32_t seed, uint64_t *cyc
     uint64_t q0 = t, q1 = t + 1, q2 = t + 2, q3 = t + 3, q4 = t + 4, q5 = t + 5, q6 = t + 6, q7 = t + 7;
     uint32_t sh = (seed & 7) + 1;
     uint32_t sacc = 0;
+    asm volatile("v_mov_b32 v40, %0\n v_cmp_gt_u32_e32 vcc, 7, v40\n s_mov_b64 s[40:41], vcc" :: "v"(t) : "v40", "vcc", "s40", "s41");
     __syncthreads();
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
 #pragma unroll 1
@@ -66,6 +71,8 @@ __global__ __launch_bounds__(1024) void rate_kernel(uint32_t seed, uint64_t *cyc
         else if constexpr (KIND == DPP_WAVE) K32(OP_WSHR);
         else if constexpr (KIND == MAX3) K32(OP_MAX3);
         else if constexpr (KIND == CNDMASK) K32(OP_CND);
+        else if constexpr (KIND == CNDMASK_S) K32(OP_CNDS);
+        else if constexpr (KIND == CMP_CND) K32(OP_CMPCND);
         else if constexpr (KIND == SHL64) K64(OP_SHL64);
         else if constexpr (KIND == SHR64) K64(OP_SHR64);
         else if constexpr (KIND == ADD64) K64(OP_ADD64);
@@ -93,21 +100,25 @@ __global__ __launch_bounds__(1024) void rate_kernel(uint32_t seed, uint64_t *cyc
 
 template <int KIND>
 static int run(int ncu, int wps, double &cpi_wave, double &cpi_simd) {
-    const int waves = 4 * wps;   // one block per CU, wps waves on each of its 4 SIMDs
+    const int bpc = wps > 4 ? wps / 4 : 1;   // blocks per CU (<= 16 waves per block)
+    const int waves = 4 * wps / bpc;         // waves per block: wps waves on each of a CU's 4 SIMDs
     uint64_t *dc;
     uint32_t *ds;
-    CHK(hipMalloc(&dc, sizeof(uint64_t) * ncu * waves));
+    CHK(hipMalloc(&dc, sizeof(uint64_t) * ncu * bpc * waves));
     CHK(hipMalloc(&ds, 4));
-    hipLaunchKernelGGL(rate_kernel<KIND>, dim3(ncu), dim3(64 * waves), 0, 0, 1u, dc, ds);   // warm
+    hipLaunchKernelGGL(rate_kernel<KIND>, dim3(ncu * bpc), dim3(64 * waves), 0, 0, 1u, dc, ds);   // warm
+    CHK(hipGetLastError());
     CHK(hipDeviceSynchronize());
-    hipLaunchKernelGGL(rate_kernel<KIND>, dim3(ncu), dim3(64 * waves), 0, 0, 2u, dc, ds);
+    CHK(hipMemset(dc, 0, sizeof(uint64_t) * ncu * bpc * waves));
+    hipLaunchKernelGGL(rate_kernel<KIND>, dim3(ncu * bpc), dim3(64 * waves), 0, 0, 2u, dc, ds);
+    CHK(hipGetLastError());
     CHK(hipDeviceSynchronize());
-    std::vector<uint64_t> c(ncu * waves);
+    std::vector<uint64_t> c(ncu * bpc * waves);
     CHK(hipMemcpy(c.data(), dc, c.size() * 8, hipMemcpyDeviceToHost));
     double avg = 0;
     for (auto v : c) avg += (double)v;
     avg /= (double)c.size();
-    const double instr = (double)ITERS * (KIND == READLANE ? 16 : PER_ITER);
+    const double instr = (double)ITERS * (KIND == READLANE ? 16 : KIND == CMP_CND ? 2 * PER_ITER : PER_ITER);
     cpi_wave = avg / instr;
     cpi_simd = avg / (instr * wps);
     (void)hipFree(dc);
@@ -133,8 +144,8 @@ int main() {
     printf("{\"device_cus\": %d, \"iters\": %d, \"note\": \"shader cycles (s_memtime) per instruction; w = waves per "
            "SIMD; one instruction kind per stream, 8 independent registers\", \"rates\": [\n", ncu, ITERS);
     int rc = row<ADD>(ncu) | row<FFBL>(ncu) | row<ALIGN>(ncu) | row<DPP_ROW>(ncu) | row<DPP_WAVE>(ncu) |
-             row<MAX3>(ncu) | row<CNDMASK>(ncu) | row<SHL64>(ncu) | row<SHR64>(ncu) | row<ADD64>(ncu) |
-             row<READLANE>(ncu);
+             row<MAX3>(ncu) | row<CNDMASK>(ncu) | row<CNDMASK_S>(ncu) | row<CMP_CND>(ncu) | row<SHL64>(ncu) |
+             row<SHR64>(ncu) | row<ADD64>(ncu) | row<READLANE>(ncu);
     printf("]}\n");
     return rc;
 }
