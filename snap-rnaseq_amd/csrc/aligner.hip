@@ -1498,13 +1498,19 @@ static int launch_passes(snapgpu_aligner_t *a, int li, const PassIO &io, const A
     (void)hipGetLastError();   // clear any stale error of an unrelated earlier runtime call
     if (prev && !a->overlapKernels) HIPCHK(hipStreamWaitEvent(L.stream, prev->e[2], 0));
     HIPCHK(hipMemsetAsync(L.counter, 0, 64, L.stream));
-    // pass 0: first-round seed lookups of every read (8 reads per 64-lane block)
+    // pass 0: first-round seed lookups of every read (8 reads per 64-lane block); it also routes the
+    // reads -- pass 1's list (reads <= 128 bases) into the pass-2 output buffer, which pass 2 only
+    // writes after pass 1 has finished with it, and the longer reads straight onto pass 2's list
     A.seedRecs = nullptr;
+    A.shortList = io.defer2;
+    A.shortCount = L.counter + 5;
     HIPCHK(hipEventRecord(ev.e[3], L.stream));
     hipLaunchKernelGGL(seed_lookup_kernel, dim3((unsigned)((io.n + 7) / 8)), dim3(64), 0, L.stream, A, io.seeds,
                        L.lookupStats);
     HIPCHK(hipGetLastError());
     A.seedRecs = reinterpret_cast<const uint4 *>(io.seeds);
+    A.readList = io.defer2; A.readCount = L.counter + 5;
+    A.shortList = nullptr; A.shortCount = nullptr;
     HIPCHK(hipEventRecord(ev.e[0], L.stream));
     const bool ext = x.search || x.maxHitsToGet;
     if (ext) hipLaunchKernelGGL((align_kernel<128, true>), dim3(grid), dim3(64), 0, L.stream, A);
