@@ -86,7 +86,6 @@ template <int MAXLEN> using ElemOf = typename ElemSel<MAXLEN>::type;
 
 struct KArgs {
     uint32_t *diag;              // this aligner's watchdog record {code, read, detail, 0} (diag_report)
-    uint32_t *skArr;             // bit-plane kernels: selection keys of elements >= SKCAP (sk_hbm)
     // index (HBM)
     const uint32_t *slots;
     const uint64_t *tableBase;
@@ -734,29 +733,17 @@ __device__ __forceinline__ uint32_t chain_find(const KArgs &A, const Lds<MAXLEN>
     return e;
 }
 
-// selection keys: LDS for the first SKCAP elements of a read, HBM beyond.  The bit-plane kernels
-// keep the HBM keys in a compact per-wave array (KArgs::skArr: the tail of the lane's arena
-// allocation, which is sized for 144-B Elem512 while these kernels use 96-B Elem128), transposed by
-// owner lane -- key of element e at [(e % 64) * W + e / 64], W = ceil(arenaElems / 64) -- so the
-// keys of one owner lane (its elements e == owner mod 64) are contiguous: a selection recompute
-// reads them in one coalesced load, not one line per element.  The byte path keeps them in the
-// element (Elem512 fills the allocation).
+// selection keys: LDS for the first SKCAP elements of a read, HBM (the element) beyond.  (A compact
+// owner-transposed HBM key array -- one coalesced load per selection recompute -- measured 3% slower
+// on C2 and 5% on C3 in round 3: profiles/r03/ab/compact_sk_ab.txt.)
 template <int MAXLEN>
-__device__ __forceinline__ uint32_t *sk_hbm(const KArgs &A, uint32_t e) {
-    const uint32_t W = (uint32_t)((A.arenaElems + 63) >> 6);
-    return A.skArr + ((uint64_t)blockIdx.x * 64u + (e & 63u)) * W + (e >> 6);
+__device__ __forceinline__ uint32_t sk_get(const KArgs &, const Lds<MAXLEN> &S, const ElemOf<MAXLEN> *ar, uint32_t e) {
+    return e < SKCAP ? S.sk[e] : ar[e].sortkey;
 }
 template <int MAXLEN>
-__device__ __forceinline__ uint32_t sk_get(const KArgs &A, const Lds<MAXLEN> &S, const ElemOf<MAXLEN> *ar, uint32_t e) {
-    if (e < SKCAP) return S.sk[e];
-    if constexpr (Lds<MAXLEN>::BYTE_PATH) return ar[e].sortkey;
-    else return *sk_hbm<MAXLEN>(A, e);
-}
-template <int MAXLEN>
-__device__ __forceinline__ void sk_set(const KArgs &A, Lds<MAXLEN> &S, ElemOf<MAXLEN> *ar, uint32_t e, uint32_t v) {
+__device__ __forceinline__ void sk_set(const KArgs &, Lds<MAXLEN> &S, ElemOf<MAXLEN> *ar, uint32_t e, uint32_t v) {
     if (e < SKCAP) S.sk[e] = v;
-    else if constexpr (Lds<MAXLEN>::BYTE_PATH) ar[e].sortkey = v;
-    else *sk_hbm<MAXLEN>(A, e) = v;
+    else ar[e].sortkey = v;
 }
 
 // recompute of `owner`'s selection maximum (elements e == owner mod 64), the whole wave

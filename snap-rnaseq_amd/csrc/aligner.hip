@@ -657,12 +657,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MAXLEN <= 25
     ElemOf<MAXLEN> *ar = reinterpret_cast<ElemOf<MAXLEN> *>(A.arena) + (uint64_t)blockIdx.x * A.arenaElems;
     const int lane = lane_id();
     const uint32_t total = A.readList ? uni(*A.readCount) : A.nReads;
+    // a read is listed at most once per pass, so a list as long as the batch holds every read: take
+    // them in input order without the list load (pass 1 of an all-short batch -- the bench's case --
+    // or pass 2 of an all-long one)
+    const uint32_t *list = A.readList && total != A.nReads ? A.readList : nullptr;
     for (;;) {
         uint32_t i = 0;
         if (lane == 0) i = atomicAdd(A.counter, 1u);
         i = uni((uint32_t)readlane((int)i, 0));
         if (i >= total) break;
-        const uint32_t r = A.readList ? uni(A.readList[i]) : i;
+        const uint32_t r = list ? uni(list[i]) : i;
         if (__hip_atomic_load(&A.diag[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;   // watchdog: drain
         if (r == A.tripRead && lane == 0) diag_report(A.diag, DIAG_TEST_TRIP, r, 0);   // test hook
         align_one<MAXLEN, EXT>(A, S, ar, r);
@@ -1484,10 +1488,6 @@ static int launch_passes(snapgpu_aligner_t *a, int li, const PassIO &io, const A
     A.bases = io.bases; A.quals = io.quals; A.offsets = io.offsets; A.lengths = io.lengths;
     A.nReads = (uint32_t)io.n; A.out = io.out;
     A.counter = L.counter; A.arena = L.arena; A.arenaElems = a->arenaElems;
-    // the arena is sized for a->grid Elem512 regions; the bit-plane kernels' Elem128 regions leave
-    // a tail of a->grid * arenaElems * 48 B, which holds their compact selection keys (sk_hbm)
-    A.skArr = reinterpret_cast<uint32_t *>(static_cast<char *>(L.arena) + (uint64_t)a->grid * a->arenaElems * sizeof(Elem128));
-    static_assert(sizeof(Elem512) - sizeof(Elem128) >= 8, "sk tail");
     A.deferList = io.defer; A.deferCount = L.counter + 2; A.readList = nullptr;
     A.search = x.search; A.maxHitsToGet = x.maxHitsToGet;
     A.hitSlot = x.maxHitsToGet < 512 ? x.maxHitsToGet : 512;

@@ -38,16 +38,21 @@ constexpr int PER_ITER = 16;   // instructions of the measured kind per loop ite
 #define OP_WSHR(i) "v_mov_b32_dpp %" #i ", %" #i " wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
 #define OP_MAX3(i) "v_max3_i32 %" #i ", %" #i ", %8, %" #i "\n"
 #define OP_CND(i) "v_cndmask_b32 %" #i ", %" #i ", v40, vcc\n"
+#define OP_CNDV64(i) "v_cndmask_b32_e64 %" #i ", %" #i ", v40, vcc\n"
+#define OP_MIX(i) "v_add_u32 %" #i ", %" #i ", %8\n v_add_u32 %" #i ", %" #i ", %8\n v_add_u32 %" #i ", %" #i ", %8\n v_cndmask_b32 %" #i ", %" #i ", v40, vcc\n"
+#define OP_CMPV(i) "v_cmp_gt_u32_e32 vcc, %" #i ", v40\n v_cndmask_b32 %" #i ", %" #i ", v40, vcc\n"
 #define OP_CNDS(i) "v_cndmask_b32_e64 %" #i ", %" #i ", v40, s[40:41]\n"
 #define OP_CMPCND(i) "v_cmp_gt_u32_e64 s[40:41], %" #i ", v40\n v_cndmask_b32_e64 %" #i ", %" #i ", v40, s[40:41]\n"
 #define OP_SHL64(i) "v_lshlrev_b64 %" #i ", %8, %" #i "\n"
 #define OP_SHR64(i) "v_lshrrev_b64 %" #i ", %8, %" #i "\n"
 #define OP_ADD64(i) "v_lshl_add_u64 %" #i ", %" #i ", 0, %" #i "\n"
 
-enum Kind { ADD, FFBL, ALIGN, DPP_ROW, DPP_WAVE, MAX3, CNDMASK, CNDMASK_S, CMP_CND, SHL64, SHR64, ADD64, READLANE,
-            NKIND };
+enum Kind { ADD, FFBL, ALIGN, DPP_ROW, DPP_WAVE, MAX3, CNDMASK, CNDMASK_V64, MIX_CND, CMP_V, CNDMASK_S, CMP_CND, SHL64,
+            SHR64, ADD64, READLANE, NKIND };
 static const char *kName[NKIND] = {"v_add_u32", "v_ffbl_b32", "v_alignbit_b32", "v_mov_b32_dpp row_shr:1",
                                    "v_mov_b32_dpp wave_shr:1", "v_max3_i32", "v_cndmask_b32 (vcc)",
+                                   "v_cndmask_b32_e64 (vcc operand)", "3 x v_add_u32 + v_cndmask_b32 (vcc)",
+                                   "v_cmp_gt_u32_e32 vcc + v_cndmask_b32 (vcc)",
                                    "v_cndmask_b32_e64 (SGPR-pair mask)", "v_cmp_gt_u32_e64 + v_cndmask_b32_e64 (pair)",
                                    "v_lshlrev_b64", "v_lshrrev_b64", "v_lshl_add_u64",
                                    "v_readlane_b32 (+ s_add_u32 on the result)"};
@@ -71,6 +76,9 @@ __global__ __launch_bounds__(1024) void rate_kernel(uint32_t seed, uint64_t *cyc
         else if constexpr (KIND == DPP_WAVE) K32(OP_WSHR);
         else if constexpr (KIND == MAX3) K32(OP_MAX3);
         else if constexpr (KIND == CNDMASK) K32(OP_CND);
+        else if constexpr (KIND == CNDMASK_V64) K32(OP_CNDV64);
+        else if constexpr (KIND == MIX_CND) K32(OP_MIX);
+        else if constexpr (KIND == CMP_V) K32(OP_CMPV);
         else if constexpr (KIND == CNDMASK_S) K32(OP_CNDS);
         else if constexpr (KIND == CMP_CND) K32(OP_CMPCND);
         else if constexpr (KIND == SHL64) K64(OP_SHL64);
@@ -118,7 +126,8 @@ static int run(int ncu, int wps, double &cpi_wave, double &cpi_simd) {
     double avg = 0;
     for (auto v : c) avg += (double)v;
     avg /= (double)c.size();
-    const double instr = (double)ITERS * (KIND == READLANE ? 16 : KIND == CMP_CND ? 2 * PER_ITER : PER_ITER);
+    const double instr = (double)ITERS * (KIND == READLANE ? 16 : (KIND == CMP_CND || KIND == CMP_V) ? 2 * PER_ITER :
+                                          KIND == MIX_CND ? 4 * PER_ITER : PER_ITER);
     cpi_wave = avg / instr;
     cpi_simd = avg / (instr * wps);
     (void)hipFree(dc);
@@ -144,7 +153,7 @@ int main() {
     printf("{\"device_cus\": %d, \"iters\": %d, \"note\": \"shader cycles (s_memtime) per instruction; w = waves per "
            "SIMD; one instruction kind per stream, 8 independent registers\", \"rates\": [\n", ncu, ITERS);
     int rc = row<ADD>(ncu) | row<FFBL>(ncu) | row<ALIGN>(ncu) | row<DPP_ROW>(ncu) | row<DPP_WAVE>(ncu) |
-             row<MAX3>(ncu) | row<CNDMASK>(ncu) | row<CNDMASK_S>(ncu) | row<CMP_CND>(ncu) | row<SHL64>(ncu) |
+             row<MAX3>(ncu) | row<CNDMASK>(ncu) | row<CNDMASK_V64>(ncu) | row<MIX_CND>(ncu) | row<CMP_V>(ncu) | row<CNDMASK_S>(ncu) | row<CMP_CND>(ncu) | row<SHL64>(ncu) |
              row<SHR64>(ncu) | row<ADD64>(ncu) | row<READLANE>(ncu);
     printf("]}\n");
     return rc;

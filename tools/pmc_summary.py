@@ -106,6 +106,21 @@ def main(src, dst):
                                                                 "SQ_ACTIVE_INST_LDS") if x in c}
         if "SQ_THREAD_CYCLES_VALU" in c and "SQ_ACTIVE_INST_VALU" in c and c["SQ_ACTIVE_INST_VALU"]:
             e["valu_lane_utilisation"] = c["SQ_THREAD_CYCLES_VALU"] / (64.0 * c["SQ_ACTIVE_INST_VALU"])
+    # seed_lookup_kernel on serialised streams (prof.sh serial_kt / serial_pmc): rocprof's average
+    # dispatch duration is the kernel's own, FETCH_SIZE (KiB) per dispatch over it is its HBM rate
+    sk = os.path.join(src, "serial_kt", "run_kernel_stats.csv")
+    sp = os.path.join(src, "serial_pmc", "run_counter_collection.csv")
+    if os.path.exists(sk) and os.path.exists(sp):
+        dur = {kname(r["Name"]): float(r["AverageNs"]) / 1e9 for r in csv.DictReader(open(sk)) if kname(r["Name"])}
+        fc = per_dispatch(sp)
+        if "lookup" in dur and "lookup" in fc and "FETCH_SIZE" in fc["lookup"]:
+            fb = fc["lookup"]["FETCH_SIZE"] * 1024
+            shutil.copy(sk, os.path.join(dst, "kernel_stats_serial.csv"))
+            out["kernels"]["lookup"]["serialised"] = {
+                "avg_dispatch_ms": dur["lookup"] * 1e3, "fetch_bytes_per_dispatch_raw": fb,
+                "fetch_GBps": fb / dur["lookup"] / 1e9, "frac_of_8TBps": fb / dur["lookup"] / 1e9 / 8000.0,
+                "note": "SNAPGPU_OVERLAP=0: no align kernel shares the GPU with the lookup dispatches; FETCH_SIZE "
+                        "uncorrected (MI355X_MICROARCH.md calibrates it for 16-B streaming reads only)"}
     a = out["kernels"].get("align", {})
     if "counters_per_dispatch" in a:
         c = a["counters_per_dispatch"]
