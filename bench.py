@@ -308,7 +308,11 @@ def rna_leg(args, idx, local, build_threads):
         parity = rna_parity(args, pa, ta, gtf, r0, r1, work)
         return {"parity": parity, "value": 2 * n / dt, "unit": "reads/s", "pairs_per_s": n / dt, "pairs": n, "ms_per_batch": dt * 1e3,
                 "read_len": 150, "workload": info, "transcriptome_bases": tidx.info()["nBases"],
-                "stage_ms": {x: round(st[x], 2) for x in ("alignMs", "filterMs", "seedMs", "cigarMs", "writeMs")},
+                "stage_ms": {x: round(st[x], 2) for x in ("prepMs", "alignMs", "filterMs", "seedMs", "countMs", "cigarMs",
+                                                          "writeMs", "wallMs")},
+                "sub_batches": st["subBatches"],
+                "stage_note": "stage times are sums over the pipelined sub-batches (stage A: the GPU aligners of "
+                              "sub-batch s+1 overlaps stage B: filter, seed census, CIGARs, records of s)",
                 "records": {x: st[x] for x in ("singleHits", "multiHits", "notFound", "transcriptomeRecords")},
                 "partial_pairs": st["partialPairs"], "partial_matches": st["partialMatches"],
                 "seed_runs": st["seedRuns"], "prep_s": round(t_prep, 1),

@@ -669,13 +669,16 @@ typedef struct snapgpu_rna_paired_stats {
     double alignMs, filterMs, seedMs, cigarMs, writeMs, wallMs;
     double prepMs;     /* clipping, ID check, pre-filter, batch views (before alignMs) */
     double countMs;    /* spacing / MAPQ adjustments and the GTF read counts (after seedMs) */
+    uint64_t subBatches;   /* pipelined sub-batches (SNAPGPU_RNA_SUBBATCH pairs each, default 16384): the
+                              stage times above are sums over them and overlap one another in wallMs */
 } snapgpu_rna_paired_stats_t;
 
 /* pairedAligner: the genome aligner (snapgpu_paired_aligner_create with the paired CLI defaults);
  * transcriptomeAligner: a BaseAligner over the transcriptome index (maxHits 16000, maxK 15,
  * 8 seeds); reads0 / reads1 FASTQ batches with ids, clipped here.  samPath (or NULL) receives the
- * header and two lines per pair in input order; out (or NULL) one record per pair; the gtf's
- * read counters are advanced. */
+ * header and two lines per pair in input order (BAM records when it ends in ".bam"); out (or NULL)
+ * one record per pair; the gtf's read counters are advanced (all of the batch's count events, or
+ * none when one names an unknown transcript or gene). */
 int snapgpu_rna_paired_align(snapgpu_paired_aligner_t *pairedAligner, snapgpu_aligner_t *transcriptomeAligner,
                              snapgpu_gtf_t *gtf, snapgpu_reads_t *reads0, snapgpu_reads_t *reads1,
                              const snapgpu_rna_paired_options_t *opt, const char *samPath,

@@ -121,13 +121,13 @@ struct KArgs {
     // 256 bases and the IUPAC ones to align_kernel<512>
     uint32_t *deferList;         // passes 1 and 2 append the read indices they defer here
     uint32_t *deferCount;        //   (atomic append count)
-    const uint32_t *readList;    // read indices: pass 1 (pass 0's routing), passes 2 and 3 (the previous pass's defers)
+    const uint32_t *readList;    // passes 2 and 3: read indices (the previous passes' defers; nullptr in pass 1)
     const uint32_t *readCount;   //   and their number (the previous pass's deferCount)
     const uint4 *seedRecs;       // seed_lookup_kernel records (SeedRec, 8 per read), or nullptr
-    // pass 0 routes every read: <= 128 bases to shortList (pass 1's read list), longer ones straight
-    // to deferList (pass 2's), with one atomic per 8 reads instead of pass 1 deferring them one by one
-    uint32_t *shortList;
-    uint32_t *shortCount;
+    // pass 0 puts the reads longer than 128 bases straight onto deferList (pass 2's list) with one
+    // atomic per 8-read wave that holds any, and counts them in longCount; pass 1 (longCount set)
+    // then skips them instead of deferring them one by one, and ends at once when every read is long
+    uint32_t *longCount;
     unsigned long long *phaseBuf;   // diagnostic (SNAPGPU_PHASES=1): per-block [PH_SLOTS] cycle sums, else null
     // windowed search + multi-hit export (snapgpu_align_batch_ex; BaseAligner.h:73-86)
     const snapgpu_search_t *search;     // per read, or nullptr (= unconstrained)

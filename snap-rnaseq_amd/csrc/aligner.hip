@@ -359,7 +359,10 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
     const uint32_t numWeightLists = maxSeeds + 1;
     bool run = true;
     if constexpr (!Lds<MAXLEN>::BYTE_PATH) {   // bit-plane kernels: longer reads go on to the next pass
-        if (n > (uint32_t)MAXLEN) { defer_read(A, r); return; }
+        if (n > (uint32_t)MAXLEN) {
+            if (!(MAXLEN == 128 && A.longCount)) defer_read(A, r);   // (pass 0 has listed them already)
+            return;
+        }
     }
     // search window (BaseAligner.cpp:596-602); multiHitsFound = 0 up front (:586-590)
     uint32_t radius = 0, sDir = 0, minLoc = 0, maxLoc = INVALID;
@@ -656,10 +659,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MAXLEN <= 25
     __shared__ Lds<MAXLEN> S;
     ElemOf<MAXLEN> *ar = reinterpret_cast<ElemOf<MAXLEN> *>(A.arena) + (uint64_t)blockIdx.x * A.arenaElems;
     const int lane = lane_id();
-    const uint32_t total = A.readList ? uni(*A.readCount) : A.nReads;
+    uint32_t total = A.readList ? uni(*A.readCount) : A.nReads;
+    // pass 1 after pass 0's routing: nothing to do when every read is long
+    if (!A.readList && A.longCount && uni(*A.longCount) == A.nReads) total = 0;
     // a read is listed at most once per pass, so a list as long as the batch holds every read: take
-    // them in input order without the list load (pass 1 of an all-short batch -- the bench's case --
-    // or pass 2 of an all-long one)
+    // them in input order without the list load (pass 2 of an all-long batch)
     const uint32_t *list = A.readList && total != A.nReads ? A.readList : nullptr;
     for (;;) {
         uint32_t i = 0;
@@ -1498,19 +1502,15 @@ static int launch_passes(snapgpu_aligner_t *a, int li, const PassIO &io, const A
     (void)hipGetLastError();   // clear any stale error of an unrelated earlier runtime call
     if (prev && !a->overlapKernels) HIPCHK(hipStreamWaitEvent(L.stream, prev->e[2], 0));
     HIPCHK(hipMemsetAsync(L.counter, 0, 64, L.stream));
-    // pass 0: first-round seed lookups of every read (8 reads per 64-lane block); it also routes the
-    // reads -- pass 1's list (reads <= 128 bases) into the pass-2 output buffer, which pass 2 only
-    // writes after pass 1 has finished with it, and the longer reads straight onto pass 2's list
+    // pass 0: first-round seed lookups of every read (8 reads per 64-lane block); it also puts the
+    // reads longer than 128 bases straight onto pass 2's list
     A.seedRecs = nullptr;
-    A.shortList = io.defer2;
-    A.shortCount = L.counter + 5;
+    A.longCount = L.counter + 5;
     HIPCHK(hipEventRecord(ev.e[3], L.stream));
     hipLaunchKernelGGL(seed_lookup_kernel, dim3((unsigned)((io.n + 7) / 8)), dim3(64), 0, L.stream, A, io.seeds,
                        L.lookupStats);
     HIPCHK(hipGetLastError());
     A.seedRecs = reinterpret_cast<const uint4 *>(io.seeds);
-    A.readList = io.defer2; A.readCount = L.counter + 5;
-    A.shortList = nullptr; A.shortCount = nullptr;
     HIPCHK(hipEventRecord(ev.e[0], L.stream));
     const bool ext = x.search || x.maxHitsToGet;
     if (ext) hipLaunchKernelGGL((align_kernel<128, true>), dim3(grid), dim3(64), 0, L.stream, A);

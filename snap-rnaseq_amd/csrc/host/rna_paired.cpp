@@ -20,8 +20,10 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <condition_variable>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -319,6 +321,394 @@ bool idsMatch(const char *a, uint32_t la, const char *b, uint32_t lb) {   // rea
     return true;
 }
 
+
+// One snapgpu_rna_paired_align call: what its sub-batches share.
+struct RnaRun {
+    snapgpu_paired_aligner_t *pa;
+    snapgpu_aligner_t *ta, *ga;
+    const snapgpu_index_t *gi, *ti;
+    snapgpu_gtf_t *gtf;
+    snapgpu_reads_t *R[2];
+    const snapgpu_rna_paired_options_t *opt;
+    const std::vector<uint8_t> *useful;
+    std::mutex *mT, *mG;   // the transcriptome / genome aligner's lock
+    const Ctx *C;
+    bool bam;
+};
+
+// Pairs [a, b) of the batch through the path; stage A fills the aligner outputs, stage B the rest.
+struct RnaSub {
+    uint64_t a = 0, b = 0;
+    std::vector<uint64_t> ui;                 // the useful pairs (batch indices)
+    snapgpu_reads_t *U[2] = {nullptr, nullptr};
+    std::vector<uint64_t> uo[2];
+    std::vector<uint32_t> ul[2];
+    std::vector<snapgpu_result_t> tr[2];
+    std::vector<int32_t> tf[2];
+    std::vector<uint64_t> thOff[2];           // useful pair j's hits: th[k][thOff[k][j] .. thOff[k][j + 1])
+    std::vector<snapgpu_multi_hit_t> th[2];
+    std::vector<snapgpu_pair_result_t> gr;
+    std::vector<FilterState> fs;              // per useful pair
+    std::vector<GtfPairQuery> cq;             // count events (pointing into fs), input order
+    std::vector<PairOut> po;                  // per pair of [a, b)
+    std::string part;                         // the SAM lines / BAM records of [a, b)
+    uint64_t single = 0, multi = 0, notFound = 0, partialPairs = 0, partialMatches = 0, seedRuns = 0;
+    uint64_t transcriptomeRecords = 0;
+    double alignMs = 0, filterMs = 0, seedMs = 0, countMs = 0, cigarMs = 0, writeMs = 0;
+    int rc = SNAPGPU_OK;
+    std::string err;
+    RnaSub() = default;
+    RnaSub(const RnaSub &) = delete;
+    ~RnaSub() { snapgpu_reads_free(U[0]); snapgpu_reads_free(U[1]); }
+    void fail(int code, const std::string &m) { if (rc == SNAPGPU_OK) { rc = code; err = m; } }
+};
+
+// Stage A: the useful pairs' batch views, the transcriptome AlignRead of both ends with 1000
+// multi-hits (PairedAligner.cpp:601-605) and, on a thread of its own, the genome
+// ChimericPairedEndAligner (:625) -- the two aligners have their own streams and device buffers.
+void rnaStageA(const RnaRun &Rr, RnaSub &X) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t i = X.a; i < X.b; i++) if ((*Rr.useful)[i]) X.ui.push_back(i);
+    const uint64_t nu = X.ui.size();
+    for (int k = 0; k < 2; k++) {
+        X.uo[k].resize(nu + 1); X.ul[k].resize(nu + 1);
+        for (uint64_t j = 0; j < nu; j++) { X.uo[k][j] = Rr.R[k]->offsets[X.ui[j]]; X.ul[k][j] = Rr.R[k]->lengths[X.ui[j]]; }
+        X.U[k] = snapgpu_reads_from_arrays(nu, Rr.R[k]->bases, Rr.R[k]->quals, X.uo[k].data(), X.ul[k].data());
+        if (!X.U[k]) { X.fail(SNAPGPU_ENOMEM, "rna_paired_align: out of memory"); return; }
+    }
+    X.gr.resize(nu + 1);
+    if (nu) {
+        int grc = SNAPGPU_OK;
+        std::string gerr;
+        auto genomePairs = [&] {
+            std::lock_guard<std::mutex> lk(*Rr.mG);
+            grc = snapgpu_paired_align_batch(Rr.pa, X.U[0], X.U[1], X.gr.data());
+            if (grc) gerr = snapgpu_last_error();
+        };
+        const bool overlap = Rr.ta != Rr.ga;
+        std::thread gt;
+        if (overlap) gt = std::thread(genomePairs);
+        int rc = SNAPGPU_OK;
+        std::string terr;
+        {
+            std::lock_guard<std::mutex> lk(*Rr.mT);
+            for (int k = 0; k < 2 && rc == SNAPGPU_OK; k++) {
+                X.tr[k].resize(nu); X.tf[k].resize(nu);
+                rc = snapgpu_internal_align_batch_packed(Rr.ta, X.U[k], nullptr, Rr.opt->maxHitsToGet, X.tr[k].data(),
+                                                         X.tf[k].data(), X.thOff[k], X.th[k]);
+            }
+            if (rc) terr = snapgpu_last_error();
+        }
+        if (overlap) gt.join();
+        else if (rc == SNAPGPU_OK) genomePairs();
+        if (rc) { X.fail(rc, terr); return; }
+        if (grc) { X.fail(grc, gerr); return; }
+    }
+    X.alignMs = msSince(t0);
+}
+
+// Stage B: AlignmentFilter (AddAlignment + Filter, AlignmentFilter.cpp:113-739) on host threads,
+// FindPartialMatches' seed census as one GPU batch, the spacing / MAPQ adjustments and the count
+// events (PairedAligner.cpp:648-663), the CIGARs of both ends as GPU batches (genome; transcriptome
+// + insertSpliceJunctions) and the records of writePair (ReadWriter.cpp:133-217).  lastNm: the BAM
+// NM carry-over from the previous sub-batch (the reference's writeRead leaves an unmapped record
+// with the previous record's editDistance).
+void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
+    const Ctx &C = *Rr.C;
+    const snapgpu_rna_paired_options_t *opt = Rr.opt;
+    snapgpu_reads_t *const *R = Rr.R;
+    const uint64_t nu = X.ui.size(), nb = X.b - X.a;
+    auto t0 = std::chrono::steady_clock::now();
+    X.fs.assign(nu + 1, FilterState());
+    std::vector<Err> errs(16);
+    parallel(nu, [&](unsigned t, uint64_t b, uint64_t e) {
+        AlignmentMap mate0, mate1;
+        for (uint64_t j = b; j < e && errs[t].msg.empty(); j++) {
+            mate0.clear(); mate1.clear();
+            const uint32_t len0 = X.ul[0][j], len1 = X.ul[1][j];
+            for (int k = 0; k < 2; k++)
+                for (uint64_t h = X.thOff[k][j]; h < X.thOff[k][j + 1]; h++) {
+                    const snapgpu_multi_hit_t &m = X.th[k][h];
+                    addAlignment(C, mate0, mate1, m.location, m.direction, m.score, 0, true, k == 1, len0, len1, errs[t]);
+                }
+            const snapgpu_pair_result_t &g = X.gr[j];
+            addAlignment(C, mate0, mate1, g.location[0], g.direction[0], g.score[0], g.mapq[0], false, false, len0, len1, errs[t]);
+            addAlignment(C, mate0, mate1, g.location[1], g.direction[1], g.score[1], g.mapq[1], false, true, len0, len1, errs[t]);
+            FilterState &S = X.fs[j];
+            S.r.fromAlignTogether = g.fromAlignTogether;
+            S.r.alignedAsPair = g.alignedAsPair;
+            filterPair(C, mate0, mate1, len0, len1, S, errs[t]);
+        }
+    });
+    for (auto &e : errs) if (!e.msg.empty()) { X.fail(SNAPGPU_EFORMAT, "rna_paired_align: " + e.msg); return; }
+    X.filterMs = msSince(t0);
+    // FindPartialMatches: CharacterizeSeeds of both reads of the pairs that need it, one GPU batch
+    t0 = std::chrono::steady_clock::now();
+    std::vector<uint64_t> need;
+    for (uint64_t j = 0; j < nu; j++) if (X.fs[j].needPartial) need.push_back(j);
+    X.partialPairs = need.size();
+    if (!need.empty()) {
+        // both reads in one batch: read0 of need[i] at 2i, read1 at 2i + 1
+        std::vector<uint64_t> po(2 * need.size() + 1);
+        std::vector<uint32_t> pl(2 * need.size() + 1);
+        std::string bb, qq;
+        for (size_t i = 0; i < need.size(); i++)
+            for (int k = 0; k < 2; k++) {
+                const uint64_t o = X.uo[k][need[i]];
+                po[2 * i + k] = bb.size();
+                pl[2 * i + k] = X.ul[k][need[i]];
+                bb.append(R[k]->bases + o, X.ul[k][need[i]]);
+                qq.append(R[k]->quals + o, X.ul[k][need[i]]);
+            }
+        snapgpu_reads_t *both = snapgpu_reads_from_arrays(2 * need.size(), bb.data(), qq.data(), po.data(), pl.data());
+        if (!both) { X.fail(SNAPGPU_ENOMEM, "rna_paired_align: out of memory"); return; }
+        snapgpu_charseeds_params_t cp;
+        snapgpu_charseeds_params_default(&cp);   // the partial aligner: maxHits 300, 12 seeds (:518-527)
+        cp.maxK = opt->maxDist;
+        snapgpu_seed_runs_t *runs;
+        {
+            std::lock_guard<std::mutex> lk(*Rr.mG);
+            runs = snapgpu_characterize_seeds(Rr.ga, both, nullptr, 0, &cp);
+            if (!runs) X.fail(SNAPGPU_EDEVICE, snapgpu_last_error());
+        }
+        snapgpu_reads_free(both);
+        if (!runs) return;
+        std::unique_ptr<snapgpu_seed_runs_t, void (*)(snapgpu_seed_runs_t *)> hold(runs, snapgpu_seed_runs_free);
+        for (uint64_t i = 0; i < 2 * need.size(); i++)
+            if (runs->flags[i] & SNAPGPU_FLAG_READ_TOO_LONG) {
+                X.fail(SNAPGPU_EINVAL, "rna_paired_align: read longer than maxReadSize (the reference exits, BaseAligner.cpp:272-275)");
+                return;
+            }
+        X.seedRuns = runs->nRuns;
+        std::vector<uint8_t> hit(need.size(), 0);
+        parallel(need.size(), [&](unsigned t, uint64_t b, uint64_t e) {
+            for (uint64_t i = b; i < e; i++)
+                hit[i] = partialMatch(C, runs, 2 * i, 2 * i + 1, X.ul[0][need[i]], X.ul[1][need[i]], errs[t]);
+        });
+        for (auto &e : errs) if (!e.msg.empty()) { X.fail(SNAPGPU_EFORMAT, "rna_paired_align: " + e.msg); return; }
+        for (size_t i = 0; i < need.size(); i++)
+            if (hit[i]) {
+                PairOut &r = X.fs[need[i]].r;
+                r.status[0] = r.status[1] = SNAPGPU_MULTIPLE_HITS;
+                r.mapq[0] = r.mapq[1] = 1;
+                X.partialMatches++;
+            }
+    }
+    X.seedMs = msSince(t0);
+    t0 = std::chrono::steady_clock::now();
+    // spacing and MAPQ adjustments (PairedAligner.cpp:648-663); the count events in input order
+    // (applied for the whole batch at the end: gtfCountPairs)
+    for (uint64_t j = 0; j < nu; j++) {
+        PairOut &r = X.fs[j].r;
+        if (opt->forceSpacing && (r.status[0] == SNAPGPU_SINGLE_HIT) != (r.status[1] == SNAPGPU_SINGLE_HIT)) {
+            r.status[0] = r.status[1] = SNAPGPU_NOT_FOUND;
+            r.location[0] = r.location[1] = kInvalidLocation;
+        }
+        if (r.score[0] + r.score[1] >= 5)
+            for (int k = 0; k < 2; k++) if (r.mapq[k] < 50) r.mapq[k] /= 2;
+        const FilterState &S = X.fs[j];
+        if (S.countPair) X.cq.push_back(GtfPairQuery{&S.tid0, S.tstart0, S.start0, S.len0, &S.tid1, S.tstart1, S.start1, S.len1});
+    }
+    // the pairs' records, in input order; filtered pairs: NotFound, InvalidGenomeLocation
+    X.po.assign(nb, PairOut());
+    for (uint64_t j = 0; j < nu; j++) X.po[X.ui[j] - X.a] = X.fs[j].r;
+    X.countMs = msSince(t0);
+    // CIGARs on the GPU (writeRead, SAM.cpp:1040-1066): genome records at the location, the
+    // transcriptome records on the transcriptome at tlocation.  Only the records with a location
+    // go to the GPU, as compact batches (a read without one has no CIGAR: edit distance -1, no
+    // ops); the genome (ga) and transcriptome (ta) batches run on two host threads.
+    t0 = std::chrono::steady_clock::now();
+    struct CigarSet {
+        std::vector<int64_t> slot;   // record -> row in ed/nOps/ops, -1: no location
+        std::vector<uint64_t> off;
+        std::vector<uint32_t> len, loc, nOps, ops;
+        std::vector<uint8_t> dir;
+        std::vector<int32_t> ed;
+        int32_t edOf(uint64_t i) const { return slot[i] >= 0 ? ed[slot[i]] : -1; }
+        uint32_t nOpsOf(uint64_t i) const { return slot[i] >= 0 ? nOps[slot[i]] : 0u; }
+        const uint32_t *opsOf(uint64_t i) const {
+            static const uint32_t kNone[1] = {0};
+            return slot[i] >= 0 ? ops.data() + slot[i] * SNAPGPU_CIGAR_MAX_OPS : kNone;
+        }
+        void add(uint64_t i, uint64_t o, uint32_t ln, uint32_t l, uint8_t d) {
+            slot[i] = (int64_t)loc.size();
+            off.push_back(o);
+            len.push_back(ln);
+            loc.push_back(l);
+            dir.push_back(d);
+        }
+        int run(snapgpu_aligner_t *a, const snapgpu_reads_t *r, int useM, std::mutex &m) {
+            const uint64_t cnt = loc.size();
+            ed.assign(cnt + 1, -1);
+            nOps.assign(cnt + 1, 0);
+            ops.resize((cnt + 1) * SNAPGPU_CIGAR_MAX_OPS);
+            if (!cnt) return SNAPGPU_OK;
+            snapgpu_reads_t *v = snapgpu_reads_from_arrays(cnt, r->bases, r->quals, off.data(), len.data());
+            if (!v) return SNAPGPU_ENOMEM;
+            std::lock_guard<std::mutex> lk(m);
+            const int rc = snapgpu_cigar_batch(a, v, loc.data(), dir.data(), useM, ed.data(), nOps.data(), ops.data());
+            snapgpu_reads_free(v);
+            return rc;
+        }
+    };
+    CigarSet gc[2], tc[2];
+    std::vector<uint8_t> isT[2];
+    for (int k = 0; k < 2; k++) {
+        isT[k].assign(nb, 0);
+        gc[k].slot.assign(nb, -1);
+        tc[k].slot.assign(nb, -1);
+        for (uint64_t q = 0; q < nb; q++) {
+            const PairOut &r = X.po[q];
+            const uint64_t i = X.a + q;
+            const uint32_t loc = r.status[k] != SNAPGPU_NOT_FOUND ? r.location[k] : kInvalidLocation;
+            const bool t = loc != kInvalidLocation && r.isTranscriptome[k];
+            isT[k][q] = t;
+            if (t) tc[k].add(q, R[k]->offsets[i], R[k]->lengths[i], r.tlocation[k], (uint8_t)r.direction[k]);
+            else if (loc != kInvalidLocation) gc[k].add(q, R[k]->offsets[i], R[k]->lengths[i], loc, (uint8_t)r.direction[k]);
+        }
+        X.transcriptomeRecords += tc[k].loc.size();
+    }
+    {
+        int grc = SNAPGPU_OK, rc = SNAPGPU_OK;
+        std::string gerr, terr;
+        auto genomeCigars = [&] {
+            for (int k = 0; k < 2 && grc == SNAPGPU_OK; k++) grc = gc[k].run(Rr.ga, R[k], (int)opt->useM, *Rr.mG);
+            if (grc) gerr = snapgpu_last_error();
+        };
+        // one aligner's stream, events and upload state serve one host thread at a time: the two
+        // CIGAR loops overlap only when the transcriptome and genome aligners are distinct
+        const bool overlap = Rr.ta != Rr.ga;
+        std::thread gt;
+        if (overlap) gt = std::thread(genomeCigars);
+        for (int k = 0; k < 2 && rc == SNAPGPU_OK; k++) rc = tc[k].run(Rr.ta, R[k], (int)opt->useM, *Rr.mT);
+        if (rc) terr = snapgpu_last_error();
+        if (overlap) gt.join();
+        else if (rc == SNAPGPU_OK) genomeCigars();
+        if (rc) { X.fail(rc, terr); return; }
+        if (grc) { X.fail(grc, gerr); return; }
+    }
+    // transcriptome records: computeCigarString's tokens through insertSpliceJunctions
+    const Genome &tg = *Rr.ti->genome;
+    std::vector<std::string> splice[2];
+    for (int k = 0; k < 2; k++) {
+        splice[k].assign(nb, std::string());
+        parallel(nb, [&](unsigned, uint64_t b, uint64_t e) {
+            std::vector<std::pair<uint32_t, char>> tk;
+            static const char kOp[] = "MIDNSHP=X";
+            for (uint64_t q = b; q < e; q++) {
+                if (!isT[k][q]) continue;
+                tk.clear();
+                const PairOut &r = X.po[q];
+                const uint64_t i = X.a + q;
+                if (tc[k].edOf(q) >= 0) {
+                    const uint32_t full = R[k]->unclippedLength[i], front = R[k]->frontClipped[i];
+                    const uint32_t back = full - R[k]->lengths[i] - front;
+                    const bool rcd = r.direction[k] == SNAPGPU_RC;
+                    const uint32_t before = rcd ? back : front, after = rcd ? front : back;
+                    if (before) tk.push_back({before, 'S'});
+                    const uint32_t *tops = tc[k].opsOf(q);
+                    for (uint32_t z = 0; z < tc[k].nOpsOf(q); z++) {
+                        const uint32_t op = tops[z];
+                        tk.push_back({op >> 4, kOp[op & 15]});
+                    }
+                    if (after) tk.push_back({after, 'S'});
+                }
+                const int p = pieceAt(tg, r.tlocation[k]);
+                const GtfTranscript *t = p >= 0 ? gtfTranscript(Rr.gtf, tg.pieceNames[p]) : nullptr;
+                if (t) gtfSpliceCigar(t, r.tlocation[k] - tg.pieceOffsets[p] + 1, tk, splice[k][q]);
+            }
+        });
+    }
+    X.cigarMs = msSince(t0);
+    // writePair (ReadWriter.cpp:133-217): the end at the lower location first
+    t0 = std::chrono::steady_clock::now();
+    const unsigned ntd = nb < 2048 ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::string> parts(ntd);
+    std::vector<uint64_t> cnt(3 * ntd, 0);
+    // BAM: NM is set only for a record with a location; the others repeat the previous record's
+    // value, so a serial pass in write order fixes each record's NM
+    std::vector<int32_t> bamNm;
+    std::vector<uint8_t> bamBad(ntd, 0);
+    if (Rr.bam) {
+        bamNm.resize(2 * nb);
+        for (uint64_t q = 0; q < nb; q++) {
+            const PairOut &r = X.po[q];
+            uint32_t locs[2];
+            for (int k = 0; k < 2; k++) locs[k] = r.status[k] != SNAPGPU_NOT_FOUND ? r.location[k] : kInvalidLocation;
+            const int first = locs[0] > locs[1];
+            for (int w = 0; w < 2; w++) {
+                const int k = w == 0 ? first : 1 - first;
+                if (locs[k] != kInvalidLocation) lastNm = isT[k][q] ? tc[k].edOf(q) : gc[k].edOf(q);
+                bamNm[2 * q + w] = lastNm;
+            }
+        }
+    }
+    const Genome &gg = *Rr.gi->genome;
+    parallel(nb, [&](unsigned t, uint64_t b, uint64_t e) {
+        std::string &o = parts[t];
+        o.reserve((e - b) * 640);
+        for (uint64_t q = b; q < e; q++) {
+            const PairOut &r = X.po[q];
+            const uint64_t i = X.a + q;
+            uint32_t idLen[2] = {R[0]->idLengths[i], R[1]->idLengths[i]};
+            const char *id[2] = {R[0]->ids + R[0]->idOffsets[i], R[1]->ids + R[1]->idOffsets[i]};
+            if (idLen[0] == idLen[1] && idLen[0] > 2 && id[0][idLen[0] - 2] == '/' && id[1][idLen[0] - 2] == '/') {
+                const char c0 = id[0][idLen[0] - 1], c1 = id[1][idLen[1] - 1];
+                if ((c0 == '1' || c0 == '2') && (c0 == '1' || c1 == '2') && c0 != c1) { idLen[0] -= 2; idLen[1] -= 2; }
+            }
+            uint32_t locs[2];
+            for (int k = 0; k < 2; k++) locs[k] = r.status[k] != SNAPGPU_NOT_FOUND ? r.location[k] : kInvalidLocation;
+            const int first = locs[0] > locs[1], second = 1 - first;
+            for (int w = 0; w < 2; w++) {
+                const int k = w == 0 ? first : second, m = 1 - k;
+                SamLine L;
+                L.id = id[k];
+                L.idLen = R[k]->idLengths[i];
+                L.qnameLen = idLen[k];
+                L.front = R[k]->frontClipped[i];
+                L.clippedLen = R[k]->lengths[i];
+                L.fullLen = R[k]->unclippedLength[i];
+                L.bases = R[k]->bases + R[k]->offsets[i] - L.front;
+                L.quals = R[k]->quals + R[k]->offsets[i] - L.front;
+                L.rg = opt->readGroup;
+                L.result = r.status[k];
+                L.loc = locs[k];
+                L.dir = r.direction[k];
+                L.mapq = r.mapq[k];
+                if (isT[k][q]) {
+                    L.cigar = &splice[k][q];
+                    L.ed = tc[k].edOf(q);
+                } else {
+                    L.ed = gc[k].edOf(q);
+                    L.ops = gc[k].opsOf(q);
+                    L.nOps = gc[k].nOpsOf(q);
+                }
+                L.hasMate = true;
+                L.firstInPair = w == 0;
+                L.mateLoc = locs[m];
+                L.mateDir = r.direction[m];
+                L.mateFront = R[m]->frontClipped[i];
+                L.mateClippedLen = R[m]->lengths[i];
+                L.mateFullLen = R[m]->unclippedLength[i];
+                if (!Rr.bam) samAppendLine(o, gg, L);
+                else if (!bamAppendRecord(o, gg, L, bamNm[2 * q + w])) bamBad[t] = 1;
+                cnt[3 * t + (r.status[k] == SNAPGPU_SINGLE_HIT ? 0 : r.status[k] == SNAPGPU_MULTIPLE_HITS ? 1 : 2)]++;
+            }
+        }
+    });
+    for (unsigned t = 0; t < ntd; t++)
+        if (bamBad[t]) {
+            X.fail(SNAPGPU_EINVAL, "rna_paired_align: BAM record not written (QNAME longer than 254 characters, Bam.cpp:723-726)");
+            return;
+        }
+    for (unsigned t = 0; t < ntd; t++) { X.single += cnt[3 * t]; X.multi += cnt[3 * t + 1]; X.notFound += cnt[3 * t + 2]; }
+    size_t tot = 0;
+    for (auto &p : parts) tot += p.size();
+    X.part.reserve(tot);
+    for (auto &p : parts) X.part += p;
+    X.writeMs = msSince(t0);
+}
+
 }  // namespace
 
 extern "C" {
@@ -358,13 +748,19 @@ int snapgpu_rna_paired_align(snapgpu_paired_aligner_t *pa, snapgpu_aligner_t *ta
         const int rc = snapgpu_reads_clip(R[k], opt->clipping, nullptr, nullptr);   // FASTQReader (FASTQ.cpp:250)
         if (rc) return rc;
     }
-    if (!opt->ignoreMismatchedIDs)   // Read::checkIdMatch (Read.cpp:37-49): the reference exits
-        for (uint64_t i = 0; i < n; i++)
-            if (!idsMatch(reads0->ids + reads0->idOffsets[i], reads0->idLengths[i], reads1->ids + reads1->idOffsets[i],
-                          reads1->idLengths[i])) {
-                setError("rna_paired_align: unmatched read IDs at pair " + std::to_string(i) + " (ignoreMismatchedIDs)");
-                return SNAPGPU_EINVAL;
-            }
+    if (!opt->ignoreMismatchedIDs) {   // Read::checkIdMatch (Read.cpp:37-49): the reference exits
+        std::vector<uint64_t> bad(16, n);   // first mismatching pair of each thread's range
+        parallel(n, [&](unsigned t, uint64_t b, uint64_t e) {
+            for (uint64_t i = b; i < e; i++)
+                if (!idsMatch(reads0->ids + reads0->idOffsets[i], reads0->idLengths[i],
+                              reads1->ids + reads1->idOffsets[i], reads1->idLengths[i])) { bad[t] = i; break; }
+        });
+        const uint64_t i = *std::min_element(bad.begin(), bad.end());
+        if (i < n) {
+            setError("rna_paired_align: unmatched read IDs at pair " + std::to_string(i) + " (ignoreMismatchedIDs)");
+            return SNAPGPU_EINVAL;
+        }
+    }
     // pre-filter (PairedAligner.cpp:555-575): length / Ns per read, quality of read0 (sic, :564)
     std::vector<uint8_t> useful(n, 0);
     parallel(n, [&](unsigned, uint64_t b, uint64_t e) {
@@ -384,394 +780,139 @@ int snapgpu_rna_paired_align(snapgpu_paired_aligner_t *pa, snapgpu_aligner_t *ta
             useful[i] = !((!u[0] && !u[1]) || !q[0]);
         }
     });
-    std::vector<uint64_t> ui;
-    for (uint64_t i = 0; i < n; i++) if (useful[i]) ui.push_back(i);
-    const uint64_t nu = ui.size();
-    st.usefulPairs = nu;
-    // the useful pairs as batches (views of the clipped reads)
-    snapgpu_reads_t *U[2] = {nullptr, nullptr};
-    std::vector<uint64_t> uo[2];
-    std::vector<uint32_t> ul[2];
-    for (int k = 0; k < 2; k++) {
-        uo[k].resize(nu + 1); ul[k].resize(nu + 1);
-        for (uint64_t j = 0; j < nu; j++) { uo[k][j] = R[k]->offsets[ui[j]]; ul[k][j] = R[k]->lengths[ui[j]]; }
-        U[k] = snapgpu_reads_from_arrays(nu, R[k]->bases, R[k]->quals, uo[k].data(), ul[k].data());
-        if (!U[k]) { snapgpu_reads_free(U[0]); return SNAPGPU_ENOMEM; }
-    }
-    snapgpu_seed_runs_t *runs = nullptr;
-    auto fail = [&](int code) {
-        snapgpu_reads_free(U[0]); snapgpu_reads_free(U[1]);
-        snapgpu_seed_runs_free(runs);
-        return code;
-    };
-    int rc = SNAPGPU_OK;
-    const uint32_t mh = opt->maxHitsToGet;
-    std::vector<snapgpu_result_t> tr[2];
-    std::vector<int32_t> tf[2];
-    std::vector<uint64_t> thOff[2];              // read j's hits: th[k][thOff[k][j] .. thOff[k][j + 1])
-    std::vector<snapgpu_multi_hit_t> th[2];
-    std::vector<snapgpu_pair_result_t> gr(nu + 1);
+    for (uint64_t i = 0; i < n; i++) st.usefulPairs += useful[i];
     st.prepMs = msSince(w0);
-    auto t0 = std::chrono::steady_clock::now();
-    if (nu) {
-        // g_aligner->align(read0, read1, &result) (:625) on a thread of its own, concurrently with
-        // the transcriptome batches: the two aligners have their own streams and device buffers
-        // (results are per aligner, so the order of the calls does not matter)
-        int grc = SNAPGPU_OK;
-        std::string gerr;
-        auto genomePairs = [&] {
-            grc = snapgpu_paired_align_batch(pa, U[0], U[1], gr.data());
-            if (grc) gerr = snapgpu_last_error();
-        };
-        const bool overlap = ta != ga;
-        std::thread gt;
-        if (overlap) gt = std::thread(genomePairs);
-        // transcriptomeAligner->AlignRead(read0 / read1, ..., maxHitsToGet 1000, multiHits) (:601-605)
-        for (int k = 0; k < 2 && rc == SNAPGPU_OK; k++) {
-            tr[k].resize(nu); tf[k].resize(nu);
-            rc = snapgpu_internal_align_batch_packed(ta, U[k], nullptr, mh, tr[k].data(), tf[k].data(), thOff[k], th[k]);
-        }
-        if (overlap) gt.join();
-        else if (rc == SNAPGPU_OK) genomePairs();
-        if (rc) return fail(rc);
-        if (grc) { setError(gerr); return fail(grc); }
-    }
-    st.alignMs = msSince(t0);
-    // AddAlignment + Filter up to FindPartialMatches, on host threads
-    t0 = std::chrono::steady_clock::now();
     Ctx C{gi->genome, ti->genome, gtf, {}, opt};
     for (size_t p = 0; p < gi->genome->pieceNames.size(); p++) C.pieceByName.insert({gi->genome->pieceNames[p], gi->genome->pieceOffsets[p]});
-    std::vector<FilterState> fs(nu + 1);
-    std::vector<Err> errs(16);
-    parallel(nu, [&](unsigned t, uint64_t b, uint64_t e) {
-        AlignmentMap mate0, mate1;
-        for (uint64_t j = b; j < e && errs[t].msg.empty(); j++) {
-            mate0.clear(); mate1.clear();
-            const uint32_t len0 = ul[0][j], len1 = ul[1][j];
-            for (int k = 0; k < 2; k++)
-                for (uint64_t h = thOff[k][j]; h < thOff[k][j + 1]; h++) {
-                    const snapgpu_multi_hit_t &m = th[k][h];
-                    addAlignment(C, mate0, mate1, m.location, m.direction, m.score, 0, true, k == 1, len0, len1, errs[t]);
-                }
-            const snapgpu_pair_result_t &g = gr[j];
-            addAlignment(C, mate0, mate1, g.location[0], g.direction[0], g.score[0], g.mapq[0], false, false, len0, len1, errs[t]);
-            addAlignment(C, mate0, mate1, g.location[1], g.direction[1], g.score[1], g.mapq[1], false, true, len0, len1, errs[t]);
-            FilterState &S = fs[j];
-            S.r.fromAlignTogether = g.fromAlignTogether;
-            S.r.alignedAsPair = g.alignedAsPair;
-            filterPair(C, mate0, mate1, len0, len1, S, errs[t]);
-        }
-    });
-    for (auto &e : errs) if (!e.msg.empty()) { setError("rna_paired_align: " + e.msg); return fail(SNAPGPU_EFORMAT); }
-    st.filterMs = msSince(t0);
-    // FindPartialMatches: CharacterizeSeeds of both reads of the pairs that need it, one GPU batch
-    t0 = std::chrono::steady_clock::now();
-    std::vector<uint64_t> need;
-    for (uint64_t j = 0; j < nu; j++) if (fs[j].needPartial) need.push_back(j);
-    st.partialPairs = need.size();
-    if (!need.empty()) {
-        // both reads in one batch: read0 of need[i] at 2i, read1 at 2i + 1
-        std::vector<uint64_t> po(2 * need.size() + 1);
-        std::vector<uint32_t> pl(2 * need.size() + 1);
-        std::string bb, qq;
-        for (size_t i = 0; i < need.size(); i++)
-            for (int k = 0; k < 2; k++) {
-                const uint64_t o = uo[k][need[i]];
-                po[2 * i + k] = bb.size();
-                pl[2 * i + k] = ul[k][need[i]];
-                bb.append(R[k]->bases + o, ul[k][need[i]]);
-                qq.append(R[k]->quals + o, ul[k][need[i]]);
-            }
-        snapgpu_reads_t *both = snapgpu_reads_from_arrays(2 * need.size(), bb.data(), qq.data(), po.data(), pl.data());
-        if (!both) return fail(SNAPGPU_ENOMEM);
-        snapgpu_charseeds_params_t cp;
-        snapgpu_charseeds_params_default(&cp);   // the partial aligner: maxHits 300, 12 seeds (:518-527)
-        cp.maxK = opt->maxDist;
-        runs = snapgpu_characterize_seeds(ga, both, nullptr, 0, &cp);
-        snapgpu_reads_free(both);
-        if (!runs) return fail(SNAPGPU_EDEVICE);
-        for (uint64_t i = 0; i < 2 * need.size(); i++)
-            if (runs->flags[i] & SNAPGPU_FLAG_READ_TOO_LONG) {
-                setError("rna_paired_align: read longer than maxReadSize (the reference exits, BaseAligner.cpp:272-275)");
-                return fail(SNAPGPU_EINVAL);
-            }
-        st.seedRuns = runs->nRuns;
-        std::vector<uint8_t> hit(need.size(), 0);
-        parallel(need.size(), [&](unsigned t, uint64_t b, uint64_t e) {
-            for (uint64_t i = b; i < e; i++)
-                hit[i] = partialMatch(C, runs, 2 * i, 2 * i + 1, ul[0][need[i]], ul[1][need[i]], errs[t]);
-        });
-        for (auto &e : errs) if (!e.msg.empty()) { setError("rna_paired_align: " + e.msg); return fail(SNAPGPU_EFORMAT); }
-        for (size_t i = 0; i < need.size(); i++)
-            if (hit[i]) {
-                PairOut &r = fs[need[i]].r;
-                r.status[0] = r.status[1] = SNAPGPU_MULTIPLE_HITS;
-                r.mapq[0] = r.mapq[1] = 1;
-                st.partialMatches++;
-            }
-    }
-    st.seedMs = msSince(t0);
-    t0 = std::chrono::steady_clock::now();
-    // spacing and MAPQ adjustments (PairedAligner.cpp:648-663); read counts in input order
-    // (interval queries on host threads, counter updates in pair order: gtfCountPairs)
-    std::vector<GtfPairQuery> cq;
-    for (uint64_t j = 0; j < nu; j++) {
-        PairOut &r = fs[j].r;
-        if (opt->forceSpacing && (r.status[0] == SNAPGPU_SINGLE_HIT) != (r.status[1] == SNAPGPU_SINGLE_HIT)) {
-            r.status[0] = r.status[1] = SNAPGPU_NOT_FOUND;
-            r.location[0] = r.location[1] = kInvalidLocation;
-        }
-        if (r.score[0] + r.score[1] >= 5)
-            for (int k = 0; k < 2; k++) if (r.mapq[k] < 50) r.mapq[k] /= 2;
-        const FilterState &S = fs[j];
-        if (S.countPair) cq.push_back(GtfPairQuery{&S.tid0, S.tstart0, S.start0, S.len0, &S.tid1, S.tstart1, S.start1, S.len1});
-    }
-    if (gtfCountPairs(gtf, cq) >= 0) {
-        setError("rna_paired_align: read count for an unknown transcript or gene");
-        return fail(SNAPGPU_EFORMAT);
-    }
-    // the pairs' records, in input order; filtered pairs: NotFound, InvalidGenomeLocation
-    std::vector<PairOut> po(n);
-    {
-        std::vector<int64_t> uidx(n, -1);
-        for (uint64_t j = 0; j < nu; j++) uidx[ui[j]] = (int64_t)j;
-        for (uint64_t i = 0; i < n; i++) if (uidx[i] >= 0) po[i] = fs[uidx[i]].r;
-    }
-    st.countMs = msSince(t0);
-    // CIGARs on the GPU (writeRead, SAM.cpp:1040-1066): genome records at the location, the
-    // transcriptome records on the transcriptome at tlocation
-    t0 = std::chrono::steady_clock::now();
-    // Only the records with a location go to the GPU, as compact batches (a read without one has
-    // no CIGAR: edit distance -1, no ops); the genome (ga) and transcriptome (ta) batches run
-    // on two host threads.
-    struct CigarSet {
-        std::vector<int64_t> slot;   // record -> row in ed/nOps/ops, -1: no location
-        std::vector<uint64_t> off;
-        std::vector<uint32_t> len, loc, nOps, ops;
-        std::vector<uint8_t> dir;
-        std::vector<int32_t> ed;
-        int32_t edOf(uint64_t i) const { return slot[i] >= 0 ? ed[slot[i]] : -1; }
-        uint32_t nOpsOf(uint64_t i) const { return slot[i] >= 0 ? nOps[slot[i]] : 0u; }
-        const uint32_t *opsOf(uint64_t i) const {
-            static const uint32_t kNone[1] = {0};
-            return slot[i] >= 0 ? ops.data() + slot[i] * SNAPGPU_CIGAR_MAX_OPS : kNone;
-        }
-        void add(uint64_t i, const snapgpu_reads_t *r, uint32_t l, uint8_t d) {
-            slot[i] = (int64_t)loc.size();
-            off.push_back(r->offsets[i]);
-            len.push_back(r->lengths[i]);
-            loc.push_back(l);
-            dir.push_back(d);
-        }
-        int run(snapgpu_aligner_t *a, const snapgpu_reads_t *r, int useM) {
-            const uint64_t m = loc.size();
-            ed.assign(m + 1, -1);
-            nOps.assign(m + 1, 0);
-            ops.resize((m + 1) * SNAPGPU_CIGAR_MAX_OPS);
-            if (!m) return SNAPGPU_OK;
-            snapgpu_reads_t *v = snapgpu_reads_from_arrays(m, r->bases, r->quals, off.data(), len.data());
-            if (!v) return SNAPGPU_ENOMEM;
-            const int rc = snapgpu_cigar_batch(a, v, loc.data(), dir.data(), useM, ed.data(), nOps.data(), ops.data());
-            snapgpu_reads_free(v);
-            return rc;
-        }
-    };
-    CigarSet gc[2], tc[2];
-    std::vector<uint8_t> isT[2];
-    for (int k = 0; k < 2; k++) {
-        isT[k].assign(n, 0);
-        gc[k].slot.assign(n, -1);
-        tc[k].slot.assign(n, -1);
-        for (uint64_t i = 0; i < n; i++) {
-            const PairOut &r = po[i];
-            const uint32_t loc = r.status[k] != SNAPGPU_NOT_FOUND ? r.location[k] : kInvalidLocation;
-            const bool t = loc != kInvalidLocation && r.isTranscriptome[k];
-            isT[k][i] = t;
-            if (t) tc[k].add(i, R[k], r.tlocation[k], (uint8_t)r.direction[k]);
-            else if (loc != kInvalidLocation) gc[k].add(i, R[k], loc, (uint8_t)r.direction[k]);
-        }
-        st.transcriptomeRecords += tc[k].loc.size();
-    }
-    {
-        int grc = SNAPGPU_OK;
-        std::string gerr;
-        auto genomeCigars = [&] {
-            for (int k = 0; k < 2 && grc == SNAPGPU_OK; k++) grc = gc[k].run(ga, R[k], (int)opt->useM);
-            if (grc) gerr = snapgpu_last_error();
-        };
-        // one aligner's stream, events and upload state serve one host thread at a time: the two
-        // CIGAR loops overlap only when the transcriptome and genome aligners are distinct
-        const bool overlap = ta != ga;
-        std::thread gt;
-        if (overlap) gt = std::thread(genomeCigars);
-        for (int k = 0; k < 2 && rc == SNAPGPU_OK; k++) rc = tc[k].run(ta, R[k], (int)opt->useM);
-        if (overlap) gt.join();
-        else if (rc == SNAPGPU_OK) genomeCigars();
-        if (rc) return fail(rc);
-        if (grc) { setError(gerr); return fail(grc); }
-    }
-    // transcriptome records: computeCigarString's tokens through insertSpliceJunctions
-    std::vector<std::string> splice[2];
-    for (int k = 0; k < 2; k++) {
-        splice[k].assign(n, std::string());
-        parallel(n, [&](unsigned, uint64_t b, uint64_t e) {
-            std::vector<std::pair<uint32_t, char>> tk;
-            static const char kOp[] = "MIDNSHP=X";
-            for (uint64_t i = b; i < e; i++) {
-                if (!isT[k][i]) continue;
-                tk.clear();
-                const PairOut &r = po[i];
-                if (tc[k].edOf(i) >= 0) {
-                    const uint32_t full = R[k]->unclippedLength[i], front = R[k]->frontClipped[i];
-                    const uint32_t back = full - R[k]->lengths[i] - front;
-                    const bool rcd = r.direction[k] == SNAPGPU_RC;
-                    const uint32_t before = rcd ? back : front, after = rcd ? front : back;
-                    if (before) tk.push_back({before, 'S'});
-                    const uint32_t *tops = tc[k].opsOf(i);
-                    for (uint32_t q = 0; q < tc[k].nOpsOf(i); q++) {
-                        const uint32_t op = tops[q];
-                        tk.push_back({op >> 4, kOp[op & 15]});
-                    }
-                    if (after) tk.push_back({after, 'S'});
-                }
-                const Genome &tg = *ti->genome;
-                const int p = pieceAt(tg, r.tlocation[k]);
-                const GtfTranscript *t = p >= 0 ? gtfTranscript(gtf, tg.pieceNames[p]) : nullptr;
-                if (t) gtfSpliceCigar(t, r.tlocation[k] - tg.pieceOffsets[p] + 1, tk, splice[k][i]);
-            }
-        });
-    }
-    st.cigarMs = msSince(t0);
-    // writePair (ReadWriter.cpp:133-217): the end at the lower location first
-    t0 = std::chrono::steady_clock::now();
-    const unsigned ntd = n < 2048 ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    std::vector<std::string> parts(ntd);
-    std::vector<uint64_t> cnt(3 * ntd, 0);
-    // BAM when the path ends in ".bam" (BAMFormat::writeRead for both ends, Bam.cpp:596-790).  Its NM
-    // is set only for a record with a location; the others repeat the previous record's value, so a
-    // serial pass in write order (per pair: the end at the lower location first) fixes each NM.
     const size_t spl = samPath ? strlen(samPath) : 0;
+    // BAM when the path ends in ".bam" (BAMFormat::writeRead for both ends, Bam.cpp:596-790)
     const bool bam = spl >= 4 && strcmp(samPath + spl - 4, ".bam") == 0;
-    std::vector<int32_t> bamNm;
-    std::vector<uint8_t> bamBad(ntd, 0);
-    if (bam) {
-        bamNm.resize(2 * n);
-        int32_t last = 0;   // before any mapped record the reference writes its stack's leftover
-        for (uint64_t i = 0; i < n; i++) {
-            const PairOut &r = po[i];
-            uint32_t locs[2];
-            for (int k = 0; k < 2; k++) locs[k] = r.status[k] != SNAPGPU_NOT_FOUND ? r.location[k] : kInvalidLocation;
-            const int first = locs[0] > locs[1];
-            for (int w = 0; w < 2; w++) {
-                const int k = w == 0 ? first : 1 - first;
-                if (locs[k] != kInvalidLocation) last = isT[k][i] ? tc[k].edOf(i) : gc[k].edOf(i);
-                bamNm[2 * i + w] = last;
-            }
-        }
+    // One aligner serves one host thread at a time: the stage-A align calls and the stage-B
+    // seed-census / CIGAR calls of the next sub-batch take the aligner's lock (ga also runs the
+    // paired aligner's single-end fallback).
+    std::mutex mG, mTown;
+    std::mutex &mT = ta == ga ? mG : mTown;
+    RnaRun Rr{pa, ta, ga, gi, ti, gtf, {R[0], R[1]}, opt, &useful, &mT, &mG, &C, bam};
+    // Sub-batches of the pairs, pipelined: stage A (the GPU aligners) of sub-batch s + 1 runs while
+    // stage B (filter, seed census, counts, CIGARs, records) of sub-batch s runs on another thread.
+    // Every stage keeps the reference's per-pair semantics; records and count events are kept in
+    // input order across sub-batches.
+    uint64_t per = 16384;
+    if (const char *e = getenv("SNAPGPU_RNA_SUBBATCH"); e && atoll(e) > 0) per = (uint64_t)atoll(e);
+    const uint64_t S = n ? (n + per - 1) / per : 0;
+    std::vector<std::unique_ptr<RnaSub>> subs(S);
+    for (uint64_t k = 0; k < S; k++) {
+        subs[k].reset(new RnaSub);
+        subs[k]->a = k * per;
+        subs[k]->b = std::min(n, (k + 1) * per);
     }
-    parallel(n, [&](unsigned t, uint64_t b, uint64_t e) {
-        std::string &o = parts[t];
-        o.reserve((e - b) * 640);
-        for (uint64_t i = b; i < e; i++) {
-            const PairOut &r = po[i];
-            uint32_t idLen[2] = {R[0]->idLengths[i], R[1]->idLengths[i]};
-            const char *id[2] = {R[0]->ids + R[0]->idOffsets[i], R[1]->ids + R[1]->idOffsets[i]};
-            if (idLen[0] == idLen[1] && idLen[0] > 2 && id[0][idLen[0] - 2] == '/' && id[1][idLen[0] - 2] == '/') {
-                const char c0 = id[0][idLen[0] - 1], c1 = id[1][idLen[1] - 1];
-                if ((c0 == '1' || c0 == '2') && (c0 == '1' || c1 == '2') && c0 != c1) { idLen[0] -= 2; idLen[1] -= 2; }
+    std::mutex qm;
+    std::condition_variable cv;
+    uint64_t aDone = 0;
+    bool stop = false;
+    int32_t lastNm = 0;   // BAM NM carry-over, in write order across sub-batches
+    std::thread stageB([&] {
+        for (uint64_t k = 0; k < S; k++) {
+            {
+                std::unique_lock<std::mutex> lk(qm);
+                cv.wait(lk, [&] { return aDone > k || stop; });
+                if (stop && aDone <= k) return;
             }
-            uint32_t locs[2];
-            for (int k = 0; k < 2; k++) locs[k] = r.status[k] != SNAPGPU_NOT_FOUND ? r.location[k] : kInvalidLocation;
-            const int first = locs[0] > locs[1], second = 1 - first;
-            for (int w = 0; w < 2; w++) {
-                const int k = w == 0 ? first : second, m = 1 - k;
-                SamLine L;
-                L.id = id[k];
-                L.idLen = R[k]->idLengths[i];
-                L.qnameLen = idLen[k];
-                L.front = R[k]->frontClipped[i];
-                L.clippedLen = R[k]->lengths[i];
-                L.fullLen = R[k]->unclippedLength[i];
-                L.bases = R[k]->bases + R[k]->offsets[i] - L.front;
-                L.quals = R[k]->quals + R[k]->offsets[i] - L.front;
-                L.rg = opt->readGroup;
-                L.result = r.status[k];
-                L.loc = locs[k];
-                L.dir = r.direction[k];
-                L.mapq = r.mapq[k];
-                if (isT[k][i]) {
-                    L.cigar = &splice[k][i];
-                    L.ed = tc[k].edOf(i);
-                } else {
-                    L.ed = gc[k].edOf(i);
-                    L.ops = gc[k].opsOf(i);
-                    L.nOps = gc[k].nOpsOf(i);
-                }
-                L.hasMate = true;
-                L.firstInPair = w == 0;
-                L.mateLoc = locs[m];
-                L.mateDir = r.direction[m];
-                L.mateFront = R[m]->frontClipped[i];
-                L.mateClippedLen = R[m]->lengths[i];
-                L.mateFullLen = R[m]->unclippedLength[i];
-                if (!bam) samAppendLine(o, *gi->genome, L);
-                else if (!bamAppendRecord(o, *gi->genome, L, bamNm[2 * i + w])) bamBad[t] = 1;
-                cnt[3 * t + (r.status[k] == SNAPGPU_SINGLE_HIT ? 0 : r.status[k] == SNAPGPU_MULTIPLE_HITS ? 1 : 2)]++;
+            RnaSub &X = *subs[k];
+            if (X.rc == SNAPGPU_OK) rnaStageB(Rr, X, lastNm);
+            if (X.rc != SNAPGPU_OK) {
+                std::lock_guard<std::mutex> lk(qm);
+                stop = true;
+                cv.notify_all();
+                return;
             }
         }
     });
-    for (unsigned t = 0; t < ntd; t++)
-        if (bamBad[t]) {
-            setError("rna_paired_align: BAM record not written (QNAME longer than 254 characters, Bam.cpp:723-726)");
-            return fail(SNAPGPU_EINVAL);
+    for (uint64_t k = 0; k < S; k++) {
+        {
+            std::lock_guard<std::mutex> lk(qm);
+            if (stop) break;
         }
-    for (unsigned t = 0; t < ntd; t++) { st.singleHits += cnt[3 * t]; st.multiHits += cnt[3 * t + 1]; st.notFound += cnt[3 * t + 2]; }
+        rnaStageA(Rr, *subs[k]);
+        std::lock_guard<std::mutex> lk(qm);
+        aDone = k + 1;
+        if (subs[k]->rc != SNAPGPU_OK) stop = true;
+        cv.notify_all();
+    }
+    stageB.join();
+    for (auto &x : subs)
+        if (x->rc != SNAPGPU_OK) {
+            setError(x->err);
+            return x->rc;
+        }
+    // GTFReader::IncrementReadCount for every counted pair, in input order, all or nothing
+    {
+        const auto t1 = std::chrono::steady_clock::now();
+        std::vector<GtfPairQuery> cq;
+        for (auto &x : subs) cq.insert(cq.end(), x->cq.begin(), x->cq.end());
+        if (gtfCountPairs(gtf, cq) >= 0) {
+            setError("rna_paired_align: read count for an unknown transcript or gene");
+            return SNAPGPU_EFORMAT;
+        }
+        st.countMs += msSince(t1);
+    }
+    for (auto &x : subs) {
+        st.singleHits += x->single; st.multiHits += x->multi; st.notFound += x->notFound;
+        st.partialPairs += x->partialPairs; st.partialMatches += x->partialMatches; st.seedRuns += x->seedRuns;
+        st.transcriptomeRecords += x->transcriptomeRecords;
+        st.alignMs += x->alignMs; st.filterMs += x->filterMs; st.seedMs += x->seedMs; st.countMs += x->countMs;
+        st.cigarMs += x->cigarMs; st.writeMs += x->writeMs;
+    }
     if (samPath) {
+        const auto t1 = std::chrono::steady_clock::now();
         FILE *f = fopen(samPath, "w");
-        if (!f) { setError(std::string("cannot write ") + samPath); return fail(SNAPGPU_EIO); }
+        if (!f) { setError(std::string("cannot write ") + samPath); return SNAPGPU_EIO; }
         uint64_t hlen = 0;
         snapgpu_sam_header(gi, 0, opt->commandLine ? opt->commandLine : "", opt->version ? opt->version : "", nullptr,
                            nullptr, 0, &hlen);
         std::string hdr(hlen, '\0');
-        if ((rc = snapgpu_sam_header(gi, 0, opt->commandLine ? opt->commandLine : "", opt->version ? opt->version : "",
-                                     nullptr, &hdr[0], hlen, &hlen))) { fclose(f); return fail(rc); }
+        int rc = snapgpu_sam_header(gi, 0, opt->commandLine ? opt->commandLine : "", opt->version ? opt->version : "",
+                                    nullptr, &hdr[0], hlen, &hlen);
+        if (rc) { fclose(f); return rc; }
         bool ok = true;
         if (bam) {   // BGZF stream: header, then the records (64 KB blocks), then the EOF block
             hdr.resize(strnlen(hdr.data(), hdr.size()));
             const std::string bh = bamHeader(*gi->genome, hdr);
             ok = bgzfWrite(f, bh.data(), bh.size(), false);
             std::string all;
-            for (auto &p : parts) all += p;
+            for (auto &x : subs) all += x->part;
             ok = ok && bgzfWrite(f, all.data(), all.size(), true);
         } else {
             ok = fwrite(hdr.data(), 1, hdr.size(), f) == hdr.size();
-            for (auto &p : parts) ok = ok && fwrite(p.data(), 1, p.size(), f) == p.size();
+            for (auto &x : subs) ok = ok && fwrite(x->part.data(), 1, x->part.size(), f) == x->part.size();
         }
         ok = (fclose(f) == 0) && ok;
-        if (!ok) { setError(std::string("write failed: ") + samPath); return fail(SNAPGPU_EIO); }
+        if (!ok) { setError(std::string("write failed: ") + samPath); return SNAPGPU_EIO; }
+        st.writeMs += msSince(t1);
     }
     if (out)
-        for (uint64_t i = 0; i < n; i++) {
-            const PairOut &r = po[i];
-            snapgpu_rna_pair_result_t &o = out[i];
-            memset(&o, 0, sizeof(o));
-            for (int k = 0; k < 2; k++) {
-                o.status[k] = (uint8_t)r.status[k];
-                o.location[k] = r.status[k] != SNAPGPU_NOT_FOUND ? r.location[k] : kInvalidLocation;
-                o.tlocation[k] = r.tlocation[k];
-                o.direction[k] = (uint8_t)r.direction[k];
-                o.score[k] = r.score[k];
-                o.mapq[k] = r.mapq[k];
-                o.isTranscriptome[k] = r.isTranscriptome[k];
+        for (auto &x : subs)
+            for (uint64_t i = x->a; i < x->b; i++) {
+                const PairOut &r = x->po[i - x->a];
+                snapgpu_rna_pair_result_t &o = out[i];
+                memset(&o, 0, sizeof(o));
+                for (int k = 0; k < 2; k++) {
+                    o.status[k] = (uint8_t)r.status[k];
+                    o.location[k] = r.status[k] != SNAPGPU_NOT_FOUND ? r.location[k] : kInvalidLocation;
+                    o.tlocation[k] = r.tlocation[k];
+                    o.direction[k] = (uint8_t)r.direction[k];
+                    o.score[k] = r.score[k];
+                    o.mapq[k] = r.mapq[k];
+                    o.isTranscriptome[k] = r.isTranscriptome[k];
+                }
+                o.fromAlignTogether = r.fromAlignTogether;
+                o.alignedAsPair = r.alignedAsPair;
+                o.useful = useful[i];
             }
-            o.fromAlignTogether = r.fromAlignTogether;
-            o.alignedAsPair = r.alignedAsPair;
-            o.useful = useful[i];
-        }
-    st.writeMs = msSince(t0);
+    st.subBatches = S;
     st.wallMs = msSince(w0);
     if (stats) *stats = st;
-    return fail(SNAPGPU_OK);
+    return SNAPGPU_OK;
 }
 
 }  // extern "C"

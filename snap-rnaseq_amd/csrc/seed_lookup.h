@@ -148,20 +148,19 @@ __global__ __launch_bounds__(64) void seed_lookup_kernel(KArgs A, SeedRec *out, 
         }
     }
     if (have) out[(uint64_t)r * SEEDS_PER_READ + k] = rec;
-    // route the wave's 8 reads (lane 8j speaks for read j): pass 1 list or straight to pass 2
-    if (A.shortList) {
-        const bool isShort = have && n <= 128, isLong = have && n > 128;
-        const uint64_t ms = ballot(k == 0 && isShort), ml = ballot(k == 0 && isLong);
-        uint32_t bs = 0, bl = 0;
-        if (lane == 0) {
-            if (ms) bs = atomicAdd(A.shortCount, (uint32_t)__popcll(ms));
-            if (ml) bl = atomicAdd(A.deferCount, (uint32_t)__popcll(ml));
+    // route the wave's long reads (lane 8j speaks for read j) straight onto pass 2's list
+    if (A.longCount) {
+        const bool isLong = have && n > 128;
+        const uint64_t ml = ballot(k == 0 && isLong);
+        if (ml) {
+            uint32_t bl = 0;
+            if (lane == 0) {
+                bl = atomicAdd(A.deferCount, (uint32_t)__popcll(ml));
+                atomicAdd(A.longCount, (uint32_t)__popcll(ml));
+            }
+            bl = (uint32_t)readlane((int)bl, 0);
+            if (k == 0 && isLong) A.deferList[bl + (uint32_t)__popcll(ml & ((1ull << lane) - 1))] = r;
         }
-        bs = (uint32_t)readlane((int)bs, 0);
-        bl = (uint32_t)readlane((int)bl, 0);
-        const uint64_t below = (1ull << lane) - 1;
-        if (k == 0 && isShort) A.shortList[bs + (uint32_t)__popcll(ms & below)] = r;
-        if (k == 0 && isLong) A.deferList[bl + (uint32_t)__popcll(ml & below)] = r;
     }
     if (stats) {
         uint64_t v = (uint64_t)nProbe | ((uint64_t)nSeed << 32) | ((uint64_t)nOvfRead << 44);

@@ -189,7 +189,7 @@ class RnaPairedStats(C.Structure):
     _fields_ = [(f, C.c_uint64) for f in ("totalPairs", "usefulPairs", "singleHits", "multiHits", "notFound",
                                           "transcriptomeRecords", "partialPairs", "partialMatches", "seedRuns")] + \
                [(f, C.c_double) for f in ("alignMs", "filterMs", "seedMs", "cigarMs", "writeMs", "wallMs", "prepMs",
-                                           "countMs")]
+                                           "countMs")] + [("subBatches", C.c_uint64)]
 
 
 class SingleStats(C.Structure):

@@ -79,10 +79,21 @@ def _fastq_block(path, a, b, dst):
 
 # stem: 2 x <=101 pairs (rna_*.fq) and 2 x 150 pairs, BASELINE configs[4]'s read length (rna150_*.fq:
 # 150-b mates through align_kernel<256> multi-hit, paired_kernel<256>, 150-b CIGARs and splices)
+@pytest.fixture
+def subbatch(request, monkeypatch):
+    """SNAPGPU_RNA_SUBBATCH: pairs per pipelined sub-batch of snapgpu_rna_paired_align (None: the
+    default 16384, so a fixture block is one sub-batch; small values cut a block into several)."""
+    if request.param:
+        monkeypatch.setenv("SNAPGPU_RNA_SUBBATCH", str(request.param))
+    else:
+        monkeypatch.delenv("SNAPGPU_RNA_SUBBATCH", raising=False)
+    return request.param
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("stem", ["rna", "rna150"])
-@pytest.mark.parametrize("use_m", [0, 1])
-def test_rna_paired_product_path_matches_reference(gpu_available, tmp_path, use_m, stem):
+@pytest.mark.parametrize("stem,use_m,subbatch", [("rna", 0, None), ("rna", 1, None), ("rna150", 0, None),
+                                                 ("rna150", 1, None), ("rna150", 0, 37)], indirect=["subbatch"])
+def test_rna_paired_product_path_matches_reference(gpu_available, tmp_path, use_m, stem, subbatch):
     fixture = f"expected_{stem}_paired{'_M' if use_m else ''}.sam.gz"
     gtf, gidx, tidx = _indexes(tmp_path)
     pa = snapgpu.PairedAligner(gidx, device=0)   # paired CLI defaults (maxHits 16000, maxK 15, 8 seeds)
@@ -100,6 +111,7 @@ def test_rna_paired_product_path_matches_reference(gpu_available, tmp_path, use_
         res, st = snapgpu.rna_paired_align(pa, ta, gtf, r0, r1, sam, useM=use_m)
         for k in totals:
             totals[k] += st[k]
+        assert st["subBatches"] == (-(-(a1 - a0) // subbatch) if subbatch else 1)
         lines = open(sam).read().splitlines(keepends=True)
         if b == 0:
             body += [l for l in lines if l.startswith("@") and not l.startswith("@PG")]
@@ -124,13 +136,14 @@ def test_rna_paired_product_path_matches_reference(gpu_available, tmp_path, use_
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("stem", ["rna", "rna150"])
-@pytest.mark.parametrize("use_m", [0, 1])
-def test_rna_paired_bam_matches_reference(gpu_available, tmp_path, use_m, stem):
+@pytest.mark.parametrize("stem,use_m,subbatch", [("rna", 0, None), ("rna", 1, None), ("rna150", 0, None),
+                                                 ("rna150", 1, None), ("rna", 0, 29)], indirect=["subbatch"])
+def test_rna_paired_bam_matches_reference(gpu_available, tmp_path, use_m, stem, subbatch):
     """`snap-rna paired ... -o out.bam`: SimpleReadWriter::writePair -> BAMFormat::writeRead of both
     ends with their mate fields (ReadWriter.cpp:133-217, Bam.cpp:596-790) in a BGZF stream; the
     decompressed records of every block equal the reference's byte for byte, including the NM the
-    reference carries over onto unmapped records (fixtures: make_golden.py --only-rna-bam).  As for
+    reference carries over onto unmapped records (fixtures: make_golden.py --only-rna-bam), also across
+pipelined sub-batches (subbatch 29).  As for
     the single-end BAM, a transcriptome record may differ only by the trailing uninitialised CIGAR
     slot the reference counts in n_cigar_op (insertSpliceJunctions)."""
     import json
