@@ -669,7 +669,7 @@ typedef struct snapgpu_rna_paired_stats {
     double alignMs, filterMs, seedMs, cigarMs, writeMs, wallMs;
     double prepMs;     /* clipping, ID check, pre-filter, batch views (before alignMs) */
     double countMs;    /* spacing / MAPQ adjustments and the GTF read counts (after seedMs) */
-    uint64_t subBatches;   /* pipelined sub-batches (SNAPGPU_RNA_SUBBATCH pairs each, default 16384): the
+    uint64_t subBatches;   /* pipelined sub-batches (SNAPGPU_RNA_SUBBATCH pairs each; default: one): the
                               stage times above are sums over them and overlap one another in wallMs */
 } snapgpu_rna_paired_stats_t;
 

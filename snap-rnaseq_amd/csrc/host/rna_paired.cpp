@@ -793,11 +793,15 @@ int snapgpu_rna_paired_align(snapgpu_paired_aligner_t *pa, snapgpu_aligner_t *ta
     std::mutex mG, mTown;
     std::mutex &mT = ta == ga ? mG : mTown;
     RnaRun Rr{pa, ta, ga, gi, ti, gtf, {R[0], R[1]}, opt, &useful, &mT, &mG, &C, bam};
-    // Sub-batches of the pairs, pipelined: stage A (the GPU aligners) of sub-batch s + 1 runs while
-    // stage B (filter, seed census, counts, CIGARs, records) of sub-batch s runs on another thread.
-    // Every stage keeps the reference's per-pair semantics; records and count events are kept in
-    // input order across sub-batches.
-    uint64_t per = 16384;
+    // Optional sub-batches of the pairs (SNAPGPU_RNA_SUBBATCH pairs each), pipelined: stage A (the
+    // GPU aligners) of sub-batch s + 1 runs while stage B (filter, seed census, counts, CIGARs,
+    // records) of sub-batch s runs on another thread.  Every stage keeps the reference's per-pair
+    // semantics; records and count events stay in input order across sub-batches.  Off by default:
+    // each aligner call pays the tail of its slowest read (the persistent kernels end with the
+    // heaviest repeat / multi-hit reads), so 7 sub-batches of 16k pairs made a 100k-pair batch 2x
+    // slower (alignMs 80 -> 230, profiles/r03/ab/rna_subbatch_ab.txt); the caller's batches are the
+    // unit of overlap instead.
+    uint64_t per = n ? n : 1;
     if (const char *e = getenv("SNAPGPU_RNA_SUBBATCH"); e && atoll(e) > 0) per = (uint64_t)atoll(e);
     const uint64_t S = n ? (n + per - 1) / per : 0;
     std::vector<std::unique_ptr<RnaSub>> subs(S);
