@@ -125,7 +125,7 @@ struct KArgs {
     const uint32_t *readCount;   //   and their number (the previous pass's deferCount)
     const uint4 *seedRecs;       // seed_lookup_kernel records (SeedRec, 8 per read), or nullptr
     // pass 0 puts the reads longer than 128 bases straight onto deferList (pass 2's list) with one
-    // atomic per 8-read wave that holds any, and counts them in longCount; pass 1 (longCount set)
+    // atomic per 4-read wave that holds any, and counts them in longCount; pass 1 (longCount set)
     // then skips them instead of deferring them one by one, and ends at once when every read is long
     uint32_t *longCount;
     unsigned long long *phaseBuf;   // diagnostic (SNAPGPU_PHASES=1): per-block [PH_SLOTS] cycle sums, else null

@@ -277,12 +277,14 @@ __device__ __forceinline__ void lv_prob_pair(const DevTables *tab, const GroupLd
     const bool runEnd = valid && (j == e || pmv != 0 || an != a);
     // offset before step j: inclusive scan of delta over the half-wave, minus own delta
     const int delta = valid ? (a == 1 ? -1 : 1) + pmv : 0;
+    // inclusive scan over each half-wave in DPP, no LDS round trips: Hillis-Steele inside each
+    // 16-lane row, then rows 1 and 3 add the last lane of rows 0 and 2 (row_bcast:15)
     int incl = delta;
-#pragma unroll
-    for (int o = 1; o < 32; o <<= 1) {
-        const int v = shfl_idx(incl, lane - o < 0 ? lane : lane - o);
-        if ((lane & 31) >= o) incl += v;
-    }
+    incl += __builtin_amdgcn_update_dpp(0, incl, 0x111, 0xf, 0xf, true);   // row_shr:1
+    incl += __builtin_amdgcn_update_dpp(0, incl, 0x112, 0xf, 0xf, true);   // row_shr:2
+    incl += __builtin_amdgcn_update_dpp(0, incl, 0x114, 0xf, 0xf, true);   // row_shr:4
+    incl += __builtin_amdgcn_update_dpp(0, incl, 0x118, 0xf, 0xf, true);   // row_shr:8
+    incl += __builtin_amdgcn_update_dpp(0, incl, 0x142, 0xa, 0xf, false);  // row_bcast:15 into rows 1, 3
     const int offset = L0 + incl - delta;
     // indel run length = distance to the previous run end of this direction
     const uint64_t ends = ballot(runEnd);
@@ -422,6 +424,8 @@ __device__ __forceinline__ void lv_pass(const KArgs &A, Lds<MAXLEN> &S, uint32_t
 // order (BaseAligner.cpp:1129-1384).  Returns true when the read is finished
 // (stopOnFirstHit).  GS is a template parameter so group indexing is shifts and the
 // per-group loops unroll.
+constexpr int FETCH_NLD = (EB * Elem128::DWORDS + WAVE - 1) / WAVE;   // dwords per lane of a popped batch
+
 template <int GS, bool EXT, int MAXLEN>
 __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem128 *ar, ReadState &st, uint32_t i0, int m,
                                            int k, uint32_t n, uint32_t nb, uint32_t &lastSlot, bool &lastSkip,
@@ -583,7 +587,7 @@ __device__ __forceinline__ bool forced_sort(const KArgs &A, Lds<MAXLEN> &S, Elem
                                             const uint64_t *&sorted, uint32_t &nLinked) {
     if (((uint64_t)A.arenaElems - nE) * sizeof(Elem128) < 16ull * nE + 64) return false;
     uint64_t *bufA = reinterpret_cast<uint64_t *>(ar + nE), *bufB = bufA + nE;
-    uint32_t n = 0;
+    uint32_t n = 0, kOr = 0, kAnd = 0xffffffffu;
     for (uint32_t e0 = 0; e0 < nE; e0 += WAVE) {   // linked elements, compacted in index order
         const int lane = lane_id();
         const uint32_t e = e0 + (uint32_t)lane;
@@ -591,10 +595,16 @@ __device__ __forceinline__ bool forced_sort(const KArgs &A, Lds<MAXLEN> &S, Elem
         const uint64_t m = ballot(k != 0u);
         if (k) bufA[n + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = ((uint64_t)k << 32) | e;
         n += (uint32_t)__popcll(m);
+        kOr |= k;
+        kAnd &= k ? k : 0xffffffffu;
     }
+    // a digit that is the same in every key leaves a stable pass's order unchanged: skip its pass
+    // (the keys' timestamp bits above the read's hit count are all ones, and weights fit in 5 bits)
+    const uint32_t varying = (uint32_t)or_reduce64(kOr) ^ ~(uint32_t)or_reduce64(~kAnd);   // OR ^ AND
     wave_sync();
     uint32_t *hist = reinterpret_cast<uint32_t *>(&S.u.sc.rows8[0][0]);
     for (int pass = 0; pass < 4; pass++) {
+        if (((varying >> (8 * pass)) & 255u) == 0u) continue;
         const int lane = lane_id();
         const int sh = 32 + 8 * pass;
         for (int j = lane; j < 256; j += WAVE) hist[j] = 0u;
@@ -757,19 +767,20 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, El
         }
         PH_ADD(A, S, PH_SEL, tpop);
         PH_T(A, tfe);
-        // ---- fetch the batch from the arena in one round trip
+        // ---- fetch the batch from the arena in one round trip.  (Loading the next forced batch
+        // during this one's passes measured 1% slower: the 9 VGPRs it holds across the pass loop,
+        // profiles/r03/ab/micro_opts_ab.txt.)
         {
             constexpr int ED = Elem128::DWORDS;
-            constexpr int NLD = (EB * ED + WAVE - 1) / WAVE;
             const uint32_t tot = nb * ED;
-            uint32_t v[NLD];
+            uint32_t v[FETCH_NLD];
 #pragma unroll
-            for (int j = 0; j < NLD; j++) {
+            for (int j = 0; j < FETCH_NLD; j++) {
                 const uint32_t idx = (uint32_t)(j * WAVE + lane);
                 v[j] = idx < tot ? ((const uint32_t *)(ar + G.eidx[idx / ED]))[idx % ED] : 0u;
             }
 #pragma unroll
-            for (int j = 0; j < NLD; j++) {
+            for (int j = 0; j < FETCH_NLD; j++) {
                 const uint32_t idx = (uint32_t)(j * WAVE + lane);
                 if (idx < tot) G.ecache[idx / ED][idx % ED] = v[j];
             }

@@ -450,7 +450,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
         // first-round lookups resolved by seed_lookup_kernel: lane 4k+f holds field f of record k
         uint32_t srec = 0, pfIdx = SEEDS_PER_READ;
         if (MAXLEN == 128 && A.seedRecs && A.maxHits < 0xffffu && radius == 0) {
-            srec = ((const uint32_t *)(A.seedRecs + (uint64_t)r * SEEDS_PER_READ))[lane & 31];
+            srec = ((const uint32_t *)(A.seedRecs + (uint64_t)r * SEEDS_PER_READ))[lane & (4 * SEEDS_PER_READ - 1)];
             pfIdx = 0;
         }
         // One call site for the scorer (it is large): `force` marks the final scoring
@@ -1502,12 +1502,12 @@ static int launch_passes(snapgpu_aligner_t *a, int li, const PassIO &io, const A
     (void)hipGetLastError();   // clear any stale error of an unrelated earlier runtime call
     if (prev && !a->overlapKernels) HIPCHK(hipStreamWaitEvent(L.stream, prev->e[2], 0));
     HIPCHK(hipMemsetAsync(L.counter, 0, 64, L.stream));
-    // pass 0: first-round seed lookups of every read (8 reads per 64-lane block); it also puts the
+    // pass 0: the first SEEDS_PER_READ seed lookups of every read (4 reads per 64-lane block); it also puts the
     // reads longer than 128 bases straight onto pass 2's list
     A.seedRecs = nullptr;
     A.longCount = L.counter + 5;
     HIPCHK(hipEventRecord(ev.e[3], L.stream));
-    hipLaunchKernelGGL(seed_lookup_kernel, dim3((unsigned)((io.n + 7) / 8)), dim3(64), 0, L.stream, A, io.seeds,
+    hipLaunchKernelGGL(seed_lookup_kernel, dim3((unsigned)((io.n + 3) / 4)), dim3(64), 0, L.stream, A, io.seeds,
                        L.lookupStats);
     HIPCHK(hipGetLastError());
     A.seedRecs = reinterpret_cast<const uint4 *>(io.seeds);

@@ -1,27 +1,29 @@
-// seed_lookup.h -- first-round seed lookups of every read, resolved up front.
+// seed_lookup.h -- the first SEEDS_PER_READ seed lookups of every read, resolved up front.
 //
-// In BaseAligner::AlignRead the seed offsets tried first are 0, seedLen, 2*seedLen,
-// ... (a seed containing a non-ACGT base is skipped and the next one starts one base
-// later; BaseAligner.cpp:686-746): they depend only on the read's bases, not on any
-// lookup result.  seed_lookup_kernel resolves GenomeIndex::lookupSeed
-// (GenomeIndex.cpp:971-1086, SNAPHashTable::Lookup HashTable.h:74-105) for those
-// seeds of every read <= 128 bases, one lane per (read, seed): 8 reads per wave,
-// thousands of independent probe chains in flight, so the hash-table gather runs at
-// memory throughput instead of as ~3 dependent HBM round trips inside each read's
-// sequential aligner.  align_kernel<128> consumes the records when its seed loop
-// reaches the same offset and counts probes / overflow lists exactly as before.
+// In BaseAligner::AlignRead the sequence of seed offsets is 0, seedLen, 2*seedLen, ...,
+// then the wrapped rounds (GetWrappedNextSeedToTest, skipping offsets already used; a seed
+// containing a non-ACGT base is marked used and skipped without the +seedLen advance;
+// BaseAligner.cpp:686-746): it depends only on the read's bases, not on any lookup result --
+// results decide only how far along it a read gets.  seed_lookup_kernel resolves
+// GenomeIndex::lookupSeed (GenomeIndex.cpp:971-1086, SNAPHashTable::Lookup HashTable.h:74-105)
+// for the first 16 seeds of that sequence for every read <= 128 bases, one lane per (read, seed):
+// 4 reads per wave, thousands of independent probe chains in flight, so the hash-table gather
+// runs at memory throughput instead of as ~3 dependent HBM round trips inside each read's
+// sequential aligner.  align_kernel<128> consumes the records when its seed loop reaches the same
+// offset and counts probes / overflow lists exactly as before (a read that stops earlier leaves
+// its later records unused).
 #pragma once
 #include "align_device.h"
 
 namespace sgk {
 
-// 16 bytes per (read, first-round seed k < 8)
+// 16 bytes per (read, seed k of the sequence, k < SEEDS_PER_READ)
 struct SeedRec {
     uint32_t meta;      // bit31 valid, [7:0] offset, bit8 found, bit9 comp, bit10 palindrome, [30:16] probes
     uint32_t v1, v2;    // slot values (GenomeIndex.cpp:1004-1010 swaps them when comp)
     uint32_t cnt;       // overflow counts, u16 each, saturated: [15:0] value1 side, [31:16] value2 side
 };
-constexpr int SEEDS_PER_READ = 8;
+constexpr int SEEDS_PER_READ = 16;   // = lanes per read in seed_lookup_kernel: 4 reads per wave
 
 // bits [p, p+len) of a 128-bit value (len <= 32)
 __device__ __forceinline__ uint32_t win128(uint64_t lo, uint64_t hi, int p, int len) {
@@ -46,8 +48,9 @@ __device__ __forceinline__ uint64_t spread2(uint32_t x32) {
 // bytes); slot = block % 256
 __global__ __launch_bounds__(64) void seed_lookup_kernel(KArgs A, SeedRec *out, unsigned long long *stats) {
     const int lane = lane_id();
-    const uint32_t r = blockIdx.x * 8 + (lane >> 3);
-    const int k = lane & 7;
+    const uint32_t r = blockIdx.x * 4 + (lane >> 4);
+    const int k = lane & 15;
+    const int sub = k & 7;          // lanes k < 8 load the read, 16 bases each
     const bool have = r < A.nReads;
     const uint32_t n = have ? A.lengths[r] : 0;
     const uint64_t off = have ? A.offsets[r] : 0;
@@ -55,12 +58,12 @@ __global__ __launch_bounds__(64) void seed_lookup_kernel(KArgs A, SeedRec *out, 
     // 16 bases per lane (read buffer carries >= 64 bytes of slack past the last read)
     uint64_t chunk = 0;   // [15:0] bit0 of the seed code, [31:16] bit1, [47:32] not-ACGT / past the end
     {
-        const uint64_t b0 = off + 16 * (uint64_t)k;
+        const uint64_t b0 = off + 16 * (uint64_t)sub;
         const uint32_t *src = (const uint32_t *)(A.bases + (b0 & ~3ull));
         const uint32_t sh = (uint32_t)(b0 & 3) * 8;
         uint32_t w[5];
 #pragma unroll
-        for (int i = 0; i < 5; i++) w[i] = have && n > 16u * k ? src[i] : 0u;
+        for (int i = 0; i < 5; i++) w[i] = have && k < 8 && n > 16u * sub ? src[i] : 0u;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             const uint32_t d = __builtin_amdgcn_alignbit(w[i + 1], w[i], sh);
@@ -68,7 +71,7 @@ __global__ __launch_bounds__(64) void seed_lookup_kernel(KArgs A, SeedRec *out, 
             for (int b = 0; b < 4; b++) {
                 uint32_t c = (d >> (8 * b)) & 0xff;
                 if (c >= 'a' && c <= 'z') c -= 0x20;   // Read::init upper-cases (Read.h:289-328)
-                const int pos = 16 * k + 4 * i + b;
+                const int pos = 16 * sub + 4 * i + b;
                 const int v = base_value(c);            // Seed encoding A0 G1 C2 T3 (Tables.cpp:41-48)
                 const bool inv = pos >= (int)n || v > 3;
                 const int bit = 4 * i + b;
@@ -81,7 +84,7 @@ __global__ __launch_bounds__(64) void seed_lookup_kernel(KArgs A, SeedRec *out, 
     uint64_t P0[2] = {0, 0}, P1[2] = {0, 0}, IV[2] = {0, 0};
 #pragma unroll
     for (int j = 0; j < 8; j++) {
-        const int src = (lane & ~7) + j;
+        const int src = (lane & ~15) + j;
         const uint32_t lo = (uint32_t)shfl_idx((int)(uint32_t)chunk, src);
         const uint32_t hi = (uint32_t)shfl_idx((int)(uint32_t)(chunk >> 32), src);
         const int wd = j >> 2, s = 16 * (j & 3);
@@ -92,11 +95,20 @@ __global__ __launch_bounds__(64) void seed_lookup_kernel(KArgs A, SeedRec *out, 
     SeedRec rec = {0u, 0u, 0u, 0u};
     uint32_t nSeed = 0, nProbe = 0, nOvfRead = 0;
     if (have && n <= 128 && (int)n >= L) {
-        // k-th first-round seed offset
+        // offset of the k-th seed of the sequence (BaseAligner.cpp:686-746), simulated with the
+        // read's seedUsed bits: rounds 0, seedLen, ... then the wrap table's starts
         const int nPossible = (int)n - L + 1;
-        int p = 0, idx = 0, my = -1;
-        while (p < nPossible) {
-            if (win128(IV[0], IV[1], p, L)) { p++; continue; }   // BaseAligner.cpp:740-744
+        uint64_t u0 = 0, u1 = 0;   // seedUsed, positions 0..127
+        int p = 0, wrap = 0, idx = 0, my = -1;
+        for (int guard = 0; guard < 4 * 128; guard++) {   // each step marks, wraps or ends
+            if (p >= nPossible) {
+                if (++wrap >= L) break;                      // wrapCount == seedLen: the read is scored
+                p = (int)A.tab->wrap[wrap];
+            }
+            while (p < nPossible && (((p < 64 ? u0 >> p : u1 >> (p - 64)) & 1ull) != 0)) p++;
+            if (p >= nPossible) continue;
+            if (p < 64) u0 |= 1ull << p; else u1 |= 1ull << (p - 64);
+            if (win128(IV[0], IV[1], p, L)) continue;        // not a seed: used, no advance (:740-744)
             if (idx == k) { my = p; break; }
             idx++;
             p += L;
@@ -148,7 +160,7 @@ __global__ __launch_bounds__(64) void seed_lookup_kernel(KArgs A, SeedRec *out, 
         }
     }
     if (have) out[(uint64_t)r * SEEDS_PER_READ + k] = rec;
-    // route the wave's long reads (lane 8j speaks for read j) straight onto pass 2's list
+    // route the wave's long reads (lane 16j speaks for read j) straight onto pass 2's list
     if (A.longCount) {
         const bool isLong = have && n > 128;
         const uint64_t ml = ballot(k == 0 && isLong);
