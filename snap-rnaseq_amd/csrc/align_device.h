@@ -52,6 +52,7 @@ struct DevTables {
     double seedProb;          // __powidf2(0.999, seedLen), BaseAligner.cpp:1227
     uint32_t wrap[32];        // GetWrappedNextSeedToTest order (SeedSequencer.h)
     double mapqT[72];         // mapqT[q] = 10^(-q/10) (glibc pow): MAPQ thresholds, no device log10
+    uint32_t maxSeedsForLen[513];   // (int)(seedCoverage * n / seedLen) per read length n (BaseAligner.cpp:563-568)
 };
 // The seedLen-independent tables (indel, phred, perfect, mapqT), one copy per device, set
 // once by the host: a global's address is a constant the compiler rematerializes, where a
@@ -138,28 +139,6 @@ struct KArgs {
     int32_t *multiFound;                // per read
     snapgpu_multi_hit_t *multiHits;     // [nReads][maxHitsToGet]
 };
-
-// ------------------------------------------------------------ streaming loads
-// Index, genome-plane and hit-list loads are touched once per use; with SNAPGPU_NT they carry
-// the non-temporal hint so they do not push the element arena (re-read and re-written all
-// through a read) out of L2.
-#ifndef SNAPGPU_NT
-#define SNAPGPU_NT 0
-#endif
-typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-template <typename T>
-__device__ __forceinline__ T ld_stream(const T *p) {
-    if constexpr (SNAPGPU_NT) return __builtin_nontemporal_load(p);
-    else return *p;
-}
-__device__ __forceinline__ uint4 ld_stream4(const uint4 *p) {
-    if constexpr (SNAPGPU_NT) {
-        const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t *>(p));
-        return make_uint4(v.x, v.y, v.z, v.w);
-    } else {
-        return *p;
-    }
-}
 
 // ------------------------------------------------------------ wave helpers
 // Lane id through volatile asm: the compiler cannot hoist it (or the per-lane LDS

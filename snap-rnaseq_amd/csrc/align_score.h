@@ -378,9 +378,11 @@ __device__ __forceinline__ void lv_pass(const KArgs &A, Lds<MAXLEN> &S, uint32_t
         const int64_t gp = (int64_t)P.loc + (li - c) + PACK_GUARD;
         const uint4 *src = A.gpl + (gp >> 5);
         const uint32_t sh = (uint32_t)gp & 31;
-        uint4 w[2 * NW + 1];
+        // {hi, lo, notACGT} of each 16-B plane word: 12-B loads, the padding dword is never read
+        struct alignas(4) Plane3 { uint32_t x, y, z; };
+        Plane3 w[2 * NW + 1];
 #pragma unroll
-        for (int j = 0; j < 2 * NW + 1; j++) w[j] = ld_stream4(src + j);
+        for (int j = 0; j < 2 * NW + 1; j++) w[j] = *reinterpret_cast<const Plane3 *>(src + j);
         const uint64_t *rp = &G.rpl[P.dir][0][0];
         uint64_t RHw[NW], RLw[NW], RMw[NW];
 #pragma unroll

@@ -226,7 +226,7 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
         const uint32_t lpsNow = dir ? st.lps[1] : st.lps[0];
         const bool allowAlloc = lpsNow <= st.scoreLimit;
         bool valid = i < lim;
-        uint32_t h = valid ? (list ? ld_stream(list + ii) : (dir ? single1 : single0)) : 0;
+        uint32_t h = valid ? (list ? list[ii] : (dir ? single1 : single0)) : 0;
         uint32_t loc = h - offset;
         valid = valid && h >= offset;
         if constexpr (EXT) valid = valid && loc >= minLoc && loc <= maxLoc;   // BaseAligner.cpp:849-853
@@ -355,7 +355,10 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
     uint32_t flags = MAXLEN > 128 ? SNAPGPU_FLAG_DEFERRED : 0u;   // passes 2 and 3 align only deferred reads
     if constexpr (Lds<MAXLEN>::BYTE_PATH) flags |= SNAPGPU_FLAG_BYTE_PATH;
     int result = SNAPGPU_NOT_FOUND;
-    const uint32_t maxSeeds = A.maxSeedsCmd ? A.maxSeedsCmd : (uint32_t)(int)(A.seedCoverage * n / seedLen);
+    // maxSeedsToUse from the seed coverage (BaseAligner.cpp:563-568) by a host table, no device
+    // double division (its hoisted operand was align_kernel<256>'s one scratch spill); a read
+    // longer than 512 bases is not aligned (READ_TOO_LONG)
+    const uint32_t maxSeeds = A.maxSeedsCmd ? A.maxSeedsCmd : (n <= 512u ? A.tab->maxSeedsForLen[n] : 0u);
     const uint32_t numWeightLists = maxSeeds + 1;
     bool run = true;
     if constexpr (!Lds<MAXLEN>::BYTE_PATH) {   // bit-plane kernels: longer reads go on to the next pass
@@ -523,7 +526,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
                     if (pos >= size) pos %= size;
                     uint32_t kj = 0, v1j = INVALID, v2j = 0;
                     bool beyond = j > size + 5;
-                    if (lane < 8 && !beyond) { kj = ld_stream(T + 3 * pos); v1j = ld_stream(T + 3 * pos + 1); v2j = ld_stream(T + 3 * pos + 2); }
+                    if (lane < 8 && !beyond) { kj = T[3 * pos]; v1j = T[3 * pos + 1]; v2j = T[3 * pos + 2]; }
                     bool stop = (j == 0) ? (kj == key && v1j != INVALID) : (kj == key || v1j == INVALID);
                     uint64_t m = ballot(lane < 8 && (stop || beyond)) & 0xffull;
                     if (m) {
@@ -546,7 +549,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
                     if (vf < A.nBases) { nH0 = 1; sg0 = vf; }
                     else if (vf != UNUSED_SIDE) {
                         uint32_t o = vf - A.nBases;
-                        nH0 = pre ? (pcnt & 0xffff) : uni(ld_stream(A.overflow + o));
+                        nH0 = pre ? (pcnt & 0xffff) : uni(A.overflow[o]);
                         ls0 = A.overflow + o + 1;
                         sv_add(st, lane, SV_OVF, 1);
                     }
@@ -554,7 +557,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
                     else if (vr < A.nBases) { nH1 = 1; sg1 = vr; }
                     else if (vr != UNUSED_SIDE) {
                         uint32_t o = vr - A.nBases;
-                        nH1 = pre ? (pcnt >> 16) : uni(ld_stream(A.overflow + o));
+                        nH1 = pre ? (pcnt >> 16) : uni(A.overflow[o]);
                         ls1 = A.overflow + o + 1;
                         sv_add(st, lane, SV_OVF, 1);
                     }
@@ -1356,6 +1359,8 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
         return fail("pieces", e);
     DevTables t;
     fillTables(t, idx->seedLen);
+    for (uint32_t len = 0; len <= 512; len++)   // BaseAligner.cpp:563-568, double arithmetic as there
+        t.maxSeedsForLen[len] = (uint32_t)(int)(params->maxSeedCoverage * (double)len / (double)idx->seedLen);
     if ((e = hipMalloc(&a->dTab, sizeof(DevTables))) != hipSuccess) return fail("tables", e);
     if ((e = hipMemcpy(a->dTab, &t, sizeof(t), hipMemcpyHostToDevice)) != hipSuccess) return fail("tables", e);
     // persistent grid: waves resident on the device; element arena per wave and lane

@@ -134,11 +134,11 @@ __global__ __launch_bounds__(64) void seed_lookup_kernel(KArgs A, SeedRec *out, 
                 const uint32_t S_j = j <= 4 ? j * (j + 1) * (2 * j + 1) / 6 : 30 + (j - 4);
                 uint64_t pos = h0 + S_j;
                 if (pos >= size) pos %= size;
-                const uint32_t kj = ld_stream(T + 3 * pos), v1j = ld_stream(T + 3 * pos + 1);
+                const uint32_t kj = T[3 * pos], v1j = T[3 * pos + 1];
                 const bool stop = (j == 0) ? (kj == key && v1j != INVALID) : (kj == key || v1j == INVALID);
                 if (stop) {
                     probes = j + 1;
-                    if (j == 0 || v1j != INVALID) { found = true; v1 = v1j; v2 = ld_stream(T + 3 * pos + 2); }
+                    if (j == 0 || v1j != INVALID) { found = true; v1 = v1j; v2 = T[3 * pos + 2]; }
                     break;
                 }
             }
@@ -148,8 +148,8 @@ __global__ __launch_bounds__(64) void seed_lookup_kernel(KArgs A, SeedRec *out, 
             if (found) {   // overflow list lengths (GenomeIndex.cpp:1013-1086)
                 const uint32_t vf = comp ? v2 : v1, vr = comp ? v1 : v2;
                 uint32_t cf = 0, cr = 0;
-                if (vf >= A.nBases && vf != UNUSED_SIDE) { cf = ld_stream(A.overflow + (vf - A.nBases)); nOvfRead++; }
-                if (f != rcv && vr >= A.nBases && vr != UNUSED_SIDE) { cr = ld_stream(A.overflow + (vr - A.nBases)); nOvfRead++; }
+                if (vf >= A.nBases && vf != UNUSED_SIDE) { cf = A.overflow[vf - A.nBases]; nOvfRead++; }
+                if (f != rcv && vr >= A.nBases && vr != UNUSED_SIDE) { cr = A.overflow[vr - A.nBases]; nOvfRead++; }
                 cnt = (cf < 0xffffu ? cf : 0xffffu) | ((cr < 0xffffu ? cr : 0xffffu) << 16);
             }
             rec.meta = 0x80000000u | (uint32_t)my | (found ? 0x100u : 0u) | (comp ? 0x200u : 0u) |
