@@ -272,6 +272,31 @@ def rna_parity(args, pa, ta, gtf, r0, r1, work):
                     "pairs, genome, GTF"}
 
 
+def rna_roofline(ta, r0):
+    """Roofline of the RNA leg's dominant kernel, align_kernel<256> (the 2 x 150 mates' pass), on the
+    transcriptome aligner over end 0 (untimed extra call): SURVEY 8(d) d3 algorithmic bytes of the
+    records (each read at its own length) / the pass-2+3 kernel time (HIP events)."""
+    res = ta.AlignReads(r0)
+    ks = []
+    for _ in range(3):
+        ta.AlignReads(r0, out=res)
+        ks.append(ta.timing()["spillKernelMs"])
+    lens = np.array([len(r0.get(i)[0]) for i in range(r0.n)], dtype=np.int64)
+    P = res["nProbes"].astype(np.int64)
+    H = res["nHitWords"].astype(np.int64)
+    V = res["nOverflowLists"].astype(np.int64)
+    S = res["nLocationsScored"].astype(np.int64)
+    b = int((2 * lens + 16 + 12 * P + 4 * (H + V) + (lens + MAX_K) * S).sum())
+    ms = float(min(ks))
+    return {"kernel": "align_kernel<256, false> (+ the empty <512> pass)", "reads": int(r0.n),
+            "kernel_ms": ms, "algorithmic_bytes": b, "achieved": b / (ms / 1000.0) / 1e9, "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": b / (ms / 1000.0) / 1e9 / HBM_PEAK_GBS,
+            "per_read": {"P": float(P.mean()), "H": float(H.mean()), "V": float(V.mean()), "S": float(S.mean())},
+            "params": "transcriptome aligner of the RNA path: maxHits 16000, maxK 15, 8 seeds, extra 2",
+            "note": "end 0 of the batch through snapgpu_align_batch (plain AlignRead; the product path's "
+                    "multi-hit calls run the EXT twin of the same kernel)"}
+
+
 def rna_leg(args, idx, local, build_threads):
     """SURVEY.md 8(f) f4 (BASELINE configs[4] shape on this workload's genome): the RNA paired
     product path (`snap-rna paired`: transcriptome multi-hit + chimeric genome aligners,
@@ -306,7 +331,8 @@ def rna_leg(args, idx, local, build_threads):
         dt, st = ts[k], sts[k]
         n = r0.n
         parity = rna_parity(args, pa, ta, gtf, r0, r1, work)
-        return {"parity": parity, "value": 2 * n / dt, "unit": "reads/s", "pairs_per_s": n / dt, "pairs": n, "ms_per_batch": dt * 1e3,
+        roof = rna_roofline(ta, r0)
+        return {"parity": parity, "roofline": roof, "value": 2 * n / dt, "unit": "reads/s", "pairs_per_s": n / dt, "pairs": n, "ms_per_batch": dt * 1e3,
                 "read_len": 150, "workload": info, "transcriptome_bases": tidx.info()["nBases"],
                 "stage_ms": {x: round(st[x], 2) for x in ("prepMs", "alignMs", "filterMs", "seedMs", "countMs", "cigarMs",
                                                           "writeMs", "wallMs")},
