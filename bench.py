@@ -589,7 +589,9 @@ def main():
                                          "note": "64-B lines per random access (SURVEY 8(d) d3)"},
                     "launches_per_step": n_launch, "reads_per_launch": reads_launch,
                     "algorithmic_bytes_per_launch": bytes_launch, "algorithmic_bytes_per_read": bytes_all / len(res),
-                    "binding_resource": "VALU issue (DESIGN.md section 4), not HBM bandwidth",
+                    "binding_resource": "instruction issue of one serial wave per read (VALU issue 0.66 of what 4 "
+                                        "waves/SIMD can give, plus dependent memory round trips), not HBM "
+                                        "bandwidth (DESIGN.md section 4)",
                     "valu_issue": valu_issue, "pmc_source": pmc_src, "lib_sha256": sha,
                     "kernel_source_sha256": src_sha}
         counts = {int(k): int(v) for k, v in zip(*np.unique(res["result"], return_counts=True))}

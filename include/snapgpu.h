@@ -336,6 +336,8 @@ typedef struct snapgpu_timing {
     double lookupKernelBusyMs;/* union of the pass-0 launch intervals */
     uint64_t nByteReads;     /* reads deferred by pass 2 to the byte-compare pass 3 (> 256 bases,
                                 or IUPAC codes in both read and genome) */
+    uint64_t nArenaOverflow; /* reads that outgrew a capped element arena in passes 1-3 and were
+                                aligned again by the big-arena pass (worst-case arenas, small grid) */
 } snapgpu_timing_t;
 int snapgpu_last_timing(snapgpu_aligner_t *a, snapgpu_timing_t *t);
 

@@ -85,6 +85,13 @@ template <> struct ElemSel<128> { using type = Elem128; };
 template <> struct ElemSel<256> { using type = Elem128; };
 template <int MAXLEN> using ElemOf = typename ElemSel<MAXLEN>::type;
 
+// Genome bit planes: 32 bases per 12-byte word, 3 bits per base -- the 2-bit code (A=00 C=01 G=10
+// T=11) as two planes plus the not-ACGT plane a byte-exact comparison needs (N and IUPAC bytes
+// match nothing).  A window of 2*NW+1 words is one 12-B-strided run (60 B for a 128-base read),
+// one or two 128-B lines.
+struct alignas(4) GPlane { uint32_t hi, lo, nm; };
+static_assert(sizeof(GPlane) == 12, "GPlane layout");
+
 struct KArgs {
     uint32_t *diag;              // this aligner's watchdog record {code, read, detail, 0} (diag_report)
     // index (HBM)
@@ -114,8 +121,15 @@ struct KArgs {
     uint32_t *counter;
     void *arena;                 // ElemOf<MAXLEN> per block
     uint64_t arenaElems;         // per-wave capacity
-    // genome bit planes {hi, lo, notACGT, 0} per 32 bases, word 0 = position -PACK_GUARD
-    const uint4 *gpl;
+    // Main passes run on arenas capped below the worst case (maxSeeds + 2) * maxHits when that would
+    // not fit the whole grid (the RNA aligners' maxHits 16000): a read that outgrows its arena is
+    // abandoned (no record written) and listed here for the big-arena pass (align_kernel<512> on a
+    // small grid with worst-case arenas).  nullptr: the arena is worst-case sized (arena full =
+    // watchdog record, cannot happen).
+    uint32_t *ovfList;
+    uint32_t *ovfCount;
+    // genome bit planes {hi, lo, notACGT} per 32 bases (GPlane), word 0 = position -PACK_GUARD
+    const struct GPlane *gpl;
     uint32_t hasIupac;
     // three-pass dispatch: align_kernel<128> defers reads it cannot take (longer than 128
     // bases, or IUPAC codes on both sides) to align_kernel<256>, which defers reads longer than
@@ -668,7 +682,7 @@ struct ReadState {
     uint32_t ts;                 // running hit counter (FIFO timestamps)
     uint32_t statv;              // per-read counters, one per lane (SV_*): a VGPR instead of 6 SGPRs
     uint32_t rid;                // read index (watchdog reports)
-    uint32_t abort;              // watchdog tripped: finish the read now
+    uint32_t abort;              // watchdog tripped (1) or capped arena full (2): finish the read now
     uint32_t tick;               // overdue(): calls left until the next clock read
     uint64_t t0;                 // s_memrealtime at read start
 };

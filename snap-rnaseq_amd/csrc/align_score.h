@@ -376,13 +376,11 @@ __device__ __forceinline__ void lv_pass(const KArgs &A, Lds<MAXLEN> &S, uint32_t
     MaskW<NW> F;
     {
         const int64_t gp = (int64_t)P.loc + (li - c) + PACK_GUARD;
-        const uint4 *src = A.gpl + (gp >> 5);
+        const GPlane *src = A.gpl + (gp >> 5);
         const uint32_t sh = (uint32_t)gp & 31;
-        // {hi, lo, notACGT} of each 16-B plane word: 12-B loads, the padding dword is never read
-        struct alignas(4) Plane3 { uint32_t x, y, z; };
-        Plane3 w[2 * NW + 1];
+        GPlane w[2 * NW + 1];
 #pragma unroll
-        for (int j = 0; j < 2 * NW + 1; j++) w[j] = *reinterpret_cast<const Plane3 *>(src + j);
+        for (int j = 0; j < 2 * NW + 1; j++) w[j] = src[j];
         const uint64_t *rp = &G.rpl[P.dir][0][0];
         uint64_t RHw[NW], RLw[NW], RMw[NW];
 #pragma unroll
@@ -390,9 +388,9 @@ __device__ __forceinline__ void lv_pass(const KArgs &A, Lds<MAXLEN> &S, uint32_t
         uint32_t f[2 * NW];
 #pragma unroll
         for (int j = 0; j < 2 * NW; j++) {
-            const uint32_t gh = __builtin_amdgcn_alignbit(w[j + 1].x, w[j].x, sh);
-            const uint32_t gl = __builtin_amdgcn_alignbit(w[j + 1].y, w[j].y, sh);
-            const uint32_t gm = __builtin_amdgcn_alignbit(w[j + 1].z, w[j].z, sh);
+            const uint32_t gh = __builtin_amdgcn_alignbit(w[j + 1].hi, w[j].hi, sh);
+            const uint32_t gl = __builtin_amdgcn_alignbit(w[j + 1].lo, w[j].lo, sh);
+            const uint32_t gm = __builtin_amdgcn_alignbit(w[j + 1].nm, w[j].nm, sh);
             const uint64_t RH = RHw[j / 2], RL = RLw[j / 2], RM = RMw[j / 2];
             const uint32_t sft = 32 * (j & 1);
             f[j] = (gh ^ (uint32_t)(RH >> sft)) | (gl ^ (uint32_t)(RL >> sft)) | gm | (uint32_t)(RM >> sft);

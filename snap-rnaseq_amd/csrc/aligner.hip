@@ -277,7 +277,7 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
                         // allocateNewCandidate (BaseAligner.cpp:1485-1568): tail of weight list 1
                         e = atomicAdd(&S.nElems, 1u);
                         if (e >= (uint32_t)A.arenaElems) {
-                            diag_report(A.diag, DIAG_ARENA, st.rid, e);
+                            if (!A.ovfList) diag_report(A.diag, DIAG_ARENA, st.rid, e);
                             overflow = true;
                             break;
                         }
@@ -321,7 +321,9 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
                 }
             }
         }
-        if (ballot(overflow)) st.abort = 1;   // the watchdog record makes the host call fail
+        // a capped arena hands the read to the big-arena pass (align_one); a worst-case one cannot
+        // fill up, and if it did the watchdog record makes the host call fail
+        if (ballot(overflow)) st.abort = A.ovfList ? 2u : 1u;
         wave_sync();
     }
     st.ts += lim;
@@ -625,6 +627,12 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
         PH_ADD(A, S, PH_SEEDLOOP, tsl);
     }
     PH_T(A, tout);
+    if (st.abort == 2u) {   // outgrew the capped arena: no record here, the big-arena pass aligns it afresh
+        if (lane == 0) A.ovfList[atomicAdd(A.ovfCount, 1u)] = r;
+        wave_sync();
+        PH_ADD(A, S, PH_OUT, tout);
+        return;
+    }
     const uint32_t svLookups = sv_get(st, SV_LOOKUPS), svScored = sv_get(st, SV_SCORED);
     const uint32_t svPopular = sv_get(st, SV_POPULAR), svProbes = sv_get(st, SV_PROBES);
     const uint32_t svHitWords = sv_get(st, SV_HITWORDS), svOvf = sv_get(st, SV_OVF);
@@ -928,8 +936,11 @@ struct ChunkSlot {
 
 struct ExecLane {
     hipStream_t stream = nullptr;
-    void *arena = nullptr;
-    uint32_t *counter = nullptr;               // [0] pass-1 work, [1] pass-3 work, [2] pass-1 defers, [3] pass-2 work, [4] pass-2 defers
+    void *arena = nullptr;                     // main passes: arenaCap elements per wave
+    void *bigArena = nullptr;                  // big-arena pass: arenaElems per wave (only when arenaCap < arenaElems)
+    uint32_t *counter = nullptr;               // [0] pass-1 work, [1] pass-3 work, [2] pass-1 defers, [3] pass-2 work,
+                                               // [4] pass-2 defers, [5] long reads (pass 0), [6] arena overflows,
+                                               // [7] big-arena pass work
     unsigned long long *lookupStats = nullptr; // seed_lookup_kernel: [256][4] seeds, probes, overflow counts (per call)
     hipEvent_t done = nullptr;                 // scratch event: waitLane, cross-lane ordering
     // chunk buffers of the pipelined snapgpu_align_batch (grown on demand)
@@ -970,7 +981,7 @@ struct snapgpu_aligner {
     uint32_t *dSlots = nullptr, *dOverflow = nullptr, *dPieces = nullptr;
     uint64_t *dTableBase = nullptr, *dTableSize = nullptr;
     char *dGenomeAlloc = nullptr;
-    uint4 *dGPlanes = nullptr;    // genome bit planes (KArgs::gpl)
+    GPlane *dGPlanes = nullptr;   // genome bit planes (KArgs::gpl)
     const char *dGenome = nullptr;
     DevTables *dTab = nullptr;
     ExecLane lane[2];
@@ -988,8 +999,9 @@ struct snapgpu_aligner {
     uint64_t chunkSeq = 0;        // submission order of pipelined chunks (finished oldest first)
     hipStream_t copyStream = nullptr;   // H2D of the pipelined chunks
     std::chrono::steady_clock::time_point streamStart;
-    uint64_t arenaElems = 0;
-    int grid = 0, grid256 = 0, grid512 = 0;
+    uint64_t arenaElems = 0;      // worst case per read: (maxSeeds + 2) * maxHits (+ 64)
+    uint64_t arenaCap = 0;        // per wave in the main passes (= arenaElems unless that cannot fit the grid)
+    int grid = 0, grid256 = 0, grid512 = 0, gridBig = 0;
     // snapgpu_align_batch chunk (SNAPGPU_CHUNK_READS): a streaming caller's 1M-read batches go
     // as one chunk each, alternating lanes (fewest persistent-kernel tails; A/B in
     // profiles/r02/ab/chunk_size_slots.txt); resident runs keep 2^18-read chunks over both lanes
@@ -1069,10 +1081,10 @@ __global__ __launch_bounds__(256) void compact_hits_kernel(const snapgpu_multi_h
     }
 }
 
-// Genome bit planes {hi, lo, notACGT, 0} for 32 bases per uint4 (KArgs::gpl), built on the
+// Genome bit planes {hi, lo, notACGT} for 32 bases per 12-B GPlane (KArgs::gpl), built on the
 // device from the uploaded genome bytes: word w covers device-genome bytes [32w, 32w + 32)
 // of the guarded copy (position -kDevGuard at byte 0); bytes past `span` are not ACGT.
-__global__ __launch_bounds__(256) void pack_planes_kernel(const char *g, uint64_t span, uint64_t nWords, uint4 *out) {
+__global__ __launch_bounds__(256) void pack_planes_kernel(const char *g, uint64_t span, uint64_t nWords, sgk::GPlane *out) {
     const uint64_t w = (uint64_t)blockIdx.x * 256u + threadIdx.x;
     if (w >= nWords) return;
     uint32_t hi = 0, lo = 0, nm = 0;
@@ -1085,7 +1097,7 @@ __global__ __launch_bounds__(256) void pack_planes_kernel(const char *g, uint64_
         if (v > 3) nm |= bit;
         else { if (v & 2) hi |= bit; if (v & 1) lo |= bit; }
     }
-    out[w] = make_uint4(hi, lo, nm, 0u);
+    out[w] = sgk::GPlane{hi, lo, nm};
 }
 
 // ------------------------------------------------------------------ host helpers
@@ -1259,7 +1271,7 @@ void snapgpu_aligner_free(snapgpu_aligner_t *a) {
     devFree(a, a->dGPlanes); devFree(a, a->dPhase); devFree(a, a->dDiag);
     for (auto &L : a->lane) {
         freeLaneChunkBuffers(a, L);
-        devFree(a, L.arena); devFree(a, L.counter); devFree(a, L.lookupStats);
+        devFree(a, L.arena); devFree(a, L.bigArena); devFree(a, L.counter); devFree(a, L.lookupStats);
         hostPinnedFree(L.hLookupStats);
         if (L.done) hipEventDestroy(L.done);
         for (ChunkSlot &S : L.slot) {
@@ -1329,12 +1341,12 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
     if (uploadLarge(s0, a->dGenomeAlloc + kDevGuard, idx->genome->bases(), nBases)) { snapgpu_aligner_free(a); return nullptr; }
     a->dGenome = a->dGenomeAlloc + kDevGuard;
     {
-        // genome bit planes {hi, lo, notACGT, 0}, 32 bases per uint4, covering genome
+        // genome bit planes {hi, lo, notACGT}, 32 bases per 12-B GPlane, covering genome
         // positions [-kDevGuard, nBases + kDevGuard): the per-lane LV mismatch masks of
         // align_kernel<128> are built from these with funnel shifts (align_score.h).
         const uint64_t span = (uint64_t)nBases + 2 * kDevGuard;
         const uint64_t nw = (span + 31) / 32 + 8;
-        if ((e = hipMalloc(&a->dGPlanes, nw * 16)) != hipSuccess) return fail("hipMalloc planes", e);
+        if ((e = hipMalloc(&a->dGPlanes, nw * sizeof(GPlane))) != hipSuccess) return fail("hipMalloc planes", e);
         hipLaunchKernelGGL(pack_planes_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s0, a->dGenomeAlloc,
                            span, nw, a->dGPlanes);
         if ((e = hipGetLastError()) != hipSuccess) return fail("pack_planes_kernel", e);
@@ -1373,10 +1385,23 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
     uint32_t maxSeeds = params->maxSeedsToUse ? params->maxSeedsToUse
                                               : (uint32_t)(params->maxSeedCoverage * params->maxReadSize / idx->seedLen);
     a->arenaElems = (uint64_t)(maxSeeds + 2) * params->maxHitsToConsider + 64;
-    const uint64_t budget = 24ull << 30;   // HBM for the arenas of one lane
-    while (a->grid > 64 && (uint64_t)a->grid * a->arenaElems * sizeof(Elem512) > budget) a->grid /= 2;
-    for (auto &L : a->lane)
-        if ((e = hipMalloc(&L.arena, (uint64_t)a->grid * a->arenaElems * sizeof(Elem512))) != hipSuccess) return fail("arena", e);
+    // Element arenas.  The whole grid keeps its occupancy: when worst-case arenas for every wave
+    // would pass the lane's budget (maxHits 16000 of the RNA aligners: 23 MB per wave), the main
+    // passes run on capped arenas and the rare read that outgrows one is aligned again by the
+    // big-arena pass, align_kernel<512> on a small grid of worst-case arenas (KArgs::ovfList).
+    // (Round 2 halved the grid instead: the RNA aligners ran at 1 wave per SIMD.)
+    const uint64_t budget = 8ull << 30, bigBudget = 4ull << 30;   // HBM per lane: main and big-arena pass
+    a->arenaCap = std::min<uint64_t>(a->arenaElems, budget / ((uint64_t)a->grid * sizeof(Elem512)));
+    if (const char *t = getenv("SNAPGPU_ARENA_CAP"); t && atoll(t) >= 64)   // test hook: force the overflow path
+        a->arenaCap = std::min<uint64_t>(a->arenaCap, (uint64_t)atoll(t));
+    if (a->arenaCap < a->arenaElems)
+        a->gridBig = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)a->grid, bigBudget / (a->arenaElems * sizeof(Elem512))));
+    for (auto &L : a->lane) {
+        if ((e = hipMalloc(&L.arena, (uint64_t)a->grid * a->arenaCap * sizeof(Elem512))) != hipSuccess) return fail("arena", e);
+        if (a->gridBig &&
+            (e = hipMalloc(&L.bigArena, (uint64_t)a->gridBig * a->arenaElems * sizeof(Elem512))) != hipSuccess)
+            return fail("big arena", e);
+    }
     int perCU256 = 0;   // passes 2 and 3 (deferred reads) reuse the arenas of the first a->grid blocks
     hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU256, (const void *)align_kernel<256, false>, 64, 0);
     if (perCU256 <= 0) perCU256 = 4;
@@ -1418,7 +1443,7 @@ snapgpu_device_reads_t *snapgpu_reads_upload(snapgpu_aligner_t *a, const snapgpu
     HIPCHKN(hipMalloc(&d->dOffsets, (r->n + 1) * 8));
     HIPCHKN(hipMalloc(&d->dLengths, (r->n + 1) * 4));
     HIPCHKN(hipMalloc(&d->dOut, (r->n + 1) * sizeof(snapgpu_result_t)));
-    HIPCHKN(hipMalloc(&d->dDefer, 2 * (r->n + 1) * sizeof(uint32_t)));   // pass-1 and pass-2 defer lists
+    HIPCHKN(hipMalloc(&d->dDefer, 3 * (r->n + 1) * sizeof(uint32_t)));   // pass-1 / pass-2 defers, arena overflows
     HIPCHKN(hipMalloc(&d->dSeeds, (r->n + 8) * SEEDS_PER_READ * sizeof(SeedRec)));
     HIPCHKN(hipMemsetAsync(d->dBases, 0, bytes, s));
     HIPCHKN(hipMemsetAsync(d->dQuals, 0, bytes, s));
@@ -1465,6 +1490,7 @@ struct PassIO {
     snapgpu_result_t *out;
     uint32_t *defer;    // pass 1 -> pass 2 read list
     uint32_t *defer2;   // pass 2 -> pass 3 read list
+    uint32_t *ovf;      // passes 1-3 -> big-arena pass (reads that outgrew a capped arena)
     SeedRec *seeds;
 };
 
@@ -1496,7 +1522,8 @@ static int launch_passes(snapgpu_aligner_t *a, int li, const PassIO &io, const A
     A.tab = a->dTab;
     A.bases = io.bases; A.quals = io.quals; A.offsets = io.offsets; A.lengths = io.lengths;
     A.nReads = (uint32_t)io.n; A.out = io.out;
-    A.counter = L.counter; A.arena = L.arena; A.arenaElems = a->arenaElems;
+    A.counter = L.counter; A.arena = L.arena; A.arenaElems = a->arenaCap;
+    if (a->arenaCap < a->arenaElems) { A.ovfList = io.ovf; A.ovfCount = L.counter + 6; }
     A.deferList = io.defer; A.deferCount = L.counter + 2; A.readList = nullptr;
     A.search = x.search; A.maxHitsToGet = x.maxHitsToGet;
     A.hitSlot = x.maxHitsToGet < 512 ? x.maxHitsToGet : 512;
@@ -1544,6 +1571,22 @@ static int launch_passes(snapgpu_aligner_t *a, int li, const PassIO &io, const A
     if (ext) hipLaunchKernelGGL((align_kernel<512, true>), dim3(grid2), dim3(64), 0, L.stream, B);
     else hipLaunchKernelGGL((align_kernel<512, false>), dim3(grid2), dim3(64), 0, L.stream, B);
     HIPCHK(hipGetLastError());
+    if (a->gridBig) {
+        // big-arena pass: the reads passes 1-3 abandoned when they outgrew a capped arena, aligned
+        // from scratch by the byte-compare kernel (any read length) on worst-case arenas
+        KArgs V = A;
+        V.counter = L.counter + 7;
+        V.readList = io.ovf; V.readCount = L.counter + 6;
+        V.deferList = nullptr; V.deferCount = nullptr;
+        V.ovfList = nullptr; V.ovfCount = nullptr;
+        V.seedRecs = nullptr;
+        V.arena = L.bigArena; V.arenaElems = a->arenaElems;
+        int gridV = a->gridBig;
+        if ((uint64_t)gridV > io.n) gridV = (int)io.n;
+        if (ext) hipLaunchKernelGGL((align_kernel<512, true>), dim3(gridV), dim3(64), 0, L.stream, V);
+        else hipLaunchKernelGGL((align_kernel<512, false>), dim3(gridV), dim3(64), 0, L.stream, V);
+        HIPCHK(hipGetLastError());
+    }
     HIPCHK(hipEventRecord(ev.e[2], L.stream));
     HIPCHK(hipMemcpyAsync(ev.hCounter, L.counter, 32, hipMemcpyDeviceToHost, L.stream));
     return SNAPGPU_OK;
@@ -1610,6 +1653,7 @@ static int accountEvSet(snapgpu_aligner_t *a, const EvSet &v) {
     a->timing.nLaunches++;
     a->timing.nSpilled += v.hCounter[2];
     a->timing.nByteReads += v.hCounter[4];
+    a->timing.nArenaOverflow += v.hCounter[6];
     return SNAPGPU_OK;
 }
 
@@ -1635,7 +1679,7 @@ static int launch_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, cons
         EvSet *ev = nextEvSet(a);
         if (!ev) return SNAPGPU_EDEVICE;
         PassIO io{d->dBases, d->dQuals, d->dOffsets + b, d->dLengths + b, m, d->dOut + b, d->dDefer + b,
-                  d->dDefer + (n + 1) + b, d->dSeeds + b * SEEDS_PER_READ};
+                  d->dDefer + (n + 1) + b, d->dDefer + 2 * (n + 1) + b, d->dSeeds + b * SEEDS_PER_READ};
         if ((rc = launch_passes(a, (int)(c & 1), io, x, *ev, c ? &a->evs[a->nEvUsed - 2] : nullptr))) return rc;
     }
     a->lastReads = d;
@@ -1746,7 +1790,7 @@ static int ensureLaneCapacity(snapgpu_aligner_t *a, ExecLane &L, uint64_t reads,
         HIPCHK(hipHostMalloc(&S.hLengths, (reads + 1) * 4, hipHostMallocDefault));
         HIPCHK(hipHostMalloc(&S.hOut, (reads + 1) * sizeof(snapgpu_result_t), hipHostMallocDefault));
     }
-    HIPCHK(hipMalloc(&L.dDefer, 2 * (reads + 1) * 4));   // pass-1 and pass-2 defer lists
+    HIPCHK(hipMalloc(&L.dDefer, 3 * (reads + 1) * 4));   // pass-1 / pass-2 defers, arena overflows
     HIPCHK(hipMalloc(&L.dOut, (reads + 1) * sizeof(snapgpu_result_t)));
     HIPCHK(hipMalloc(&L.dSeeds, (reads + 8) * SEEDS_PER_READ * sizeof(SeedRec)));
     L.capReads = reads;
@@ -1895,7 +1939,8 @@ int snapgpu_align_batch_submit(snapgpu_aligner_t *a, const snapgpu_reads_t *read
         HIPBRK(hipMemcpyAsync(S.dLengths, S.hLengths, m * 4, hipMemcpyHostToDevice, cs));
         HIPBRK(hipEventRecord(S.h2d, cs));
         HIPBRK(hipStreamWaitEvent(s, S.h2d, 0));
-        PassIO io{S.dBases, S.dQuals, S.dOffsets, S.dLengths, m, L.dOut, L.dDefer, L.dDefer + (L.capReads + 1), L.dSeeds};
+        PassIO io{S.dBases, S.dQuals, S.dOffsets, S.dLengths, m, L.dOut, L.dDefer, L.dDefer + (L.capReads + 1),
+                  L.dDefer + 2 * (L.capReads + 1), L.dSeeds};
         EvSet *ev = nextEvSet(a);
         if (!ev) { rc = SNAPGPU_EDEVICE; break; }
         if ((rc = launch_passes(a, li, io, AlignExt(), *ev, a->nEvUsed >= 2 ? &a->evs[a->nEvUsed - 2] : nullptr))) break;

@@ -308,9 +308,9 @@ __device__ void score_location(const PArgs &P, PLds<MAXLEN> &S, int r, int dir, 
         // lane l holds diagonal x = l - 31: F_x[m] = read[m] != genome[loc + x + m] from the genome
         // and read bit planes (as lv_pass, align_score.h); bytes past the read are not ACGT
         const int64_t gp = (int64_t)loc + (lane - 31) + PACK_GUARD;
-        const uint4 *src = X.gpl + (gp >> 5);
+        const GPlane *src = X.gpl + (gp >> 5);
         const uint32_t sh = (uint32_t)gp & 31;
-        uint4 w[2 * NB + 1];
+        GPlane w[2 * NB + 1];
 #pragma unroll
         for (int j = 0; j < 2 * NB + 1; j++) w[j] = src[j];
         const uint64_t(*rp)[PLds<MAXLEN>::PW] = S.rpl[r][dir];
@@ -320,9 +320,9 @@ __device__ void score_location(const PArgs &P, PLds<MAXLEN> &S, int r, int dir, 
 #pragma unroll
             for (int h = 0; h < 2; h++) {
                 const int j = 2 * b + h;
-                const uint32_t gh = __builtin_amdgcn_alignbit(w[j + 1].x, w[j].x, sh);
-                const uint32_t gl = __builtin_amdgcn_alignbit(w[j + 1].y, w[j].y, sh);
-                const uint32_t gm = __builtin_amdgcn_alignbit(w[j + 1].z, w[j].z, sh);
+                const uint32_t gh = __builtin_amdgcn_alignbit(w[j + 1].hi, w[j].hi, sh);
+                const uint32_t gl = __builtin_amdgcn_alignbit(w[j + 1].lo, w[j].lo, sh);
+                const uint32_t gm = __builtin_amdgcn_alignbit(w[j + 1].nm, w[j].nm, sh);
                 const uint32_t sft = 32 * h;
                 f[h] = (gh ^ (uint32_t)(rp[0][b] >> sft)) | (gl ^ (uint32_t)(rp[1][b] >> sft)) | gm | (uint32_t)(rp[2][b] >> sft);
             }

@@ -156,6 +156,7 @@ class Timing(C.Structure):
         ("mainKernelBusyMs", C.c_double),
         ("lookupKernelBusyMs", C.c_double),
         ("nByteReads", C.c_uint64),
+        ("nArenaOverflow", C.c_uint64),
     ]
 
 

@@ -161,3 +161,18 @@ def test_gpu_mh1000_aliasing_matches_reference(repeat_index):
     got = canonical_tsv_ex(res, found, hits)
     want = open(os.path.join(G, "expected_repeat_mh1000.tsv")).read()
     assert got == want, _first_diff(got, want)
+
+
+@pytest.mark.gpu
+def test_gpu_mh1000_arena_overflow_matches_reference(repeat_index, monkeypatch):
+    """The multi-hit path (align_kernel<*, true>) through the big-arena pass: with 256-element
+    arenas in passes 1-3 the repeat reads outgrow them, are aligned again on worst-case arenas,
+    and the hits still equal the reference's."""
+    monkeypatch.setenv("SNAPGPU_ARENA_CAP", "256")
+    reads = snapgpu.Reads.from_fastq(os.path.join(G, "repeat_reads.fq"))
+    al = snapgpu.BaseAligner(repeat_index, **REPEAT_KW)
+    res, found, hits = al.AlignReadsEx(reads, None, 1000)
+    assert al.timing()["nArenaOverflow"] > 0
+    got = canonical_tsv_ex(res, found, hits)
+    want = open(os.path.join(G, "expected_repeat_mh1000.tsv")).read()
+    assert got == want, _first_diff(got, want)
