@@ -1028,6 +1028,13 @@ struct snapgpu_aligner {
     // snapgpu_align_batch_ex buffers, kept across calls (grow-only): search windows, multi-hit
     // scratch per block, found counts, hit rows, compaction offsets and the packed hits
     struct ExBuf { void *p = nullptr; uint64_t cap = 0; } exSearch, exScratch, exFound, exHits, exOff, exDense;
+    // snapgpu_cigar_batch (device inputs, device outputs, pinned staging of the packed inputs) and
+    // the internal scratch slots of snapgpu_internal_devbuf (charseeds.hip), grow-only: a
+    // hipMalloc / hipFree pair per call cost more than the kernels, and hipFree waits for the
+    // whole device (the RNA path's other host thread included)
+    ExBuf cgIn, cgOut, aux[8];
+    void *cgPin = nullptr;
+    uint64_t cgPinCap = 0;
     hipStream_t stream() const { return lane[0].stream; }
 };
 
@@ -1286,6 +1293,9 @@ void snapgpu_aligner_free(snapgpu_aligner_t *a) {
         hostPinnedFree(v.hCounter);
     }
     for (auto &e : a->cev) if (e) hipEventDestroy(e);
+    for (auto *b : {&a->cgIn, &a->cgOut}) devFree(a, b->p);
+    for (auto &b : a->aux) devFree(a, b.p);
+    hostPinnedFree(a->cgPin);
     for (auto *b : {&a->exSearch, &a->exScratch, &a->exFound, &a->exHits, &a->exOff, &a->exDense}) devFree(a, b->p);
     delete a;
 }
@@ -1392,7 +1402,7 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
     // (Round 2 halved the grid instead: the RNA aligners ran at 1 wave per SIMD.)
     const uint64_t budget = 8ull << 30, bigBudget = 4ull << 30;   // HBM per lane: main and big-arena pass
     a->arenaCap = std::min<uint64_t>(a->arenaElems, budget / ((uint64_t)a->grid * sizeof(Elem512)));
-    if (const char *t = getenv("SNAPGPU_ARENA_CAP"); t && atoll(t) >= 64)   // test hook: force the overflow path
+    if (const char *t = getenv("SNAPGPU_ARENA_CAP"); t && atoll(t) >= 1)   // test hook: force the overflow path
         a->arenaCap = std::min<uint64_t>(a->arenaCap, (uint64_t)atoll(t));
     if (a->arenaCap < a->arenaElems)
         a->gridBig = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)a->grid, bigBudget / (a->arenaElems * sizeof(Elem512))));
@@ -2313,6 +2323,25 @@ static CigarArgs cigar_args(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, int
     return C;
 }
 
+// cigar_kernel over n reads on the aligner's stream (timing events around it)
+static int cigar_kernel_launch(snapgpu_aligner_t *a, const CigarArgs &C, uint64_t n) {
+    if (!a->cigarGrid) {
+        hipDeviceProp_t prop;
+        HIPCHK(hipGetDeviceProperties(&prop, a->device));
+        int perCU = 0;
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, (const void *)cigar_kernel, 64, 0);
+        a->cigarGrid = prop.multiProcessorCount * (perCU > 0 ? perCU : 8);
+    }
+    int grid = a->cigarGrid;
+    if ((uint64_t)grid > n) grid = (int)n;
+    if (grid == 0) return SNAPGPU_OK;
+    HIPCHK(hipEventRecord(a->cev[0], a->stream()));
+    hipLaunchKernelGGL(cigar_kernel, dim3(grid), dim3(64), 0, a->stream(), C);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(a->cev[1], a->stream()));
+    return SNAPGPU_OK;
+}
+
 static int cigar_launch(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, CigarArgs C) {
     if (d->maxLen > (uint32_t)CIG_MAXLEN) { snapgpu::setError("cigar: read longer than 512 bases"); return SNAPGPU_EINVAL; }
     if (d->n > 0xffffffffull) { snapgpu::setError("batch too large"); return SNAPGPU_EINVAL; }
@@ -2322,21 +2351,7 @@ static int cigar_launch(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, CigarAr
         HIPCHK(hipMalloc(&d->dCigOps, (d->n + 1) * CIG_MAX_OPS * 4));
     }
     C.outEd = d->dCigEd; C.outNOps = d->dCigN; C.outOps = d->dCigOps;
-    if (!a->cigarGrid) {
-        hipDeviceProp_t prop;
-        HIPCHK(hipGetDeviceProperties(&prop, a->device));
-        int perCU = 0;
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, (const void *)cigar_kernel, 64, 0);
-        a->cigarGrid = prop.multiProcessorCount * (perCU > 0 ? perCU : 8);
-    }
-    int grid = a->cigarGrid;
-    if ((uint64_t)grid > d->n) grid = (int)d->n;
-    if (grid == 0) return SNAPGPU_OK;
-    HIPCHK(hipEventRecord(a->cev[0], a->stream()));
-    hipLaunchKernelGGL(cigar_kernel, dim3(grid), dim3(64), 0, a->stream(), C);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(a->cev[1], a->stream()));
-    return SNAPGPU_OK;
+    return cigar_kernel_launch(a, C, d->n);
 }
 
 int snapgpu_cigar_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, int useM) {
@@ -2375,29 +2390,85 @@ int snapgpu_cigar_last_ms(snapgpu_aligner_t *a, double *ms) {
 int snapgpu_cigar_batch(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, const uint32_t *locations,
                         const uint8_t *directions, int useM, int32_t *editDistance, uint32_t *nOps, uint32_t *ops) {
     if (!a || !reads || !locations || !directions || !editDistance || !nOps || !ops) return SNAPGPU_EINVAL;
+    if (a->failed) { snapgpu::setError("aligner failed earlier (device timeout)"); return SNAPGPU_EDEVICE; }
+    const uint64_t n = reads->n;
+    if (n == 0) return SNAPGPU_OK;
+    if (n > 0xffffffffull) { snapgpu::setError("batch too large"); return SNAPGPU_EINVAL; }
     HIPCHK(hipSetDevice(a->device));
-    snapgpu_device_reads_t *d = snapgpu_reads_upload(a, reads);
-    if (!d) return SNAPGPU_EDEVICE;
-    uint32_t *dLoc = nullptr;
-    uint8_t *dDir = nullptr;
-    int rc = SNAPGPU_OK;
-    if (hipMalloc(&dLoc, (reads->n + 1) * 4) != hipSuccess || hipMalloc(&dDir, reads->n + 1) != hipSuccess) {
-        snapgpu::setError("cigar_batch: hipMalloc");
-        rc = SNAPGPU_ENOMEM;
+    // one packed upload: the reads' bases back to back (the caller's batch view may point into a
+    // much larger buffer), offsets, lengths, locations, directions; no qualities (CIGARs use none)
+    uint64_t total = 0;
+    uint32_t maxLen = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        total += reads->lengths[i];
+        maxLen = std::max(maxLen, reads->lengths[i]);
     }
-    if (!rc && reads->n) {
-        hipMemcpy(dLoc, locations, reads->n * 4, hipMemcpyHostToDevice);
-        hipMemcpy(dDir, directions, reads->n, hipMemcpyHostToDevice);
-        CigarArgs C = cigar_args(a, d, useM);
-        C.locations = dLoc;
-        C.directions = dDir;
-        rc = cigar_launch(a, d, C);
-        if (!rc) rc = snapgpu_cigar_download(a, d, editDistance, nOps, ops);
+    if (maxLen > (uint32_t)CIG_MAXLEN) { snapgpu::setError("cigar: read longer than 512 bases"); return SNAPGPU_EINVAL; }
+    auto al8 = [](uint64_t x) { return (x + 7) & ~7ull; };
+    const uint64_t oOff = 0, oLen = al8(oOff + (n + 1) * 8), oLoc = al8(oLen + (n + 1) * 4), oDir = al8(oLoc + (n + 1) * 4),
+                   oBases = al8(oDir + n + 1), inBytes = al8(oBases + total + 64);
+    const uint64_t rEd = 0, rN = al8((n + 1) * 4), rOps = al8(rN + (n + 1) * 4), outBytes = rOps + (n + 1) * CIG_MAX_OPS * 4;
+    auto ensure = [a](snapgpu_aligner::ExBuf &b, uint64_t bytes) -> hipError_t {
+        if (bytes <= b.cap) return hipSuccess;
+        devFree(a, b.p);
+        b.p = nullptr;
+        b.cap = 0;
+        const uint64_t want = bytes + bytes / 4 + 256;
+        hipError_t e = hipMalloc(&b.p, want);
+        if (e == hipSuccess) b.cap = want;
+        return e;
+    };
+    HIPCHK(ensure(a->cgIn, inBytes));
+    HIPCHK(ensure(a->cgOut, outBytes));
+    if (inBytes > a->cgPinCap) {
+        hostPinnedFree(a->cgPin);
+        a->cgPin = nullptr;
+        a->cgPinCap = 0;
+        const uint64_t want = inBytes + inBytes / 4 + 256;
+        HIPCHK(hipHostMalloc(&a->cgPin, want, hipHostMallocDefault));
+        a->cgPinCap = want;
     }
-    hipFree(dLoc);
-    hipFree(dDir);
-    snapgpu_device_reads_free(d);
-    return rc;
+    char *h = (char *)a->cgPin;
+    uint64_t *hOff = (uint64_t *)(h + oOff);
+    uint64_t at = 0;
+    for (uint64_t i = 0; i < n; i++) { hOff[i] = at; at += reads->lengths[i]; }
+    hOff[n] = at;
+    memcpy(h + oLen, reads->lengths, n * 4);
+    memcpy(h + oLoc, locations, n * 4);
+    memcpy(h + oDir, directions, n);
+    {
+        // pack the bases (several threads for big batches: the copy is the host's part of the call)
+        const unsigned nt = n < 16384 ? 1u : std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+        auto pack = [&](uint64_t b, uint64_t e) {
+            for (uint64_t i = b; i < e; i++) memcpy(h + oBases + hOff[i], reads->bases + reads->offsets[i], reads->lengths[i]);
+        };
+        std::vector<std::thread> th;
+        for (unsigned t = 1; t < nt; t++) th.emplace_back(pack, n * t / nt, n * (t + 1) / nt);
+        pack(0, n / nt);
+        for (auto &x : th) x.join();
+        memset(h + oBases + total, 0, inBytes - oBases - total);
+    }
+    hipStream_t st = a->stream();
+    char *dIn = (char *)a->cgIn.p, *dOut = (char *)a->cgOut.p;
+    HIPCHK(hipMemcpyAsync(dIn, h, inBytes, hipMemcpyHostToDevice, st));
+    CigarArgs C;
+    memset(&C, 0, sizeof(C));
+    const snapgpu_index_t *idx = a->idx;
+    C.genome = a->dGenome; C.pieces = a->dPieces; C.nPieces = (int32_t)idx->genome->pieceOffsets.size();
+    C.nBases = idx->genome->nBases; C.padding = idx->genome->chromosomePadding;
+    C.bases = dIn + oBases; C.offsets = (const uint64_t *)(dIn + oOff); C.lengths = (const uint32_t *)(dIn + oLen);
+    C.nReads = (uint32_t)n;
+    C.locations = (const uint32_t *)(dIn + oLoc);
+    C.directions = (const uint8_t *)(dIn + oDir);
+    C.useM = useM ? 1 : 0;
+    C.outEd = (int32_t *)(dOut + rEd); C.outNOps = (uint32_t *)(dOut + rN); C.outOps = (uint32_t *)(dOut + rOps);
+    int rc = cigar_kernel_launch(a, C, n);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(editDistance, dOut + rEd, n * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(nOps, dOut + rN, n * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(ops, dOut + rOps, n * CIG_MAX_OPS * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return SNAPGPU_OK;
 }
 
 int snapgpu_gather_peak(snapgpu_aligner_t *a, uint32_t nLoads, double *ms) {
@@ -2457,6 +2528,23 @@ int snapgpu_copy_peak(snapgpu_aligner_t *a, uint64_t bytes, double *ms) {
 // ------------------------------------------------- internal hand-off to paired.hip
 // The paired-end aligner (paired.hip) runs over the index one snapgpu_aligner uploaded (the one
 // its chimeric fallback uses): the index, genome and table arguments of its kernels.
+int snapgpu_internal_devbuf(snapgpu_aligner_t *a, int slot, uint64_t bytes, void **p) {
+    if (!a || slot < 0 || slot >= 8 || !p) return SNAPGPU_EINVAL;
+    if (a->failed) return SNAPGPU_EDEVICE;
+    auto &b = a->aux[slot];
+    if (bytes > b.cap) {
+        devFree(a, b.p);
+        b.p = nullptr;
+        b.cap = 0;
+        const uint64_t want = bytes + bytes / 4 + 256;
+        if (hipMalloc(&b.p, want) != hipSuccess) return SNAPGPU_ENOMEM;
+        b.cap = want;
+    }
+    *p = b.p;
+    return SNAPGPU_OK;
+}
+hipStream_t snapgpu_internal_stream(snapgpu_aligner_t *a) { return a->stream(); }
+
 int snapgpu_internal_index_args(const snapgpu_aligner_t *a, sgk::KArgs *A, int *device) {
     if (!a || !A) return SNAPGPU_EINVAL;
     memset(A, 0, sizeof(*A));

@@ -28,6 +28,8 @@
 #include "internal.h"
 
 int snapgpu_internal_index_args(const snapgpu_aligner_t *a, sgk::KArgs *A, int *device);
+int snapgpu_internal_devbuf(snapgpu_aligner_t *a, int slot, uint64_t bytes, void **p);   // grow-only, the aligner's
+hipStream_t snapgpu_internal_stream(snapgpu_aligner_t *a);
 
 namespace sgk {
 namespace cs {
@@ -335,29 +337,37 @@ snapgpu_seed_runs_t *snapgpu_characterize_seeds(snapgpu_aligner_t *a, const snap
     uint32_t *dL = nullptr, *dList = nullptr, *dCnt = nullptr;
     Run *dPool = nullptr;
     ReadRec *dRec = nullptr;
+    // device buffers: the aligner's grow-only scratch slots (a hipMalloc / hipFree per call, the
+    // pool up to 3 GB, cost more than the kernel and hipFree waits for the whole device)
+    auto buf = [&](int slot, uint64_t bytes, auto *&ptr) -> hipError_t {
+        void *v = nullptr;
+        if (snapgpu_internal_devbuf(a, slot, bytes, &v)) return hipErrorOutOfMemory;
+        ptr = reinterpret_cast<std::remove_reference_t<decltype(ptr)>>(v);
+        return hipSuccess;
+    };
     const uint64_t perRead = (uint64_t)(p->numSeeds + 1) * p->maxHits;
     const uint64_t CH = 65536;   // reads per launch: pool <= 65536 * 3900 * 12 B = 3 GB
     uint64_t total = 0;
     int grid = 0;
     rc = SNAPGPU_OK;
     CCHK(hipSetDevice(device));
-    CCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    s = snapgpu_internal_stream(a);
     {
         int ncu = 0;
         CCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
         grid = ncu * 4;   // 33 KB LDS per wave: 4 waves per CU
     }
-    CCHK(hipMalloc(&dB, reads->totalBytes + 1024));
+    CCHK(buf(0, reads->totalBytes + 1024, dB));
     CCHK(hipMemsetAsync(dB + reads->totalBytes, 0, 1024, s));
     CCHK(hipMemcpyAsync(dB, reads->bases, reads->totalBytes, hipMemcpyHostToDevice, s));
-    CCHK(hipMalloc(&dO, reads->n * 8 + 8));
-    CCHK(hipMalloc(&dL, reads->n * 4 + 4));
+    CCHK(buf(1, reads->n * 8 + 8, dO));
+    CCHK(buf(2, reads->n * 4 + 4, dL));
     CCHK(hipMemcpyAsync(dO, reads->offsets, reads->n * 8, hipMemcpyHostToDevice, s));
     CCHK(hipMemcpyAsync(dL, reads->lengths, reads->n * 4, hipMemcpyHostToDevice, s));
-    CCHK(hipMalloc(&dCnt, 16));
-    CCHK(hipMalloc(&dList, CH * 4));
-    CCHK(hipMalloc(&dRec, CH * sizeof(ReadRec)));
-    CCHK(hipMalloc(&dPool, std::min(CH, n ? n : 1) * perRead * sizeof(Run)));
+    CCHK(buf(3, 16, dCnt));
+    CCHK(buf(4, CH * 4, dList));
+    CCHK(buf(5, CH * sizeof(ReadRec), dRec));
+    CCHK(buf(6, std::min(CH, n ? n : 1) * perRead * sizeof(Run), dPool));
     recs.resize(CH);
     for (uint64_t c0 = 0; c0 < n; c0 += CH) {
         const uint64_t m = std::min(CH, n - c0);
@@ -418,14 +428,7 @@ snapgpu_seed_runs_t *snapgpu_characterize_seeds(snapgpu_aligner_t *a, const snap
         out->start[n] = at;
     }
 done:
-    if (dB) (void)hipFree(dB);
-    if (dO) (void)hipFree(dO);
-    if (dL) (void)hipFree(dL);
-    if (dList) (void)hipFree(dList);
-    if (dCnt) (void)hipFree(dCnt);
-    if (dPool) (void)hipFree(dPool);
-    if (dRec) (void)hipFree(dRec);
-    if (s) (void)hipStreamDestroy(s);
+    if (rc && s) (void)hipStreamSynchronize(s);   // nothing of this call left in flight on the scratch
     if (rc) { snapgpu_seed_runs_free(out); return nullptr; }
     return out;
 }

@@ -351,7 +351,7 @@ struct RnaSub {
     std::vector<FilterState> fs;              // per useful pair
     std::vector<GtfPairQuery> cq;             // count events (pointing into fs), input order
     std::vector<PairOut> po;                  // per pair of [a, b)
-    std::string part;                         // the SAM lines / BAM records of [a, b)
+    std::vector<std::string> parts;           // the SAM lines / BAM records of [a, b), in order
     uint64_t single = 0, multi = 0, notFound = 0, partialPairs = 0, partialMatches = 0, seedRuns = 0;
     uint64_t transcriptomeRecords = 0;
     double alignMs = 0, filterMs = 0, seedMs = 0, countMs = 0, cigarMs = 0, writeMs = 0;
@@ -521,14 +521,15 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
     struct CigarSet {
         std::vector<int64_t> slot;   // record -> row in ed/nOps/ops, -1: no location
         std::vector<uint64_t> off;
-        std::vector<uint32_t> len, loc, nOps, ops;
+        std::vector<uint32_t> len, loc, nOps;
+        std::unique_ptr<uint32_t[]> ops;   // [rows][SNAPGPU_CIGAR_MAX_OPS], every row written by the download
         std::vector<uint8_t> dir;
         std::vector<int32_t> ed;
         int32_t edOf(uint64_t i) const { return slot[i] >= 0 ? ed[slot[i]] : -1; }
         uint32_t nOpsOf(uint64_t i) const { return slot[i] >= 0 ? nOps[slot[i]] : 0u; }
         const uint32_t *opsOf(uint64_t i) const {
             static const uint32_t kNone[1] = {0};
-            return slot[i] >= 0 ? ops.data() + slot[i] * SNAPGPU_CIGAR_MAX_OPS : kNone;
+            return slot[i] >= 0 ? ops.get() + slot[i] * SNAPGPU_CIGAR_MAX_OPS : kNone;
         }
         void add(uint64_t i, uint64_t o, uint32_t ln, uint32_t l, uint8_t d) {
             slot[i] = (int64_t)loc.size();
@@ -541,12 +542,12 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
             const uint64_t cnt = loc.size();
             ed.assign(cnt + 1, -1);
             nOps.assign(cnt + 1, 0);
-            ops.resize((cnt + 1) * SNAPGPU_CIGAR_MAX_OPS);
+            ops.reset(new uint32_t[(cnt + 1) * SNAPGPU_CIGAR_MAX_OPS]);
             if (!cnt) return SNAPGPU_OK;
             snapgpu_reads_t *v = snapgpu_reads_from_arrays(cnt, r->bases, r->quals, off.data(), len.data());
             if (!v) return SNAPGPU_ENOMEM;
             std::lock_guard<std::mutex> lk(m);
-            const int rc = snapgpu_cigar_batch(a, v, loc.data(), dir.data(), useM, ed.data(), nOps.data(), ops.data());
+            const int rc = snapgpu_cigar_batch(a, v, loc.data(), dir.data(), useM, ed.data(), nOps.data(), ops.get());
             snapgpu_reads_free(v);
             return rc;
         }
@@ -702,10 +703,7 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
             return;
         }
     for (unsigned t = 0; t < ntd; t++) { X.single += cnt[3 * t]; X.multi += cnt[3 * t + 1]; X.notFound += cnt[3 * t + 2]; }
-    size_t tot = 0;
-    for (auto &p : parts) tot += p.size();
-    X.part.reserve(tot);
-    for (auto &p : parts) X.part += p;
+    X.parts.swap(parts);
     X.writeMs = msSince(t0);
 }
 
@@ -884,11 +882,13 @@ int snapgpu_rna_paired_align(snapgpu_paired_aligner_t *pa, snapgpu_aligner_t *ta
             const std::string bh = bamHeader(*gi->genome, hdr);
             ok = bgzfWrite(f, bh.data(), bh.size(), false);
             std::string all;
-            for (auto &x : subs) all += x->part;
+            for (auto &x : subs)
+                for (auto &p : x->parts) all += p;
             ok = ok && bgzfWrite(f, all.data(), all.size(), true);
         } else {
             ok = fwrite(hdr.data(), 1, hdr.size(), f) == hdr.size();
-            for (auto &x : subs) ok = ok && fwrite(x->part.data(), 1, x->part.size(), f) == x->part.size();
+            for (auto &x : subs)
+                for (auto &p : x->parts) ok = ok && fwrite(p.data(), 1, p.size(), f) == p.size();
         }
         ok = (fclose(f) == 0) && ok;
         if (!ok) { setError(std::string("write failed: ") + samPath); return SNAPGPU_EIO; }

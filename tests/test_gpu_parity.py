@@ -183,9 +183,9 @@ def test_forced_radix_order_vs_oracle(gpu_available, small_world, monkeypatch, k
 def test_arena_overflow_pass_vs_oracle(gpu_available, small_world, monkeypatch, kw):
     """Capped element arenas (snapgpu_aligner_create, KArgs::ovfList): a read that outgrows its
     arena in passes 1-3 is abandoned and aligned again from scratch by the big-arena pass
-    (align_kernel<512> on worst-case arenas).  Forced here with a 64-element cap: every output
+    (align_kernel<512> on worst-case arenas).  Forced here with a 4-element cap: every output
     still equals the oracle."""
-    monkeypatch.setenv("SNAPGPU_ARENA_CAP", "64")
+    monkeypatch.setenv("SNAPGPU_ARENA_CAP", "4")
     idx = small_world["index"]
     reads = snapgpu.Reads.from_list(edge_reads(small_world["genome"]) + [
         small_world["reads"].get(i) for i in range(3000)])
@@ -195,4 +195,4 @@ def test_arena_overflow_pass_vs_oracle(gpu_available, small_world, monkeypatch, 
     cpu = oracle_align(idx, reads, al.params)
     bad = mismatches(gpu, cpu)
     assert len(bad) == 0, f"{len(bad)} of {len(gpu)} differ\n" + _report(gpu, cpu, reads, bad)
-    assert t["nArenaOverflow"] == int((gpu["nElements"] > 64).sum()) > 20   # the overflowing reads took the big pass
+    assert t["nArenaOverflow"] == int((gpu["nElements"] > 4).sum()) > 20   # the overflowing reads took the big pass
