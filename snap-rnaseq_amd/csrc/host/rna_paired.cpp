@@ -145,16 +145,15 @@ void addAlignment(const Ctx &C, AlignmentMap &mate0, AlignmentMap &mate1, uint32
         }
     }
     if (pos == 0) return;
-    Alignment a;
-    a.location = location; a.direction = direction; a.score = score; a.mapq = mapq; a.rname = rname;
-    a.pos = pos; a.posEnd = posEnd; a.posOriginal = posOriginal; a.isTranscriptome = isT;
-    a.transcriptId = tid; a.geneId = gid;
     AlignmentMap &m = isMate0 ? mate0 : mate1;
-    const std::string key = rname + '_' + std::to_string(pos);
+    std::string key = rname + '_' + std::to_string(pos);
     auto it = m.find(key);
-    if (it == m.end()) m.insert({key, a});
-    else if (a.score < it->second.score) it->second = a;
-    else if (a.score == it->second.score && a.isTranscriptome) it->second = a;
+    // replaced only by a lower score, or an equal transcriptome score (the element stays put)
+    if (it != m.end() && !(score < it->second.score || (score == it->second.score && isT))) return;
+    Alignment &a = it != m.end() ? it->second : m.emplace(std::move(key), Alignment()).first->second;
+    a.location = location; a.direction = direction; a.score = score; a.mapq = mapq; a.rname = std::move(rname);
+    a.pos = pos; a.posEnd = posEnd; a.posOriginal = posOriginal; a.isTranscriptome = isT;
+    a.transcriptId = std::move(tid); a.geneId = std::move(gid);
 }
 
 bool checkBoundary(const Ctx &C, const std::string &geneId, const std::string &chr, uint32_t pos, Err &err) {

@@ -253,3 +253,21 @@ def test_gpu_clipped_sam_matches_reference(gpu_available, small, use_m):
     want = _clipped_lines(use_m)
     bad = [(a, b) for a, b in zip(got, want) if a != b]
     assert len(got) == len(want) and not bad, f"{len(bad)} differ: {bad[:2]}"
+
+
+@pytest.mark.gpu
+def test_gpu_cigar_batch_views_and_buffer_reuse(gpu_available, small_world):
+    """snapgpu_cigar_batch packs the listed reads into the aligner's grow-only buffers: batch views
+    into a larger read buffer (slices), calls of growing and shrinking sizes and useM switches give
+    the rows a single whole-batch call gives."""
+    idx, reads = small_world["index"], small_world["reads"]
+    res = oracle_align(idx, reads, snapgpu.default_params())
+    loc, dirs = snapgpu.cigar_inputs(res)
+    al = snapgpu.BaseAligner(idx)
+    for use_m in (0, 1):
+        whole = al.Cigars(reads, loc, dirs, useM=use_m)
+        for s, c in ((1000, 37), (0, 3000), (2999, 1), (5, reads.n - 5), (123, 456)):
+            part = al.Cigars(reads.slice(s, c), loc[s:s + c], dirs[s:s + c], useM=use_m)
+            assert np.array_equal(part.editDistance, whole.editDistance[s:s + c])
+            assert np.array_equal(part.nOps, whole.nOps[s:s + c])
+            assert np.array_equal(part.ops, whole.ops[s:s + c])
