@@ -1033,6 +1033,11 @@ struct snapgpu_aligner {
     // hipMalloc / hipFree pair per call cost more than the kernels, and hipFree waits for the
     // whole device (the RNA path's other host thread included)
     ExBuf cgIn, cgOut, aux[8];
+    // snapgpu_internal_align_batch_packed: its device reads, kept (grow-only) across calls -- a
+    // snapgpu_reads_upload / _free per call is ten hipMalloc / hipFree pairs, and each hipFree waits
+    // for the whole device, the RNA path's concurrent genome aligner included
+    snapgpu_device_reads_t *exReads = nullptr;
+    uint64_t exReadsCapN = 0, exReadsCapBytes = 0;
     void *cgPin = nullptr;
     uint64_t cgPinCap = 0;
     hipStream_t stream() const { return lane[0].stream; }
@@ -1296,6 +1301,7 @@ void snapgpu_aligner_free(snapgpu_aligner_t *a) {
     for (auto *b : {&a->cgIn, &a->cgOut}) devFree(a, b->p);
     for (auto &b : a->aux) devFree(a, b.p);
     hostPinnedFree(a->cgPin);
+    snapgpu_device_reads_free(a->exReads);
     for (auto *b : {&a->exSearch, &a->exScratch, &a->exFound, &a->exHits, &a->exOff, &a->exDense}) devFree(a, b->p);
     delete a;
 }
@@ -1997,6 +2003,53 @@ int snapgpu_align_batch(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, snap
     return snapgpu_align_batch_wait(a);
 }
 
+// The reads of a snapgpu_internal_align_batch_packed call in the aligner's own grow-only device
+// reads (what snapgpu_reads_upload allocates per call), uploaded on the aligner's stream.
+static snapgpu_device_reads_t *uploadCachedReads(snapgpu_aligner_t *a, const snapgpu_reads_t *r) {
+    uint64_t bytes = 0;
+    uint32_t maxLen = 0;
+    for (uint64_t i = 0; i < r->n; i++) {
+        bytes = std::max<uint64_t>(bytes, r->offsets[i] + r->lengths[i]);
+        maxLen = std::max(maxLen, r->lengths[i]);
+    }
+    bytes += 64;
+    if (!a->exReads || r->n > a->exReadsCapN || bytes > a->exReadsCapBytes) {
+        snapgpu_device_reads_free(a->exReads);
+        a->exReads = nullptr;
+        a->exReadsCapN = a->exReadsCapBytes = 0;
+        auto *d = new snapgpu_device_reads_t();
+        d->owner = a;
+        d->device = a->device;
+        const uint64_t capN = r->n + r->n / 4 + 64, capB = bytes + bytes / 4 + 4096;
+        bool ok = hipMalloc(&d->dBases, capB) == hipSuccess && hipMalloc(&d->dQuals, capB) == hipSuccess &&
+                  hipMalloc(&d->dOffsets, (capN + 1) * 8) == hipSuccess && hipMalloc(&d->dLengths, (capN + 1) * 4) == hipSuccess &&
+                  hipMalloc(&d->dOut, (capN + 1) * sizeof(snapgpu_result_t)) == hipSuccess &&
+                  hipMalloc(&d->dDefer, 3 * (capN + 1) * sizeof(uint32_t)) == hipSuccess &&
+                  hipMalloc(&d->dSeeds, (capN + 8) * SEEDS_PER_READ * sizeof(SeedRec)) == hipSuccess;
+        if (!ok) { snapgpu_device_reads_free(d); snapgpu::setError("reads_upload: hipMalloc"); return nullptr; }
+        a->exReads = d;
+        a->exReadsCapN = capN;
+        a->exReadsCapBytes = capB;
+    }
+    snapgpu_device_reads_t *d = a->exReads;
+    d->n = r->n;
+    d->maxLen = maxLen;
+    const_cast<snapgpu_reads_t *>(r)->nUploads++;   // clipping is refused from now on
+    hipStream_t s = a->stream();
+    // the deferred lists are laid out by the batch size (launch_resident): 3 * (n + 1) entries
+    if (hipMemcpyAsync(d->dBases, r->bases, bytes - 64, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemsetAsync(d->dBases + bytes - 64, 0, 64, s) != hipSuccess ||
+        hipMemcpyAsync(d->dQuals, r->quals, bytes - 64, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemsetAsync(d->dQuals + bytes - 64, 0, 64, s) != hipSuccess ||
+        hipMemcpyAsync(d->dOffsets, r->offsets, r->n * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(d->dLengths, r->lengths, r->n * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+        snapgpu::setError("reads_upload: copy");
+        return nullptr;
+    }
+    return d;
+}
+
 // The extended AlignRead over a batch with the multi-hits returned packed: read i's hits are
 // packed[off[i] .. off[i+1]) (off has n + 1 entries).  snapgpu_align_batch_ex scatters them into
 // the caller's rows; the RNA path reads them packed (a row layout of 1000 hits per read would
@@ -2022,7 +2075,7 @@ extern "C++" int snapgpu_internal_align_batch_packed(snapgpu_aligner_t *a, const
                 return SNAPGPU_EINVAL;
             }
     if (reads->n == 0) return SNAPGPU_OK;
-    snapgpu_device_reads_t *d = snapgpu_reads_upload(a, reads);
+    snapgpu_device_reads_t *d = uploadCachedReads(a, reads);
     if (!d) return SNAPGPU_EDEVICE;
     AlignExt x;
     // grow-only device buffers of the aligner (hipMalloc / hipFree of the hit rows, ~1 GB for
@@ -2037,10 +2090,7 @@ extern "C++" int snapgpu_internal_align_batch_packed(snapgpu_aligner_t *a, const
         if (e == hipSuccess) b.cap = want;
         return e;
     };
-    auto cleanup = [&]() {
-        snapgpu_device_reads_free(d);
-        a->lastReads = nullptr;
-    };
+    auto cleanup = [&]() { a->lastReads = nullptr; };   // d stays the aligner's (grow-only)
     hipError_t e = hipSuccess;
     const uint64_t n = reads->n;
     void *dScratch = nullptr, *dFound = nullptr, *dHits = nullptr;
