@@ -405,6 +405,7 @@ int snapgpu_lv_group_batch(int device, int direction, uint32_t n,
  * location, no substring (Genome::getSubstring NULL) or no alignment within k),
  * nOps, and ops[i * SNAPGPU_CIGAR_MAX_OPS ..] as BAM ops (count << 4 | code, code
  * index into "MIDNSHP=X"; useM != 0 is the `-M` form: '=' and 'X' merged into 'M').
+ * snapgpu_cigar_batch writes the first nOps[i] entries of row i only.
  * Reads longer than 512 bases are rejected (SNAPGPU_EINVAL). */
 #define SNAPGPU_CIGAR_MAX_OPS 64
 

@@ -1038,8 +1038,8 @@ struct snapgpu_aligner {
     // for the whole device, the RNA path's concurrent genome aligner included
     snapgpu_device_reads_t *exReads = nullptr;
     uint64_t exReadsCapN = 0, exReadsCapBytes = 0;
-    void *cgPin = nullptr;
-    uint64_t cgPinCap = 0;
+    void *cgPin = nullptr, *cgPinOut = nullptr;
+    uint64_t cgPinCap = 0, cgPinOutCap = 0;
     hipStream_t stream() const { return lane[0].stream; }
 };
 
@@ -1301,6 +1301,7 @@ void snapgpu_aligner_free(snapgpu_aligner_t *a) {
     for (auto *b : {&a->cgIn, &a->cgOut}) devFree(a, b->p);
     for (auto &b : a->aux) devFree(a, b.p);
     hostPinnedFree(a->cgPin);
+    hostPinnedFree(a->cgPinOut);
     snapgpu_device_reads_free(a->exReads);
     for (auto *b : {&a->exSearch, &a->exScratch, &a->exFound, &a->exHits, &a->exOff, &a->exDense}) devFree(a, b->p);
     delete a;
@@ -2470,14 +2471,18 @@ int snapgpu_cigar_batch(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, cons
     };
     HIPCHK(ensure(a->cgIn, inBytes));
     HIPCHK(ensure(a->cgOut, outBytes));
-    if (inBytes > a->cgPinCap) {
-        hostPinnedFree(a->cgPin);
-        a->cgPin = nullptr;
-        a->cgPinCap = 0;
-        const uint64_t want = inBytes + inBytes / 4 + 256;
-        HIPCHK(hipHostMalloc(&a->cgPin, want, hipHostMallocDefault));
-        a->cgPinCap = want;
-    }
+    auto pinned = [](void *&p, uint64_t &cap, uint64_t bytes) -> hipError_t {
+        if (bytes <= cap) return hipSuccess;
+        hostPinnedFree(p);
+        p = nullptr;
+        cap = 0;
+        const uint64_t want = bytes + bytes / 4 + 256;
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e == hipSuccess) cap = want;
+        return e;
+    };
+    HIPCHK(pinned(a->cgPin, a->cgPinCap, inBytes));
+    HIPCHK(pinned(a->cgPinOut, a->cgPinOutCap, outBytes));
     char *h = (char *)a->cgPin;
     uint64_t *hOff = (uint64_t *)(h + oOff);
     uint64_t at = 0;
@@ -2514,10 +2519,18 @@ int snapgpu_cigar_batch(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, cons
     C.outEd = (int32_t *)(dOut + rEd); C.outNOps = (uint32_t *)(dOut + rN); C.outOps = (uint32_t *)(dOut + rOps);
     int rc = cigar_kernel_launch(a, C, n);
     if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(editDistance, dOut + rEd, n * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(nOps, dOut + rN, n * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(ops, dOut + rOps, n * CIG_MAX_OPS * 4, hipMemcpyDeviceToHost, st));
+    // outputs through pinned memory (one D2H), then only each row's nOps ops to the caller (rows hold
+    // a few of their 64 slots; a pageable D2H of every full row was most of the call)
+    char *ho = (char *)a->cgPinOut;
+    HIPCHK(hipMemcpyAsync(ho, dOut, outBytes, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    memcpy(editDistance, ho + rEd, n * 4);
+    memcpy(nOps, ho + rN, n * 4);
+    const uint32_t *hops = (const uint32_t *)(ho + rOps);
+    for (uint64_t i = 0; i < n; i++) {
+        const uint32_t k = std::min<uint32_t>(nOps[i], (uint32_t)CIG_MAX_OPS);
+        memcpy(ops + i * CIG_MAX_OPS, hops + i * CIG_MAX_OPS, k * 4);
+    }
     return SNAPGPU_OK;
 }
 
