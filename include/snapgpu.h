@@ -494,6 +494,11 @@ typedef struct snapgpu_single_options {
     const char *readGroup;           /* default "FASTQ" (AlignerOptions.cpp:65) */
     const char *commandLine;         /* @PG CL: */
     const char *version;             /* @PG VN: */
+    /* -ct: the contamination database (SingleAligner.cpp:205-218, 282-293): reads the filter left
+     * NotFound go through this BaseAligner (same parameters as the genome aligner) and each one it
+     * aligns is counted in `contaminants` (both NULL: no contamination database) */
+    struct snapgpu_aligner *contaminationAligner;
+    struct snapgpu_contaminants *contaminants;
 } snapgpu_single_options_t;
 void snapgpu_single_options_default(snapgpu_single_options_t *o);
 
@@ -508,6 +513,22 @@ typedef struct snapgpu_single_stats {   /* AlignerStats (AlignerStats.h:40-69) *
 int snapgpu_single_align(snapgpu_aligner_t *genomeAligner, snapgpu_aligner_t *transcriptomeAligner,
                          snapgpu_gtf_t *gtf, snapgpu_reads_t *reads, const snapgpu_single_options_t *opt,
                          const char *samPath, snapgpu_single_stats_t *stats);
+/* ------------------------------------------ contamination database (-ct) counts */
+/* ContaminationFilter (ContaminationFilter.cpp:22-112): contaminant alignments counted per contig
+ * of the contamination genome (a location maps to its piece, Genome::getPieceAtLocation; an
+ * invalid location counts nothing).  Counts accumulate over the product-path calls that carry the
+ * object in their options; thread-safe. */
+typedef struct snapgpu_contaminants snapgpu_contaminants_t;
+snapgpu_contaminants_t *snapgpu_contaminants_create(const snapgpu_index_t *contamination);
+void snapgpu_contaminants_free(snapgpu_contaminants_t *c);
+int snapgpu_contaminants_add(snapgpu_contaminants_t *c, uint32_t location);   /* AddAlignment */
+/* ContaminationFilter::Write: "<prefix>.contaminants.txt" with prefix = outputFileTemplate up to
+ * its last '.' ("default" for NULL), one "contig<TAB>count" line per contig, by count descending
+ * (the reference's std::sort over the name-ordered counts, reverse iterators) */
+int snapgpu_contaminants_write(const snapgpu_contaminants_t *c, const char *outputFileTemplate);
+/* the same text into out (at most cap bytes; *used = the size needed) */
+int snapgpu_contaminants_format(const snapgpu_contaminants_t *c, char *out, uint64_t cap, uint64_t *used);
+
 /* The index an aligner was created over (BaseAligner's GenomeIndex; getGenome for the SAM writer). */
 const snapgpu_index_t *snapgpu_aligner_index(const snapgpu_aligner_t *a);
 int snapgpu_aligner_get_params(const snapgpu_aligner_t *a, snapgpu_aligner_params_t *p);
@@ -650,6 +671,11 @@ typedef struct snapgpu_rna_paired_options {
     const char *readGroup;           /* default "FASTQ" */
     const char *commandLine;         /* @PG CL: */
     const char *version;             /* @PG VN: */
+    /* -ct: the contamination database (PairedAligner.cpp:487-505, 632-645): pairs the filter left
+     * NotFound on both ends go through this paired aligner (the genome one's parameters); a pair
+     * it aligns on both ends adds both ends to `contaminants` (both NULL: none) */
+    struct snapgpu_paired_aligner *contaminationAligner;
+    struct snapgpu_contaminants *contaminants;
 } snapgpu_rna_paired_options_t;
 void snapgpu_rna_paired_options_default(snapgpu_rna_paired_options_t *o);
 

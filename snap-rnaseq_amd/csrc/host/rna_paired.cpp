@@ -495,6 +495,34 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
     }
     X.seedMs = msSince(t0);
     t0 = std::chrono::steady_clock::now();
+    // -ct (PairedAligner.cpp:632-645): pairs still NotFound on both ends through the contamination
+    // paired aligner, one GPU batch; a pair it aligns on both ends adds both ends' contigs
+    if (opt->contaminationAligner && opt->contaminants) {
+        std::vector<uint64_t> co[2];
+        std::vector<uint32_t> cl[2];
+        for (uint64_t j = 0; j < nu; j++) {
+            const PairOut &r = X.fs[j].r;
+            if (r.status[0] != SNAPGPU_NOT_FOUND || r.status[1] != SNAPGPU_NOT_FOUND) continue;
+            for (int k = 0; k < 2; k++) { co[k].push_back(X.uo[k][j]); cl[k].push_back(X.ul[k][j]); }
+        }
+        if (!co[0].empty()) {
+            snapgpu_reads_t *cv[2];
+            for (int k = 0; k < 2; k++) cv[k] = snapgpu_reads_from_arrays(co[k].size(), R[k]->bases, R[k]->quals, co[k].data(), cl[k].data());
+            std::vector<snapgpu_pair_result_t> cr(co[0].size());
+            int rc = cv[0] && cv[1] ? snapgpu_paired_align_batch(opt->contaminationAligner, cv[0], cv[1], cr.data()) : SNAPGPU_ENOMEM;
+            if (rc && rc != SNAPGPU_ENOMEM) X.fail(rc, snapgpu_last_error());
+            else if (rc) X.fail(rc, "rna_paired_align: out of memory");
+            for (auto *v : cv) snapgpu_reads_free(v);
+            if (X.rc != SNAPGPU_OK) return;
+            for (auto &r : cr)
+                if (r.status[0] != SNAPGPU_NOT_FOUND && r.status[1] != SNAPGPU_NOT_FOUND)
+                    for (int k = 0; k < 2; k++)
+                        if ((rc = snapgpu_contaminants_add(opt->contaminants, r.location[k]))) {
+                            X.fail(rc, snapgpu_last_error());
+                            return;
+                        }
+        }
+    }
     // spacing and MAPQ adjustments (PairedAligner.cpp:648-663); the count events in input order
     // (applied for the whole batch at the end: gtfCountPairs)
     for (uint64_t j = 0; j < nu; j++) {

@@ -237,6 +237,25 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
     for (auto &e : errs) if (!e.empty()) { setError("single_align: " + e); return fail(SNAPGPU_EFORMAT); }
     for (uint64_t j = 0; j < nu; j++)   // gene read counts (FilterSingle :260-262, :290-292)
         if (fo[j].countTranscript) gtfCountSingle(gtf, *fo[j].countTranscript);
+    // -ct (SingleAligner.cpp:282-293): the reads still NotFound through the contamination
+    // BaseAligner, one GPU batch; every read it aligns counts its contig (ContaminationFilter)
+    if (opt->contaminationAligner && opt->contaminants && nu) {
+        std::vector<uint64_t> co;
+        std::vector<uint32_t> cl;
+        for (uint64_t j = 0; j < nu; j++)
+            if (fo[j].result == SNAPGPU_NOT_FOUND) { co.push_back(uo[j]); cl.push_back(ul[j]); }
+        if (!co.empty()) {
+            snapgpu_reads_t *cb = snapgpu_reads_from_arrays(co.size(), reads->bases, reads->quals, co.data(), cl.data());
+            if (!cb) return fail(SNAPGPU_ENOMEM);
+            std::vector<snapgpu_result_t> cr(co.size());
+            rc = snapgpu_align_batch(opt->contaminationAligner, cb, cr.data());
+            snapgpu_reads_free(cb);
+            if (rc) return fail(rc);
+            for (auto &r : cr)
+                if (r.result != SNAPGPU_NOT_FOUND && (rc = snapgpu_contaminants_add(opt->contaminants, r.location)))
+                    return fail(rc);
+        }
+    }
     st.filterMs = msSince(t0);
     // CIGARs on the GPU: genome records at the filter's location (NotFound keeps location 0 and
     // the forward read, SAM.cpp:1040-1048), transcriptome records on the transcriptome at tlocation

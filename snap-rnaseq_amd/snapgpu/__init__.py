@@ -71,7 +71,8 @@ class SnapGpuError(RuntimeError):
 
 _PTR_CALLS = ("genome_from_fasta", "genome_synthetic", "index_build", "index_load", "index_attach", "gtf_load",
               "reads_synthetic",
-              "reads_from_fastq", "reads_from_arrays", "aligner_create", "reads_upload", "paired_aligner_create")
+              "reads_from_fastq", "reads_from_arrays", "aligner_create", "reads_upload", "paired_aligner_create",
+              "contaminants_create")
 
 
 def _check(value, what):
@@ -764,6 +765,43 @@ class Gtf:
             self._h = None
 
 
+class Contaminants:
+    """The contamination database's counts (`-ct`, ContaminationFilter): contaminant alignments per
+    contig of the contamination index, accumulated over the product-path calls given
+    contamination=(aligner, this); write() leaves `<prefix>.contaminants.txt` as the reference."""
+
+    def __init__(self, contamination_index):
+        self._index = contamination_index
+        self._h = _check(lib().snapgpu_contaminants_create(contamination_index._h), "contaminants_create")
+
+    def add(self, location):
+        """ContaminationFilter::AddAlignment of one aligned location of the contamination genome."""
+        _check(lib().snapgpu_contaminants_add(self._h, int(location)), "contaminants_add")
+
+    def text(self):
+        used = C.c_uint64()
+        _check(lib().snapgpu_contaminants_format(self._h, None, 0, C.byref(used)), "contaminants_format")
+        buf = C.create_string_buffer(max(1, used.value))
+        _check(lib().snapgpu_contaminants_format(self._h, buf, used.value, C.byref(used)), "contaminants_format")
+        return C.string_at(buf, used.value).decode()
+
+    def write(self, output_template):
+        _check(lib().snapgpu_contaminants_write(self._h, None if output_template is None else str(output_template).encode()),
+               "contaminants_write")
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().snapgpu_contaminants_free(self._h)
+            self._h = None
+
+
+def _contamination_opts(o, contamination):
+    if contamination is not None:
+        aligner, counts = contamination
+        o.contaminationAligner = aligner._h
+        o.contaminants = counts._h
+
+
 def single_options(**kw):
     o = _ffi.SingleOptions()
     lib().snapgpu_single_options_default(C.byref(o))
@@ -772,10 +810,12 @@ def single_options(**kw):
     return o
 
 
-def single_align(genome_aligner, transcriptome_aligner, gtf, reads, sam_path, **options):
+def single_align(genome_aligner, transcriptome_aligner, gtf, reads, sam_path, contamination=None, **options):
     """`snap-rna single` (SingleAligner.cpp:141-320) over a FASTQ batch, both AlignRead calls and
-    the CIGARs on the GPU; writes sam_path.  options: SingleOptions fields.  -> stats dict."""
+    the CIGARs on the GPU; writes sam_path.  options: SingleOptions fields; contamination:
+    (BaseAligner over the contamination index, Contaminants) for `-ct`.  -> stats dict."""
     o = single_options(**options)
+    _contamination_opts(o, contamination)
     st = _ffi.SingleStats()
     _check(lib().snapgpu_single_align(genome_aligner._h, transcriptome_aligner._h, gtf._h, reads._p, C.byref(o),
                                       str(sam_path).encode(), C.byref(st)), "single_align")
@@ -798,11 +838,13 @@ def rna_paired_options(**kw):
     return o
 
 
-def rna_paired_align(paired_aligner, transcriptome_aligner, gtf, reads0, reads1, sam_path=None, **options):
+def rna_paired_align(paired_aligner, transcriptome_aligner, gtf, reads0, reads1, sam_path=None, contamination=None,
+                     **options):
     """`snap-rna paired` (PairedAligner.cpp:405-689) over a FASTQ pair batch: the transcriptome and
     genome aligners, the seed census of FindPartialMatches and the CIGARs on the GPU; writes
     sam_path (if given) and advances gtf's read counters.  -> (RNA_PAIR_RESULT_DTYPE[n], stats)."""
     o = rna_paired_options(**options)
+    _contamination_opts(o, contamination)   # (PairedAligner over the contamination index, Contaminants): -ct
     st = _ffi.RnaPairedStats()
     out = np.zeros(max(1, reads0.n), dtype=RNA_PAIR_RESULT_DTYPE)
     _check(lib().snapgpu_rna_paired_align(paired_aligner._h, transcriptome_aligner._h, gtf._h, reads0._p, reads1._p,

@@ -173,6 +173,8 @@ class SingleOptions(C.Structure):
         ("readGroup", C.c_char_p),
         ("commandLine", C.c_char_p),
         ("version", C.c_char_p),
+        ("contaminationAligner", C.c_void_p),
+        ("contaminants", C.c_void_p),
     ]
 
 
@@ -182,7 +184,7 @@ class RnaPairedOptions(C.Structure):
         ("maxSpacing", C.c_uint32), ("forceSpacing", C.c_uint32), ("minPercentAbovePhred", C.c_float),
         ("minPhred", C.c_uint32), ("phredOffset", C.c_uint32), ("useM", C.c_uint32), ("maxHitsToGet", C.c_uint32),
         ("ignoreMismatchedIDs", C.c_uint32), ("readGroup", C.c_char_p), ("commandLine", C.c_char_p),
-        ("version", C.c_char_p),
+        ("version", C.c_char_p), ("contaminationAligner", C.c_void_p), ("contaminants", C.c_void_p),
     ]
 
 
@@ -333,6 +335,11 @@ _PROTOS += [
                                            C.POINTER(RnaPairedOptions), C.c_char_p, C.c_void_p,
                                            C.POINTER(RnaPairedStats)]),
     ("snapgpu_gtf_write_counts", C.c_int, [C.c_void_p, C.c_char_p]),
+    ("snapgpu_contaminants_create", C.c_void_p, [C.c_void_p]),
+    ("snapgpu_contaminants_free", None, [C.c_void_p]),
+    ("snapgpu_contaminants_add", C.c_int, [C.c_void_p, C.c_uint32]),
+    ("snapgpu_contaminants_write", C.c_int, [C.c_void_p, C.c_char_p]),
+    ("snapgpu_contaminants_format", C.c_int, [C.c_void_p, C.c_char_p, C.c_uint64, C.POINTER(C.c_uint64)]),
     ("snapgpu_gtf_reset_counts", C.c_int, [C.c_void_p]),
     ("snapgpu_characterize_seeds", C.POINTER(SeedRuns), [C.c_void_p, C.POINTER(Reads), C.c_void_p, C.c_uint64,
                                                          C.POINTER(CharSeedsParams)]),

@@ -17,6 +17,7 @@ TSV/JSON expected outputs.
     python3 tests/golden/make_golden.py --only-long      # 129..256-base reads + long LV vectors (align_kernel<256>)
     python3 tests/golden/make_golden.py --only-bam       # `snap-rna single ... -o out.bam` records (BAMFormat)
     python3 tests/golden/make_golden.py --only-rna150    # `snap-rna paired` on 2 x 150 pairs (configs[4] length)
+    python3 tests/golden/make_golden.py --only-contam    # `snap-rna single|paired ... -ct <contamination index>`
     python3 tests/golden/make_golden.py --only-rna-bench # digest of the reference on bench.py's RNA workload
     python3 tests/golden/make_golden.py --only-rna-bam   # `snap-rna paired ... -o out.bam` records (both RNA sets)
 """
@@ -712,6 +713,97 @@ def rna_paired_fixtures(work, variant=""):
                 dst.write("".join(counts))
 
 
+def contamination_fixtures(work):
+    """`snap-rna single|paired ... -ct <contamination index>` (SingleAligner.cpp:205-293,
+    PairedAligner.cpp:487-645, ContaminationFilter.cpp): reads left NotFound by the filter are
+    aligned to the contamination index and every aligned contaminant counted by contig;
+    ContaminationFilter::Write leaves `<output prefix>.contaminants.txt` (contig, count; by count,
+    descending).  contam.fa: five random contigs (the counts tie on purpose); the read sets mix
+    reads of the existing single / 2 x 150 RNA fixtures with reads and pairs from the contigs
+    (mutated, either strand).  The SAM output must not change with -ct (checked here)."""
+    import gzip
+    rng = random.Random(1907)
+    comp = str.maketrans("ACGT", "TGCA")
+    rc = lambda x: x.translate(comp)[::-1]
+    contigs = {f"cont{i}": "".join(rng.choice("ACGT") for _ in range(ln))
+               for i, ln in enumerate((6000, 9000, 4000, 7000, 5000), 1)}
+    cfa = os.path.join(HERE, "contam.fa")
+    with open(cfa, "w") as f:
+        for name, seq in contigs.items():
+            f.write(f">{name}\n")
+            f.write("".join(seq[i:i + 60] + "\n" for i in range(0, len(seq), 60)))
+    cidx = os.path.join(work, "cidx")
+    ref_index(cfa, cidx)
+
+    def mutate(x):
+        x = list(x)
+        for _ in range(rng.choice([0, 0, 1, 2, 3])):
+            x[rng.randrange(len(x))] = rng.choice("ACGT")
+        return "".join(x)
+
+    # per contig how many reads / pairs: equal counts for some contigs (the sort's ties)
+    plan = {"cont1": 20, "cont2": 35, "cont3": 20, "cont4": 8, "cont5": 20}
+    fa = os.path.join(HERE, "small.fa")
+    gidx = os.path.join(work, "gidx")
+    ref_index(fa, gidx)
+    gtf = os.path.join(HERE, "small.gtf")
+    twd = os.path.join(work, "tx")
+    os.makedirs(twd, exist_ok=True)
+    run([SNAP, "transcriptome", gtf, fa, "tidx", "-O1000"], cwd=twd)
+    # single: 300 reads of single_reads.fq + contaminant reads, shuffled in
+    recs = open(os.path.join(HERE, "single_reads.fq")).read().splitlines()
+    base = [recs[4 * i:4 * i + 4] for i in range(300)]
+    extra = []
+    for name, k in plan.items():
+        for j in range(k):
+            p = rng.randrange(0, len(contigs[name]) - 100)
+            x = mutate(contigs[name][p:p + 100])
+            extra.append([f"@c_{name}_{j}", x if rng.random() < 0.5 else rc(x), "+", "I" * 100])
+    allr = base + extra
+    rng.shuffle(allr)
+    sfq = os.path.join(HERE, "contam_single.fq")
+    with open(sfq, "w") as f:
+        f.write("".join("\n".join(r) + "\n" for r in allr))
+    outs = {}
+    for tag, extra_args in (("plain", []), ("x", ["-ct", cidx])):
+        out = os.path.join(work, f"cs_{tag}.sam")
+        run([SNAP, "single", gidx, os.path.join(twd, "tidx"), gtf, sfq, "-t", "1", "-o", out] + extra_args, cwd=work)
+        outs[tag] = [l for l in open(out).read().splitlines() if not l.startswith("@PG")]
+    assert outs["plain"] == outs["x"], "the SAM output changed with -ct"
+    with open(os.path.join(HERE, "expected_contam_single.sam.gz"), "wb") as dst:
+        dst.write(gzip.compress(open(os.path.join(work, "cs_x.sam"), "rb").read(), compresslevel=9, mtime=0))
+    shutil.copy(os.path.join(work, "cs_x.contaminants.txt"), os.path.join(HERE, "expected_contam_single.contaminants.txt"))
+    # paired: 150 pairs of the 2 x 150 RNA set + contaminant pairs (insert 250-450, FR)
+    r0 = open(os.path.join(HERE, "rna150_1.fq")).read().splitlines()
+    r1 = open(os.path.join(HERE, "rna150_2.fq")).read().splitlines()
+    pairs = [(r0[4 * i:4 * i + 4], r1[4 * i:4 * i + 4]) for i in range(150)]
+    for name, k in plan.items():
+        for j in range(k):
+            ins = rng.randrange(250, 450)
+            p = rng.randrange(0, len(contigs[name]) - ins)
+            frag = contigs[name][p:p + ins]
+            a, b = mutate(frag[:150]), mutate(rc(frag)[:150])
+            if rng.random() < 0.5:
+                a, b = b, a
+            nm = f"@cp_{name}_{j}"
+            pairs.append(([nm + "/1", a, "+", "I" * 150], [nm + "/2", b, "+", "I" * 150]))
+    rng.shuffle(pairs)
+    pfq = [os.path.join(HERE, f"contam_paired_{k}.fq") for k in (1, 2)]
+    for k in range(2):
+        with open(pfq[k], "w") as f:
+            f.write("".join("\n".join(pr[k]) + "\n" for pr in pairs))
+    outs = {}
+    for tag, extra_args in (("plain", []), ("x", ["-ct", cidx])):
+        out = os.path.join(work, f"cp_{tag}.sam")
+        run([SNAP, "paired", gidx, os.path.join(twd, "tidx"), gtf, pfq[0], pfq[1], "-t", "1", "-o", out] + extra_args,
+            cwd=work)
+        outs[tag] = [l for l in open(out).read().splitlines() if not l.startswith("@PG")]
+    assert outs["plain"] == outs["x"], "the SAM output changed with -ct"
+    with open(os.path.join(HERE, "expected_contam_paired.sam.gz"), "wb") as dst:
+        dst.write(gzip.compress(open(os.path.join(work, "cp_x.sam"), "rb").read(), compresslevel=9, mtime=0))
+    shutil.copy(os.path.join(work, "cp_x.contaminants.txt"), os.path.join(HERE, "expected_contam_paired.contaminants.txt"))
+
+
 def _rna_blocks_bisect(recs, n, attempt, work, fq0, fq1, stem):
     """Block partition for the RNA fixtures whose every block is a clean `snap-rna paired` run in
     BOTH modes (default and -M), the very runs whose outputs are kept.  The reference's crash in
@@ -1042,6 +1134,11 @@ def main():
         rna_bam_fixtures(work)
         shutil.rmtree(work, ignore_errors=True)
         print("RNA paired BAM fixtures written to", HERE)
+        return
+    if "--only-contam" in sys.argv:
+        contamination_fixtures(work)
+        shutil.rmtree(work, ignore_errors=True)
+        print("contamination-database fixtures written to", HERE)
         return
     if "--only-rna150" in sys.argv:
         rna_paired_fixtures(work, "150")
