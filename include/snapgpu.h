@@ -490,7 +490,8 @@ typedef struct snapgpu_single_options {
     uint32_t minPhred;               /* -fm, default 20 */
     uint32_t phredOffset;            /* -fo, default 33 */
     uint32_t useM;                   /* -M */
-    uint32_t reserved;
+    uint32_t sortOutput;             /* -so: SAM records stable-sorted by location, @HD SO:coordinate
+                                        (SortedDataWriter.cpp:186-240; one block per call; not for BAM) */
     const char *readGroup;           /* default "FASTQ" (AlignerOptions.cpp:65) */
     const char *commandLine;         /* @PG CL: */
     const char *version;             /* @PG VN: */
@@ -513,6 +514,13 @@ typedef struct snapgpu_single_stats {   /* AlignerStats (AlignerStats.h:40-69) *
 int snapgpu_single_align(snapgpu_aligner_t *genomeAligner, snapgpu_aligner_t *transcriptomeAligner,
                          snapgpu_gtf_t *gtf, snapgpu_reads_t *reads, const snapgpu_single_options_t *opt,
                          const char *samPath, snapgpu_single_stats_t *stats);
+/* `-so` for SAM text (SortedDataFilter::onNextBatch, SortedDataWriter.cpp:186-240): the records
+ * (lines) of `in` stable-sorted by SAMFormat::getSortInfo's location (SAM.cpp:639-685) over idx's
+ * genome; header lines (starting '@') are not records and must not be in `in`.  Writes at most cap
+ * bytes to out, *used = the size (= n); the product paths use it with sortOutput set. */
+int snapgpu_sam_sort_records(const snapgpu_index_t *idx, const char *in, uint64_t n, char *out, uint64_t cap,
+                             uint64_t *used);
+
 /* ------------------------------------------ contamination database (-ct) counts */
 /* ContaminationFilter (ContaminationFilter.cpp:22-112): contaminant alignments counted per contig
  * of the contamination genome (a location maps to its piece, Genome::getPieceAtLocation; an
@@ -676,6 +684,7 @@ typedef struct snapgpu_rna_paired_options {
      * it aligns on both ends adds both ends to `contaminants` (both NULL: none) */
     struct snapgpu_paired_aligner *contaminationAligner;
     struct snapgpu_contaminants *contaminants;
+    uint32_t sortOutput;             /* -so: as snapgpu_single_options_t.sortOutput */
 } snapgpu_rna_paired_options_t;
 void snapgpu_rna_paired_options_default(snapgpu_rna_paired_options_t *o);
 

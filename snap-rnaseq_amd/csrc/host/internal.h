@@ -124,6 +124,10 @@ struct SamLine {
     uint32_t mateFront = 0, mateClippedLen = 0, mateFullLen = 0;
 };
 void samAppendLine(std::string &o, const Genome &g, const SamLine &L);
+// `-so` for SAM output (SortedDataFilter::onNextBatch, SortedDataWriter.cpp:186-240, with
+// SAMFormat::getSortInfo, SAM.cpp:639-685): the records of `parts` (whole lines, in write order)
+// stable-sorted by their location key, concatenated
+std::string samSortRecords(const Genome &g, const std::vector<std::string> &parts);
 // bam.cpp: BAMFormat::writeRead of a read without mate, the BAM header, a BGZF writer
 bool bamAppendRecord(std::string &o, const Genome &g, const SamLine &L, int32_t nm);
 std::string bamHeader(const Genome &g, const std::string &samText);

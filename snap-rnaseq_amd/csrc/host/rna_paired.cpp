@@ -761,6 +761,10 @@ int snapgpu_rna_paired_align(snapgpu_paired_aligner_t *pa, snapgpu_aligner_t *ta
     const auto w0 = std::chrono::steady_clock::now();
     if (!pa || !ta || !gtf || !reads0 || !reads1 || !opt) { setError("rna_paired_align: null argument"); return SNAPGPU_EINVAL; }
     if (reads0->n != reads1->n) { setError("rna_paired_align: the two read batches differ in length"); return SNAPGPU_EINVAL; }
+    if (opt->sortOutput && samPath && strlen(samPath) >= 4 && strcmp(samPath + strlen(samPath) - 4, ".bam") == 0) {
+        setError("rna_paired_align: sorted output is built for SAM only");   // sorted BAM + BAMIndexSupplier's .bai
+        return SNAPGPU_EUNSUPPORTED;
+    }
     if (!reads0->ids || !reads1->ids) { setError("rna_paired_align: the reads carry no ids (use snapgpu_reads_from_fastq)"); return SNAPGPU_EINVAL; }
     snapgpu_aligner_t *ga = snapgpu_paired_aligner_single(pa);   // the genome index upload (BaseAligner)
     const snapgpu_index_t *gi = snapgpu_aligner_index(ga), *ti = snapgpu_aligner_index(ta);
@@ -897,10 +901,11 @@ int snapgpu_rna_paired_align(snapgpu_paired_aligner_t *pa, snapgpu_aligner_t *ta
         FILE *f = fopen(samPath, "w");
         if (!f) { setError(std::string("cannot write ") + samPath); return SNAPGPU_EIO; }
         uint64_t hlen = 0;
-        snapgpu_sam_header(gi, 0, opt->commandLine ? opt->commandLine : "", opt->version ? opt->version : "", nullptr,
+        const int so = opt->sortOutput ? 1 : 0;   // @HD SO:coordinate (SAMFormat::writeHeader, sorted)
+        snapgpu_sam_header(gi, so, opt->commandLine ? opt->commandLine : "", opt->version ? opt->version : "", nullptr,
                            nullptr, 0, &hlen);
         std::string hdr(hlen, '\0');
-        int rc = snapgpu_sam_header(gi, 0, opt->commandLine ? opt->commandLine : "", opt->version ? opt->version : "",
+        int rc = snapgpu_sam_header(gi, so, opt->commandLine ? opt->commandLine : "", opt->version ? opt->version : "",
                                     nullptr, &hdr[0], hlen, &hlen);
         if (rc) { fclose(f); return rc; }
         bool ok = true;
@@ -914,8 +919,16 @@ int snapgpu_rna_paired_align(snapgpu_paired_aligner_t *pa, snapgpu_aligner_t *ta
             ok = ok && bgzfWrite(f, all.data(), all.size(), true);
         } else {
             ok = fwrite(hdr.data(), 1, hdr.size(), f) == hdr.size();
-            for (auto &x : subs)
-                for (auto &p : x->parts) ok = ok && fwrite(p.data(), 1, p.size(), f) == p.size();
+            if (opt->sortOutput) {   // one block: the whole call's records, stable-sorted by location
+                std::vector<std::string> all;
+                for (auto &x : subs)
+                    for (auto &p : x->parts) all.push_back(std::move(p));
+                const std::string sorted = samSortRecords(*gi->genome, all);
+                ok = ok && fwrite(sorted.data(), 1, sorted.size(), f) == sorted.size();
+            } else {
+                for (auto &x : subs)
+                    for (auto &p : x->parts) ok = ok && fwrite(p.data(), 1, p.size(), f) == p.size();
+            }
         }
         ok = (fclose(f) == 0) && ok;
         if (!ok) { setError(std::string("write failed: ") + samPath); return SNAPGPU_EIO; }

@@ -9,6 +9,8 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <map>
+#include <string>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -429,5 +431,66 @@ extern "C" int snapgpu_sam_header(const snapgpu_index_t *idx, int sorted, const 
         return SNAPGPU_EINVAL;
     }
     memcpy(out, o.data(), o.size());
+    return SNAPGPU_OK;
+}
+
+namespace snapgpu {
+
+// SAMFormat::getSortInfo's location of one record (SAM.cpp:639-685 with SAMReader::parsePieceName
+// and parseLocation, :408-468): POS empty or '*' -> the mate's RNEXT/PNEXT (UINT32_MAX when PNEXT is
+// '*' too), else RNAME/POS; an RNAME that is '*' gives InvalidGenomeLocation, a name the genome does
+// not know (RNEXT "=") offset 0; location = piece offset + POS - 1.
+static uint32_t samSortKey(const std::map<std::string, uint32_t> &pieces, const char *line, size_t len) {
+    const char *f[9];
+    size_t fl[9];
+    size_t k = 0, start = 0;
+    for (size_t i = 0; i <= len && k < 9; i++)
+        if (i == len || line[i] == '\t') { f[k] = line + start; fl[k] = i - start; k++; start = i + 1; }
+    for (; k < 9; k++) { f[k] = line + len; fl[k] = 0; }
+    auto loc = [&](int rf, int pf) -> uint32_t {
+        if (fl[rf] == 0 || fl[pf] == 0 || f[rf][0] == '*' || f[pf][0] == '*') return 0xffffffffu;
+        const auto it = pieces.find(std::string(f[rf], fl[rf]));
+        const uint32_t off = it == pieces.end() ? 0u : it->second;
+        uint32_t pos = 0;
+        for (size_t i = 0; i < fl[pf] && f[pf][i] >= '0' && f[pf][i] <= '9'; i++) pos = pos * 10 + (uint32_t)(f[pf][i] - '0');
+        return off + pos - 1;
+    };
+    if (fl[3] == 0 || f[3][0] == '*') return (fl[7] == 0 || f[7][0] == '*') ? 0xffffffffu : loc(6, 7);
+    return loc(2, 3);
+}
+
+std::string samSortRecords(const Genome &g, const std::vector<std::string> &parts) {
+    std::map<std::string, uint32_t> pieces;
+    for (size_t i = 0; i < g.pieceNames.size(); i++) pieces.emplace(g.pieceNames[i], g.pieceOffsets[i]);
+    struct Rec { uint32_t key; const char *p; size_t n; };
+    std::vector<Rec> recs;
+    size_t total = 0;
+    for (const auto &s : parts) {
+        total += s.size();
+        size_t b = 0;
+        while (b < s.size()) {
+            size_t e = s.find('\n', b);
+            e = e == std::string::npos ? s.size() : e + 1;
+            recs.push_back(Rec{samSortKey(pieces, s.data() + b, e - b - (s[e - 1] == '\n')), s.data() + b, e - b});
+            b = e;
+        }
+    }
+    std::stable_sort(recs.begin(), recs.end(), [](const Rec &a, const Rec &b) { return a.key < b.key; });
+    std::string out;
+    out.reserve(total);
+    for (const auto &r : recs) out.append(r.p, r.n);
+    return out;
+}
+
+}  // namespace snapgpu
+
+extern "C" int snapgpu_sam_sort_records(const snapgpu_index_t *idx, const char *in, uint64_t n, char *out, uint64_t cap,
+                                        uint64_t *used) {
+    if (!idx || !idx->genome || (!in && n) || !used) return SNAPGPU_EINVAL;
+    *used = n;
+    if (!out) return SNAPGPU_OK;
+    if (cap < n) return SNAPGPU_EINVAL;
+    const std::string sorted = samSortRecords(*idx->genome, std::vector<std::string>{std::string(in, n)});
+    memcpy(out, sorted.data(), sorted.size());
     return SNAPGPU_OK;
 }

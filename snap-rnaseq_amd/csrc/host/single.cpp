@@ -318,6 +318,10 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
     // repeat the previous record's value -- a serial pass in output order fixes each record's NM.
     const size_t pl = strlen(samPath);
     const bool bam = pl >= 4 && strcmp(samPath + pl - 4, ".bam") == 0;
+    if (bam && opt->sortOutput) {   // sorted BAM (+ BAMIndexSupplier's .bai) is not built
+        setError("single_align: sorted output is built for SAM only");
+        return fail(SNAPGPU_EUNSUPPORTED);
+    }
     std::vector<int32_t> bamNm;
     if (bam) {
         bamNm.resize(n);
@@ -379,10 +383,11 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
     FILE *f = fopen(samPath, "w");
     if (!f) { setError(std::string("cannot write ") + samPath); return fail(SNAPGPU_EIO); }
     uint64_t hlen = 0;
-    snapgpu_sam_header(gi, 0, opt->commandLine ? opt->commandLine : "", opt->version ? opt->version : "", nullptr,
+    const int so = opt->sortOutput ? 1 : 0;   // @HD SO:coordinate (SAMFormat::writeHeader, sorted)
+    snapgpu_sam_header(gi, so, opt->commandLine ? opt->commandLine : "", opt->version ? opt->version : "", nullptr,
                        nullptr, 0, &hlen);
     std::string hdr(hlen, '\0');
-    if ((rc = snapgpu_sam_header(gi, 0, opt->commandLine ? opt->commandLine : "", opt->version ? opt->version : "",
+    if ((rc = snapgpu_sam_header(gi, so, opt->commandLine ? opt->commandLine : "", opt->version ? opt->version : "",
                                  nullptr, &hdr[0], hlen, &hlen))) { fclose(f); return fail(rc); }
     bool ok = true;
     if (bam) {   // BGZF stream: header, then the records (64 KB blocks), then the EOF block
@@ -394,7 +399,12 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
         ok = ok && bgzfWrite(f, all.data(), all.size(), true);
     } else {
         ok = fwrite(hdr.data(), 1, hdr.size(), f) == hdr.size();
-        for (auto &p : parts) ok = ok && fwrite(p.data(), 1, p.size(), f) == p.size();
+        if (opt->sortOutput) {
+            const std::string sorted = samSortRecords(*gi->genome, parts);
+            ok = ok && fwrite(sorted.data(), 1, sorted.size(), f) == sorted.size();
+        } else {
+            for (auto &p : parts) ok = ok && fwrite(p.data(), 1, p.size(), f) == p.size();
+        }
     }
     ok = (fclose(f) == 0) && ok;
     if (!ok) { setError(std::string("write failed: ") + samPath); return fail(SNAPGPU_EIO); }

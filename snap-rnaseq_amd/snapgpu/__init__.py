@@ -765,6 +765,14 @@ class Gtf:
             self._h = None
 
 
+def sam_sort_records(index, text):
+    """`-so`: SAM record lines (bytes, no header) stable-sorted by SAMFormat::getSortInfo's location."""
+    used = C.c_uint64()
+    buf = C.create_string_buffer(max(1, len(text)))
+    _check(lib().snapgpu_sam_sort_records(index._h, text, len(text), buf, len(text), C.byref(used)), "sam_sort_records")
+    return C.string_at(buf, used.value)
+
+
 class Contaminants:
     """The contamination database's counts (`-ct`, ContaminationFilter): contaminant alignments per
     contig of the contamination index, accumulated over the product-path calls given

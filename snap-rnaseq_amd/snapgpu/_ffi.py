@@ -169,7 +169,7 @@ class SingleOptions(C.Structure):
         ("minPhred", C.c_uint32),
         ("phredOffset", C.c_uint32),
         ("useM", C.c_uint32),
-        ("reserved", C.c_uint32),
+        ("sortOutput", C.c_uint32),
         ("readGroup", C.c_char_p),
         ("commandLine", C.c_char_p),
         ("version", C.c_char_p),
@@ -185,6 +185,7 @@ class RnaPairedOptions(C.Structure):
         ("minPhred", C.c_uint32), ("phredOffset", C.c_uint32), ("useM", C.c_uint32), ("maxHitsToGet", C.c_uint32),
         ("ignoreMismatchedIDs", C.c_uint32), ("readGroup", C.c_char_p), ("commandLine", C.c_char_p),
         ("version", C.c_char_p), ("contaminationAligner", C.c_void_p), ("contaminants", C.c_void_p),
+        ("sortOutput", C.c_uint32),
     ]
 
 
@@ -335,6 +336,8 @@ _PROTOS += [
                                            C.POINTER(RnaPairedOptions), C.c_char_p, C.c_void_p,
                                            C.POINTER(RnaPairedStats)]),
     ("snapgpu_gtf_write_counts", C.c_int, [C.c_void_p, C.c_char_p]),
+    ("snapgpu_sam_sort_records", C.c_int, [C.c_void_p, C.c_char_p, C.c_uint64, C.c_char_p, C.c_uint64,
+                                           C.POINTER(C.c_uint64)]),
     ("snapgpu_contaminants_create", C.c_void_p, [C.c_void_p]),
     ("snapgpu_contaminants_free", None, [C.c_void_p]),
     ("snapgpu_contaminants_add", C.c_int, [C.c_void_p, C.c_uint32]),

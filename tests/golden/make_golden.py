@@ -18,6 +18,7 @@ TSV/JSON expected outputs.
     python3 tests/golden/make_golden.py --only-bam       # `snap-rna single ... -o out.bam` records (BAMFormat)
     python3 tests/golden/make_golden.py --only-rna150    # `snap-rna paired` on 2 x 150 pairs (configs[4] length)
     python3 tests/golden/make_golden.py --only-contam    # `snap-rna single|paired ... -ct <contamination index>`
+    python3 tests/golden/make_golden.py --only-sorted    # `snap-rna single|paired ... -so` (sorted SAM)
     python3 tests/golden/make_golden.py --only-rna-bench # digest of the reference on bench.py's RNA workload
     python3 tests/golden/make_golden.py --only-rna-bam   # `snap-rna paired ... -o out.bam` records (both RNA sets)
 """
@@ -804,6 +805,30 @@ def contamination_fixtures(work):
     shutil.copy(os.path.join(work, "cp_x.contaminants.txt"), os.path.join(HERE, "expected_contam_paired.contaminants.txt"))
 
 
+def sorted_fixtures(work):
+    """`-so` (SortedDataWriter.cpp:186-240, SAMFormat::getSortInfo SAM.cpp:639-685): the SAM records of
+    `snap-rna single ... single_reads.fq -t 1 -o out.sam -so` and of `snap-rna paired ...
+    contam_paired_{1,2}.fq -t 1 -o out.sam -so` (one sort block each at these sizes)."""
+    import gzip
+    fa = os.path.join(HERE, "small.fa")
+    gidx = os.path.join(work, "gidx")
+    ref_index(fa, gidx)
+    gtf = os.path.join(HERE, "small.gtf")
+    twd = os.path.join(work, "tx")
+    os.makedirs(twd, exist_ok=True)
+    run([SNAP, "transcriptome", gtf, fa, "tidx", "-O1000"], cwd=twd)
+    out = os.path.join(work, "ss.sam")
+    run([SNAP, "single", gidx, os.path.join(twd, "tidx"), gtf, os.path.join(HERE, "single_reads.fq"), "-t", "1",
+         "-o", out, "-so"], cwd=work)
+    with open(out, "rb") as src, open(os.path.join(HERE, "expected_single_sorted.sam.gz"), "wb") as dst:
+        dst.write(gzip.compress(src.read(), compresslevel=9, mtime=0))
+    out = os.path.join(work, "ps.sam")
+    run([SNAP, "paired", gidx, os.path.join(twd, "tidx"), gtf, os.path.join(HERE, "contam_paired_1.fq"),
+         os.path.join(HERE, "contam_paired_2.fq"), "-t", "1", "-o", out, "-so"], cwd=work)
+    with open(out, "rb") as src, open(os.path.join(HERE, "expected_paired_sorted.sam.gz"), "wb") as dst:
+        dst.write(gzip.compress(src.read(), compresslevel=9, mtime=0))
+
+
 def _rna_blocks_bisect(recs, n, attempt, work, fq0, fq1, stem):
     """Block partition for the RNA fixtures whose every block is a clean `snap-rna paired` run in
     BOTH modes (default and -M), the very runs whose outputs are kept.  The reference's crash in
@@ -1134,6 +1159,11 @@ def main():
         rna_bam_fixtures(work)
         shutil.rmtree(work, ignore_errors=True)
         print("RNA paired BAM fixtures written to", HERE)
+        return
+    if "--only-sorted" in sys.argv:
+        sorted_fixtures(work)
+        shutil.rmtree(work, ignore_errors=True)
+        print("sorted-output fixtures written to", HERE)
         return
     if "--only-contam" in sys.argv:
         contamination_fixtures(work)
