@@ -158,6 +158,20 @@ def log(rank, msg, t0=[time.time()]):
         print(f"[bench {time.time() - t0[0]:7.1f}s] {msg}", file=sys.stderr, flush=True)
 
 
+_RESULT_OUT = sys.stdout   # where the one JSON line goes (the real stdout; see _stdout_to_stderr)
+
+
+def _stdout_to_stderr():
+    """stdout carries exactly rank 0's JSON line: everything else written to fd 1 from here on --
+    gloo's "[Gloo] Rank i is connected to ..." lines, HIP/ROCm warnings, library prints -- goes to
+    stderr, and the line is written to a duplicate of the original stdout."""
+    global _RESULT_OUT
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    _RESULT_OUT = os.fdopen(saved, "w")
+
+
 def _free_port():
     import socket
     with socket.socket() as s:
@@ -425,7 +439,7 @@ def standin_main(args, wl, world, rank, local, dist):
                   "data": "synthetic", "config": {"workload": args.workload, "genome_bases": wl["genome_bases"],
                                                   "reads_per_gpu": wl["reads"], "index": index_info,
                                                   "per_rank": per_rank}}
-        print(json.dumps(result), flush=True)
+        print(json.dumps(result), file=_RESULT_OUT, flush=True)
     if dist:
         dist.barrier()
         shared_index.cleanup(rank, world)
@@ -456,6 +470,7 @@ def main():
                          "shard instead of the GPU aligner; the line is marked `standin` and is not a measurement")
     args = ap.parse_args()
     self_launch(args, sys.argv[1:])
+    _stdout_to_stderr()
     wl = dict(WORKLOADS[args.workload])
     if args.reads:
         wl["reads"] = args.reads
@@ -749,7 +764,7 @@ def main():
             "parity": parity,
         }
         result.update(extras)
-        print(json.dumps(result), flush=True)
+        print(json.dumps(result), file=_RESULT_OUT, flush=True)
     if dist:
         dist.barrier()
         shared_index.cleanup(rank, world)

@@ -202,8 +202,7 @@ __device__ __forceinline__ int lv_group(GroupLdsT<NW> &G, uint8_t (*rows8)[WAVE]
                     if ((gm >> lp) & 1) { wd = j; break; }
                     if (j > 0 && ((gm >> ln) & 1)) { wd = -j; break; }
                 }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                __asm__ volatile("" ::: "memory");   // the row stores before the backtrace reads (wave_sync)
                 // backtrace; the action of a cell is recomputed from the previous row exactly
                 // as the row step chose it (X, then D, then I if strictly greater).  L of the
                 // current cell is carried (patternLen at the hit); the three cells of row
