@@ -15,3 +15,4 @@ for i in 1 2; do for v in cur hm; do
 done; done
 rm -f /dev/shm/snapgpu_ab_c3.bin
 cat gpurun_out/r03s/c3_ab.log
+timeout -k 10 400 python -u tools/rna_probe.py > gpurun_out/r03s/rna_probe.log 2>&1 || exit $?; tail -1 gpurun_out/r03s/rna_probe.log
