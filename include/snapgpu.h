@@ -709,6 +709,8 @@ typedef struct snapgpu_rna_paired_stats {
     double countMs;    /* spacing / MAPQ adjustments and the GTF read counts (after seedMs) */
     uint64_t subBatches;   /* pipelined sub-batches (SNAPGPU_RNA_SUBBATCH pairs each; default: one): the
                               stage times above are sums over them and overlap one another in wallMs */
+    double cigarGpuMs;  /* of cigarMs: the CIGAR batches (genome and transcriptome threads) */
+    double spliceMs;    /* of cigarMs: insertSpliceJunctions of the transcriptome records */
 } snapgpu_rna_paired_stats_t;
 
 /* pairedAligner: the genome aligner (snapgpu_paired_aligner_create with the paired CLI defaults);

@@ -81,7 +81,28 @@ struct Alignment {
     bool isTranscriptome = false;
     std::string transcriptId, geneId;
 };
-typedef std::map<std::string, Alignment> AlignmentMap;   // alignment_map, keyed by rname_pos
+// alignment_map (AlignmentFilter.h: std::map<string, Alignment> keyed by rname_pos): a vector kept
+// sorted by key -- the map's iteration order -- with the same find / insert / replace semantics; a
+// mate holds a few entries, and clear() keeps the storage, so a pair allocates no tree nodes
+struct AlignmentMap {
+    std::vector<std::pair<std::string, Alignment>> v;
+    void clear() { v.clear(); }
+    std::vector<std::pair<std::string, Alignment>>::iterator begin() { return v.begin(); }
+    std::vector<std::pair<std::string, Alignment>>::iterator end() { return v.end(); }
+    // the entry of `key` (inserted default when absent); *isNew says which
+    Alignment &at(std::string &&key, bool *isNew) {
+        auto it = std::lower_bound(v.begin(), v.end(), key,
+                                   [](const std::pair<std::string, Alignment> &e, const std::string &k) { return e.first < k; });
+        *isNew = it == v.end() || it->first != key;
+        if (*isNew) it = v.emplace(it, std::move(key), Alignment());
+        return it->second;
+    }
+    const Alignment *find(const std::string &key) const {
+        auto it = std::lower_bound(v.begin(), v.end(), key,
+                                   [](const std::pair<std::string, Alignment> &e, const std::string &k) { return e.first < k; });
+        return it != v.end() && it->first == key ? &it->second : nullptr;
+    }
+};
 
 // AlignmentPair (AlignmentFilter.cpp:63-98): score unsigned, distance int (unsigned differences)
 struct AlignmentPair {
@@ -147,10 +168,10 @@ void addAlignment(const Ctx &C, AlignmentMap &mate0, AlignmentMap &mate1, uint32
     if (pos == 0) return;
     AlignmentMap &m = isMate0 ? mate0 : mate1;
     std::string key = rname + '_' + std::to_string(pos);
-    auto it = m.find(key);
     // replaced only by a lower score, or an equal transcriptome score (the element stays put)
-    if (it != m.end() && !(score < it->second.score || (score == it->second.score && isT))) return;
-    Alignment &a = it != m.end() ? it->second : m.emplace(std::move(key), Alignment()).first->second;
+    if (const Alignment *cur = m.find(key); cur && !(score < cur->score || (score == cur->score && isT))) return;
+    bool isNew;
+    Alignment &a = m.at(std::move(key), &isNew);
     a.location = location; a.direction = direction; a.score = score; a.mapq = mapq; a.rname = std::move(rname);
     a.pos = pos; a.posEnd = posEnd; a.posOriginal = posOriginal; a.isTranscriptome = isT;
     a.transcriptId = std::move(tid); a.geneId = std::move(gid);
@@ -353,7 +374,7 @@ struct RnaSub {
     std::vector<std::string> parts;           // the SAM lines / BAM records of [a, b), in order
     uint64_t single = 0, multi = 0, notFound = 0, partialPairs = 0, partialMatches = 0, seedRuns = 0;
     uint64_t transcriptomeRecords = 0;
-    double alignMs = 0, filterMs = 0, seedMs = 0, countMs = 0, cigarMs = 0, writeMs = 0;
+    double alignMs = 0, filterMs = 0, seedMs = 0, countMs = 0, cigarMs = 0, writeMs = 0, cigarGpuMs = 0, spliceMs = 0;
     int rc = SNAPGPU_OK;
     std::string err;
     RnaSub() = default;
@@ -597,6 +618,7 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
         X.transcriptomeRecords += tc[k].loc.size();
     }
     {
+        const auto tg0 = std::chrono::steady_clock::now();
         int grc = SNAPGPU_OK, rc = SNAPGPU_OK;
         std::string gerr, terr;
         auto genomeCigars = [&] {
@@ -614,8 +636,10 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
         else if (rc == SNAPGPU_OK) genomeCigars();
         if (rc) { X.fail(rc, terr); return; }
         if (grc) { X.fail(grc, gerr); return; }
+        X.cigarGpuMs = msSince(tg0);
     }
     // transcriptome records: computeCigarString's tokens through insertSpliceJunctions
+    const auto ts0 = std::chrono::steady_clock::now();
     const Genome &tg = *Rr.ti->genome;
     std::vector<std::string> splice[2];
     for (int k = 0; k < 2; k++) {
@@ -647,6 +671,7 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
             }
         });
     }
+    X.spliceMs = msSince(ts0);
     X.cigarMs = msSince(t0);
     // writePair (ReadWriter.cpp:133-217): the end at the lower location first
     t0 = std::chrono::steady_clock::now();
@@ -895,6 +920,7 @@ int snapgpu_rna_paired_align(snapgpu_paired_aligner_t *pa, snapgpu_aligner_t *ta
         st.transcriptomeRecords += x->transcriptomeRecords;
         st.alignMs += x->alignMs; st.filterMs += x->filterMs; st.seedMs += x->seedMs; st.countMs += x->countMs;
         st.cigarMs += x->cigarMs; st.writeMs += x->writeMs;
+        st.cigarGpuMs += x->cigarGpuMs; st.spliceMs += x->spliceMs;
     }
     if (samPath) {
         const auto t1 = std::chrono::steady_clock::now();

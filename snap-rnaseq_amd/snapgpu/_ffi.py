@@ -193,7 +193,8 @@ class RnaPairedStats(C.Structure):
     _fields_ = [(f, C.c_uint64) for f in ("totalPairs", "usefulPairs", "singleHits", "multiHits", "notFound",
                                           "transcriptomeRecords", "partialPairs", "partialMatches", "seedRuns")] + \
                [(f, C.c_double) for f in ("alignMs", "filterMs", "seedMs", "cigarMs", "writeMs", "wallMs", "prepMs",
-                                           "countMs")] + [("subBatches", C.c_uint64)]
+                                           "countMs")] + [("subBatches", C.c_uint64)] + \
+               [(f, C.c_double) for f in ("cigarGpuMs", "spliceMs")]
 
 
 class SingleStats(C.Structure):
