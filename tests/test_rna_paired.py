@@ -186,3 +186,19 @@ pipelined sub-batches (subbatch 29).  As for
     assert not bad, f"{len(bad)} records differ:\n" + "\n".join(f"#{k} {d}" for k, d in diffs)
     paired = sum(1 for r in want if _bam_fields(r)["flag"] & 0x2)
     assert paired > 100 and extra <= len(want) // 50, (paired, extra)
+
+
+@pytest.mark.gpu
+def test_rna_paired_through_big_arena_pass_matches_reference(gpu_available, tmp_path, monkeypatch):
+    """The whole RNA paired product path with every aligner's arena capped at 32 elements: the
+    transcriptome multi-hit reads, the chimeric fallback's reads and the reads of the seed census
+    that outgrow it are aligned again by the big-arena pass (align_kernel<512> on worst-case arenas);
+    the 2 x 150 SAM records still equal the reference CLI's."""
+    monkeypatch.setenv("SNAPGPU_ARENA_CAP", "32")
+    test_rna_paired_product_path_matches_reference(gpu_available, tmp_path, 0, "rna150", None)
+    gtf, gidx, tidx = _indexes(tmp_path)
+    ta = snapgpu.BaseAligner(tidx, maxHitsToConsider=16000, maxK=15, maxSeedsToUse=8, extraSearchDepth=2)
+    r0 = snapgpu.Reads.from_fastq(os.path.join(G, "rna150_1.fq"))
+    r0.clip(3)
+    ta.AlignReadsEx(r0, maxHitsToGet=1000)
+    assert ta.timing()["nArenaOverflow"] > 0   # the cap really sent reads through the big-arena pass
