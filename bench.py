@@ -717,7 +717,13 @@ def main():
                    "per_core_reads_per_s": ns / cdt / nthr, "host": cpus,
                    "note": "cores = the CPUs this job may use (affinity mask capped by the cgroup quota); "
                            "nproc counts the whole host"}
-            parity = {"reads_compared": ns, "mismatches": int(len(mismatches(res[:ns], cres)))}
+            parity = {"reads_compared": ns, "mismatches": int(len(mismatches(res[:ns], cres))),
+                      "against": "oracle/snap_oracle.c (pinned bit-exact to the compiled reference by "
+                                 "tests/test_oracle_golden.py)" + (
+                                     "; the reference's own digest of all C2 records is tests/test_gpu_golden.py's"
+                                     if args.workload == "c2" else
+                                     "; no reference digest at this size (the compiled reference needs more RAM "
+                                     "than the build container has)")}
             if "sam_records" in extras:   # CIGAR parity on a 20k-read sample
                 from oracle_ffi import oracle_cigars
                 nc = min(20000, wl["reads"])
