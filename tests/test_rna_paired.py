@@ -190,11 +190,11 @@ pipelined sub-batches (subbatch 29).  As for
 
 @pytest.mark.gpu
 def test_rna_paired_through_big_arena_pass_matches_reference(gpu_available, tmp_path, monkeypatch):
-    """The whole RNA paired product path with every aligner's arena capped at 32 elements: the
+    """The whole RNA paired product path with every aligner's arena capped at 2 elements: the
     transcriptome multi-hit reads, the chimeric fallback's reads and the reads of the seed census
     that outgrow it are aligned again by the big-arena pass (align_kernel<512> on worst-case arenas);
     the 2 x 150 SAM records still equal the reference CLI's."""
-    monkeypatch.setenv("SNAPGPU_ARENA_CAP", "32")
+    monkeypatch.setenv("SNAPGPU_ARENA_CAP", "2")
     test_rna_paired_product_path_matches_reference(gpu_available, tmp_path, 0, "rna150", None)
     gtf, gidx, tidx = _indexes(tmp_path)
     ta = snapgpu.BaseAligner(tidx, maxHitsToConsider=16000, maxK=15, maxSeedsToUse=8, extraSearchDepth=2)
