@@ -117,14 +117,16 @@ def load_pmc(sha, src_sha):
 
 def valu_cycles():
     """SIMD cycles one wave64 VALU instruction of align_kernel<128>'s mix occupies at 4 waves/SIMD:
-    the mean of the measured op kinds (profiles/r03/valu_rates.json, tools/gpu/valu_rates.hip) or
-    the guide's 2 cycles."""
+    the median of the measured op kinds (profiles/r03/valu_rates.json, tools/gpu/valu_rates.hip) or
+    the guide's 2 cycles.  The median, not the mean: the back-to-back v_cndmask_b32 (vcc) chain
+    costs 12.7 cycles (a vcc read-after-write stall on every instruction), which the kernel never
+    issues -- its vcc selects follow a v_cmp, measured at 2.66 -- and alone lifts the mean to 3.62."""
     p = os.path.join(ROOT, "profiles", "r03", "valu_rates.json")
     if os.path.exists(p):
         d = json.load(open(p))
         xs = [r["w4"]["cycles_per_instr_per_simd"] for r in d["rates"] if not r["instruction"].startswith("v_readlane")]
         if xs:
-            return float(np.mean(xs)), f"profiles/r03/valu_rates.json (mean of {len(xs)} op kinds at 4 waves/SIMD)"
+            return float(np.median(xs)), f"profiles/r03/valu_rates.json (median of {len(xs)} op kinds at 4 waves/SIMD)"
     return 2.0, "MI355X_MICROARCH.md: wave64 on a 32-lane SIMD"
 
 
