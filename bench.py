@@ -609,9 +609,10 @@ def main():
                                          "note": "64-B lines per random access (SURVEY 8(d) d3)"},
                     "launches_per_step": n_launch, "reads_per_launch": reads_launch,
                     "algorithmic_bytes_per_launch": bytes_launch, "algorithmic_bytes_per_read": bytes_all / len(res),
-                    "binding_resource": "instruction issue of one serial wave per read (VALU issue 0.66 of what 4 "
-                                        "waves/SIMD can give, plus dependent memory round trips), not HBM "
-                                        "bandwidth (DESIGN.md section 4)",
+                    "binding_resource": "instruction issue of one serial wave per read (VALU issue "
+                                        + (f"{valu_issue['pipe_occupancy']:.2f}" if valu_issue else "0.66-0.70")
+                                        + " of what 4 waves/SIMD can give, plus dependent memory round trips), "
+                                        "not HBM bandwidth (DESIGN.md section 4)",
                     "valu_issue": valu_issue, "pmc_source": pmc_src, "lib_sha256": sha,
                     "kernel_source_sha256": src_sha}
         counts = {int(k): int(v) for k, v in zip(*np.unique(res["result"], return_counts=True))}
@@ -653,11 +654,13 @@ def main():
                       "frac": lk_bytes / lk_s / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": lk_bytes,
                       "seeds_per_launch": t["lookupSeeds"] / t["nLaunches"],
                       "probes_per_launch": t["lookupProbes"] / t["nLaunches"],
-                      # the probes the align kernel makes itself (seeds past the first round, reads the
-                      # pass-0 records do not cover): the records' per-read total minus pass 0's
-                      "in_kernel_probes_per_read": float(res["nProbes"].astype(np.int64).sum() - t["lookupProbes"]) /
-                                                   len(res),
-                      "pass0_probes_per_read": t["lookupProbes"] / len(res)}
+                      # pass 0 looks up SEEDS_PER_READ (16) seeds of every read speculatively; a read
+                      # applies fewer (the reference stops after <= 13 lookups), so its record's nProbes
+                      # (the probes of the seeds it used, from pass 0's records or probed in the align
+                      # kernel) is not pass 0's count plus an in-kernel remainder: both are reported
+                      "pass0_probes_per_read": t["lookupProbes"] / len(res),
+                      "pass0_probes_per_seed": t["lookupProbes"] / max(1, t["lookupSeeds"]),
+                      "applied_probes_per_read": float(res["nProbes"].astype(np.int64).sum()) / len(res)}
             # measured ceilings: random 12-B slot gathers from the resident table (>= 2^28 loads) and a
             # streaming copy (4 GiB read + 4 GiB written)
             n_g = 1 << 28
