@@ -493,12 +493,28 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem1
         PH_CNT(A, S, PH_NSUCC, 1);
         const int s0 = readlane(P.s, ln), t0 = s0 + (int)A.seedLen;
         const uint32_t dir = cKey & 1;
+        const uint32_t ebase = (cKey >> 1) * ELEM;
+        const uint32_t elemLoc = ebase + cbit;
+        // the nearby element (BaseAligner.cpp:1272-1331) does not depend on the match probability:
+        // found and loaded before lv_prob_pair, so its chain walk and load overlap the product
+        uint32_t nbPre;
+        int csPre = -1;
+        uint32_t nvPre = 0;
+        {
+            const uint32_t nl = elemLoc + (2 * (elemLoc % ELEM / (ELEM / 2)) - 1) * (ELEM / 2);
+            const uint32_t nkey = ((nl / ELEM) << 1) | dir;
+            nbPre = uni(chain_find(A, S, ar, nkey, (uint32_t)A.arenaElems));
+            if (nbPre != NONE) {
+                const uint64_t inb = ballot((uint32_t)lane < nb && G.eidx[lane < EB ? lane : 0] == nbPre);
+                csPre = inb ? (int)__builtin_ctzll(inb) : -1;
+                if (csPre >= 0) nvPre = lane < 12 ? G.ecache[csPre][lane] : 0u;
+                else nvPre = lane < 12 ? ((const uint32_t *)(ar + nbPre))[lane] : 0u;
+            }
+        }
         double q1, q2;
         int net2;
         lv_prob_pair(tab, G, gs, gs * 2 * GS, (int)n, s0, t0, dir ? S.rcQ : S.fwdQ, q1, q2, net2);
         const double prob = q1 * q2 * tab->seedProb;
-        const uint32_t ebase = (cKey >> 1) * ELEM;
-        const uint32_t elemLoc = ebase + cbit;
         const uint32_t loc = elemLoc + (uint32_t)net2;
         const bool anyNearby0 = cScored != 0;
         cScored |= 1ull << cbit;
@@ -510,17 +526,9 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem1
         uint32_t nb2 = NONE;
         int cs = -1;
         uint32_t nv = 0;
-        if (take) {
-            const uint32_t nl = elemLoc + (2 * (elemLoc % ELEM / (ELEM / 2)) - 1) * (ELEM / 2);
-            const uint32_t nkey = ((nl / ELEM) << 1) | dir;
-            nb2 = uni(chain_find(A, S, ar, nkey, (uint32_t)A.arenaElems));
-        }
+        if (take) { nb2 = nbPre; cs = csPre; nv = nvPre; }
         if (nb2 != NONE) {
-            // the nearby element may be in this batch: its cache is authoritative
-            const uint64_t inb = ballot((uint32_t)lane < nb && G.eidx[lane < EB ? lane : 0] == nb2);
-            cs = inb ? (int)__builtin_ctzll(inb) : -1;
-            if (cs >= 0) nv = lane < 12 ? G.ecache[cs][lane] : 0u;
-            else nv = lane < 12 ? ((const uint32_t *)(ar + nb2))[lane] : 0u;
+            // the nearby element may be in this batch: its cache is authoritative (read above)
             if (rl64(nv, 2) == 0) nb2 = NONE;   // nearby element not scored yet
             if (nb2 != NONE) {
                 const uint32_t nbase = (rl(nv, 6) >> 1) * ELEM;

@@ -6,7 +6,7 @@ L=snap-rnaseq_amd/snapgpu
 for i in 1 2; do
   for v in cur "$@"; do
     if [ "$v" = cur ]; then lib=$PWD/$L/libsnapgpu.so; else lib=$PWD/$L/libsnapgpu_$v.so; fi
-    SNAPGPU_LIB=$lib timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/abn_${v}_$i.log 2>&1 || exit $?
+    SNAPGPU_LIB=$lib timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/abn_${v}_$i.log 2> gpurun_out/abn_${v}_$i.err || exit $?
   done
 done
 python3 - "$@" <<'PY'
