@@ -52,27 +52,29 @@ WORKLOADS = {
 
 
 def algorithmic_bytes(res):
-    """B_read = 2*readLen + 16 + 12*P + 4*(H + V) + (readLen + MAX_K)*S."""
+    """B_read = 2*readLen + 16 + 64*P + 4*(H + V) + (readLen + MAX_K)*S, P = 64-B bucket
+    lines of the seed tables' device image (csrc/bucket_table.h) the read's lookups loaded (the reference's
+    12-B slot probes before round 4: the line is now the unit a lookup reads)."""
     P = res["nProbes"].astype(np.int64).sum()
     H = res["nHitWords"].astype(np.int64).sum()
     V = res["nOverflowLists"].astype(np.int64).sum()
     S = res["nLocationsScored"].astype(np.int64).sum()
     n = len(res)
-    return int(n * (2 * READ_LEN + 16) + 12 * P + 4 * (H + V) + (READ_LEN + MAX_K) * S), dict(
+    return int(n * (2 * READ_LEN + 16) + 64 * P + 4 * (H + V) + (READ_LEN + MAX_K) * S), dict(
         P=P / n, H=H / n, V=V / n, S=S / n)
 
 
 def granule_bytes(res):
     """SURVEY.md 8(d) d3, granule-adjusted: every random access moves whole 64-B lines -- the read's
-    bases and qualities, its record, one line per hash probe, per overflow list its count line plus
-    ceil(4 H / 64) hit lines, and per LV-scored candidate the genome window's lines
+    bases and qualities, its record, one line per bucket line probed, per overflow list
+    ceil(4 H / 64) hit lines (the list length travels in the bucket entry), and per LV-scored candidate the genome window's lines
     (64 * ceil((readLen + MAX_K) / 64), the byte genome of the reference's layout)."""
     P = res["nProbes"].astype(np.int64)
     H = res["nHitWords"].astype(np.int64)
     V = res["nOverflowLists"].astype(np.int64)
     S = res["nLocationsScored"].astype(np.int64)
     line = 64
-    per_read = (2 * line * -(-READ_LEN // line) + line + line * P + line * (V + (4 * H + line - 1) // line) +
+    per_read = (2 * line * -(-READ_LEN // line) + line + line * P + line * ((4 * H + line - 1) // line) +
                 line * -(-(READ_LEN + MAX_K) // line) * S)
     return int(per_read.sum())
 
@@ -304,7 +306,7 @@ def rna_roofline(ta, r0):
     H = res["nHitWords"].astype(np.int64)
     V = res["nOverflowLists"].astype(np.int64)
     S = res["nLocationsScored"].astype(np.int64)
-    b = int((2 * lens + 16 + 12 * P + 4 * (H + V) + (lens + MAX_K) * S).sum())
+    b = int((2 * lens + 16 + 64 * P + 4 * (H + V) + (lens + MAX_K) * S).sum())
     ms = float(min(ks))
     return {"kernel": "align_kernel<256, false> (+ the <512> byte pass and the big-arena pass over the reads "
                       "that outgrew a capped arena)", "reads": int(r0.n), "arena_overflow_reads": ovf,
@@ -633,9 +635,9 @@ def main():
                                   "same_results": bool(np.array_equal(rres.view(np.uint8), res.view(np.uint8))),
                                   "note": "reads already in HBM, records left in HBM (snapgpu_align_resident)"}
             # seed_lookup_kernel (pass 0) measured with the two streams' pass sets serialised, so
-            # no align kernel shares the GPU with it: read bytes + offsets/lengths + 8 records of
-            # 16 B per read, then per looked-up seed its table's (size, base), 12 B per probed
-            # entry, 4 B per overflow count
+            # no align kernel shares the GPU with it: read bytes + offsets/lengths + 16 records of
+            # 16 B per read, then per looked-up seed its table's (bucket base, count), 64 B per
+            # bucket line loaded, 4 B per saturated overflow count re-read from its list
             aligner.set_overlap(False)
             lookup_ms, lk_busy_ms, launches = [], [], []
             for _ in range(3):
@@ -646,7 +648,7 @@ def main():
                 lk_busy_ms.append(t["lookupKernelBusyMs"])
                 launches.append(t["nLaunches"])
             aligner.set_overlap(True)
-            lk_bytes = int(wl["reads"] * (READ_LEN + 12 + 128) + 16 * t["lookupSeeds"] + 12 * t["lookupProbes"] +
+            lk_bytes = int(wl["reads"] * (READ_LEN + 12 + 256) + 12 * t["lookupSeeds"] + 64 * t["lookupProbes"] +
                            4 * t["lookupOverflowReads"]) / t["nLaunches"]
             lk_s = float(np.mean(lk_busy_ms)) / float(np.mean(launches)) / 1000.0
             lookup = {"kernel": "seed_lookup_kernel", "kernel_ms_per_launch": lk_s * 1000.0,
@@ -661,12 +663,13 @@ def main():
                       "pass0_probes_per_read": t["lookupProbes"] / len(res),
                       "pass0_probes_per_seed": t["lookupProbes"] / max(1, t["lookupSeeds"]),
                       "applied_probes_per_read": float(res["nProbes"].astype(np.int64).sum()) / len(res)}
-            # measured ceilings: random 12-B slot gathers from the resident table (>= 2^28 loads) and a
+            # measured ceilings: random 64-B bucket-line gathers from the resident image (2^28 lines) and a
             # streaming copy (4 GiB read + 4 GiB written)
             n_g = 1 << 28
             g_ms = aligner.gather_peak_ms(n_g)
             lookup["gather_peak"] = {"loads": n_g, "ms": g_ms, "loads_per_s": n_g / (g_ms / 1000.0),
-                                     "note": "independent random 12-B slot loads, best of 3"}
+                                     "note": "independent random 64-B bucket-line loads, best of 3"}
+            lookup["bucket_image"] = aligner.bucket_info()
             lookup["probe_rate_frac_of_gather_peak"] = (lookup["probes_per_launch"] / lk_s) / (n_g / (g_ms / 1000.0))
             c_bytes = 4 << 30
             c_ms = aligner.copy_peak_ms(c_bytes)

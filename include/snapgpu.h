@@ -79,7 +79,7 @@ typedef struct snapgpu_result {
     uint32_t nLocationsScored;    /* getLocationsScored() delta */
     uint16_t popularSeedsSkipped; /* BaseAligner::popularSeedsSkipped */
     uint16_t nHitsIgnored;        /* getNHitsIgnoredBecauseOfTooHighPopularity() delta */
-    uint32_t nProbes;             /* hash-table entries probed (roofline P) */
+    uint32_t nProbes;             /* 64-B bucket lines of the seed-table image loaded (roofline P; device statistic) */
     uint32_t nHitWords;           /* hit words consumed (roofline H) */
     uint32_t nOverflowLists;      /* overflow lists visited (roofline V) */
     uint32_t nElements;           /* candidate elements allocated (BaseAligner.cpp:1485-1568) */
@@ -328,7 +328,7 @@ typedef struct snapgpu_timing {
     uint64_t nMapqFixed;
     double lookupKernelMs;   /* pass 0: seed_lookup_kernel (first-round seed lookups) */
     uint64_t lookupSeeds;    /* seeds it looked up */
-    uint64_t lookupProbes;   /* hash-table entries it probed */
+    uint64_t lookupProbes;   /* bucket lines it loaded */
     uint64_t lookupOverflowReads; /* overflow-list counts it read */
     uint64_t nLaunches;      /* pass sets the figures above sum over (chunks of snapgpu_align_batch) */
     double wallMs;           /* snapgpu_align_batch: host reads in -> records out, whole call */
@@ -542,9 +542,31 @@ const snapgpu_index_t *snapgpu_aligner_index(const snapgpu_aligner_t *a);
 int snapgpu_aligner_get_params(const snapgpu_aligner_t *a, snapgpu_aligner_params_t *p);
 
 /* Roofline calibration (diagnostic, no reference equivalent): time of nLoads independent
- * 12-byte SNAPHashTable slot loads at hashed positions of this aligner's resident table
+ * 64-byte bucket-line loads at hashed positions of this aligner's resident bucket image
  * (the access pattern of the seed lookups without their dependency chain), best of 3, ms. */
 int snapgpu_gather_peak(snapgpu_aligner_t *a, uint32_t nLoads, double *ms);
+
+/* The device image of the seed tables (no reference equivalent: SNAPHashTable's key -> value map
+ * re-laid into 64-byte buckets of four {key, value1, value2, counts} entries when the aligner is
+ * created; GenomeIndex::lookupSeed answers are unchanged).  Diagnostic figures of that image. */
+typedef struct snapgpu_bucket_info {
+    uint64_t nSlots;            /* reference-format slots the image was built from */
+    uint64_t nKeys;             /* keys it holds (slots SNAPHashTable::Lookup can return) */
+    uint64_t nBuckets;          /* 64-byte buckets */
+    uint64_t nOverflowBuckets;  /* buckets flagged: a key homed there lives in a later bucket */
+    uint64_t maxDisplacement;   /* most buckets a key lives past its home */
+    uint64_t bytes;             /* HBM of the image */
+    double buildMs;             /* slots upload + count + build, wall */
+} snapgpu_bucket_info_t;
+int snapgpu_aligner_bucket_info(const snapgpu_aligner_t *a, snapgpu_bucket_info_t *info);
+/* GenomeIndex::lookupSeed + fillInLookedUpResults (GenomeIndex.cpp:971-1086, unwindowed) of n seeds
+ * (seedLen ACGT bases each, concatenated) on the device, through the bucket image: mode 0 = one lane
+ * per seed (the lookup of seed_lookup_kernel and the paired kernel), 1 = the whole wave per seed (the
+ * aligner's and CharacterizeSeeds' in-kernel lookups).  out[6 i ..]: hits forward, hits RC,
+ * hash of the forward hits, of the RC hits (acc = acc * 1000003 + hit, list order, mod 2^64),
+ * first forward hit, first RC hit (~0 when none); lines[i] = bucket lines loaded. */
+int snapgpu_aligner_lookup_seeds(snapgpu_aligner_t *a, const char *seedBases, uint64_t n, int mode, uint64_t *out,
+                                 uint32_t *lines);
 
 /* HBM streaming-copy ceiling (diagnostic): best-of-3 time (ms) of copy_peak_kernel reading
  * `bytes` and writing `bytes` with 16-byte vector accesses. */

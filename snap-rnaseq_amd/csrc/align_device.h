@@ -14,7 +14,8 @@
 //   MAPQ        mapq.h:32-65
 //
 // Lane roles:
-//   * hash-probe: lane j loads probe j of SNAPHashTable's probe sequence.
+//   * hash-probe: lanes 0-7 load the 16-B entries of a key's home bucket and the next one
+//     (bucket_table.h).
 //   * hit insertion: lane i handles hit i of a 64-hit batch; duplicates inside
 //     the batch are grouped through an LDS table and applied in hit order by
 //     the group's first lane (so FIFO/weight semantics are exactly sequential).
@@ -94,10 +95,11 @@ static_assert(sizeof(GPlane) == 12, "GPlane layout");
 
 struct KArgs {
     uint32_t *diag;              // this aligner's watchdog record {code, read, detail, 0} (diag_report)
-    // index (HBM)
-    const uint32_t *slots;
-    const uint64_t *tableBase;
-    const uint64_t *tableSize;
+    // index (HBM): the seed tables as 64-B buckets (bucket_table.h), per table base (in buckets)
+    // and bucket count; the overflow lists as the reference stores them
+    const uint4 *buckets;
+    const uint64_t *bucketBase;
+    const uint32_t *bucketCount;
     const uint32_t *overflow;
     const char *genome;          // base 0; >= 256 guard bytes each side
     const uint32_t *pieces;

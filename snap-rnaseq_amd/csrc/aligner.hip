@@ -21,6 +21,8 @@
 
 using namespace sgk;
 
+int snapgpu_internal_index_args(const snapgpu_aligner_t *a, sgk::KArgs *A, int *device);   // below
+
 namespace sgk {
 
 // ------------------------------------------------------------------ score()
@@ -491,7 +493,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
                     wave_sync();
                 }
                 bool found = false, comp = false, pal = false, pre = false;
-                uint32_t v1 = 0, v2 = 0, pcnt = 0;
+                uint32_t v1 = 0, v2 = 0, cntF = 0, cntR = 0;   // overflow-list lengths, value-forward / -reverse side
                 if (pfIdx < (uint32_t)SEEDS_PER_READ) {
                     const uint32_t meta = readlaneu(srec, 4 * pfIdx);
                     pre = (meta >> 31) && (meta & 0xff) == next && ((meta >> 16) & 0x7fff) != 0x7fff;
@@ -500,7 +502,8 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
                         sv_add(st, lane, SV_PROBES, (meta >> 16) & 0x7fff);
                         v1 = readlaneu(srec, 4 * pfIdx + 1);
                         v2 = readlaneu(srec, 4 * pfIdx + 2);
-                        pcnt = readlaneu(srec, 4 * pfIdx + 3);
+                        const uint32_t pcnt = readlaneu(srec, 4 * pfIdx + 3);   // u16 each, saturated (maxHits < 0xffff)
+                        cntF = pcnt & 0xffff; cntR = pcnt >> 16;
                         pfIdx++;
                     }
                 }
@@ -518,28 +521,14 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
                 const uint64_t canon = comp ? rcv : f;
                 const uint32_t table = (uint32_t)(canon >> 32);
                 const uint32_t key = (uint32_t)canon;
-                const uint32_t size = (uint32_t)A.tableSize[table];   // < 2^31 (snapgpu_aligner_create)
-                const uint32_t *T = A.slots + 3 * A.tableBase[table];
-                const uint32_t h0 = fmix32(key) % size;
-                for (uint32_t j0 = 0;; j0 += 8) {
-                    uint32_t j = j0 + (lane & 7);
-                    const uint32_t S_j = j <= 4 ? j * (j + 1) * (2 * j + 1) / 6 : 30 + (j - 4);
-                    uint64_t pos = h0 + S_j;
-                    if (pos >= size) pos %= size;
-                    uint32_t kj = 0, v1j = INVALID, v2j = 0;
-                    bool beyond = j > size + 5;
-                    if (lane < 8 && !beyond) { kj = T[3 * pos]; v1j = T[3 * pos + 1]; v2j = T[3 * pos + 2]; }
-                    bool stop = (j == 0) ? (kj == key && v1j != INVALID) : (kj == key || v1j == INVALID);
-                    uint64_t m = ballot(lane < 8 && (stop || beyond)) & 0xffull;
-                    if (m) {
-                        int jl = __builtin_ctzll(m);
-                        uint32_t jj = j0 + jl;
-                        bool bey = readlane(beyond ? 1 : 0, jl);
-                        sv_add(st, lane, SV_PROBES, bey ? jj : jj + 1);
-                        uint32_t kv1 = readlaneu(v1j, jl);
-                        if (!bey && (jj == 0 || kv1 != INVALID)) { found = true; v1 = kv1; v2 = readlaneu(v2j, jl); }
-                        break;
-                    }
+                uint32_t aux = 0, lines = 0;   // the bucket image (bucket_table.h): home line + the next
+                found = bucket_lookup_wave(A, table, key, lane, v1, v2, aux, lines);
+                sv_add(st, lane, SV_PROBES, lines);
+                if (found) {   // the entry's overflow-list lengths (a saturated one re-read from the list)
+                    const uint32_t c1 = aux & BK_CSAT, c2 = (aux >> 15) & BK_CSAT;
+                    const uint32_t vf = comp ? v2 : v1, vr = comp ? v1 : v2;
+                    if (vf >= A.nBases && vf != UNUSED_SIDE) cntF = uni(bucket_count(A, comp ? c2 : c1, vf));
+                    if (vr >= A.nBases && vr != UNUSED_SIDE) cntR = uni(bucket_count(A, comp ? c1 : c2, vr));
                 }
                 }
                 if (overdue(A, st, 6)) break;
@@ -551,7 +540,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
                     if (vf < A.nBases) { nH0 = 1; sg0 = vf; }
                     else if (vf != UNUSED_SIDE) {
                         uint32_t o = vf - A.nBases;
-                        nH0 = pre ? (pcnt & 0xffff) : uni(A.overflow[o]);
+                        nH0 = cntF;
                         ls0 = A.overflow + o + 1;
                         sv_add(st, lane, SV_OVF, 1);
                     }
@@ -559,7 +548,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
                     else if (vr < A.nBases) { nH1 = 1; sg1 = vr; }
                     else if (vr != UNUSED_SIDE) {
                         uint32_t o = vr - A.nBases;
-                        nH1 = pre ? (pcnt >> 16) : uni(A.overflow[o]);
+                        nH1 = cntR;
                         ls1 = A.overflow + o + 1;
                         sv_add(st, lane, SV_OVF, 1);
                     }
@@ -978,8 +967,12 @@ struct snapgpu_aligner {
     int device = 0;
     const snapgpu_index_t *idx = nullptr;
     snapgpu_aligner_params_t p{};
-    uint32_t *dSlots = nullptr, *dOverflow = nullptr, *dPieces = nullptr;
-    uint64_t *dTableBase = nullptr, *dTableSize = nullptr;
+    uint32_t *dOverflow = nullptr, *dPieces = nullptr;
+    // the seed tables' bucket image (bucket_table.h), built on the device at creation
+    uint4 *dBuckets = nullptr;
+    uint64_t *dBucketBase = nullptr;
+    uint32_t *dBucketCount = nullptr;
+    snapgpu_bucket_info_t bucketInfo{};
     char *dGenomeAlloc = nullptr;
     GPlane *dGPlanes = nullptr;   // genome bit planes (KArgs::gpl)
     const char *dGenome = nullptr;
@@ -1047,19 +1040,21 @@ static const size_t kDevGuard = 1024;
 static std::atomic<uint64_t> g_devFrees{0};   // hipFree calls made by devFree (selftest)
 
 // Random-gather ceiling of the hash-table memory (roofline calibration for
-// seed_lookup_kernel): one independent 12-byte slot load per lane at a
-// hashed position of the resident SNAPHashTable slots -- the lookup kernel's access
-// pattern without its dependency chain.  The xor of the loaded words goes to `sink` only
-// when it equals the salt (practically never), so the loads cannot be dropped.
-__global__ __launch_bounds__(256) void gather_peak_kernel(const uint32_t *slots, uint32_t nSlots, uint32_t nLoads,
+// seed_lookup_kernel): one independent 64-byte bucket line per load, four
+// loads per lane, at hashed positions of the resident bucket image -- the lookup kernel's access
+// pattern (one whole line per lookup, four 16-B loads) without its dependency chain.  The xor of
+// the loaded words goes to `sink` only when it equals the salt (practically never), so the loads
+// cannot be dropped.
+__global__ __launch_bounds__(256) void gather_peak_kernel(const uint4 *buckets, uint32_t nBuckets, uint32_t nLoads,
                                                           uint32_t salt, uint32_t *sink) {
-    const uint32_t i = (blockIdx.x * 256u + threadIdx.x) * 4u;   // 4 independent loads per lane
+    const uint32_t i = (blockIdx.x * 256u + threadIdx.x) * 4u;   // 4 independent lines per lane
     uint32_t x = 0;
 #pragma unroll
     for (uint32_t j = 0; j < 4; j++)
         if (i + j < nLoads) {
-            const uint32_t *p = slots + 3ull * (sgk::fmix32((i + j) ^ salt) % nSlots);
-            x ^= p[0] ^ p[1] ^ p[2];
+            const uint4 *p = buckets + 4ull * (sgk::fmix32((i + j) ^ salt) % nBuckets);
+#pragma unroll
+            for (int q = 0; q < 4; q++) { const uint4 v = p[q]; x ^= v.x ^ v.y ^ v.z ^ v.w; }
         }
     if (x == salt) sink[0] = x;   // data-dependent: the loads stay
 }
@@ -1110,6 +1105,157 @@ __global__ __launch_bounds__(256) void pack_planes_kernel(const char *g, uint64_
         else { if (v & 2) hi |= bit; if (v & 1) lo |= bit; }
     }
     out[w] = sgk::GPlane{hi, lo, nm};
+}
+
+// ------------------------------------------------- bucket image of the seed tables (bucket_table.h)
+// Table of global slot i: tables are concatenated in order (tableBase ascending, sizes >= 1).
+__device__ __forceinline__ uint32_t table_of_slot(const uint64_t *tableBase, uint32_t nTables, uint64_t i) {
+    uint32_t lo = 0, hi = nTables;   // largest t with tableBase[t] <= i
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (tableBase[mid] <= i) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+// SNAPHashTable::Lookup (HashTable.h:74-105) of `key` in table T of `size` slots: the slot it
+// stops at when it reports the key found, else ~0.
+__device__ __forceinline__ uint64_t ref_lookup_slot(const uint32_t *T, uint32_t size, uint32_t key) {
+    const uint32_t h0 = sgk::fmix32(key) % size;
+    for (uint32_t j = 0;; j++) {
+        if (j > size + 5) return ~0ull;
+        const uint32_t S_j = j <= 4 ? j * (j + 1) * (2 * j + 1) / 6 : 30 + (j - 4);
+        uint64_t pos = h0 + S_j;
+        if (pos >= size) pos %= size;
+        const uint32_t kj = T[3 * pos], v1j = T[3 * pos + 1];
+        const bool stop = (j == 0) ? (kj == key && v1j != sgk::INVALID) : (kj == key || v1j == sgk::INVALID);
+        if (stop) return (j == 0 || v1j != sgk::INVALID) ? pos : ~0ull;
+    }
+}
+
+// Per table, the slots the reference's Lookup of their own key returns (the keys the bucket image
+// holds): each thread counts 256 consecutive slots and adds per table it crossed.
+__global__ __launch_bounds__(256) void bucket_count_kernel(const uint32_t *slots, const uint64_t *tableBase,
+                                                           const uint64_t *tableSize, uint32_t nTables,
+                                                           uint64_t nSlots, unsigned long long *cnt) {
+    const uint64_t i0 = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 256u;
+    if (i0 >= nSlots) return;
+    const uint64_t i1 = i0 + 256 < nSlots ? i0 + 256 : nSlots;
+    uint32_t t = table_of_slot(tableBase, nTables, i0);
+    uint64_t end = tableBase[t] + tableSize[t];
+    unsigned long long c = 0;
+    for (uint64_t i = i0; i < i1; i++) {
+        while (i >= end) {
+            if (c) atomicAdd(cnt + t, c);
+            c = 0;
+            t++;
+            end = tableBase[t] + tableSize[t];
+        }
+        if (slots[3 * i + 1] == sgk::INVALID) continue;
+        const uint64_t b = tableBase[t];
+        if (ref_lookup_slot(slots + 3 * b, (uint32_t)tableSize[t], slots[3 * i]) == i - b) c++;
+    }
+    if (c) atomicAdd(cnt + t, c);
+}
+
+// Insert every slot the reference's Lookup returns into its table's buckets: home bucket, else the
+// first later one with a free entry (claimed by CAS on aux), flagging each full bucket passed over.
+// info: [0] keys inserted, [1] buckets flagged, [2] keys that found no room (build error), [3] most
+// buckets a key moved past its home.
+__global__ __launch_bounds__(256) void bucket_build_kernel(const uint32_t *slots, const uint64_t *tableBase,
+                                                           const uint64_t *tableSize, uint32_t nTables, uint64_t nSlots,
+                                                           const uint32_t *overflow, uint64_t nOverflow, uint32_t nBases,
+                                                           uint4 *buckets, const uint64_t *bucketBase,
+                                                           const uint32_t *bucketCount, unsigned long long *info) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < nSlots; i += (uint64_t)gridDim.x * 256u) {
+        const uint32_t v1 = slots[3 * i + 1];
+        if (v1 == sgk::INVALID) continue;
+        const uint32_t t = table_of_slot(tableBase, nTables, i);
+        const uint64_t b0 = tableBase[t];
+        const uint32_t key = slots[3 * i], v2 = slots[3 * i + 2];
+        if (ref_lookup_slot(slots + 3 * b0, (uint32_t)tableSize[t], key) != i - b0) continue;   // unreachable slot
+        uint32_t c[2] = {0, 0};
+        const uint32_t vs[2] = {v1, v2};
+        for (int s = 0; s < 2; s++)   // overflow-list lengths (GenomeIndex.cpp:1013-1086), saturated
+            if (vs[s] >= nBases && vs[s] != sgk::UNUSED_SIDE && (uint64_t)(vs[s] - nBases) < nOverflow) {
+                const uint32_t n = overflow[vs[s] - nBases];
+                c[s] = n < sgk::BK_CSAT ? n : sgk::BK_CSAT;
+            }
+        const uint32_t aux = sgk::BK_OCC | c[0] | (c[1] << 15);
+        const uint32_t nB = bucketCount[t];
+        uint4 *T = buckets + 4ull * bucketBase[t];
+        uint32_t b = sgk::bucket_home(key, nB);
+        bool placed = false;
+        for (uint32_t step = 0; step < nB && !placed; step++) {
+            uint4 *B = T + 4ull * b;
+            for (int e = 0; e < 4; e++) {
+                if (atomicCAS(&B[e].w, 0u, aux) == 0u) {
+                    B[e].x = key; B[e].y = v1; B[e].z = v2;
+                    placed = true;
+                    if (step) atomicMax(info + 3, (unsigned long long)step);
+                    break;
+                }
+            }
+            if (!placed) {
+                if (!(atomicOr(&B[0].w, sgk::BK_OVF) & sgk::BK_OVF)) atomicAdd(info + 1, 1ull);
+                b = sgk::bucket_next(b, nB);
+            }
+        }
+        atomicAdd(info + (placed ? 0 : 2), 1ull);
+    }
+}
+
+// snapgpu_aligner_lookup_seeds: GenomeIndex::lookupSeed + fillInLookedUpResults (GenomeIndex.cpp:
+// 971-1086, unwindowed) of given seeds through the bucket image, by either device lookup: lane per
+// seed (bucket_lookup_lane, mode 0) or the whole wave per seed (bucket_lookup_wave, mode 1).  Per
+// seed: {nFwd, nRc, hash of the forward hits, of the RC hits, first forward hit, first RC hit}, the
+// hash acc = acc * 1000003 + hit over the hits in list order; `lines` = bucket lines loaded.
+__device__ __forceinline__ void lookup_fill(const KArgs &A, uint32_t v, uint32_t c, uint64_t *o) {
+    uint32_t n = 0;
+    uint64_t acc = 0, first = ~0ull;
+    if (v < A.nBases) { n = 1; acc = v; first = v; }
+    else if (v != UNUSED_SIDE) {
+        n = bucket_count(A, c, v);
+        const uint32_t *ls = A.overflow + (v - A.nBases) + 1;
+        for (uint32_t i = 0; i < n; i++) acc = acc * 1000003ull + ls[i];
+        if (n) first = ls[0];
+    }
+    o[0] = n; o[1] = acc; o[2] = first;
+}
+__global__ __launch_bounds__(64) void lookup_seeds_kernel(KArgs A, const char *seeds, uint32_t n, int mode,
+                                                          unsigned long long *out, uint32_t *lines) {
+    const int lane = lane_id();
+    const uint32_t L = A.seedLen;
+    for (uint32_t base = blockIdx.x * 64u; base < n; base += gridDim.x * 64u) {
+        const uint32_t cnt = n - base < 64u ? n - base : 64u;
+        for (uint32_t k = 0; k < (mode ? cnt : 1u); k++) {
+            const uint32_t i = mode ? base + k : base + lane;   // mode 1: seed base+k, uniform
+            if (!mode && (uint32_t)lane >= cnt) break;
+            uint64_t f = 0, rc = 0;
+            for (uint32_t j = 0; j < L; j++) {
+                const int v = base_value((uint8_t)seeds[(uint64_t)i * L + j]) & 3;
+                f |= (uint64_t)v << ((L - j - 1) * 2);
+                rc |= (uint64_t)(v ^ 3) << (j * 2);
+            }
+            const bool comp = (int64_t)f > (int64_t)rc;
+            const uint64_t canon = comp ? rc : f;
+            uint32_t v1 = 0, v2 = 0, aux = 0, ln = 0;
+            const bool found = mode ? bucket_lookup_wave(A, (uint32_t)(canon >> 32), (uint32_t)canon, lane, v1, v2, aux, ln)
+                                    : bucket_lookup_lane(A, (uint32_t)(canon >> 32), (uint32_t)canon, v1, v2, aux, ln);
+            if (mode && lane != 0) continue;
+            uint64_t o[6] = {0, 0, 0, 0, ~0ull, ~0ull};
+            if (found) {
+                const uint32_t c1 = aux & BK_CSAT, c2 = (aux >> 15) & BK_CSAT;
+                uint64_t a[3], b[3];
+                lookup_fill(A, comp ? v2 : v1, comp ? c2 : c1, a);
+                if (f == rc) { b[0] = a[0]; b[1] = a[1]; b[2] = a[2]; }   // palindrome (GenomeIndex.cpp:1003-1006)
+                else lookup_fill(A, comp ? v1 : v2, comp ? c1 : c2, b);
+                o[0] = a[0]; o[1] = b[0]; o[2] = a[1]; o[3] = b[1]; o[4] = a[2]; o[5] = b[2];
+            }
+            for (int q = 0; q < 6; q++) out[6ull * i + q] = o[q];
+            lines[i] = ln;
+        }
+    }
 }
 
 // ------------------------------------------------------------------ host helpers
@@ -1258,6 +1404,81 @@ int snapgpu_device_count(void) {
     return n;
 }
 
+// The seed tables' bucket image (bucket_table.h): the reference-format slots go to the device once,
+// bucket_count_kernel counts per table the keys SNAPHashTable::Lookup can return, the host sizes
+// the tables (ceil(keys / BK_KEYS_PER_BUCKET) buckets each), bucket_build_kernel inserts, and the
+// slots are freed again: the kernels read only the buckets.
+static int buildBuckets(snapgpu_aligner_t *a, hipStream_t s0) {
+    const snapgpu_index_t *idx = a->idx;
+    const auto t0 = std::chrono::steady_clock::now();
+    const uint64_t nSlots = idx->slots.size() / 3;
+    const uint32_t nT = idx->nTables;
+    uint32_t *dSlots = nullptr;
+    uint64_t *dTB = nullptr, *dTS = nullptr;
+    unsigned long long *dCnt = nullptr;
+    int rc = SNAPGPU_OK;
+    hipError_t e = hipSuccess;
+    auto chk = [&](hipError_t x, const char *what) {
+        if (x != hipSuccess && rc == SNAPGPU_OK) {
+            e = x;
+            snapgpu::setError(std::string("bucket image: ") + what + ": " + hipGetErrorString(x));
+            rc = x == hipErrorOutOfMemory ? SNAPGPU_ENOMEM : SNAPGPU_EDEVICE;
+        }
+        return rc == SNAPGPU_OK;
+    };
+    std::vector<unsigned long long> cnt(nT + 4, 0);
+    if (chk(hipMalloc(&dSlots, nSlots * 12 + 16), "slots") && uploadLarge(s0, dSlots, idx->slots.data(), nSlots * 12))
+        rc = SNAPGPU_EDEVICE;
+    if (rc == SNAPGPU_OK && chk(hipMalloc(&dTB, nT * 8ull), "tables") && chk(hipMalloc(&dTS, nT * 8ull), "tables") &&
+        chk(hipMalloc(&dCnt, (nT + 4) * 8ull), "counts") &&
+        chk(hipMemcpyAsync(dTB, idx->tableBase.data(), nT * 8ull, hipMemcpyHostToDevice, s0), "tables") &&
+        chk(hipMemcpyAsync(dTS, idx->tableSize.data(), nT * 8ull, hipMemcpyHostToDevice, s0), "tables") &&
+        chk(hipMemsetAsync(dCnt, 0, (nT + 4) * 8ull, s0), "counts")) {
+        const uint64_t nThreads = (nSlots + 255) / 256;
+        hipLaunchKernelGGL(bucket_count_kernel, dim3((unsigned)((nThreads + 255) / 256)), dim3(256), 0, s0, dSlots, dTB, dTS,
+                           nT, nSlots, dCnt);
+        if (chk(hipGetLastError(), "bucket_count_kernel") &&
+            chk(hipMemcpyAsync(cnt.data(), dCnt, nT * 8ull, hipMemcpyDeviceToHost, s0), "counts") &&
+            chk(hipStreamSynchronize(s0), "bucket_count_kernel")) {
+            std::vector<uint64_t> base(nT);
+            std::vector<uint32_t> nb(nT);
+            uint64_t total = 0, keys = 0;
+            for (uint32_t t = 0; t < nT; t++) {
+                const uint64_t want = std::max<uint64_t>(1, (cnt[t] + BK_KEYS_PER_BUCKET - 1) / BK_KEYS_PER_BUCKET);
+                if (want >= (1ull << 32)) { snapgpu::setError("bucket image: table too large"); rc = SNAPGPU_EINVAL; break; }
+                base[t] = total; nb[t] = (uint32_t)want; total += want; keys += cnt[t];
+            }
+            if (rc == SNAPGPU_OK && chk(hipMalloc(&a->dBuckets, total * 64), "buckets") &&
+                chk(hipMalloc(&a->dBucketBase, nT * 8ull), "buckets") && chk(hipMalloc(&a->dBucketCount, nT * 4ull), "buckets") &&
+                chk(hipMemsetAsync(a->dBuckets, 0, total * 64, s0), "buckets") &&
+                chk(hipMemcpyAsync(a->dBucketBase, base.data(), nT * 8ull, hipMemcpyHostToDevice, s0), "buckets") &&
+                chk(hipMemcpyAsync(a->dBucketCount, nb.data(), nT * 4ull, hipMemcpyHostToDevice, s0), "buckets") &&
+                chk(hipMemsetAsync(dCnt, 0, 4 * 8, s0), "counts")) {
+                hipLaunchKernelGGL(bucket_build_kernel, dim3((unsigned)std::min<uint64_t>((nSlots + 255) / 256, 1u << 20)),
+                                   dim3(256), 0, s0, dSlots, dTB, dTS, nT, nSlots, a->dOverflow,
+                                   (uint64_t)idx->overflow.size(), idx->genome->nBases, a->dBuckets, a->dBucketBase,
+                                   a->dBucketCount, dCnt);
+                unsigned long long info[4] = {0, 0, 0, 0};
+                if (chk(hipGetLastError(), "bucket_build_kernel") &&
+                    chk(hipMemcpyAsync(info, dCnt, sizeof(info), hipMemcpyDeviceToHost, s0), "counts") &&
+                    chk(hipStreamSynchronize(s0), "bucket_build_kernel")) {
+                    if (info[2] || info[0] != keys) {
+                        snapgpu::setError("bucket image: " + std::to_string(info[2]) + " keys found no bucket, " +
+                                          std::to_string(info[0]) + " of " + std::to_string(keys) + " inserted");
+                        rc = SNAPGPU_EDEVICE;
+                    }
+                    snapgpu_bucket_info_t &bi = a->bucketInfo;
+                    bi.nBuckets = total; bi.nKeys = info[0]; bi.nSlots = nSlots;
+                    bi.nOverflowBuckets = info[1]; bi.maxDisplacement = info[3]; bi.bytes = total * 64;
+                }
+            }
+        }
+    }
+    devFree(a, dSlots); devFree(a, dTB); devFree(a, dTS); devFree(a, dCnt);
+    a->bucketInfo.buildMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
+}
+
 static void freeLaneChunkBuffers(snapgpu_aligner_t *a, ExecLane &L) {
     devFree(a, L.dDefer); devFree(a, L.dOut); devFree(a, L.dSeeds);
     L.dDefer = nullptr; L.dOut = nullptr; L.dSeeds = nullptr;
@@ -1278,8 +1499,8 @@ void snapgpu_aligner_free(snapgpu_aligner_t *a) {
     }
     hipSetDevice(a->device);
     for (auto &L : a->lane) if (L.stream) hipStreamSynchronize(L.stream);
-    devFree(a, a->dSlots); devFree(a, a->dOverflow); devFree(a, a->dPieces);
-    devFree(a, a->dTableBase); devFree(a, a->dTableSize); devFree(a, a->dGenomeAlloc); devFree(a, a->dTab);
+    devFree(a, a->dBuckets); devFree(a, a->dOverflow); devFree(a, a->dPieces);
+    devFree(a, a->dBucketBase); devFree(a, a->dBucketCount); devFree(a, a->dGenomeAlloc); devFree(a, a->dTab);
     devFree(a, a->dGPlanes); devFree(a, a->dPhase); devFree(a, a->dDiag);
     for (auto &L : a->lane) {
         freeLaneChunkBuffers(a, L);
@@ -1368,20 +1589,15 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
                            span, nw, a->dGPlanes);
         if ((e = hipGetLastError()) != hipSuccess) return fail("pack_planes_kernel", e);
     }
-    if ((e = hipMalloc(&a->dSlots, idx->slots.size() * 4)) != hipSuccess) return fail("hipMalloc slots", e);
-    if (uploadLarge(s0, a->dSlots, idx->slots.data(), idx->slots.size() * 4)) { snapgpu_aligner_free(a); return nullptr; }
     if ((e = hipMalloc(&a->dOverflow, idx->overflow.size() * 4 + 16)) != hipSuccess) return fail("hipMalloc ovf", e);
     if (uploadLarge(s0, a->dOverflow, idx->overflow.data(), idx->overflow.size() * 4)) { snapgpu_aligner_free(a); return nullptr; }
-    if ((e = hipMalloc(&a->dTableBase, idx->nTables * 8)) != hipSuccess) return fail("tb", e);
-    if ((e = hipMalloc(&a->dTableSize, idx->nTables * 8)) != hipSuccess) return fail("ts", e);
-    for (uint32_t t = 0; t < idx->nTables; t++)   // the kernels hash with 32-bit modulo
+    for (uint32_t t = 0; t < idx->nTables; t++)   // the builder hashes with 32-bit modulo
         if (idx->tableSize[t] == 0 || idx->tableSize[t] >= (1ull << 31)) {
             snapgpu::setError("hash table size must be in [1, 2^31)");
             snapgpu_aligner_free(a);
             return nullptr;
         }
-    if ((e = hipMemcpy(a->dTableBase, idx->tableBase.data(), idx->nTables * 8, hipMemcpyHostToDevice)) != hipSuccess) return fail("tb", e);
-    if ((e = hipMemcpy(a->dTableSize, idx->tableSize.data(), idx->nTables * 8, hipMemcpyHostToDevice)) != hipSuccess) return fail("ts", e);
+    if (int rc = buildBuckets(a, s0)) { (void)rc; snapgpu_aligner_free(a); return nullptr; }
     size_t np = idx->genome->pieceOffsets.size();
     if ((e = hipMalloc(&a->dPieces, np * 4 + 16)) != hipSuccess) return fail("pieces", e);
     if (np && (e = hipMemcpy(a->dPieces, idx->genome->pieceOffsets.data(), np * 4, hipMemcpyHostToDevice)) != hipSuccess)
@@ -1524,7 +1740,7 @@ static int launch_passes(snapgpu_aligner_t *a, int li, const PassIO &io, const A
     KArgs A;
     memset(&A, 0, sizeof(A));
     const snapgpu_index_t *idx = a->idx;
-    A.slots = a->dSlots; A.tableBase = a->dTableBase; A.tableSize = a->dTableSize; A.overflow = a->dOverflow;
+    A.buckets = a->dBuckets; A.bucketBase = a->dBucketBase; A.bucketCount = a->dBucketCount; A.overflow = a->dOverflow;
     A.genome = a->dGenome; A.pieces = a->dPieces; A.nPieces = (int32_t)idx->genome->pieceOffsets.size();
     A.gpl = a->dGPlanes; A.hasIupac = idx->hasIupac ? 1u : 0u;
     A.phaseBuf = a->dPhase;
@@ -2534,16 +2750,59 @@ int snapgpu_cigar_batch(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, cons
     return SNAPGPU_OK;
 }
 
+int snapgpu_aligner_lookup_seeds(snapgpu_aligner_t *a, const char *seedBases, uint64_t n, int mode, uint64_t *out,
+                                 uint32_t *lines) {
+    if (!a || (n && (!seedBases || !out || !lines)) || mode < 0 || mode > 1) return SNAPGPU_EINVAL;
+    if (n == 0) return SNAPGPU_OK;
+    if (n >= (1ull << 31)) { snapgpu::setError("lookup_seeds: too many seeds"); return SNAPGPU_EINVAL; }
+    if (a->failed) return SNAPGPU_EDEVICE;
+    const uint32_t L = a->idx->seedLen;
+    for (uint64_t i = 0; i < n * L; i++) {   // GenomeIndex::lookupSeed takes ACGT seeds only
+        const char c = seedBases[i];
+        if (c != 'A' && c != 'C' && c != 'G' && c != 'T') { snapgpu::setError("lookup_seeds: non-ACGT base"); return SNAPGPU_EINVAL; }
+    }
+    HIPCHK(hipSetDevice(a->device));
+    KArgs A;
+    if (int rc = snapgpu_internal_index_args(a, &A, nullptr)) return rc;
+    char *dS = nullptr;
+    unsigned long long *dO = nullptr;
+    uint32_t *dL = nullptr;
+    int rc = SNAPGPU_OK;
+    hipStream_t st = a->stream();
+    if (hipMalloc(&dS, n * L) != hipSuccess || hipMalloc(&dO, n * 48) != hipSuccess || hipMalloc(&dL, n * 4) != hipSuccess) {
+        snapgpu::setError("lookup_seeds: hipMalloc");
+        rc = SNAPGPU_ENOMEM;
+    } else if (hipMemcpyAsync(dS, seedBases, n * L, hipMemcpyHostToDevice, st) != hipSuccess) {
+        rc = SNAPGPU_EDEVICE;
+    } else {
+        const unsigned grid = (unsigned)std::min<uint64_t>((n + 63) / 64, 4096);
+        hipLaunchKernelGGL(lookup_seeds_kernel, dim3(grid), dim3(64), 0, st, A, dS, (uint32_t)n, mode, dO, dL);
+        if (hipGetLastError() != hipSuccess || hipMemcpyAsync(out, dO, n * 48, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipMemcpyAsync(lines, dL, n * 4, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
+            snapgpu::setError("lookup_seeds: kernel");
+            rc = SNAPGPU_EDEVICE;
+        }
+    }
+    devFree(a, dS); devFree(a, dO); devFree(a, dL);
+    return rc;
+}
+
+int snapgpu_aligner_bucket_info(const snapgpu_aligner_t *a, snapgpu_bucket_info_t *info) {
+    if (!a || !info) return SNAPGPU_EINVAL;
+    *info = a->bucketInfo;
+    return SNAPGPU_OK;
+}
+
 int snapgpu_gather_peak(snapgpu_aligner_t *a, uint32_t nLoads, double *ms) {
     if (!a || !ms || nLoads == 0) return SNAPGPU_EINVAL;
     HIPCHK(hipSetDevice(a->device));
-    const uint64_t nSlots = a->idx->slots.size() / 3;
-    if (nSlots == 0 || nSlots >= (1ull << 32)) { snapgpu::setError("gather_peak: slot count"); return SNAPGPU_EINVAL; }
+    const uint64_t nBk = a->bucketInfo.nBuckets;
+    if (nBk == 0 || nBk >= (1ull << 32)) { snapgpu::setError("gather_peak: bucket count"); return SNAPGPU_EINVAL; }
     const unsigned grid = (nLoads + 1023) / 1024;
     float best = 0;
     for (int rep = 0; rep < 3; rep++) {
         HIPCHK(hipEventRecord(a->cev[0], a->stream()));
-        hipLaunchKernelGGL(gather_peak_kernel, dim3(grid), dim3(256), 0, a->stream(), a->dSlots, (uint32_t)nSlots, nLoads,
+        hipLaunchKernelGGL(gather_peak_kernel, dim3(grid), dim3(256), 0, a->stream(), a->dBuckets, (uint32_t)nBk, nLoads,
                            0x5bd1e995u * (rep + 1), a->lane[0].counter + 8);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(a->cev[1], a->stream()));
@@ -2612,7 +2871,7 @@ int snapgpu_internal_index_args(const snapgpu_aligner_t *a, sgk::KArgs *A, int *
     if (!a || !A) return SNAPGPU_EINVAL;
     memset(A, 0, sizeof(*A));
     const snapgpu_index_t *idx = a->idx;
-    A->slots = a->dSlots; A->tableBase = a->dTableBase; A->tableSize = a->dTableSize; A->overflow = a->dOverflow;
+    A->buckets = a->dBuckets; A->bucketBase = a->dBucketBase; A->bucketCount = a->dBucketCount; A->overflow = a->dOverflow;
     A->genome = a->dGenome; A->pieces = a->dPieces; A->nPieces = (int32_t)idx->genome->pieceOffsets.size();
     A->gpl = a->dGPlanes; A->hasIupac = idx->hasIupac ? 1u : 0u;
     A->nBases = idx->genome->nBases; A->seedLen = idx->seedLen; A->nTables = idx->nTables;

@@ -1,0 +1,97 @@
+// bucket_table.h -- the device image of the seed index, laid out for coalesced bucket probes.
+//
+// GenomeIndex::lookupSeed (GenomeIndex.cpp:971-1011) needs one thing from SNAPHashTable: the map
+// key -> (value1, value2) that SNAPHashTable::Lookup (HashTable.h:74-105) defines.  The on-disk
+// table answers it with 12-byte slots and a quadratic-then-linear probe sequence (+1, +4, +9, +16
+// slots, then linear), so a lookup that misses its home slot touches two to four different 64-B
+// lines, one dependent round trip each.  At aligner creation the device re-lays that map into
+// 64-byte buckets -- one HBM line, four 16-byte entries:
+//
+//     entry = {key, value1, value2, aux}
+//     aux   = [31] occupied | [30] (entry 0) overflow | [29:15] count(value2) | [14:0] count(value1)
+//
+// A key lives in its home bucket `home(key)` or, when that was full, in the first later bucket
+// (wrapping) with room; every bucket passed over is flagged `overflow`.  A lookup loads the home
+// line: the key is there, or the line proves it absent (no overflow flag) -- one line in the common
+// case (C2: 2 keys per bucket on average, a few % of buckets overflow).  The counts are the lengths
+// of the overflow lists the values point at (saturated at 0x7fff; a saturated count is re-read from
+// the overflow table), so the list length needs no second dependent load either.
+//
+// Exactness: the builder (bucket_build_kernel) runs the reference's own probe sequence for every
+// used slot and keeps exactly the slots that SNAPHashTable::Lookup of their key returns, so the
+// bucket map answers every key as the reference table does (found or not, same values).  Which
+// keys share a line depends on insertion order (atomic claims), so the per-read count of lines
+// probed (snapgpu_result_t::nProbes) is a device statistic, not a reference quantity.
+#pragma once
+#include "align_device.h"
+
+namespace sgk {
+
+constexpr uint32_t BK_OCC = 1u << 31;    // entry holds a key
+constexpr uint32_t BK_OVF = 1u << 30;    // entry 0: a key homed at or before this bucket lives after it
+constexpr uint32_t BK_CSAT = 0x7fffu;    // overflow-list count saturation (and field mask)
+constexpr uint32_t BK_KEYS_PER_BUCKET = 2;   // sizing: buckets = ceil(keys / 2) per table (load 0.5)
+
+// home bucket of `key` in a table of nB buckets: multiply-shift of a second 32-bit mixer (the
+// slot hash fmix32 stays the reference's; this one only spreads keys over buckets)
+__device__ __forceinline__ uint32_t bucket_home(uint32_t key, uint32_t nB) {
+    uint32_t h = key * 0x9e3779b1u;
+    h ^= h >> 15; h *= 0x2c1b3c6du; h ^= h >> 12; h *= 0x297a2d39u; h ^= h >> 15;
+    return (uint32_t)(((uint64_t)h * nB) >> 32);
+}
+__device__ __forceinline__ uint32_t bucket_next(uint32_t b, uint32_t nB) { return b + 1 == nB ? 0u : b + 1; }
+
+// overflow-list length of side value v (v >= nBases, v != UNUSED_SIDE) from its entry count
+__device__ __forceinline__ uint32_t bucket_count(const KArgs &A, uint32_t cnt, uint32_t v) {
+    return cnt < BK_CSAT ? cnt : A.overflow[v - A.nBases];
+}
+
+// One lane, one lookup: the whole 64-B line in four 16-B loads per bucket visited.
+// -> found; v1/v2 as the slot holds them; aux of the entry (counts); lines = buckets loaded.
+__device__ __forceinline__ bool bucket_lookup_lane(const KArgs &A, uint32_t table, uint32_t key, uint32_t &v1,
+                                                   uint32_t &v2, uint32_t &aux, uint32_t &lines) {
+    const uint32_t nB = A.bucketCount[table];
+    const uint4 *T = A.buckets + 4ull * A.bucketBase[table];
+    uint32_t b = bucket_home(key, nB);
+    for (lines = 1;; lines++) {
+        const uint4 *p = T + 4ull * b;
+        uint4 e[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) e[i] = p[i];
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            if ((e[i].w & BK_OCC) && e[i].x == key) { v1 = e[i].y; v2 = e[i].z; aux = e[i].w; return true; }
+        if (!(e[0].w & BK_OVF) || lines >= nB) return false;
+        b = bucket_next(b, nB);
+    }
+}
+
+// The whole wave, one lookup (uniform key): lanes 0-3 load the four entries of bucket b, lanes 4-7
+// those of bucket b+1 (the adjacent line: a key that spilled over is found without a further round
+// trip).  Results are wave-uniform; lines = buckets a sequential lookup would have loaded.
+__device__ __forceinline__ bool bucket_lookup_wave(const KArgs &A, uint32_t table, uint32_t key, int lane, uint32_t &v1,
+                                                   uint32_t &v2, uint32_t &aux, uint32_t &lines) {
+    const uint32_t nB = A.bucketCount[table];
+    const uint4 *T = A.buckets + 4ull * A.bucketBase[table];
+    uint32_t b = bucket_home(key, nB);
+    for (uint32_t step = 0;; step += 2) {
+        const uint32_t bl = (lane & 4) ? bucket_next(b, nB) : b;
+        uint4 e = make_uint4(0u, 0u, 0u, 0u);
+        if (lane < 8) e = T[4ull * bl + (lane & 3)];
+        const uint64_t hit = ballot(lane < 8 && (e.w & BK_OCC) && e.x == key);
+        const uint64_t ovf = ballot(lane < 8 && (lane & 3) == 0 && (e.w & BK_OVF));
+        const uint64_t h0 = hit & 0xfull, h1 = hit & 0xf0ull;
+        int src = -1;
+        if (h0) { src = __builtin_ctzll(h0); lines = step + 1; }
+        else if (!(ovf & 1ull) || step + 1 >= nB) { lines = step + 1; return false; }
+        else if (h1) { src = __builtin_ctzll(h1); lines = step + 2; }
+        else if (!(ovf & 0x10ull) || step + 2 >= nB) { lines = step + 2; return false; }
+        if (src >= 0) {
+            v1 = readlaneu(e.y, src); v2 = readlaneu(e.z, src); aux = readlaneu(e.w, src);
+            return true;
+        }
+        b = bucket_next(bucket_next(b, nB), nB);
+    }
+}
+
+}  // namespace sgk

@@ -8,7 +8,7 @@
 // table), looks each one up, and inserts every hit of a direction that is not popular into a
 // std::map<unsigned, std::set<unsigned>>.  Here one wave owns a read:
 //   * the seed walk is wave-uniform scalar code (as align_kernel's), the 2-bit encoding one base
-//     per lane, the SNAPHashTable probe sequence 8 slots per round on lanes 0-7;
+//     per lane, the lookup one bucket line (bucket_table.h) on lanes 0-3, the next on 4-7;
 //   * the hits of an applied direction are appended one per lane as 42-bit keys
 //     dir << 41 | location << 9 | seedOffset into an LDS array (at most (numSeeds + 1) * maxHits
 //     <= 4096 keys: the loop tests the applied count once per seed, a seed applies <= 2 sides);
@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "align_device.h"
+#include "bucket_table.h"
 #include "internal.h"
 
 int snapgpu_internal_index_args(const snapgpu_aligner_t *a, sgk::KArgs *A, int *device);
@@ -135,41 +136,22 @@ __global__ __launch_bounds__(64) void charseeds_kernel(CArgs C) {
                 const bool comp = (int64_t)f > (int64_t)rcv, pal = f == rcv;
                 const uint64_t canon = comp ? rcv : f;
                 const uint32_t table = (uint32_t)(canon >> 32), key = (uint32_t)canon;
-                const uint32_t size = (uint32_t)A.tableSize[table];
-                const uint32_t *T = A.slots + 3 * A.tableBase[table];
-                const uint32_t h0 = fmix32(key) % size;
-                bool found = false;
-                uint32_t v1 = 0, v2 = 0;
-                for (uint32_t j0 = 0;; j0 += 8) {
-                    const uint32_t j = j0 + (lane & 7);
-                    const uint32_t S_j = j <= 4 ? j * (j + 1) * (2 * j + 1) / 6 : 30 + (j - 4);
-                    uint64_t pos = h0 + S_j;
-                    if (pos >= size) pos %= size;
-                    uint32_t kj = 0, v1j = INVALID, v2j = 0;
-                    const bool beyond = j > size + 5;
-                    if (lane < 8 && !beyond) { kj = T[3 * pos]; v1j = T[3 * pos + 1]; v2j = T[3 * pos + 2]; }
-                    const bool stop = (j == 0) ? (kj == key && v1j != INVALID) : (kj == key || v1j == INVALID);
-                    const uint64_t m = ballot(lane < 8 && (stop || beyond)) & 0xffull;
-                    if (m) {
-                        const int jl = __builtin_ctzll(m);
-                        const bool bey = readlane(beyond ? 1 : 0, jl);
-                        const uint32_t kv1 = readlaneu(v1j, jl);
-                        if (!bey && (j0 + jl == 0 || kv1 != INVALID)) { found = true; v1 = kv1; v2 = readlaneu(v2j, jl); }
-                        break;
-                    }
-                }
+                // SNAPHashTable::Lookup answered by the bucket image (bucket_table.h)
+                uint32_t v1 = 0, v2 = 0, aux = 0, lines = 0;
+                const bool found = bucket_lookup_wave(A, table, key, lane, v1, v2, aux, lines);
                 // fillInLookedUpResults (GenomeIndex.cpp:1013-1086), unwindowed (minSeedLoc 0, maxSeedLoc ~0: :384-386)
                 uint32_t nH[2] = {0, 0}, sg[2] = {0, 0};
                 const uint32_t *ls[2] = {nullptr, nullptr};
                 if (found) {
                     const uint32_t vs[2] = {comp ? v2 : v1, comp ? v1 : v2};
+                    const uint32_t cs[2] = {comp ? (aux >> 15) & BK_CSAT : aux & BK_CSAT, comp ? aux & BK_CSAT : (aux >> 15) & BK_CSAT};
                     for (int sd = 0; sd < 2; sd++) {
                         if (sd == 1 && pal) { nH[1] = nH[0]; sg[1] = sg[0]; ls[1] = ls[0]; break; }
                         const uint32_t vv = vs[sd];
                         if (vv < A.nBases) { nH[sd] = 1; sg[sd] = vv; }
                         else if (vv != UNUSED_SIDE) {
                             const uint32_t o = vv - A.nBases;
-                            nH[sd] = uni(A.overflow[o]);
+                            nH[sd] = uni(bucket_count(A, cs[sd], vv));
                             ls[sd] = A.overflow + o + 1;
                         }
                     }

@@ -32,6 +32,7 @@
 #include <vector>
 
 #include "align_device.h"
+#include "bucket_table.h"
 #include "internal.h"
 
 int snapgpu_internal_index_args(const snapgpu_aligner_t *a, sgk::KArgs *A, int *device);
@@ -464,33 +465,19 @@ __device__ __forceinline__ void lookup_seeds(const PArgs &P, PLds<MAXLEN> &S, co
         const bool comp = (int64_t)f > (int64_t)rv;
         const uint64_t canon = comp ? rv : f;
         const uint32_t table = (uint32_t)(canon >> 32), key = (uint32_t)canon;
-        const uint32_t size = (uint32_t)X.tableSize[table];
-        const uint32_t *T = X.slots + 3 * X.tableBase[table];
-        const uint32_t h0 = fmix32(key) % size;
-        bool found = false;
-        uint32_t v1 = 0, v2 = 0;
-        for (uint32_t j = 0;; j++) {   // SNAPHashTable::Lookup probe order (HashTable.h:74-105)
-            if (j > size + 5) break;
-            const uint32_t Sj = j <= 4 ? j * (j + 1) * (2 * j + 1) / 6 : 30 + (j - 4);
-            uint64_t pos = h0 + Sj;
-            if (pos >= size) pos %= size;
-            const uint32_t kj = T[3 * pos], v1j = T[3 * pos + 1];
-            const bool stop = (j == 0) ? (kj == key && v1j != INVALID) : (kj == key || v1j == INVALID);
-            if (stop) {
-                if (j == 0 || v1j != INVALID) { found = true; v1 = v1j; v2 = T[3 * pos + 2]; }
-                break;
-            }
-        }
+        // SNAPHashTable::Lookup (HashTable.h:74-105) answered by the bucket image (bucket_table.h)
+        uint32_t v1 = 0, v2 = 0, aux = 0, lines = 0;
+        const bool found = bucket_lookup_lane(X, table, key, v1, v2, aux, lines);
         uint32_t nh[2] = {0, 0}, at[2] = {0, 0}, sg[2] = {0, 0};
         if (found) {
             for (int side = 0; side < 2; side++) {
                 if (side == 1 && f == rv) { nh[1] = nh[0]; at[1] = at[0]; sg[1] = sg[0]; break; }
-                const uint32_t v = (side == 0) == !comp ? v1 : v2;
+                const bool first = (side == 0) == !comp;
+                const uint32_t v = first ? v1 : v2;
                 if (v < X.nBases) { nh[side] = 1; at[side] = v; sg[side] = 1; }
-                else if (v != UNUSED_SIDE) {
-                    const uint32_t o = v - X.nBases;
-                    nh[side] = X.overflow[o];
-                    at[side] = o + 1;
+                else if (v != UNUSED_SIDE) {   // the list length from the entry (saturated: from the list)
+                    nh[side] = bucket_count(X, first ? (aux & BK_CSAT) : ((aux >> 15) & BK_CSAT), v);
+                    at[side] = v - X.nBases + 1;
                 }
             }
         }

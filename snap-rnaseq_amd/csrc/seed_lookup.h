@@ -12,8 +12,12 @@
 // sequential aligner.  align_kernel<128> consumes the records when its seed loop reaches the same
 // offset and counts probes / overflow lists exactly as before (a read that stops earlier leaves
 // its later records unused).
+//
+// The lookups go to the bucket image of the tables (bucket_table.h): one 64-B line per lookup in
+// the common case, the overflow-list lengths carried in the entry.
 #pragma once
 #include "align_device.h"
+#include "bucket_table.h"
 
 namespace sgk {
 
@@ -124,32 +128,19 @@ __global__ __launch_bounds__(64) void seed_lookup_kernel(KArgs A, SeedRec *out, 
             const uint64_t canon = comp ? rcv : f;
             const uint32_t table = (uint32_t)(canon >> 32);
             const uint32_t key = (uint32_t)canon;
-            const uint32_t size = (uint32_t)A.tableSize[table];   // < 2^31 (snapgpu_aligner_create)
-            const uint32_t *T = A.slots + 3 * A.tableBase[table];
-            const uint32_t h0 = fmix32(key) % size;
-            bool found = false;
-            uint32_t v1 = 0, v2 = 0, probes = 0;
-            for (uint32_t j = 0;; j++) {   // SNAPHashTable::Lookup probe order
-                if (j > size + 5) { probes = j; break; }
-                const uint32_t S_j = j <= 4 ? j * (j + 1) * (2 * j + 1) / 6 : 30 + (j - 4);
-                uint64_t pos = h0 + S_j;
-                if (pos >= size) pos %= size;
-                const uint32_t kj = T[3 * pos], v1j = T[3 * pos + 1];
-                const bool stop = (j == 0) ? (kj == key && v1j != INVALID) : (kj == key || v1j == INVALID);
-                if (stop) {
-                    probes = j + 1;
-                    if (j == 0 || v1j != INVALID) { found = true; v1 = v1j; v2 = T[3 * pos + 2]; }
-                    break;
-                }
-            }
+            // SNAPHashTable::Lookup's answer from the bucket image: one 64-B line per bucket visited
+            uint32_t v1 = 0, v2 = 0, aux = 0, probes = 0;
+            const bool found = bucket_lookup_lane(A, table, key, v1, v2, aux, probes);
             uint32_t cnt = 0;
             nSeed = 1;
             nProbe = probes;
-            if (found) {   // overflow list lengths (GenomeIndex.cpp:1013-1086)
+            if (found) {   // overflow list lengths (GenomeIndex.cpp:1013-1086), from the entry
+                const uint32_t c1 = aux & BK_CSAT, c2 = (aux >> 15) & BK_CSAT;
                 const uint32_t vf = comp ? v2 : v1, vr = comp ? v1 : v2;
+                const uint32_t nf = comp ? c2 : c1, nr = comp ? c1 : c2;
                 uint32_t cf = 0, cr = 0;
-                if (vf >= A.nBases && vf != UNUSED_SIDE) { cf = A.overflow[vf - A.nBases]; nOvfRead++; }
-                if (f != rcv && vr >= A.nBases && vr != UNUSED_SIDE) { cr = A.overflow[vr - A.nBases]; nOvfRead++; }
+                if (vf >= A.nBases && vf != UNUSED_SIDE) { cf = bucket_count(A, nf, vf); nOvfRead += nf >= BK_CSAT; }
+                if (f != rcv && vr >= A.nBases && vr != UNUSED_SIDE) { cr = bucket_count(A, nr, vr); nOvfRead += nr >= BK_CSAT; }
                 cnt = (cf < 0xffffu ? cf : 0xffffu) | ((cr < 0xffffu ? cr : 0xffffu) << 16);
             }
             rec.meta = 0x80000000u | (uint32_t)my | (found ? 0x100u : 0u) | (comp ? 0x200u : 0u) |

@@ -412,9 +412,28 @@ class BaseAligner:
                    "cigar_batch")
         return c
 
+    def bucket_info(self):
+        """The device bucket image of the seed tables (snapgpu_aligner_bucket_info) as a dict."""
+        b = _ffi.BucketInfo()
+        _check(lib().snapgpu_aligner_bucket_info(self._h, C.byref(b)), "bucket_info")
+        return {f: getattr(b, f) for f, _ in b._fields_}
+
+    def lookup_seeds(self, seeds, mode=0):
+        """GenomeIndex::lookupSeed of ACGT seeds on the device, through the bucket image
+        (snapgpu_aligner_lookup_seeds; mode 0 = lane per seed, 1 = wave per seed).
+        -> (uint64[n, 6] {nFwd, nRc, hashFwd, hashRc, firstFwd, firstRc}, uint32[n] lines)."""
+        seeds = [s.encode() if isinstance(s, str) else bytes(s) for s in seeds]
+        n = len(seeds)
+        out = np.zeros((max(1, n), 6), dtype=np.uint64)
+        lines = np.zeros(max(1, n), dtype=np.uint32)
+        if n:
+            _check(lib().snapgpu_aligner_lookup_seeds(self._h, b"".join(seeds), n, int(mode), out.ctypes.data,
+                                                       lines.ctypes.data), "lookup_seeds")
+        return out[:n], lines[:n]
+
     def gather_peak_ms(self, n_loads):
-        """Diagnostic: best-of-3 time (ms) of n_loads independent random 12-byte slot loads
-        from the resident hash table (roofline calibration for the seed lookups)."""
+        """Diagnostic: best-of-3 time (ms) of n_loads independent random 64-byte bucket-line
+        loads from the resident bucket image (roofline calibration for the seed lookups)."""
         ms = C.c_double()
         _check(lib().snapgpu_gather_peak(self._h, int(n_loads), C.byref(ms)), "gather_peak")
         return ms.value

@@ -227,6 +227,12 @@ class AlignerStats(C.Structure):
 
 assert C.sizeof(Result) == 64, C.sizeof(Result)
 
+class BucketInfo(C.Structure):   # snapgpu_bucket_info_t
+    _fields_ = [("nSlots", C.c_uint64), ("nKeys", C.c_uint64), ("nBuckets", C.c_uint64),
+                ("nOverflowBuckets", C.c_uint64), ("maxDisplacement", C.c_uint64), ("bytes", C.c_uint64),
+                ("buildMs", C.c_double)]
+
+
 # (name, restype, argtypes)
 _PROTOS = [
     ("snapgpu_abi_version", C.c_int, []),
@@ -304,6 +310,8 @@ _PROTOS = [
     ("snapgpu_sam_header", C.c_int, [C.c_void_p, C.c_int, C.c_char_p, C.c_char_p, C.c_char_p, C.c_void_p,
                                      C.c_uint64, C.POINTER(C.c_uint64)]),
     ("snapgpu_gather_peak", C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_double)]),
+    ("snapgpu_aligner_bucket_info", C.c_int, [C.c_void_p, C.POINTER(BucketInfo)]),
+    ("snapgpu_aligner_lookup_seeds", C.c_int, [C.c_void_p, C.c_char_p, C.c_uint64, C.c_int, C.c_void_p, C.c_void_p]),
     ("snapgpu_copy_peak", C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_double)]),
     ("snapgpu_selftest_timeout_path", C.c_int, []),
     ("snapgpu_sam_format", C.c_int, [C.c_void_p, C.POINTER(Reads), C.c_char_p, C.c_void_p, C.c_void_p, C.c_void_p,

@@ -198,8 +198,11 @@ def oracle_lv(direction, text, pattern, quals, k):
     return e, net.value, prob.value
 
 
+# Every record field, bitwise -- except nProbes: on the device it counts the 64-B lines of the
+# seed tables' bucket image a read's lookups loaded (include/snapgpu.h), in the oracle the
+# reference's SNAPHashTable probes; neither is an AlignRead output.
 COMPARE_FIELDS = ("result", "location", "direction", "score", "mapq", "nLookups", "nLocationsScored",
-                  "popularSeedsSkipped", "nHitsIgnored", "nProbes", "nHitWords", "nOverflowLists", "nElements",
+                  "popularSeedsSkipped", "nHitsIgnored", "nHitWords", "nOverflowLists", "nElements",
                   "probabilityOfAllCandidates", "probabilityOfBestCandidate")
 
 

@@ -89,7 +89,7 @@ def test_gpu_long_reads_match_reference(gpu_available, small_index, long_reads, 
     bad = _diff(canonical_tsv(res), open(os.path.join(G, f"expected_small_long_{name}.tsv")).read())
     assert not bad, f"{len(bad)} differ, first: {bad[:3]}"
     cpu = oracle_align(small_index, long_reads, al.params, n_threads=4)   # counters too
-    for f in ("nProbes", "nLookups", "nLocationsScored", "nHitWords", "nElements"):
+    for f in ("nLookups", "nLocationsScored", "nHitWords", "nElements"):   # nProbes: bucket lines, device-only
         assert np.array_equal(res[f], cpu[f]), f
 
 
