@@ -50,6 +50,44 @@ std::string formatCounts(const snapgpu_contaminants *c) {
 
 }  // namespace
 
+namespace snapgpu {
+
+// Every location's contig, or -1 when the location lies before the first contig (the reference
+// dereferences the NULL piece there); -2 for a location that counts nothing ("*", or position 0).
+static int contigOf(const Genome &g, uint32_t location) {
+    if (location == 0xffffffffu) return -2;   // rname "*", pos 0: nothing counted
+    const auto &po = g.pieceOffsets;
+    int lo = 0, hi = (int)po.size() - 1, p = -1;
+    while (lo <= hi) {   // Genome::getPieceAtLocation (Genome.cpp:356-374)
+        const int mid = (lo + hi) / 2;
+        if (po[mid] <= location && (mid == (int)po.size() - 1 || po[mid + 1] > location)) { p = mid; break; }
+        else if (po[mid] <= location) lo = mid + 1;
+        else hi = mid - 1;
+    }
+    if (p < 0) return -1;
+    return location - po[p] + 1 == 0 ? -2 : p;
+}
+
+// AddAlignment of every location, all or nothing: the locations are resolved first, and a call
+// with one unresolvable location changes no count (the product paths add a call's contaminants
+// only after every step that can fail has passed).  apply = false only checks.
+int contaminantsAddAll(snapgpu_contaminants_t *c, const std::vector<uint32_t> &locations, bool apply) {
+    const Genome &g = *c->genome;
+    std::vector<int> piece(locations.size());
+    for (size_t i = 0; i < locations.size(); i++)
+        if ((piece[i] = contigOf(g, locations[i])) == -1) {
+            setError("contaminants_add: location before the first contig");
+            return SNAPGPU_EINVAL;
+        }
+    if (!apply) return SNAPGPU_OK;
+    std::lock_guard<std::mutex> lk(c->mu);
+    for (int p : piece)
+        if (p >= 0) c->counts[g.pieceNames[p]]++;
+    return SNAPGPU_OK;
+}
+
+}  // namespace snapgpu
+
 extern "C" {
 
 snapgpu_contaminants_t *snapgpu_contaminants_create(const snapgpu_index_t *contamination) {
@@ -65,24 +103,7 @@ void snapgpu_contaminants_free(snapgpu_contaminants_t *c) { delete c; }
 // (Genome::getPieceAtLocation) and 1-based position; counted when the position is not 0
 int snapgpu_contaminants_add(snapgpu_contaminants_t *c, uint32_t location) {
     if (!c) return SNAPGPU_EINVAL;
-    if (location == 0xffffffffu) return SNAPGPU_OK;   // rname "*", pos 0: nothing counted
-    const Genome &g = *c->genome;
-    const auto &po = g.pieceOffsets;
-    int lo = 0, hi = (int)po.size() - 1, p = -1;
-    while (lo <= hi) {   // Genome::getPieceAtLocation (Genome.cpp:356-374)
-        const int mid = (lo + hi) / 2;
-        if (po[mid] <= location && (mid == (int)po.size() - 1 || po[mid + 1] > location)) { p = mid; break; }
-        else if (po[mid] <= location) lo = mid + 1;
-        else hi = mid - 1;
-    }
-    if (p < 0) {   // the reference dereferences the NULL piece here
-        setError("contaminants_add: location before the first contig");
-        return SNAPGPU_EINVAL;
-    }
-    if (location - po[p] + 1 == 0) return SNAPGPU_OK;
-    std::lock_guard<std::mutex> lk(c->mu);
-    c->counts[g.pieceNames[p]]++;
-    return SNAPGPU_OK;
+    return snapgpu::contaminantsAddAll(c, std::vector<uint32_t>{location});
 }
 
 int snapgpu_contaminants_format(const snapgpu_contaminants_t *c, char *out, uint64_t cap, uint64_t *used) {

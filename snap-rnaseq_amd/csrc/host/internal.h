@@ -141,6 +141,10 @@ struct GtfPairQuery {
     uint32_t tstart1, start1, len1;
 };
 
+// contam.cpp: ContaminationFilter::AddAlignment of every location, all or nothing (apply = false:
+// only check that every location resolves)
+int contaminantsAddAll(snapgpu_contaminants_t *c, const std::vector<uint32_t> &locations, bool apply = true);
+
 }  // namespace snapgpu
 // aligner.hip: snapgpu_align_batch_ex with the multi-hits packed (read i: dense[off[i] .. off[i+1]))
 int snapgpu_internal_align_batch_packed(snapgpu_aligner_t *a, const snapgpu_reads_t *reads,

@@ -370,6 +370,7 @@ struct RnaSub {
     std::vector<snapgpu_pair_result_t> gr;
     std::vector<FilterState> fs;              // per useful pair
     std::vector<GtfPairQuery> cq;             // count events (pointing into fs), input order
+    std::vector<uint32_t> contamLocs;         // -ct: both ends of the pairs the contamination aligner placed
     std::vector<PairOut> po;                  // per pair of [a, b)
     std::vector<std::string> parts;           // the SAM lines / BAM records of [a, b), in order
     uint64_t single = 0, multi = 0, notFound = 0, partialPairs = 0, partialMatches = 0, seedRuns = 0;
@@ -535,13 +536,9 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
             else if (rc) X.fail(rc, "rna_paired_align: out of memory");
             for (auto *v : cv) snapgpu_reads_free(v);
             if (X.rc != SNAPGPU_OK) return;
-            for (auto &r : cr)
+            for (auto &r : cr)   // added with the GTF counts at the end of the call, all or nothing
                 if (r.status[0] != SNAPGPU_NOT_FOUND && r.status[1] != SNAPGPU_NOT_FOUND)
-                    for (int k = 0; k < 2; k++)
-                        if ((rc = snapgpu_contaminants_add(opt->contaminants, r.location[k]))) {
-                            X.fail(rc, snapgpu_last_error());
-                            return;
-                        }
+                    for (int k = 0; k < 2; k++) X.contamLocs.push_back(r.location[k]);
         }
     }
     // spacing and MAPQ adjustments (PairedAligner.cpp:648-663); the count events in input order
@@ -908,10 +905,17 @@ int snapgpu_rna_paired_align(snapgpu_paired_aligner_t *pa, snapgpu_aligner_t *ta
         const auto t1 = std::chrono::steady_clock::now();
         std::vector<GtfPairQuery> cq;
         for (auto &x : subs) cq.insert(cq.end(), x->cq.begin(), x->cq.end());
+        std::vector<uint32_t> contamLocs;
+        for (auto &x : subs) contamLocs.insert(contamLocs.end(), x->contamLocs.begin(), x->contamLocs.end());
+        if (!contamLocs.empty()) {   // resolved before anything is counted: a bad location counts nothing
+            const int rc = contaminantsAddAll(opt->contaminants, contamLocs, false);
+            if (rc) return rc;
+        }
         if (gtfCountPairs(gtf, cq) >= 0) {
             setError("rna_paired_align: read count for an unknown transcript or gene");
             return SNAPGPU_EFORMAT;
         }
+        if (!contamLocs.empty()) contaminantsAddAll(opt->contaminants, contamLocs);   // checked above
         st.countMs += msSince(t1);
     }
     for (auto &x : subs) {

@@ -487,6 +487,10 @@ std::string samSortRecords(const Genome &g, const std::vector<std::string> &part
 extern "C" int snapgpu_sam_sort_records(const snapgpu_index_t *idx, const char *in, uint64_t n, char *out, uint64_t cap,
                                         uint64_t *used) {
     if (!idx || !idx->genome || (!in && n) || !used) return SNAPGPU_EINVAL;
+    if (n && in[n - 1] != '\n') {   // a last record without its newline would be joined to the next
+        setError("sam_sort_records: the records must end with a newline");
+        return SNAPGPU_EINVAL;
+    }
     *used = n;
     if (!out) return SNAPGPU_OK;
     if (cap < n) return SNAPGPU_EINVAL;

@@ -175,6 +175,15 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
     const auto w0 = std::chrono::steady_clock::now();
     if (!ga || !ta || !gtf || !reads || !opt || !samPath) { setError("single_align: null argument"); return SNAPGPU_EINVAL; }
     if (!reads->ids) { setError("single_align: the reads carry no ids (use snapgpu_reads_from_fastq)"); return SNAPGPU_EINVAL; }
+    // BAM output when the path ends in ".bam" (AlignerOptions: "SAM or BAM format, depending on the
+    // file extension"); sorted BAM (+ BAMIndexSupplier's .bai) is not built -- refused before any
+    // alignment or counting, so a refused call leaves the caller's GTF and contamination counts alone
+    const size_t pl = strlen(samPath);
+    const bool bam = pl >= 4 && strcmp(samPath + pl - 4, ".bam") == 0;
+    if (bam && opt->sortOutput) {
+        setError("single_align: sorted output is built for SAM only");
+        return SNAPGPU_EUNSUPPORTED;
+    }
     const snapgpu_index_t *gi = snapgpu_aligner_index(ga), *ti = snapgpu_aligner_index(ta);
     snapgpu_single_stats_t st{};
     int rc = snapgpu_reads_clip(reads, opt->clipping, nullptr, nullptr);   // FASTQReader (FASTQ.cpp:250)
@@ -235,10 +244,9 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
         }
     });
     for (auto &e : errs) if (!e.empty()) { setError("single_align: " + e); return fail(SNAPGPU_EFORMAT); }
-    for (uint64_t j = 0; j < nu; j++)   // gene read counts (FilterSingle :260-262, :290-292)
-        if (fo[j].countTranscript) gtfCountSingle(gtf, *fo[j].countTranscript);
     // -ct (SingleAligner.cpp:282-293): the reads still NotFound through the contamination
     // BaseAligner, one GPU batch; every read it aligns counts its contig (ContaminationFilter)
+    std::vector<uint32_t> contamLocs;   // added with the GTF counts once nothing can fail any more
     if (opt->contaminationAligner && opt->contaminants && nu) {
         std::vector<uint64_t> co;
         std::vector<uint32_t> cl;
@@ -252,8 +260,7 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
             snapgpu_reads_free(cb);
             if (rc) return fail(rc);
             for (auto &r : cr)
-                if (r.result != SNAPGPU_NOT_FOUND && (rc = snapgpu_contaminants_add(opt->contaminants, r.location)))
-                    return fail(rc);
+                if (r.result != SNAPGPU_NOT_FOUND) contamLocs.push_back(r.location);
         }
     }
     st.filterMs = msSince(t0);
@@ -313,15 +320,8 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
     const unsigned nt = n < 4096 ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     std::vector<std::string> parts(nt);
     std::vector<uint64_t> cnt(3 * nt, 0);
-    // BAM output when the path ends in ".bam" (AlignerOptions: "SAM or BAM format, depending on the
-    // file extension").  BAMFormat::writeRead sets NM only for a record with a location; the others
-    // repeat the previous record's value -- a serial pass in output order fixes each record's NM.
-    const size_t pl = strlen(samPath);
-    const bool bam = pl >= 4 && strcmp(samPath + pl - 4, ".bam") == 0;
-    if (bam && opt->sortOutput) {   // sorted BAM (+ BAMIndexSupplier's .bai) is not built
-        setError("single_align: sorted output is built for SAM only");
-        return fail(SNAPGPU_EUNSUPPORTED);
-    }
+    // BAMFormat::writeRead sets NM only for a record with a location; the others repeat the
+    // previous record's value -- a serial pass in output order fixes each record's NM.
     std::vector<int32_t> bamNm;
     if (bam) {
         bamNm.resize(n);
@@ -408,6 +408,11 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
     }
     ok = (fclose(f) == 0) && ok;
     if (!ok) { setError(std::string("write failed: ") + samPath); return fail(SNAPGPU_EIO); }
+    // the call's counts, all or nothing: gene read counts (FilterSingle :260-262, :290-292) and
+    // the -ct contaminants (ContaminationFilter::AddAlignment)
+    if (!contamLocs.empty() && (rc = contaminantsAddAll(opt->contaminants, contamLocs))) return fail(rc);
+    for (uint64_t j = 0; j < nu; j++)
+        if (fo[j].countTranscript) gtfCountSingle(gtf, *fo[j].countTranscript);
     st.writeMs = msSince(t0);
     st.wallMs = msSince(w0);
     if (stats) *stats = st;

@@ -95,3 +95,28 @@ def test_paired_contamination_matches_reference(gpu_available, tmp_path):
     counts.write(out)
     assert (tmp_path / "out.contaminants.txt").read_text() == \
         open(os.path.join(G, "expected_contam_paired.contaminants.txt")).read()
+
+
+@pytest.mark.gpu
+def test_refused_single_call_leaves_counts_unchanged(gpu_available, tmp_path):
+    """A sorted-BAM single-end call is refused (not built) before any alignment or counting, so the
+    caller's GTF read counts and contamination counts are what they were; the same call as SAM then
+    counts exactly as the reference's -ct run."""
+    gtf, gidx, tidx, cidx = _indexes(tmp_path)
+    ga, ta, ca = snapgpu.BaseAligner(gidx), snapgpu.BaseAligner(tidx), snapgpu.BaseAligner(cidx)
+    counts = snapgpu.Contaminants(cidx)
+    reads = snapgpu.Reads.from_fastq(os.path.join(G, "contam_single.fq"))
+    gtf.write_counts(tmp_path / "before")
+    with pytest.raises(snapgpu.SnapGpuError, match="sorted output is built for SAM only"):
+        snapgpu.single_align(ga, ta, gtf, reads, tmp_path / "out.bam", sortOutput=1, contamination=(ca, counts))
+    assert counts.text() == ""
+    gtf.write_counts(tmp_path / "after")
+    files = sorted(tmp_path.glob("before.*counts.txt"))
+    assert len(files) == 6
+    for f in files:
+        assert f.read_bytes() == (tmp_path / f.name.replace("before", "after", 1)).read_bytes(), f.name
+    out = tmp_path / "out.sam"
+    snapgpu.single_align(ga, ta, gtf, reads, out, contamination=(ca, counts), version="0.1alpha", commandLine="x")
+    counts.write(out)
+    assert (tmp_path / "out.contaminants.txt").read_text() == \
+        open(os.path.join(G, "expected_contam_single.contaminants.txt")).read()

@@ -71,3 +71,11 @@ def test_paired_sorted_output_matches_reference(gpu_available, tmp_path, gidx):
     f1 = snapgpu.Reads.from_fastq(os.path.join(G, "contam_paired_2.fq"))
     with pytest.raises(snapgpu.SnapGpuError, match="sorted output is built for SAM only"):   # sorted BAM: not built
         snapgpu.rna_paired_align(pa, ta, gtf, f0, f1, tmp_path / "out.bam", sortOutput=1)
+
+
+def test_sort_refuses_records_without_final_newline(gidx):
+    body = _body(os.path.join(G, "expected_single.sam.gz"))
+    assert body.endswith(b"\n")
+    with pytest.raises(snapgpu.SnapGpuError, match="must end with a newline"):
+        snapgpu.sam_sort_records(gidx, body[:-1])
+    assert snapgpu.sam_sort_records(gidx, b"") == b""
