@@ -318,6 +318,23 @@ def rna_roofline(ta, r0):
                     "multi-hit calls run the EXT twin of the same kernel)"}
 
 
+def rna_cpu_baseline(args):
+    """configs[4]'s CPU baseline: the reference CLI itself (`snap-rna paired -t T`) on a sample of this
+    leg's workload, timed by its own stats line in the build container (tests/golden/rna_cpu_baseline.py;
+    the reference does not travel to the GPU box).  Only for the default C2 workload it was run on."""
+    path = os.path.join(ROOT, "tests", "golden", "rna_cpu_baseline.json")
+    if not os.path.exists(path) or args.workload != "c2" or args.genome_bases:
+        return None
+    runs = json.load(open(path))
+    out = {}
+    for key, r in sorted(runs.items()):
+        out[key] = {x: r[x] for x in ("value", "unit", "cores", "kind", "sample", "host", "crashed_blocks")}
+    one = runs.get("threads_1")
+    if one:
+        out.update({x: one[x] for x in ("value", "unit", "cores", "kind", "sample")})
+    return out
+
+
 def rna_leg(args, idx, local, build_threads):
     """SURVEY.md 8(f) f4 (BASELINE configs[4] shape on this workload's genome): the RNA paired
     product path (`snap-rna paired`: transcriptome multi-hit + chimeric genome aligners,
@@ -353,7 +370,7 @@ def rna_leg(args, idx, local, build_threads):
         n = r0.n
         parity = rna_parity(args, pa, ta, gtf, r0, r1, work)
         roof = rna_roofline(ta, r0)
-        return {"parity": parity, "roofline": roof, "value": 2 * n / dt, "unit": "reads/s", "pairs_per_s": n / dt, "pairs": n, "ms_per_batch": dt * 1e3,
+        return {"parity": parity, "roofline": roof, "cpu_baseline": rna_cpu_baseline(args), "value": 2 * n / dt, "unit": "reads/s", "pairs_per_s": n / dt, "pairs": n, "ms_per_batch": dt * 1e3,
                 "read_len": 150, "workload": info, "transcriptome_bases": tidx.info()["nBases"],
                 "stage_ms": {x: round(st[x], 2) for x in ("prepMs", "alignMs", "filterMs", "seedMs", "countMs", "cigarMs",
                                                           "writeMs", "wallMs")},

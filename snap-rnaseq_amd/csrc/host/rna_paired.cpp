@@ -71,36 +71,67 @@ void parallel(uint64_t n, F &&f) {
     for (auto &x : th) x.join();
 }
 
-// Alignment (AlignmentFilter.h:41-70)
+const std::string kNoName;   // transcriptId / geneId of a genome alignment
+
+// Alignment (AlignmentFilter.h:41-70).  The names point into storage that outlives the call (the
+// genomes' piece names, the GTF's transcript records), so an alignment allocates nothing.
 struct Alignment {
     uint32_t location = 0;
     int direction = 0;
     int score = 0, mapq = 0;
-    std::string rname;
+    const std::string *rname = &kNoName;
     uint32_t pos = 0, posEnd = 0, posOriginal = 0;
     bool isTranscriptome = false;
-    std::string transcriptId, geneId;
+    const std::string *transcriptId = &kNoName, *geneId = &kNoName;
+    const GtfGene *gene = nullptr;   // gtfGene(geneId), resolved once per transcript
 };
+
+// alignment_map's key, the string `rname + '_' + std::to_string(pos)` (AlignmentFilter.cpp:183),
+// compared as that string without building it: the map's iteration order -- which the filter's
+// pair lists and their std::sort inherit -- is the string order.
+struct AlignKey {
+    const std::string *rname;
+    uint32_t pos;
+    char digits[10];
+    uint8_t nd;
+    AlignKey(const std::string *r, uint32_t p) : rname(r), pos(p) {
+        char t[10];
+        int n = 0;
+        do { t[n++] = (char)('0' + p % 10); p /= 10; } while (p);
+        nd = (uint8_t)n;
+        for (int i = 0; i < n; i++) digits[i] = t[n - 1 - i];
+    }
+    size_t size() const { return rname->size() + 1 + nd; }
+    char at(size_t i) const {
+        const size_t rn = rname->size();
+        return i < rn ? (*rname)[i] : (i == rn ? '_' : digits[i - rn - 1]);
+    }
+};
+int keyCompare(const AlignKey &a, const AlignKey &b) {
+    if (a.rname == b.rname || *a.rname == *b.rname) {   // same prefix "rname_": the digit strings decide
+        const int c = memcmp(a.digits, b.digits, std::min(a.nd, b.nd));
+        return c ? c : (int)a.nd - (int)b.nd;
+    }
+    const size_t la = a.size(), lb = b.size(), l = std::min(la, lb);
+    for (size_t i = 0; i < l; i++) {
+        const unsigned char x = (unsigned char)a.at(i), y = (unsigned char)b.at(i);
+        if (x != y) return x < y ? -1 : 1;
+    }
+    return la < lb ? -1 : (la > lb ? 1 : 0);
+}
+
 // alignment_map (AlignmentFilter.h: std::map<string, Alignment> keyed by rname_pos): a vector kept
 // sorted by key -- the map's iteration order -- with the same find / insert / replace semantics; a
-// mate holds a few entries, and clear() keeps the storage, so a pair allocates no tree nodes
+// mate holds a few entries, and clear() keeps the storage, so a pair allocates nothing
 struct AlignmentMap {
-    std::vector<std::pair<std::string, Alignment>> v;
+    std::vector<std::pair<AlignKey, Alignment>> v;
     void clear() { v.clear(); }
-    std::vector<std::pair<std::string, Alignment>>::iterator begin() { return v.begin(); }
-    std::vector<std::pair<std::string, Alignment>>::iterator end() { return v.end(); }
-    // the entry of `key` (inserted default when absent); *isNew says which
-    Alignment &at(std::string &&key, bool *isNew) {
-        auto it = std::lower_bound(v.begin(), v.end(), key,
-                                   [](const std::pair<std::string, Alignment> &e, const std::string &k) { return e.first < k; });
-        *isNew = it == v.end() || it->first != key;
-        if (*isNew) it = v.emplace(it, std::move(key), Alignment());
-        return it->second;
-    }
-    const Alignment *find(const std::string &key) const {
-        auto it = std::lower_bound(v.begin(), v.end(), key,
-                                   [](const std::pair<std::string, Alignment> &e, const std::string &k) { return e.first < k; });
-        return it != v.end() && it->first == key ? &it->second : nullptr;
+    std::vector<std::pair<AlignKey, Alignment>>::iterator begin() { return v.begin(); }
+    std::vector<std::pair<AlignKey, Alignment>>::iterator end() { return v.end(); }
+    std::vector<std::pair<AlignKey, Alignment>>::iterator lower(const AlignKey &key) {
+        return std::lower_bound(v.begin(), v.end(), key, [](const std::pair<AlignKey, Alignment> &e, const AlignKey &k) {
+            return keyCompare(e.first, k) < 0;
+        });
     }
 };
 
@@ -131,6 +162,10 @@ struct Ctx {
     snapgpu_gtf_t *gtf;
     std::map<std::string, uint32_t> pieceByName;   // Genome::getOffsetOfPiece
     const snapgpu_rna_paired_options_t *opt;
+    // per transcriptome piece: GTFReader::GetTranscript of its name (nullptr: "No transcript") and
+    // GetGene of the transcript's gene (nullptr: "No gene"), looked up once per call
+    std::vector<const GtfTranscript *> tByPiece;
+    std::vector<const GtfGene *> gByPiece;
 };
 
 struct Err {
@@ -143,44 +178,48 @@ struct Err {
 void addAlignment(const Ctx &C, AlignmentMap &mate0, AlignmentMap &mate1, uint32_t location, int direction, int score,
                   int mapq, bool isT, bool isMate0, uint32_t len0, uint32_t len1, Err &err) {
     if ((uint32_t)score > C.opt->maxDist) return;   // `score > maxDist`, unsigned
-    std::string rname = "*", tid, gid;
+    static const std::string kStar = "*";
+    const std::string *rname = &kStar, *tid = &kNoName, *gid = &kNoName;
+    const GtfGene *gene = nullptr;
     uint32_t pos = 0, posEnd = 0, posOriginal = 0;
     const uint32_t span = isMate0 ? len1 : len0;
     if (location != kInvalidLocation) {
         const Genome &g = isT ? *C.transcriptome : *C.genome;
         const int p = pieceAt(g, location);
         if (p < 0) { err.set("AddAlignment: location before the first piece (the reference dereferences NULL)"); return; }
-        rname = g.pieceNames[p];
+        rname = &g.pieceNames[p];
         posOriginal = location - g.pieceOffsets[p] + 1;
         pos = posOriginal;
         if (!isT) {
             posEnd = pos + span - 1;
         } else {
-            const GtfTranscript *t = gtfTranscript(C.gtf, rname);
-            if (!t) { err.set("No transcript " + rname); return; }   // GTFReader::GetTranscript exits
+            const GtfTranscript *t = C.tByPiece[p];
+            if (!t) { err.set("No transcript " + *rname); return; }   // GTFReader::GetTranscript exits
             tid = rname;
-            gid = gtfTranscriptGene(t);
-            rname = gtfTranscriptChr(t);
+            gid = &gtfTranscriptGene(t);
+            gene = C.gByPiece[p];
+            rname = &gtfTranscriptChr(t);
             posEnd = gtfGenomicPosition(t, pos + span - 1, 0);
             pos = gtfGenomicPosition(t, pos, span);
         }
     }
     if (pos == 0) return;
     AlignmentMap &m = isMate0 ? mate0 : mate1;
-    std::string key = rname + '_' + std::to_string(pos);
+    const AlignKey key(rname, pos);
+    auto it = m.lower(key);
+    const bool isNew = it == m.end() || keyCompare(it->first, key) != 0;
     // replaced only by a lower score, or an equal transcriptome score (the element stays put)
-    if (const Alignment *cur = m.find(key); cur && !(score < cur->score || (score == cur->score && isT))) return;
-    bool isNew;
-    Alignment &a = m.at(std::move(key), &isNew);
-    a.location = location; a.direction = direction; a.score = score; a.mapq = mapq; a.rname = std::move(rname);
+    if (!isNew && !(score < it->second.score || (score == it->second.score && isT))) return;
+    if (isNew) it = m.v.emplace(it, key, Alignment());
+    Alignment &a = it->second;
+    a.location = location; a.direction = direction; a.score = score; a.mapq = mapq; a.rname = rname;
     a.pos = pos; a.posEnd = posEnd; a.posOriginal = posOriginal; a.isTranscriptome = isT;
-    a.transcriptId = std::move(tid); a.geneId = std::move(gid);
+    a.transcriptId = tid; a.geneId = gid; a.gene = gene;
 }
 
-bool checkBoundary(const Ctx &C, const std::string &geneId, const std::string &chr, uint32_t pos, Err &err) {
-    const GtfGene *ge = gtfGene(C.gtf, geneId);
-    if (!ge) { err.set("No gene " + geneId); return false; }   // GTFReader::GetGene exits
-    return gtfGeneCheckBoundary(ge, chr, pos, 1000);
+bool checkBoundary(const Alignment &a, const std::string &chr, uint32_t pos, Err &err) {
+    if (!a.gene) { err.set("No gene " + *a.geneId); return false; }   // GTFReader::GetGene exits
+    return gtfGeneCheckBoundary(a.gene, chr, pos, 1000);
 }
 
 // AlignmentFilter::ProcessPairs (:1061-1180)
@@ -191,8 +230,8 @@ void processPairs(const Ctx &C, PairOut &r, std::vector<AlignmentPair> &pairs, u
     for (int k = 0; k < 2; k++) {
         if (a[k]->isTranscriptome) {
             r.tlocation[k] = a[k]->location;
-            auto po = C.pieceByName.find(a[k]->rname);
-            if (po == C.pieceByName.end()) { err.set("chromosome " + a[k]->rname + " not in the genome"); return; }
+            auto po = C.pieceByName.find(*a[k]->rname);
+            if (po == C.pieceByName.end()) { err.set("chromosome " + *a[k]->rname + " not in the genome"); return; }
             r.location[k] = po->second + a[k]->pos - 1;
         } else {
             r.tlocation[k] = 0;
@@ -218,7 +257,7 @@ void processPairs(const Ctx &C, PairOut &r, std::vector<AlignmentPair> &pairs, u
 // AlignmentFilter::CheckNoRC (:1039-1059)
 void checkNoRC(PairOut &r, const std::vector<AlignmentPair> &noRc) {
     for (auto &it : noRc)
-        if (it.a1->rname == it.a2->rname && it.score < (uint32_t)(r.score[0] + r.score[1])) {
+        if (*it.a1->rname == *it.a2->rname && it.score < (uint32_t)(r.score[0] + r.score[1])) {
             r.status[0] = r.status[1] = SNAPGPU_MULTIPLE_HITS;
             r.mapq[0] = r.mapq[1] = 1;
         }
@@ -242,18 +281,19 @@ void filterPair(const Ctx &C, AlignmentMap &mate0, AlignmentMap &mate1, uint32_t
         for (auto &m1 : mate1) {
             const Alignment &x = m0.second, &y = m1.second;
             if ((x.direction && y.direction) || (!x.direction && !y.direction)) { noRc.emplace_back(&y, &x); continue; }
+            const bool sameChr = x.rname == y.rname || *x.rname == *y.rname;
             if (x.isTranscriptome && y.isTranscriptome) {
-                if (x.rname != y.rname) inter.emplace_back(&y, &x);
-                else if (checkBoundary(C, x.geneId, y.rname, y.pos, err)) intragene.emplace_back(&y, &x);
-                else if (checkBoundary(C, y.geneId, x.rname, x.pos, err)) intragene.emplace_back(&y, &x);
+                if (!sameChr) inter.emplace_back(&y, &x);
+                else if (checkBoundary(x, *y.rname, y.pos, err)) intragene.emplace_back(&y, &x);
+                else if (checkBoundary(y, *x.rname, x.pos, err)) intragene.emplace_back(&y, &x);
                 else intra.emplace_back(&y, &x);
             } else if (x.isTranscriptome) {
-                if (x.rname != y.rname) inter.emplace_back(&y, &x);
-                else if (checkBoundary(C, x.geneId, y.rname, y.pos, err)) intragene.emplace_back(&y, &x);
+                if (!sameChr) inter.emplace_back(&y, &x);
+                else if (checkBoundary(x, *y.rname, y.pos, err)) intragene.emplace_back(&y, &x);
                 else intra.emplace_back(&y, &x);
             } else if (y.isTranscriptome) {
-                if (x.rname != y.rname) inter.emplace_back(&y, &x);
-                else if (checkBoundary(C, y.geneId, x.rname, x.pos, err)) intragene.emplace_back(&y, &x);
+                if (!sameChr) inter.emplace_back(&y, &x);
+                else if (checkBoundary(y, *x.rname, x.pos, err)) intragene.emplace_back(&y, &x);
                 else intra.emplace_back(&y, &x);
             } else {
                 intragene.emplace_back(&y, &x);
@@ -265,8 +305,8 @@ void filterPair(const Ctx &C, AlignmentMap &mate0, AlignmentMap &mate1, uint32_t
         if (r.status[0] == SNAPGPU_SINGLE_HIT) {
             const AlignmentPair &p = intragene[0];
             S.countPair = true;
-            S.tid0 = p.a1->transcriptId; S.tstart0 = p.a1->posOriginal; S.start0 = p.a1->pos; S.len0 = len1;
-            S.tid1 = p.a2->transcriptId; S.tstart1 = p.a2->posOriginal; S.start1 = p.a2->pos; S.len1 = len0;
+            S.tid0 = *p.a1->transcriptId; S.tstart0 = p.a1->posOriginal; S.start0 = p.a1->pos; S.len0 = len1;
+            S.tid1 = *p.a2->transcriptId; S.tstart1 = p.a2->posOriginal; S.start1 = p.a2->pos; S.len1 = len0;
         }
         r.fromAlignTogether = false;
         r.alignedAsPair = true;
@@ -835,6 +875,11 @@ int snapgpu_rna_paired_align(snapgpu_paired_aligner_t *pa, snapgpu_aligner_t *ta
     st.prepMs = msSince(w0);
     Ctx C{gi->genome, ti->genome, gtf, {}, opt};
     for (size_t p = 0; p < gi->genome->pieceNames.size(); p++) C.pieceByName.insert({gi->genome->pieceNames[p], gi->genome->pieceOffsets[p]});
+    for (const std::string &name : ti->genome->pieceNames) {
+        const GtfTranscript *t = gtfTranscript(gtf, name);
+        C.tByPiece.push_back(t);
+        C.gByPiece.push_back(t ? gtfGene(gtf, gtfTranscriptGene(t)) : nullptr);
+    }
     const size_t spl = samPath ? strlen(samPath) : 0;
     // BAM when the path ends in ".bam" (BAMFormat::writeRead for both ends, Bam.cpp:596-790)
     const bool bam = spl >= 4 && strcmp(samPath + spl - 4, ".bam") == 0;
