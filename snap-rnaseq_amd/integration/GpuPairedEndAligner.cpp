@@ -14,7 +14,7 @@ GpuPairedEndAligner::GpuPairedEndAligner(const char *indexDir, int device, unsig
                                          unsigned maxK, unsigned numSeeds, double seedCoverage, unsigned minSpacing,
                                          unsigned maxSpacing, unsigned maxBigHits, unsigned extraSearchDepth,
                                          unsigned maxCandidatePoolSize, bool forceSpacing)
-    : idx(NULL), gpu(NULL), locationsScored(0)
+    : idx(NULL), gpu(NULL), locationsScored(0), nPerPair(0)
 {
     idx = snapgpu_index_load(indexDir);
     if (idx == NULL) pairedFail("index load");
@@ -43,6 +43,9 @@ GpuPairedEndAligner::~GpuPairedEndAligner()
 
 void GpuPairedEndAligner::align(Read *read0, Read *read1, PairedAlignmentResult *result)
 {
+    if (nPerPair++ == 0)
+        fprintf(stderr, "MI355X paired aligner: align() aligns one pair per GPU batch (copy in, the passes, copy out); "
+                        "batch the caller through GpuPairedEndAligner::alignBatch\n");
     alignBatch(&read0, &read1, 1, result);
 }
 

@@ -34,4 +34,5 @@ private:
     snapgpu_index_t *idx;
     snapgpu_paired_aligner_t *gpu;
     _int64 locationsScored;
+    _int64 nPerPair;   // align() calls (one-pair batches)
 };

@@ -17,7 +17,7 @@ static void gpuFail(const char *what) {
 GpuBaseAligner::GpuBaseAligner(const char *indexDir, int device, unsigned maxHits, unsigned maxK,
                                unsigned maxReadSize, unsigned numSeeds, double seedCoverage,
                                unsigned extraSearchDepth, bool explorePopular, bool stopOnFirst)
-    : idx(NULL), gpu(NULL), ignoredReads(0)
+    : idx(NULL), gpu(NULL), ignoredReads(0), nPerRead(0)
 {
     idx = snapgpu_index_load(indexDir);
     if (idx == NULL) gpuFail("index load");
@@ -41,27 +41,92 @@ GpuBaseAligner::~GpuBaseAligner()
     snapgpu_index_free(idx);
 }
 
-AlignmentResult GpuBaseAligner::AlignRead(Read *read, unsigned *genomeLocation, Direction *hitDirection,
-                                          int *finalScore, int *mapq)
+// The reads copied into one batch (a Read is only valid until the next getNextRead, Read.h:135)
+snapgpu_reads_t *GpuBaseAligner::copyReads(Read **reads, unsigned n)
 {
-    uint64_t off = 0;
-    uint32_t len = read->getDataLength();
-    // a Read is only valid until the next getNextRead (Read.h:135): the batch copies it
-    snapgpu_reads_t *r = snapgpu_reads_from_arrays(1, read->getData(), read->getQuality(), &off, &len);
+    std::vector<char> b, q;
+    std::vector<uint64_t> off(n + 1);
+    std::vector<uint32_t> len(n + 1);
+    for (unsigned i = 0; i < n; i++) {
+        off[i] = b.size();
+        len[i] = reads[i]->getDataLength();
+        b.insert(b.end(), reads[i]->getData(), reads[i]->getData() + len[i]);
+        q.insert(q.end(), reads[i]->getQuality(), reads[i]->getQuality() + len[i]);
+    }
+    b.push_back(0);
+    q.push_back(0);
+    snapgpu_reads_t *r = snapgpu_reads_from_arrays(n, &b[0], &q[0], &off[0], &len[0]);
     if (r == NULL) gpuFail("read copy");
-    snapgpu_result_t o;
-    const int rc = snapgpu_align_batch(gpu, r, &o);
-    snapgpu_reads_free(r);
-    if (rc != SNAPGPU_OK) gpuFail("align");
+    return r;
+}
+
+static void tooLong(const snapgpu_result_t &o)
+{
     if (o.flags & SNAPGPU_FLAG_READ_TOO_LONG) {   // BaseAligner.cpp:609-613
         fprintf(stderr, "Read is too long\n");
         soft_exit(1);
     }
-    *genomeLocation = o.location;
-    *hitDirection = (Direction)o.direction;
-    if (finalScore != NULL) *finalScore = o.score;
-    if (mapq != NULL) *mapq = o.mapq;
-    return (AlignmentResult)o.result;
+}
+
+AlignmentResult GpuBaseAligner::AlignRead(Read *read, unsigned *genomeLocation, Direction *hitDirection,
+                                          int *finalScore, int *mapq)
+{
+    if (nPerRead++ == 0)
+        fprintf(stderr, "MI355X aligner: AlignRead aligns one read per GPU batch (copy in, the passes, copy out); "
+                        "batch the caller through GpuBaseAligner::AlignReads / AlignReadsMultiHit\n");
+    AlignmentResult r;
+    int s = 0, q = 0;
+    AlignReads(&read, 1, &r, genomeLocation, hitDirection, &s, &q);
+    if (finalScore != NULL) *finalScore = s;
+    if (mapq != NULL) *mapq = q;
+    return r;
+}
+
+void GpuBaseAligner::AlignReads(Read **reads, unsigned n, AlignmentResult *results, unsigned *genomeLocations,
+                                Direction *hitDirections, int *finalScores, int *mapqs)
+{
+    if (n == 0) return;
+    snapgpu_reads_t *r = copyReads(reads, n);
+    std::vector<snapgpu_result_t> o(n);
+    const int rc = snapgpu_align_batch(gpu, r, &o[0]);
+    snapgpu_reads_free(r);
+    if (rc != SNAPGPU_OK) gpuFail("align");
+    for (unsigned i = 0; i < n; i++) {
+        tooLong(o[i]);
+        results[i] = (AlignmentResult)o[i].result;
+        genomeLocations[i] = o[i].location;
+        hitDirections[i] = (Direction)o[i].direction;
+        if (finalScores != NULL) finalScores[i] = o[i].score;
+        if (mapqs != NULL) mapqs[i] = o[i].mapq;
+    }
+}
+
+void GpuBaseAligner::AlignReadsMultiHit(Read **reads, unsigned n, unsigned maxHitsToGet, AlignmentResult *results,
+                                        unsigned *genomeLocations, Direction *hitDirections, int *finalScores,
+                                        int *mapqs, int *multiHitsFound, unsigned *multiHitLocations,
+                                        bool *multiHitRCs, int *multiHitScores)
+{
+    if (n == 0) return;
+    snapgpu_reads_t *r = copyReads(reads, n);
+    std::vector<snapgpu_result_t> o(n);
+    std::vector<snapgpu_multi_hit_t> h((size_t)n * (maxHitsToGet > 0 ? maxHitsToGet : 1));
+    const int rc = snapgpu_align_batch_ex(gpu, r, NULL, maxHitsToGet, &o[0], multiHitsFound, &h[0]);
+    snapgpu_reads_free(r);
+    if (rc != SNAPGPU_OK) gpuFail("align (multi-hit)");
+    for (unsigned i = 0; i < n; i++) {
+        tooLong(o[i]);
+        results[i] = (AlignmentResult)o[i].result;
+        genomeLocations[i] = o[i].location;
+        hitDirections[i] = (Direction)o[i].direction;
+        if (finalScores != NULL) finalScores[i] = o[i].score;
+        if (mapqs != NULL) mapqs[i] = o[i].mapq;
+        for (int j = 0; j < multiHitsFound[i]; j++) {
+            const snapgpu_multi_hit_t &m = h[(size_t)i * maxHitsToGet + j];
+            multiHitLocations[(size_t)i * maxHitsToGet + j] = m.location;
+            multiHitRCs[(size_t)i * maxHitsToGet + j] = m.direction != 0;
+            multiHitScores[(size_t)i * maxHitsToGet + j] = m.score;
+        }
+    }
 }
 
 snapgpu_aligner_stats_t GpuBaseAligner::stats() const

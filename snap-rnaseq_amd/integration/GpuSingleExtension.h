@@ -4,8 +4,12 @@
 // dialect (C++98); tests/test_integration_build.py compiles and links it with the reference's
 // objects in the build container.
 //
-//  * GpuBaseAligner : Aligner -- BaseAligner::AlignRead (BaseAligner.cpp:196-200) one read at a
-//    time through snapgpu_align_batch, for any existing caller of Aligner*.
+//  * GpuBaseAligner : Aligner -- BaseAligner::AlignRead (BaseAligner.cpp:196-200).  The Aligner
+//    interface aligns one read per call, which on the GPU is a one-read batch (H2D, the passes,
+//    D2H per read): it works for any existing caller of Aligner* but is slower than the CPU, and
+//    says so on stderr the first time.  Batching callers use AlignReads (n reads, one batch) and
+//    AlignReadsMultiHit (the richer AlignRead with multi-hit export that PairedAligner.cpp:602-605
+//    calls per pair, for n reads in one batch).
 //  * GpuSingleExtension : AlignerExtension -- the hook SingleAlignerContext::runIterationThread
 //    calls first (SingleAligner.cpp:150-153, AlignerContext.h:157): the thread's reads are taken
 //    in batches, both AlignRead calls of every read run as two GPU batches, and the unchanged
@@ -29,6 +33,18 @@ public:
 
     virtual AlignmentResult AlignRead(Read *read, unsigned *genomeLocation, Direction *hitDirection,
                                       int *finalScore = NULL, int *mapq = NULL);
+    // AlignRead of reads[0..n) in one GPU batch; outputs per read as AlignRead returns them
+    // (finalScores / mapqs may be NULL)
+    void AlignReads(Read **reads, unsigned n, AlignmentResult *results, unsigned *genomeLocations,
+                    Direction *hitDirections, int *finalScores, int *mapqs);
+    // BaseAligner::AlignRead(read, &loc, &dir, &score, &mapq, 0, 0, 0, maxHitsToGet, &multiHitsFound,
+    // multiHitLocations, multiHitRCs, multiHitScores) (BaseAligner.h:73-86, as PairedAligner.cpp:
+    // 602-605 calls it) of reads[0..n) in one GPU batch; read i's hits are at [i * maxHitsToGet, ...)
+    void AlignReadsMultiHit(Read **reads, unsigned n, unsigned maxHitsToGet, AlignmentResult *results,
+                            unsigned *genomeLocations, Direction *hitDirections, int *finalScores, int *mapqs,
+                            int *multiHitsFound, unsigned *multiHitLocations, bool *multiHitRCs,
+                            int *multiHitScores);
+    _int64 perReadCalls() const { return nPerRead; }
     virtual _int64 getNHashTableLookups() const;
     virtual _int64 getLocationsScored() const;
     virtual _int64 getNHitsIgnoredBecauseOfTooHighPopularity() const;
@@ -41,9 +57,11 @@ public:
 
 private:
     snapgpu_aligner_stats_t stats() const;
+    snapgpu_reads_t *copyReads(Read **reads, unsigned n);
     snapgpu_index_t *idx;
     snapgpu_aligner_t *gpu;
     _int64 ignoredReads;
+    _int64 nPerRead;   // AlignRead calls (one-read batches)
 };
 
 class GpuSingleExtension : public AlignerExtension {
