@@ -47,9 +47,9 @@ def _host_rows(index, seeds, cap=1 << 16):
     return rows
 
 
-def _seed_set(genome, seed_len, n_present, n_random, seed=5):
+def _seed_set(g, seed_len, n_present, n_random, seed=5):
+    """g: genome bytes"""
     rng = np.random.default_rng(seed)
-    g = genome.bases()
     out = []
     while len(out) < n_present:   # seeds at random genome positions (ACGT only), either strand
         p = int(rng.integers(0, len(g) - seed_len))
@@ -96,8 +96,10 @@ def test_gpu_lookups_on_reference_built_index(gpu_available, tmp_path):
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed_len", [16, 20, 25])
 def test_gpu_lookups_match_host(gpu_available, small_world, seed_len):
-    g = small_world["genome"]
-    idx = small_world["index"] if seed_len == 20 else snapgpu.GenomeIndex.build(g, seed_len, 8)
+    g = small_world["genome"].bases()
+    # GenomeIndex.build takes ownership of its genome: the other seed lengths index a fresh copy
+    idx = small_world["index"] if seed_len == 20 else snapgpu.GenomeIndex.build(
+        snapgpu.Genome.synthetic(1_000_000, seed=2121, n_contigs=3, n_repeat_families=60), seed_len, 8)
     al = snapgpu.BaseAligner(idx)
     seeds = _seed_set(g, seed_len, 6000, 3000)
     want = _host_rows(idx, seeds)
@@ -128,9 +130,10 @@ def test_gpu_lookups_saturated_counts(gpu_available, tmp_path):
     fa = tmp_path / "tandem.fa"
     fa.write_bytes(b">tandem\n" + b"\n".join(body[i:i + 80] for i in range(0, len(body), 80)) + b"\n")
     g = snapgpu.Genome.from_fasta(str(fa), 500)
+    gb = g.bases()
     idx = snapgpu.GenomeIndex.build(g, 20, 8)
     al = snapgpu.BaseAligner(idx)
-    seeds = [(b"AACGT" * 5)[k:k + 20].decode() for k in range(5)] + _seed_set(g, 20, 500, 200)
+    seeds = [(b"AACGT" * 5)[k:k + 20].decode() for k in range(5)] + _seed_set(gb, 20, 500, 200)
     want = _host_rows(idx, seeds)
     assert max(int(w.split("\t")[0]) for w in want[:5]) > 0x7fff
     for mode in (0, 1):
