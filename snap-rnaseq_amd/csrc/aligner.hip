@@ -1158,22 +1158,76 @@ __global__ __launch_bounds__(256) void bucket_count_kernel(const uint32_t *slots
     if (c) atomicAdd(cnt + t, c);
 }
 
-// Insert every slot the reference's Lookup returns into its table's buckets: home bucket, else the
-// first later one with a free entry (claimed by CAS on aux), flagging each full bucket passed over.
-// info: [0] keys inserted, [1] buckets flagged, [2] keys that found no room (build error), [3] most
-// buckets a key moved past its home.
-__global__ __launch_bounds__(256) void bucket_build_kernel(const uint32_t *slots, const uint64_t *tableBase,
+// Place every key the reference's Lookup returns into its table's buckets, deterministically.
+// Phase 1 (bucket_place_kernel) works on the entries' first 8 bytes {key, 1 = occupied} only:
+// bucketed linear probing from the key's home bucket in which a smaller key has priority -- a key
+// that finds its bucket full takes the entry of the largest occupant greater than itself (64-bit
+// CAS) and that occupant moves on to the next bucket, else the key moves on; a bucket left behind
+// is flagged BK_OVF.  Keys only ever move forward, and the layout that results is the one
+// sequential insertion in ascending key order gives, whatever order the claims race in
+// (priority-ordered linear probing, Shun & Blelloch 2014), so which keys share a line -- the
+// lookups' line counts, snapgpu_result_t::nProbes -- is the same on every build.  Phase 2
+// (bucket_fill_kernel) gives each placed key its values and overflow-list counts from the
+// reference table.  info: [0] keys placed, [1] buckets flagged, [2] keys that found no room (build
+// error), [3] most buckets a key lives past its home.
+__global__ __launch_bounds__(256) void bucket_place_kernel(const uint32_t *slots, const uint64_t *tableBase,
                                                            const uint64_t *tableSize, uint32_t nTables, uint64_t nSlots,
-                                                           const uint32_t *overflow, uint64_t nOverflow, uint32_t nBases,
                                                            uint4 *buckets, const uint64_t *bucketBase,
                                                            const uint32_t *bucketCount, unsigned long long *info) {
+    constexpr uint64_t OCC = 1ull << 32;
     for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < nSlots; i += (uint64_t)gridDim.x * 256u) {
-        const uint32_t v1 = slots[3 * i + 1];
-        if (v1 == sgk::INVALID) continue;
+        if (slots[3 * i + 1] == sgk::INVALID) continue;
         const uint32_t t = table_of_slot(tableBase, nTables, i);
         const uint64_t b0 = tableBase[t];
-        const uint32_t key = slots[3 * i], v2 = slots[3 * i + 2];
-        if (ref_lookup_slot(slots + 3 * b0, (uint32_t)tableSize[t], key) != i - b0) continue;   // unreachable slot
+        uint32_t x = slots[3 * i];
+        if (ref_lookup_slot(slots + 3 * b0, (uint32_t)tableSize[t], x) != i - b0) continue;   // unreachable slot
+        const uint32_t nB = bucketCount[t];
+        uint4 *T = buckets + 4ull * bucketBase[t];
+        uint32_t b = sgk::bucket_home(x, nB), moved = 0;
+        bool placed = false;
+        // every bucket step is a key moving forward: at most (keys in the table) * nB steps in all
+        for (uint64_t guard = 0; guard < 8ull * nB + 64; guard++) {
+            unsigned long long *E = reinterpret_cast<unsigned long long *>(T + 4ull * b);   // entry e: E[2e]
+            int free = -1, victim = -1;
+            uint32_t vk = 0;
+            for (int e = 0; e < 4; e++) {
+                const unsigned long long w = __hip_atomic_load(E + 2 * e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (w == 0ull) { if (free < 0) free = e; }
+                else if ((uint32_t)w > x && (victim < 0 || (uint32_t)w > vk)) { victim = e; vk = (uint32_t)w; }
+            }
+            if (free >= 0) {
+                if (atomicCAS(E + 2 * free, 0ull, OCC | x) == 0ull) {
+                    const uint32_t d = (b + nB - sgk::bucket_home(x, nB)) % nB;
+                    if (d) atomicMax(info + 3, (unsigned long long)d);
+                    placed = true;
+                    break;
+                }
+                continue;   // lost the entry: look at the bucket again
+            }
+            if (victim >= 0) {
+                if (atomicCAS(E + 2 * victim, OCC | vk, OCC | x) != (OCC | vk)) continue;
+                x = vk;   // the larger key moves on
+            }
+            if (!(atomicOr(&T[4ull * b].w, sgk::BK_OVF) & sgk::BK_OVF)) atomicAdd(info + 1, 1ull);
+            b = sgk::bucket_next(b, nB);
+            if (++moved > nB) break;
+        }
+        atomicAdd(info + (placed ? 0 : 2), 1ull);
+    }
+}
+
+// Phase 2: {key, value1, value2, counts} of every placed key (the entry 0 flag kept).  Thread per entry.
+__global__ __launch_bounds__(256) void bucket_fill_kernel(const uint32_t *slots, const uint64_t *tableBase,
+                                                          const uint64_t *tableSize, uint32_t nTables,
+                                                          const uint32_t *overflow, uint64_t nOverflow, uint32_t nBases,
+                                                          uint4 *buckets, const uint64_t *bucketBase, uint64_t nEntries) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < nEntries; i += (uint64_t)gridDim.x * 256u) {
+        uint4 &E = buckets[i];
+        if (E.y != 1u) continue;   // empty
+        const uint32_t t = table_of_slot(bucketBase, nTables, i / 4);
+        const uint64_t b0 = tableBase[t];
+        const uint64_t slot = ref_lookup_slot(slots + 3 * b0, (uint32_t)tableSize[t], E.x);
+        const uint32_t v1 = slots[3 * (b0 + slot) + 1], v2 = slots[3 * (b0 + slot) + 2];
         uint32_t c[2] = {0, 0};
         const uint32_t vs[2] = {v1, v2};
         for (int s = 0; s < 2; s++)   // overflow-list lengths (GenomeIndex.cpp:1013-1086), saturated
@@ -1181,27 +1235,9 @@ __global__ __launch_bounds__(256) void bucket_build_kernel(const uint32_t *slots
                 const uint32_t n = overflow[vs[s] - nBases];
                 c[s] = n < sgk::BK_CSAT ? n : sgk::BK_CSAT;
             }
-        const uint32_t aux = sgk::BK_OCC | c[0] | (c[1] << 15);
-        const uint32_t nB = bucketCount[t];
-        uint4 *T = buckets + 4ull * bucketBase[t];
-        uint32_t b = sgk::bucket_home(key, nB);
-        bool placed = false;
-        for (uint32_t step = 0; step < nB && !placed; step++) {
-            uint4 *B = T + 4ull * b;
-            for (int e = 0; e < 4; e++) {
-                if (atomicCAS(&B[e].w, 0u, aux) == 0u) {
-                    B[e].x = key; B[e].y = v1; B[e].z = v2;
-                    placed = true;
-                    if (step) atomicMax(info + 3, (unsigned long long)step);
-                    break;
-                }
-            }
-            if (!placed) {
-                if (!(atomicOr(&B[0].w, sgk::BK_OVF) & sgk::BK_OVF)) atomicAdd(info + 1, 1ull);
-                b = sgk::bucket_next(b, nB);
-            }
-        }
-        atomicAdd(info + (placed ? 0 : 2), 1ull);
+        E.y = v1;
+        E.z = v2;
+        E.w = (E.w & sgk::BK_OVF) | sgk::BK_OCC | c[0] | (c[1] << 15);
     }
 }
 
@@ -1406,8 +1442,9 @@ int snapgpu_device_count(void) {
 
 // The seed tables' bucket image (bucket_table.h): the reference-format slots go to the device once,
 // bucket_count_kernel counts per table the keys SNAPHashTable::Lookup can return, the host sizes
-// the tables (ceil(keys / BK_KEYS_PER_BUCKET) buckets each), bucket_build_kernel inserts, and the
-// slots are freed again: the kernels read only the buckets.
+// the tables (ceil(keys / BK_KEYS_PER_BUCKET) buckets each), bucket_place_kernel places the keys
+// (deterministically) and bucket_fill_kernel their values, and the slots are freed again: the
+// kernels read only the buckets.
 static int buildBuckets(snapgpu_aligner_t *a, hipStream_t s0) {
     const snapgpu_index_t *idx = a->idx;
     const auto t0 = std::chrono::steady_clock::now();
@@ -1454,14 +1491,16 @@ static int buildBuckets(snapgpu_aligner_t *a, hipStream_t s0) {
                 chk(hipMemcpyAsync(a->dBucketBase, base.data(), nT * 8ull, hipMemcpyHostToDevice, s0), "buckets") &&
                 chk(hipMemcpyAsync(a->dBucketCount, nb.data(), nT * 4ull, hipMemcpyHostToDevice, s0), "buckets") &&
                 chk(hipMemsetAsync(dCnt, 0, 4 * 8, s0), "counts")) {
-                hipLaunchKernelGGL(bucket_build_kernel, dim3((unsigned)std::min<uint64_t>((nSlots + 255) / 256, 1u << 20)),
-                                   dim3(256), 0, s0, dSlots, dTB, dTS, nT, nSlots, a->dOverflow,
-                                   (uint64_t)idx->overflow.size(), idx->genome->nBases, a->dBuckets, a->dBucketBase,
+                hipLaunchKernelGGL(bucket_place_kernel, dim3((unsigned)std::min<uint64_t>((nSlots + 255) / 256, 1u << 20)),
+                                   dim3(256), 0, s0, dSlots, dTB, dTS, nT, nSlots, a->dBuckets, a->dBucketBase,
                                    a->dBucketCount, dCnt);
+                hipLaunchKernelGGL(bucket_fill_kernel, dim3((unsigned)std::min<uint64_t>((4 * total + 255) / 256, 1u << 20)),
+                                   dim3(256), 0, s0, dSlots, dTB, dTS, nT, a->dOverflow, (uint64_t)idx->overflow.size(),
+                                   idx->genome->nBases, a->dBuckets, a->dBucketBase, 4 * total);
                 unsigned long long info[4] = {0, 0, 0, 0};
-                if (chk(hipGetLastError(), "bucket_build_kernel") &&
+                if (chk(hipGetLastError(), "bucket_place_kernel / bucket_fill_kernel") &&
                     chk(hipMemcpyAsync(info, dCnt, sizeof(info), hipMemcpyDeviceToHost, s0), "counts") &&
-                    chk(hipStreamSynchronize(s0), "bucket_build_kernel")) {
+                    chk(hipStreamSynchronize(s0), "bucket image build")) {
                     if (info[2] || info[0] != keys) {
                         snapgpu::setError("bucket image: " + std::to_string(info[2]) + " keys found no bucket, " +
                                           std::to_string(info[0]) + " of " + std::to_string(keys) + " inserted");

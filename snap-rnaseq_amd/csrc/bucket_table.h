@@ -17,11 +17,13 @@
 // of the overflow lists the values point at (saturated at 0x7fff; a saturated count is re-read from
 // the overflow table), so the list length needs no second dependent load either.
 //
-// Exactness: the builder (bucket_build_kernel) runs the reference's own probe sequence for every
-// used slot and keeps exactly the slots that SNAPHashTable::Lookup of their key returns, so the
-// bucket map answers every key as the reference table does (found or not, same values).  Which
-// keys share a line depends on insertion order (atomic claims), so the per-read count of lines
-// probed (snapgpu_result_t::nProbes) is a device statistic, not a reference quantity.
+// Exactness: the builder (bucket_place_kernel / bucket_fill_kernel, aligner.hip) runs the
+// reference's own probe sequence for every used slot and keeps exactly the slots that
+// SNAPHashTable::Lookup of their key returns, so the bucket map answers every key as the reference
+// table does (found or not, same values).  Which keys share a line is fixed too: placement is
+// priority-ordered (a smaller key keeps its entry), which gives the layout of sequential insertion
+// in key order on every build.  The per-read count of lines probed (snapgpu_result_t::nProbes) is
+// therefore deterministic, but it is a device statistic, not a reference quantity.
 #pragma once
 #include "align_device.h"
 
