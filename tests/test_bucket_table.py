@@ -145,3 +145,17 @@ def test_gpu_lookup_rejects_non_acgt(gpu_available, small_world):
     al = snapgpu.BaseAligner(small_world["index"])
     with pytest.raises(snapgpu.SnapGpuError):
         al.lookup_seeds(["ACGTNACGTACGTACGTACG"])
+
+
+@pytest.mark.gpu
+def test_gpu_bucket_layout_is_deterministic(gpu_available, small_world):
+    """Two aligners build the image independently (racing atomic placements): the layout -- and so
+    the lines every lookup loads, snapgpu_result_t::nProbes -- is the same."""
+    idx = small_world["index"]
+    seeds = _seed_set(small_world["genome"].bases(), 20, 4000, 2000, seed=9)
+    a, b = snapgpu.BaseAligner(idx), snapgpu.BaseAligner(idx)
+    la, lb = a.lookup_seeds(seeds, mode=0)[1], b.lookup_seeds(seeds, mode=0)[1]
+    assert np.array_equal(la, lb)
+    assert a.bucket_info()["nOverflowBuckets"] == b.bucket_info()["nOverflowBuckets"]
+    reads = small_world["reads"]
+    assert np.array_equal(a.AlignReads(reads)["nProbes"], b.AlignReads(reads)["nProbes"])
