@@ -26,6 +26,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "snapgpu.h"
 
 namespace sgk {
@@ -256,7 +258,8 @@ __device__ __forceinline__ uint32_t complement_of(uint32_t c) {   // BaseAligner
 constexpr int64_t PACK_GUARD = 1024;     // bit-plane word 0 = genome position -1024
 constexpr int EB = 8;                    // elements popped per batch (forced mode)
 constexpr int CANDCAP = EB * ELEM;       // candidate list capacity
-constexpr uint32_t ORDCAP = 256;         // forced-mode pop order (u16)
+constexpr uint32_t ORDCAP = 128;         // forced-mode pop order window (u16; reads with more linked
+                                         // elements rank in several windows, or radix-sort: radixMin)
 
 // Scorer state of the bit-plane kernels align_kernel<128> / <256> (align_score.h); NW =
 // 64-position words of the read masks.
@@ -266,8 +269,11 @@ struct GroupLdsT {
     uint32_t ecache[EB][24];             // popped Elem128s (authoritative while in the batch)
     uint32_t eidx[EB];
     uint16_t cand[CANDCAP];              // slot << 8 | bit
-    int16_t pm[2][128];                  // LV path per [direction][group*2*GS + row]: matched-run length
-    int8_t pa[2][128];                   //   and action (0 X, 1 D, 2 I); probabilities in apply
+    // LV path per [direction][group * GS/2 + row] (a group of GS lanes runs at k < GS/2, so rows
+    // 1..k fit its GS/2 slots; 32 per direction): matched-run length and action (0 X, 1 D, 2 I);
+    // probabilities in apply
+    uint8_t pm[2][32];
+    int8_t pa[2][32];
     int16_t pL0[2][8];                   //   exact prefix L[0][0] per group
     int8_t plen[2][8];                   //   path length (0: exact match, prob = perfect[patternLen])
 };
@@ -278,12 +284,20 @@ struct Lds {
     static constexpr int NB = MAXLEN / 64;          // 64-position blocks
     static constexpr bool BYTE_PATH = MAXLEN > 256; // byte-compare LV (align_device.h) vs bit planes
     static constexpr int NW = BYTE_PATH ? 1 : NB;   // bit-plane mask words
-    char fwd[MAXLEN + 64];                          // read[FORWARD], zero slack
-    char rc[MAXLEN + 64];                           // read[RC]
-    char fwdQ[MAXLEN + 64];
-    char rcQ[MAXLEN + 64];
+    // The bit-plane kernels keep only the forward read: the reverse complement's planes are built
+    // from it, its qualities read backwards.  The byte path keeps both, with 64 bytes of slack.
+    static constexpr int RL = BYTE_PATH ? MAXLEN + 64 : MAXLEN;
+    static constexpr int RCL = BYTE_PATH ? MAXLEN + 64 : 1;
+    // element hash-chain heads: u16 on the bit-plane kernels (arenas capped below 0xffff elements,
+    // snapgpu_aligner_create), u32 on the byte path (the big-arena pass's worst-case arenas)
+    using HeadT = typename std::conditional<BYTE_PATH, uint32_t, uint16_t>::type;
+    static constexpr HeadT HEAD_NONE = (HeadT)~(HeadT)0;
+    char fwd[RL];                                   // read[FORWARD], zero slack
+    char rc[RCL];                                   // read[RC] (byte path)
+    char fwdQ[RL];
+    char rcQ[RCL];
     uint32_t win[BYTE_PATH ? (MAXLEN + 192) / 4 : 1];   // genome window [g-64, g+n+64+64)
-    uint32_t head[NBUCKET];                         // element hash chains
+    HeadT head[NBUCKET];                            // element hash chains
     // hit insertion and scoring never overlap in time: their scratch shares LDS (the
     // insertion table is cleared again after every score call that used it)
     union {
@@ -293,9 +307,10 @@ struct Lds {
             uint32_t scrLoc[WAVE];                  // batch scratch: hit location per lane
         } ins;
         struct {
-            // LV rows (L + 2 per row, lane; actions recomputed); between passes, the staged
-            // selection keys of the forced-mode ranking
-            alignas(16) uint8_t rows8[BYTE_PATH ? 1 : MAX_K][WAVE];
+            // LV rows 1..MAX_K-1 (L + 2 per row, lane; actions recomputed; row 0 is never stored:
+            // lv_rows() maps row e to rows8[e - 1]); between passes, the staged selection keys of
+            // the forced-mode ranking
+            alignas(16) uint8_t rows8[BYTE_PATH ? 1 : MAX_K - 1][WAVE];
             uint16_t order[ORDCAP];                 // forced-mode pop order
         } sc;
     } u;
@@ -311,6 +326,35 @@ struct Lds {
     uint16_t rows[BYTE_PATH ? MAX_K : 1][WAVE];     // byte-path LV rows: (L+2) | action<<12
     GroupLdsT<NW> grp[BYTE_PATH ? 0 : 1];           // scorer of align_kernel<128> / <256>
 };
+// LV row e (1 <= e < MAX_K) of the bit-plane scorer at rows8[e - 1]
+template <int MAXLEN>
+__device__ __forceinline__ uint8_t (*lv_rows(Lds<MAXLEN> &S))[WAVE] {
+    return reinterpret_cast<uint8_t (*)[WAVE]>(&S.u.sc.rows8[0][0] - WAVE);
+}
+// head of element hash chain h (NONE when empty)
+template <int MAXLEN>
+__device__ __forceinline__ uint32_t head_get(const Lds<MAXLEN> &S, uint32_t h) {
+    const auto v = S.head[h];
+    return v == Lds<MAXLEN>::HEAD_NONE ? NONE : (uint32_t)v;
+}
+// head[h] = e, returning the previous head (NONE when empty); leaders of one insertion step may
+// share a bucket, so the exchange is atomic (a CAS on the dword holding a u16 head)
+template <int MAXLEN>
+__device__ __forceinline__ uint32_t head_exchange(Lds<MAXLEN> &S, uint32_t h, uint32_t e) {
+    if constexpr (Lds<MAXLEN>::BYTE_PATH) {
+        return atomicExch(&S.head[h], e);
+    } else {
+        uint32_t *w = reinterpret_cast<uint32_t *>(&S.head[h & ~1u]);
+        const uint32_t sh = 16u * (h & 1u);
+        uint32_t old = *w, assumed;
+        do {
+            assumed = old;
+            old = atomicCAS(w, assumed, (assumed & ~(0xffffu << sh)) | ((e & 0xffffu) << sh));
+        } while (old != assumed);
+        const uint32_t o = (old >> sh) & 0xffffu;
+        return o == 0xffffu ? NONE : o;
+    }
+}
 
 // ------------------------------------------------------------ LV engine
 // Per-lane mismatch bitmap over read positions m in [0, NB*64):
@@ -716,7 +760,7 @@ __device__ __forceinline__ uint32_t elem_hash(uint32_t key) { return (key * 2654
 template <int MAXLEN>
 __device__ __forceinline__ uint32_t chain_find(const KArgs &A, const Lds<MAXLEN> &S, const ElemOf<MAXLEN> *ar, uint32_t key,
                                                uint32_t cap) {
-    uint32_t e = S.head[elem_hash(key)];
+    uint32_t e = head_get(S, elem_hash(key));
     for (uint32_t steps = 0; e != NONE; steps++) {
         if (steps > cap) { diag_report(A.diag, DIAG_CHAIN, key, e); return NONE; }
         if (e < MIRCAP) {

@@ -150,7 +150,7 @@ __device__ __forceinline__ int lv_group(GroupLdsT<NW> &G, uint8_t (*rows8)[WAVE]
     const bool gfirst = li == 0, glast = li == GS - 1;   // group boundaries of the row shifts
     const int d = DIR > 0 ? li - c : c - li;
     const int ad = d < 0 ? -d : d;                      // diagonal d is in row e's band iff |d| <= e
-    const int pbase = gi * 2 * GS;                       // this group's path slots
+    const int pbase = gi * (GS / 2);                     // this group's path slots: rows 1..k, k < GS / 2
     if (k > MAX_K - 1) k = MAX_K - 1;
     outE = -1;
     uint32_t done = gact ? 0u : 1u;   // a VGPR flag: ballot(done == 0) is one v_cmp
@@ -240,7 +240,7 @@ __device__ __forceinline__ int lv_group(GroupLdsT<NW> &G, uint8_t (*rows8)[WAVE]
                     const int Lsrc = a == 2 ? right - 1 : (a == 1 ? left : x1 - 1);
                     if (li == 0) {
                         G.pa[dx][pbase + ce] = (int8_t)a;
-                        G.pm[dx][pbase + ce] = (int16_t)(a == 1 ? Lcur - Lsrc : Lcur - Lsrc - 1);
+                        G.pm[dx][pbase + ce] = (uint8_t)(a == 1 ? Lcur - Lsrc : Lcur - Lsrc - 1);
                     }
                     curD = src;
                     Lcur = Lsrc;
@@ -264,7 +264,7 @@ __device__ __forceinline__ int lv_group(GroupLdsT<NW> &G, uint8_t (*rows8)[WAVE]
 // reference's order (x * 1.0 == x, so steps without a factor multiply by 1.0).
 template <int NW>
 __device__ __forceinline__ void lv_prob_pair(const DevTables *tab, const GroupLdsT<NW> &G, int g, int pbase, int n, int s0,
-                                             int t0, const char *qual, double &p1, double &p2, int &net2) {
+                                             int t0, const char *fwdQ, uint32_t rcRead, double &p1, double &p2, int &net2) {
     const int lane = lane_id();
     const int dx = lane >> 5, j = (lane & 31) + 1;               // step j of direction dx
     const int e = G.plen[dx][g];
@@ -296,7 +296,10 @@ __device__ __forceinline__ void lv_prob_pair(const DevTables *tab, const GroupLd
     if (qi > patternLen - 1) qi = patternLen - 1;
     const int DIR = dx ? -1 : 1;
     double f = 1.0;
-    if (valid && a == 0) f = g_tab.phred[(uint8_t)qual[p0 + DIR * qi]];
+    if (valid && a == 0) {   // quality of read[dir] position p: the forward read's, reversed for RC
+        const int p = p0 + DIR * qi;
+        f = g_tab.phred[(uint8_t)fwdQ[rcRead ? n - 1 - p : p]];
+    }
     else if (runEnd) f = g_tab.indel[cnt];
     const double perf = lane == 0 || lane == 32 ? g_tab.perfect[patternLen - e] : 1.0;
     const int e1 = G.plen[0][g], e2 = G.plen[1][g];
@@ -400,7 +403,7 @@ __device__ __forceinline__ void lv_pass(const KArgs &A, Lds<MAXLEN> &S, uint32_t
     PH_ADD(A, S, PH_STAGE, tst);
     PH_T(A, tf);
     const int t = P.s + (int)A.seedLen;
-    const int rf = lv_group<1, GS, NW, true>(G, S.u.sc.rows8, F, P.act, t, (int)n - t, P.glen - t, k, k, e1);
+    const int rf = lv_group<1, GS, NW, true>(G, lv_rows(S), F, P.act, t, (int)n - t, P.glen - t, k, k, e1);
     PH_ADD(A, S, PH_LVF, tf);
     PH_CNT(A, S, PH_ROWSF, rf);
     PH_CNT(A, S, GS <= 16 ? PH_NPASS16 : (GS == 32 ? PH_NPASS32 : PH_NPASS64), 1);
@@ -412,7 +415,7 @@ __device__ __forceinline__ void lv_pass(const KArgs &A, Lds<MAXLEN> &S, uint32_t
     if (kmax2 >= 0) {
         // reverse LV: pattern = read[s-1 .. 0], text = genome backwards from loc+s-1 (BaseAligner.cpp:1216-1220)
         const MaskW<NW> R = mk_reverse(F);
-        const int rr = lv_group<-1, GS, NW>(G, S.u.sc.rows8, R, ract, 64 * NW - 1 - (P.s - 1), P.s, P.s + MAX_K, k2,
+        const int rr = lv_group<-1, GS, NW>(G, lv_rows(S), R, ract, 64 * NW - 1 - (P.s - 1), P.s, P.s + MAX_K, k2,
                                             kmax2, e2);
         PH_CNT(A, S, PH_ROWSR, rr);
     }
@@ -513,7 +516,7 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem1
         }
         double q1, q2;
         int net2;
-        lv_prob_pair(tab, G, gs, gs * 2 * GS, (int)n, s0, t0, dir ? S.rcQ : S.fwdQ, q1, q2, net2);
+        lv_prob_pair(tab, G, gs, gs * (GS / 2), (int)n, s0, t0, S.fwdQ, dir, q1, q2, net2);
         const double prob = q1 * q2 * tab->seedProb;
         const uint32_t loc = elemLoc + (uint32_t)net2;
         const bool anyNearby0 = cScored != 0;

@@ -285,7 +285,7 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
                         }
                         isNew = true;
                         w11 = (lpsNow & 0xffu) << 8;
-                        const uint32_t old = atomicExch(&S.head[elem_hash(key)], e);
+                        const uint32_t old = head_exchange(S, elem_hash(key), e);
                         if (e < MIRCAP) { S.ekey[e] = key; S.enext[e] = (uint16_t)(old == NONE ? 0xffffu : old); }
                         chainNext = old;
                         used = 1ull << bit;
@@ -391,15 +391,17 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
         // Read::init upper-casing + BaseAligner.cpp:636-650 (RC read, qualities)
         uint32_t nN = 0;
         bool other = false;
-        for (int i = lane; i < MAXLEN + 64; i += WAVE) {
+        for (int i = lane; i < Lds<MAXLEN>::RL; i += WAVE) {
             uint32_t c = 0, q = 0;
             if (i < (int)n) {
                 c = (uint8_t)A.bases[off + i];
                 q = (uint8_t)A.quals[off + i];
                 if (c >= 'a' && c <= 'z') c -= 0x20;
-                S.rc[n - 1 - i] = (char)complement_of(c);
-                S.rcQ[n - 1 - i] = (char)q;
-            } else {
+                if constexpr (Lds<MAXLEN>::BYTE_PATH) {
+                    S.rc[n - 1 - i] = (char)complement_of(c);
+                    S.rcQ[n - 1 - i] = (char)q;
+                }
+            } else if constexpr (Lds<MAXLEN>::BYTE_PATH) {
                 S.rc[i] = 0;
                 S.rcQ[i] = 0;
             }
@@ -413,7 +415,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
             // non-ACGTN bytes (an IUPAC code could then match itself): byte path
             if (A.hasIupac && other) { defer_read(A, r); return; }
         }
-        for (int i = lane; i < NBUCKET; i += WAVE) S.head[i] = NONE;
+        for (int i = lane; i < NBUCKET; i += WAVE) S.head[i] = Lds<MAXLEN>::HEAD_NONE;
         for (int i = lane; i < BT; i += WAVE) { S.u.ins.btKey[i] = NONE; S.u.ins.btMask[i] = 0; }
         S.laneMax[lane] = 0;
         if (lane == 0) S.nElems = 0;
@@ -422,12 +424,20 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
 #pragma unroll
             for (int b = 0; b < NB; b++) { rbF[b] = (uint8_t)S.fwd[b * 64 + lane]; rbR[b] = (uint8_t)S.rc[b * 64 + lane]; }
         } else {
-            // read bit planes {hi, lo, notACGT} of both directions; zero slack past n is not ACGT
+            // read bit planes {hi, lo, notACGT} of both directions; zero slack past n is not ACGT.
+            // read[RC][m] = complement of read[FORWARD][n-1-m] (BaseAligner.cpp:636-650): the 2-bit
+            // code xor 3 (A<->T, C<->G); N and the other bytes stay not ACGT
 #pragma unroll
             for (int dr = 0; dr < 2; dr++)
 #pragma unroll
                 for (int h = 0; h < NB; h++) {
-                    const uint32_t code = packed_code((uint8_t)(dr ? S.rc : S.fwd)[h * 64 + lane]);
+                    const int m = h * 64 + lane;
+                    uint32_t code;
+                    if (dr == 0) code = packed_code((uint8_t)S.fwd[m]);
+                    else {
+                        code = m < (int)n ? packed_code((uint8_t)S.fwd[n - 1 - m]) : 4u;
+                        if (code < 4) code ^= 3u;
+                    }
                     const uint64_t bh = ballot(code < 4 && (code & 2)), bl = ballot(code < 4 && (code & 1));
                     const uint64_t bm = ballot(code > 3);
                     if (lane == 0) { S.grp[0].rpl[dr][0][h] = bh; S.grp[0].rpl[dr][1][h] = bl; S.grp[0].rpl[dr][2][h] = bm; }
@@ -753,8 +763,8 @@ __device__ __forceinline__ void lvg_run(Lds<64 * NW> &S, const LvgTask &T, const
 #pragma unroll
     for (int j = 0; j < NW; j++) F.w[j] = ((uint64_t)f[2 * j + 1] << 32) | f[2 * j];
     int e = -1;
-    if (DIR > 0) lv_group<1, GS, NW>(G, S.u.sc.rows8, F, act, 0, pl, tl, T.k, T.k, e);
-    else lv_group<-1, GS, NW>(G, S.u.sc.rows8, mk_reverse(F), act, 64 * NW - 1 - (pl - 1), pl, tl, T.k, T.k, e);
+    if (DIR > 0) lv_group<1, GS, NW>(G, lv_rows(S), F, act, 0, pl, tl, T.k, T.k, e);
+    else lv_group<-1, GS, NW>(G, lv_rows(S), mk_reverse(F), act, 64 * NW - 1 - (pl - 1), pl, tl, T.k, T.k, e);
     e = readlane(e, 0);
     wave_sync();
     double p1 = 1.0, p2 = 1.0;
@@ -763,7 +773,7 @@ __device__ __forceinline__ void lvg_run(Lds<64 * NW> &S, const LvgTask &T, const
         if (lane == 0) G.plen[DIR > 0 ? 1 : 0][0] = 0;   // only this direction's path
         wave_sync();
         // forward: patternLen = n - t0 = pl (t0 = 0); reverse: patternLen = s0 = pl (t0 = n)
-        lv_prob_pair(nullptr, G, 0, 0, pl, DIR > 0 ? 0 : pl, DIR > 0 ? 0 : pl, S.fwdQ, p1, p2, net2);
+        lv_prob_pair(nullptr, G, 0, 0, pl, DIR > 0 ? 0 : pl, DIR > 0 ? 0 : pl, S.fwdQ, 0u, p1, p2, net2);
     }
     if (lane == 0) {
         outScore[blockIdx.x] = e;
@@ -780,7 +790,7 @@ __global__ __launch_bounds__(64) void lv_group_kernel(const LvgTask *tasks, cons
     const int lane = lane_id();
     const LvgTask T = tasks[blockIdx.x];
     // qualities in read coordinates (reverse: read[m] = pattern[pl-1-m])
-    for (int m = lane; m < 64 * NW + 64; m += WAVE)
+    for (int m = lane; m < Lds<64 * NW>::RL; m += WAVE)
         S.fwdQ[m] = m < T.pl ? (T.dir > 0 ? quals[T.pOff + m] : quals[T.pOff + T.pl - 1 - m]) : 0;
     wave_sync();
     const int k = T.k < MAX_K - 1 ? T.k : MAX_K - 1;
@@ -1664,6 +1674,8 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
     // (Round 2 halved the grid instead: the RNA aligners ran at 1 wave per SIMD.)
     const uint64_t budget = 8ull << 30, bigBudget = 4ull << 30;   // HBM per lane: main and big-arena pass
     a->arenaCap = std::min<uint64_t>(a->arenaElems, budget / ((uint64_t)a->grid * sizeof(Elem512)));
+    // the bit-plane kernels keep u16 element indices in their LDS chain heads (Lds::HeadT)
+    a->arenaCap = std::min<uint64_t>(a->arenaCap, 0xfffeu);
     if (const char *t = getenv("SNAPGPU_ARENA_CAP"); t && atoll(t) >= 1)   // test hook: force the overflow path
         a->arenaCap = std::min<uint64_t>(a->arenaCap, (uint64_t)atoll(t));
     if (a->arenaCap < a->arenaElems)
