@@ -680,7 +680,7 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, El
     const DevTables *tab = A.tab;
     for (int d = 0; d < 2; d++)
         if (st.mostSeeds[d]) {
-            const uint32_t v = st.nSeedsApplied[d] / st.mostSeeds[d];
+            const uint32_t v = uni(st.nSeedsApplied[d] / st.mostSeeds[d]);   // (VALU division: back to an SGPR)
             if (v > st.lps[d]) st.lps[d] = v;
         }
     const uint32_t minLps = st.lps[0] < st.lps[1] ? st.lps[0] : st.lps[1];

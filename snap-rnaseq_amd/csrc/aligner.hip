@@ -37,7 +37,7 @@ __device__ __forceinline__ bool score_wave(const KArgs &A, Lds<MAXLEN> &S, Elem5
     const DevTables *tab = A.tab;
     for (int d = 0; d < 2; d++)
         if (st.mostSeeds[d]) {
-            uint32_t v = st.nSeedsApplied[d] / st.mostSeeds[d];
+            uint32_t v = uni(st.nSeedsApplied[d] / st.mostSeeds[d]);
             if (v > st.lps[d]) st.lps[d] = v;
         }
     do {
@@ -668,7 +668,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
     }
     PH_T(A, tout);
     if (st.abort == 2u) {   // outgrew the capped arena: no record here, the big-arena pass aligns it afresh
-        if (lane == 0) A.ovfList[atomicAdd(A.ovfCount, 1u)] = r;
+        if (lane_id() == 0) A.ovfList[atomicAdd(A.ovfCount, 1u)] = r;
         wave_sync();
         PH_ADD(A, S, PH_OUT, tout);
         return;
@@ -676,7 +676,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
     const uint32_t svLookups = sv_get(st, SV_LOOKUPS), svScored = sv_get(st, SV_SCORED);
     const uint32_t svPopular = sv_get(st, SV_POPULAR), svProbes = sv_get(st, SV_PROBES);
     const uint32_t svHitWords = sv_get(st, SV_HITWORDS), svOvf = sv_get(st, SV_OVF);
-    if (lane == 0) {
+    if (lane_id() == 0) {   // (re-read: the setup's lane id is not kept live across the seed loop)
         snapgpu_result_t o;
         o.location = st.outLoc;
         o.score = st.outScore;
