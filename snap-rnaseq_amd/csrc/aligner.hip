@@ -1866,7 +1866,8 @@ static int launch_passes(snapgpu_aligner_t *a, int li, const PassIO &io, const A
     A.seedRecs = nullptr;
     A.longCount = L.counter + 5;
     HIPCHK(hipEventRecord(ev.e[3], L.stream));
-    hipLaunchKernelGGL(seed_lookup_kernel, dim3((unsigned)((io.n + 3) / 4)), dim3(64), 0, L.stream, A, io.seeds,
+    hipLaunchKernelGGL(seed_lookup_kernel, dim3((unsigned)((io.n + 4 * LOOKUP_WAVES - 1) / (4 * LOOKUP_WAVES))),
+                       dim3(64 * LOOKUP_WAVES), 0, L.stream, A, io.seeds,
                        L.lookupStats);
     HIPCHK(hipGetLastError());
     A.seedRecs = reinterpret_cast<const uint4 *>(io.seeds);
