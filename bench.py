@@ -41,11 +41,12 @@ METRIC = "aligned reads/sec (100 bp SE, k=20 seed) at 1/2/4/8 GPUs + CPU baselin
 
 WORKLOADS = {
     # configs[1]: GRCh38 chr21-sized index in HBM, 1M reads on 1 GPU
-    "c2": dict(genome_bases=46_709_983, n_contigs=1, reads=1_000_000, families=200,
+    "c2": dict(genome_bases=46_709_983, n_contigs=1, reads=1_000_000, families=200, paired_pairs=500_000,
                desc="C2: chr21-sized (46,709,983 bp) synthetic repeat-rich genome, seed-20 index in HBM, "
                     "{reads} x 100 bp SE reads per GPU (configs[1] shape)"),
     # configs[2]: full GRCh38-sized index, 50M reads over 8 GPUs -> the per-GPU shard
-    "c3": dict(genome_bases=3_100_000_000, n_contigs=25, reads=6_250_000, families=2000,
+    # (its paired leg: configs[3]'s 25M 2 x 101 pairs over 8 GPUs -> 3,125,000 pairs per GPU)
+    "c3": dict(genome_bases=3_100_000_000, n_contigs=25, reads=6_250_000, families=2000, paired_pairs=3_125_000,
                desc="C3 per-GPU shard: ~3.1 Gb 25-contig synthetic repeat-rich genome, seed-20 index in HBM, "
                     "{reads} x 100 bp SE reads per GPU (configs[2]: 50M reads / 8 GPUs)"),
 }
@@ -239,6 +240,7 @@ def paired_leg(args, idx, local, rank, cpus):
            "status_pairs": {int(k): int(v) for k, v in zip(*np.unique(res["status"][:, 0], return_counts=True))},
            "deferred_to_pass2": int(((inter["flags"] & snapgpu.PFLAG_DEFERRED) != 0).sum()),
            "params": "paired CLI defaults: maxHits 16000, maxDist 15, 8 seeds, extra 2, spacing 50..1000",
+           "workload": args.workload + (" (configs[3] per-GPU shard: 25M pairs / 8 GPUs)" if n == 3_125_000 else ""),
            "boundary": "host pairs in -> host PairedAlignmentResult out (snapgpu_paired_align_batch)"}
     if not args.no_cpu_baseline:
         from oracle_ffi import oracle_paired
@@ -477,8 +479,9 @@ def main():
     ap.add_argument("--reads", type=int, default=None, help="reads per GPU (default: the workload's)")
     ap.add_argument("--genome-bases", type=int, default=None)
     ap.add_argument("--resident-steps", type=int, default=5)
-    ap.add_argument("--paired-pairs", type=int, default=500_000,
-                    help="extras.paired: 2 x 101 bp pairs through the GPU ChimericPairedEndAligner (0: skip)")
+    ap.add_argument("--paired-pairs", type=int, default=None,
+                    help="extras.paired: 2 x 101 bp pairs through the GPU ChimericPairedEndAligner (0: skip; default: "
+                         "the workload's -- 500k on c2, configs[3]'s per-GPU shard of 3,125,000 on c3)")
     ap.add_argument("--rna-pairs", type=int, default=100_000,
                     help="extras.rna_paired: 2 x 150 bp pairs through the RNA paired product path (0: skip)")
     ap.add_argument("--mode", choices=("stream", "sync"), default="stream",
@@ -493,6 +496,8 @@ def main():
     self_launch(args, sys.argv[1:])
     _stdout_to_stderr()
     wl = dict(WORKLOADS[args.workload])
+    if args.paired_pairs is None:
+        args.paired_pairs = wl["paired_pairs"]
     if args.reads:
         wl["reads"] = args.reads
     if args.genome_bases:

@@ -62,10 +62,16 @@ struct DevTables {
 // table pointer argument is one more SGPR pair to keep live (and spill) in the scorer.
 static __device__ DevTables g_tab;   // per translation unit (aligner.hip, paired.hip): each sets its own
 
-// HashTableElement (BaseAligner.h:188-214) in the HBM arena: a 48-byte header of
-// the fields the kernels read and write, then the per-candidate seed offsets.  Reads
-// of <= 256 bases (the bit-plane kernels) keep u8 offsets (96-B elements); the byte
-// path keeps u16 (144 B).
+// HashTableElement (BaseAligner.h:188-214) in the HBM arena: a 48-byte header of the fields the
+// kernels read and write, then the per-candidate seed offsets.
+//
+// The byte path (reads > 256 bases) keeps every candidate's u16 offset in the element (Elem512,
+// 144 B).  The bit-plane kernels (reads <= 256 bases, u8 offsets) keep an element in one 64-B
+// line (Elem64): most elements use one or two of their 48 candidates, so the header is followed
+// by eight (bit + 1, offset) byte pairs in first-use order; an element that uses a ninth
+// candidate gets a spill block -- a 64-B slot taken from the top of the wave's arena, offsets by
+// bit -- into which the eight are copied, and its offsets live there from then on (w11.spill).
+// A read's elements then stay one line each (round 3: 96 B, two or three lines per pair).
 template <typename OffT>
 struct ElemT {
     uint64_t used;            // candidatesUsed
@@ -80,12 +86,56 @@ struct ElemT {
     OffT seedOffset[ELEM];
     static constexpr int DWORDS = (48 + ELEM * (int)sizeof(OffT)) / 4;
 };
-using Elem128 = ElemT<uint8_t>;
 using Elem512 = ElemT<uint16_t>;
-static_assert(sizeof(Elem128) == 96 && sizeof(Elem512) == 144, "Elem layout");
+struct Elem64 {
+    uint64_t used;            // dw 0-1   candidatesUsed
+    uint64_t scored;          // dw 2-3   candidatesScored
+    double prob;              // dw 4-5   matchProbabilityForBestScore
+    uint32_t key;             // dw 6     (base/48)<<1 | direction
+    uint32_t next;            // dw 7     hash chain
+    uint32_t bestScore;       // dw 8
+    uint32_t bestLoc;         // dw 9     bestScoreGenomeLocation
+    uint32_t sortkey;         // dw 10    linked ? weight<<24 | (0xffffff - ts) : 0
+    uint32_t w11;             // dw 11    weight | lps << 8 | allScored << 16 | spill << 17
+    uint32_t slot[4];         // dw 12-15 (bit + 1, seed offset) byte pairs, first-use order; 0 = free
+    static constexpr int DWORDS = 16;
+};
+static_assert(sizeof(Elem512) == 144 && sizeof(Elem64) == 64, "Elem layout");
+constexpr uint32_t W11_ALLSCORED = 1u << 16;
+constexpr int W11_SPILL_SHIFT = 17;                  // spill block index (0 = none), 15 bits
+constexpr uint32_t ELEM64_MAX = 0x7fffu;             // bit-plane arenas: at most this many 64-B slots
+constexpr int NSLOT = 8;                             // inline offsets per Elem64
+// an Elem64's spill block (an arena slot index; 0 = none): its bytes 0..47 are the seed offsets by bit
+__device__ __forceinline__ uint32_t spill_index(uint32_t w11) { return w11 >> W11_SPILL_SHIFT; }
+// seed offset of candidate `bit` from an Elem64's four slot dwords (0xffffffff when not held there)
+__device__ __forceinline__ uint32_t slot_offset(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, uint32_t bit) {
+    const uint32_t tag = bit + 1u;
+    uint32_t r = 0xffffffffu;
+    const uint32_t s[4] = {s0, s1, s2, s3};
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        if ((s[i] & 0xffu) == tag) r = (s[i] >> 8) & 0xffu;
+        if (((s[i] >> 16) & 0xffu) == tag) r = s[i] >> 24;
+    }
+    return r;
+}
+// the inline slot (0..7) holding candidate `bit` (NSLOT when none)
+__device__ __forceinline__ uint32_t slot_of(const uint32_t (&s)[4], uint32_t bit) {
+    uint32_t r = NSLOT;
+#pragma unroll
+    for (int q = NSLOT - 1; q >= 0; q--)
+        if (((s[q >> 1] >> (16 * (q & 1))) & 0xffu) == bit + 1u) r = (uint32_t)q;
+    return r;
+}
+// slot k := (bit + 1, offset), registers only (selects, no dynamic indexing)
+__device__ __forceinline__ void slot_set(uint32_t (&s)[4], uint32_t k, uint32_t bit, uint32_t offset) {
+    const uint32_t sh = 16u * (k & 1u), v = ((offset & 0xffu) << 8 | (bit + 1u)) << sh, keep = ~(0xffffu << sh);
+#pragma unroll
+    for (int d = 0; d < 4; d++) s[d] = (k >> 1) == (uint32_t)d ? (s[d] & keep) | v : s[d];
+}
 template <int MAXLEN> struct ElemSel { using type = Elem512; };
-template <> struct ElemSel<128> { using type = Elem128; };
-template <> struct ElemSel<256> { using type = Elem128; };
+template <> struct ElemSel<128> { using type = Elem64; };
+template <> struct ElemSel<256> { using type = Elem64; };
 template <int MAXLEN> using ElemOf = typename ElemSel<MAXLEN>::type;
 
 // Genome bit planes: 32 bases per 12-byte word, 3 bits per base -- the 2-bit code (A=00 C=01 G=10
@@ -266,7 +316,7 @@ constexpr uint32_t ORDCAP = 128;         // forced-mode pop order window (u16; r
 template <int NW>
 struct GroupLdsT {
     uint64_t rpl[2][3][NW];              // read[dir] bit planes {hi, lo, notACGT}, positions 0..64*NW-1
-    uint32_t ecache[EB][24];             // popped Elem128s (authoritative while in the batch)
+    uint32_t ecache[EB][16];             // popped Elem64s (authoritative while in the batch)
     uint32_t eidx[EB];
     uint16_t cand[CANDCAP];              // slot << 8 | bit
     // LV path per [direction][group * GS/2 + row] (a group of GS lanes runs at k < GS/2, so rows
@@ -316,7 +366,9 @@ struct Lds {
     } u;
     uint64_t laneMax[WAVE];                         // per-owner-lane max (sortkey<<32 | idx)
     uint32_t nElems;
-    uint32_t pad_[3];
+    uint32_t nSpill;                                // Elem64 spill blocks, taken from the arena's top
+    uint32_t nUsed;                                 // nElems + nSpill: the arena is full at arenaElems
+    uint32_t pad_[1];
     alignas(16) uint32_t sk[SKCAP];                 // selection keys of elements < SKCAP
     uint32_t ekey[MIRCAP];                          // element key / hash-chain link of elements < MIRCAP
     uint16_t enext[MIRCAP];                         //   (0xffff = end of chain)

@@ -339,8 +339,8 @@ struct PassLane {
 
 // One speculative pass over up to G = 64/GS candidates [i0, i0+m) of the list.
 template <int GS, int MAXLEN>
-__device__ __forceinline__ void lv_pass(const KArgs &A, Lds<MAXLEN> &S, uint32_t i0, int m, int k, uint32_t n,
-                                        PassLane &P, int &e1, int &e2) {
+__device__ __forceinline__ void lv_pass(const KArgs &A, Lds<MAXLEN> &S, const Elem64 *ar, uint32_t i0, int m, int k,
+                                        uint32_t n, PassLane &P, int &e1, int &e2) {
     constexpr int NW = Lds<MAXLEN>::NW;
     GroupLdsT<NW> &G = S.grp[0];
     const int lane = lane_id();
@@ -351,11 +351,14 @@ __device__ __forceinline__ void lv_pass(const KArgs &A, Lds<MAXLEN> &S, uint32_t
     if (P.act) {
         const uint32_t cw = G.cand[i0 + gi];
         const uint32_t sl = cw >> 8, bit = cw & 0xff;
-        const uint32_t key = G.ecache[sl][6];
+        const uint32_t *ec = G.ecache[sl];
+        const uint32_t key = ec[6], sp = spill_index(ec[11]);
         P.cw = cw;
         P.loc = (key >> 1) * ELEM + bit;
         P.dir = (int)(key & 1);
-        P.s = (int)((G.ecache[sl][12 + bit / 4] >> (8 * (bit & 3))) & 0xff);
+        // the candidate's seed offset: the element's inline slots, or its spill block
+        P.s = (int)(sp ? (uint32_t)reinterpret_cast<const uint8_t *>(ar + sp)[bit]
+                       : slot_offset(ec[12], ec[13], ec[14], ec[15], bit));
         uint32_t glen = n + MAX_K;
         bool ok = substring_ok(A, P.loc, glen);
         if (!ok) {   // BaseAligner.cpp:1163-1185
@@ -426,10 +429,10 @@ __device__ __forceinline__ void lv_pass(const KArgs &A, Lds<MAXLEN> &S, uint32_t
 // order (BaseAligner.cpp:1129-1384).  Returns true when the read is finished
 // (stopOnFirstHit).  GS is a template parameter so group indexing is shifts and the
 // per-group loops unroll.
-constexpr int FETCH_NLD = (EB * Elem128::DWORDS + WAVE - 1) / WAVE;   // dwords per lane of a popped batch
+constexpr int FETCH_NLD = (EB * Elem64::DWORDS + WAVE - 1) / WAVE;   // dwords per lane of a popped batch
 
 template <int GS, bool EXT, int MAXLEN>
-__device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem128 *ar, ReadState &st, uint32_t i0, int m,
+__device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem64 *ar, ReadState &st, uint32_t i0, int m,
                                            int k, uint32_t n, uint32_t nb, uint32_t &lastSlot, bool &lastSkip,
                                            int *result) {
     const int lane = lane_id();
@@ -437,7 +440,7 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem1
     const DevTables *tab = A.tab;
     PassLane P;
     int e1, e2;
-    lv_pass<GS, MAXLEN>(A, S, i0, m, k, n, P, e1, e2);
+    lv_pass<GS, MAXLEN>(A, S, ar, i0, m, k, n, P, e1, e2);
     PH_T(A, tapp);
     // ---- apply in order with the limit in force at each candidate.  Group
     // leaders (lane g*GS) hold candidate g.  A failure only sets its scored bit
@@ -593,9 +596,10 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem1
 // pops then read it from the top.  O(n) per pass where the windowed ranks cost O(n^2) per
 // 256-element window.  Returns false (rank path) when the arena tail cannot hold two buffers.
 template <int MAXLEN>
-__device__ __forceinline__ bool forced_sort(const KArgs &A, Lds<MAXLEN> &S, Elem128 *ar, uint32_t nE,
+__device__ __forceinline__ bool forced_sort(const KArgs &A, Lds<MAXLEN> &S, Elem64 *ar, uint32_t nE,
                                             const uint64_t *&sorted, uint32_t &nLinked) {
-    if (((uint64_t)A.arenaElems - nE) * sizeof(Elem128) < 16ull * nE + 64) return false;
+    // the free slots between the elements and the spill blocks at the arena's top
+    if (((uint64_t)A.arenaElems - S.nSpill - nE) * sizeof(Elem64) < 16ull * nE + 64) return false;
     uint64_t *bufA = reinterpret_cast<uint64_t *>(ar + nE), *bufB = bufA + nE;
     uint32_t n = 0, kOr = 0, kAnd = 0xffffffffu;
     for (uint32_t e0 = 0; e0 < nE; e0 += WAVE) {   // linked elements, compacted in index order
@@ -669,14 +673,14 @@ __device__ __forceinline__ bool forced_sort(const KArgs &A, Lds<MAXLEN> &S, Elem
 
 // BaseAligner::score (BaseAligner.cpp:977-1399) over batches of popped elements.
 template <bool EXT, int MAXLEN>
-__device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, Elem128 *ar, ReadState &st, bool force,
+__device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, Elem64 *ar, ReadState &st, bool force,
                                            uint32_t n, int *result, uint32_t *flags) {
     const int lane = lane_id();
     auto &G = S.grp[0];
     const DevTables *tab = A.tab;
     for (int d = 0; d < 2; d++)
         if (st.mostSeeds[d]) {
-            const uint32_t v = st.nSeedsApplied[d] / st.mostSeeds[d];
+            const uint32_t v = uni(st.nSeedsApplied[d] / st.mostSeeds[d]);   // (VALU division: back to an SGPR)
             if (v > st.lps[d]) st.lps[d] = v;
         }
     const uint32_t minLps = st.lps[0] < st.lps[1] ? st.lps[0] : st.lps[1];
@@ -781,7 +785,7 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, El
         // during this one's passes measured 1% slower: the 9 VGPRs it holds across the pass loop,
         // profiles/r03/ab/micro_opts_ab.txt.)
         {
-            constexpr int ED = Elem128::DWORDS;
+            constexpr int ED = Elem64::DWORDS;
             const uint32_t tot = nb * ED;
             uint32_t v[FETCH_NLD];
 #pragma unroll
@@ -854,7 +858,7 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, El
             const uint32_t dw = f < 4 ? 2 + f : (f == 4 ? 8 : (f == 5 ? 9 : 11));
             if (f < 7) {
                 uint32_t w = G.ecache[sl][dw];
-                if (dw == 11) w = (w & ~0x00ff0000u) | (1u << 16);
+                if (dw == 11) w |= W11_ALLSCORED;   // (the spill index above it stays)
                 ((uint32_t *)(ar + G.eidx[sl]))[dw] = w;
             }
         }

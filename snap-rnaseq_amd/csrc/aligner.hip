@@ -37,7 +37,7 @@ __device__ __forceinline__ bool score_wave(const KArgs &A, Lds<MAXLEN> &S, Elem5
     const DevTables *tab = A.tab;
     for (int d = 0; d < 2; d++)
         if (st.mostSeeds[d]) {
-            uint32_t v = st.nSeedsApplied[d] / st.mostSeeds[d];
+            uint32_t v = uni(st.nSeedsApplied[d] / st.mostSeeds[d]);
             if (v > st.lps[d]) st.lps[d] = v;
         }
     do {
@@ -216,6 +216,7 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
                                             const uint32_t *list0, const uint32_t *list1, uint32_t single0,
                                             uint32_t single1, uint32_t numWeightLists, uint32_t minLoc,
                                             uint32_t maxLoc) {
+    constexpr bool C64 = std::is_same<ElemOf<MAXLEN>, Elem64>::value;
     const int lane = lane_id();
     const uint32_t lim = lim0 + lim1;
     for (uint32_t b0 = 0; b0 < lim; b0 += WAVE) {
@@ -259,15 +260,20 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
             if (e != NONE || allowAlloc) {
                 uint64_t used = 0;
                 uint32_t weight = 0, allScored = 0, sortkey = 0;
-                // header dword 11 = weight | lps << 8 | allScored << 16; a new element's header is
-                // written at the end in three 16-byte stores instead of field by field
+                // header dword 11 = weight | lps << 8 | allScored << 16 (| Elem64 spill << 17); a new
+                // element's header is written at the end in 16-byte stores instead of field by field
                 uint32_t w11 = 0, chainNext = NONE;
+                uint32_t sl4[4] = {0u, 0u, 0u, 0u};   // Elem64: the inline (bit + 1, offset) slots
                 bool isNew = false;
                 if (e != NONE) {
                     const uint32_t *eh = reinterpret_cast<const uint32_t *>(ar + e);
                     used = *reinterpret_cast<const uint64_t *>(eh);
                     w11 = eh[11];
-                    weight = w11 & 0xff; allScored = (w11 >> 16) & 0xff; sortkey = sk_get(A, S, ar, e);
+                    if constexpr (C64) {
+                        const uint4 q = *reinterpret_cast<const uint4 *>(eh + 12);
+                        sl4[0] = q.x; sl4[1] = q.y; sl4[2] = q.z; sl4[3] = q.w;
+                    }
+                    weight = w11 & 0xff; allScored = (w11 >> 16) & 1u; sortkey = sk_get(A, S, ar, e);
                 }
                 uint64_t m = grp;
                 while (m) {
@@ -275,48 +281,83 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
                     m &= m - 1;
                     uint32_t bit = S.u.ins.scrLoc[j] % ELEM;
                     uint32_t t = st.ts + b0 + j;
+                    const uint64_t cb = 1ull << bit;
+                    const bool had = (used & cb) != 0;
                     if (e == NONE) {
                         // allocateNewCandidate (BaseAligner.cpp:1485-1568): tail of weight list 1
-                        e = atomicAdd(&S.nElems, 1u);
-                        if (e >= (uint32_t)A.arenaElems) {
-                            if (!A.ovfList) diag_report(A.diag, DIAG_ARENA, st.rid, e);
+                        if (atomicAdd(&S.nUsed, 1u) >= (uint32_t)A.arenaElems) {
+                            if (!A.ovfList) diag_report(A.diag, DIAG_ARENA, st.rid, S.nElems);
                             overflow = true;
                             break;
                         }
+                        e = atomicAdd(&S.nElems, 1u);
                         isNew = true;
                         w11 = (lpsNow & 0xffu) << 8;
                         const uint32_t old = head_exchange(S, elem_hash(key), e);
                         if (e < MIRCAP) { S.ekey[e] = key; S.enext[e] = (uint16_t)(old == NONE ? 0xffffu : old); }
                         chainNext = old;
-                        used = 1ull << bit;
+                        used = cb;
                         weight = 1;
                         allScored = 0;
                         sortkey = (1u << 24) | (0xffffffu - t);
                     } else {
                         // findCandidate (BaseAligner.cpp:1474-1479) + incrementWeight (1689-1727)
-                        uint64_t cb = 1ull << bit;
-                        allScored = (allScored && (used & cb)) ? 1 : 0;
+                        allScored = (allScored && had) ? 1 : 0;
                         used |= cb;
                         if (!allScored && weight < numWeightLists - 1) {
                             weight++;
                             sortkey = (weight << 24) | (0xffffffu - t);
                         }
                     }
-                    ar[e].seedOffset[bit] = (std::remove_reference_t<decltype(ar[e].seedOffset[0])>)offset;
+                    // candidate->seedOffset = offset (BaseAligner.cpp:858)
+                    if constexpr (C64) {
+                        const uint32_t sp = spill_index(w11);
+                        if (sp) {
+                            reinterpret_cast<uint8_t *>(ar + sp)[bit] = (uint8_t)offset;
+                        } else {
+                            // slots hold the used candidates in first-use order: candidate `bit` has
+                            // one iff it was used before; a new one takes slot popcount(used before)
+                            const uint32_t k = had ? slot_of(sl4, bit) : (uint32_t)__popcll(used & ~cb);
+                            if (k < (uint32_t)NSLOT) {
+                                slot_set(sl4, k, bit, offset);
+                            } else {
+                                // a ninth candidate: a spill block from the arena's top takes them all
+                                if (atomicAdd(&S.nUsed, 1u) >= (uint32_t)A.arenaElems) {
+                                    if (!A.ovfList) diag_report(A.diag, DIAG_ARENA, st.rid, S.nElems);
+                                    overflow = true;
+                                    break;
+                                }
+                                const uint32_t spn = (uint32_t)A.arenaElems - 1u - atomicAdd(&S.nSpill, 1u);
+                                uint8_t *blk = reinterpret_cast<uint8_t *>(ar + spn);
+#pragma unroll
+                                for (int q = 0; q < NSLOT; q++) {
+                                    const uint32_t pr = (sl4[q >> 1] >> (16 * (q & 1))) & 0xffffu;
+                                    blk[(pr & 0xffu) - 1u] = (uint8_t)(pr >> 8);
+                                }
+                                blk[bit] = (uint8_t)offset;
+                                w11 |= spn << W11_SPILL_SHIFT;
+                            }
+                        }
+                    } else {
+                        ar[e].seedOffset[bit] = (std::remove_reference_t<decltype(ar[e].seedOffset[0])>)offset;
+                    }
                 }
                 if (overflow) e = NONE;
                 if (e != NONE) {
                     uint32_t *eh = reinterpret_cast<uint32_t *>(ar + e);
-                    w11 = (w11 & 0xff00ff00u) | (weight & 0xffu) | ((allScored & 0xffu) << 16);
+                    w11 = (w11 & 0xfffeff00u) | (weight & 0xffu) | ((allScored & 1u) << 16);
                     if (isNew) {
                         // {used, scored = 0}, {prob = 0, key, next}, {bestScore, bestLoc, sortkey, w11}
                         uint4 *h4 = reinterpret_cast<uint4 *>(eh);
                         h4[0] = make_uint4((uint32_t)used, (uint32_t)(used >> 32), 0u, 0u);
                         h4[1] = make_uint4(0u, 0u, key, chainNext);
                         h4[2] = make_uint4(UNUSED_SCORE, 0u, sortkey, w11);
+                        if constexpr (C64) h4[3] = make_uint4(sl4[0], sl4[1], sl4[2], sl4[3]);
                     } else {
                         *reinterpret_cast<uint64_t *>(eh) = used;
                         eh[11] = w11;
+                        if constexpr (C64)
+                            if (!spill_index(w11)) *reinterpret_cast<uint4 *>(eh + 12) = make_uint4(sl4[0], sl4[1], sl4[2], sl4[3]);
                     }
                     sk_set(A, S, ar, e, sortkey);
                     if (sortkey) atomicMax((unsigned long long *)&S.laneMax[e % WAVE], ((uint64_t)sortkey << 32) | e);
@@ -418,7 +459,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
         for (int i = lane; i < NBUCKET; i += WAVE) S.head[i] = Lds<MAXLEN>::HEAD_NONE;
         for (int i = lane; i < BT; i += WAVE) { S.u.ins.btKey[i] = NONE; S.u.ins.btMask[i] = 0; }
         S.laneMax[lane] = 0;
-        if (lane == 0) S.nElems = 0;
+        if (lane == 0) { S.nElems = 0; S.nSpill = 0; S.nUsed = 0; }
         wave_sync();
         if constexpr (Lds<MAXLEN>::BYTE_PATH) {
 #pragma unroll
@@ -627,7 +668,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
     }
     PH_T(A, tout);
     if (st.abort == 2u) {   // outgrew the capped arena: no record here, the big-arena pass aligns it afresh
-        if (lane == 0) A.ovfList[atomicAdd(A.ovfCount, 1u)] = r;
+        if (lane_id() == 0) A.ovfList[atomicAdd(A.ovfCount, 1u)] = r;
         wave_sync();
         PH_ADD(A, S, PH_OUT, tout);
         return;
@@ -635,7 +676,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
     const uint32_t svLookups = sv_get(st, SV_LOOKUPS), svScored = sv_get(st, SV_SCORED);
     const uint32_t svPopular = sv_get(st, SV_POPULAR), svProbes = sv_get(st, SV_PROBES);
     const uint32_t svHitWords = sv_get(st, SV_HITWORDS), svOvf = sv_get(st, SV_OVF);
-    if (lane == 0) {
+    if (lane_id() == 0) {   // (re-read: the setup's lane id is not kept live across the seed loop)
         snapgpu_result_t o;
         o.location = st.outLoc;
         o.score = st.outScore;
@@ -1676,6 +1717,8 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
     a->arenaCap = std::min<uint64_t>(a->arenaElems, budget / ((uint64_t)a->grid * sizeof(Elem512)));
     // the bit-plane kernels keep u16 element indices in their LDS chain heads (Lds::HeadT)
     a->arenaCap = std::min<uint64_t>(a->arenaCap, 0xfffeu);
+    // and at most ELEM64_MAX slots (an Elem64's spill index is 15 bits of w11)
+    a->arenaCap = std::min<uint64_t>(a->arenaCap, ELEM64_MAX);
     if (const char *t = getenv("SNAPGPU_ARENA_CAP"); t && atoll(t) >= 1)   // test hook: force the overflow path
         a->arenaCap = std::min<uint64_t>(a->arenaCap, (uint64_t)atoll(t));
     if (a->arenaCap < a->arenaElems)
@@ -1823,7 +1866,8 @@ static int launch_passes(snapgpu_aligner_t *a, int li, const PassIO &io, const A
     A.seedRecs = nullptr;
     A.longCount = L.counter + 5;
     HIPCHK(hipEventRecord(ev.e[3], L.stream));
-    hipLaunchKernelGGL(seed_lookup_kernel, dim3((unsigned)((io.n + 3) / 4)), dim3(64), 0, L.stream, A, io.seeds,
+    hipLaunchKernelGGL(seed_lookup_kernel, dim3((unsigned)((io.n + 4 * LOOKUP_WAVES - 1) / (4 * LOOKUP_WAVES))),
+                       dim3(64 * LOOKUP_WAVES), 0, L.stream, A, io.seeds,
                        L.lookupStats);
     HIPCHK(hipGetLastError());
     A.seedRecs = reinterpret_cast<const uint4 *>(io.seeds);

@@ -50,6 +50,7 @@ __device__ __forceinline__ uint32_t bucket_count(const KArgs &A, uint32_t cnt, u
 
 // One lane, one lookup: the whole 64-B line in four 16-B loads per bucket visited.
 // -> found; v1/v2 as the slot holds them; aux of the entry (counts); lines = buckets loaded.
+// (Named entries, not an array: an indexed uint4[4] went to scratch.)
 __device__ __forceinline__ bool bucket_lookup_lane(const KArgs &A, uint32_t table, uint32_t key, uint32_t &v1,
                                                    uint32_t &v2, uint32_t &aux, uint32_t &lines) {
     const uint32_t nB = A.bucketCount[table];
@@ -57,13 +58,15 @@ __device__ __forceinline__ bool bucket_lookup_lane(const KArgs &A, uint32_t tabl
     uint32_t b = bucket_home(key, nB);
     for (lines = 1;; lines++) {
         const uint4 *p = T + 4ull * b;
-        uint4 e[4];
-#pragma unroll
-        for (int i = 0; i < 4; i++) e[i] = p[i];
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-            if ((e[i].w & BK_OCC) && e[i].x == key) { v1 = e[i].y; v2 = e[i].z; aux = e[i].w; return true; }
-        if (!(e[0].w & BK_OVF) || lines >= nB) return false;
+        const uint4 e0 = p[0], e1 = p[1], e2 = p[2], e3 = p[3];
+        const bool h0 = (e0.w & BK_OCC) && e0.x == key, h1 = (e1.w & BK_OCC) && e1.x == key;
+        const bool h2 = (e2.w & BK_OCC) && e2.x == key, h3 = (e3.w & BK_OCC) && e3.x == key;
+        if (h0 | h1 | h2 | h3) {
+            const uint4 e = h0 ? e0 : (h1 ? e1 : (h2 ? e2 : e3));
+            v1 = e.y; v2 = e.z; aux = e.w;
+            return true;
+        }
+        if (!(e0.w & BK_OVF) || lines >= nB) return false;
         b = bucket_next(b, nB);
     }
 }

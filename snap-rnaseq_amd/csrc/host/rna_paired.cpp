@@ -272,9 +272,15 @@ struct FilterState {
     uint32_t tstart0 = 0, start0 = 0, len0 = 0, tstart1 = 0, start1 = 0, len1 = 0;
 };
 
-void filterPair(const Ctx &C, AlignmentMap &mate0, AlignmentMap &mate1, uint32_t len0, uint32_t len1, FilterState &S,
-                Err &err) {
+// the pair lists of one filterPair call, kept by the calling thread (cleared per pair, no allocations)
+struct PairLists {
     std::vector<AlignmentPair> noRc, intragene, intra, inter;
+};
+
+void filterPair(const Ctx &C, AlignmentMap &mate0, AlignmentMap &mate1, uint32_t len0, uint32_t len1, FilterState &S,
+                PairLists &L, Err &err) {
+    L.noRc.clear(); L.intragene.clear(); L.intra.clear(); L.inter.clear();
+    std::vector<AlignmentPair> &noRc = L.noRc, &intragene = L.intragene, &intra = L.intra, &inter = L.inter;
     uint32_t genomeMapq = 70;   // genome_mapq(maxMAPQ)
     // mate0 / mate1 empty: UnalignedRead (:742-933) only feeds the interval report (not built)
     for (auto &m0 : mate0)
@@ -484,6 +490,7 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
     std::vector<Err> errs(16);
     parallel(nu, [&](unsigned t, uint64_t b, uint64_t e) {
         AlignmentMap mate0, mate1;
+        PairLists lists;
         for (uint64_t j = b; j < e && errs[t].msg.empty(); j++) {
             mate0.clear(); mate1.clear();
             const uint32_t len0 = X.ul[0][j], len1 = X.ul[1][j];
@@ -498,7 +505,7 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
             FilterState &S = X.fs[j];
             S.r.fromAlignTogether = g.fromAlignTogether;
             S.r.alignedAsPair = g.alignedAsPair;
-            filterPair(C, mate0, mate1, len0, len1, S, errs[t]);
+            filterPair(C, mate0, mate1, len0, len1, S, lists, errs[t]);
         }
     });
     for (auto &e : errs) if (!e.msg.empty()) { X.fail(SNAPGPU_EFORMAT, "rna_paired_align: " + e.msg); return; }
@@ -703,7 +710,7 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
                     if (after) tk.push_back({after, 'S'});
                 }
                 const int p = pieceAt(tg, r.tlocation[k]);
-                const GtfTranscript *t = p >= 0 ? gtfTranscript(Rr.gtf, tg.pieceNames[p]) : nullptr;
+                const GtfTranscript *t = p >= 0 ? C.tByPiece[p] : nullptr;
                 if (t) gtfSpliceCigar(t, r.tlocation[k] - tg.pieceOffsets[p] + 1, tk, splice[k][q]);
             }
         });

@@ -28,6 +28,7 @@ struct SeedRec {
     uint32_t cnt;       // overflow counts, u16 each, saturated: [15:0] value1 side, [31:16] value2 side
 };
 constexpr int SEEDS_PER_READ = 16;   // = lanes per read in seed_lookup_kernel: 4 reads per wave
+constexpr int LOOKUP_WAVES = 4;      // waves per seed_lookup_kernel block (16 reads)
 
 // bits [p, p+len) of a 128-bit value (len <= 32)
 __device__ __forceinline__ uint32_t win128(uint64_t lo, uint64_t hi, int p, int len) {
@@ -50,9 +51,13 @@ __device__ __forceinline__ uint64_t spread2(uint32_t x32) {
 
 // stats[4*slot + 0..2] += seeds looked up, hash entries probed, overflow counts read (roofline
 // bytes); slot = block % 256
-__global__ __launch_bounds__(64) void seed_lookup_kernel(KArgs A, SeedRec *out, unsigned long long *stats) {
+__global__ __launch_bounds__(64 * LOOKUP_WAVES) void seed_lookup_kernel(KArgs A, SeedRec *out, unsigned long long *stats) {
+    // the wrap table (GetWrappedNextSeedToTest order) in LDS: the walk below reads it per lane
+    __shared__ uint32_t wrapT[32];
+    if (threadIdx.x < 32) wrapT[threadIdx.x] = A.tab->wrap[threadIdx.x];
+    __syncthreads();
     const int lane = lane_id();
-    const uint32_t r = blockIdx.x * 4 + (lane >> 4);
+    const uint32_t r = (blockIdx.x * LOOKUP_WAVES + threadIdx.x / 64) * 4 + (lane >> 4);
     const int k = lane & 15;
     const int sub = k & 7;          // lanes k < 8 load the read, 16 bases each
     const bool have = r < A.nReads;
@@ -107,7 +112,7 @@ __global__ __launch_bounds__(64) void seed_lookup_kernel(KArgs A, SeedRec *out, 
         for (int guard = 0; guard < 4 * 128; guard++) {   // each step marks, wraps or ends
             if (p >= nPossible) {
                 if (++wrap >= L) break;                      // wrapCount == seedLen: the read is scored
-                p = (int)A.tab->wrap[wrap];
+                p = (int)wrapT[wrap];
             }
             while (p < nPossible && (((p < 64 ? u0 >> p : u1 >> (p - 64)) & 1ull) != 0)) p++;
             if (p >= nPossible) continue;
@@ -174,7 +179,7 @@ __global__ __launch_bounds__(64) void seed_lookup_kernel(KArgs A, SeedRec *out, 
             v += ((uint64_t)hi << 32) | lo;
         }
         if (lane == 0) {   // 256 slot groups: no single-address atomic hot spot
-            unsigned long long *st = stats + 4 * (blockIdx.x & 255);
+            unsigned long long *st = stats + 4 * ((blockIdx.x * LOOKUP_WAVES + threadIdx.x / 64) & 255);
             atomicAdd(st + 0, (unsigned long long)((v >> 32) & 0xfff));
             atomicAdd(st + 1, (unsigned long long)(v & 0xffffffffull));
             atomicAdd(st + 2, (unsigned long long)(v >> 44));

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Register / LDS / scratch report of the kernels (compiler remarks, gfx950, the Makefile's flags).
-cd /root/repo/snap-rnaseq_amd && /opt/rocm/bin/hipcc -DSNAPGPU_PHASE_TIMERS=${PHASE_TIMERS:-0} -O3 -std=c++17 -fPIC \
+cd "$(dirname "$0")/../snap-rnaseq_amd" && /opt/rocm/bin/hipcc -DSNAPGPU_PHASE_TIMERS=${PHASE_TIMERS:-0} -O3 -std=c++17 -fPIC \
   --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -munsafe-fp-atomics -I../include -Icsrc/host -Icsrc \
   -Wno-unused-result -Wno-unused-value -mllvm -disable-machine-licm --cuda-device-only \
   -c csrc/aligner.hip -o /tmp/kres.o -Rpass-analysis=kernel-resource-usage 2>&1 |
