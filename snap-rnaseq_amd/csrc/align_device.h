@@ -47,6 +47,7 @@ constexpr uint32_t MIRCAP = 256;          // elements whose key / chain link are
 constexpr int ELEM_DWORDS = 36;           // dwords of Elem512 (byte path)
 constexpr int BT = 128;                   // insertion-batch dedupe table (LDS)
 constexpr uint32_t NONE = 0xffffffffu;
+constexpr uint32_t ELCAP = 32;            // Elem64 kernels: elements 0..ELCAP-1 of a read are kept in LDS
 
 struct DevTables {
     double indel[64];
@@ -377,6 +378,8 @@ struct Lds {
     int16_t btMatched[BYTE_PATH ? MAX_K + 1 : 1];
     uint16_t rows[BYTE_PATH ? MAX_K : 1][WAVE];     // byte-path LV rows: (L+2) | action<<12
     GroupLdsT<NW> grp[BYTE_PATH ? 0 : 1];           // scorer of align_kernel<128> / <256>
+    // the read's first ELCAP candidate elements (Elem64) live here, not in the HBM arena
+    alignas(16) uint32_t eloc[BYTE_PATH ? 1 : ELCAP][16];
 };
 // LV row e (1 <= e < MAX_K) of the bit-plane scorer at rows8[e - 1]
 template <int MAXLEN>
