@@ -833,9 +833,14 @@ __device__ __forceinline__ uint32_t chain_find(const KArgs &A, const Lds<MAXLEN>
 // selection keys: LDS for the first SKCAP elements of a read, HBM (the element) beyond.  (A compact
 // owner-transposed HBM key array -- one coalesced load per selection recompute -- measured 3% slower
 // on C2 and 5% on C3 in round 3: profiles/r03/ab/compact_sk_ab.txt.)
+// (The asm after the HBM load keeps the two loads apart: merged into one load of a selected
+// pointer they became a flat load, which waits on both the LDS and the vector-memory counters.)
 template <int MAXLEN>
 __device__ __forceinline__ uint32_t sk_get(const KArgs &, const Lds<MAXLEN> &S, const ElemOf<MAXLEN> *ar, uint32_t e) {
-    return e < SKCAP ? S.sk[e] : ar[e].sortkey;
+    uint32_t v;
+    if (e < SKCAP) v = S.sk[e];
+    else { v = ar[e].sortkey; __asm__ volatile("" :: "v"(v)); }
+    return v;
 }
 template <int MAXLEN>
 __device__ __forceinline__ void sk_set(const KArgs &, Lds<MAXLEN> &S, ElemOf<MAXLEN> *ar, uint32_t e, uint32_t v) {

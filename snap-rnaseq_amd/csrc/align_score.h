@@ -218,11 +218,11 @@ __device__ __forceinline__ int lv_group(GroupLdsT<NW> &G, uint8_t (*rows8)[WAVE]
                         vp = curD == -1 ? L0 : -2;
                     } else {
                         const int i0 = gi * GS + (DIR > 0 ? c + curD - 1 : c - curD - 1);   // lowest byte
-                        const uint8_t *rp = &rows8[r][0] + i0;
-                        const uint32_t *p4 = reinterpret_cast<const uint32_t *>(
-                            reinterpret_cast<uintptr_t>(rp) & ~(uintptr_t)3);   // ds_read2_b32
-                        const uint64_t w = ((uint64_t)p4[1] << 32) | p4[0];
-                        const uint32_t sh = 8u * (uint32_t)(reinterpret_cast<uintptr_t>(rp) & 3);
+                        // the two dwords holding bytes i0..i0+2 of row r, indexed off the row base (an
+                        // address rounded through an integer loses its LDS address space: a flat load)
+                        const uint32_t *row4 = reinterpret_cast<const uint32_t *>(&rows8[r][0]);
+                        const uint64_t w = ((uint64_t)row4[(i0 >> 2) + 1] << 32) | row4[i0 >> 2];   // ds_read2_b32
+                        const uint32_t sh = 8u * (uint32_t)(i0 & 3);
                         const int b0 = (int)((w >> sh) & 0xff) - 2, b1 = (int)((w >> (sh + 8)) & 0xff) - 2;
                         const int b2 = (int)((w >> (sh + 16)) & 0xff) - 2;
                         vm = DIR > 0 ? b0 : b2;
