@@ -57,6 +57,9 @@ struct DevTables {
     uint32_t wrap[32];        // GetWrappedNextSeedToTest order (SeedSequencer.h)
     double mapqT[72];         // mapqT[q] = 10^(-q/10) (glibc pow): MAPQ thresholds, no device log10
     uint32_t maxSeedsForLen[513];   // (int)(seedCoverage * n / seedLen) per read length n (BaseAligner.cpp:563-568)
+    // The first 16 seed offsets of the seed sequence (BaseAligner.cpp:686-746) of a read of length n
+    // whose bases are all ACGT: the sequence then depends on n and seedLen only (0xff: not reached)
+    uint8_t seedSeq[129][16];
 };
 // The seedLen-independent tables (indel, phred, perfect, mapqT), one copy per device, set
 // once by the host: a global's address is a constant the compiler rematerializes, where a

@@ -922,6 +922,26 @@ void fillTables(DevTables &t, uint32_t seedLen) {
     for (int q = 0; q < 72; q++) t.mapqT[q] = q < 70 ? pow(10.0, -q / 10.0) : 0.0;
     if (seedLen >= 16 && seedLen <= 25)
         for (int i = 0; i < 25; i++) t.wrap[i] = kWrap[seedLen - 16][i];
+    // seed_lookup_kernel's walk (seed_lookup.h) on an all-ACGT read of each length: rounds 0,
+    // seedLen, ... then the wrap table's starts, skipping used offsets (BaseAligner.cpp:686-746)
+    memset(t.seedSeq, 0xff, sizeof(t.seedSeq));
+    const int L = (int)seedLen;
+    for (int n = L; n <= 128; n++) {
+        const int nPossible = n - L + 1;
+        bool used[128] = {};
+        int p = 0, wrap = 0, idx = 0;
+        for (int guard = 0; guard < 4 * 128 && idx < 16; guard++) {
+            if (p >= nPossible) {
+                if (++wrap >= L) break;
+                p = (int)t.wrap[wrap];
+            }
+            while (p < nPossible && used[p]) p++;
+            if (p >= nPossible) continue;
+            used[p] = true;
+            t.seedSeq[n][idx++] = (uint8_t)p;
+            p += L;
+        }
+    }
 }
 
 // g_tab (align_device.h) on the current device, once per device per process
