@@ -47,6 +47,7 @@ constexpr uint32_t MIRCAP = 256;          // elements whose key / chain link are
 constexpr int ELEM_DWORDS = 36;           // dwords of Elem512 (byte path)
 constexpr int BT = 128;                   // insertion-batch dedupe table (LDS)
 constexpr uint32_t NONE = 0xffffffffu;
+constexpr uint32_t ELCAP = 32;            // Elem64 kernels: elements 0..ELCAP-1 of a read are kept in LDS
 
 struct DevTables {
     double indel[64];
@@ -56,6 +57,9 @@ struct DevTables {
     uint32_t wrap[32];        // GetWrappedNextSeedToTest order (SeedSequencer.h)
     double mapqT[72];         // mapqT[q] = 10^(-q/10) (glibc pow): MAPQ thresholds, no device log10
     uint32_t maxSeedsForLen[513];   // (int)(seedCoverage * n / seedLen) per read length n (BaseAligner.cpp:563-568)
+    // The first 16 seed offsets of the seed sequence (BaseAligner.cpp:686-746) of a read of length n
+    // whose bases are all ACGT: the sequence then depends on n and seedLen only (0xff: not reached)
+    uint8_t seedSeq[129][16];
 };
 // The seedLen-independent tables (indel, phred, perfect, mapqT), one copy per device, set
 // once by the host: a global's address is a constant the compiler rematerializes, where a
@@ -377,6 +381,8 @@ struct Lds {
     int16_t btMatched[BYTE_PATH ? MAX_K + 1 : 1];
     uint16_t rows[BYTE_PATH ? MAX_K : 1][WAVE];     // byte-path LV rows: (L+2) | action<<12
     GroupLdsT<NW> grp[BYTE_PATH ? 0 : 1];           // scorer of align_kernel<128> / <256>
+    // the read's first ELCAP candidate elements (Elem64) live here, not in the HBM arena
+    alignas(16) uint32_t eloc[BYTE_PATH ? 1 : ELCAP][16];
 };
 // LV row e (1 <= e < MAX_K) of the bit-plane scorer at rows8[e - 1]
 template <int MAXLEN>
@@ -830,9 +836,14 @@ __device__ __forceinline__ uint32_t chain_find(const KArgs &A, const Lds<MAXLEN>
 // selection keys: LDS for the first SKCAP elements of a read, HBM (the element) beyond.  (A compact
 // owner-transposed HBM key array -- one coalesced load per selection recompute -- measured 3% slower
 // on C2 and 5% on C3 in round 3: profiles/r03/ab/compact_sk_ab.txt.)
+// (The asm after the HBM load keeps the two loads apart: merged into one load of a selected
+// pointer they became a flat load, which waits on both the LDS and the vector-memory counters.)
 template <int MAXLEN>
 __device__ __forceinline__ uint32_t sk_get(const KArgs &, const Lds<MAXLEN> &S, const ElemOf<MAXLEN> *ar, uint32_t e) {
-    return e < SKCAP ? S.sk[e] : ar[e].sortkey;
+    uint32_t v;
+    if (e < SKCAP) v = S.sk[e];
+    else { v = ar[e].sortkey; __asm__ volatile("" :: "v"(v)); }
+    return v;
 }
 template <int MAXLEN>
 __device__ __forceinline__ void sk_set(const KArgs &, Lds<MAXLEN> &S, ElemOf<MAXLEN> *ar, uint32_t e, uint32_t v) {

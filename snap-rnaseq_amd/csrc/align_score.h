@@ -218,11 +218,11 @@ __device__ __forceinline__ int lv_group(GroupLdsT<NW> &G, uint8_t (*rows8)[WAVE]
                         vp = curD == -1 ? L0 : -2;
                     } else {
                         const int i0 = gi * GS + (DIR > 0 ? c + curD - 1 : c - curD - 1);   // lowest byte
-                        const uint8_t *rp = &rows8[r][0] + i0;
-                        const uint32_t *p4 = reinterpret_cast<const uint32_t *>(
-                            reinterpret_cast<uintptr_t>(rp) & ~(uintptr_t)3);   // ds_read2_b32
-                        const uint64_t w = ((uint64_t)p4[1] << 32) | p4[0];
-                        const uint32_t sh = 8u * (uint32_t)(reinterpret_cast<uintptr_t>(rp) & 3);
+                        // the two dwords holding bytes i0..i0+2 of row r, indexed off the row base (an
+                        // address rounded through an integer loses its LDS address space: a flat load)
+                        const uint32_t *row4 = reinterpret_cast<const uint32_t *>(&rows8[r][0]);
+                        const uint64_t w = ((uint64_t)row4[(i0 >> 2) + 1] << 32) | row4[i0 >> 2];   // ds_read2_b32
+                        const uint32_t sh = 8u * (uint32_t)(i0 & 3);
                         const int b0 = (int)((w >> sh) & 0xff) - 2, b1 = (int)((w >> (sh + 8)) & 0xff) - 2;
                         const int b2 = (int)((w >> (sh + 16)) & 0xff) - 2;
                         vm = DIR > 0 ? b0 : b2;
@@ -514,6 +514,7 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem6
                 const uint64_t inb = ballot((uint32_t)lane < nb && G.eidx[lane < EB ? lane : 0] == nbPre);
                 csPre = inb ? (int)__builtin_ctzll(inb) : -1;
                 if (csPre >= 0) nvPre = lane < 12 ? G.ecache[csPre][lane] : 0u;
+                else if (nbPre < ELCAP) nvPre = lane < 12 ? S.eloc[nbPre][lane] : 0u;
                 else nvPre = lane < 12 ? ((const uint32_t *)(ar + nbPre))[lane] : 0u;
             }
         }
@@ -549,6 +550,7 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem6
                 else {
                     st.pAll = st.pAll - np > 0.0 ? st.pAll - np : 0.0;
                     if (cs >= 0) { if (lane == 4 || lane == 5) G.ecache[cs][lane] = 0u; }
+                    else if (nb2 < ELCAP) { if (lane == 4 || lane == 5) S.eloc[nb2][lane] = 0u; }
                     else if (lane == 4 || lane == 5) ((uint32_t *)(ar + nb2))[lane] = 0u;
                 }
             }
@@ -791,7 +793,8 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, El
 #pragma unroll
             for (int j = 0; j < FETCH_NLD; j++) {
                 const uint32_t idx = (uint32_t)(j * WAVE + lane);
-                v[j] = idx < tot ? ((const uint32_t *)(ar + G.eidx[idx / ED]))[idx % ED] : 0u;
+                const uint32_t e = idx < tot ? G.eidx[idx / ED] : 0u;
+                v[j] = idx >= tot ? 0u : (e < ELCAP ? S.eloc[e][idx % ED] : ((const uint32_t *)(ar + e))[idx % ED]);
             }
 #pragma unroll
             for (int j = 0; j < FETCH_NLD; j++) {
@@ -859,7 +862,9 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, El
             if (f < 7) {
                 uint32_t w = G.ecache[sl][dw];
                 if (dw == 11) w |= W11_ALLSCORED;   // (the spill index above it stays)
-                ((uint32_t *)(ar + G.eidx[sl]))[dw] = w;
+                const uint32_t e = G.eidx[sl];
+                if (e < ELCAP) S.eloc[e][dw] = w;
+                else ((uint32_t *)(ar + e))[dw] = w;
             }
         }
         wave_sync();

@@ -266,13 +266,16 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
                 uint32_t sl4[4] = {0u, 0u, 0u, 0u};   // Elem64: the inline (bit + 1, offset) slots
                 bool isNew = false;
                 if (e != NONE) {
-                    const uint32_t *eh = reinterpret_cast<const uint32_t *>(ar + e);
-                    used = *reinterpret_cast<const uint64_t *>(eh);
-                    w11 = eh[11];
-                    if constexpr (C64) {
-                        const uint4 q = *reinterpret_cast<const uint4 *>(eh + 12);
-                        sl4[0] = q.x; sl4[1] = q.y; sl4[2] = q.z; sl4[3] = q.w;
-                    }
+                    auto rd = [&](const uint32_t *eh) __attribute__((always_inline)) {
+                        used = *reinterpret_cast<const uint64_t *>(eh);
+                        w11 = eh[11];
+                        if constexpr (C64) {
+                            const uint4 q = *reinterpret_cast<const uint4 *>(eh + 12);
+                            sl4[0] = q.x; sl4[1] = q.y; sl4[2] = q.z; sl4[3] = q.w;
+                        }
+                    };
+                    if (C64 && e < ELCAP) rd(S.eloc[e]);   // (two call sites: LDS and global loads, not flat)
+                    else rd(reinterpret_cast<const uint32_t *>(ar + e));
                     weight = w11 & 0xff; allScored = (w11 >> 16) & 1u; sortkey = sk_get(A, S, ar, e);
                 }
                 uint64_t m = grp;
@@ -344,21 +347,24 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
                 }
                 if (overflow) e = NONE;
                 if (e != NONE) {
-                    uint32_t *eh = reinterpret_cast<uint32_t *>(ar + e);
                     w11 = (w11 & 0xfffeff00u) | (weight & 0xffu) | ((allScored & 1u) << 16);
-                    if (isNew) {
-                        // {used, scored = 0}, {prob = 0, key, next}, {bestScore, bestLoc, sortkey, w11}
-                        uint4 *h4 = reinterpret_cast<uint4 *>(eh);
-                        h4[0] = make_uint4((uint32_t)used, (uint32_t)(used >> 32), 0u, 0u);
-                        h4[1] = make_uint4(0u, 0u, key, chainNext);
-                        h4[2] = make_uint4(UNUSED_SCORE, 0u, sortkey, w11);
-                        if constexpr (C64) h4[3] = make_uint4(sl4[0], sl4[1], sl4[2], sl4[3]);
-                    } else {
-                        *reinterpret_cast<uint64_t *>(eh) = used;
-                        eh[11] = w11;
-                        if constexpr (C64)
-                            if (!spill_index(w11)) *reinterpret_cast<uint4 *>(eh + 12) = make_uint4(sl4[0], sl4[1], sl4[2], sl4[3]);
-                    }
+                    auto wr = [&](uint32_t *eh) __attribute__((always_inline)) {
+                        if (isNew) {
+                            // {used, scored = 0}, {prob = 0, key, next}, {bestScore, bestLoc, sortkey, w11}
+                            uint4 *h4 = reinterpret_cast<uint4 *>(eh);
+                            h4[0] = make_uint4((uint32_t)used, (uint32_t)(used >> 32), 0u, 0u);
+                            h4[1] = make_uint4(0u, 0u, key, chainNext);
+                            h4[2] = make_uint4(UNUSED_SCORE, 0u, sortkey, w11);
+                            if constexpr (C64) h4[3] = make_uint4(sl4[0], sl4[1], sl4[2], sl4[3]);
+                        } else {
+                            *reinterpret_cast<uint64_t *>(eh) = used;
+                            eh[11] = w11;
+                            if constexpr (C64)
+                                if (!spill_index(w11)) *reinterpret_cast<uint4 *>(eh + 12) = make_uint4(sl4[0], sl4[1], sl4[2], sl4[3]);
+                        }
+                    };
+                    if (C64 && e < ELCAP) wr(S.eloc[e]);
+                    else wr(reinterpret_cast<uint32_t *>(ar + e));
                     sk_set(A, S, ar, e, sortkey);
                     if (sortkey) atomicMax((unsigned long long *)&S.laneMax[e % WAVE], ((uint64_t)sortkey << 32) | e);
                 }
@@ -916,6 +922,26 @@ void fillTables(DevTables &t, uint32_t seedLen) {
     for (int q = 0; q < 72; q++) t.mapqT[q] = q < 70 ? pow(10.0, -q / 10.0) : 0.0;
     if (seedLen >= 16 && seedLen <= 25)
         for (int i = 0; i < 25; i++) t.wrap[i] = kWrap[seedLen - 16][i];
+    // seed_lookup_kernel's walk (seed_lookup.h) on an all-ACGT read of each length: rounds 0,
+    // seedLen, ... then the wrap table's starts, skipping used offsets (BaseAligner.cpp:686-746)
+    memset(t.seedSeq, 0xff, sizeof(t.seedSeq));
+    const int L = (int)seedLen;
+    for (int n = L; n <= 128; n++) {
+        const int nPossible = n - L + 1;
+        bool used[128] = {};
+        int p = 0, wrap = 0, idx = 0;
+        for (int guard = 0; guard < 4 * 128 && idx < 16; guard++) {
+            if (p >= nPossible) {
+                if (++wrap >= L) break;
+                p = (int)t.wrap[wrap];
+            }
+            while (p < nPossible && used[p]) p++;
+            if (p >= nPossible) continue;
+            used[p] = true;
+            t.seedSeq[n][idx++] = (uint8_t)p;
+            p += L;
+        }
+    }
 }
 
 // g_tab (align_device.h) on the current device, once per device per process

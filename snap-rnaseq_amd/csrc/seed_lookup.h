@@ -66,6 +66,7 @@ __global__ __launch_bounds__(64 * LOOKUP_WAVES) void seed_lookup_kernel(KArgs A,
     const int L = (int)A.seedLen;
     // 16 bases per lane (read buffer carries >= 64 bytes of slack past the last read)
     uint64_t chunk = 0;   // [15:0] bit0 of the seed code, [31:16] bit1, [47:32] not-ACGT / past the end
+    bool bad = false;     // a base of the read (position < n) that is not ACGT
     {
         const uint64_t b0 = off + 16 * (uint64_t)sub;
         const uint32_t *src = (const uint32_t *)(A.bases + (b0 & ~3ull));
@@ -83,6 +84,7 @@ __global__ __launch_bounds__(64 * LOOKUP_WAVES) void seed_lookup_kernel(KArgs A,
                 const int pos = 16 * sub + 4 * i + b;
                 const int v = base_value(c);            // Seed encoding A0 G1 C2 T3 (Tables.cpp:41-48)
                 const bool inv = pos >= (int)n || v > 3;
+                bad |= pos < (int)n && v > 3;
                 const int bit = 4 * i + b;
                 if (!inv) chunk |= ((uint64_t)(v & 1) << bit) | ((uint64_t)(v >> 1) << (16 + bit));
                 else chunk |= 1ull << (32 + bit);
@@ -103,13 +105,19 @@ __global__ __launch_bounds__(64 * LOOKUP_WAVES) void seed_lookup_kernel(KArgs A,
     }
     SeedRec rec = {0u, 0u, 0u, 0u};
     uint32_t nSeed = 0, nProbe = 0, nOvfRead = 0;
+    // a read whose bases are all ACGT walks the sequence its length alone fixes: a table entry
+    const bool clean = ((ballot(bad) >> (lane & ~15)) & 0xffffull) == 0;
     if (have && n <= 128 && (int)n >= L) {
         // offset of the k-th seed of the sequence (BaseAligner.cpp:686-746), simulated with the
         // read's seedUsed bits: rounds 0, seedLen, ... then the wrap table's starts
         const int nPossible = (int)n - L + 1;
         uint64_t u0 = 0, u1 = 0;   // seedUsed, positions 0..127
         int p = 0, wrap = 0, idx = 0, my = -1;
-        for (int guard = 0; guard < 4 * 128; guard++) {   // each step marks, wraps or ends
+        if (clean) {
+            const uint32_t t = A.tab->seedSeq[n][k];
+            my = t == 0xffu ? -1 : (int)t;
+        }
+        for (int guard = 0; !clean && guard < 4 * 128; guard++) {   // each step marks, wraps or ends
             if (p >= nPossible) {
                 if (++wrap >= L) break;                      // wrapCount == seedLen: the read is scored
                 p = (int)wrapT[wrap];
