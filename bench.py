@@ -119,18 +119,18 @@ def load_pmc(sha, src_sha):
 
 
 def valu_cycles():
-    """SIMD cycles one wave64 VALU instruction of align_kernel<128>'s mix occupies at 4 waves/SIMD:
-    the median of the measured op kinds (profiles/r03/valu_rates.json, tools/gpu/valu_rates.hip) or
-    the guide's 2 cycles.  The median, not the mean: the back-to-back v_cndmask_b32 (vcc) chain
-    costs 12.7 cycles (a vcc read-after-write stall on every instruction), which the kernel never
-    issues -- its vcc selects follow a v_cmp, measured at 2.66 -- and alone lifts the mean to 3.62."""
+    """SIMD cycles one wave64 VALU instruction of align_kernel<128>'s mix occupies at 4 waves/SIMD, from the
+    measured op kinds (profiles/r03/valu_rates.json, tools/gpu/valu_rates.hip): (median, mean, source), or the
+    guide's 2 cycles for both.  Both are reported: the back-to-back v_cndmask_b32 (vcc) chain costs 12.7
+    cycles (a vcc read-after-write stall on every instruction), which the kernel never issues -- its vcc
+    selects follow a v_cmp, measured at 2.66 -- and alone lifts the mean (3.62) above the median (3.13)."""
     p = os.path.join(ROOT, "profiles", "r03", "valu_rates.json")
     if os.path.exists(p):
         d = json.load(open(p))
         xs = [r["w4"]["cycles_per_instr_per_simd"] for r in d["rates"] if not r["instruction"].startswith("v_readlane")]
         if xs:
-            return float(np.median(xs)), f"profiles/r03/valu_rates.json (median of {len(xs)} op kinds at 4 waves/SIMD)"
-    return 2.0, "MI355X_MICROARCH.md: wave64 on a 32-lane SIMD"
+            return float(np.median(xs)), float(np.mean(xs)), f"profiles/r03/valu_rates.json ({len(xs)} op kinds at 4 waves/SIMD)"
+    return 2.0, 2.0, "MI355X_MICROARCH.md: wave64 on a 32-lane SIMD"
 
 
 def cpu_info():
@@ -612,11 +612,26 @@ def main():
                 # or more waves issue (MI355X_MICROARCH.md "Wave scheduling"); the measured issue cost of
                 # the kernel's dominant op kinds at its 4 waves/SIMD (tools/gpu/valu_rates.hip) when
                 # committed, 4 SIMDs per CU at 2.4 GHz
-                cyc, cyc_src = valu_cycles()
+                cyc, cyc_mean, cyc_src = valu_cycles()
+                simd_cycles = 4 * n_cu * (kms_launch / 1000.0) * 2.4e9
                 valu_issue = {"valu_insts_per_launch": v, "simds": 4 * n_cu, "clock_ghz": 2.4,
-                              "cycles_per_valu": cyc, "cycles_source": cyc_src,
-                              "pipe_occupancy": v * cyc / (4 * n_cu * (kms_launch / 1000.0) * 2.4e9),
+                              "cycles_per_valu_median": cyc, "cycles_per_valu_mean": cyc_mean, "cycles_source": cyc_src,
+                              "pipe_occupancy": v * cyc / simd_cycles,
+                              "pipe_occupancy_mean_priced": v * cyc_mean / simd_cycles,
+                              "pipe_occupancy_guide_2cyc": v * 2.0 / simd_cycles,
+                              "wave_state": pmc.get("wave_state"),
                               "source": pmc_src}
+        ws = (valu_issue or {}).get("wave_state") or {}
+        if ws:   # the measured split of the waves' time (rocprofv3 SQ counters of this build)
+            binding = (f"latency of one serial wave per read: its waves spend {ws['SQ_WAIT_ANY']:.0%} of their time "
+                       f"waiting on memory counters and {ws['SQ_WAIT_INST_ANY']:.0%} waiting for dependencies, "
+                       f"{ws['SQ_ACTIVE_INST_ANY']:.0%} issuing ({ws['SQ_ACTIVE_INST_VALU']:.0%} VALU); VALU pipe "
+                       f"{valu_issue['pipe_occupancy']:.2f} (median-priced) / {valu_issue['pipe_occupancy_mean_priced']:.2f} "
+                       f"(mean-priced) / {valu_issue['pipe_occupancy_guide_2cyc']:.2f} (2 cycles) busy -- not HBM "
+                       "bandwidth (DESIGN.md section 4)")
+        else:
+            binding = ("instruction issue of one serial wave per read plus dependent memory round trips, not HBM "
+                       "bandwidth (DESIGN.md section 4; no PMC data of this build)")
         roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                     "kernel": "align_kernel<128, false>", "kernel_ms_per_launch": kms_launch,
@@ -633,10 +648,7 @@ def main():
                                          "note": "64-B lines per random access (SURVEY 8(d) d3)"},
                     "launches_per_step": n_launch, "reads_per_launch": reads_launch,
                     "algorithmic_bytes_per_launch": bytes_launch, "algorithmic_bytes_per_read": bytes_all / len(res),
-                    "binding_resource": "instruction issue of one serial wave per read (VALU issue "
-                                        + (f"{valu_issue['pipe_occupancy']:.2f}" if valu_issue else "0.66-0.70")
-                                        + " of what 4 waves/SIMD can give, plus dependent memory round trips), "
-                                        "not HBM bandwidth (DESIGN.md section 4)",
+                    "binding_resource": binding,
                     "valu_issue": valu_issue, "pmc_source": pmc_src, "lib_sha256": sha,
                     "kernel_source_sha256": src_sha}
         counts = {int(k): int(v) for k, v in zip(*np.unique(res["result"], return_counts=True))}

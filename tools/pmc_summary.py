@@ -133,6 +133,10 @@ def main(src, dst):
                    "fetch_bytes_per_read": hb.get("fetch", 0) / reads_per_launch,
                    "write_bytes_per_read": hb.get("write", 0) / reads_per_launch,
                    "valu_insts_per_read": per_read.get("SQ_INSTS_VALU"),
+                   "salu_insts_per_read": per_read.get("SQ_INSTS_SALU"),
+                   # share of the waves' lifetime (SQ_WAVE_CYCLES) each state takes: issuing VALU / any
+                   # instruction, waiting on a counter (memory), waiting for a dependency to issue
+                   "wave_state": a.get("wave_state"),
                    "source": os.path.join(dst, "summary.json"),
                    "note": "rocprofv3 FETCH_SIZE + WRITE_SIZE (KiB x 1024) per dispatch / reads per dispatch; "
                            "uncorrected (random 4-16 B gathers: the guide's x2 streaming factor does not apply)"}
