@@ -74,22 +74,32 @@ __global__ __launch_bounds__(64 * LOOKUP_WAVES) void seed_lookup_kernel(KArgs A,
         uint32_t w[5];
 #pragma unroll
         for (int i = 0; i < 5; i++) w[i] = have && k < 8 && n > 16u * sub ? src[i] : 0u;
+        // branch-free per byte: upper-case (Read::init, Read.h:289-328), the seed code A0 G1 C2 T3
+        // (Tables.cpp:41-48) from bits 2:1 of the upper-cased letter (A 00, C 01, G 11, T 10), and
+        // ACGT membership from a bit mask over 0x40..0x5f
+        uint32_t p0 = 0, p1 = 0, iv = 0;   // 16 positions each: code bit 0, code bit 1, not ACGT
+        const int lim = (int)n - 16 * sub;   // positions of this lane's 16 that lie in the read
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             const uint32_t d = __builtin_amdgcn_alignbit(w[i + 1], w[i], sh);
 #pragma unroll
             for (int b = 0; b < 4; b++) {
-                uint32_t c = (d >> (8 * b)) & 0xff;
-                if (c >= 'a' && c <= 'z') c -= 0x20;   // Read::init upper-cases (Read.h:289-328)
-                const int pos = 16 * sub + 4 * i + b;
-                const int v = base_value(c);            // Seed encoding A0 G1 C2 T3 (Tables.cpp:41-48)
-                const bool inv = pos >= (int)n || v > 3;
-                bad |= pos < (int)n && v > 3;
+                const uint32_t c = (d >> (8 * b)) & 0xffu;
+                const uint32_t uc = (c >= 'a' && c <= 'z') ? c - 0x20u : c;
+                const uint32_t o = uc - 0x40u;
+                constexpr uint32_t kAcgt = (1u << 1) | (1u << 3) | (1u << 7) | (1u << 20);   // A C G T
+                const bool acgt = o < 32u && ((kAcgt >> (o & 31u)) & 1u);
+                const uint32_t x0 = (uc >> 1) & 1u, x1 = (uc >> 2) & 1u;
                 const int bit = 4 * i + b;
-                if (!inv) chunk |= ((uint64_t)(v & 1) << bit) | ((uint64_t)(v >> 1) << (16 + bit));
-                else chunk |= 1ull << (32 + bit);
+                const bool inside = bit < lim;
+                const bool inv = !inside || !acgt;
+                bad |= k < 8 && inside && !acgt;   // (lanes 8..15 load nothing)
+                p0 |= (inv ? 0u : x1) << bit;               // code bit 0: A 0, G 1, C 0, T 1
+                p1 |= (inv ? 0u : (x0 ^ x1)) << bit;        // code bit 1: A 0, G 0, C 1, T 1
+                iv |= (inv ? 1u : 0u) << bit;
             }
         }
+        chunk = (uint64_t)p0 | ((uint64_t)p1 << 16) | ((uint64_t)iv << 32);
     }
     // the read's full 128-position planes in every lane of its group
     uint64_t P0[2] = {0, 0}, P1[2] = {0, 0}, IV[2] = {0, 0};
