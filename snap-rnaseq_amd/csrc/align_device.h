@@ -293,6 +293,15 @@ __device__ __forceinline__ uint32_t max_reduce32(uint32_t v) {
     return m;
 }
 __device__ __forceinline__ uint64_t or_reduce64(uint64_t v) { return wave_reduce64<false>(v); }
+// wave sum (uniform): quad xor 1, xor 2, then the mirrored half-row / row partners (disjoint groups
+// of equal sums at every step), one readlane per row
+__device__ __forceinline__ uint32_t sum_reduce32(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false);    // quad_perm [1,0,3,2]
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, false);    // quad_perm [2,3,0,1]
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xf, 0xf, false);   // row_half_mirror
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xf, 0xf, false);   // row_mirror
+    return readlaneu(v, 0) + readlaneu(v, 16) + readlaneu(v, 32) + readlaneu(v, 48);
+}
 
 __device__ __forceinline__ uint32_t fmix32(uint32_t k) {   // HashTable.h:60-72
     k ^= k >> 16; k *= 0x85ebca6bu; k ^= k >> 13; k *= 0xc2b2ae35u; k ^= k >> 16;

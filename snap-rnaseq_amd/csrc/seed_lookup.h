@@ -189,18 +189,14 @@ __global__ __launch_bounds__(64 * LOOKUP_WAVES) void seed_lookup_kernel(KArgs A,
         }
     }
     if (stats) {
-        uint64_t v = (uint64_t)nProbe | ((uint64_t)nSeed << 32) | ((uint64_t)nOvfRead << 44);
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t lo = (uint32_t)shfl_idx((int)(uint32_t)v, lane ^ o);
-            const uint32_t hi = (uint32_t)shfl_idx((int)(uint32_t)(v >> 32), lane ^ o);
-            v += ((uint64_t)hi << 32) | lo;
-        }
+        const uint32_t seeds = (uint32_t)__popcll(ballot(nSeed != 0));
+        const uint32_t ovf = (uint32_t)__popcll(ballot(nOvfRead >= 1)) + (uint32_t)__popcll(ballot(nOvfRead >= 2));
+        const uint32_t probes = sum_reduce32(nProbe);
         if (lane == 0) {   // 256 slot groups: no single-address atomic hot spot
             unsigned long long *st = stats + 4 * ((blockIdx.x * LOOKUP_WAVES + threadIdx.x / 64) & 255);
-            atomicAdd(st + 0, (unsigned long long)((v >> 32) & 0xfff));
-            atomicAdd(st + 1, (unsigned long long)(v & 0xffffffffull));
-            atomicAdd(st + 2, (unsigned long long)(v >> 44));
+            atomicAdd(st + 0, (unsigned long long)seeds);
+            atomicAdd(st + 1, (unsigned long long)probes);
+            atomicAdd(st + 2, (unsigned long long)ovf);
         }
     }
 }
