@@ -101,47 +101,72 @@ __global__ __launch_bounds__(64 * LOOKUP_WAVES) void seed_lookup_kernel(KArgs A,
         }
         chunk = (uint64_t)p0 | ((uint64_t)p1 << 16) | ((uint64_t)iv << 32);
     }
-    // the read's full 128-position planes in every lane of its group
-    uint64_t P0[2] = {0, 0}, P1[2] = {0, 0}, IV[2] = {0, 0};
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-        const int src = (lane & ~15) + j;
-        const uint32_t lo = (uint32_t)shfl_idx((int)(uint32_t)chunk, src);
-        const uint32_t hi = (uint32_t)shfl_idx((int)(uint32_t)(chunk >> 32), src);
-        const int wd = j >> 2, s = 16 * (j & 3);
-        P0[wd] |= (uint64_t)(lo & 0xffff) << s;
-        P1[wd] |= (uint64_t)(lo >> 16) << s;
-        IV[wd] |= (uint64_t)(hi & 0xffff) << s;
-    }
     SeedRec rec = {0u, 0u, 0u, 0u};
     uint32_t nSeed = 0, nProbe = 0, nOvfRead = 0;
-    // a read whose bases are all ACGT walks the sequence its length alone fixes: a table entry
-    const bool clean = ((ballot(bad) >> (lane & ~15)) & 0xffffull) == 0;
-    if (have && n <= 128 && (int)n >= L) {
-        // offset of the k-th seed of the sequence (BaseAligner.cpp:686-746), simulated with the
-        // read's seedUsed bits: rounds 0, seedLen, ... then the wrap table's starts
-        const int nPossible = (int)n - L + 1;
-        uint64_t u0 = 0, u1 = 0;   // seedUsed, positions 0..127
-        int p = 0, wrap = 0, idx = 0, my = -1;
-        if (clean) {
+    const int grp = lane & ~15;
+    const uint64_t badMask = ballot(bad);
+    const bool can = have && n <= 128 && (int)n >= L;
+    int my = -1;             // offset of this lane's seed k of the sequence (-1: none)
+    uint32_t w0 = 0, w1 = 0;   // code bits 0 and 1 of the seed's positions my .. my + L - 1
+    if (badMask == 0) {
+        // every read of the wave is all ACGT: its sequence of seed offsets depends on its length
+        // alone (a table entry), and a seed's bits come from the three chunks it can span
+        if (can) {
             const uint32_t t = A.tab->seedSeq[n][k];
             my = t == 0xffu ? -1 : (int)t;
         }
-        for (int guard = 0; !clean && guard < 4 * 128; guard++) {   // each step marks, wraps or ends
-            if (p >= nPossible) {
-                if (++wrap >= L) break;                      // wrapCount == seedLen: the read is scored
-                p = (int)wrapT[wrap];
-            }
-            while (p < nPossible && (((p < 64 ? u0 >> p : u1 >> (p - 64)) & 1ull) != 0)) p++;
-            if (p >= nPossible) continue;
-            if (p < 64) u0 |= 1ull << p; else u1 |= 1ull << (p - 64);
-            if (win128(IV[0], IV[1], p, L)) continue;        // not a seed: used, no advance (:740-744)
-            if (idx == k) { my = p; break; }
-            idx++;
-            p += L;
+        const int c0 = my > 0 ? my >> 4 : 0;
+        const uint32_t a = (uint32_t)shfl_idx((int)(uint32_t)chunk, grp + c0);
+        const uint32_t b = (uint32_t)shfl_idx((int)(uint32_t)chunk, grp + (c0 + 1 < 8 ? c0 + 1 : 7));
+        const uint32_t c = (uint32_t)shfl_idx((int)(uint32_t)chunk, grp + (c0 + 2 < 8 ? c0 + 2 : 7));
+        const uint64_t q0 = (uint64_t)(a & 0xffffu) | ((uint64_t)(b & 0xffffu) << 16) | ((uint64_t)(c & 0xffffu) << 32);
+        const uint64_t q1 = (uint64_t)(a >> 16) | ((uint64_t)(b >> 16) << 16) | ((uint64_t)(c >> 16) << 32);
+        const int sh = my > 0 ? my - 16 * c0 : 0;
+        const uint32_t M = (uint32_t)((1ull << L) - 1);
+        w0 = (uint32_t)(q0 >> sh) & M;
+        w1 = (uint32_t)(q1 >> sh) & M;
+    } else {
+        // the read's full 128-position planes in every lane of its group
+        uint64_t P0[2] = {0, 0}, P1[2] = {0, 0}, IV[2] = {0, 0};
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int src = grp + j;
+            const uint32_t lo = (uint32_t)shfl_idx((int)(uint32_t)chunk, src);
+            const uint32_t hi = (uint32_t)shfl_idx((int)(uint32_t)(chunk >> 32), src);
+            const int wd = j >> 2, s = 16 * (j & 3);
+            P0[wd] |= (uint64_t)(lo & 0xffff) << s;
+            P1[wd] |= (uint64_t)(lo >> 16) << s;
+            IV[wd] |= (uint64_t)(hi & 0xffff) << s;
         }
+        const bool clean = ((badMask >> grp) & 0xffffull) == 0;
+        if (can) {
+            // offset of the k-th seed of the sequence (BaseAligner.cpp:686-746), simulated with the
+            // read's seedUsed bits: rounds 0, seedLen, ... then the wrap table's starts
+            const int nPossible = (int)n - L + 1;
+            uint64_t u0 = 0, u1 = 0;   // seedUsed, positions 0..127
+            int p = 0, wrap = 0, idx = 0;
+            if (clean) {
+                const uint32_t t = A.tab->seedSeq[n][k];
+                my = t == 0xffu ? -1 : (int)t;
+            }
+            for (int guard = 0; !clean && guard < 4 * 128; guard++) {   // each step marks, wraps or ends
+                if (p >= nPossible) {
+                    if (++wrap >= L) break;                      // wrapCount == seedLen: the read is scored
+                    p = (int)wrapT[wrap];
+                }
+                while (p < nPossible && (((p < 64 ? u0 >> p : u1 >> (p - 64)) & 1ull) != 0)) p++;
+                if (p >= nPossible) continue;
+                if (p < 64) u0 |= 1ull << p; else u1 |= 1ull << (p - 64);
+                if (win128(IV[0], IV[1], p, L)) continue;        // not a seed: used, no advance (:740-744)
+                if (idx == k) { my = p; break; }
+                idx++;
+                p += L;
+            }
+            if (my >= 0) { w0 = win128(P0[0], P0[1], my, L); w1 = win128(P1[0], P1[1], my, L); }
+        }
+    }
+    {
         if (my >= 0) {
-            const uint32_t w0 = win128(P0[0], P0[1], my, L), w1 = win128(P1[0], P1[1], my, L);
             const uint32_t M = (uint32_t)((1ull << L) - 1);
             // Seed.h:38-51: first base most significant; reverse complement = reverse of code ^ 3
             const uint32_t r0 = __builtin_bitreverse32(w0) >> (32 - L), r1 = __builtin_bitreverse32(w1) >> (32 - L);
