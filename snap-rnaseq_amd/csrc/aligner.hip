@@ -820,7 +820,7 @@ __device__ __forceinline__ void lvg_run(Lds<64 * NW> &S, const LvgTask &T, const
         if (lane == 0) G.plen[DIR > 0 ? 1 : 0][0] = 0;   // only this direction's path
         wave_sync();
         // forward: patternLen = n - t0 = pl (t0 = 0); reverse: patternLen = s0 = pl (t0 = n)
-        lv_prob_pair(&g_tab, G, 0, 0, pl, DIR > 0 ? 0 : pl, DIR > 0 ? 0 : pl, S.fwdQ, 0u, p1, p2, net2);
+        lv_prob_pair(nullptr, G, 0, 0, pl, DIR > 0 ? 0 : pl, DIR > 0 ? 0 : pl, S.fwdQ, 0u, p1, p2, net2);
     }
     if (lane == 0) {
         outScore[blockIdx.x] = e;
