@@ -298,10 +298,10 @@ __device__ __forceinline__ void lv_prob_pair(const DevTables *tab, const GroupLd
     double f = 1.0;
     if (valid && a == 0) {   // quality of read[dir] position p: the forward read's, reversed for RC
         const int p = p0 + DIR * qi;
-        f = tab->phred[(uint8_t)fwdQ[rcRead ? n - 1 - p : p]];
+        f = g_tab.phred[(uint8_t)fwdQ[rcRead ? n - 1 - p : p]];
     }
-    else if (runEnd) f = tab->indel[cnt];
-    const double perf = lane == 0 || lane == 32 ? tab->perfect[patternLen - e] : 1.0;
+    else if (runEnd) f = g_tab.indel[cnt];
+    const double perf = lane == 0 || lane == 32 ? g_tab.perfect[patternLen - e] : 1.0;
     const int e1 = G.plen[0][g], e2 = G.plen[1][g];
     double q = 1.0;
     for (int i = 0; i < e1; i++) q *= readlaned(f, i);

@@ -820,7 +820,7 @@ __device__ __forceinline__ void lvg_run(Lds<64 * NW> &S, const LvgTask &T, const
         if (lane == 0) G.plen[DIR > 0 ? 1 : 0][0] = 0;   // only this direction's path
         wave_sync();
         // forward: patternLen = n - t0 = pl (t0 = 0); reverse: patternLen = s0 = pl (t0 = n)
-        lv_prob_pair(&g_tab, G, 0, 0, pl, DIR > 0 ? 0 : pl, DIR > 0 ? 0 : pl, S.fwdQ, 0u, p1, p2, net2);
+        lv_prob_pair(nullptr, G, 0, 0, pl, DIR > 0 ? 0 : pl, DIR > 0 ? 0 : pl, S.fwdQ, 0u, p1, p2, net2);
     }
     if (lane == 0) {
         outScore[blockIdx.x] = e;
@@ -2778,8 +2778,16 @@ int snapgpu_cigar_last_ms(snapgpu_aligner_t *a, double *ms) {
 int snapgpu_cigar_batch(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, const uint32_t *locations,
                         const uint8_t *directions, int useM, int32_t *editDistance, uint32_t *nOps, uint32_t *ops) {
     if (!a || !reads || !locations || !directions || !editDistance || !nOps || !ops) return SNAPGPU_EINVAL;
+    return snapgpu_internal_cigar_view(a, reads->bases, reads->offsets, reads->lengths, reads->n, locations, directions,
+                                       useM, editDistance, nOps, ops);
+}
+
+// snapgpu_cigar_batch over read i = bases[offsets[i] .. + lengths[i]) of any buffer (the product
+// paths pass both ends of a pair batch at once, offsets from a common base), without a batch copy
+int snapgpu_internal_cigar_view(snapgpu_aligner_t *a, const char *bases, const uint64_t *offsets, const uint32_t *lengths,
+                                uint64_t n, const uint32_t *locations, const uint8_t *directions, int useM,
+                                int32_t *editDistance, uint32_t *nOps, uint32_t *ops) {
     if (a->failed) { snapgpu::setError("aligner failed earlier (device timeout)"); return SNAPGPU_EDEVICE; }
-    const uint64_t n = reads->n;
     if (n == 0) return SNAPGPU_OK;
     if (n > 0xffffffffull) { snapgpu::setError("batch too large"); return SNAPGPU_EINVAL; }
     HIPCHK(hipSetDevice(a->device));
@@ -2788,8 +2796,8 @@ int snapgpu_cigar_batch(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, cons
     uint64_t total = 0;
     uint32_t maxLen = 0;
     for (uint64_t i = 0; i < n; i++) {
-        total += reads->lengths[i];
-        maxLen = std::max(maxLen, reads->lengths[i]);
+        total += lengths[i];
+        maxLen = std::max(maxLen, lengths[i]);
     }
     if (maxLen > (uint32_t)CIG_MAXLEN) { snapgpu::setError("cigar: read longer than 512 bases"); return SNAPGPU_EINVAL; }
     auto al8 = [](uint64_t x) { return (x + 7) & ~7ull; };
@@ -2823,16 +2831,16 @@ int snapgpu_cigar_batch(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, cons
     char *h = (char *)a->cgPin;
     uint64_t *hOff = (uint64_t *)(h + oOff);
     uint64_t at = 0;
-    for (uint64_t i = 0; i < n; i++) { hOff[i] = at; at += reads->lengths[i]; }
+    for (uint64_t i = 0; i < n; i++) { hOff[i] = at; at += lengths[i]; }
     hOff[n] = at;
-    memcpy(h + oLen, reads->lengths, n * 4);
+    memcpy(h + oLen, lengths, n * 4);
     memcpy(h + oLoc, locations, n * 4);
     memcpy(h + oDir, directions, n);
     {
         // pack the bases (several threads for big batches: the copy is the host's part of the call)
         const unsigned nt = n < 16384 ? 1u : std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
         auto pack = [&](uint64_t b, uint64_t e) {
-            for (uint64_t i = b; i < e; i++) memcpy(h + oBases + hOff[i], reads->bases + reads->offsets[i], reads->lengths[i]);
+            for (uint64_t i = b; i < e; i++) memcpy(h + oBases + hOff[i], bases + offsets[i], lengths[i]);
         };
         std::vector<std::thread> th;
         for (unsigned t = 1; t < nt; t++) th.emplace_back(pack, n * t / nt, n * (t + 1) / nt);

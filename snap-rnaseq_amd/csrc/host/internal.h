@@ -26,6 +26,10 @@ void setError(const std::string &msg);
 void *hostAlloc(size_t bytes, bool *pinned);
 void hostFree(void *p, bool pinned);
 
+// snapgpu_reads_t::hostFlags bit 2: a view of another batch's buffers (readsView), which it does not free
+constexpr uint32_t kReadsView = 4u;
+snapgpu_reads_t *readsView(const snapgpu_reads_t *parent, uint64_t n, const uint64_t *offsets, const uint32_t *lengths);
+
 struct Genome {
     std::vector<char> buf;          // guard + bases + guard (built or loaded genomes)
     const char *ext = nullptr;      // or: the same layout in a mapped shared index (snapgpu_index_attach)
@@ -146,6 +150,11 @@ struct GtfPairQuery {
 int contaminantsAddAll(snapgpu_contaminants_t *c, const std::vector<uint32_t> &locations, bool apply = true);
 
 }  // namespace snapgpu
+// aligner.hip: snapgpu_cigar_batch over reads bases[offsets[i] .. + lengths[i]) (no batch copy)
+extern "C" int snapgpu_internal_cigar_view(snapgpu_aligner_t *a, const char *bases, const uint64_t *offsets,
+                                           const uint32_t *lengths, uint64_t n, const uint32_t *locations,
+                                           const uint8_t *directions, int useM, int32_t *editDistance, uint32_t *nOps,
+                                           uint32_t *ops);
 // aligner.hip: snapgpu_align_batch_ex with the multi-hits packed (read i: dense[off[i] .. off[i+1]))
 int snapgpu_internal_align_batch_packed(snapgpu_aligner_t *a, const snapgpu_reads_t *reads,
                                         const snapgpu_search_t *search, uint32_t maxHitsToGet,

@@ -239,6 +239,33 @@ snapgpu_reads_t *snapgpu_reads_from_arrays(uint64_t n, const char *bases, const 
     return r;
 }
 
+}  // extern "C"
+
+namespace snapgpu {
+
+// reads[offsets[i] .. + lengths[i]) of the parent's buffers, without copying them: the view shares
+// the parent's bases, qualities and byte size (the kernels' uploads and the +64 slack past the last
+// read are the parent's), owns only its offsets and lengths, and must not outlive the parent.
+snapgpu_reads_t *readsView(const snapgpu_reads_t *parent, uint64_t n, const uint64_t *offsets, const uint32_t *lengths) {
+    auto *r = new snapgpu_reads_t();
+    r->n = n;
+    r->totalBytes = parent->totalBytes;
+    r->bases = parent->bases;
+    r->quals = parent->quals;
+    r->hostFlags = (parent->hostFlags & 3u) | kReadsView;
+    r->offsets = new uint64_t[n + 1]();
+    r->lengths = new uint32_t[n + 1]();
+    if (n) {
+        memcpy(r->offsets, offsets, n * 8);
+        memcpy(r->lengths, lengths, n * 4);
+    }
+    return r;
+}
+
+}  // namespace snapgpu
+
+extern "C" {
+
 snapgpu_reads_t *snapgpu_reads_from_fastq(const char *path) {
     // FASTQReader::getNextRead (FASTQ.cpp:196-253): 4-line records, id = header line without
     // '@' (trailing CR/LF removed), bases, '+' line, qualities.
@@ -311,8 +338,10 @@ int snapgpu_reads_write_fastq(const snapgpu_reads_t *r, const char *path) {
 
 void snapgpu_reads_free(snapgpu_reads_t *r) {
     if (!r) return;
-    hostFree(r->bases, r->hostFlags & 1u);
-    hostFree(r->quals, r->hostFlags & 2u);
+    if (!(r->hostFlags & kReadsView)) {   // a view's bases and qualities belong to its parent
+        hostFree(r->bases, r->hostFlags & 1u);
+        hostFree(r->quals, r->hostFlags & 2u);
+    }
     delete[] r->offsets; delete[] r->lengths;
     delete[] r->truthLocation; delete[] r->truthDirection;
     delete[] r->frontClipped; delete[] r->unclippedLength;

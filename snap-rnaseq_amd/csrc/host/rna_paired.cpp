@@ -440,7 +440,7 @@ void rnaStageA(const RnaRun &Rr, RnaSub &X) {
     for (int k = 0; k < 2; k++) {
         X.uo[k].resize(nu + 1); X.ul[k].resize(nu + 1);
         for (uint64_t j = 0; j < nu; j++) { X.uo[k][j] = Rr.R[k]->offsets[X.ui[j]]; X.ul[k][j] = Rr.R[k]->lengths[X.ui[j]]; }
-        X.U[k] = snapgpu_reads_from_arrays(nu, Rr.R[k]->bases, Rr.R[k]->quals, X.uo[k].data(), X.ul[k].data());
+        X.U[k] = readsView(Rr.R[k], nu, X.uo[k].data(), X.ul[k].data());   // no copy of the reads
         if (!X.U[k]) { X.fail(SNAPGPU_ENOMEM, "rna_paired_align: out of memory"); return; }
     }
     X.gr.resize(nu + 1);
@@ -576,7 +576,7 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
         }
         if (!co[0].empty()) {
             snapgpu_reads_t *cv[2];
-            for (int k = 0; k < 2; k++) cv[k] = snapgpu_reads_from_arrays(co[k].size(), R[k]->bases, R[k]->quals, co[k].data(), cl[k].data());
+            for (int k = 0; k < 2; k++) cv[k] = readsView(R[k], co[k].size(), co[k].data(), cl[k].data());
             std::vector<snapgpu_pair_result_t> cr(co[0].size());
             int rc = cv[0] && cv[1] ? snapgpu_paired_align_batch(opt->contaminationAligner, cv[0], cv[1], cr.data()) : SNAPGPU_ENOMEM;
             if (rc && rc != SNAPGPU_ENOMEM) X.fail(rc, snapgpu_last_error());
@@ -610,71 +610,74 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
     // go to the GPU, as compact batches (a read without one has no CIGAR: edit distance -1, no
     // ops); the genome (ga) and transcriptome (ta) batches run on two host threads.
     t0 = std::chrono::steady_clock::now();
+    // Both ends of the sub-batch in one set per aligner, one GPU call each: a read's bytes are
+    // addressed from the lower of the two ends' buffers (no copy of the batch).
+    const char *cbase = std::min(R[0]->bases, R[1]->bases);
     struct CigarSet {
-        std::vector<int64_t> slot;   // record -> row in ed/nOps/ops, -1: no location
-        std::vector<uint64_t> off;
+        std::vector<int64_t> slot[2];   // end k, record -> row in ed/nOps/ops, -1: no location
+        std::vector<uint64_t> off;      // from cbase
         std::vector<uint32_t> len, loc, nOps;
         std::unique_ptr<uint32_t[]> ops;   // [rows][SNAPGPU_CIGAR_MAX_OPS], every row written by the download
         std::vector<uint8_t> dir;
         std::vector<int32_t> ed;
-        int32_t edOf(uint64_t i) const { return slot[i] >= 0 ? ed[slot[i]] : -1; }
-        uint32_t nOpsOf(uint64_t i) const { return slot[i] >= 0 ? nOps[slot[i]] : 0u; }
-        const uint32_t *opsOf(uint64_t i) const {
+        int32_t edOf(int k, uint64_t i) const { return slot[k][i] >= 0 ? ed[slot[k][i]] : -1; }
+        uint32_t nOpsOf(int k, uint64_t i) const { return slot[k][i] >= 0 ? nOps[slot[k][i]] : 0u; }
+        const uint32_t *opsOf(int k, uint64_t i) const {
             static const uint32_t kNone[1] = {0};
-            return slot[i] >= 0 ? ops.get() + slot[i] * SNAPGPU_CIGAR_MAX_OPS : kNone;
+            return slot[k][i] >= 0 ? ops.get() + slot[k][i] * SNAPGPU_CIGAR_MAX_OPS : kNone;
         }
-        void add(uint64_t i, uint64_t o, uint32_t ln, uint32_t l, uint8_t d) {
-            slot[i] = (int64_t)loc.size();
+        void add(int k, uint64_t i, uint64_t o, uint32_t ln, uint32_t l, uint8_t d) {
+            slot[k][i] = (int64_t)loc.size();
             off.push_back(o);
             len.push_back(ln);
             loc.push_back(l);
             dir.push_back(d);
         }
-        int run(snapgpu_aligner_t *a, const snapgpu_reads_t *r, int useM, std::mutex &m) {
+        uint64_t rows() const { return loc.size(); }
+        int run(snapgpu_aligner_t *a, const char *base, int useM, std::mutex &m) {
             const uint64_t cnt = loc.size();
             ed.assign(cnt + 1, -1);
             nOps.assign(cnt + 1, 0);
             ops.reset(new uint32_t[(cnt + 1) * SNAPGPU_CIGAR_MAX_OPS]);
             if (!cnt) return SNAPGPU_OK;
-            snapgpu_reads_t *v = snapgpu_reads_from_arrays(cnt, r->bases, r->quals, off.data(), len.data());
-            if (!v) return SNAPGPU_ENOMEM;
             std::lock_guard<std::mutex> lk(m);
-            const int rc = snapgpu_cigar_batch(a, v, loc.data(), dir.data(), useM, ed.data(), nOps.data(), ops.get());
-            snapgpu_reads_free(v);
-            return rc;
+            return snapgpu_internal_cigar_view(a, base, off.data(), len.data(), cnt, loc.data(), dir.data(), useM, ed.data(),
+                                               nOps.data(), ops.get());
         }
     };
-    CigarSet gc[2], tc[2];
+    CigarSet gc, tc;
     std::vector<uint8_t> isT[2];
     for (int k = 0; k < 2; k++) {
         isT[k].assign(nb, 0);
-        gc[k].slot.assign(nb, -1);
-        tc[k].slot.assign(nb, -1);
+        gc.slot[k].assign(nb, -1);
+        tc.slot[k].assign(nb, -1);
+        const uint64_t shift = (uint64_t)(R[k]->bases - cbase);
         for (uint64_t q = 0; q < nb; q++) {
             const PairOut &r = X.po[q];
             const uint64_t i = X.a + q;
             const uint32_t loc = r.status[k] != SNAPGPU_NOT_FOUND ? r.location[k] : kInvalidLocation;
             const bool t = loc != kInvalidLocation && r.isTranscriptome[k];
             isT[k][q] = t;
-            if (t) tc[k].add(q, R[k]->offsets[i], R[k]->lengths[i], r.tlocation[k], (uint8_t)r.direction[k]);
-            else if (loc != kInvalidLocation) gc[k].add(q, R[k]->offsets[i], R[k]->lengths[i], loc, (uint8_t)r.direction[k]);
+            const uint64_t o = shift + R[k]->offsets[i];
+            if (t) tc.add(k, q, o, R[k]->lengths[i], r.tlocation[k], (uint8_t)r.direction[k]);
+            else if (loc != kInvalidLocation) gc.add(k, q, o, R[k]->lengths[i], loc, (uint8_t)r.direction[k]);
         }
-        X.transcriptomeRecords += tc[k].loc.size();
     }
+    X.transcriptomeRecords += tc.rows();
     {
         const auto tg0 = std::chrono::steady_clock::now();
         int grc = SNAPGPU_OK, rc = SNAPGPU_OK;
         std::string gerr, terr;
         auto genomeCigars = [&] {
-            for (int k = 0; k < 2 && grc == SNAPGPU_OK; k++) grc = gc[k].run(Rr.ga, R[k], (int)opt->useM, *Rr.mG);
+            grc = gc.run(Rr.ga, cbase, (int)opt->useM, *Rr.mG);
             if (grc) gerr = snapgpu_last_error();
         };
         // one aligner's stream, events and upload state serve one host thread at a time: the two
-        // CIGAR loops overlap only when the transcriptome and genome aligners are distinct
+        // CIGAR calls overlap only when the transcriptome and genome aligners are distinct
         const bool overlap = Rr.ta != Rr.ga;
         std::thread gt;
         if (overlap) gt = std::thread(genomeCigars);
-        for (int k = 0; k < 2 && rc == SNAPGPU_OK; k++) rc = tc[k].run(Rr.ta, R[k], (int)opt->useM, *Rr.mT);
+        rc = tc.run(Rr.ta, cbase, (int)opt->useM, *Rr.mT);
         if (rc) terr = snapgpu_last_error();
         if (overlap) gt.join();
         else if (rc == SNAPGPU_OK) genomeCigars();
@@ -696,14 +699,14 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
                 tk.clear();
                 const PairOut &r = X.po[q];
                 const uint64_t i = X.a + q;
-                if (tc[k].edOf(q) >= 0) {
+                if (tc.edOf(k, q) >= 0) {
                     const uint32_t full = R[k]->unclippedLength[i], front = R[k]->frontClipped[i];
                     const uint32_t back = full - R[k]->lengths[i] - front;
                     const bool rcd = r.direction[k] == SNAPGPU_RC;
                     const uint32_t before = rcd ? back : front, after = rcd ? front : back;
                     if (before) tk.push_back({before, 'S'});
-                    const uint32_t *tops = tc[k].opsOf(q);
-                    for (uint32_t z = 0; z < tc[k].nOpsOf(q); z++) {
+                    const uint32_t *tops = tc.opsOf(k, q);
+                    for (uint32_t z = 0; z < tc.nOpsOf(k, q); z++) {
                         const uint32_t op = tops[z];
                         tk.push_back({op >> 4, kOp[op & 15]});
                     }
@@ -735,7 +738,7 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
             const int first = locs[0] > locs[1];
             for (int w = 0; w < 2; w++) {
                 const int k = w == 0 ? first : 1 - first;
-                if (locs[k] != kInvalidLocation) lastNm = isT[k][q] ? tc[k].edOf(q) : gc[k].edOf(q);
+                if (locs[k] != kInvalidLocation) lastNm = isT[k][q] ? tc.edOf(k, q) : gc.edOf(k, q);
                 bamNm[2 * q + w] = lastNm;
             }
         }
@@ -774,11 +777,11 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
                 L.mapq = r.mapq[k];
                 if (isT[k][q]) {
                     L.cigar = &splice[k][q];
-                    L.ed = tc[k].edOf(q);
+                    L.ed = tc.edOf(k, q);
                 } else {
-                    L.ed = gc[k].edOf(q);
-                    L.ops = gc[k].opsOf(q);
-                    L.nOps = gc[k].nOpsOf(q);
+                    L.ed = gc.edOf(k, q);
+                    L.ops = gc.opsOf(k, q);
+                    L.nOps = gc.nOpsOf(k, q);
                 }
                 L.hasMate = true;
                 L.firstInPair = w == 0;

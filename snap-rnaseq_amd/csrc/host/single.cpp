@@ -212,7 +212,7 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
     std::vector<uint64_t> uo(nu + 1);
     std::vector<uint32_t> ul(nu + 1);
     for (uint64_t j = 0; j < nu; j++) { uo[j] = reads->offsets[ui[j]]; ul[j] = reads->lengths[ui[j]]; }
-    snapgpu_reads_t *ub = snapgpu_reads_from_arrays(nu, reads->bases, reads->quals, uo.data(), ul.data());
+    snapgpu_reads_t *ub = readsView(reads, nu, uo.data(), ul.data());   // the useful reads, no copy
     if (!ub) return SNAPGPU_ENOMEM;
     std::vector<snapgpu_result_t> tr(nu + 1), gr(nu + 1);
     std::vector<FilterOut> fo(nu + 1);
@@ -253,7 +253,7 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
         for (uint64_t j = 0; j < nu; j++)
             if (fo[j].result == SNAPGPU_NOT_FOUND) { co.push_back(uo[j]); cl.push_back(ul[j]); }
         if (!co.empty()) {
-            snapgpu_reads_t *cb = snapgpu_reads_from_arrays(co.size(), reads->bases, reads->quals, co.data(), cl.data());
+            snapgpu_reads_t *cb = readsView(reads, co.size(), co.data(), cl.data());
             if (!cb) return fail(SNAPGPU_ENOMEM);
             std::vector<snapgpu_result_t> cr(co.size());
             rc = snapgpu_align_batch(opt->contaminationAligner, cb, cr.data());

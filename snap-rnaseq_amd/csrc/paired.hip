@@ -1193,7 +1193,7 @@ int snapgpu_paired_align_batch(snapgpu_paired_aligner_t *pa, const snapgpu_reads
         l[e].resize(fb.size());
         res[e].resize(fb.size());
         for (size_t j = 0; j < fb.size(); j++) { o[e][j] = R[e]->offsets[fb[j]]; l[e][j] = R[e]->lengths[fb[j]]; }
-        sub[e] = snapgpu_reads_from_arrays(fb.size(), R[e]->bases, R[e]->quals, o[e].data(), l[e].data());
+        sub[e] = snapgpu::readsView(R[e], fb.size(), o[e].data(), l[e].data());   // the fallback ends, no copy
         if (!sub[e]) { rc = SNAPGPU_ENOMEM; break; }
         rc = snapgpu_align_batch_submit(pa->single, sub[e], res[e].data());
     }
