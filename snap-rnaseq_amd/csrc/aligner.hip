@@ -1730,6 +1730,9 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
     int perCU = 0;
     hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, (const void *)align_kernel<128, false>, 64, 0);
     if (perCU <= 0) perCU = 8;
+    // occupancy test hook: fewer resident waves per CU than the kernel's resources allow
+    // (the same code, LDS caps and registers; only the persistent grid shrinks)
+    if (const char *t = getenv("SNAPGPU_WAVES_PER_CU"); t && atoi(t) > 0) perCU = std::min(perCU, atoi(t));
     a->grid = prop.multiProcessorCount * perCU;
     uint32_t maxSeeds = params->maxSeedsToUse ? params->maxSeedsToUse
                                               : (uint32_t)(params->maxSeedCoverage * params->maxReadSize / idx->seedLen);
