@@ -366,8 +366,8 @@ int snapgpu_aligner_debug_trip(snapgpu_aligner_t *a, uint32_t read_index);
 const char *snapgpu_source_sha256(void);
 /* Diagnostic (no reference equivalent): with SNAPGPU_PHASES=1 in the environment at
  * snapgpu_aligner_create, align_kernel<128> sums shader cycles per phase and event
- * counts into out32[0..31] (order: snapgpu.BaseAligner.PHASES); reset != 0 zeroes them. */
-int snapgpu_phase_cycles(snapgpu_aligner_t *a, uint64_t *out32, int reset);
+ * counts into out40[0..39] (order: snapgpu.BaseAligner.PHASES); reset != 0 zeroes them. */
+int snapgpu_phase_cycles(snapgpu_aligner_t *a, uint64_t *out40, int reset);
 const char *snapgpu_aligner_name(const snapgpu_aligner_t *a);    /* getName() */
 
 /* -------------------------------------------------------- Landau-Vishkin */

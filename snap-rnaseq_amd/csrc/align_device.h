@@ -321,8 +321,10 @@ __device__ __forceinline__ uint32_t complement_of(uint32_t c) {   // BaseAligner
 constexpr int64_t PACK_GUARD = 1024;     // bit-plane word 0 = genome position -1024
 constexpr int EB = 8;                    // elements popped per batch (forced mode)
 constexpr int CANDCAP = EB * ELEM;       // candidate list capacity
-constexpr uint32_t ORDCAP = 128;         // forced-mode pop order window (u16; reads with more linked
+constexpr uint32_t ORDCAP = 256;         // forced-mode pop order window, <128> (u16; reads with more linked
                                          // elements rank in several windows, or radix-sort: radixMin)
+// <256> keeps 128 entries: its LDS stays within 10,240 B (16 waves per CU)
+constexpr uint32_t ordcap(int maxlen) { return maxlen <= 128 ? ORDCAP : 128u; }
 
 // Scorer state of the bit-plane kernels align_kernel<128> / <256> (align_score.h); NW =
 // 64-position words of the read masks.
@@ -344,6 +346,7 @@ using GroupLds = GroupLdsT<2>;
 
 template <int MAXLEN>
 struct Lds {
+    static constexpr uint32_t ORD = ordcap(MAXLEN);
     static constexpr int NB = MAXLEN / 64;          // 64-position blocks
     static constexpr bool BYTE_PATH = MAXLEN > 256; // byte-compare LV (align_device.h) vs bit planes
     static constexpr int NW = BYTE_PATH ? 1 : NB;   // bit-plane mask words
@@ -374,7 +377,7 @@ struct Lds {
             // lv_rows() maps row e to rows8[e - 1]); between passes, the staged selection keys of
             // the forced-mode ranking
             alignas(16) uint8_t rows8[BYTE_PATH ? 1 : MAX_K - 1][WAVE];
-            uint16_t order[ORDCAP];                 // forced-mode pop order
+            uint16_t order[ordcap(MAXLEN)];         // forced-mode pop order
         } sc;
     } u;
     uint64_t laneMax[WAVE];                         // per-owner-lane max (sortkey<<32 | idx)
@@ -733,7 +736,8 @@ __device__ __forceinline__ uint32_t count_above_desc(const uint32_t *L, uint32_t
 enum : int { PH_SETUP = 0, PH_LOOKUP, PH_INSERT, PH_SCORE, PH_POP, PH_DESC, PH_STAGE, PH_LVF, PH_LVR, PH_APPLY,
              PH_WB, PH_OUT, PH_NPASS, PH_NCAND, PH_NREAD, PH_NPASS16, PH_NPASS32, PH_NPASS64, PH_ROWSF, PH_ROWSR,
              PH_NSCORECALL, PH_NFORCED, PH_NPOPPED, PH_NSUCC, PH_PASSLOOP, PH_SEL, PH_FETCH, PH_SEEDLOOP, PH_NBATCH,
-             PH_RANK, PH_NELEMSF, PH_CANDL, PH_SLOTS = 32 };
+             PH_RANK, PH_NELEMSF, PH_CANDL, PH_SUCC, PH_NEARBY, PH_PROB, PH_FAILS, PH_NFAILSTEP, PH_SUCCWB,
+             PH_SLOTS = 40 };
 __device__ __forceinline__ uint64_t clk() { return __builtin_amdgcn_s_memtime(); }
 #if SNAPGPU_PHASE_TIMERS
 #define PH_T(A, v) const uint64_t v = (A).phaseBuf ? sgk::clk() : 0

@@ -463,6 +463,7 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem6
         const int gs = sm ? (int)__builtin_ctzll(sm) / GS : m;
         const bool fail = leader && !skip && gq >= g0 && gq < gs;
         const uint64_t fm = ballot(fail);
+        PH_T(A, tfl);
         if (fm) {
             // An element's candidates are contiguous in the list: its first failing
             // candidate of this step records score -1 if nothing of the element was scored
@@ -479,6 +480,8 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem6
             }
             sv_add(st, lane, SV_SCORED, (uint32_t)__popcll(fm));
             wave_sync();
+            PH_ADD(A, S, PH_FAILS, tfl);
+            PH_CNT(A, S, PH_NFAILSTEP, 1);
         }
         if (gs >= m) {
             lastSlot = readlaneu(sl, (m - 1) * GS);
@@ -487,6 +490,7 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem6
         }
         lastSlot = readlaneu(sl, gs * GS);
         lastSkip = false;
+        PH_T(A, tsu);
         // ---- the success at group gs: full bookkeeping (BaseAligner.cpp:1227-1384)
         const int ln = gs * GS;
         const uint32_t csl = readlaneu(sl, ln), cbit = readlaneu(bit, ln);
@@ -506,6 +510,7 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem6
         uint32_t nbPre;
         int csPre = -1;
         uint32_t nvPre = 0;
+        PH_T(A, tnb);
         {
             const uint32_t nl = elemLoc + (2 * (elemLoc % ELEM / (ELEM / 2)) - 1) * (ELEM / 2);
             const uint32_t nkey = ((nl / ELEM) << 1) | dir;
@@ -518,10 +523,14 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem6
                 else nvPre = lane < 12 ? ((const uint32_t *)(ar + nbPre))[lane] : 0u;
             }
         }
+        PH_ADD(A, S, PH_NEARBY, tnb);
+        PH_T(A, tpr);
         double q1, q2;
         int net2;
         lv_prob_pair(tab, G, gs, gs * (GS / 2), (int)n, s0, t0, S.fwdQ, dir, q1, q2, net2);
         const double prob = q1 * q2 * tab->seedProb;
+        PH_ADD(A, S, PH_PROB, tpr);
+        PH_T(A, twt);
         const uint32_t loc = elemLoc + (uint32_t)net2;
         const bool anyNearby0 = cScored != 0;
         cScored |= 1ull << cbit;
@@ -570,7 +579,8 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem6
             }
             wave_sync();
         }
-        if (!take) continue;
+        PH_ADD(A, S, PH_SUCCWB, twt);
+        if (!take) { PH_ADD(A, S, PH_SUCC, tsu); continue; }
         st.pAll = st.pAll - cProb > 0.0 ? st.pAll - cProb : 0.0;
         st.pAll += prob;
         if (st.bestScore > sc || (st.bestScore == sc && prob > st.pBest)) {
@@ -587,6 +597,7 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem6
             return true;
         }
         st.scoreLimit = (st.bestScore < A.maxK ? st.bestScore : A.maxK) + A.extra;
+        PH_ADD(A, S, PH_SUCC, tsu);
     }
     PH_ADD(A, S, PH_APPLY, tapp);
     return false;
@@ -760,12 +771,12 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, El
                             rank += (k4.x > ke) + (k4.y > ke) + (k4.z > ke) + (k4.w > ke);
                         }
                     }
-                    const bool in = ke != 0 && rank >= ordBase && rank < ordBase + ORDCAP;
+                    const bool in = ke != 0 && rank >= ordBase && rank < ordBase + Lds<MAXLEN>::ORD;
                     if (in) order[rank - ordBase] = (uint16_t)e;
                     inRange += (uint32_t)__popcll(ballot(in));
                 }
                 fAvail = ordBase + inRange;
-                fMore = inRange == ORDCAP;
+                fMore = inRange == Lds<MAXLEN>::ORD;
                 wave_sync();
                 PH_ADD(A, S, PH_RANK, trk);
             }

@@ -469,11 +469,12 @@ class BaseAligner:
     PHASES = ("setup", "lookup", "insert", "score", "pop", "desc", "stage", "lv_fwd", "lv_rev", "apply",
               "writeback", "out", "n_pass", "n_cand", "n_read", "n_pass16", "n_pass32", "n_pass64", "rows_fwd",
               "rows_rev", "n_score_calls", "n_forced", "n_popped", "n_succ", "passloop", "select", "fetch", "seedloop",
-              "n_batch", "rank", "n_elems_forced", "candlist")
+              "n_batch", "rank", "n_elems_forced", "candlist", "succ", "nearby", "prob", "fails", "n_fail_steps",
+              "succ_tail")
 
     def phase_cycles(self, reset=True):
         """Diagnostic per-phase shader-cycle sums (needs SNAPGPU_PHASES=1 at construction)."""
-        buf = (C.c_uint64 * 32)()
+        buf = (C.c_uint64 * 40)()
         _check(lib().snapgpu_phase_cycles(self._h, buf, int(reset)), "phase_cycles")
         return {k: int(buf[i]) for i, k in enumerate(self.PHASES)}
 

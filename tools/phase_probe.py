@@ -40,5 +40,10 @@ ph["cycles_per_read_total"] = tot
 out = {"kernel_ms": ms, "reads": args.reads, "cycles_per_read": {k: ph[k] / args.reads for k in ph}}
 out["share_of_wave_time"] = {k: round(ph[k] / tot, 4) for k in ("setup", "lookup", "insert", "score", "pop", "desc",
                                                                  "stage", "lv_fwd", "lv_rev", "apply", "writeback", "out",
-                                                                 "select", "fetch", "passloop", "rank", "candlist")}
+                                                                 "select", "fetch", "passloop", "rank", "candlist", "succ",
+                                                                 "nearby", "prob", "fails", "succ_tail")}
+n = max(ph["n_succ"], 1)
+out["cycles_per_success"] = {k: round(ph[k] / n, 1) for k in ("succ", "nearby", "prob", "succ_tail")}
+out["cycles_per_pass"] = {k: round(ph[k] / max(ph["n_pass"], 1), 1) for k in ("passloop", "stage", "lv_fwd", "lv_rev", "apply", "fails", "succ")}
+out["pass_overhead_per_pass"] = round((ph["passloop"] - ph["stage"] - ph["lv_fwd"] - ph["lv_rev"] - ph["apply"]) / max(ph["n_pass"], 1), 1)
 print(json.dumps(out, indent=1))
