@@ -264,7 +264,8 @@ __device__ __forceinline__ int lv_group(GroupLdsT<NW> &G, uint8_t (*rows8)[WAVE]
 // reference's order (x * 1.0 == x, so steps without a factor multiply by 1.0).
 template <int NW>
 __device__ __forceinline__ void lv_prob_pair(const DevTables *tab, const GroupLdsT<NW> &G, int g, int pbase, int n, int s0,
-                                             int t0, const char *fwdQ, uint32_t rcRead, double &p1, double &p2, int &net2) {
+                                             int t0, const char *fwdQ, const double *facQ, const double *facI,
+                                             uint32_t rcRead, double &p1, double &p2, int &net2) {
     const int lane = lane_id();
     const int dx = lane >> 5, j = (lane & 31) + 1;               // step j of direction dx
     const int e = G.plen[dx][g];
@@ -298,9 +299,10 @@ __device__ __forceinline__ void lv_prob_pair(const DevTables *tab, const GroupLd
     double f = 1.0;
     if (valid && a == 0) {   // quality of read[dir] position p: the forward read's, reversed for RC
         const int p = p0 + DIR * qi;
-        f = g_tab.phred[(uint8_t)fwdQ[rcRead ? n - 1 - p : p]];
+        const uint32_t qc = (uint8_t)fwdQ[rcRead ? n - 1 - p : p];
+        f = qc - FACQ_LO < 64u ? facQ[qc - FACQ_LO] : g_tab.phred[qc];   // (LDS copy of g_tab.phred)
     }
-    else if (runEnd) f = g_tab.indel[cnt];
+    else if (runEnd) f = cnt < 32 ? facI[cnt] : g_tab.indel[cnt];
     const double perf = lane == 0 || lane == 32 ? g_tab.perfect[patternLen - e] : 1.0;
     const int e1 = G.plen[0][g], e2 = G.plen[1][g];
     double q = 1.0;
@@ -527,7 +529,7 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem6
         PH_T(A, tpr);
         double q1, q2;
         int net2;
-        lv_prob_pair(tab, G, gs, gs * (GS / 2), (int)n, s0, t0, S.fwdQ, dir, q1, q2, net2);
+        lv_prob_pair(tab, G, gs, gs * (GS / 2), (int)n, s0, t0, S.fwdQ, S.facQ, S.facI, dir, q1, q2, net2);
         const double prob = q1 * q2 * tab->seedProb;
         PH_ADD(A, S, PH_PROB, tpr);
         PH_T(A, twt);

@@ -716,6 +716,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MAXLEN <= 25
     __shared__ Lds<MAXLEN> S;
     ElemOf<MAXLEN> *ar = reinterpret_cast<ElemOf<MAXLEN> *>(A.arena) + (uint64_t)blockIdx.x * A.arenaElems;
     const int lane = lane_id();
+    if constexpr (!Lds<MAXLEN>::BYTE_PATH) {   // the success step's factor tables, once per wave
+        S.facQ[lane] = g_tab.phred[FACQ_LO + lane];
+        if (lane < 32) S.facI[lane] = g_tab.indel[lane];
+        wave_sync();
+    }
     uint32_t total = A.readList ? uni(*A.readCount) : A.nReads;
     // pass 1 after pass 0's routing: nothing to do when every read is long
     if (!A.readList && A.longCount && uni(*A.longCount) == A.nReads) total = 0;
@@ -820,7 +825,10 @@ __device__ __forceinline__ void lvg_run(Lds<64 * NW> &S, const LvgTask &T, const
         if (lane == 0) G.plen[DIR > 0 ? 1 : 0][0] = 0;   // only this direction's path
         wave_sync();
         // forward: patternLen = n - t0 = pl (t0 = 0); reverse: patternLen = s0 = pl (t0 = n)
-        lv_prob_pair(nullptr, G, 0, 0, pl, DIR > 0 ? 0 : pl, DIR > 0 ? 0 : pl, S.fwdQ, 0u, p1, p2, net2);
+        S.facQ[lane] = g_tab.phred[FACQ_LO + lane];
+        if (lane < 32) S.facI[lane] = g_tab.indel[lane];
+        wave_sync();
+        lv_prob_pair(nullptr, G, 0, 0, pl, DIR > 0 ? 0 : pl, DIR > 0 ? 0 : pl, S.fwdQ, S.facQ, S.facI, 0u, p1, p2, net2);
     }
     if (lane == 0) {
         outScore[blockIdx.x] = e;
