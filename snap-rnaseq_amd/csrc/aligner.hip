@@ -735,18 +735,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MAXLEN <= 25
         const uint32_t r = list ? uni(list[i]) : i;
         if (__hip_atomic_load(&A.diag[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;   // watchdog: drain
         if (r == A.tripRead && lane == 0) diag_report(A.diag, DIAG_TEST_TRIP, r, 0);   // test hook
-        {
-            // the kernel arguments re-read from the kernarg segment per read (scalar loads) instead of
-            // kept live in SGPRs across the persistent loop and spilled to VGPR lanes, where every use
-            // is a v_readlane: a VALU instruction, and VALU issue is what bounds this kernel
-#if defined(__HIP_DEVICE_COMPILE__)
-            const KArgs *kp = reinterpret_cast<const KArgs *>(__builtin_amdgcn_kernarg_segment_ptr());
-            __asm__ volatile("" : "+s"(kp));
-#else
-            const KArgs *kp = &A;   // (host pass: the kernel body is not code-generated)
-#endif
-            align_one<MAXLEN, EXT>(*kp, S, ar, r);
-        }
+        align_one<MAXLEN, EXT>(A, S, ar, r);
     }
 }
 
