@@ -384,7 +384,7 @@ struct Lds {
     uint32_t nElems;
     uint32_t nSpill;                                // Elem64 spill blocks, taken from the arena's top
     uint32_t nUsed;                                 // nElems + nSpill: the arena is full at arenaElems
-    uint32_t pad_[1];
+    uint32_t qOut;                                  // a quality byte of the read lies outside facQ's range
     alignas(16) uint32_t sk[SKCAP];                 // selection keys of elements < SKCAP
     uint32_t ekey[MIRCAP];                          // element key / hash-chain link of elements < MIRCAP
     uint16_t enext[MIRCAP];                         //   (0xffff = end of chain)
