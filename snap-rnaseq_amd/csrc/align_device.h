@@ -47,7 +47,7 @@ constexpr uint32_t MIRCAP = 256;          // elements whose key / chain link are
 constexpr int ELEM_DWORDS = 36;           // dwords of Elem512 (byte path)
 constexpr int BT = 128;                   // insertion-batch dedupe table (LDS)
 constexpr uint32_t NONE = 0xffffffffu;
-constexpr uint32_t ELCAP = 20;            // Elem64 kernels: elements 0..ELCAP-1 of a read are kept in LDS
+constexpr uint32_t ELCAP = 32;            // Elem64 kernels: elements 0..ELCAP-1 of a read are kept in LDS
 
 struct DevTables {
     double indel[64];
@@ -384,7 +384,7 @@ struct Lds {
     uint32_t nElems;
     uint32_t nSpill;                                // Elem64 spill blocks, taken from the arena's top
     uint32_t nUsed;                                 // nElems + nSpill: the arena is full at arenaElems
-    uint32_t qOut;                                  // a quality byte of the read lies outside facQ's range
+    uint32_t pad_[1];
     alignas(16) uint32_t sk[SKCAP];                 // selection keys of elements < SKCAP
     uint32_t ekey[MIRCAP];                          // element key / hash-chain link of elements < MIRCAP
     uint16_t enext[MIRCAP];                         //   (0xffff = end of chain)
@@ -395,12 +395,7 @@ struct Lds {
     GroupLdsT<NW> grp[BYTE_PATH ? 0 : 1];           // scorer of align_kernel<128> / <256>
     // the read's first ELCAP candidate elements (Elem64) live here, not in the HBM arena
     alignas(16) uint32_t eloc[BYTE_PATH ? 1 : ELCAP][16];
-    // the match-probability factors of a success (lv_prob_pair), copied from g_tab once per wave:
-    // phred[q] for quality bytes FACQ_LO .. FACQ_LO + 63, indel[cnt] for run lengths < MAX_K + 1
-    double facQ[BYTE_PATH ? 1 : 64];
-    double facI[BYTE_PATH ? 1 : 32];
 };
-constexpr uint32_t FACQ_LO = 32;   // facQ covers quality bytes 32..95 (Phred+33 up to Q62)
 // LV row e (1 <= e < MAX_K) of the bit-plane scorer at rows8[e - 1]
 template <int MAXLEN>
 __device__ __forceinline__ uint8_t (*lv_rows(Lds<MAXLEN> &S))[WAVE] {

@@ -264,8 +264,7 @@ __device__ __forceinline__ int lv_group(GroupLdsT<NW> &G, uint8_t (*rows8)[WAVE]
 // reference's order (x * 1.0 == x, so steps without a factor multiply by 1.0).
 template <int NW>
 __device__ __forceinline__ void lv_prob_pair(const DevTables *tab, const GroupLdsT<NW> &G, int g, int pbase, int n, int s0,
-                                             int t0, const char *fwdQ, const double *facQ, const double *facI,
-                                             uint32_t rcRead, double &p1, double &p2, int &net2) {
+                                             int t0, const char *fwdQ, uint32_t rcRead, double &p1, double &p2, int &net2) {
     const int lane = lane_id();
     const int dx = lane >> 5, j = (lane & 31) + 1;               // step j of direction dx
     const int e = G.plen[dx][g];
@@ -299,19 +298,16 @@ __device__ __forceinline__ void lv_prob_pair(const DevTables *tab, const GroupLd
     double f = 1.0;
     if (valid && a == 0) {   // quality of read[dir] position p: the forward read's, reversed for RC
         const int p = p0 + DIR * qi;
-        const uint32_t qc = (uint8_t)fwdQ[rcRead ? n - 1 - p : p];
-        f = facQ ? facQ[qc - FACQ_LO] : g_tab.phred[qc];   // facQ: LDS copy of g_tab.phred (null: a
-    }                                                        // quality of this read lies outside it)
-    else if (runEnd) f = facI[cnt & 31];   // runEnd => step j <= e <= MAX_K - 1 => cnt <= 30
+        f = g_tab.phred[(uint8_t)fwdQ[rcRead ? n - 1 - p : p]];
+    }
+    else if (runEnd) f = g_tab.indel[cnt];
     const double perf = lane == 0 || lane == 32 ? g_tab.perfect[patternLen - e] : 1.0;
-    // the product in step order over the steps whose factor is not 1.0 (x * 1.0 == x exactly;
-    // lanes past a direction's path length hold 1.0)
-    const uint64_t fm = ballot(f != 1.0);
+    const int e1 = G.plen[0][g], e2 = G.plen[1][g];
     double q = 1.0;
-    for (uint64_t m = fm & 0xffffffffull; m; m &= m - 1) q *= readlaned(f, (int)__builtin_ctzll(m));
+    for (int i = 0; i < e1; i++) q *= readlaned(f, i);
     p1 = q * readlaned(perf, 0);
     q = 1.0;
-    for (uint64_t m = fm >> 32; m; m &= m - 1) q *= readlaned(f, 32 + (int)__builtin_ctzll(m));
+    for (int i = 0; i < e2; i++) q *= readlaned(f, 32 + i);
     p2 = q * readlaned(perf, 32);
     const uint64_t ins = ballot(valid && dx == 1 && a == 2), del = ballot(valid && dx == 1 && a == 1);
     net2 = __popcll(ins) - __popcll(del);
@@ -531,8 +527,7 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem6
         PH_T(A, tpr);
         double q1, q2;
         int net2;
-        lv_prob_pair(tab, G, gs, gs * (GS / 2), (int)n, s0, t0, S.fwdQ, uni(S.qOut) ? nullptr : S.facQ, S.facI, dir, q1,
-                     q2, net2);
+        lv_prob_pair(tab, G, gs, gs * (GS / 2), (int)n, s0, t0, S.fwdQ, dir, q1, q2, net2);
         const double prob = q1 * q2 * tab->seedProb;
         PH_ADD(A, S, PH_PROB, tpr);
         PH_T(A, twt);

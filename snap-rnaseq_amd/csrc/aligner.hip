@@ -437,7 +437,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
     if (run) {
         // Read::init upper-casing + BaseAligner.cpp:636-650 (RC read, qualities)
         uint32_t nN = 0;
-        bool other = false, qOut = false;
+        bool other = false;
         for (int i = lane; i < Lds<MAXLEN>::RL; i += WAVE) {
             uint32_t c = 0, q = 0;
             if (i < (int)n) {
@@ -456,7 +456,6 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
             S.fwdQ[i] = (char)q;
             nN += __popcll(ballot(i < (int)n && c == 'N'));
             other |= ballot(i < (int)n && c != 'A' && c != 'C' && c != 'G' && c != 'T' && c != 'N') != 0;
-            qOut |= ballot(i < (int)n && q - FACQ_LO >= 64u) != 0;
         }
         if constexpr (!Lds<MAXLEN>::BYTE_PATH) {
             // bit planes compare bytes exactly unless both the read and the genome hold
@@ -466,7 +465,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
         for (int i = lane; i < NBUCKET; i += WAVE) S.head[i] = Lds<MAXLEN>::HEAD_NONE;
         for (int i = lane; i < BT; i += WAVE) { S.u.ins.btKey[i] = NONE; S.u.ins.btMask[i] = 0; }
         S.laneMax[lane] = 0;
-        if (lane == 0) { S.nElems = 0; S.nSpill = 0; S.nUsed = 0; S.qOut = qOut ? 1u : 0u; }
+        if (lane == 0) { S.nElems = 0; S.nSpill = 0; S.nUsed = 0; }
         wave_sync();
         if constexpr (Lds<MAXLEN>::BYTE_PATH) {
 #pragma unroll
@@ -717,11 +716,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MAXLEN <= 25
     __shared__ Lds<MAXLEN> S;
     ElemOf<MAXLEN> *ar = reinterpret_cast<ElemOf<MAXLEN> *>(A.arena) + (uint64_t)blockIdx.x * A.arenaElems;
     const int lane = lane_id();
-    if constexpr (!Lds<MAXLEN>::BYTE_PATH) {   // the success step's factor tables, once per wave
-        S.facQ[lane] = g_tab.phred[FACQ_LO + lane];
-        if (lane < 32) S.facI[lane] = g_tab.indel[lane];
-        wave_sync();
-    }
     uint32_t total = A.readList ? uni(*A.readCount) : A.nReads;
     // pass 1 after pass 0's routing: nothing to do when every read is long
     if (!A.readList && A.longCount && uni(*A.longCount) == A.nReads) total = 0;
@@ -826,9 +820,7 @@ __device__ __forceinline__ void lvg_run(Lds<64 * NW> &S, const LvgTask &T, const
         if (lane == 0) G.plen[DIR > 0 ? 1 : 0][0] = 0;   // only this direction's path
         wave_sync();
         // forward: patternLen = n - t0 = pl (t0 = 0); reverse: patternLen = s0 = pl (t0 = n)
-        if (lane < 32) S.facI[lane] = g_tab.indel[lane];   // (qualities from g_tab: any byte value)
-        wave_sync();
-        lv_prob_pair(nullptr, G, 0, 0, pl, DIR > 0 ? 0 : pl, DIR > 0 ? 0 : pl, S.fwdQ, nullptr, S.facI, 0u, p1, p2, net2);
+        lv_prob_pair(nullptr, G, 0, 0, pl, DIR > 0 ? 0 : pl, DIR > 0 ? 0 : pl, S.fwdQ, 0u, p1, p2, net2);
     }
     if (lane == 0) {
         outScore[blockIdx.x] = e;
