@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round 4: non-temporal loads for the streaming reads of align_kernel<128> (nt: genome plane
 # windows, bucket lines, read bases / qualities, seed records) so the element arena's lines stay in
-# L2 longer -- A/B time (C2, three alternating rounds) and FETCH_SIZE / WRITE_SIZE per read of both.
+# L2 longer -- A/B time (C2, three alternating rounds) and FETCH_SIZE / WRITE_SIZE per read of both;
+# unib: the success step's branches on f64 comparisons made wave-uniform (readfirstlane).
 export TMPDIR=/tmp SNAPGPU_TIMEOUT_S=120
 O=gpurun_out/r04n; mkdir -p $O
 L=$PWD/snap-rnaseq_amd/snapgpu
@@ -13,6 +14,7 @@ C2="--steps 10 --warmup 2 --no-cpu-baseline --no-extras"
 for i in 1 2 3; do
   run cur_$i $L/libsnapgpu.so $C2
   run nt_$i $L/libsnapgpu_nt.so $C2
+  run unib_$i $L/libsnapgpu_unib.so $C2
 done
 B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras"
 for v in cur nt; do
@@ -26,7 +28,7 @@ def row(n):
     d = json.loads(open(f'gpurun_out/r04n/{n}.json').readline())
     return f"{n:8s} {d['value'] / 1e6:7.3f} M reads/s  kernel {d['roofline']['kernel_ms_per_launch']:7.2f} ms/launch"
 for i in (1, 2, 3):
-    for n in ("cur", "nt"):
+    for n in ("cur", "nt", "unib"):
         print(row(f'{n}_{i}'))
 for v in ("cur", "nt"):
     out = {}
