@@ -71,6 +71,67 @@ __device__ __forceinline__ bool bucket_lookup_lane(const KArgs &A, uint32_t tabl
     }
 }
 
+// One lookup per lane, four lanes per line: in round t (0..3) lane 4i + p loads entry p of the home
+// bucket of lane 16t + i's key, so each 16-B load instruction covers 16 whole 64-B lines where
+// bucket_lookup_lane has every lane touch a different line (4x the line requests for the same
+// bytes).  The entries found go back to their lanes by ds_bpermute.  A key absent from its home
+// bucket whose home bucket is flagged overflow continues lane by lane from the next bucket, so
+// the answer and `lines` equal bucket_lookup_lane's.  Every lane of the wave must call it.
+__device__ __forceinline__ bool bucket_lookup_quad(const KArgs &A, bool act, uint32_t table, uint32_t key,
+                                                   uint32_t &v1, uint32_t &v2, uint32_t &aux, uint32_t &lines) {
+    const int lane = lane_id();
+    uint32_t nB = 1;
+    uint64_t tb = 0;
+    if (act) { nB = A.bucketCount[table]; tb = A.bucketBase[table]; }
+    const uint32_t hb = act ? bucket_home(key, nB) : 0u;
+    const uint64_t line = tb + hb;   // bucket index in the whole image
+    bool found = false, ovf = false;
+    v1 = v2 = aux = 0;
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        const int src = 16 * t + (lane >> 2);
+        const uint32_t lo = (uint32_t)shfl_idx((int)(uint32_t)line, src);
+        const uint32_t hi = (uint32_t)shfl_idx((int)(uint32_t)(line >> 32), src);
+        const uint32_t k = (uint32_t)shfl_idx((int)key, src);
+        const bool a = shfl_idx(act ? 1 : 0, src) != 0;
+        uint4 e = make_uint4(0u, 0u, 0u, 0u);
+        if (a) e = A.buckets[4ull * (((uint64_t)hi << 32) | lo) + (uint32_t)(lane & 3)];
+        const uint64_t hm = ballot(a && (e.w & BK_OCC) && e.x == k);
+        const uint64_t om = ballot(a && (lane & 3) == 0 && (e.w & BK_OVF));
+        const bool mine = (lane >> 4) == t;          // lanes 16t .. 16t+15 own this round's keys
+        const int i = lane & 15;
+        const uint32_t nib = (uint32_t)(hm >> (4 * i)) & 0xfu;
+        const int from = 4 * i + (nib ? (int)__builtin_ctz(nib) : 0);
+        const uint32_t y = (uint32_t)shfl_idx((int)e.y, from), z = (uint32_t)shfl_idx((int)e.z, from);
+        const uint32_t w = (uint32_t)shfl_idx((int)e.w, from);
+        if (mine) {
+            found = nib != 0;
+            ovf = ((om >> (4 * i)) & 1ull) != 0;
+            if (found) { v1 = y; v2 = z; aux = w; }
+        }
+    }
+    lines = 1;
+    if (act && !found && ovf && nB > 1) {   // past the home bucket, as bucket_lookup_lane continues
+        const uint4 *T = A.buckets + 4ull * tb;
+        uint32_t b = bucket_next(hb, nB);
+        for (lines = 2;; lines++) {
+            const uint4 *p = T + 4ull * b;
+            const uint4 e0 = p[0], e1 = p[1], e2 = p[2], e3 = p[3];
+            const bool h0 = (e0.w & BK_OCC) && e0.x == key, h1 = (e1.w & BK_OCC) && e1.x == key;
+            const bool h2 = (e2.w & BK_OCC) && e2.x == key, h3 = (e3.w & BK_OCC) && e3.x == key;
+            if (h0 | h1 | h2 | h3) {
+                const uint4 e = h0 ? e0 : (h1 ? e1 : (h2 ? e2 : e3));
+                v1 = e.y; v2 = e.z; aux = e.w;
+                found = true;
+                break;
+            }
+            if (!(e0.w & BK_OVF) || lines >= nB) break;
+            b = bucket_next(b, nB);
+        }
+    }
+    return found;
+}
+
 // The whole wave, one lookup (uniform key): lanes 0-3 load the four entries of bucket b, lanes 4-7
 // those of bucket b+1 (the adjacent line: a key that spilled over is found without a further round
 // trip).  Results are wave-uniform; lines = buckets a sequential lookup would have loaded.

@@ -166,19 +166,20 @@ __global__ __launch_bounds__(64 * LOOKUP_WAVES) void seed_lookup_kernel(KArgs A,
         }
     }
     {
+        const uint32_t M = (uint32_t)((1ull << L) - 1);
+        // Seed.h:38-51: first base most significant; reverse complement = reverse of code ^ 3
+        const uint32_t r0 = __builtin_bitreverse32(w0) >> (32 - L), r1 = __builtin_bitreverse32(w1) >> (32 - L);
+        const uint64_t f = (spread2(r1) << 1) | spread2(r0);
+        const uint64_t rcv = (spread2(~w1 & M) << 1) | spread2(~w0 & M);
+        const bool comp = (int64_t)f > (int64_t)rcv;
+        const uint64_t canon = comp ? rcv : f;
+        const uint32_t table = (uint32_t)(canon >> 32);
+        const uint32_t key = (uint32_t)canon;
+        // SNAPHashTable::Lookup's answer from the bucket image: one 64-B line per bucket visited,
+        // four lanes per line (the whole wave takes part)
+        uint32_t v1 = 0, v2 = 0, aux = 0, probes = 0;
+        const bool found = bucket_lookup_quad(A, my >= 0, table, key, v1, v2, aux, probes);
         if (my >= 0) {
-            const uint32_t M = (uint32_t)((1ull << L) - 1);
-            // Seed.h:38-51: first base most significant; reverse complement = reverse of code ^ 3
-            const uint32_t r0 = __builtin_bitreverse32(w0) >> (32 - L), r1 = __builtin_bitreverse32(w1) >> (32 - L);
-            const uint64_t f = (spread2(r1) << 1) | spread2(r0);
-            const uint64_t rcv = (spread2(~w1 & M) << 1) | spread2(~w0 & M);
-            const bool comp = (int64_t)f > (int64_t)rcv;
-            const uint64_t canon = comp ? rcv : f;
-            const uint32_t table = (uint32_t)(canon >> 32);
-            const uint32_t key = (uint32_t)canon;
-            // SNAPHashTable::Lookup's answer from the bucket image: one 64-B line per bucket visited
-            uint32_t v1 = 0, v2 = 0, aux = 0, probes = 0;
-            const bool found = bucket_lookup_lane(A, table, key, v1, v2, aux, probes);
             uint32_t cnt = 0;
             nSeed = 1;
             nProbe = probes;
