@@ -114,18 +114,15 @@ __device__ __forceinline__ bool bucket_lookup_quad(const KArgs &A, bool act, uin
     if (act && !found && ovf && nB > 1) {   // past the home bucket, as bucket_lookup_lane continues
         const uint4 *T = A.buckets + 4ull * tb;
         uint32_t b = bucket_next(hb, nB);
-        for (lines = 2;; lines++) {
+        for (lines = 2;; lines++) {   // (entry by entry: this rare path must not raise the kernel's VGPRs)
             const uint4 *p = T + 4ull * b;
-            const uint4 e0 = p[0], e1 = p[1], e2 = p[2], e3 = p[3];
-            const bool h0 = (e0.w & BK_OCC) && e0.x == key, h1 = (e1.w & BK_OCC) && e1.x == key;
-            const bool h2 = (e2.w & BK_OCC) && e2.x == key, h3 = (e3.w & BK_OCC) && e3.x == key;
-            if (h0 | h1 | h2 | h3) {
-                const uint4 e = h0 ? e0 : (h1 ? e1 : (h2 ? e2 : e3));
-                v1 = e.y; v2 = e.z; aux = e.w;
-                found = true;
-                break;
+            bool ovfB = false;
+            for (int q = 0; q < 4 && !found; q++) {
+                const uint4 e = p[q];
+                if (q == 0) ovfB = (e.w & BK_OVF) != 0;
+                if ((e.w & BK_OCC) && e.x == key) { v1 = e.y; v2 = e.z; aux = e.w; found = true; }
             }
-            if (!(e0.w & BK_OVF) || lines >= nB) break;
+            if (found || !ovfB || lines >= nB) break;
             b = bucket_next(b, nB);
         }
     }

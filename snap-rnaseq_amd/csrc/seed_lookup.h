@@ -149,12 +149,14 @@ __global__ __launch_bounds__(64 * LOOKUP_WAVES) void seed_lookup_kernel(KArgs A,
                 const uint32_t t = A.tab->seedSeq[n][k];
                 my = t == 0xffu ? -1 : (int)t;
             }
+#pragma nounroll
             for (int guard = 0; !clean && guard < 4 * 128; guard++) {   // each step marks, wraps or ends
                 if (p >= nPossible) {
                     if (++wrap >= L) break;                      // wrapCount == seedLen: the read is scored
                     p = (int)wrapT[wrap];
                 }
-                while (p < nPossible && (((p < 64 ? u0 >> p : u1 >> (p - 64)) & 1ull) != 0)) p++;
+#pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
+                while (p < nPossible && (((p < 64 ? u0 >> p : u1 >> (p - 64)) & 1ull) != 0)) p++;   // (rolled: rare path)
                 if (p >= nPossible) continue;
                 if (p < 64) u0 |= 1ull << p; else u1 |= 1ull << (p - 64);
                 if (win128(IV[0], IV[1], p, L)) continue;        // not a seed: used, no advance (:740-744)
