@@ -29,6 +29,7 @@ def row(n):
     d = json.loads(open(f'gpurun_out/r04q/{n}.json').readline())
     return f"{n:9s} {d['value'] / 1e6:7.3f} M reads/s  kernel {d['roofline']['kernel_ms_per_launch']:7.2f} ms/launch"
 for i in (1, 2, 3):
+    for n in ("cur", "q8"):
         print(row(f'{n}_{i}'))
 for v in ("cur", "q8"):
     ks = glob.glob(f"gpurun_out/r04q/skt_{v}/**/run_kernel_stats.csv", recursive=True)[0]
