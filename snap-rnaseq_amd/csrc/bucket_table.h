@@ -78,15 +78,11 @@ __device__ __forceinline__ bool bucket_lookup_lane(const KArgs &A, uint32_t tabl
 // bucket whose home bucket is flagged overflow continues lane by lane from the next bucket, so
 // the answer and `lines` equal bucket_lookup_lane's.  Every lane of the wave must call it.
 __device__ __forceinline__ bool bucket_lookup_quad(const KArgs &A, bool act, uint32_t table, uint32_t key,
-                                                   uint32_t &v1, uint32_t &v2, uint32_t &aux, uint32_t &lines,
-                                                   const uint32_t *cntL = nullptr, const uint64_t *baseL = nullptr) {
+                                                   uint32_t &v1, uint32_t &v2, uint32_t &aux, uint32_t &lines) {
     const int lane = lane_id();
     uint32_t nB = 1;
     uint64_t tb = 0;
-    if (act) {   // the table's bucket range: from the caller's LDS copy when it has one
-        if (cntL) { nB = cntL[table]; tb = baseL[table]; }
-        else { nB = A.bucketCount[table]; tb = A.bucketBase[table]; }
-    }
+    if (act) { nB = A.bucketCount[table]; tb = A.bucketBase[table]; }
     const uint32_t hb = act ? bucket_home(key, nB) : 0u;
     const uint64_t line = tb + hb;   // bucket index in the whole image
     bool found = false, ovf = false;

@@ -29,7 +29,6 @@ struct SeedRec {
 };
 constexpr int SEEDS_PER_READ = 16;   // = lanes per read in seed_lookup_kernel: 4 reads per wave
 constexpr int LOOKUP_WAVES = 4;      // waves per seed_lookup_kernel block (16 reads)
-constexpr uint32_t LK_TABLES = 256;  // seed tables whose bucket ranges the lookup kernel keeps in LDS
 
 // bits [p, p+len) of a 128-bit value (len <= 32)
 __device__ __forceinline__ uint32_t win128(uint64_t lo, uint64_t hi, int p, int len) {
@@ -53,23 +52,10 @@ __device__ __forceinline__ uint64_t spread2(uint32_t x32) {
 // stats[4*slot + 0..2] += seeds looked up, hash entries probed, overflow counts read (roofline
 // bytes); slot = block % 256
 __global__ __launch_bounds__(64 * LOOKUP_WAVES) void seed_lookup_kernel(KArgs A, SeedRec *out, unsigned long long *stats) {
-    // Per block, in LDS: the wrap table (GetWrappedNextSeedToTest order) the walk below reads per
-    // lane, the seed-offset table, and -- when the index has at most LK_TABLES seed tables (seedLen
-    // <= 20) -- the tables' bucket counts and bases.  Loaded in parallel with the reads' bases, they
-    // take two dependent global round trips (length -> table row, key -> table's bucket range) off
-    // each lookup's chain.
+    // the wrap table (GetWrappedNextSeedToTest order) in LDS: the walk below reads it per lane
     __shared__ uint32_t wrapT[32];
-    __shared__ uint32_t seqT[129 * 16 / 4];
-    __shared__ uint32_t bCntL[LK_TABLES];
-    __shared__ uint64_t bBaseL[LK_TABLES];
-    const bool tabL = A.nTables <= LK_TABLES;
     if (threadIdx.x < 32) wrapT[threadIdx.x] = A.tab->wrap[threadIdx.x];
-    for (uint32_t i = threadIdx.x; i < 129 * 16 / 4; i += 64 * LOOKUP_WAVES)
-        seqT[i] = reinterpret_cast<const uint32_t *>(&A.tab->seedSeq[0][0])[i];
-    if (tabL)
-        for (uint32_t i = threadIdx.x; i < A.nTables; i += 64 * LOOKUP_WAVES) { bCntL[i] = A.bucketCount[i]; bBaseL[i] = A.bucketBase[i]; }
     __syncthreads();
-    const uint8_t *seqB = reinterpret_cast<const uint8_t *>(seqT);
     const int lane = lane_id();
     const uint32_t r = (blockIdx.x * LOOKUP_WAVES + threadIdx.x / 64) * 4 + (lane >> 4);
     const int k = lane & 15;
@@ -126,7 +112,7 @@ __global__ __launch_bounds__(64 * LOOKUP_WAVES) void seed_lookup_kernel(KArgs A,
         // every read of the wave is all ACGT: its sequence of seed offsets depends on its length
         // alone (a table entry), and a seed's bits come from the three chunks it can span
         if (can) {
-            const uint32_t t = seqB[16 * n + k];
+            const uint32_t t = A.tab->seedSeq[n][k];
             my = t == 0xffu ? -1 : (int)t;
         }
         const int c0 = my > 0 ? my >> 4 : 0;
@@ -160,7 +146,7 @@ __global__ __launch_bounds__(64 * LOOKUP_WAVES) void seed_lookup_kernel(KArgs A,
             uint64_t u0 = 0, u1 = 0;   // seedUsed, positions 0..127
             int p = 0, wrap = 0, idx = 0;
             if (clean) {
-                const uint32_t t = seqB[16 * n + k];
+                const uint32_t t = A.tab->seedSeq[n][k];
                 my = t == 0xffu ? -1 : (int)t;
             }
 #pragma nounroll
@@ -194,8 +180,7 @@ __global__ __launch_bounds__(64 * LOOKUP_WAVES) void seed_lookup_kernel(KArgs A,
         // SNAPHashTable::Lookup's answer from the bucket image: one 64-B line per bucket visited,
         // four lanes per line (the whole wave takes part)
         uint32_t v1 = 0, v2 = 0, aux = 0, probes = 0;
-        const bool found = bucket_lookup_quad(A, my >= 0, table, key, v1, v2, aux, probes, tabL ? bCntL : nullptr,
-                                              tabL ? bBaseL : nullptr);
+        const bool found = bucket_lookup_quad(A, my >= 0, table, key, v1, v2, aux, probes);
         if (my >= 0) {
             uint32_t cnt = 0;
             nSeed = 1;
