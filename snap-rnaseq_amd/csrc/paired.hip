@@ -1118,6 +1118,13 @@ snapgpu_paired_aligner_t *snapgpu_paired_aligner_create(int device, const snapgp
     // pass 2 (reads of 129..512 bases): pass 1's pool sizes on the full <512> grid
     if (allocPass(pa->pass[2], prop.multiProcessorCount * perCU2, c1, std::max<uint32_t>(1, std::min(pa->refPool / 2, c1 / 2)), c1))
         { snapgpu_paired_aligner_free(pa); return nullptr; }
+    // test hook: at most this many waves per pass, so each wave aligns many pairs in a row (a pair's
+    // result must not depend on the pairs its wave aligned before: tests/test_paired.py)
+    if (const char *t = getenv("SNAPGPU_PAIRED_GRID"); t && atoi(t) > 0) {
+        const int g = atoi(t);
+        for (auto &pp : pa->pass) pp.grid = std::min(pp.grid, g);
+        pa->grid256 = std::min(pa->grid256, g);
+    }
     return pa;
 }
 

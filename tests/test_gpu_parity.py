@@ -196,3 +196,24 @@ def test_arena_overflow_pass_vs_oracle(gpu_available, small_world, monkeypatch, 
     bad = mismatches(gpu, cpu)
     assert len(bad) == 0, f"{len(bad)} of {len(gpu)} differ\n" + _report(gpu, cpu, reads, bad)
     assert t["nArenaOverflow"] == int((gpu["nElements"] > 4).sum()) > 20   # the overflowing reads took the big pass
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kw", [dict(), dict(maxHitsToConsider=16000, maxK=15, maxSeedsToUse=8, extraSearchDepth=2)],
+                         ids=["defaults", "rna_transcriptome"])
+def test_align_independent_of_wave_history(gpu_available, small_world, monkeypatch, kw):
+    """A read's record must not depend on the reads its persistent wave aligned before (LDS, arena or
+    spill-block state left behind): the batch on one wave per CU (256 waves, ~16 reads each)
+    equals the full grid's records bitwise, nProbes included, and the oracle."""
+    idx = small_world["index"]
+    reads = snapgpu.Reads.from_list(edge_reads(small_world["genome"]) + [
+        small_world["reads"].get(i) for i in range(small_world["reads"].n)])
+    full = snapgpu.BaseAligner(idx, **kw).AlignReads(reads)
+    monkeypatch.setenv("SNAPGPU_WAVES_PER_CU", "1")
+    al = snapgpu.BaseAligner(idx, **kw)
+    few = al.AlignReads(reads)
+    bad = [i for i in range(len(full)) if full[i].tobytes() != few[i].tobytes()]
+    assert not bad, f"{len(bad)} of {len(full)} records differ on one wave per CU, first {bad[:5]}"
+    cpu = oracle_align(idx, reads, al.params)
+    bad = mismatches(few, cpu)
+    assert len(bad) == 0, f"{len(bad)} of {len(few)} differ from the oracle\n" + _report(few, cpu, reads, bad)

@@ -113,6 +113,24 @@ def test_gpu_intersecting_matches_reference_and_oracle(gpu_available, world, run
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("grid", [1, 7])
+def test_gpu_intersecting_independent_of_wave_history(gpu_available, world, grid, monkeypatch):
+    """A pair's result must not depend on the pairs its wave aligned before (LDS or pool state left
+    behind): the whole batch on `grid` waves (each aligns hundreds of pairs in a row) equals the
+    full-grid run, every field bitwise, under each PAIRED_RUNS parameter set."""
+    idx, r0, r1 = world
+    fields = ("status", "location", "direction", "score", "mapq", "nLocationsScored", "popularSeedsSkipped",
+              "probabilityOfAllPairs", "probabilityOfBestPair")
+    for run in PAIRED_RUNS:
+        full = _gpu_aligner(idx, run).intersect(r0, r1)
+        monkeypatch.setenv("SNAPGPU_PAIRED_GRID", str(grid))
+        few = _gpu_aligner(idx, run).intersect(r0, r1)
+        monkeypatch.delenv("SNAPGPU_PAIRED_GRID")
+        bad = _bitwise(few, full, fields)
+        assert len(bad) == 0, f"{run}: {len(bad)} pairs differ on {grid} waves, e.g. pair {bad[0]}"
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("run", list(PAIRED_RUNS))
 def test_gpu_chimeric_matches_reference(gpu_available, world, run):
     idx, r0, r1 = world
