@@ -6,7 +6,8 @@
 //     candidate being scored, the Landau-Vishkin row history, the candidate
 //     element hash buckets, insertion-batch scratch, per-lane selection maxima.
 //   * HBM: a private element arena (worst-case sized: (maxSeeds+1)*maxHits
-//     elements), 192-byte elements, one read = one arena lifetime.
+//     elements), 64-B Elem64 (reads <= 256 b; the first ELCAP in LDS) or 144-B Elem512 elements,
+//     one read = one arena lifetime.
 //
 // Reference semantics restated (all citations SNAPLib/...):
 //   AlignRead   BaseAligner.cpp:510-938   score  BaseAligner.cpp:977-1399
@@ -47,7 +48,8 @@ constexpr uint32_t MIRCAP = 256;          // elements whose key / chain link are
 constexpr int ELEM_DWORDS = 36;           // dwords of Elem512 (byte path)
 constexpr int BT = 128;                   // insertion-batch dedupe table (LDS)
 constexpr uint32_t NONE = 0xffffffffu;
-constexpr uint32_t ELCAP = 32;            // Elem64 kernels: elements 0..ELCAP-1 of a read are kept in LDS
+constexpr uint32_t ELCAP = 6;             // Elem64 kernels: elements 0..ELCAP-1 of a read are kept in LDS
+                                         // (32 fit 4 waves/SIMD; 6 keep <128> within the 8 KB of 5 waves/SIMD)
 
 struct DevTables {
     double indel[64];
@@ -321,9 +323,9 @@ __device__ __forceinline__ uint32_t complement_of(uint32_t c) {   // BaseAligner
 constexpr int64_t PACK_GUARD = 1024;     // bit-plane word 0 = genome position -1024
 constexpr int EB = 8;                    // elements popped per batch (forced mode)
 constexpr int CANDCAP = EB * ELEM;       // candidate list capacity
-constexpr uint32_t ORDCAP = 256;         // forced-mode pop order window, <128> (u16; reads with more linked
+constexpr uint32_t ORDCAP = 128;         // forced-mode pop order window (u16; reads with more linked
                                          // elements rank in several windows, or radix-sort: radixMin)
-// <256> keeps 128 entries: its LDS stays within 10,240 B (16 waves per CU)
+// (256 entries were 0.35 ms faster at 4 waves/SIMD; 128 keep <128> within the 8 KB of 5 waves/SIMD)
 constexpr uint32_t ordcap(int maxlen) { return maxlen <= 128 ? ORDCAP : 128u; }
 
 // Scorer state of the bit-plane kernels align_kernel<128> / <256> (align_score.h); NW =
