@@ -630,8 +630,9 @@ def main():
             binding = (f"VALU instruction issue: the VALU pipe is {valu_issue['pipe_occupancy_4cyc']:.2f} busy at 4 cycles "
                        f"per wave64 instruction ({valu_issue['pipe_occupancy']:.2f} at the microbenchmark's median "
                        f"{valu_issue['cycles_per_valu_median']:.2f} cycles, {valu_issue['pipe_occupancy_guide_2cyc']:.2f} at 2); "
-                       "the same binary at 2 waves/SIMD is only 5 % slower than at 4 (occupancy_r04j.txt), so a "
-                       f"per-SIMD pipe, not memory latency, is saturated; waves spend {ws['SQ_WAIT_ANY']:.0%} of their time "
+                       "the same binary at 2 waves/SIMD is only 5 % slower than at 4 and 3.5 % faster at 5 "
+                       "(occupancy_r04j.txt, occupancy5_r04s.txt): mostly issue bound, a latency share a fifth "
+                       f"wave still hides; waves spend {ws['SQ_WAIT_ANY']:.0%} of their time "
                        f"waiting on memory counters, {ws['SQ_WAIT_INST_ANY']:.0%} for dependencies, "
                        f"{ws['SQ_ACTIVE_INST_ANY']:.0%} issuing -- not HBM bandwidth (DESIGN.md section 4)")
         else:
