@@ -236,26 +236,49 @@ __device__ __forceinline__ void insert_hits(const KArgs &A, Lds<MAXLEN> &S, Elem
         uint32_t key = ((loc / ELEM) << 1) | dir;
         S.u.ins.scrLoc[lane] = loc;
         uint32_t slot = 0;
-        if (valid) {
-            uint32_t s = (key * 2654435761u) >> 25;
-            for (int probe = 0;; probe++) {
-                uint32_t old = atomicCAS(&S.u.ins.btKey[s], NONE, key);
-                if (old == NONE || old == key) break;
-                if (probe >= BT) { diag_report(A.diag, DIAG_BATCH_TABLE, st.rid, key); valid = false; break; }
-                s = (s + 1) & (BT - 1);
+        // Group the batch's hits by element.  A seed's hits come in descending location order (the
+        // index keeps overflow lists sorted), so the hits of one element are neighbours among the valid
+        // lanes: a lane leads its group when its key differs from the previous valid lane's, and the
+        // group runs to the next leader.  A batch whose keys are not ordered that way (within each
+        // direction) takes the LDS hash table instead.
+        const uint64_t vm = ballot(valid);
+        const uint64_t lowV = vm & ((1ull << lane) - 1);
+        const bool hasPrev = lowV != 0;
+        const uint32_t pkey = (uint32_t)shfl_idx((int)key, hasPrev ? 63 - (int)__builtin_clzll(lowV) : lane);
+        const bool useTab = ballot(valid && hasPrev && ((pkey ^ key) & 1u) == 0 && key > pkey) != 0;
+        uint64_t grp;
+        bool leader;
+        if (!useTab) {
+            leader = valid && (!hasPrev || pkey != key);
+            const uint64_t lm = ballot(leader);
+            const uint64_t above = lm & ~((2ull << lane) - 1);              // leaders after this lane
+            const uint64_t upto = above ? (above & (~above + 1)) - 1 : ~0ull;  // lanes before the next one
+            grp = leader ? vm & upto & ~((1ull << lane) - 1) : 0ull;
+            wave_sync();
+        } else {
+            if (valid) {
+                uint32_t s = (key * 2654435761u) >> 25;
+                for (int probe = 0;; probe++) {
+                    uint32_t old = atomicCAS(&S.u.ins.btKey[s], NONE, key);
+                    if (old == NONE || old == key) break;
+                    if (probe >= BT) { diag_report(A.diag, DIAG_BATCH_TABLE, st.rid, key); valid = false; break; }
+                    s = (s + 1) & (BT - 1);
+                }
+                slot = s;
             }
-            slot = s;
+            wave_sync();
+            if (valid) atomicOr((unsigned long long *)&S.u.ins.btMask[slot], 1ull << lane);
+            wave_sync();
+            grp = valid ? S.u.ins.btMask[slot] : 0;
+            leader = valid && (__builtin_ctzll(grp) == lane);
+            wave_sync();
         }
-        wave_sync();
-        if (valid) atomicOr((unsigned long long *)&S.u.ins.btMask[slot], 1ull << lane);
-        wave_sync();
-        uint64_t grp = valid ? S.u.ins.btMask[slot] : 0;
-        bool leader = valid && (__builtin_ctzll(grp) == lane);
-        wave_sync();
         bool overflow = false;   // element arena exhausted (cannot happen at (maxSeeds+2)*maxHits; guarded)
         if (leader) {
-            S.u.ins.btKey[slot] = NONE;
-            S.u.ins.btMask[slot] = 0;
+            if (useTab) {
+                S.u.ins.btKey[slot] = NONE;
+                S.u.ins.btMask[slot] = 0;
+            }
             uint32_t e = chain_find(A, S, ar, key, (uint32_t)A.arenaElems);
             if (e != NONE || allowAlloc) {
                 uint64_t used = 0;
