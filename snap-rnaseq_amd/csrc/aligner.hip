@@ -2162,8 +2162,10 @@ static int ensureLaneCapacity(snapgpu_aligner_t *a, ExecLane &L, uint64_t reads,
     for (ChunkSlot &S : L.slot) {
         HIPCHK(hipMalloc(&S.dBases, cb));
         HIPCHK(hipMalloc(&S.dQuals, cb));
-        HIPCHK(hipMemset(S.dBases, 0, cb));
-        HIPCHK(hipMemset(S.dQuals, 0, cb));
+        // zeroed on the copy stream, ahead of the uploads into them: a plain hipMemset runs on the
+        // null stream, which the non-blocking copy stream does not wait for
+        HIPCHK(hipMemsetAsync(S.dBases, 0, cb, a->copyStream));
+        HIPCHK(hipMemsetAsync(S.dQuals, 0, cb, a->copyStream));
         HIPCHK(hipMalloc(&S.dOffsets, (reads + 1) * 8));
         HIPCHK(hipMalloc(&S.dLengths, (reads + 1) * 4));
         HIPCHK(hipHostMalloc(&S.hOffsets, (reads + 1) * 8, hipHostMallocDefault));

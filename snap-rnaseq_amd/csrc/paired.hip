@@ -912,8 +912,10 @@ static int ensurePairCapacity(snapgpu_paired_aligner_t *pa, uint64_t n, const ui
             const uint64_t c = bytes[r] + (bytes[r] >> 3) + 4096;
             PCHK(hipMalloc(&pa->dB[r], c));
             PCHK(hipMalloc(&pa->dQ[r], c));
-            PCHK(hipMemset(pa->dB[r], 0, c));
-            PCHK(hipMemset(pa->dQ[r], 0, c));
+            // zeroed on the aligner's stream, ahead of the uploads into them: a plain hipMemset runs
+            // on the null stream, which the non-blocking aligner stream does not wait for
+            PCHK(hipMemsetAsync(pa->dB[r], 0, c, pa->stream));
+            PCHK(hipMemsetAsync(pa->dQ[r], 0, c, pa->stream));
             pa->capBytes[r] = c;
         }
     return SNAPGPU_OK;
