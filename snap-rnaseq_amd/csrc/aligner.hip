@@ -2585,7 +2585,10 @@ int snapgpu_phase_cycles(snapgpu_aligner_t *a, uint64_t *out, int reset) {
     std::vector<uint64_t> buf((size_t)a->grid * PH_SLOTS);
     HIPCHK(hipMemcpy(buf.data(), a->dPhase, buf.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
     for (size_t i = 0; i < buf.size(); i++) out[i % PH_SLOTS] += buf[i];
-    if (reset) HIPCHK(hipMemset(a->dPhase, 0, buf.size() * sizeof(uint64_t)));
+    if (reset) {   // null-stream fill: finished before the next pass set's kernels on the lane streams
+        HIPCHK(hipMemset(a->dPhase, 0, buf.size() * sizeof(uint64_t)));
+        HIPCHK(hipDeviceSynchronize());
+    }
     return SNAPGPU_OK;
 }
 const snapgpu_index_t *snapgpu_aligner_index(const snapgpu_aligner_t *a) { return a ? a->idx : nullptr; }
