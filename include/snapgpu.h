@@ -30,7 +30,9 @@
 extern "C" {
 #endif
 
-#define SNAPGPU_ABI_VERSION 1
+/* 2: snapgpu_timing_t.nNulReads / nUnwritten, SNAPGPU_FLAG_NUL_BYTE, SNAPGPU_PFLAG_NUL_BYTE, the
+ *    buffer length of snapgpu_phase_cycles */
+#define SNAPGPU_ABI_VERSION 2
 
 enum {
     SNAPGPU_OK = 0,
@@ -55,6 +57,10 @@ enum { SNAPGPU_FORWARD = 0, SNAPGPU_RC = 1 };
 #define SNAPGPU_FLAG_TOO_MANY_NS    0x08u  /* countOfNs > maxK (BaseAligner.cpp:652-655) */
 #define SNAPGPU_FLAG_BYTE_PATH      0x10u  /* aligned by the byte-compare pass 3, align_kernel<512> (read
                                               > 256 bases, or IUPAC codes in both read and genome) */
+#define SNAPGPU_FLAG_NUL_BYTE       0x20u  /* the read holds a 0x00 byte inside its length: no FASTQ/SAM
+                                              reader produces one, so it marks a corrupted or unfinished
+                                              upload (the aligner still treats it as a non-ACGT base, as
+                                              the reference would); counted in snapgpu_timing_t.nNulReads */
 
 /*
  * Result of one AlignRead call (BaseAligner.cpp:510-938).  location / direction /
@@ -338,6 +344,10 @@ typedef struct snapgpu_timing {
                                 or IUPAC codes in both read and genome) */
     uint64_t nArenaOverflow; /* reads that outgrew a capped element arena in passes 1-3 and were
                                 aligned again by the big-arena pass (worst-case arenas, small grid) */
+    uint64_t nNulReads;      /* records with SNAPGPU_FLAG_NUL_BYTE (0 for any FASTQ input) */
+    uint64_t nUnwritten;     /* records no pass wrote (the device output is pre-filled with 0xff
+                                and every read must get exactly one record): always 0, else the
+                                call fails with SNAPGPU_EDEVICE */
 } snapgpu_timing_t;
 int snapgpu_last_timing(snapgpu_aligner_t *a, snapgpu_timing_t *t);
 
@@ -366,8 +376,8 @@ int snapgpu_aligner_debug_trip(snapgpu_aligner_t *a, uint32_t read_index);
 const char *snapgpu_source_sha256(void);
 /* Diagnostic (no reference equivalent): with SNAPGPU_PHASES=1 in the environment at
  * snapgpu_aligner_create, align_kernel<128> sums shader cycles per phase and event
- * counts into out40[0..39] (order: snapgpu.BaseAligner.PHASES); reset != 0 zeroes them. */
-int snapgpu_phase_cycles(snapgpu_aligner_t *a, uint64_t *out40, int reset);
+ * counts into out[0..min(len, 40)) (order: snapgpu.BaseAligner.PHASES); reset != 0 zeroes them. */
+int snapgpu_phase_cycles(snapgpu_aligner_t *a, uint64_t *out, uint32_t len, int reset);
 const char *snapgpu_aligner_name(const snapgpu_aligner_t *a);    /* getName() */
 
 /* -------------------------------------------------------- Landau-Vishkin */
@@ -610,7 +620,9 @@ typedef struct snapgpu_pair_result {
     uint32_t nLocationsScored;     /* IntersectingPairedEndAligner::getLocationsScored() delta */
     uint32_t nSingleScored;        /* the fallback BaseAligner's getLocationsScored() delta */
     uint32_t popularSeedsSkipped;  /* both reads' popular seeds (the MAPQ input, :741) */
-    uint32_t reserved;
+    uint32_t writtenBy;            /* routing (diagnostic): the intersecting pass that wrote the record --
+                                      1 pass 1 (<128>), 2 pass 1b (<256>), 3 pass 2 (<512>), 4 pass 3
+                                      (the reference's pools); 0 for a pair whose mates are both < 50 */
     double   probabilityOfAllPairs;   /* the intersecting aligner's MAPQ inputs (align()'s locals) */
     double   probabilityOfBestPair;
 } snapgpu_pair_result_t;   /* 64 bytes */
@@ -618,6 +630,8 @@ typedef struct snapgpu_pair_result {
 #define SNAPGPU_PFLAG_READ_TOO_LONG  0x02   /* the reference soft_exits (IntersectingPairedEndAligner.cpp:211-215) */
 #define SNAPGPU_PFLAG_DEFERRED       0x04   /* left pass 1: aligned by the long-read pass or the large-pool pass */
 #define SNAPGPU_PFLAG_MAPQ_FIXED     0x08   /* MAPQ re-derived on the host (threshold case) */
+#define SNAPGPU_PFLAG_NUL_BYTE       0x10   /* a read of the pair holds a 0x00 byte inside its length (a
+                                               corrupted upload; see SNAPGPU_FLAG_NUL_BYTE) */
 
 void snapgpu_paired_params_default(snapgpu_paired_params_t *p);
 typedef struct snapgpu_paired_aligner snapgpu_paired_aligner_t;

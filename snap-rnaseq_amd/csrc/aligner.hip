@@ -460,7 +460,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
     if (run) {
         // Read::init upper-casing + BaseAligner.cpp:636-650 (RC read, qualities)
         uint32_t nN = 0;
-        bool other = false;
+        bool other = false, nul = false;
         for (int i = lane; i < Lds<MAXLEN>::RL; i += WAVE) {
             uint32_t c = 0, q = 0;
             if (i < (int)n) {
@@ -479,7 +479,9 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
             S.fwdQ[i] = (char)q;
             nN += __popcll(ballot(i < (int)n && c == 'N'));
             other |= ballot(i < (int)n && c != 'A' && c != 'C' && c != 'G' && c != 'T' && c != 'N') != 0;
+            nul |= ballot(i < (int)n && c == 0) != 0;   // no reader produces 0x00: a corrupted upload
         }
+        if (nul) flags |= SNAPGPU_FLAG_NUL_BYTE;
         if constexpr (!Lds<MAXLEN>::BYTE_PATH) {
             // bit planes compare bytes exactly unless both the read and the genome hold
             // non-ACGTN bytes (an IUPAC code could then match itself): byte path
@@ -1706,10 +1708,13 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
     }
     if ((e = hipStreamCreateWithFlags(&a->copyStream, hipStreamNonBlocking)) != hipSuccess) return fail("stream", e);
     for (auto &ev : a->cev) if ((e = hipEventCreate(&ev)) != hipSuccess) return fail("event", e);
-    if ((e = hipMalloc(&a->dDiag, 4 * sizeof(uint32_t))) != hipSuccess) return fail("watchdog record", e);
-    if ((e = hipMemset(a->dDiag, 0, 4 * sizeof(uint32_t))) != hipSuccess) return fail("watchdog record", e);
-    if ((e = ensureDeviceTables(device)) != hipSuccess) return fail("device tables", e);
     hipStream_t s0 = a->stream();
+    // Every buffer is initialised on the stream of its first consumer or before the device-wide
+    // synchronisation at the end of this function (stream audit): no
+    // null-stream fill or copy may race the non-blocking lane streams.
+    if ((e = hipMalloc(&a->dDiag, 4 * sizeof(uint32_t))) != hipSuccess) return fail("watchdog record", e);
+    if ((e = hipMemsetAsync(a->dDiag, 0, 4 * sizeof(uint32_t), s0)) != hipSuccess) return fail("watchdog record", e);
+    if ((e = ensureDeviceTables(device)) != hipSuccess) return fail("device tables", e);
     // index upload: genome with guards, tables, overflow, pieces
     const uint32_t nBases = idx->genome->nBases;
     const size_t gbytes = kDevGuard + nBases + kDevGuard;
@@ -1794,7 +1799,7 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
     if (const char *t = getenv("SNAPGPU_PHASES"); t && atoi(t)) {
         const size_t pb = (size_t)a->grid * PH_SLOTS * sizeof(unsigned long long);
         if ((e = hipMalloc(&a->dPhase, pb)) != hipSuccess) return fail("phase buffer", e);
-        hipMemset(a->dPhase, 0, pb);
+        if ((e = hipMemsetAsync(a->dPhase, 0, pb, s0)) != hipSuccess) return fail("phase buffer", e);
     }
     if ((e = hipDeviceSynchronize()) != hipSuccess) return fail("sync", e);
     return a;
@@ -1913,6 +1918,10 @@ static int launch_passes(snapgpu_aligner_t *a, int li, const PassIO &io, const A
     (void)hipGetLastError();   // clear any stale error of an unrelated earlier runtime call
     if (prev && !a->overlapKernels) HIPCHK(hipStreamWaitEvent(L.stream, prev->e[2], 0));
     HIPCHK(hipMemsetAsync(L.counter, 0, 64, L.stream));
+    // every record pre-filled with 0xff (result 0xff is no AlignmentResult): a read that no pass
+    // writes -- lost in the routing between passes -- fails the call on the host (finishChunk /
+    // finishRecords) instead of coming back as a stale or zeroed NotFound-looking record
+    HIPCHK(hipMemsetAsync(io.out, 0xff, io.n * sizeof(snapgpu_result_t), L.stream));
     // pass 0: the first SEEDS_PER_READ seed lookups of every read (4 reads per 64-lane block); it also puts the
     // reads longer than 128 bases straight onto pass 2's list
     A.seedRecs = nullptr;
@@ -2119,10 +2128,23 @@ int snapgpu_synchronize(snapgpu_aligner_t *a) {
 
 // Records -> caller: MAPQ fix-ups (ratio within 1e-9 of a threshold 10^(-q/10), mapq_dev,
 // re-derived with glibc log10) and the aligner statistics, over out[0, n).
-static void finishRecords(snapgpu_aligner_t *a, snapgpu_result_t *out, uint64_t n) {
-    uint64_t fixed = 0;
+// A record whose result byte is still the 0xff pre-fill was written by no pass: the call fails.
+static int checkRecords(snapgpu_aligner_t *a, uint64_t unwritten, uint64_t firstUnwritten) {
+    a->timing.nUnwritten += unwritten;
+    if (!unwritten) return SNAPGPU_OK;
+    // a tripped watchdog drains the kernels (its reads stay unwritten): report it as such
+    if (int rc = checkWatchdog(a)) return rc;
+    snapgpu::setError("align: " + std::to_string(unwritten) + " read record(s) written by no pass (first: read " +
+                      std::to_string(firstUnwritten) + " of the call); results are not valid");
+    return SNAPGPU_EDEVICE;
+}
+
+static int finishRecords(snapgpu_aligner_t *a, snapgpu_result_t *out, uint64_t n) {
+    uint64_t fixed = 0, nul = 0, unwritten = 0, first = 0;
     for (uint64_t i = 0; i < n; i++) {
         snapgpu_result_t &o = out[i];
+        if (o.result > SNAPGPU_UNKNOWN) { if (!unwritten++) first = i; continue; }
+        nul += (o.flags & SNAPGPU_FLAG_NUL_BYTE) ? 1 : 0;
         if (o.flags & SNAPGPU_FLAG_MAPQ_FIXED) {
             o.mapq = hostMapq(o.probabilityOfAllCandidates, o.probabilityOfBestCandidate, o.score, o.popularSeedsSkipped);
             o.result = o.mapq >= 10 ? SNAPGPU_SINGLE_HIT : SNAPGPU_MULTIPLE_HITS;
@@ -2135,6 +2157,8 @@ static void finishRecords(snapgpu_aligner_t *a, snapgpu_result_t *out, uint64_t 
         a->stats.nReads++;
     }
     a->timing.nMapqFixed += fixed;
+    a->timing.nNulReads += nul;
+    return checkRecords(a, unwritten, first);
 }
 
 int snapgpu_results_download(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, snapgpu_result_t *out) {
@@ -2146,9 +2170,11 @@ int snapgpu_results_download(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, sn
     HIPCHK(hipStreamSynchronize(a->stream()));
     auto t0 = std::chrono::steady_clock::now();
     a->timing.nMapqFixed = 0;
-    finishRecords(a, out, d->n);
+    a->timing.nNulReads = 0;
+    a->timing.nUnwritten = 0;
+    rc = finishRecords(a, out, d->n);
     a->timing.fixupMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    return SNAPGPU_OK;
+    return rc;
 }
 
 // (Re)allocate a lane's chunk buffers for `reads` reads spanning `bytes` read bytes.
@@ -2195,12 +2221,14 @@ static int finishChunk(snapgpu_aligner_t *a, ChunkSlot &L) {
     snapgpu_result_t *dst = out + L.chunkBegin;
     const unsigned nt = n >= 65536 ? std::max(1u, std::min(4u, std::thread::hardware_concurrency())) : 1u;
     std::vector<snapgpu_aligner_stats_t> st(nt, snapgpu_aligner_stats_t{});
-    std::vector<uint64_t> fixed(nt, 0);
+    std::vector<uint64_t> fixed(nt, 0), nul(nt, 0), unwritten(nt, 0), first(nt, 0);
     auto work = [&](unsigned t) {
         const uint64_t b = n * t / nt, e = n * (t + 1) / nt;
         memcpy(dst + b, L.hOut + b, (e - b) * sizeof(snapgpu_result_t));
         for (uint64_t i = b; i < e; i++) {
             snapgpu_result_t &o = dst[i];
+            if (o.result > SNAPGPU_UNKNOWN) { if (!unwritten[t]++) first[t] = L.chunkBegin + i; continue; }
+            nul[t] += (o.flags & SNAPGPU_FLAG_NUL_BYTE) ? 1 : 0;
             if (o.flags & SNAPGPU_FLAG_MAPQ_FIXED) {
                 o.mapq = hostMapq(o.probabilityOfAllCandidates, o.probabilityOfBestCandidate, o.score, o.popularSeedsSkipped);
                 o.result = o.mapq >= 10 ? SNAPGPU_SINGLE_HIT : SNAPGPU_MULTIPLE_HITS;
@@ -2224,10 +2252,13 @@ static int finishChunk(snapgpu_aligner_t *a, ChunkSlot &L) {
         a->stats.nHitsIgnoredBecauseOfTooHighPopularity += st[t].nHitsIgnoredBecauseOfTooHighPopularity;
         a->stats.nReadsIgnoredBecauseOfTooManyNs += st[t].nReadsIgnoredBecauseOfTooManyNs;
         a->timing.nMapqFixed += fixed[t];
+        a->timing.nNulReads += nul[t];
     }
     a->stats.nReads += n;
     a->timing.fixupMs += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    return SNAPGPU_OK;
+    uint64_t uw = 0, f0 = 0;
+    for (unsigned t = 0; t < nt; t++) { if (unwritten[t] && !uw) f0 = first[t]; uw += unwritten[t]; }
+    return checkRecords(a, uw, f0);
 }
 
 // The host tail of the oldest pipelined chunk still pending (any lane); false if none.
@@ -2572,23 +2603,25 @@ int snapgpu_aligner_get_stats(const snapgpu_aligner_t *a, snapgpu_aligner_stats_
     *s = a->stats;
     return SNAPGPU_OK;
 }
-int snapgpu_phase_cycles(snapgpu_aligner_t *a, uint64_t *out, int reset) {
+int snapgpu_phase_cycles(snapgpu_aligner_t *a, uint64_t *out, uint32_t len, int reset) {
     if (!a || !out) return SNAPGPU_EINVAL;
-    memset(out, 0, PH_SLOTS * sizeof(uint64_t));
+    const uint32_t m = len < (uint32_t)PH_SLOTS ? len : (uint32_t)PH_SLOTS;   // the caller's buffer length
+    memset(out, 0, m * sizeof(uint64_t));
 #if !SNAPGPU_PHASE_TIMERS
     snapgpu::setError("library built without phase timers (make PHASE_TIMERS=1)");
     return SNAPGPU_EUNSUPPORTED;
 #endif
     if (!a->dPhase) { snapgpu::setError("phase diagnostics off (set SNAPGPU_PHASES=1 before aligner_create)"); return SNAPGPU_EINVAL; }
     HIPCHK(hipSetDevice(a->device));
-    HIPCHK(hipStreamSynchronize(a->stream()));
+    for (auto &L : a->lane) HIPCHK(hipStreamSynchronize(L.stream));   // both lanes' pass sets add to it
     std::vector<uint64_t> buf((size_t)a->grid * PH_SLOTS);
-    HIPCHK(hipMemcpy(buf.data(), a->dPhase, buf.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
-    for (size_t i = 0; i < buf.size(); i++) out[i % PH_SLOTS] += buf[i];
-    if (reset) {   // null-stream fill: finished before the next pass set's kernels on the lane streams
-        HIPCHK(hipMemset(a->dPhase, 0, buf.size() * sizeof(uint64_t)));
-        HIPCHK(hipDeviceSynchronize());
-    }
+    hipStream_t s0 = a->stream();
+    HIPCHK(hipMemcpyAsync(buf.data(), a->dPhase, buf.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, s0));
+    // zeroed on lane 0's stream; the sync below orders it before any later pass set of either lane
+    if (reset) HIPCHK(hipMemsetAsync(a->dPhase, 0, buf.size() * sizeof(uint64_t), s0));
+    HIPCHK(hipStreamSynchronize(s0));
+    for (size_t i = 0; i < buf.size(); i++)
+        if (i % PH_SLOTS < m) out[i % PH_SLOTS] += buf[i];
     return SNAPGPU_OK;
 }
 const snapgpu_index_t *snapgpu_aligner_index(const snapgpu_aligner_t *a) { return a ? a->idx : nullptr; }

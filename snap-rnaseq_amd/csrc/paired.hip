@@ -64,6 +64,7 @@ struct PArgs {
     uint32_t refPool;                       // the reference's scoringCandidatePoolSize (:128)
     uint32_t maxLen;                        // reads this pass takes (128 or 512)
     uint32_t deferred;                      // the pairs of this pass were deferred (passes 1b, 2, 3)
+    uint32_t passId;                        // snapgpu_pair_result_t::writtenBy of this launch's records
 };
 
 struct Lookup {                             // HashTableLookup (IntersectingPairedEndAligner.h:101-134);
@@ -364,7 +365,11 @@ struct PairOut {
 
 template <int MAXLEN>
 __device__ void write_result(const PArgs &P, uint32_t pi, const snapgpu_pair_result_t &res) {
-    if (lane_id() == 0) P.out[pi] = res;
+    if (lane_id() == 0) {
+        snapgpu_pair_result_t o = res;
+        o.writtenBy = P.passId;   // routing record (diagnostic): which pass wrote it
+        P.out[pi] = o;
+    }
 }
 
 __device__ __forceinline__ void pre_state(snapgpu_pair_result_t &r) {
@@ -374,7 +379,7 @@ __device__ __forceinline__ void pre_state(snapgpu_pair_result_t &r) {
     r.status[0] = r.status[1] = SNAPGPU_NOT_FOUND;
     r.direction[0] = r.direction[1] = 0;
     r.fromAlignTogether = 0; r.alignedAsPair = 0; r.flags = 0;
-    r.nLocationsScored = 0; r.nSingleScored = 0; r.popularSeedsSkipped = 0; r.reserved = 0;
+    r.nLocationsScored = 0; r.nSingleScored = 0; r.popularSeedsSkipped = 0; r.writtenBy = 0;
     r.probabilityOfAllPairs = 0; r.probabilityOfBestPair = 0;
 }
 
@@ -525,7 +530,8 @@ __device__ __forceinline__ void record_hits(const PArgs &P, HitSet (&hs)[2], con
 }
 
 // Read r of the pair into LDS: Read::init upper-cases; RC data and reversed qualities
-// (:217-224); zero slack.  Returns this lane's count of 'N' (:220).
+// (:217-224); zero slack.  Returns this lane's count of 'N' (:220), plus 0x10000 per 0x00 byte
+// inside the read (SNAPGPU_PFLAG_NUL_BYTE: a corrupted upload; no reader produces one).
 template <int MAXLEN>
 __device__ __forceinline__ uint32_t load_read(const PArgs &P, PLds<MAXLEN> &S, const int r, const uint32_t nr,
                                               const uint64_t offr) {
@@ -539,7 +545,7 @@ __device__ __forceinline__ uint32_t load_read(const PArgs &P, PLds<MAXLEN> &S, c
             if (c >= 'a' && c <= 'z') c = (char)(c - 0x20);
             cq = q[i];
             cc = c == 'A' ? 'T' : c == 'G' ? 'C' : c == 'C' ? 'G' : c == 'T' ? 'A' : c == 'N' ? 'N' : 0;
-            ns += c == 'N';
+            ns += c == 'N' ? 1u : (c == 0 ? 0x10000u : 0u);
             S.rd[r][1][nr - 1 - i] = cc;
             S.rq[r][1][nr - 1 - i] = cq;
         } else {
@@ -598,6 +604,8 @@ __device__ void align_pair(const PArgs &P, PLds<MAXLEN> &S, Cand *cand, Mate *ma
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) countNs += (uint32_t)__shfl_xor((int)countNs, o);
     countNs = uni(countNs);
+    if (countNs >> 16) res.flags |= SNAPGPU_PFLAG_NUL_BYTE;
+    countNs &= 0xffffu;
     if (countNs > maxK) { write_result<MAXLEN>(P, pi, res); return; }              // :226-228
     uint32_t maxSeeds = P.maxSeedsCmd ? P.maxSeedsCmd
                                       : (uint32_t)((n0 > n1 ? n0 : n1) * P.seedCoverage / seedLen);   // :150-155
@@ -946,6 +954,9 @@ static int runIntersect(snapgpu_paired_aligner_t *pa, const snapgpu_reads_t *r0,
         PCHK(hipMemcpyAsync(pa->dL[r], R[r]->lengths, n * 4, hipMemcpyHostToDevice, s));
     }
     PCHK(hipMemsetAsync(pa->dCounter, 0, 32, s));
+    // records pre-filled with 0xff (status 0xff is no AlignmentResult): a pair that no pass writes
+    // fails the call below instead of coming back as a stale or zeroed NotFound-looking record
+    PCHK(hipMemsetAsync(pa->dOut, 0xff, n * sizeof(snapgpu_pair_result_t), s));
     PArgs P;
     memset(&P, 0, sizeof(P));
     P.X = pa->X;
@@ -967,14 +978,16 @@ static int runIntersect(snapgpu_paired_aligner_t *pa, const snapgpu_reads_t *r0,
     for (uint64_t i = 0; i < n; i++)
         (R[0]->lengths[i] > 128 || R[1]->lengths[i] > 128 ? longL : shortL).push_back((uint32_t)i);
     if (!longL.empty()) {
-        const uint32_t nLong = (uint32_t)longL.size();
+        // longL / shortL outlive the copies (the stream is synchronised below, before they go out of
+        // scope); the pass-1 defer count starts at the long pairs' count, set by value (a stack
+        // scalar as the source of an asynchronous copy could be read after its scope ended)
         PCHK(hipMemcpyAsync(pa->dDefer, longL.data(), longL.size() * 4, hipMemcpyHostToDevice, s));
-        PCHK(hipMemcpyAsync(pa->dCounter + 2, &nLong, 4, hipMemcpyHostToDevice, s));
+        PCHK(hipMemsetD32Async((hipDeviceptr_t)(pa->dCounter + 2), (int)longL.size(), 1, s));
         if (!shortL.empty()) PCHK(hipMemcpyAsync(pa->dDefer2, shortL.data(), shortL.size() * 4, hipMemcpyHostToDevice, s));
     }
     // pass 1: reads <= 128 bases, pools for ordinary pairs, the full grid
     P.nPairs = (uint32_t)shortL.size(); P.pairList = longL.empty() ? nullptr : pa->dDefer2; P.counter = pa->dCounter;
-    P.maxLen = 128;
+    P.maxLen = 128; P.passId = 1;
     P.deferList = pa->dDefer; P.deferCount = pa->dCounter + 2;
     usePool(pa->pass[0]);
     int grid = pa->pass[0].grid;
@@ -986,7 +999,7 @@ static int runIntersect(snapgpu_paired_aligner_t *pa, const snapgpu_reads_t *r0,
     PCHK(hipMemcpyAsync(&nDefer, pa->dCounter + 2, 4, hipMemcpyDeviceToHost, s));
     PCHK(hipStreamSynchronize(s));
     if (nDefer) {   // pass 1b: reads of 129..256 bases on the 256-bit planes, pass 1's pools
-        P.nPairs = nDefer; P.pairList = pa->dDefer; P.counter = pa->dCounter + 5; P.maxLen = 256;
+        P.nPairs = nDefer; P.pairList = pa->dDefer; P.counter = pa->dCounter + 5; P.maxLen = 256; P.passId = 2;
         P.deferList = pa->dDefer2; P.deferCount = pa->dCounter + 6;
         usePool(pa->pass[0]);
         grid = pa->grid256;
@@ -998,7 +1011,7 @@ static int runIntersect(snapgpu_paired_aligner_t *pa, const snapgpu_reads_t *r0,
     }
     if (nDefer) {   // pass 2: reads of 257..512 bases, IUPAC cases and pool overflows, ordinary pools, full grid
         // (pass 1b has consumed list 1: it is pass 2's output)
-        P.nPairs = nDefer; P.pairList = pa->dDefer2; P.counter = pa->dCounter + 3; P.maxLen = 512;
+        P.nPairs = nDefer; P.pairList = pa->dDefer2; P.counter = pa->dCounter + 3; P.maxLen = 512; P.passId = 3;
         P.deferList = pa->dDefer; P.deferCount = pa->dCounter + 4;
         usePool(pa->pass[2]);
         grid = pa->pass[2].grid;
@@ -1009,7 +1022,7 @@ static int runIntersect(snapgpu_paired_aligner_t *pa, const snapgpu_reads_t *r0,
         PCHK(hipStreamSynchronize(s));
     }
     if (nDefer) {   // pass 3: pool overflows, the reference's pool sizes on a small grid
-        P.nPairs = nDefer; P.pairList = pa->dDefer; P.counter = pa->dCounter + 1; P.maxLen = 512;
+        P.nPairs = nDefer; P.pairList = pa->dDefer; P.counter = pa->dCounter + 1; P.maxLen = 512; P.passId = 4;
         P.deferList = nullptr; P.deferCount = nullptr;
         usePool(pa->pass[1]);
         grid = pa->pass[1].grid;
@@ -1019,6 +1032,14 @@ static int runIntersect(snapgpu_paired_aligner_t *pa, const snapgpu_reads_t *r0,
     }
     PCHK(hipMemcpyAsync(out, pa->dOut, n * sizeof(snapgpu_pair_result_t), hipMemcpyDeviceToHost, s));
     PCHK(hipStreamSynchronize(s));
+    uint64_t unwritten = 0, first = 0;
+    for (uint64_t i = 0; i < n; i++)
+        if (out[i].status[0] > SNAPGPU_UNKNOWN && !unwritten++) first = i;
+    if (unwritten) {
+        snapgpu::setError("paired: " + std::to_string(unwritten) + " pair record(s) written by no pass (first: pair " +
+                          std::to_string(first) + "); results are not valid");
+        return SNAPGPU_EDEVICE;
+    }
     // MAPQ threshold cases re-derived with glibc log10 (as snapgpu_results_download does)
     for (uint64_t i = 0; i < n; i++) {
         snapgpu_pair_result_t &r = out[i];

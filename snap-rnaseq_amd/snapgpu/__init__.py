@@ -24,6 +24,7 @@ FLAG_MAPQ_FIXED = 0x02
 FLAG_DEFERRED = 0x04
 FLAG_BYTE_PATH = 0x10
 FLAG_TOO_MANY_NS = 0x08
+FLAG_NUL_BYTE = 0x20     # a 0x00 byte inside the read: a corrupted upload (no reader produces one)
 
 RESULT_DTYPE = np.dtype([
     ("location", "<u4"), ("score", "<i4"), ("mapq", "<i4"), ("result", "u1"), ("direction", "u1"),
@@ -38,11 +39,12 @@ assert RESULT_DTYPE.itemsize == C.sizeof(_ffi.Result)
 PAIR_RESULT_DTYPE = np.dtype([
     ("location", "<u4", (2,)), ("score", "<i4", (2,)), ("mapq", "<i4", (2,)), ("status", "u1", (2,)),
     ("direction", "u1", (2,)), ("fromAlignTogether", "u1"), ("alignedAsPair", "u1"), ("flags", "<u2"),
-    ("nLocationsScored", "<u4"), ("nSingleScored", "<u4"), ("popularSeedsSkipped", "<u4"), ("reserved", "<u4"),
+    ("nLocationsScored", "<u4"), ("nSingleScored", "<u4"), ("popularSeedsSkipped", "<u4"), ("writtenBy", "<u4"),
     ("probabilityOfAllPairs", "<f8"), ("probabilityOfBestPair", "<f8"),
 ])
 assert PAIR_RESULT_DTYPE.itemsize == 64
 PFLAG_POOL_EXHAUSTED, PFLAG_READ_TOO_LONG, PFLAG_DEFERRED, PFLAG_MAPQ_FIXED = 0x01, 0x02, 0x04, 0x08
+PFLAG_NUL_BYTE = 0x10
 
 # snapgpu_search_t / snapgpu_multi_hit_t (include/snapgpu.h)
 SEARCH_DTYPE = np.dtype([("searchRadius", "<u4"), ("searchLocation", "<u4"), ("searchDirection", "<u4"),
@@ -475,7 +477,7 @@ class BaseAligner:
     def phase_cycles(self, reset=True):
         """Diagnostic per-phase shader-cycle sums (needs SNAPGPU_PHASES=1 at construction)."""
         buf = (C.c_uint64 * 40)()
-        _check(lib().snapgpu_phase_cycles(self._h, buf, int(reset)), "phase_cycles")
+        _check(lib().snapgpu_phase_cycles(self._h, buf, 40, int(reset)), "phase_cycles")
         return {k: int(buf[i]) for i, k in enumerate(self.PHASES)}
 
     def stats(self):

@@ -157,6 +157,8 @@ class Timing(C.Structure):
         ("lookupKernelBusyMs", C.c_double),
         ("nByteReads", C.c_uint64),
         ("nArenaOverflow", C.c_uint64),
+        ("nNulReads", C.c_uint64),
+        ("nUnwritten", C.c_uint64),
     ]
 
 
@@ -287,7 +289,7 @@ _PROTOS = [
     ("snapgpu_aligner_set_overlap", C.c_int, [C.c_void_p, C.c_int]),
     ("snapgpu_aligner_debug_trip", C.c_int, [C.c_void_p, C.c_uint32]),
     ("snapgpu_source_sha256", C.c_char_p, []),
-    ("snapgpu_phase_cycles", C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]),
+    ("snapgpu_phase_cycles", C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_uint32, C.c_int]),
     ("snapgpu_aligner_name", C.c_char_p, [C.c_void_p]),
     ("snapgpu_lv_batch", C.c_int, [C.c_int, C.c_int, C.c_uint32, C.c_char_p, C.POINTER(C.c_uint64),
                                    C.POINTER(C.c_uint32), C.c_char_p, C.c_char_p, C.POINTER(C.c_uint64),

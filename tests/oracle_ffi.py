@@ -206,8 +206,23 @@ COMPARE_FIELDS = ("result", "location", "direction", "score", "mapq", "nLookups"
                   "probabilityOfAllCandidates", "probabilityOfBestCandidate")
 
 
+NUL_FLAG = 0x20   # SNAPGPU_FLAG_NUL_BYTE: a read holds a 0x00 byte (a corrupted upload)
+
+
+def assert_no_corrupt_reads(res):
+    """No record of a GPU result array may carry SNAPGPU_FLAG_NUL_BYTE: every test input comes from
+    FASTQ or the synthetic generators, neither of which produces a 0x00 byte inside a read, so a
+    flagged record means the device saw bytes the host did not send."""
+    if "flags" in res.dtype.names:
+        nul = np.nonzero(res["flags"] & NUL_FLAG)[0]
+        assert len(nul) == 0, f"{len(nul)} reads arrived on the device with 0x00 bytes, first {nul[:5]}"
+
+
 def mismatches(a, b, fields=COMPARE_FIELDS):
-    """Indices where two result arrays differ in any field (doubles compared bitwise)."""
+    """Indices where two result arrays differ in any field (doubles compared bitwise).  Both arrays
+    are also checked for records of corrupted uploads (assert_no_corrupt_reads)."""
+    assert_no_corrupt_reads(a)
+    assert_no_corrupt_reads(b)
     bad = np.zeros(len(a), dtype=bool)
     for f in fields:
         if a.dtype[f].kind == "f":

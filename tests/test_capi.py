@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 def test_struct_layout():
     assert C.sizeof(_ffi.Result) == 64
     assert snapgpu.RESULT_DTYPE.itemsize == 64
-    assert _ffi.lib().snapgpu_abi_version() == 1
+    assert _ffi.lib().snapgpu_abi_version() == 2
 
 
 def test_default_params_match_reference_defaults():

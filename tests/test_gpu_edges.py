@@ -68,3 +68,32 @@ def test_paired_read_past_max_read_size_is_a_status_code(gpu_available, small_wo
         pa.intersect(long0, ok1)
     got = pa.intersect(ok0, ok1)
     assert len(got) == 1
+
+
+def test_nul_bytes_are_flagged_not_silent(gpu_available, small_world):
+    """A read that reaches the device with 0x00 bytes (what a zero-fill racing an upload leaves behind)
+    is aligned as the reference would align it -- 0x00 is a non-ACGT base -- but its record carries
+    SNAPGPU_FLAG_NUL_BYTE (paired: SNAPGPU_PFLAG_NUL_BYTE), which every parity test asserts absent
+    (oracle_ffi.assert_no_corrupt_reads).  Clean reads of the same batch stay unflagged."""
+    from oracle_ffi import COMPARE_FIELDS, NUL_FLAG
+    idx, g = small_world["index"], small_world["genome"]
+    s = g.bases(5000, 1200).decode().upper()
+    t = g.bases(200_000, 300).decode().upper()
+    clean = [(s[:100], "I" * 100), (t[:100], "I" * 100)]
+    holed = [(s[:40] + "\0" + s[41:100], "I" * 100), ("\0" * 100, "I" * 100), (t[:99] + "\0", "I" * 100)]
+    reads = snapgpu.Reads.from_list(clean + holed)
+    al = snapgpu.BaseAligner(idx)
+    gpu = al.AlignReads(reads)
+    cpu = oracle_align(idx, reads, al.params)
+    for f in COMPARE_FIELDS:
+        x, y = gpu[f], cpu[f]
+        if x.dtype.kind == "f":
+            x, y = x.view(np.uint64), y.view(np.uint64)
+        assert np.array_equal(x, y), f
+    assert list((gpu["flags"] & NUL_FLAG) != 0) == [False, False, True, True, True]
+    assert al.timing()["nNulReads"] == 3 and al.timing()["nUnwritten"] == 0
+    r0 = snapgpu.Reads.from_list([clean[0], holed[0]])
+    r1 = snapgpu.Reads.from_list([(s[700:800], "I" * 100), (s[700:800], "I" * 100)])
+    got = snapgpu.PairedAligner(idx).intersect(r0, r1)
+    assert list((got["flags"] & snapgpu.PFLAG_NUL_BYTE) != 0) == [False, True]
+    assert list(got["writtenBy"]) == [1, 1]

@@ -50,6 +50,31 @@ def _cmp(got_rows, want_rows):
     return bad
 
 
+def _no_corrupt_reads(got):
+    """No pair may carry SNAPGPU_PFLAG_NUL_BYTE (a 0x00 byte reached the device: a corrupted upload)."""
+    nul = np.nonzero(got["flags"] & snapgpu.PFLAG_NUL_BYTE)[0]
+    assert len(nul) == 0, f"{len(nul)} pairs arrived on the device with 0x00 bytes, first {nul[:5]}"
+
+
+def _dump_failure(tag, got, bad, r0, r1):
+    """A failing comparison keeps its evidence: the differing pairs' rows, expected rows and routing
+    (the pass that wrote each record, its flags, both read lengths) in gpurun_out/failures/, which a
+    GPU run brings back."""
+    import json
+    d = os.path.join(os.path.dirname(HERE), "gpurun_out", "failures")
+    os.makedirs(d, exist_ok=True)
+    l0, l1 = r0.lengths(), r1.lengths()
+    rows = [{"pair": int(i), "got": g, "want": w, "writtenBy": int(got["writtenBy"][i]), "flags": int(got["flags"][i]),
+             "len0": int(l0[i]), "len1": int(l1[i])} for i, g, w in bad]
+    by = {}
+    for x in rows:
+        by[x["writtenBy"]] = by.get(x["writtenBy"], 0) + 1
+    with open(os.path.join(d, f"paired_{tag}.json"), "w") as f:
+        json.dump({"n_bad": len(bad), "by_pass": by,
+                   "pass_counts": {int(k): int(v) for k, v in zip(*np.unique(got["writtenBy"], return_counts=True))},
+                   "rows": rows}, f, indent=1)
+
+
 @pytest.mark.parametrize("run", list(PAIRED_RUNS))
 def test_oracle_paired_matches_reference(world, run):
     idx, r0, r1 = world
@@ -98,9 +123,11 @@ def test_gpu_intersecting_matches_reference_and_oracle(gpu_available, world, run
     idx, r0, r1 = world
     pa = _gpu_aligner(idx, run)
     got = pa.intersect(r0, r1)
+    _no_corrupt_reads(got)
     inter_want, _ = ref_paired_rows(os.path.join(G, f"expected_paired_{run}.tsv"))
     bad = _cmp(paired_tsv_rows(got, chimeric=False), inter_want)
     if bad:   # diagnosis only (the test fails either way): does the same aligner repeat the error?
+        _dump_failure(f"intersect_{run}", got, bad, r0, r1)
         again = _cmp(paired_tsv_rows(pa.intersect(r0, r1), chimeric=False), inter_want)
         fresh = _cmp(paired_tsv_rows(_gpu_aligner(idx, run).intersect(r0, r1), chimeric=False), inter_want)
         pytest.fail(f"{len(bad)} pairs differ from the reference, first {bad[:3]}; the same aligner's second "
@@ -126,7 +153,14 @@ def test_gpu_intersecting_independent_of_wave_history(gpu_available, world, grid
         monkeypatch.setenv("SNAPGPU_PAIRED_GRID", str(grid))
         few = _gpu_aligner(idx, run).intersect(r0, r1)
         monkeypatch.delenv("SNAPGPU_PAIRED_GRID")
+        _no_corrupt_reads(full)
+        _no_corrupt_reads(few)
         bad = _bitwise(few, full, fields)
+        if len(bad):
+            inter_want, _ = ref_paired_rows(os.path.join(G, f"expected_paired_{run}.tsv"))
+            for tag, got in (("full", full), ("few", few)):
+                _dump_failure(f"history_{grid}_{run}_{tag}", got,
+                              _cmp(paired_tsv_rows(got, chimeric=False), inter_want), r0, r1)
         assert len(bad) == 0, f"{run}: {len(bad)} pairs differ on {grid} waves, e.g. pair {bad[0]}"
 
 
@@ -141,7 +175,11 @@ def test_gpu_intersecting_first_call_of_fresh_aligners(gpu_available, world):
     for run in PAIRED_RUNS:
         inter_want, _ = ref_paired_rows(os.path.join(G, f"expected_paired_{run}.tsv"))
         for k in range(4):
-            bad = _cmp(paired_tsv_rows(_gpu_aligner(idx, run).intersect(r0, r1), chimeric=False), inter_want)
+            got = _gpu_aligner(idx, run).intersect(r0, r1)
+            _no_corrupt_reads(got)
+            bad = _cmp(paired_tsv_rows(got, chimeric=False), inter_want)
+            if bad:
+                _dump_failure(f"fresh_{run}_{k}", got, bad, r0, r1)
             assert not bad, f"{run}, fresh aligner {k}: {len(bad)} pairs differ, first {bad[:3]}"
 
 
@@ -151,8 +189,11 @@ def test_gpu_chimeric_matches_reference(gpu_available, world, run):
     idx, r0, r1 = world
     pa = _gpu_aligner(idx, run)
     got = pa.align(r0, r1)
+    _no_corrupt_reads(got)
     _, chim_want = ref_paired_rows(os.path.join(G, f"expected_paired_{run}.tsv"))
     bad = _cmp(paired_tsv_rows(got, chimeric=True), chim_want)
+    if bad:
+        _dump_failure(f"chimeric_{run}", got, bad, r0, r1)
     assert not bad, f"{len(bad)} pairs differ from the reference, first {bad[:3]}"
 
 
