@@ -571,8 +571,10 @@ typedef struct snapgpu_bucket_info {
 int snapgpu_aligner_bucket_info(const snapgpu_aligner_t *a, snapgpu_bucket_info_t *info);
 /* GenomeIndex::lookupSeed + fillInLookedUpResults (GenomeIndex.cpp:971-1086, unwindowed) of n seeds
  * (seedLen ACGT bases each, concatenated) on the device, through the bucket image: mode 0 = one lane
- * per seed (the lookup of seed_lookup_kernel and the paired kernel), 1 = the whole wave per seed (the
- * aligner's and CharacterizeSeeds' in-kernel lookups).  out[6 i ..]: hits forward, hits RC,
+ * per seed, each lane loading its whole line (bucket_lookup_lane: the paired kernel's lookup), 1 = the
+ * whole wave per seed (bucket_lookup_wave: the aligner's and CharacterizeSeeds' in-kernel lookups),
+ * 2 = one lane per seed, four lanes per line (bucket_lookup_quad: seed_lookup_kernel's lookup), run
+ * on waves with a scattered half of their lanes active.  out[6 i ..]: hits forward, hits RC,
  * hash of the forward hits, of the RC hits (acc = acc * 1000003 + hit, list order, mod 2^64),
  * first forward hit, first RC hit (~0 when none); lines[i] = bucket lines loaded. */
 int snapgpu_aligner_lookup_seeds(snapgpu_aligner_t *a, const char *seedBases, uint64_t n, int mode, uint64_t *out,

@@ -1345,7 +1345,8 @@ __global__ __launch_bounds__(256) void bucket_fill_kernel(const uint32_t *slots,
 
 // snapgpu_aligner_lookup_seeds: GenomeIndex::lookupSeed + fillInLookedUpResults (GenomeIndex.cpp:
 // 971-1086, unwindowed) of given seeds through the bucket image, by either device lookup: lane per
-// seed (bucket_lookup_lane, mode 0) or the whole wave per seed (bucket_lookup_wave, mode 1).  Per
+// seed (bucket_lookup_lane, mode 0; bucket_lookup_quad, mode 2) or the whole wave per seed
+// (bucket_lookup_wave, mode 1).  Per
 // seed: {nFwd, nRc, hash of the forward hits, of the RC hits, first forward hit, first RC hit}, the
 // hash acc = acc * 1000003 + hit over the hits in list order; `lines` = bucket lines loaded.
 __device__ __forceinline__ void lookup_fill(const KArgs &A, uint32_t v, uint32_t c, uint64_t *o) {
@@ -1366,21 +1367,30 @@ __global__ __launch_bounds__(64) void lookup_seeds_kernel(KArgs A, const char *s
     const uint32_t L = A.seedLen;
     for (uint32_t base = blockIdx.x * 64u; base < n; base += gridDim.x * 64u) {
         const uint32_t cnt = n - base < 64u ? n - base : 64u;
-        for (uint32_t k = 0; k < (mode ? cnt : 1u); k++) {
-            const uint32_t i = mode ? base + k : base + lane;   // mode 1: seed base+k, uniform
-            if (!mode && (uint32_t)lane >= cnt) break;
+        // mode 0 / 2: lane per seed; mode 2 (bucket_lookup_quad, seed_lookup_kernel's lookup) runs in
+        // two rounds, each with a scattered half of the wave's lanes active (and the tail block's
+        // lanes past n inactive in both), so partially active waves are what it is checked on
+        const uint32_t rounds = mode == 1 ? cnt : (mode == 2 ? 2u : 1u);
+        for (uint32_t k = 0; k < rounds; k++) {
+            const uint32_t i = mode == 1 ? base + k : base + lane;   // mode 1: seed base+k, uniform
+            bool act = mode == 1 || (uint32_t)lane < cnt;
+            if (mode == 2) act = act && ((fmix32(i) & 1u) == k);
+            if (mode == 0 && !act) break;
             uint64_t f = 0, rc = 0;
-            for (uint32_t j = 0; j < L; j++) {
-                const int v = base_value((uint8_t)seeds[(uint64_t)i * L + j]) & 3;
-                f |= (uint64_t)v << ((L - j - 1) * 2);
-                rc |= (uint64_t)(v ^ 3) << (j * 2);
-            }
+            if (act)
+                for (uint32_t j = 0; j < L; j++) {
+                    const int v = base_value((uint8_t)seeds[(uint64_t)i * L + j]) & 3;
+                    f |= (uint64_t)v << ((L - j - 1) * 2);
+                    rc |= (uint64_t)(v ^ 3) << (j * 2);
+                }
             const bool comp = (int64_t)f > (int64_t)rc;
             const uint64_t canon = comp ? rc : f;
             uint32_t v1 = 0, v2 = 0, aux = 0, ln = 0;
-            const bool found = mode ? bucket_lookup_wave(A, (uint32_t)(canon >> 32), (uint32_t)canon, lane, v1, v2, aux, ln)
-                                    : bucket_lookup_lane(A, (uint32_t)(canon >> 32), (uint32_t)canon, v1, v2, aux, ln);
-            if (mode && lane != 0) continue;
+            bool found;
+            if (mode == 1) found = bucket_lookup_wave(A, (uint32_t)(canon >> 32), (uint32_t)canon, lane, v1, v2, aux, ln);
+            else if (mode == 2) found = bucket_lookup_quad(A, act, (uint32_t)(canon >> 32), (uint32_t)canon, v1, v2, aux, ln);
+            else found = bucket_lookup_lane(A, (uint32_t)(canon >> 32), (uint32_t)canon, v1, v2, aux, ln);
+            if ((mode == 1 && lane != 0) || !act) continue;
             uint64_t o[6] = {0, 0, 0, 0, ~0ull, ~0ull};
             if (found) {
                 const uint32_t c1 = aux & BK_CSAT, c2 = (aux >> 15) & BK_CSAT;
@@ -2842,13 +2852,15 @@ int snapgpu_cigar_last_ms(snapgpu_aligner_t *a, double *ms) {
 int snapgpu_cigar_batch(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, const uint32_t *locations,
                         const uint8_t *directions, int useM, int32_t *editDistance, uint32_t *nOps, uint32_t *ops) {
     if (!a || !reads || !locations || !directions || !editDistance || !nOps || !ops) return SNAPGPU_EINVAL;
-    return snapgpu_internal_cigar_view(a, reads->bases, reads->offsets, reads->lengths, reads->n, locations, directions,
+    const char *const base[2] = {reads->bases, reads->bases};
+    return snapgpu_internal_cigar_view(a, base, nullptr, reads->offsets, reads->lengths, reads->n, locations, directions,
                                        useM, editDistance, nOps, ops);
 }
 
-// snapgpu_cigar_batch over read i = bases[offsets[i] .. + lengths[i]) of any buffer (the product
-// paths pass both ends of a pair batch at once, offsets from a common base), without a batch copy
-int snapgpu_internal_cigar_view(snapgpu_aligner_t *a, const char *bases, const uint64_t *offsets, const uint32_t *lengths,
+// snapgpu_cigar_batch over read i = base[mate[i]][offsets[i] .. + lengths[i]) (the product paths pass
+// both ends of a pair batch at once: two buffers, each row tagged with its end), without a batch copy
+int snapgpu_internal_cigar_view(snapgpu_aligner_t *a, const char *const base[2], const uint8_t *mate,
+                                const uint64_t *offsets, const uint32_t *lengths,
                                 uint64_t n, const uint32_t *locations, const uint8_t *directions, int useM,
                                 int32_t *editDistance, uint32_t *nOps, uint32_t *ops) {
     if (a->failed) { snapgpu::setError("aligner failed earlier (device timeout)"); return SNAPGPU_EDEVICE; }
@@ -2904,7 +2916,7 @@ int snapgpu_internal_cigar_view(snapgpu_aligner_t *a, const char *bases, const u
         // pack the bases (several threads for big batches: the copy is the host's part of the call)
         const unsigned nt = n < 16384 ? 1u : std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
         auto pack = [&](uint64_t b, uint64_t e) {
-            for (uint64_t i = b; i < e; i++) memcpy(h + oBases + hOff[i], bases + offsets[i], lengths[i]);
+            for (uint64_t i = b; i < e; i++) memcpy(h + oBases + hOff[i], base[mate ? mate[i] & 1 : 0] + offsets[i], lengths[i]);
         };
         std::vector<std::thread> th;
         for (unsigned t = 1; t < nt; t++) th.emplace_back(pack, n * t / nt, n * (t + 1) / nt);
@@ -2945,7 +2957,7 @@ int snapgpu_internal_cigar_view(snapgpu_aligner_t *a, const char *bases, const u
 
 int snapgpu_aligner_lookup_seeds(snapgpu_aligner_t *a, const char *seedBases, uint64_t n, int mode, uint64_t *out,
                                  uint32_t *lines) {
-    if (!a || (n && (!seedBases || !out || !lines)) || mode < 0 || mode > 1) return SNAPGPU_EINVAL;
+    if (!a || (n && (!seedBases || !out || !lines)) || mode < 0 || mode > 2) return SNAPGPU_EINVAL;
     if (n == 0) return SNAPGPU_OK;
     if (n >= (1ull << 31)) { snapgpu::setError("lookup_seeds: too many seeds"); return SNAPGPU_EINVAL; }
     if (a->failed) return SNAPGPU_EDEVICE;

@@ -150,8 +150,10 @@ struct GtfPairQuery {
 int contaminantsAddAll(snapgpu_contaminants_t *c, const std::vector<uint32_t> &locations, bool apply = true);
 
 }  // namespace snapgpu
-// aligner.hip: snapgpu_cigar_batch over reads bases[offsets[i] .. + lengths[i]) (no batch copy)
-extern "C" int snapgpu_internal_cigar_view(snapgpu_aligner_t *a, const char *bases, const uint64_t *offsets,
+// aligner.hip: snapgpu_cigar_batch over reads base[mate[i]][offsets[i] .. + lengths[i]) (no batch copy);
+// two base buffers (the two ends of a pair batch, separate allocations), mate == nullptr: all base[0]
+extern "C" int snapgpu_internal_cigar_view(snapgpu_aligner_t *a, const char *const base[2], const uint8_t *mate,
+                                           const uint64_t *offsets,
                                            const uint32_t *lengths, uint64_t n, const uint32_t *locations,
                                            const uint8_t *directions, int useM, int32_t *editDistance, uint32_t *nOps,
                                            uint32_t *ops);

@@ -610,12 +610,14 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
     // go to the GPU, as compact batches (a read without one has no CIGAR: edit distance -1, no
     // ops); the genome (ga) and transcriptome (ta) batches run on two host threads.
     t0 = std::chrono::steady_clock::now();
-    // Both ends of the sub-batch in one set per aligner, one GPU call each: a read's bytes are
-    // addressed from the lower of the two ends' buffers (no copy of the batch).
-    const char *cbase = std::min(R[0]->bases, R[1]->bases);
+    // Both ends of the sub-batch in one set per aligner, one GPU call each: a row is addressed by
+    // its end's buffer and its offset there (no copy of the batch, no pointer arithmetic across the
+    // two allocations).
+    const char *const cbase[2] = {R[0]->bases, R[1]->bases};
     struct CigarSet {
         std::vector<int64_t> slot[2];   // end k, record -> row in ed/nOps/ops, -1: no location
-        std::vector<uint64_t> off;      // from cbase
+        std::vector<uint64_t> off;      // in the row's end's buffer
+        std::vector<uint8_t> mate;      // the row's end
         std::vector<uint32_t> len, loc, nOps;
         std::unique_ptr<uint32_t[]> ops;   // [rows][SNAPGPU_CIGAR_MAX_OPS], every row written by the download
         std::vector<uint8_t> dir;
@@ -629,19 +631,20 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
         void add(int k, uint64_t i, uint64_t o, uint32_t ln, uint32_t l, uint8_t d) {
             slot[k][i] = (int64_t)loc.size();
             off.push_back(o);
+            mate.push_back((uint8_t)k);
             len.push_back(ln);
             loc.push_back(l);
             dir.push_back(d);
         }
         uint64_t rows() const { return loc.size(); }
-        int run(snapgpu_aligner_t *a, const char *base, int useM, std::mutex &m) {
+        int run(snapgpu_aligner_t *a, const char *const base[2], int useM, std::mutex &m) {
             const uint64_t cnt = loc.size();
             ed.assign(cnt + 1, -1);
             nOps.assign(cnt + 1, 0);
             ops.reset(new uint32_t[(cnt + 1) * SNAPGPU_CIGAR_MAX_OPS]);
             if (!cnt) return SNAPGPU_OK;
             std::lock_guard<std::mutex> lk(m);
-            return snapgpu_internal_cigar_view(a, base, off.data(), len.data(), cnt, loc.data(), dir.data(), useM, ed.data(),
+            return snapgpu_internal_cigar_view(a, base, mate.data(), off.data(), len.data(), cnt, loc.data(), dir.data(), useM, ed.data(),
                                                nOps.data(), ops.get());
         }
     };
@@ -651,14 +654,13 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
         isT[k].assign(nb, 0);
         gc.slot[k].assign(nb, -1);
         tc.slot[k].assign(nb, -1);
-        const uint64_t shift = (uint64_t)(R[k]->bases - cbase);
         for (uint64_t q = 0; q < nb; q++) {
             const PairOut &r = X.po[q];
             const uint64_t i = X.a + q;
             const uint32_t loc = r.status[k] != SNAPGPU_NOT_FOUND ? r.location[k] : kInvalidLocation;
             const bool t = loc != kInvalidLocation && r.isTranscriptome[k];
             isT[k][q] = t;
-            const uint64_t o = shift + R[k]->offsets[i];
+            const uint64_t o = R[k]->offsets[i];
             if (t) tc.add(k, q, o, R[k]->lengths[i], r.tlocation[k], (uint8_t)r.direction[k]);
             else if (loc != kInvalidLocation) gc.add(k, q, o, R[k]->lengths[i], loc, (uint8_t)r.direction[k]);
         }

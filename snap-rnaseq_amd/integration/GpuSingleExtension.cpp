@@ -1,5 +1,6 @@
 // GpuSingleExtension.cpp -- see GpuSingleExtension.h.  C++98, SNAPLib headers.
 #include "GpuSingleExtension.h"
+#include "multihit_copy.h"
 
 #include "AlignmentFilter.h"
 #include "GenomeIndex.h"
@@ -120,12 +121,9 @@ void GpuBaseAligner::AlignReadsMultiHit(Read **reads, unsigned n, unsigned maxHi
         hitDirections[i] = (Direction)o[i].direction;
         if (finalScores != NULL) finalScores[i] = o[i].score;
         if (mapqs != NULL) mapqs[i] = o[i].mapq;
-        for (int j = 0; j < multiHitsFound[i]; j++) {
-            const snapgpu_multi_hit_t &m = h[(size_t)i * maxHitsToGet + j];
-            multiHitLocations[(size_t)i * maxHitsToGet + j] = m.location;
-            multiHitRCs[(size_t)i * maxHitsToGet + j] = m.direction != 0;
-            multiHitScores[(size_t)i * maxHitsToGet + j] = m.score;
-        }
+        // nothing when maxHitsToGet == 0 (multiHitsFound is then not written), else at most a row
+        gpuCopyMultiHits(&h[0], i, maxHitsToGet, maxHitsToGet ? multiHitsFound[i] : 0, multiHitLocations,
+                         multiHitRCs, multiHitScores);
     }
 }
 

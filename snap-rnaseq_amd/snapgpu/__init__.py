@@ -422,7 +422,7 @@ class BaseAligner:
 
     def lookup_seeds(self, seeds, mode=0):
         """GenomeIndex::lookupSeed of ACGT seeds on the device, through the bucket image
-        (snapgpu_aligner_lookup_seeds; mode 0 = lane per seed, 1 = wave per seed).
+        (snapgpu_aligner_lookup_seeds; mode 0 = lane per seed, 1 = wave per seed, 2 = four lanes per line).
         -> (uint64[n, 6] {nFwd, nRc, hashFwd, hashRc, firstFwd, firstRc}, uint32[n] lines)."""
         seeds = [s.encode() if isinstance(s, str) else bytes(s) for s in seeds]
         n = len(seeds)

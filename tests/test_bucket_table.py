@@ -65,7 +65,7 @@ def _seed_set(g, seed_len, n_present, n_random, seed=5):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("mode", [0, 1, 2])
 def test_gpu_lookups_match_reference_fixture(gpu_available, mode):
     idx = snapgpu.GenomeIndex.build(snapgpu.Genome.from_fasta(os.path.join(G, "small.fa"), 500), 20, 4)
     al = snapgpu.BaseAligner(idx)
@@ -86,7 +86,7 @@ def test_gpu_lookups_on_reference_built_index(gpu_available, tmp_path):
     al = snapgpu.BaseAligner(idx)
     seeds = open(os.path.join(G, "lookup_seeds.txt")).read().split()
     want = open(os.path.join(G, "expected_lookups.tsv")).read().splitlines()
-    for mode in (0, 1):
+    for mode in (0, 1, 2):
         got = _fixture_rows(al.lookup_seeds(seeds, mode=mode)[0])
         assert got == want, mode
     bi = al.bucket_info()
@@ -103,7 +103,7 @@ def test_gpu_lookups_match_host(gpu_available, small_world, seed_len):
     al = snapgpu.BaseAligner(idx)
     seeds = _seed_set(g, seed_len, 6000, 3000)
     want = _host_rows(idx, seeds)
-    for mode in (0, 1):
+    for mode in (0, 1, 2):
         out, lines = al.lookup_seeds(seeds, mode=mode)
         got = _fixture_rows(out)
         bad = [i for i in range(len(seeds)) if got[i] != want[i]]
@@ -111,7 +111,7 @@ def test_gpu_lookups_match_host(gpu_available, small_world, seed_len):
         if mode == 0:
             lines0 = lines
         else:
-            assert np.array_equal(lines, lines0)   # both forms count the buckets a sequential lookup loads
+            assert np.array_equal(lines, lines0)   # every form counts the buckets a sequential lookup loads
     assert max(int(w.split("\t")[0]) for w in want) > 1   # overflow lists are in the set
     bi = al.bucket_info()
     info = idx.info()
@@ -136,7 +136,7 @@ def test_gpu_lookups_saturated_counts(gpu_available, tmp_path):
     seeds = [(b"AACGT" * 5)[k:k + 20].decode() for k in range(5)] + _seed_set(gb, 20, 500, 200)
     want = _host_rows(idx, seeds)
     assert max(int(w.split("\t")[0]) for w in want[:5]) > 0x7fff
-    for mode in (0, 1):
+    for mode in (0, 1, 2):
         assert _fixture_rows(al.lookup_seeds(seeds, mode=mode)[0]) == want, mode
 
 

@@ -123,6 +123,19 @@ def test_plain_c_caller(tmp_path):
     assert "ok 1" in out.stdout
 
 
+def test_multihit_copy_out_is_clamped(tmp_path):
+    """ADVICE r4: GpuBaseAligner::AlignReadsMultiHit copies nothing when maxHitsToGet == 0 (the
+    count array is then not written, by the library or the reference) and at most maxHitsToGet hits
+    per read otherwise (snap-rnaseq_amd/integration/multihit_copy.h, tests/c/multihit_copy_test.cpp)."""
+    import subprocess
+    exe = tmp_path / "multihit_copy_test"
+    subprocess.run(["g++", "-std=gnu++98", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    "-I", os.path.join(ROOT, "snap-rnaseq_amd", "integration"),
+                    os.path.join(ROOT, "tests", "c", "multihit_copy_test.cpp"), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0 and "multihit_copy: ok" in out.stdout, out.stdout + out.stderr
+
+
 def _clip_reads():
     """Reads with '#' runs at both ends (clipped), one whose clip would leave < 50 bases
     (kept whole, Read.h:393-397) and one without '#'."""
