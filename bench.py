@@ -52,32 +52,25 @@ WORKLOADS = {
 }
 
 
-def algorithmic_bytes(res):
-    """B_read = 2*readLen + 16 + 64*P + 4*(H + V) + (readLen + MAX_K)*S, P = 64-B bucket
-    lines of the seed tables' device image (csrc/bucket_table.h) the read's lookups loaded (the reference's
-    12-B slot probes before round 4: the line is now the unit a lookup reads)."""
-    P = res["nProbes"].astype(np.int64).sum()
+def algorithmic_bytes(res, ref_probes=None):
+    """B_read = 2*readLen + 16 + 12*P + 4*(H + V) + (readLen + MAX_K)*S, in the reference's
+    units: P = SNAPHashTable slot probes (12-B entries), which the oracle counts on the same reads
+    (`ref_probes`, its records' nProbes; the device counts 64-B bucket lines instead, which only
+    granule_bytes prices), a byte genome window per LV-scored candidate.  Without an oracle run P falls back
+    to the device's line count at 12 B each (marked in the returned units).  Also returns the same formula
+    on the device's own layout: 3-bit genome planes, ceil((readLen + MAX_K) * 3 / 8) bytes per window."""
     H = res["nHitWords"].astype(np.int64).sum()
     V = res["nOverflowLists"].astype(np.int64).sum()
     S = res["nLocationsScored"].astype(np.int64).sum()
     n = len(res)
-    return int(n * (2 * READ_LEN + 16) + 64 * P + 4 * (H + V) + (READ_LEN + MAX_K) * S), dict(
-        P=P / n, H=H / n, V=V / n, S=S / n)
-
-
-def granule_bytes(res):
-    """SURVEY.md 8(d) d3, granule-adjusted: every random access moves whole 64-B lines -- the read's
-    bases and qualities, its record, one line per bucket line probed, per overflow list
-    ceil(4 H / 64) hit lines (the list length travels in the bucket entry), and per LV-scored candidate the genome window's lines
-    (64 * ceil((readLen + MAX_K) / 64), the byte genome of the reference's layout)."""
-    P = res["nProbes"].astype(np.int64)
-    H = res["nHitWords"].astype(np.int64)
-    V = res["nOverflowLists"].astype(np.int64)
-    S = res["nLocationsScored"].astype(np.int64)
-    line = 64
-    per_read = (2 * line * -(-READ_LEN // line) + line + line * P + line * ((4 * H + line - 1) // line) +
-                line * -(-(READ_LEN + MAX_K) // line) * S)
-    return int(per_read.sum())
+    if ref_probes is not None:
+        P, p_unit = int(np.asarray(ref_probes, dtype=np.int64).sum()), "reference slot probes (oracle, same reads)"
+    else:
+        P, p_unit = int(res["nProbes"].astype(np.int64).sum()), "device bucket lines (no oracle run: P unpinned)"
+    base = n * (2 * READ_LEN + 16) + 12 * P + 4 * (H + V)
+    byte_genome = int(base + (READ_LEN + MAX_K) * S)
+    planes = int(base + -(-(READ_LEN + MAX_K) * 3 // 8) * S)
+    return byte_genome, dict(P=P / n, H=H / n, V=V / n, S=S / n), planes, p_unit
 
 
 def lib_sha256():
@@ -118,19 +111,53 @@ def load_pmc(sha, src_sha):
     return d, d.get("source")
 
 
-def valu_cycles():
-    """SIMD cycles one wave64 VALU instruction of align_kernel<128>'s mix occupies at 4 waves/SIMD, from the
-    measured op kinds (profiles/r03/valu_rates.json, tools/gpu/valu_rates.hip): (median, mean, source), or the
-    guide's 2 cycles for both.  Both are reported: the back-to-back v_cndmask_b32 (vcc) chain costs 12.7
-    cycles (a vcc read-after-write stall on every instruction), which the kernel never issues -- its vcc
-    selects follow a v_cmp, measured at 2.66 -- and alone lifts the mean (3.62) above the median (3.13)."""
-    p = os.path.join(ROOT, "profiles", "r03", "valu_rates.json")
+def issue_rates():
+    """Issue capacity of the CU's pipes, measured by tools/gpu/issue_rates.hip (profiles/r05/issue_rates.json):
+    shader cycles per wave64 VALU instruction per SIMD and per SALU instruction per CU once enough waves issue,
+    at the occupancy the aligner runs (20 waves per CU).  Without the file: the guide's 2 cycles per wave64
+    VALU on a SIMD-32 (MI355X_MICROARCH.md "Wave scheduling") and one SALU per cycle per CU (marked)."""
+    p = os.path.join(ROOT, "profiles", "r05", "issue_rates.json")
     if os.path.exists(p):
         d = json.load(open(p))
-        xs = [r["w4"]["cycles_per_instr_per_simd"] for r in d["rates"] if not r["instruction"].startswith("v_readlane")]
-        if xs:
-            return float(np.median(xs)), float(np.mean(xs)), f"profiles/r03/valu_rates.json ({len(xs)} op kinds at 4 waves/SIMD)"
-    return 2.0, 2.0, "MI355X_MICROARCH.md: wave64 on a 32-lane SIMD"
+        rate = {r["instruction"]: r for r in d["rates"]}
+        key = "wpc20"
+        v = rate["v_add_u32"][key]["cycles_per_instr_per_cu"] * 4   # per SIMD: 4 SIMDs per CU
+        sc = rate["s_add_u32"][key]["cycles_per_instr_per_cu"]
+        br = rate["s_cmp_eq_u32 + s_cbranch_scc1 (not taken)"][key]["cycles_per_instr_per_cu"]
+        return {"valu_cycles_per_simd": v, "salu_cycles_per_cu": sc, "branch_pair_cycles_per_cu": br,
+                "source": "profiles/r05/issue_rates.json (tools/gpu/issue_rates.hip, 20 waves per CU)"}
+    return {"valu_cycles_per_simd": 2.0, "salu_cycles_per_cu": 1.0, "branch_pair_cycles_per_cu": None,
+            "source": "MI355X_MICROARCH.md (2 cycles per wave64 VALU); SALU rate unmeasured"}
+
+
+def issue_roofline(pmc, reads_launch, kms_launch, n_cu):
+    """Instruction-issue roofline of align_kernel<128> (verdict r4 item 3): the PMC instruction counts per read
+    of this build (SQ_INSTS_*, exact counts) against what the SIMDs can issue in the measured kernel time.
+      valu_pipe_busy   VALU instructions x cycles per wave64 VALU / SIMD-cycles available
+      salu_busy        SALU instructions x cycles per SALU per CU / CU-cycles available (the scalar pipe's
+                       scope -- per CU or per SIMD -- is what issue_rates.hip measures)
+      issue_frac       every instruction (VALU, SALU, branch, LDS, VMEM, SMEM) at one issue slot per SIMD-cycle
+    SQ_ACTIVE/WAIT counters are quad-cycles (MI355X_MICROARCH.md): the wave-state shares are ratios of them."""
+    if not pmc or not pmc.get("valu_insts_per_read") or not n_cu:
+        return None
+    rates = issue_rates()
+    clk = 2.4e9
+    simd_cyc = 4 * n_cu * clk * (kms_launch / 1000.0) / reads_launch   # SIMD-cycles per read
+    cu_cyc = simd_cyc / 4
+    ins = {k: pmc.get(f"{k}_insts_per_read") for k in ("valu", "salu", "branch", "lds", "vmem", "smem")}
+    total = sum(v for v in ins.values() if v)
+    valu = ins["valu"] * rates["valu_cycles_per_simd"] / simd_cyc
+    salu = ins["salu"] * rates["salu_cycles_per_cu"] / cu_cyc if ins["salu"] else None
+    out = {"insts_per_read": {k: (round(v, 1) if v else v) for k, v in ins.items()}, "insts_total_per_read": round(total, 1),
+           "simd_cycles_per_read": simd_cyc, "clock_ghz": 2.4, "simds": 4 * n_cu,
+           "valu_pipe_busy": valu, "salu_busy": salu, "issue_frac": total / simd_cyc,
+           "valu_pipe_busy_guide_2cyc": ins["valu"] * 2.0 / simd_cyc,
+           "rates": rates, "wave_state": pmc.get("wave_state"), "source": pmc.get("source")}
+    wc = pmc.get("wave_cycles_per_read")
+    if wc:
+        out["wave_cycles_per_read"] = wc
+        out["waves_per_simd_effective"] = wc / simd_cyc
+    return out
 
 
 def cpu_info():
@@ -587,78 +614,9 @@ def main():
 
     result = None
     if rank == 0:
-        sha = lib_sha256()
-        src_sha = kernel_source_sha256()
-        bytes_all, per_read = algorithmic_bytes(res)
-        n_launch = float(np.mean(launches))
-        bytes_launch = bytes_all / n_launch
-        # the two lanes' launches overlap (one fills the other's tail): a launch's own HIP-event
-        # duration (= rocprof's per-dispatch duration) double-counts the shared time, so the
-        # roofline uses the align kernel's GPU-busy time per step (union of the launch intervals)
-        kms_launch_own = float(np.sum(kernel_ms)) / float(np.sum(launches))
-        busy_step = float(np.mean(busy_ms))
-        kms_launch = busy_step / n_launch
-        achieved = bytes_launch / (kms_launch / 1000.0) / 1e9
-        pmc, pmc_src = load_pmc(sha, src_sha)
-        reads_launch = wl["reads"] / n_launch
-        traffic = None
-        valu_issue = None
-        if pmc:
-            traffic = pmc["hbm_bytes_per_read"] * reads_launch
-            n_cu = snapgpu.device_cu_count(local)
-            if pmc.get("valu_insts_per_read") and n_cu:
-                v = pmc["valu_insts_per_read"] * reads_launch
-                # gfx950 SIMDs are 32 lanes wide: a wave64 VALU op holds the SIMD for 2 cycles once two
-                # or more waves issue (MI355X_MICROARCH.md "Wave scheduling"); the measured issue cost of
-                # the kernel's dominant op kinds at its 4 waves/SIMD (tools/gpu/valu_rates.hip) when
-                # committed, 4 SIMDs per CU at 2.4 GHz
-                cyc, cyc_mean, cyc_src = valu_cycles()
-                simd_cycles = 4 * n_cu * (kms_launch / 1000.0) * 2.4e9
-                valu_issue = {"valu_insts_per_launch": v, "simds": 4 * n_cu, "clock_ghz": 2.4,
-                              "cycles_per_valu_median": cyc, "cycles_per_valu_mean": cyc_mean, "cycles_source": cyc_src,
-                              "pipe_occupancy": v * cyc / simd_cycles,
-                              "pipe_occupancy_mean_priced": v * cyc_mean / simd_cycles,
-                              "pipe_occupancy_guide_2cyc": v * 2.0 / simd_cycles,
-                              # the occupancy sweep's reading: the same binary at 2
-                              # waves/SIMD is only 5 % slower than at 4, what a 4-cycle VALU pipe predicts
-                              "pipe_occupancy_4cyc": v * 4.0 / simd_cycles,
-                              "occupancy_sweep": "profiles/r04/ab/occupancy_r04j.txt",
-                              "wave_state": pmc.get("wave_state"),
-                              "source": pmc_src}
-        ws = (valu_issue or {}).get("wave_state") or {}
-        if ws:   # the measured split of the waves' time (rocprofv3 SQ counters of this build)
-            binding = (f"VALU instruction issue: the VALU pipe is {valu_issue['pipe_occupancy_4cyc']:.2f} busy at 4 cycles "
-                       f"per wave64 instruction ({valu_issue['pipe_occupancy']:.2f} at the microbenchmark's median "
-                       f"{valu_issue['cycles_per_valu_median']:.2f} cycles, {valu_issue['pipe_occupancy_guide_2cyc']:.2f} at 2); "
-                       "the same binary at 2 waves/SIMD is only 5 % slower than at 4 and 3.5 % faster at 5 "
-                       "(occupancy_r04j.txt, occupancy5_r04s.txt): mostly issue bound, a latency share a fifth "
-                       f"wave still hides; waves spend {ws['SQ_WAIT_ANY']:.0%} of their time "
-                       f"waiting on memory counters, {ws['SQ_WAIT_INST_ANY']:.0%} for dependencies, "
-                       f"{ws['SQ_ACTIVE_INST_ANY']:.0%} issuing -- not HBM bandwidth (DESIGN.md section 4)")
-        else:
-            binding = ("VALU instruction issue (the occupancy sweep of DESIGN.md section 4), not HBM bandwidth "
-                       "(no PMC data of this build)")
-        roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                    "kernel": "align_kernel<128, false>", "kernel_ms_per_launch": kms_launch,
-                    "kernel_busy_ms_per_step": busy_step,
-                    "launch_duration_ms": kms_launch_own,
-                    "achieved_on_launch_durations": bytes_launch / (kms_launch_own / 1000.0) / 1e9,
-                    "timing_note": "kernel_ms_per_launch = union of the step's align-kernel launch intervals / "
-                                   "launches (HIP events); launch_duration_ms = mean of each launch's own "
-                                   "interval (what rocprofv3 reports per dispatch; launches of the two "
-                                   "streams overlap)",
-                    "granule_adjusted": {"bytes_per_read": granule_bytes(res) / len(res),
-                                         "achieved": granule_bytes(res) / n_launch / (kms_launch / 1000.0) / 1e9,
-                                         "frac": granule_bytes(res) / n_launch / (kms_launch / 1000.0) / 1e9 / HBM_PEAK_GBS,
-                                         "note": "64-B lines per random access (SURVEY 8(d) d3)"},
-                    "launches_per_step": n_launch, "reads_per_launch": reads_launch,
-                    "algorithmic_bytes_per_launch": bytes_launch, "algorithmic_bytes_per_read": bytes_all / len(res),
-                    "binding_resource": binding,
-                    "valu_issue": valu_issue, "pmc_source": pmc_src, "lib_sha256": sha,
-                    "kernel_source_sha256": src_sha}
         counts = {int(k): int(v) for k, v in zip(*np.unique(res["result"], return_counts=True))}
         extras = {}
+        copy_peak_gbs = None
         if not args.no_extras:
             # device-resident rate: the same pass sets without the copies or the host tail
             dev = aligner.upload(reads)
@@ -716,7 +674,7 @@ def main():
             copy_gbs = 2 * c_bytes / (c_ms / 1000.0) / 1e9
             extras["copy_peak"] = {"GBps": copy_gbs, "ms": c_ms, "bytes_moved": 2 * c_bytes,
                                    "note": "copy_peak_kernel, 16-B loads + stores, best of 3"}
-            roofline["frac_of_measured_copy_peak"] = achieved / copy_gbs
+            copy_peak_gbs = copy_gbs
             lookup["frac_of_measured_copy_peak"] = lookup["achieved"] / copy_gbs
             extras["lookup_roofline"] = lookup
             # SAM records: GPU CIGARs of the resident records, then host SAM lines
@@ -779,6 +737,73 @@ def main():
                 want = oracle_cigars(idx, [reads.get(i)[0] for i in range(nc)], loc, dirs, 0)
                 extras["sam_records"]["parity"] = {"reads_compared": nc, "mismatches": sum(
                     1 for i in range(nc) if (int(cig.editDistance[i]), cig.string(i)) != want[i])}
+        # ---- roofline of the dominant kernel (after the CPU leg: its oracle run counts the reference's
+        # own slot probes on these reads, the P of the algorithmic bytes)
+        sha = lib_sha256()
+        src_sha = kernel_source_sha256()
+        ref_probes = cres["nProbes"] if cpu is not None and len(cres) == len(res) else None
+        bytes_all, per_read, bytes_planes, p_unit = algorithmic_bytes(res, ref_probes)
+        n_launch = float(np.mean(launches))
+        bytes_launch = bytes_all / n_launch
+        # the two lanes' launches overlap (one fills the other's tail): a launch's own HIP-event
+        # duration (= rocprof's per-dispatch duration) double-counts the shared time, so the
+        # roofline uses the align kernel's GPU-busy time per step (union of the launch intervals)
+        kms_launch_own = float(np.sum(kernel_ms)) / float(np.sum(launches))
+        busy_step = float(np.mean(busy_ms))
+        kms_launch = busy_step / n_launch
+        achieved = bytes_launch / (kms_launch / 1000.0) / 1e9
+        pmc, pmc_src = load_pmc(sha, src_sha)
+        reads_launch = wl["reads"] / n_launch
+        traffic = pmc["hbm_bytes_per_read"] * reads_launch if pmc else None
+        issue = issue_roofline(pmc, reads_launch, kms_launch, snapgpu.device_cu_count(local))
+        if issue:
+            ws = issue.get("wave_state") or {}
+            binding = (f"instruction issue and dependent latency, not HBM (frac below) and not MFMA (no matrix work): "
+                       f"{issue['insts_total_per_read']:.0f} instructions per read ({issue['insts_per_read']['valu']:.0f} VALU, "
+                       f"{issue['insts_per_read']['salu']:.0f} SALU, {issue['insts_per_read']['branch']:.0f} branch) fill "
+                       f"{issue['issue_frac']:.2f} of the SIMDs' issue slots (one per SIMD-cycle); the VALU pipe is "
+                       f"{issue['valu_pipe_busy']:.2f} busy at {issue['rates']['valu_cycles_per_simd']:.2f} cycles per wave64 "
+                       f"instruction, the scalar pipe {issue['salu_busy']:.2f} at {issue['rates']['salu_cycles_per_cu']:.2f} "
+                       f"cycles per SALU per CU ({issue['rates']['source']}); waves spend "
+                       f"{ws.get('SQ_WAIT_ANY', 0):.0%} of their time waiting on memory counters, "
+                       f"{ws.get('SQ_WAIT_INST_ANY', 0):.0%} on dependencies, {ws.get('SQ_ACTIVE_INST_ANY', 0):.0%} issuing "
+                       "(DESIGN.md section 4)")
+        else:
+            binding = ("instruction issue and dependent latency (DESIGN.md section 4), not HBM bandwidth (no PMC data of "
+                       "this build: " + str(pmc_src) + ")")
+        granule = granule_bytes(res)
+        roofline = {"bound": "issue", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                    "bound_note": "the kernel is bound by neither HBM nor MFMA: `bound` names what binds "
+                                  "(binding_resource, issue_roofline); achieved / peak / frac / traffic are the "
+                                  "contract's HBM roofline of the same launches",
+                    "issue_roofline": issue,
+                    "kernel": "align_kernel<128, false>", "kernel_ms_per_launch": kms_launch,
+                    "kernel_busy_ms_per_step": busy_step,
+                    "launch_duration_ms": kms_launch_own,
+                    "achieved_on_launch_durations": bytes_launch / (kms_launch_own / 1000.0) / 1e9,
+                    "timing_note": "kernel_ms_per_launch = union of the step's align-kernel launch intervals / "
+                                   "launches (HIP events); launch_duration_ms = mean of each launch's own "
+                                   "interval (what rocprofv3 reports per dispatch; launches of the two "
+                                   "streams overlap)",
+                    "algorithmic_bytes_note": "SURVEY 8(d) d3 in the reference's units: P = " + p_unit +
+                                              " at 12 B, a byte-genome window of readLen + MAX_K bytes per scored "
+                                              "candidate (round 4 charged 64 B per device bucket line instead)",
+                    "plane_layout": {"bytes_per_read": bytes_planes / len(res),
+                                     "achieved": bytes_planes / n_launch / (kms_launch / 1000.0) / 1e9,
+                                     "frac": bytes_planes / n_launch / (kms_launch / 1000.0) / 1e9 / HBM_PEAK_GBS,
+                                     "note": "the same formula on the layout the device reads: 3-bit genome planes, "
+                                             "ceil(131 * 3 / 8) = 50 B per window"},
+                    "granule_adjusted": {"bytes_per_read": granule / len(res),
+                                         "achieved": granule / n_launch / (kms_launch / 1000.0) / 1e9,
+                                         "frac": granule / n_launch / (kms_launch / 1000.0) / 1e9 / HBM_PEAK_GBS,
+                                         "note": "64-B lines per random access, device bucket lines (SURVEY 8(d) d3)"},
+                    "launches_per_step": n_launch, "reads_per_launch": reads_launch,
+                    "algorithmic_bytes_per_launch": bytes_launch, "algorithmic_bytes_per_read": bytes_all / len(res),
+                    "binding_resource": binding,
+                    "pmc_source": pmc_src, "lib_sha256": sha, "kernel_source_sha256": src_sha}
+        if copy_peak_gbs:
+            roofline["frac_of_measured_copy_peak"] = achieved / copy_peak_gbs
         result = {
             "metric": METRIC,
             "value": value,

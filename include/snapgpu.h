@@ -376,7 +376,7 @@ int snapgpu_aligner_debug_trip(snapgpu_aligner_t *a, uint32_t read_index);
 const char *snapgpu_source_sha256(void);
 /* Diagnostic (no reference equivalent): with SNAPGPU_PHASES=1 in the environment at
  * snapgpu_aligner_create, align_kernel<128> sums shader cycles per phase and event
- * counts into out[0..min(len, 40)) (order: snapgpu.BaseAligner.PHASES); reset != 0 zeroes them. */
+ * counts into out[0..min(len, 48)) (order: snapgpu.BaseAligner.PHASES); reset != 0 zeroes them. */
 int snapgpu_phase_cycles(snapgpu_aligner_t *a, uint64_t *out, uint32_t len, int reset);
 const char *snapgpu_aligner_name(const snapgpu_aligner_t *a);    /* getName() */
 

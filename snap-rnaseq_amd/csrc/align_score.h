@@ -856,6 +856,7 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, El
             const int Gn = 64 / GS;
             const int m = (int)(nc - i0) < Gn ? (int)(nc - i0) : Gn;
             PH_CNT(A, S, PH_NPASS, 1);
+            if (forced) PH_CNT(A, S, PH_NPASSF, 1);
             bool fin;
             if (GS == 8) fin = pass_apply<8, EXT>(A, S, ar, st, i0, m, k, n, nb, lastSlot, lastSkip, result);
             else if (GS == 16) fin = pass_apply<16, EXT>(A, S, ar, st, i0, m, k, n, nb, lastSlot, lastSkip, result);
@@ -865,6 +866,7 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, El
             i0 += (uint32_t)m;
         }
         PH_ADD(A, S, PH_PASSLOOP, tpl);
+        if (forced) { PH_ADD(A, S, PH_PASSLOOPF, tpl); PH_CNT(A, S, PH_NCANDF, nc); }
         PH_T(A, twb);
         // ---- write the batch back (scored, prob, bestScore, bestLoc, allScored = 1)
         for (uint32_t idx = lane; idx < nb * 8; idx += WAVE) {

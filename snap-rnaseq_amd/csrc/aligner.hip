@@ -732,6 +732,8 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
     if constexpr (EXT) { if (A.maxHitsToGet) fill_hits(A, r, run && fillHits); }
     wave_sync();
     PH_ADD(A, S, PH_OUT, tout);
+    PH_ADD(A, S, PH_READCYC, tsetup);
+    if (run && S.nElems >= 64) { PH_ADD(A, S, PH_HEAVYCYC, tsetup); PH_CNT(A, S, PH_NHEAVY, 1); }
 }
 
 template <int MAXLEN, bool EXT>

@@ -472,12 +472,13 @@ class BaseAligner:
               "writeback", "out", "n_pass", "n_cand", "n_read", "n_pass16", "n_pass32", "n_pass64", "rows_fwd",
               "rows_rev", "n_score_calls", "n_forced", "n_popped", "n_succ", "passloop", "select", "fetch", "seedloop",
               "n_batch", "rank", "n_elems_forced", "candlist", "succ", "nearby", "prob", "fails", "n_fail_steps",
-              "succ_tail")
+              "succ_tail", "n_pass_forced", "passloop_forced", "heavy_read_cycles", "n_heavy_reads", "n_cand_forced",
+              "read_cycles")
 
     def phase_cycles(self, reset=True):
         """Diagnostic per-phase shader-cycle sums (needs SNAPGPU_PHASES=1 at construction)."""
-        buf = (C.c_uint64 * 40)()
-        _check(lib().snapgpu_phase_cycles(self._h, buf, 40, int(reset)), "phase_cycles")
+        buf = (C.c_uint64 * 48)()
+        _check(lib().snapgpu_phase_cycles(self._h, buf, 48, int(reset)), "phase_cycles")
         return {k: int(buf[i]) for i, k in enumerate(self.PHASES)}
 
     def stats(self):

@@ -45,5 +45,11 @@ out["share_of_wave_time"] = {k: round(ph[k] / tot, 4) for k in ("setup", "lookup
 n = max(ph["n_succ"], 1)
 out["cycles_per_success"] = {k: round(ph[k] / n, 1) for k in ("succ", "nearby", "prob", "succ_tail")}
 out["cycles_per_pass"] = {k: round(ph[k] / max(ph["n_pass"], 1), 1) for k in ("passloop", "stage", "lv_fwd", "lv_rev", "apply", "fails", "succ")}
+out["forced"] = {"passes_per_read": ph["n_pass_forced"] / args.reads, "passloop_cycles_per_read": ph["passloop_forced"] / args.reads,
+                 "candidates_per_read": ph["n_cand_forced"] / args.reads,
+                 "nonforced_passes_per_read": (ph["n_pass"] - ph["n_pass_forced"]) / args.reads,
+                 "nonforced_passloop_cycles_per_read": (ph["passloop"] - ph["passloop_forced"]) / args.reads}
+out["heavy_reads"] = {"def": ">= 64 candidate elements", "share_of_reads": ph["n_heavy_reads"] / args.reads,
+                      "share_of_cycles": ph["heavy_read_cycles"] / max(1, ph["read_cycles"])}
 out["pass_overhead_per_pass"] = round((ph["passloop"] - ph["stage"] - ph["lv_fwd"] - ph["lv_rev"] - ph["apply"]) / max(ph["n_pass"], 1), 1)
 print(json.dumps(out, indent=1))

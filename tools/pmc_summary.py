@@ -134,6 +134,12 @@ def main(src, dst):
                    "write_bytes_per_read": hb.get("write", 0) / reads_per_launch,
                    "valu_insts_per_read": per_read.get("SQ_INSTS_VALU"),
                    "salu_insts_per_read": per_read.get("SQ_INSTS_SALU"),
+                   "branch_insts_per_read": per_read.get("SQ_INSTS_BRANCH"),
+                   "lds_insts_per_read": per_read.get("SQ_INSTS_LDS"),
+                   "vmem_insts_per_read": (per_read.get("SQ_INSTS_VMEM_RD") or 0) + (per_read.get("SQ_INSTS_VMEM_WR") or 0),
+                   "smem_insts_per_read": per_read.get("SQ_INSTS_SMEM"),
+                   # SQ_WAVE_CYCLES counts quad-cycles (MI355X_MICROARCH.md): x4 = shader cycles
+                   "wave_cycles_per_read": 4 * per_read["SQ_WAVE_CYCLES"] if "SQ_WAVE_CYCLES" in per_read else None,
                    # share of the waves' lifetime (SQ_WAVE_CYCLES) each state takes: issuing VALU / any
                    # instruction, waiting on a counter (memory), waiting for a dependency to issue
                    "wave_state": a.get("wave_state"),
