@@ -477,6 +477,7 @@ def standin_main(args, wl, world, rank, local, dist):
     per_rank = gather_per_rank(dist, world, {
         "rank": rank, "device": None, "reads": wl["reads"], "elapsed_s": round(own[0], 4),
         "reads_per_s": wl["reads"] * args.steps / own[0], "index_built_here": bool(index_info.get("built_by_this_rank")),
+        "index_attached": bool(index_info.get("attached")), "shared_file": index_info.get("shared_file"),
         "shard_first_read": shard_tag(reads),
         "single_hits": int((box["res"]["result"] == snapgpu.SingleHit).sum())})
     result = None
@@ -610,7 +611,8 @@ def main():
     per_rank = gather_per_rank(dist, world, {
         "rank": rank, "device": local, "reads": wl["reads"], "elapsed_s": round(own[0], 4),
         "reads_per_s": wl["reads"] * args.steps / own[0], "index_upload_s": round(t_upload, 2),
-        "index_built_here": bool(index_info.get("built_by_this_rank")), "shard_first_read": shard_tag(reads)})
+        "index_built_here": bool(index_info.get("built_by_this_rank")), "index_attached": bool(index_info.get("attached")),
+        "shard_first_read": shard_tag(reads)})
 
     result = None
     if rank == 0:

@@ -47,6 +47,11 @@ def build_once(snapgpu, genome_bases, gen, seed_len, n_threads, rank, world, dis
             idx.share(_path(tag))
             info["share_s"] = round(time.time() - t2, 2)
             info["shared_file"] = _path(tag)
+            # one image per node in host RAM: the builder drops its private index and maps the shared
+            # file like every other rank (C3: 56 GB once, not once per rank plus the file)
+            del idx, g
+            idx = snapgpu.GenomeIndex.attach(_path(tag))
+            info["attached"] = True
     if dist is not None:
         dist.barrier()
     if not builder:
@@ -55,6 +60,7 @@ def build_once(snapgpu, genome_bases, gen, seed_len, n_threads, rank, world, dis
         info["attach_s"] = round(time.time() - t3, 3)
         info["built_by_this_rank"] = False
         info["shared_file"] = _path(tag)
+        info["attached"] = True
     return idx, info
 
 

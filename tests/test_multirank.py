@@ -118,6 +118,33 @@ def test_bench_gpus_2_self_launches_two_ranks():
     assert d["ms_per_step"] * 2 / 1000.0 >= max(p["elapsed_s"] for p in pr) - 1e-3
 
 
+def test_bench_gpus_8_rehearsal_one_image_per_node():
+    """The driver's 8-GPU scaling run, rehearsed on CPU through the real self-launch (verdict r4 item 6):
+    `bench.py --gpus 8` starts 8 ranks, one builds the index, every rank -- the builder included -- maps
+    the one shared /dev/shm image (host RAM holds one copy: C3's 56 GB once, not per rank), the 8 read
+    shards are disjoint, the reduction covers all ranks, and the image is removed at the end."""
+    import json
+    import subprocess
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--oracle-standin", "--reads", "120",
+           "--genome-bases", "200000", "--steps", "1", "--warmup", "0"]
+    r = subprocess.run(cmd, capture_output=True, text=True, env=_bench_env(), timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and "standin" in d
+    pr = d["config"]["per_rank"]
+    assert sorted(p["rank"] for p in pr) == list(range(8))
+    assert sum(p["index_built_here"] for p in pr) == 1
+    assert all(p["index_attached"] for p in pr)
+    files = {p["shared_file"] for p in pr}
+    assert len(files) == 1 and not os.path.exists(files.pop())
+    assert len({p["shard_first_read"] for p in pr}) == 8
+    assert all(p["single_hits"] > 50 for p in pr)
+    assert d["ms_per_step"] / 1000.0 >= max(p["elapsed_s"] for p in pr) - 1e-3
+    assert d["value"] == pytest.approx(8 * 120 / (d["ms_per_step"] / 1000.0), rel=1e-6)
+
+
 def test_bench_refuses_world_gpus_mismatch():
     """A run whose rank count differs from --gpus exits non-zero instead of mislabelling n_gpus."""
     import subprocess
