@@ -73,6 +73,21 @@ def algorithmic_bytes(res, ref_probes=None):
     return byte_genome, dict(P=P / n, H=H / n, V=V / n, S=S / n), planes, p_unit
 
 
+def granule_bytes(res):
+    """SURVEY.md 8(d) d3, granule-adjusted: every random access moves whole 64-B lines -- the read's
+    bases and qualities, its record, one line per bucket line probed, per overflow list
+    ceil(4 H / 64) hit lines (the list length travels in the bucket entry), and per LV-scored candidate the genome window's lines
+    (64 * ceil((readLen + MAX_K) / 64), the byte genome of the reference's layout)."""
+    P = res["nProbes"].astype(np.int64)
+    H = res["nHitWords"].astype(np.int64)
+    V = res["nOverflowLists"].astype(np.int64)
+    S = res["nLocationsScored"].astype(np.int64)
+    line = 64
+    per_read = (2 * line * -(-READ_LEN // line) + line + line * P + line * ((4 * H + line - 1) // line) +
+                line * -(-(READ_LEN + MAX_K) // line) * S)
+    return int(per_read.sum())
+
+
 def lib_sha256():
     import snapgpu._ffi as F
     h = hashlib.sha256()

@@ -82,10 +82,12 @@ static int run(int ncu, int wpc, double &cpi_wave, double &cpi_cu) {
     uint32_t *ds;
     CHK(hipMalloc(&dc, sizeof(uint64_t) * ncu * wpc));
     CHK(hipMalloc(&ds, 4));
-    hipLaunchKernelGGL(rate_kernel<KIND>, dim3(ncu), dim3(64 * wpc), 0, 0, 1u, dc, ds);   // warm
+    // at most 16 waves (1024 lanes) per block: more waves per CU come as 2 blocks per CU
+    const int bpc = wpc > 16 ? 2 : 1, wpb = wpc / bpc;
+    hipLaunchKernelGGL(rate_kernel<KIND>, dim3(ncu * bpc), dim3(64 * wpb), 0, 0, 1u, dc, ds);   // warm
     CHK(hipGetLastError());
     CHK(hipDeviceSynchronize());
-    hipLaunchKernelGGL(rate_kernel<KIND>, dim3(ncu), dim3(64 * wpc), 0, 0, 2u, dc, ds);
+    hipLaunchKernelGGL(rate_kernel<KIND>, dim3(ncu * bpc), dim3(64 * wpb), 0, 0, 2u, dc, ds);
     CHK(hipGetLastError());
     CHK(hipDeviceSynchronize());
     std::vector<uint64_t> c(ncu * wpc);
@@ -118,7 +120,7 @@ int main() {
     CHK(hipGetDeviceProperties(&p, 0));
     const int ncu = p.multiProcessorCount;
     printf("{\"device\": \"%s\", \"cus\": %d, \"note\": \"shader cycles (s_memtime) per instruction; wpcN = N waves per "
-           "CU in one block (N/4 per SIMD from 4 up)\", \"rates\": [\n", p.gcnArchName, ncu);
+           "CU (one block, two above 16; N/4 per SIMD from 4 up)\", \"rates\": [\n", p.gcnArchName, ncu);
     if (row<SALU>(ncu) || row<VALU>(ncu) || row<MIX>(ncu) || row<SBR>(ncu) || row<RLCH>(ncu)) return 1;
     printf("]}\n");
     return 0;
