@@ -198,11 +198,15 @@ struct KArgs {
     uint32_t *deferCount;        //   (atomic append count)
     const uint32_t *readList;    // passes 2 and 3: read indices (the previous passes' defers; nullptr in pass 1)
     const uint32_t *readCount;   //   and their number (the previous pass's deferCount)
-    const uint4 *seedRecs;       // seed_lookup_kernel records (SeedRec, 8 per read), or nullptr
+    const uint4 *seedRecs;       // seed_lookup_kernel records (SeedRec, 16 per read; passes 1 and 2), or nullptr
     // pass 0 puts the reads longer than 128 bases straight onto deferList (pass 2's list) with one
     // atomic per 4-read wave that holds any, and counts them in longCount; pass 1 (longCount set)
     // then skips them instead of deferring them one by one, and ends at once when every read is long
     uint32_t *longCount;
+    // longest-first order of pass 2 (SNAPGPU_ORDER_LONG, default on): pass 0 writes its long reads
+    // here as read | class << 28 (class = log2 of the summed hit counts of their first seeds) and
+    // order_long_kernel moves them onto deferList heaviest class first; nullptr: straight onto deferList
+    uint32_t *orderTmp;
     unsigned long long *phaseBuf;   // diagnostic (SNAPGPU_PHASES=1): per-block [PH_SLOTS] cycle sums, else null
     // windowed search + multi-hit export (snapgpu_align_batch_ex; BaseAligner.h:73-86)
     const snapgpu_search_t *search;     // per read, or nullptr (= unconstrained)

@@ -538,7 +538,7 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
         const bool windowed = EXT && (minSeedLoc != 0 || maxSeedLoc != INVALID);
         // first-round lookups resolved by seed_lookup_kernel: lane 4k+f holds field f of record k
         uint32_t srec = 0, pfIdx = SEEDS_PER_READ;
-        if (MAXLEN == 128 && A.seedRecs && A.maxHits < 0xffffu && radius == 0) {
+        if (MAXLEN <= 256 && A.seedRecs && A.maxHits < 0xffffu && radius == 0) {
             srec = ((const uint32_t *)(A.seedRecs + (uint64_t)r * SEEDS_PER_READ))[lane & (4 * SEEDS_PER_READ - 1)];
             pfIdx = 0;
         }
@@ -1107,6 +1107,7 @@ struct snapgpu_aligner {
     // forced mode: reads with at least this many elements get a radix-sorted pop order instead of
     // windowed ranks (SNAPGPU_RADIX_MIN; beyond SKCAP the ranks stage keys from HBM per window)
     uint32_t radixMin = SKCAP + 1;
+    bool orderLong = true;        // pass 2's list longest-first (SNAPGPU_ORDER_LONG=0: pass 0's order)
     uint32_t tripRead = 0xffffffffu;   // test hook (snapgpu_aligner_debug_trip): trip the watchdog at this read
     snapgpu_timing_t timing{};
     snapgpu_aligner_stats_t stats{};
@@ -1699,6 +1700,7 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
     if (const char *t = getenv("SNAPGPU_CHUNK_READS"); t && atoll(t) > 0) a->chunkReads = (uint64_t)atoll(t);
     if (const char *t = getenv("SNAPGPU_RADIX_MIN"); t && atoll(t) > 0) a->radixMin = (uint32_t)atoll(t);
     if (const char *t = getenv("SNAPGPU_OVERLAP")) a->overlapKernels = atoi(t) != 0;
+    if (const char *t = getenv("SNAPGPU_ORDER_LONG")) a->orderLong = atoi(t) != 0;
     auto fail = [&](const char *what, hipError_t e) {
         snapgpu::setError(std::string(what) + ": " + hipGetErrorString(e));
         snapgpu_aligner_free(a);
@@ -1888,6 +1890,7 @@ struct PassIO {
     uint32_t *defer2;   // pass 2 -> pass 3 read list
     uint32_t *ovf;      // passes 1-3 -> big-arena pass (reads that outgrew a capped arena)
     SeedRec *seeds;
+    uint32_t maxLen;    // longest read (or a bound): no long reads, no order_long_kernel
 };
 
 // Queue pass 0 (seed lookups), pass 1 (align_kernel<128>), pass 2 (align_kernel<256> over the
@@ -1938,11 +1941,18 @@ static int launch_passes(snapgpu_aligner_t *a, int li, const PassIO &io, const A
     // reads longer than 128 bases straight onto pass 2's list
     A.seedRecs = nullptr;
     A.longCount = L.counter + 5;
+    // longest-first: the long reads' order list is pass 2's defer list (free until pass 2 writes it)
+    A.orderTmp = a->orderLong && io.n < (1ull << 28) ? io.defer2 : nullptr;
     HIPCHK(hipEventRecord(ev.e[3], L.stream));
     hipLaunchKernelGGL(seed_lookup_kernel, dim3((unsigned)((io.n + 4 * LOOKUP_WAVES - 1) / (4 * LOOKUP_WAVES))),
                        dim3(64 * LOOKUP_WAVES), 0, L.stream, A, io.seeds,
                        L.lookupStats);
     HIPCHK(hipGetLastError());
+    if (A.orderTmp && io.maxLen > 128) {
+        hipLaunchKernelGGL(order_long_kernel, dim3(1), dim3(1024), 0, L.stream, A.orderTmp, A.longCount, A.deferList);
+        HIPCHK(hipGetLastError());
+    }
+    A.orderTmp = nullptr;
     A.seedRecs = reinterpret_cast<const uint4 *>(io.seeds);
     HIPCHK(hipEventRecord(ev.e[0], L.stream));
     const bool ext = x.search || x.maxHitsToGet;
@@ -1954,8 +1964,7 @@ static int launch_passes(snapgpu_aligner_t *a, int li, const PassIO &io, const A
     KArgs M = A;
     M.counter = L.counter + 3;
     M.readList = io.defer; M.readCount = L.counter + 2;
-    M.deferList = io.defer2; M.deferCount = L.counter + 4;
-    M.seedRecs = nullptr;
+    M.deferList = io.defer2; M.deferCount = L.counter + 4;   // (M.seedRecs: pass 0's records, long reads too)
     int grid256 = a->grid256;
     if ((uint64_t)grid256 > io.n) grid256 = (int)io.n;
     if (ext) hipLaunchKernelGGL((align_kernel<256, true>), dim3(grid256), dim3(64), 0, L.stream, M);
@@ -2080,7 +2089,7 @@ static int launch_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, cons
         EvSet *ev = nextEvSet(a);
         if (!ev) return SNAPGPU_EDEVICE;
         PassIO io{d->dBases, d->dQuals, d->dOffsets + b, d->dLengths + b, m, d->dOut + b, d->dDefer + b,
-                  d->dDefer + (n + 1) + b, d->dDefer + 2 * (n + 1) + b, d->dSeeds + b * SEEDS_PER_READ};
+                  d->dDefer + (n + 1) + b, d->dDefer + 2 * (n + 1) + b, d->dSeeds + b * SEEDS_PER_READ, d->maxLen};
         if ((rc = launch_passes(a, (int)(c & 1), io, x, *ev, c ? &a->evs[a->nEvUsed - 2] : nullptr))) return rc;
     }
     a->lastReads = d;
@@ -2351,9 +2360,12 @@ int snapgpu_align_batch_submit(snapgpu_aligner_t *a, const snapgpu_reads_t *read
             if ((rc = finishOldest(a, &any))) break;
         if (rc) break;
         const uint64_t b = c * per, m = std::min(n, b + per) - b;
+        uint32_t maxLen = 0;
         for (uint64_t i = 0; i < m; i++) {
             S.hOffsets[i] = reads->offsets[b + i] - lo[c];
-            S.hLengths[i] = reads->lengths[b + i];
+            const uint32_t ln = reads->lengths[b + i];
+            S.hLengths[i] = ln;
+            maxLen = std::max(maxLen, ln);
         }
         const uint64_t span = std::min(hi[c] + 64, std::max(hostEnd, hi[c])) - lo[c];
         // inputs on the copy stream: they land while the lane's previous chunk is still running
@@ -2365,7 +2377,7 @@ int snapgpu_align_batch_submit(snapgpu_aligner_t *a, const snapgpu_reads_t *read
         HIPBRK(hipEventRecord(S.h2d, cs));
         HIPBRK(hipStreamWaitEvent(s, S.h2d, 0));
         PassIO io{S.dBases, S.dQuals, S.dOffsets, S.dLengths, m, L.dOut, L.dDefer, L.dDefer + (L.capReads + 1),
-                  L.dDefer + 2 * (L.capReads + 1), L.dSeeds};
+                  L.dDefer + 2 * (L.capReads + 1), L.dSeeds, maxLen};
         EvSet *ev = nextEvSet(a);
         if (!ev) { rc = SNAPGPU_EDEVICE; break; }
         if ((rc = launch_passes(a, li, io, AlignExt(), *ev, a->nEvUsed >= 2 ? &a->evs[a->nEvUsed - 2] : nullptr))) break;

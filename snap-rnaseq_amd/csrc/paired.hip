@@ -33,6 +33,7 @@
 
 #include "align_device.h"
 #include "bucket_table.h"
+#include "order_long.h"
 #include "internal.h"
 
 int snapgpu_internal_index_args(const snapgpu_aligner_t *a, sgk::KArgs *A, int *device);
@@ -835,6 +836,52 @@ __global__ __launch_bounds__(64) void paired_kernel(PArgs P) {
     }
 }
 
+// Weight of each long pair for the longest-first order of pass 1b (order_long.h): the summed hit
+// counts of both ends' seeds at offsets 0, L, 2L, .. inside their first 128 bases, a seed counted
+// only below maxBigHits (the lookups the intersecting walk records, :518-524) and only when all
+// ACGT.  Two pairs per wave, 16 lanes per end (lane 32j + 16e + k: seed k of end e of pair j).
+// list[i] (i < *count) = pair index; out[i] = pair | class << 28 for order_long_kernel.
+__global__ __launch_bounds__(256) void pair_weight_kernel(PArgs P, const uint32_t *list, const uint32_t *count, uint32_t *out) {
+    const KArgs &X = P.X;
+    const int lane = lane_id();
+    const uint32_t n = *count, L = X.seedLen;
+    const uint32_t wave = blockIdx.x * 4u + threadIdx.x / 64u, nWaves = gridDim.x * 4u;
+    for (uint32_t b = 2u * wave; b < n; b += 2u * nWaves) {   // wave-uniform trip count
+        const uint32_t i = b + (uint32_t)(lane >> 5);
+        const int e = (lane >> 4) & 1, k = lane & 15;
+        const uint32_t pi = i < n ? list[i] : 0u;
+        const uint32_t len = i < n ? P.lengths[e][pi] : 0u;
+        const uint32_t lim = len < 128u ? len : 128u;
+        const uint32_t so = (uint32_t)k * L;
+        bool act = i < n && so + L <= lim;
+        uint64_t f = 0, rv = 0;
+        if (act) {
+            const char *rd = P.bases[e] + P.offsets[e][pi] + so;
+            for (uint32_t j = 0; j < L; j++) {
+                const int v = base_value((uint8_t)rd[j]);
+                act = act && v <= 3;
+                f |= (uint64_t)(v & 3) << ((L - j - 1) * 2);
+                rv |= (uint64_t)((v & 3) ^ 3) << (j * 2);
+            }
+        }
+        const bool comp = (int64_t)f > (int64_t)rv;
+        const uint64_t canon = comp ? rv : f;
+        uint32_t v1 = 0, v2 = 0, aux = 0, lines = 0;
+        const bool found = bucket_lookup_quad(X, act, (uint32_t)(canon >> 32), (uint32_t)canon, v1, v2, aux, lines);
+        uint32_t w = 0;
+        if (act && found) {
+            auto side = [&](uint32_t v, uint32_t c) -> uint32_t {
+                const uint32_t h = v == UNUSED_SIDE ? 0u : v < X.nBases ? 1u : c >= BK_CSAT ? 0xffffu : c;
+                return h < P.maxBigHits ? h : 0u;
+            };
+            w = side(v1, aux & BK_CSAT) + (f != rv ? side(v2, (aux >> 15) & BK_CSAT) : 0u);
+        }
+#pragma unroll
+        for (int s = 16; s >= 1; s >>= 1) w += (uint32_t)__shfl_xor((int)w, s, 64);   // the pair's 32 lanes
+        if ((lane & 31) == 0 && i < n) out[i] = pi | (order_class(w) << ORDER_CLASS_SHIFT);
+    }
+}
+
 }  // namespace pe
 }  // namespace sgk
 
@@ -889,6 +936,8 @@ struct snapgpu_paired_aligner {
                                            // [3] pass 2 queue, [4] pass-2 defer count, [5] pass 1b queue,
                                            // [6] pass-1b defer count
     uint32_t *dDefer = nullptr, *dDefer2 = nullptr;
+    uint32_t *dOrder = nullptr, *dOrderW = nullptr;   // long pairs before / after pair_weight_kernel
+    bool orderLong = true;                 // pass 1b longest-first (SNAPGPU_ORDER_LONG=0: input order)
     snapgpu_pair_result_t *dOut = nullptr;
     char *dB[2] = {}, *dQ[2] = {};
     uint64_t *dO[2] = {};
@@ -901,11 +950,15 @@ static void pfree(void *p) { if (p) (void)hipFree(p); }
 static int ensurePairCapacity(snapgpu_paired_aligner_t *pa, uint64_t n, const uint64_t bytes[2]) {
     if (n > pa->capPairs) {
         pfree(pa->dOut); pfree(pa->dDefer); pfree(pa->dDefer2); pfree(pa->dO[0]); pfree(pa->dO[1]); pfree(pa->dL[0]); pfree(pa->dL[1]);
+        pfree(pa->dOrder); pfree(pa->dOrderW);
         pa->dOut = nullptr; pa->dDefer = nullptr; pa->dDefer2 = nullptr; pa->dO[0] = pa->dO[1] = nullptr; pa->dL[0] = pa->dL[1] = nullptr;
+        pa->dOrder = pa->dOrderW = nullptr;
         pa->capPairs = 0;
         PCHK(hipMalloc(&pa->dOut, n * sizeof(snapgpu_pair_result_t)));
         PCHK(hipMalloc(&pa->dDefer, n * 4 + 16));
         PCHK(hipMalloc(&pa->dDefer2, n * 4 + 16));
+        PCHK(hipMalloc(&pa->dOrder, n * 4 + 16));
+        PCHK(hipMalloc(&pa->dOrderW, n * 4 + 16));
         for (int r = 0; r < 2; r++) {
             PCHK(hipMalloc(&pa->dO[r], n * 8 + 16));
             PCHK(hipMalloc(&pa->dL[r], n * 4 + 16));
@@ -981,8 +1034,16 @@ static int runIntersect(snapgpu_paired_aligner_t *pa, const snapgpu_reads_t *r0,
         // longL / shortL outlive the copies (the stream is synchronised below, before they go out of
         // scope); the pass-1 defer count starts at the long pairs' count, set by value (a stack
         // scalar as the source of an asynchronous copy could be read after its scope ended)
-        PCHK(hipMemcpyAsync(pa->dDefer, longL.data(), longL.size() * 4, hipMemcpyHostToDevice, s));
+        const bool order = pa->orderLong && n < (1ull << ORDER_CLASS_SHIFT);
+        PCHK(hipMemcpyAsync(order ? pa->dOrder : pa->dDefer, longL.data(), longL.size() * 4, hipMemcpyHostToDevice, s));
         PCHK(hipMemsetD32Async((hipDeviceptr_t)(pa->dCounter + 2), (int)longL.size(), 1, s));
+        if (order) {   // pass 1b's list heaviest first (order_long.h); pass 1 appends its defers after it
+            const unsigned blocks = (unsigned)std::min<uint64_t>((longL.size() + 7) / 8, 2048);
+            hipLaunchKernelGGL(pair_weight_kernel, dim3(blocks), dim3(256), 0, s, P, pa->dOrder, pa->dCounter + 2, pa->dOrderW);
+            PCHK(hipGetLastError());
+            hipLaunchKernelGGL(order_long_kernel, dim3(1), dim3(1024), 0, s, pa->dOrderW, pa->dCounter + 2, pa->dDefer);
+            PCHK(hipGetLastError());
+        }
         if (!shortL.empty()) PCHK(hipMemcpyAsync(pa->dDefer2, shortL.data(), shortL.size() * 4, hipMemcpyHostToDevice, s));
     }
     // pass 1: reads <= 128 bases, pools for ordinary pairs, the full grid
@@ -1143,6 +1204,7 @@ snapgpu_paired_aligner_t *snapgpu_paired_aligner_create(int device, const snapgp
         { snapgpu_paired_aligner_free(pa); return nullptr; }
     // test hook: at most this many waves per pass, so each wave aligns many pairs in a row (a pair's
     // result must not depend on the pairs its wave aligned before: tests/test_paired.py)
+    if (const char *t = getenv("SNAPGPU_ORDER_LONG")) pa->orderLong = atoi(t) != 0;
     if (const char *t = getenv("SNAPGPU_PAIRED_GRID"); t && atoi(t) > 0) {
         const int g = atoi(t);
         for (auto &pp : pa->pass) pp.grid = std::min(pp.grid, g);
@@ -1158,7 +1220,7 @@ void snapgpu_paired_aligner_free(snapgpu_paired_aligner_t *pa) {
     } else {
         (void)hipSetDevice(pa->device);
         if (pa->stream) (void)hipStreamSynchronize(pa->stream);
-        pfree(pa->dCounter); pfree(pa->dDefer); pfree(pa->dDefer2); pfree(pa->dOut);
+        pfree(pa->dCounter); pfree(pa->dDefer); pfree(pa->dDefer2); pfree(pa->dOrder); pfree(pa->dOrderW); pfree(pa->dOut);
         for (int r = 0; r < 2; r++) { pfree(pa->dB[r]); pfree(pa->dQ[r]); pfree(pa->dO[r]); pfree(pa->dL[r]); }
         for (auto &pp : pa->pass) pfree(pp.pool);
         if (pa->stream) (void)hipStreamDestroy(pa->stream);

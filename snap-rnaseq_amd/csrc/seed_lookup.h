@@ -11,13 +11,18 @@
 // runs at memory throughput instead of as ~3 dependent HBM round trips inside each read's
 // sequential aligner.  align_kernel<128> consumes the records when its seed loop reaches the same
 // offset and counts probes / overflow lists exactly as before (a read that stops earlier leaves
-// its later records unused).
+// its later records unused).  Of a longer read it resolves the first-round seeds that lie in its
+// first 128 bases -- a prefix of the same sequence, which align_kernel<256> consumes the same way --
+// and weighs the read by their summed hit counts: the long reads go onto pass 2's list heaviest
+// first (order_long_kernel), so a read that scores thousands of candidates starts at the head of
+// the persistent kernel instead of finishing alone at its tail.  Results do not depend on the order.
 //
 // The lookups go to the bucket image of the tables (bucket_table.h): one 64-B line per lookup in
 // the common case, the overflow-list lengths carried in the entry.
 #pragma once
 #include "align_device.h"
 #include "bucket_table.h"
+#include "order_long.h"
 
 namespace sgk {
 
@@ -102,19 +107,22 @@ __global__ __launch_bounds__(64 * LOOKUP_WAVES) void seed_lookup_kernel(KArgs A,
         chunk = (uint64_t)p0 | ((uint64_t)p1 << 16) | ((uint64_t)iv << 32);
     }
     SeedRec rec = {0u, 0u, 0u, 0u};
+    uint32_t weight = 0;   // a long read's seed: its hit count (0: popular or not found)
     uint32_t nSeed = 0, nProbe = 0, nOvfRead = 0;
     const int grp = lane & ~15;
     const uint64_t badMask = ballot(bad);
-    const bool can = have && n <= 128 && (int)n >= L;
+    const bool can = have && (int)n >= L;
+    const bool lng = n > 128;   // records: the first-round seeds inside positions 0..127 only
+    const int firstRound = 128 / L;   // of a long read: offsets 0, L, .., (firstRound - 1) L (all-ACGT prefix)
     int my = -1;             // offset of this lane's seed k of the sequence (-1: none)
     uint32_t w0 = 0, w1 = 0;   // code bits 0 and 1 of the seed's positions my .. my + L - 1
     if (badMask == 0) {
         // every read of the wave is all ACGT: its sequence of seed offsets depends on its length
         // alone (a table entry), and a seed's bits come from the three chunks it can span
-        if (can) {
+        if (can && !lng) {
             const uint32_t t = A.tab->seedSeq[n][k];
             my = t == 0xffu ? -1 : (int)t;
-        }
+        } else if (can) my = k < firstRound ? k * L : -1;
         const int c0 = my > 0 ? my >> 4 : 0;
         const uint32_t a = (uint32_t)shfl_idx((int)(uint32_t)chunk, grp + c0);
         const uint32_t b = (uint32_t)shfl_idx((int)(uint32_t)chunk, grp + (c0 + 1 < 8 ? c0 + 1 : 7));
@@ -142,17 +150,18 @@ __global__ __launch_bounds__(64 * LOOKUP_WAVES) void seed_lookup_kernel(KArgs A,
         if (can) {
             // offset of the k-th seed of the sequence (BaseAligner.cpp:686-746), simulated with the
             // read's seedUsed bits: rounds 0, seedLen, ... then the wrap table's starts
-            const int nPossible = (int)n - L + 1;
+            const int nPossible = (lng ? 128 : (int)n) - L + 1;
             uint64_t u0 = 0, u1 = 0;   // seedUsed, positions 0..127
             int p = 0, wrap = 0, idx = 0;
-            if (clean) {
+            if (clean && lng) my = k < firstRound ? k * L : -1;
+            else if (clean) {
                 const uint32_t t = A.tab->seedSeq[n][k];
                 my = t == 0xffu ? -1 : (int)t;
             }
 #pragma nounroll
             for (int guard = 0; !clean && guard < 4 * 128; guard++) {   // each step marks, wraps or ends
                 if (p >= nPossible) {
-                    if (++wrap >= L) break;                      // wrapCount == seedLen: the read is scored
+                    if (lng || ++wrap >= L) break;               // wrapCount == seedLen: the read is scored
                     p = (int)wrapT[wrap];
                 }
 #pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
@@ -181,6 +190,14 @@ __global__ __launch_bounds__(64 * LOOKUP_WAVES) void seed_lookup_kernel(KArgs A,
         // four lanes per line (the whole wave takes part)
         uint32_t v1 = 0, v2 = 0, aux = 0, probes = 0;
         const bool found = bucket_lookup_quad(A, my >= 0, table, key, v1, v2, aux, probes);
+        if (my >= 0 && found && lng) {   // the long read's weight: hits of its seeds that are not popular
+            const uint32_t c1 = aux & BK_CSAT, c2 = (aux >> 15) & BK_CSAT;
+            auto side = [&](uint32_t v, uint32_t c) -> uint32_t {
+                return v == UNUSED_SIDE ? 0u : v < A.nBases ? 1u : c >= BK_CSAT ? 0xffffu : c;
+            };
+            const uint32_t h = side(v1, c1) + (f != rcv ? side(v2, c2) : 0u);
+            weight = h <= A.maxHits ? h : 0u;
+        }
         if (my >= 0) {
             uint32_t cnt = 0;
             nSeed = 1;
@@ -202,18 +219,26 @@ __global__ __launch_bounds__(64 * LOOKUP_WAVES) void seed_lookup_kernel(KArgs A,
         }
     }
     if (have) out[(uint64_t)r * SEEDS_PER_READ + k] = rec;
-    // route the wave's long reads (lane 16j speaks for read j) straight onto pass 2's list
+    // route the wave's long reads (lane 16j speaks for read j) onto pass 2's list, or with their
+    // weight class onto the order list
     if (A.longCount) {
-        const bool isLong = have && n > 128;
+        const bool isLong = have && lng;
         const uint64_t ml = ballot(k == 0 && isLong);
         if (ml) {
+            uint32_t w = weight;   // the read's summed weight, in every lane of its 16
+#pragma unroll
+            for (int s = 8; s >= 1; s >>= 1) w += (uint32_t)__shfl_xor((int)w, s, 64);
             uint32_t bl = 0;
             if (lane == 0) {
                 bl = atomicAdd(A.deferCount, (uint32_t)__popcll(ml));
                 atomicAdd(A.longCount, (uint32_t)__popcll(ml));
             }
             bl = (uint32_t)readlane((int)bl, 0);
-            if (k == 0 && isLong) A.deferList[bl + (uint32_t)__popcll(ml & ((1ull << lane) - 1))] = r;
+            const uint32_t at = bl + (uint32_t)__popcll(ml & ((1ull << lane) - 1));
+            if (k == 0 && isLong) {
+                if (A.orderTmp) A.orderTmp[at] = r | (order_class(w) << ORDER_CLASS_SHIFT);
+                else A.deferList[at] = r;
+            }
         }
     }
     if (stats) {
