@@ -473,7 +473,7 @@ class BaseAligner:
               "rows_rev", "n_score_calls", "n_forced", "n_popped", "n_succ", "passloop", "select", "fetch", "seedloop",
               "n_batch", "rank", "n_elems_forced", "candlist", "succ", "nearby", "prob", "fails", "n_fail_steps",
               "succ_tail", "n_pass_forced", "passloop_forced", "heavy_read_cycles", "n_heavy_reads", "n_cand_forced",
-              "read_cycles")
+              "read_cycles", "n_filter")
 
     def phase_cycles(self, reset=True):
         """Diagnostic per-phase shader-cycle sums (needs SNAPGPU_PHASES=1 at construction)."""
