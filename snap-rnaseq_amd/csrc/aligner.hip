@@ -1095,6 +1095,10 @@ struct snapgpu_aligner {
     uint64_t nextLane = 0;
     uint64_t chunkSeq = 0;        // submission order of pipelined chunks (finished oldest first)
     hipStream_t copyStream = nullptr;   // H2D of the pipelined chunks
+    // CIGAR (cigar_kernel) and seed-census (charseeds.hip) calls: their own stream and buffers, so a
+    // host thread can run them while another thread's align call keeps the lanes busy (the RNA
+    // paired path's sub-batch pipeline); a caller serialises them among themselves
+    hipStream_t sideStream = nullptr;
     std::chrono::steady_clock::time_point streamStart;
     uint64_t arenaElems = 0;      // worst case per read: (maxSeeds + 2) * maxHits (+ 64)
     uint64_t arenaCap = 0;        // per wave in the main passes (= arenaElems unless that cannot fit the grid)
@@ -1668,6 +1672,7 @@ void snapgpu_aligner_free(snapgpu_aligner_t *a) {
         if (L.stream) hipStreamDestroy(L.stream);
     }
     if (a->copyStream) { hipStreamSynchronize(a->copyStream); hipStreamDestroy(a->copyStream); }
+    if (a->sideStream) { hipStreamSynchronize(a->sideStream); hipStreamDestroy(a->sideStream); }
     for (auto &v : a->evs) {
         for (auto &e : v.e) if (e) hipEventDestroy(e);
         hostPinnedFree(v.hCounter);
@@ -1721,6 +1726,7 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
             return fail("pinned lookup stats", e);
     }
     if ((e = hipStreamCreateWithFlags(&a->copyStream, hipStreamNonBlocking)) != hipSuccess) return fail("stream", e);
+    if ((e = hipStreamCreateWithFlags(&a->sideStream, hipStreamNonBlocking)) != hipSuccess) return fail("stream", e);
     for (auto &ev : a->cev) if ((e = hipEventCreate(&ev)) != hipSuccess) return fail("event", e);
     hipStream_t s0 = a->stream();
     // Every buffer is initialised on the stream of its first consumer or before the device-wide
@@ -2425,23 +2431,34 @@ int snapgpu_align_batch(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, snap
 }
 
 // The reads of a snapgpu_internal_align_batch_packed call in the aligner's own grow-only device
-// reads (what snapgpu_reads_upload allocates per call), uploaded on the aligner's stream.
-static snapgpu_device_reads_t *uploadCachedReads(snapgpu_aligner_t *a, const snapgpu_reads_t *r) {
-    uint64_t bytes = 0;
+// reads (what snapgpu_reads_upload allocates per call), uploaded on the aligner's stream.  Several
+// batches (the RNA path's two ends) go into one device batch, back to back: part p's reads follow
+// part p-1's, their offsets moved past its bytes.
+static snapgpu_device_reads_t *uploadCachedReads(snapgpu_aligner_t *a, const snapgpu_reads_t *const *parts, int np) {
+    uint64_t n = 0, bytes = 0;
     uint32_t maxLen = 0;
-    for (uint64_t i = 0; i < r->n; i++) {
-        bytes = std::max<uint64_t>(bytes, r->offsets[i] + r->lengths[i]);
-        maxLen = std::max(maxLen, r->lengths[i]);
+    std::vector<uint64_t> span(np), base(np);
+    for (int p = 0; p < np; p++) {
+        const snapgpu_reads_t *r = parts[p];
+        uint64_t b = 0;
+        for (uint64_t i = 0; i < r->n; i++) {
+            b = std::max<uint64_t>(b, r->offsets[i] + r->lengths[i]);
+            maxLen = std::max(maxLen, r->lengths[i]);
+        }
+        span[p] = b;
+        base[p] = bytes;
+        bytes += (b + 63) & ~63ull;
+        n += r->n;
     }
     bytes += 64;
-    if (!a->exReads || r->n > a->exReadsCapN || bytes > a->exReadsCapBytes) {
+    if (!a->exReads || n > a->exReadsCapN || bytes > a->exReadsCapBytes) {
         snapgpu_device_reads_free(a->exReads);
         a->exReads = nullptr;
         a->exReadsCapN = a->exReadsCapBytes = 0;
         auto *d = new snapgpu_device_reads_t();
         d->owner = a;
         d->device = a->device;
-        const uint64_t capN = r->n + r->n / 4 + 64, capB = bytes + bytes / 4 + 4096;
+        const uint64_t capN = n + n / 4 + 64, capB = bytes + bytes / 4 + 4096;
         bool ok = hipMalloc(&d->dBases, capB) == hipSuccess && hipMalloc(&d->dQuals, capB) == hipSuccess &&
                   hipMalloc(&d->dOffsets, (capN + 1) * 8) == hipSuccess && hipMalloc(&d->dLengths, (capN + 1) * 4) == hipSuccess &&
                   hipMalloc(&d->dOut, (capN + 1) * sizeof(snapgpu_result_t)) == hipSuccess &&
@@ -2453,17 +2470,38 @@ static snapgpu_device_reads_t *uploadCachedReads(snapgpu_aligner_t *a, const sna
         a->exReadsCapBytes = capB;
     }
     snapgpu_device_reads_t *d = a->exReads;
-    d->n = r->n;
+    d->n = n;
     d->maxLen = maxLen;
-    const_cast<snapgpu_reads_t *>(r)->nUploads++;   // clipping is refused from now on
     hipStream_t s = a->stream();
+    // one part: its own offset / length arrays; several: concatenated, offsets moved (host copies
+    // that outlive the asynchronous copies: the stream is synchronised below)
+    std::vector<uint64_t> offs;
+    std::vector<uint32_t> lens;
+    const uint64_t *hOff = parts[0]->offsets;
+    const uint32_t *hLen = parts[0]->lengths;
+    if (np > 1) {
+        offs.reserve(n);
+        lens.reserve(n);
+        for (int p = 0; p < np; p++)
+            for (uint64_t i = 0; i < parts[p]->n; i++) {
+                offs.push_back(parts[p]->offsets[i] + base[p]);
+                lens.push_back(parts[p]->lengths[i]);
+            }
+        hOff = offs.data();
+        hLen = lens.data();
+    }
+    bool ok = true;
+    for (int p = 0; p < np && ok; p++) {
+        const_cast<snapgpu_reads_t *>(parts[p])->nUploads++;   // clipping is refused from now on
+        const uint64_t pad = (p + 1 < np ? base[p + 1] : bytes) - base[p] - span[p];   // zeroed up to the next part / end
+        ok = hipMemcpyAsync(d->dBases + base[p], parts[p]->bases, span[p], hipMemcpyHostToDevice, s) == hipSuccess &&
+             hipMemsetAsync(d->dBases + base[p] + span[p], 0, pad, s) == hipSuccess &&
+             hipMemcpyAsync(d->dQuals + base[p], parts[p]->quals, span[p], hipMemcpyHostToDevice, s) == hipSuccess &&
+             hipMemsetAsync(d->dQuals + base[p] + span[p], 0, pad, s) == hipSuccess;
+    }
     // the deferred lists are laid out by the batch size (launch_resident): 3 * (n + 1) entries
-    if (hipMemcpyAsync(d->dBases, r->bases, bytes - 64, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemsetAsync(d->dBases + bytes - 64, 0, 64, s) != hipSuccess ||
-        hipMemcpyAsync(d->dQuals, r->quals, bytes - 64, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemsetAsync(d->dQuals + bytes - 64, 0, 64, s) != hipSuccess ||
-        hipMemcpyAsync(d->dOffsets, r->offsets, r->n * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(d->dLengths, r->lengths, r->n * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
+    if (!ok || hipMemcpyAsync(d->dOffsets, hOff, n * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(d->dLengths, hLen, n * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess) {
         snapgpu::setError("reads_upload: copy");
         return nullptr;
@@ -2475,11 +2513,12 @@ static snapgpu_device_reads_t *uploadCachedReads(snapgpu_aligner_t *a, const sna
 // packed[off[i] .. off[i+1]) (off has n + 1 entries).  snapgpu_align_batch_ex scatters them into
 // the caller's rows; the RNA path reads them packed (a row layout of 1000 hits per read would
 // fault in ~8 KB of fresh host pages per read for a handful of hits).
-extern "C++" int snapgpu_internal_align_batch_packed(snapgpu_aligner_t *a, const snapgpu_reads_t *reads,
-                                                     const snapgpu_search_t *search, uint32_t maxHitsToGet,
-                                                     snapgpu_result_t *out, int32_t *multiHitsFound,
-                                                     std::vector<uint64_t> &off, std::vector<snapgpu_multi_hit_t> &dense) {
-    if (!a || !reads || !out) return SNAPGPU_EINVAL;
+static int alignPacked(snapgpu_aligner_t *a, const snapgpu_reads_t *const *parts, int np,
+                       const snapgpu_search_t *search, uint32_t maxHitsToGet,
+                       snapgpu_result_t *out, int32_t *multiHitsFound,
+                       std::vector<uint64_t> &off, std::vector<snapgpu_multi_hit_t> &dense) {
+    uint64_t nAll = 0;
+    for (int p = 0; p < np; p++) nAll += parts[p]->n;
     if (maxHitsToGet > SNAPGPU_MAX_MULTI_HITS_TO_GET || (maxHitsToGet && !multiHitsFound)) {
         snapgpu::setError("align_batch_ex: maxHitsToGet must be <= 1024 and come with multiHitsFound/multiHits");
         return SNAPGPU_EINVAL;
@@ -2490,13 +2529,13 @@ extern "C++" int snapgpu_internal_align_batch_packed(snapgpu_aligner_t *a, const
         return SNAPGPU_EUNSUPPORTED;
     }
     if (search)
-        for (uint64_t i = 0; i < reads->n; i++)
+        for (uint64_t i = 0; i < nAll; i++)
             if (search[i].searchRadius && search[i].searchDirection > 1) {
                 snapgpu::setError("align_batch_ex: searchDirection must be 0 (FORWARD) or 1 (RC)");
                 return SNAPGPU_EINVAL;
             }
-    if (reads->n == 0) return SNAPGPU_OK;
-    snapgpu_device_reads_t *d = uploadCachedReads(a, reads);
+    if (nAll == 0) return SNAPGPU_OK;
+    snapgpu_device_reads_t *d = uploadCachedReads(a, parts, np);
     if (!d) return SNAPGPU_EDEVICE;
     AlignExt x;
     // grow-only device buffers of the aligner (hipMalloc / hipFree of the hit rows, ~1 GB for
@@ -2513,7 +2552,7 @@ extern "C++" int snapgpu_internal_align_batch_packed(snapgpu_aligner_t *a, const
     };
     auto cleanup = [&]() { a->lastReads = nullptr; };   // d stays the aligner's (grow-only)
     hipError_t e = hipSuccess;
-    const uint64_t n = reads->n;
+    const uint64_t n = nAll;
     void *dScratch = nullptr, *dFound = nullptr, *dHits = nullptr;
     if (search) {
         if ((e = ensure(a->exSearch, n * sizeof(snapgpu_search_t))) == hipSuccess)
@@ -2577,6 +2616,25 @@ extern "C++" int snapgpu_internal_align_batch_packed(snapgpu_aligner_t *a, const
     }
     cleanup();
     return rc;
+}
+
+extern "C++" int snapgpu_internal_align_batch_packed(snapgpu_aligner_t *a, const snapgpu_reads_t *reads,
+                                                     const snapgpu_search_t *search, uint32_t maxHitsToGet,
+                                                     snapgpu_result_t *out, int32_t *multiHitsFound,
+                                                     std::vector<uint64_t> &off, std::vector<snapgpu_multi_hit_t> &dense) {
+    if (!a || !reads || !out) return SNAPGPU_EINVAL;
+    return alignPacked(a, &reads, 1, search, maxHitsToGet, out, multiHitsFound, off, dense);
+}
+
+// Both ends of the RNA path's pairs in one call (one upload, one pass set: a single persistent-kernel
+// tail instead of two): records and hit counts of r0's reads, then r1's; off / dense over all of them.
+extern "C++" int snapgpu_internal_align_batch_packed2(snapgpu_aligner_t *a, const snapgpu_reads_t *r0,
+                                                      const snapgpu_reads_t *r1, uint32_t maxHitsToGet,
+                                                      snapgpu_result_t *out, int32_t *multiHitsFound,
+                                                      std::vector<uint64_t> &off, std::vector<snapgpu_multi_hit_t> &dense) {
+    if (!a || !r0 || !r1 || !out) return SNAPGPU_EINVAL;
+    const snapgpu_reads_t *parts[2] = {r0, r1};
+    return alignPacked(a, parts, 2, nullptr, maxHitsToGet, out, multiHitsFound, off, dense);
 }
 
 int snapgpu_align_batch_ex(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, const snapgpu_search_t *search,
@@ -2799,7 +2857,7 @@ static CigarArgs cigar_args(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, int
     return C;
 }
 
-// cigar_kernel over n reads on the aligner's stream (timing events around it)
+// cigar_kernel over n reads on the aligner's side stream (timing events around it)
 static int cigar_kernel_launch(snapgpu_aligner_t *a, const CigarArgs &C, uint64_t n) {
     if (!a->cigarGrid) {
         hipDeviceProp_t prop;
@@ -2811,10 +2869,10 @@ static int cigar_kernel_launch(snapgpu_aligner_t *a, const CigarArgs &C, uint64_
     int grid = a->cigarGrid;
     if ((uint64_t)grid > n) grid = (int)n;
     if (grid == 0) return SNAPGPU_OK;
-    HIPCHK(hipEventRecord(a->cev[0], a->stream()));
-    hipLaunchKernelGGL(cigar_kernel, dim3(grid), dim3(64), 0, a->stream(), C);
+    HIPCHK(hipEventRecord(a->cev[0], a->sideStream));
+    hipLaunchKernelGGL(cigar_kernel, dim3(grid), dim3(64), 0, a->sideStream, C);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(a->cev[1], a->stream()));
+    HIPCHK(hipEventRecord(a->cev[1], a->sideStream));
     return SNAPGPU_OK;
 }
 
@@ -2834,9 +2892,11 @@ int snapgpu_cigar_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, int 
     if (!a || !d) return SNAPGPU_EINVAL;
     HIPCHK(hipSetDevice(a->device));
     if (a->failed) { snapgpu::setError("aligner failed earlier (device timeout)"); return SNAPGPU_EDEVICE; }
-    // the records may come from pass sets on both lanes: lane 0 waits for lane 1
-    HIPCHK(hipEventRecord(a->lane[1].done, a->lane[1].stream));
-    HIPCHK(hipStreamWaitEvent(a->lane[0].stream, a->lane[1].done, 0));
+    // the records may come from pass sets on both lanes: the side stream waits for both
+    for (auto &L : a->lane) {
+        HIPCHK(hipEventRecord(L.done, L.stream));
+        HIPCHK(hipStreamWaitEvent(a->sideStream, L.done, 0));
+    }
     CigarArgs C = cigar_args(a, d, useM);
     C.records = d->dOut;
     return cigar_launch(a, d, C);
@@ -2846,7 +2906,7 @@ int snapgpu_cigar_download(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, int3
                            uint32_t *ops) {
     if (!a || !d || !editDistance || !nOps || !ops || !d->dCigEd) return SNAPGPU_EINVAL;
     HIPCHK(hipSetDevice(a->device));
-    HIPCHK(hipStreamSynchronize(a->stream()));
+    HIPCHK(hipStreamSynchronize(a->sideStream));
     HIPCHK(hipMemcpy(editDistance, d->dCigEd, d->n * 4, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(nOps, d->dCigN, d->n * 4, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(ops, d->dCigOps, d->n * CIG_MAX_OPS * 4, hipMemcpyDeviceToHost));
@@ -2938,7 +2998,7 @@ int snapgpu_internal_cigar_view(snapgpu_aligner_t *a, const char *const base[2],
         for (auto &x : th) x.join();
         memset(h + oBases + total, 0, inBytes - oBases - total);
     }
-    hipStream_t st = a->stream();
+    hipStream_t st = a->sideStream;
     char *dIn = (char *)a->cgIn.p, *dOut = (char *)a->cgOut.p;
     HIPCHK(hipMemcpyAsync(dIn, h, inBytes, hipMemcpyHostToDevice, st));
     CigarArgs C;
@@ -3084,7 +3144,7 @@ int snapgpu_internal_devbuf(snapgpu_aligner_t *a, int slot, uint64_t bytes, void
     *p = b.p;
     return SNAPGPU_OK;
 }
-hipStream_t snapgpu_internal_stream(snapgpu_aligner_t *a) { return a->stream(); }
+hipStream_t snapgpu_internal_stream(snapgpu_aligner_t *a) { return a->sideStream; }   // charseeds.hip
 
 int snapgpu_internal_index_args(const snapgpu_aligner_t *a, sgk::KArgs *A, int *device) {
     if (!a || !A) return SNAPGPU_EINVAL;

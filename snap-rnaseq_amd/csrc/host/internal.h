@@ -162,6 +162,10 @@ int snapgpu_internal_align_batch_packed(snapgpu_aligner_t *a, const snapgpu_read
                                         const snapgpu_search_t *search, uint32_t maxHitsToGet,
                                         snapgpu_result_t *out, int32_t *multiHitsFound, std::vector<uint64_t> &off,
                                         std::vector<snapgpu_multi_hit_t> &dense);
+// ... over two batches as one (r0's reads, then r1's): one upload and one pass set
+int snapgpu_internal_align_batch_packed2(snapgpu_aligner_t *a, const snapgpu_reads_t *r0, const snapgpu_reads_t *r1,
+                                         uint32_t maxHitsToGet, snapgpu_result_t *out, int32_t *multiHitsFound,
+                                         std::vector<uint64_t> &off, std::vector<snapgpu_multi_hit_t> &dense);
 namespace snapgpu {
 
 // xoshiro256** seeded with splitmix64: deterministic on every host.

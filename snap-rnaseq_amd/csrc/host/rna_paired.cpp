@@ -397,7 +397,10 @@ struct RnaRun {
     snapgpu_reads_t *R[2];
     const snapgpu_rna_paired_options_t *opt;
     const std::vector<uint8_t> *useful;
-    std::mutex *mT, *mG;   // the transcriptome / genome aligner's lock
+    std::mutex *mT, *mG;   // the transcriptome / genome aligner's align calls
+    // their CIGAR / seed-census calls: the aligners' side stream and buffers (aligner.hip), so stage
+    // B of one sub-batch runs them while stage A of the next holds mT / mG
+    std::mutex *mTs, *mGs;
     const Ctx *C;
     bool bam;
 };
@@ -409,10 +412,12 @@ struct RnaSub {
     snapgpu_reads_t *U[2] = {nullptr, nullptr};
     std::vector<uint64_t> uo[2];
     std::vector<uint32_t> ul[2];
-    std::vector<snapgpu_result_t> tr[2];
-    std::vector<int32_t> tf[2];
-    std::vector<uint64_t> thOff[2];           // useful pair j's hits: th[k][thOff[k][j] .. thOff[k][j + 1])
-    std::vector<snapgpu_multi_hit_t> th[2];
+    // the transcriptome aligner's records of both ends, end k of useful pair j at k * nu + j, and
+    // its hits: th[thOff[k * nu + j] .. thOff[k * nu + j + 1])
+    std::vector<snapgpu_result_t> tr;
+    std::vector<int32_t> tf;
+    std::vector<uint64_t> thOff;
+    std::vector<snapgpu_multi_hit_t> th;
     std::vector<snapgpu_pair_result_t> gr;
     std::vector<FilterState> fs;              // per useful pair
     std::vector<GtfPairQuery> cq;             // count events (pointing into fs), input order
@@ -459,11 +464,10 @@ void rnaStageA(const RnaRun &Rr, RnaSub &X) {
         std::string terr;
         {
             std::lock_guard<std::mutex> lk(*Rr.mT);
-            for (int k = 0; k < 2 && rc == SNAPGPU_OK; k++) {
-                X.tr[k].resize(nu); X.tf[k].resize(nu);
-                rc = snapgpu_internal_align_batch_packed(Rr.ta, X.U[k], nullptr, Rr.opt->maxHitsToGet, X.tr[k].data(),
-                                                         X.tf[k].data(), X.thOff[k], X.th[k]);
-            }
+            // both ends in one call: one persistent-kernel tail instead of two
+            X.tr.resize(2 * nu); X.tf.resize(2 * nu);
+            rc = snapgpu_internal_align_batch_packed2(Rr.ta, X.U[0], X.U[1], Rr.opt->maxHitsToGet, X.tr.data(), X.tf.data(),
+                                                      X.thOff, X.th);
             if (rc) terr = snapgpu_last_error();
         }
         if (overlap) gt.join();
@@ -494,9 +498,9 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
         for (uint64_t j = b; j < e && errs[t].msg.empty(); j++) {
             mate0.clear(); mate1.clear();
             const uint32_t len0 = X.ul[0][j], len1 = X.ul[1][j];
-            for (int k = 0; k < 2; k++)
-                for (uint64_t h = X.thOff[k][j]; h < X.thOff[k][j + 1]; h++) {
-                    const snapgpu_multi_hit_t &m = X.th[k][h];
+            for (int k = 0; k < 2 && !X.thOff.empty(); k++)   // (no hits asked for: none recorded)
+                for (uint64_t h = X.thOff[k * nu + j]; h < X.thOff[k * nu + j + 1]; h++) {
+                    const snapgpu_multi_hit_t &m = X.th[h];
                     addAlignment(C, mate0, mate1, m.location, m.direction, m.score, 0, true, k == 1, len0, len1, errs[t]);
                 }
             const snapgpu_pair_result_t &g = X.gr[j];
@@ -535,7 +539,7 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
         cp.maxK = opt->maxDist;
         snapgpu_seed_runs_t *runs;
         {
-            std::lock_guard<std::mutex> lk(*Rr.mG);
+            std::lock_guard<std::mutex> lk(*Rr.mGs);
             runs = snapgpu_characterize_seeds(Rr.ga, both, nullptr, 0, &cp);
             if (!runs) X.fail(SNAPGPU_EDEVICE, snapgpu_last_error());
         }
@@ -671,7 +675,7 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
         int grc = SNAPGPU_OK, rc = SNAPGPU_OK;
         std::string gerr, terr;
         auto genomeCigars = [&] {
-            grc = gc.run(Rr.ga, cbase, (int)opt->useM, *Rr.mG);
+            grc = gc.run(Rr.ga, cbase, (int)opt->useM, *Rr.mGs);
             if (grc) gerr = snapgpu_last_error();
         };
         // one aligner's stream, events and upload state serve one host thread at a time: the two
@@ -679,7 +683,7 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
         const bool overlap = Rr.ta != Rr.ga;
         std::thread gt;
         if (overlap) gt = std::thread(genomeCigars);
-        rc = tc.run(Rr.ta, cbase, (int)opt->useM, *Rr.mT);
+        rc = tc.run(Rr.ta, cbase, (int)opt->useM, *Rr.mTs);
         if (rc) terr = snapgpu_last_error();
         if (overlap) gt.join();
         else if (rc == SNAPGPU_OK) genomeCigars();
@@ -895,21 +899,23 @@ int snapgpu_rna_paired_align(snapgpu_paired_aligner_t *pa, snapgpu_aligner_t *ta
     const size_t spl = samPath ? strlen(samPath) : 0;
     // BAM when the path ends in ".bam" (BAMFormat::writeRead for both ends, Bam.cpp:596-790)
     const bool bam = spl >= 4 && strcmp(samPath + spl - 4, ".bam") == 0;
-    // One aligner serves one host thread at a time: the stage-A align calls and the stage-B
-    // seed-census / CIGAR calls of the next sub-batch take the aligner's lock (ga also runs the
-    // paired aligner's single-end fallback).
-    std::mutex mG, mTown;
+    // One aligner's align calls serve one host thread at a time (mT / mG; ga also runs the paired
+    // aligner's single-end fallback), and so do its side-stream calls (seed census, CIGARs: mTs /
+    // mGs); the two kinds share no stream or buffer, so stage B of a sub-batch overlaps stage A of
+    // the next on the device too.
+    std::mutex mG, mTown, mGs, mTsOwn;
     std::mutex &mT = ta == ga ? mG : mTown;
-    RnaRun Rr{pa, ta, ga, gi, ti, gtf, {R[0], R[1]}, opt, &useful, &mT, &mG, &C, bam};
-    // Optional sub-batches of the pairs (SNAPGPU_RNA_SUBBATCH pairs each), pipelined: stage A (the
-    // GPU aligners) of sub-batch s + 1 runs while stage B (filter, seed census, counts, CIGARs,
-    // records) of sub-batch s runs on another thread.  Every stage keeps the reference's per-pair
-    // semantics; records and count events stay in input order across sub-batches.  Off by default:
-    // each aligner call pays the tail of its slowest read (the persistent kernels end with the
-    // heaviest repeat / multi-hit reads), so 7 sub-batches of 16k pairs made a 100k-pair batch 2x
-    // slower (alignMs 80 -> 230, profiles/r03/ab/rna_subbatch_ab.txt); the caller's batches are the
-    // unit of overlap instead.
-    uint64_t per = n ? n : 1;
+    std::mutex &mTs = ta == ga ? mGs : mTsOwn;
+    RnaRun Rr{pa, ta, ga, gi, ti, gtf, {R[0], R[1]}, opt, &useful, &mT, &mG, &mTs, &mGs, &C, bam};
+    // Sub-batches of the pairs, pipelined: stage A (the GPU aligners) of sub-batch s + 1 runs while
+    // stage B (filter, seed census, counts, CIGARs, records) of sub-batch s runs on another thread,
+    // its GPU calls on the aligners' side streams.  Every stage keeps the reference's per-pair
+    // semantics; records and count events stay in input order across sub-batches.  Each aligner call
+    // pays the tail of its slowest pair (a persistent kernel ends with its heaviest reads, even
+    // longest-first), so the split is coarse: two halves from 40k pairs up (100k 2 x 150 pairs:
+    // 77.0 -> 72.7 ms; three and four sub-batches 93.6 / 100.6 ms, profiles/r05/ab/rna_sub_r05k.txt).
+    // SNAPGPU_RNA_SUBBATCH = pairs per sub-batch overrides it.
+    uint64_t per = n >= 40000 ? (n + 1) / 2 : (n ? n : 1);
     if (const char *e = getenv("SNAPGPU_RNA_SUBBATCH"); e && atoll(e) > 0) per = (uint64_t)atoll(e);
     const uint64_t S = n ? (n + per - 1) / per : 0;
     std::vector<std::unique_ptr<RnaSub>> subs(S);

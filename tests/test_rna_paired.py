@@ -82,7 +82,8 @@ def _fastq_block(path, a, b, dst):
 @pytest.fixture
 def subbatch(request, monkeypatch):
     """SNAPGPU_RNA_SUBBATCH: pairs per pipelined sub-batch of snapgpu_rna_paired_align (None: the
-    default, one sub-batch; small values cut a block into several)."""
+    default, one sub-batch below 40k pairs -- these fixtures -- and two halves above; small values
+    cut a block into several)."""
     if request.param:
         monkeypatch.setenv("SNAPGPU_RNA_SUBBATCH", str(request.param))
     else:
