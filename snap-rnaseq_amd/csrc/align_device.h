@@ -339,7 +339,7 @@ struct GroupLdsT {
     uint64_t rpl[2][3][NW];              // read[dir] bit planes {hi, lo, notACGT}, positions 0..64*NW-1
     uint32_t ecache[EB][16];             // popped Elem64s (authoritative while in the batch)
     uint32_t eidx[EB];
-    uint16_t cand[CANDCAP];              // slot << 8 | bit
+    uint16_t cand[CANDCAP];              // cand_* encoding below
     // LV path per [direction][group * GS/2 + row] (a group of GS lanes runs at k < GS/2, so rows
     // 1..k fit its GS/2 slots; 32 per direction): matched-run length and action (0 X, 1 D, 2 I);
     // probabilities in apply
@@ -349,6 +349,15 @@ struct GroupLdsT {
     int8_t plen[2][8];                   //   path length (0: exact match, prob = perfect[patternLen])
 };
 using GroupLds = GroupLdsT<2>;
+// A candidate list entry: bit [5:0], the element's slot in the popped batch [8:6], and -- for a
+// candidate whose distances the forced-mode filter established (align_score.h forced_filter) --
+// known [9], forward distance [12:10], reverse distance [15:13] (7: above the filter's limit).
+__device__ __forceinline__ uint32_t cand_bit(uint32_t cw) { return cw & 63u; }
+__device__ __forceinline__ uint32_t cand_slot(uint32_t cw) { return (cw >> 6) & 7u; }
+__device__ __forceinline__ bool cand_known(uint32_t cw) { return (cw >> 9) & 1u; }
+__device__ __forceinline__ int cand_e1(uint32_t cw) { return (int)((cw >> 10) & 7u); }
+__device__ __forceinline__ int cand_e2(uint32_t cw) { return (int)((cw >> 13) & 7u); }
+static_assert(EB <= 8 && ELEM <= 64, "cand_* encoding: 3-bit slot, 6-bit bit");
 
 template <int MAXLEN>
 struct Lds {
@@ -743,7 +752,7 @@ enum : int { PH_SETUP = 0, PH_LOOKUP, PH_INSERT, PH_SCORE, PH_POP, PH_DESC, PH_S
              PH_WB, PH_OUT, PH_NPASS, PH_NCAND, PH_NREAD, PH_NPASS16, PH_NPASS32, PH_NPASS64, PH_ROWSF, PH_ROWSR,
              PH_NSCORECALL, PH_NFORCED, PH_NPOPPED, PH_NSUCC, PH_PASSLOOP, PH_SEL, PH_FETCH, PH_SEEDLOOP, PH_NBATCH,
              PH_RANK, PH_NELEMSF, PH_CANDL, PH_SUCC, PH_NEARBY, PH_PROB, PH_FAILS, PH_NFAILSTEP, PH_SUCCWB,
-             PH_NPASSF, PH_PASSLOOPF, PH_HEAVYCYC, PH_NHEAVY, PH_NCANDF, PH_READCYC,
+             PH_NPASSF, PH_PASSLOOPF, PH_HEAVYCYC, PH_NHEAVY, PH_NCANDF, PH_READCYC, PH_NFILTER,
              PH_SLOTS = 48 };
 __device__ __forceinline__ uint64_t clk() { return __builtin_amdgcn_s_memtime(); }
 #if SNAPGPU_PHASE_TIMERS

@@ -27,6 +27,7 @@
 // genome both hold IUPAC codes -- such reads are deferred to align_kernel<512>.
 #pragma once
 #include "align_device.h"
+#include "lv_lane.h"
 
 namespace sgk {
 
@@ -337,9 +338,9 @@ struct PassLane {
     uint32_t cw;       // candidate list entry (slot << 8 | bit)
 };
 
-// One speculative pass over up to G = 64/GS candidates [i0, i0+m) of the list.
+// One speculative pass over up to G = 64/GS candidates of the list: group gi takes cand[lvIdx[gi]].
 template <int GS, int MAXLEN>
-__device__ __forceinline__ void lv_pass(const KArgs &A, Lds<MAXLEN> &S, const Elem64 *ar, uint32_t i0, int m, int k,
+__device__ __forceinline__ void lv_pass(const KArgs &A, Lds<MAXLEN> &S, const Elem64 *ar, const uint16_t *lvIdx, int m, int k,
                                         uint32_t n, PassLane &P, int &e1, int &e2) {
     constexpr int NW = Lds<MAXLEN>::NW;
     GroupLdsT<NW> &G = S.grp[0];
@@ -349,8 +350,8 @@ __device__ __forceinline__ void lv_pass(const KArgs &A, Lds<MAXLEN> &S, const El
     P.act = gi < m;
     P.loc = 0; P.s = 0; P.glen = (int)n; P.dir = 0; P.cw = 0;
     if (P.act) {
-        const uint32_t cw = G.cand[i0 + gi];
-        const uint32_t sl = cw >> 8, bit = cw & 0xff;
+        const uint32_t cw = G.cand[lvIdx[gi]];
+        const uint32_t sl = cand_slot(cw), bit = cand_bit(cw);
         const uint32_t *ec = G.ecache[sl];
         const uint32_t key = ec[6], sp = spill_index(ec[11]);
         P.cw = cw;
@@ -425,179 +426,204 @@ __device__ __forceinline__ void lv_pass(const KArgs &A, Lds<MAXLEN> &S, const El
     PH_ADD(A, S, PH_LVR, tr);
 }
 
-// One LV pass over candidates [i0, i0+m) and their application in the reference's
-// order (BaseAligner.cpp:1129-1384).  Returns true when the read is finished
-// (stopOnFirstHit).  GS is a template parameter so group indexing is shifts and the
-// per-group loops unroll.
+// One LV pass over the candidates that need it and the in-order application of every candidate in
+// [i0, iEnd) of the batch's list (BaseAligner.cpp:1129-1384).  lvIdx[0..m) are the positions that
+// need LV -- those of unknown distances and those whose filter distances can still succeed at limit
+// k -- in list order, and [i0, iEnd) holds exactly those m of them; every other candidate of the
+// range has filter distances that fail at any limit <= k (align_score.h forced_filter).  Lane l of a
+// 64-position chunk applies position c0 + l with the limit in force at it.  Returns true when the
+// read is finished (stopOnFirstHit).  GS is a template parameter so group indexing is shifts and
+// the per-group loops unroll.
 constexpr int FETCH_NLD = (EB * Elem64::DWORDS + WAVE - 1) / WAVE;   // dwords per lane of a popped batch
 
+// the candidates that need an LV pass at limit k (the test pass_apply and the list gather share)
+__device__ __forceinline__ bool cand_needs_lv(uint32_t cw, int k) {
+    if (!cand_known(cw)) return true;
+    const int a = cand_e1(cw), b = cand_e2(cw);
+    return a <= k && b <= k - a;
+}
+
 template <int GS, bool EXT, int MAXLEN>
-__device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem64 *ar, ReadState &st, uint32_t i0, int m,
-                                           int k, uint32_t n, uint32_t nb, uint32_t &lastSlot, bool &lastSkip,
-                                           int *result) {
-    const int lane = lane_id();
+__device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem64 *ar, ReadState &st, uint32_t i0,
+                                           uint32_t iEnd, const uint16_t *lvIdx, int m, int k, uint32_t n, uint32_t nb,
+                                           uint32_t &lastSlot, bool &lastSkip, int *result) {
     auto &G = S.grp[0];
     const DevTables *tab = A.tab;
     PassLane P;
-    int e1, e2;
-    lv_pass<GS, MAXLEN>(A, S, ar, i0, m, k, n, P, e1, e2);
+    int e1 = -1, e2 = -1;
+    P.act = false; P.s = 0;
+    if (m > 0) lv_pass<GS, MAXLEN>(A, S, ar, lvIdx, m, k, n, P, e1, e2);
     PH_T(A, tapp);
-    // ---- apply in order with the limit in force at each candidate.  Group
-    // leaders (lane g*GS) hold candidate g.  A failure only sets its scored bit
-    // and, for an element's first scored candidate, bestLoc/bestScore/prob
-    // (BaseAligner.cpp:1253-1265 with score -1: nothing else changes), so the
-    // failures before the next success are applied together, lane-parallel.
-    const int gq = lane / GS;
-    const bool leader = (lane & (GS - 1)) == 0 && gq < m;
-    const uint32_t sl = P.cw >> 8, bit = P.cw & 0xff;
-    const uint32_t ew11 = leader ? G.ecache[sl][11] : 0u;
-    for (int g0 = 0; g0 < m;) {
-        const int lane = lane_id();   // re-read per step: `lane == c` masks are not hoisted and spilled
-        const int kNow = (int)(st.scoreLimit < (uint32_t)(MAX_K - 1) ? st.scoreLimit : MAX_K - 1);
-        // element lps test, made once when the element's first candidate is reached
-        // (BaseAligner.cpp:1129); candidates of one element are contiguous
-        const bool skip = sl == lastSlot ? lastSkip : ((ew11 >> 8) & 0xff) > st.scoreLimit;
-        const int lim2 = (int)st.scoreLimit - e1 > MAX_K - 1 ? MAX_K - 1 : (int)st.scoreLimit - e1;
-        const bool succ = leader && !skip && P.act && e1 >= 0 && e1 <= kNow && e2 >= 0 && e2 <= lim2;
-        const uint64_t sm = ballot(succ && gq >= g0);
-        const int gs = sm ? (int)__builtin_ctzll(sm) / GS : m;
-        const bool fail = leader && !skip && gq >= g0 && gq < gs;
-        const uint64_t fm = ballot(fail);
-        PH_T(A, tfl);
-        if (fm) {
-            // An element's candidates are contiguous in the list: its first failing
-            // candidate of this step records score -1 if nothing of the element was scored
-            // before; every failing candidate ORs its bit into candidatesScored (ds_or_b64).
-            const uint32_t prevSl = (uint32_t)shfl_idx((int)sl, lane >= GS ? lane - GS : lane);
-            uint32_t *ec = G.ecache[sl];
-            const bool was0 = fail && (gq == g0 || prevSl != sl) && (ec[2] | ec[3]) == 0;
-            if (fail) atomicOr(reinterpret_cast<unsigned long long *>(ec + 2), 1ull << bit);
-            if (was0) {
-                ec[9] = (ec[6] >> 1) * ELEM + bit;
-                ec[8] = FAIL_SCORE;
-                ec[4] = 0u;
-                ec[5] = 0u;
+    // ---- apply in order with the limit in force at each candidate.  A failure only sets its scored
+    // bit and, for an element's first scored candidate, bestLoc/bestScore/prob (BaseAligner.cpp:
+    // 1253-1265 with score -1: nothing else changes), so the failures before the next success are
+    // applied together, lane-parallel.
+    uint32_t gBase = 0;   // LV groups of the earlier chunks
+    for (uint32_t c0 = i0; c0 < iEnd; c0 += WAVE) {
+        const int lane = lane_id();   // re-read per chunk: `lane == x` masks are not hoisted and spilled
+        const uint32_t p = c0 + (uint32_t)lane;
+        const bool have = p < iEnd;
+        const uint32_t cw = have ? G.cand[p] : 0u;
+        const uint32_t sl = cand_slot(cw), bit = cand_bit(cw);
+        const bool lvd = have && cand_needs_lv(cw, k);
+        const uint64_t lvm = ballot(lvd);
+        const uint32_t g = gBase + (uint32_t)__popcll(lvm & ((1ull << lane) - 1));   // this position's LV group
+        const int src = (int)((g * GS) & 63u);
+        const int ge1 = shfl_idx(e1, src), ge2 = shfl_idx(e2, src), gact = shfl_idx(P.act ? 1 : 0, src);
+        const int re1 = lvd ? ge1 : (cand_e1(cw) == 7 ? -1 : cand_e1(cw));
+        const int re2 = lvd ? ge2 : (cand_e2(cw) == 7 ? -1 : cand_e2(cw));
+        const bool ract = lvd ? gact != 0 : true;
+        gBase += (uint32_t)__popcll(lvm);
+        const uint32_t ew11 = have ? G.ecache[sl][11] : 0u;
+        const int lastLane = (int)(iEnd - c0 < (uint32_t)WAVE ? iEnd - c0 : (uint32_t)WAVE) - 1;
+        for (int g0 = 0; g0 <= lastLane;) {
+            const int lane = lane_id();
+            const int kNow = (int)(st.scoreLimit < (uint32_t)(MAX_K - 1) ? st.scoreLimit : MAX_K - 1);
+            // element lps test, made once when the element's first candidate is reached
+            // (BaseAligner.cpp:1129); candidates of one element are contiguous
+            const bool skip = sl == lastSlot ? lastSkip : ((ew11 >> 8) & 0xff) > st.scoreLimit;
+            const int lim2 = (int)st.scoreLimit - re1 > MAX_K - 1 ? MAX_K - 1 : (int)st.scoreLimit - re1;
+            const bool succ = have && !skip && ract && re1 >= 0 && re1 <= kNow && re2 >= 0 && re2 <= lim2;
+            const uint64_t sm = ballot(succ && lane >= g0);
+            const int ls = sm ? (int)__builtin_ctzll(sm) : lastLane + 1;
+            const bool fail = have && !skip && lane >= g0 && lane < ls;
+            const uint64_t fm = ballot(fail);
+            PH_T(A, tfl);
+            if (fm) {
+                // An element's candidates are contiguous in the list: its first failing candidate of
+                // this step records score -1 if nothing of the element was scored before; every
+                // failing candidate ORs its bit into candidatesScored (ds_or_b64).
+                const uint32_t prevSl = (uint32_t)shfl_idx((int)sl, lane >= 1 ? lane - 1 : lane);
+                uint32_t *ec = G.ecache[sl];
+                const bool was0 = fail && (lane == g0 || prevSl != sl) && (ec[2] | ec[3]) == 0;
+                if (fail) atomicOr(reinterpret_cast<unsigned long long *>(ec + 2), 1ull << bit);
+                if (was0) {
+                    ec[9] = (ec[6] >> 1) * ELEM + bit;
+                    ec[8] = FAIL_SCORE;
+                    ec[4] = 0u;
+                    ec[5] = 0u;
+                }
+                sv_add(st, lane, SV_SCORED, (uint32_t)__popcll(fm));
+                wave_sync();
+                PH_ADD(A, S, PH_FAILS, tfl);
+                PH_CNT(A, S, PH_NFAILSTEP, 1);
             }
-            sv_add(st, lane, SV_SCORED, (uint32_t)__popcll(fm));
-            wave_sync();
-            PH_ADD(A, S, PH_FAILS, tfl);
-            PH_CNT(A, S, PH_NFAILSTEP, 1);
-        }
-        if (gs >= m) {
-            lastSlot = readlaneu(sl, (m - 1) * GS);
-            lastSkip = readlane(skip ? 1 : 0, (m - 1) * GS) != 0;
-            break;
-        }
-        lastSlot = readlaneu(sl, gs * GS);
-        lastSkip = false;
-        PH_T(A, tsu);
-        // ---- the success at group gs: full bookkeeping (BaseAligner.cpp:1227-1384)
-        const int ln = gs * GS;
-        const uint32_t csl = readlaneu(sl, ln), cbit = readlaneu(bit, ln);
-        const int r1 = readlane(e1, ln), r2 = readlane(e2, ln);
-        const uint32_t ev = lane < 12 ? G.ecache[csl][lane] : 0u;
-        uint64_t cScored = rl64(ev, 2);
-        const double cProb = rld(ev, 4);
-        const uint32_t cKey = rl(ev, 6), cBest = rl(ev, 8);
-        const uint32_t sc = (uint32_t)(r1 + r2);
-        PH_CNT(A, S, PH_NSUCC, 1);
-        const int s0 = readlane(P.s, ln), t0 = s0 + (int)A.seedLen;
-        const uint32_t dir = cKey & 1;
-        const uint32_t ebase = (cKey >> 1) * ELEM;
-        const uint32_t elemLoc = ebase + cbit;
-        // the nearby element (BaseAligner.cpp:1272-1331) does not depend on the match probability:
-        // found and loaded before lv_prob_pair, so its chain walk and load overlap the product
-        uint32_t nbPre;
-        int csPre = -1;
-        uint32_t nvPre = 0;
-        PH_T(A, tnb);
-        {
-            const uint32_t nl = elemLoc + (2 * (elemLoc % ELEM / (ELEM / 2)) - 1) * (ELEM / 2);
-            const uint32_t nkey = ((nl / ELEM) << 1) | dir;
-            nbPre = uni(chain_find(A, S, ar, nkey, (uint32_t)A.arenaElems));
-            if (nbPre != NONE) {
-                const uint64_t inb = ballot((uint32_t)lane < nb && G.eidx[lane < EB ? lane : 0] == nbPre);
-                csPre = inb ? (int)__builtin_ctzll(inb) : -1;
-                if (csPre >= 0) nvPre = lane < 12 ? G.ecache[csPre][lane] : 0u;
-                else if (nbPre < ELCAP) nvPre = lane < 12 ? S.eloc[nbPre][lane] : 0u;
-                else nvPre = lane < 12 ? ((const uint32_t *)(ar + nbPre))[lane] : 0u;
+            if (ls > lastLane) {
+                lastSlot = readlaneu(sl, lastLane);
+                lastSkip = readlane(skip ? 1 : 0, lastLane) != 0;
+                break;
             }
-        }
-        PH_ADD(A, S, PH_NEARBY, tnb);
-        PH_T(A, tpr);
-        double q1, q2;
-        int net2;
-        lv_prob_pair(tab, G, gs, gs * (GS / 2), (int)n, s0, t0, S.fwdQ, dir, q1, q2, net2);
-        const double prob = q1 * q2 * tab->seedProb;
-        PH_ADD(A, S, PH_PROB, tpr);
-        PH_T(A, twt);
-        const uint32_t loc = elemLoc + (uint32_t)net2;
-        const bool anyNearby0 = cScored != 0;
-        cScored |= 1ull << cbit;
-        record_hit<EXT>(A, loc, dir, sc);
-        sv_add(st, lane, SV_SCORED, 1);
-        g0 = gs + 1;
-        const bool passA = !(anyNearby0 && (cBest < sc || (cBest == sc && prob <= cProb)));
-        bool take = passA;
-        uint32_t nb2 = NONE;
-        int cs = -1;
-        uint32_t nv = 0;
-        if (take) { nb2 = nbPre; cs = csPre; nv = nvPre; }
-        if (nb2 != NONE) {
-            // the nearby element may be in this batch: its cache is authoritative (read above)
-            if (rl64(nv, 2) == 0) nb2 = NONE;   // nearby element not scored yet
-            if (nb2 != NONE) {
-                const uint32_t nbase = (rl(nv, 6) >> 1) * ELEM;
-                const uint32_t nbl = rl(nv, 9);
-                if (!((nbase > ebase && loc - nbl <= (uint32_t)ELEM) || (nbase < ebase && nbl <= (uint32_t)ELEM)))
-                    nb2 = NONE;   // sic: BaseAligner.cpp:1311-1312
-            }
-            if (nb2 != NONE) {
-                const uint32_t nbs = rl(nv, 8);
-                const double np = rld(nv, 4);
-                if (nbs < sc || (nbs == sc && np >= prob)) take = false;
-                else {
-                    st.pAll = st.pAll - np > 0.0 ? st.pAll - np : 0.0;
-                    if (cs >= 0) { if (lane == 4 || lane == 5) G.ecache[cs][lane] = 0u; }
-                    else if (nb2 < ELCAP) { if (lane == 4 || lane == 5) S.eloc[nb2][lane] = 0u; }
-                    else if (lane == 4 || lane == 5) ((uint32_t *)(ar + nb2))[lane] = 0u;
+            lastSlot = readlaneu(sl, ls);
+            lastSkip = false;
+            PH_T(A, tsu);
+            // ---- the success at position lane ls (LV group gs): full bookkeeping (BaseAligner.cpp:1227-1384)
+            const uint32_t csl = readlaneu(sl, ls), cbit = readlaneu(bit, ls);
+            const int r1 = readlane(re1, ls), r2 = readlane(re2, ls);
+            const int gs = readlane((int)g, ls);
+            const uint32_t ev = lane < 12 ? G.ecache[csl][lane] : 0u;
+            uint64_t cScored = rl64(ev, 2);
+            const double cProb = rld(ev, 4);
+            const uint32_t cKey = rl(ev, 6), cBest = rl(ev, 8);
+            const uint32_t sc = (uint32_t)(r1 + r2);
+            PH_CNT(A, S, PH_NSUCC, 1);
+            const int s0 = readlane(P.s, gs * GS), t0 = s0 + (int)A.seedLen;
+            const uint32_t dir = cKey & 1;
+            const uint32_t ebase = (cKey >> 1) * ELEM;
+            const uint32_t elemLoc = ebase + cbit;
+            // the nearby element (BaseAligner.cpp:1272-1331) does not depend on the match probability:
+            // found and loaded before lv_prob_pair, so its chain walk and load overlap the product
+            uint32_t nbPre;
+            int csPre = -1;
+            uint32_t nvPre = 0;
+            PH_T(A, tnb);
+            {
+                const uint32_t nl = elemLoc + (2 * (elemLoc % ELEM / (ELEM / 2)) - 1) * (ELEM / 2);
+                const uint32_t nkey = ((nl / ELEM) << 1) | dir;
+                nbPre = uni(chain_find(A, S, ar, nkey, (uint32_t)A.arenaElems));
+                if (nbPre != NONE) {
+                    const uint64_t inb = ballot((uint32_t)lane < nb && G.eidx[lane < EB ? lane : 0] == nbPre);
+                    csPre = inb ? (int)__builtin_ctzll(inb) : -1;
+                    if (csPre >= 0) nvPre = lane < 12 ? G.ecache[csPre][lane] : 0u;
+                    else if (nbPre < ELCAP) nvPre = lane < 12 ? S.eloc[nbPre][lane] : 0u;
+                    else nvPre = lane < 12 ? ((const uint32_t *)(ar + nbPre))[lane] : 0u;
                 }
             }
-        }
-        // write the element back (scored always; the rest only when taken)
-        {
-            const uint64_t pb = (uint64_t)__double_as_longlong(prob);
-            uint32_t *ec = G.ecache[csl];
-            if (lane == 2) ec[2] = (uint32_t)cScored;
-            else if (lane == 3) ec[3] = (uint32_t)(cScored >> 32);
-            // bestScoreGenomeLocation is set once the candidate passed the first check (:1266-1268)
-            if (lane == 9 && passA) ec[9] = loc;
-            if (take) {
-                if (lane == 4) ec[4] = (uint32_t)pb;
-                else if (lane == 5) ec[5] = (uint32_t)(pb >> 32);
-                else if (lane == 8) ec[8] = sc;
+            PH_ADD(A, S, PH_NEARBY, tnb);
+            PH_T(A, tpr);
+            double q1, q2;
+            int net2;
+            lv_prob_pair(tab, G, gs, gs * (GS / 2), (int)n, s0, t0, S.fwdQ, dir, q1, q2, net2);
+            const double prob = q1 * q2 * tab->seedProb;
+            PH_ADD(A, S, PH_PROB, tpr);
+            PH_T(A, twt);
+            const uint32_t loc = elemLoc + (uint32_t)net2;
+            const bool anyNearby0 = cScored != 0;
+            cScored |= 1ull << cbit;
+            record_hit<EXT>(A, loc, dir, sc);
+            sv_add(st, lane, SV_SCORED, 1);
+            g0 = ls + 1;
+            const bool passA = !(anyNearby0 && (cBest < sc || (cBest == sc && prob <= cProb)));
+            bool take = passA;
+            uint32_t nb2 = NONE;
+            int cs = -1;
+            uint32_t nv = 0;
+            if (take) { nb2 = nbPre; cs = csPre; nv = nvPre; }
+            if (nb2 != NONE) {
+                // the nearby element may be in this batch: its cache is authoritative (read above)
+                if (rl64(nv, 2) == 0) nb2 = NONE;   // nearby element not scored yet
+                if (nb2 != NONE) {
+                    const uint32_t nbase = (rl(nv, 6) >> 1) * ELEM;
+                    const uint32_t nbl = rl(nv, 9);
+                    if (!((nbase > ebase && loc - nbl <= (uint32_t)ELEM) || (nbase < ebase && nbl <= (uint32_t)ELEM)))
+                        nb2 = NONE;   // sic: BaseAligner.cpp:1311-1312
+                }
+                if (nb2 != NONE) {
+                    const uint32_t nbs = rl(nv, 8);
+                    const double np = rld(nv, 4);
+                    if (nbs < sc || (nbs == sc && np >= prob)) take = false;
+                    else {
+                        st.pAll = st.pAll - np > 0.0 ? st.pAll - np : 0.0;
+                        if (cs >= 0) { if (lane == 4 || lane == 5) G.ecache[cs][lane] = 0u; }
+                        else if (nb2 < ELCAP) { if (lane == 4 || lane == 5) S.eloc[nb2][lane] = 0u; }
+                        else if (lane == 4 || lane == 5) ((uint32_t *)(ar + nb2))[lane] = 0u;
+                    }
+                }
             }
-            wave_sync();
+            // write the element back (scored always; the rest only when taken)
+            {
+                const uint64_t pb = (uint64_t)__double_as_longlong(prob);
+                uint32_t *ec = G.ecache[csl];
+                if (lane == 2) ec[2] = (uint32_t)cScored;
+                else if (lane == 3) ec[3] = (uint32_t)(cScored >> 32);
+                // bestScoreGenomeLocation is set once the candidate passed the first check (:1266-1268)
+                if (lane == 9 && passA) ec[9] = loc;
+                if (take) {
+                    if (lane == 4) ec[4] = (uint32_t)pb;
+                    else if (lane == 5) ec[5] = (uint32_t)(pb >> 32);
+                    else if (lane == 8) ec[8] = sc;
+                }
+                wave_sync();
+            }
+            PH_ADD(A, S, PH_SUCCWB, twt);
+            if (!take) { PH_ADD(A, S, PH_SUCC, tsu); continue; }
+            st.pAll = st.pAll - cProb > 0.0 ? st.pAll - cProb : 0.0;
+            st.pAll += prob;
+            if (st.bestScore > sc || (st.bestScore == sc && prob > st.pBest)) {
+                st.bestScore = sc;
+                st.pBest = prob;
+                st.bestLoc = loc;
+                st.outLoc = loc;
+                st.outScore = (int32_t)sc;
+                st.outDir = dir;
+            }
+            if (A.stopOnFirst && st.bestScore <= A.maxK) {
+                *result = SNAPGPU_MULTIPLE_HITS;
+                st.outMapq = 0;
+                return true;
+            }
+            st.scoreLimit = (st.bestScore < A.maxK ? st.bestScore : A.maxK) + A.extra;
+            PH_ADD(A, S, PH_SUCC, tsu);
         }
-        PH_ADD(A, S, PH_SUCCWB, twt);
-        if (!take) { PH_ADD(A, S, PH_SUCC, tsu); continue; }
-        st.pAll = st.pAll - cProb > 0.0 ? st.pAll - cProb : 0.0;
-        st.pAll += prob;
-        if (st.bestScore > sc || (st.bestScore == sc && prob > st.pBest)) {
-            st.bestScore = sc;
-            st.pBest = prob;
-            st.bestLoc = loc;
-            st.outLoc = loc;
-            st.outScore = (int32_t)sc;
-            st.outDir = dir;
-        }
-        if (A.stopOnFirst && st.bestScore <= A.maxK) {
-            *result = SNAPGPU_MULTIPLE_HITS;
-            st.outMapq = 0;
-            return true;
-        }
-        st.scoreLimit = (st.bestScore < A.maxK ? st.bestScore : A.maxK) + A.extra;
-        PH_ADD(A, S, PH_SUCC, tsu);
     }
     PH_ADD(A, S, PH_APPLY, tapp);
     return false;
@@ -684,6 +710,107 @@ __device__ __forceinline__ bool forced_sort(const KArgs &A, Lds<MAXLEN> &S, Elem
     return true;
 }
 
+// ------------------------------------------------------------ forced-mode prefilter
+// In forced mode the pop order is fixed (above) and a repeat-rich read pops hundreds of elements,
+// most with one unscored candidate whose LV calls fail: lv_group would spend a pass per 4-8 of them
+// just to establish "distance > k".  forced_filter takes the next 32 elements of the order, one per
+// lane pair, and computes the distances of each one's first unscored candidate with lv_lane.h
+// (lv_pair_dist: a pair's 11 diagonals as 128-bit masks in registers, 6 per lane) at the limit k of
+// the moment.  The limit only shrinks, so a distance above it fails at every later limit too: those
+// candidates are applied as failures without an LV pass (pass_apply); the rest -- possible successes,
+// which need their LV path for the match probability -- still go through lv_group.  Result per lane:
+// FRES_VALID | bit | e1 << 8 | e2 << 11 (7: above the limit), 0 when the lane's element has no
+// candidate the filter can settle (none unscored, lps above the limit, or a window short of n + MAX_K
+// bases at a contig end, whose text bound lv_group handles).
+constexpr int FKM = 5;                     // lv_lane.h KM: the filter runs at limits k <= 5 (6 and 7 cut more
+                                           // instructions, but their masks' spills cost more: prefilter_range_r05m.txt)
+constexpr uint32_t FILTER_MIN = 16;        // elements left in the order for a filter pass to pay off
+constexpr uint32_t FWIN = WAVE / 2;        // pop-order positions per filter pass (a lane pair each)
+constexpr uint32_t FRES_VALID = 1u << 31;
+
+template <int MAXLEN>
+__device__ __forceinline__ uint32_t forced_filter(const KArgs &A, Lds<MAXLEN> &S, const Elem64 *ar, const ReadState &st,
+                                                  uint32_t n, const uint64_t *fSorted, uint32_t fAvail,
+                                                  const uint16_t *order, uint32_t ordBase, uint32_t pos0, uint32_t cnt,
+                                                  int k) {
+    static_assert(Lds<MAXLEN>::NW == 2, "forced_filter: 128-bit masks");
+    const int lane = lane_id();
+    const int c = lane >> 1, h = lane & 1;   // the lane pair (2c, 2c + 1) takes pop-order position pos0 + c
+    const uint32_t pos = pos0 + (uint32_t)c;
+    bool act = (uint32_t)c < cnt;
+    uint32_t e = 0;
+    if (act) e = fSorted ? (uint32_t)fSorted[fAvail - 1 - pos] : (uint32_t)order[pos - ordBase];
+    // the header words it needs: used, scored (dw 0-3), key (6), w11 (11), the slots (12-15)
+    uint4 h0 = make_uint4(0u, 0u, 0u, 0u), h3 = h0;
+    uint32_t key = 0, w11 = 0;
+    if (act) {
+        const uint32_t *hp = e < ELCAP ? S.eloc[e < ELCAP ? e : 0] : reinterpret_cast<const uint32_t *>(ar + e);
+        h0 = reinterpret_cast<const uint4 *>(hp)[0];
+        key = hp[6];
+        w11 = hp[11];
+        h3 = reinterpret_cast<const uint4 *>(hp)[3];
+    }
+    const uint64_t pend = (((uint64_t)h0.y << 32) | h0.x) & ~(((uint64_t)h0.w << 32) | h0.z);
+    act = act && pend != 0 && ((w11 >> 8) & 0xffu) <= st.scoreLimit;
+    const uint32_t bit = act ? (uint32_t)__builtin_ctzll(pend) : 0u;
+    const uint32_t loc = (key >> 1) * ELEM + bit, dir = key & 1u;
+    const uint32_t sp = spill_index(w11);
+    int s = 0;
+    if (act) s = (int)(sp ? (uint32_t)reinterpret_cast<const uint8_t *>(ar + sp)[bit] : slot_offset(h3.x, h3.y, h3.z, h3.w, bit));
+    act = act && substring_ok(A, loc, n + MAX_K);
+    // this half's masks: local i = forward diagonal x = h ? i : -i,
+    // F_x[m] = read[dir][m] != genome[loc + x + m] on the bit planes
+    uint64_t F[FKM + 1][2];
+    {
+        const int64_t gp = (int64_t)loc - FKM + PACK_GUARD;
+        const GPlane *src = A.gpl + (act ? (gp >> 5) : 0);
+        const uint32_t sh = (uint32_t)gp & 31;
+        uint32_t wh[6], wl[6], wm[6];
+#pragma unroll
+        for (int j = 0; j < 6; j++) {
+            const GPlane w = src[j];
+            wh[j] = w.hi; wl[j] = w.lo; wm[j] = w.nm;
+        }
+        uint32_t ah[5], al[5], am[5];   // the genome planes from position loc - FKM, 160 bits
+#pragma unroll
+        for (int j = 0; j < 5; j++) {
+            ah[j] = __builtin_amdgcn_alignbit(wh[j + 1], wh[j], sh);
+            al[j] = __builtin_amdgcn_alignbit(wl[j + 1], wl[j], sh);
+            am[j] = __builtin_amdgcn_alignbit(wm[j + 1], wm[j], sh);
+        }
+        const uint64_t *rp = &S.grp[0].rpl[dir][0][0];
+        uint32_t rh[4], rl_[4], rm[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            rh[j] = (uint32_t)(rp[j / 2] >> (32 * (j & 1)));
+            rl_[j] = (uint32_t)(rp[2 + j / 2] >> (32 * (j & 1)));
+            rm[j] = (uint32_t)(rp[4 + j / 2] >> (32 * (j & 1)));
+        }
+#pragma unroll
+        for (int i = 0; i <= FKM; i++) {   // the window shifted by FKM + x bits
+            const uint32_t cs = (uint32_t)(h ? FKM + i : FKM - i);
+            uint32_t f[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t gh = __builtin_amdgcn_alignbit(ah[j + 1], ah[j], cs);
+                const uint32_t gl = __builtin_amdgcn_alignbit(al[j + 1], al[j], cs);
+                const uint32_t gm = __builtin_amdgcn_alignbit(am[j + 1], am[j], cs);
+                f[j] = (gh ^ rh[j]) | (gl ^ rl_[j]) | gm | rm[j];
+            }
+            F[i][0] = ((uint64_t)f[1] << 32) | f[0];
+            F[i][1] = ((uint64_t)f[3] << 32) | f[2];
+        }
+    }
+    const int t = s + (int)A.seedLen;
+    const int e1 = lv_pair_dist<FKM, 1>(F, h, act, t, (int)n - t, (int)n + MAX_K - t, k);
+    int e2 = -1;
+    if (ballot(e1 >= 0)) {
+        // reverse LV: pattern = read[s-1 .. 0], text = genome backwards from loc + s - 1 (BaseAligner.cpp:1216-1220)
+        e2 = lv_pair_dist<FKM, -1>(F, h, e1 >= 0, 127 - (s - 1), s, s + MAX_K, k - e1);
+    }
+    return act ? FRES_VALID | bit | (uint32_t)(e1 < 0 ? 7 : e1) << 8 | (uint32_t)(e2 < 0 ? 7 : e2) << 11 : 0u;
+}
+
 // BaseAligner::score (BaseAligner.cpp:977-1399) over batches of popped elements.
 template <bool EXT, int MAXLEN>
 __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, Elem64 *ar, ReadState &st, bool force,
@@ -707,6 +834,8 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, El
     uint32_t fDone = 0, fAvail = 0, ordBase = 0;
     bool fMore = true;   // a ranking window came back full: elements of lower rank may remain
     const uint64_t *fSorted = nullptr;   // radix-sorted pop order (reads with >= A.radixMin elements)
+    // forced_filter's window over pop-order positions [wBase, wEnd): lanes 2j, 2j + 1 hold position wBase + j
+    uint32_t fres = 0, wBase = 0, wEnd = 0;
     for (uint32_t guard = 0;; guard++) {
         // lane id re-read per batch (volatile asm): masks and addresses derived from it are
         // recomputed in the batch instead of hoisted and kept live, spilled, across the pass loop
@@ -718,7 +847,7 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, El
         if (overdue(A, st, 1)) return true;
         PH_T(A, tpop);
         // ---- pop in weight-list order (head of the highest list first); LDS only
-        uint32_t nb = 0;
+        uint32_t nb = 0, posb = 0;   // batch size, its first pop-order position (forced mode)
         if (!forced) {
             // sort keys are unique: reduce the 32-bit keys, then take the owner lane's index
             const uint64_t lm = S.laneMax[lane];
@@ -780,6 +909,17 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, El
                 wave_sync();
                 PH_ADD(A, S, PH_RANK, trk);
             }
+            if constexpr (Lds<MAXLEN>::NW == 2) {
+                const int kf = st.scoreLimit < (uint32_t)(MAX_K - 1) ? (int)st.scoreLimit : MAX_K - 1;
+                if (fDone >= wEnd && kf <= FKM && fAvail - fDone >= FILTER_MIN) {
+                    const uint32_t cnt = fAvail - fDone < (uint32_t)FWIN ? fAvail - fDone : (uint32_t)FWIN;
+                    fres = forced_filter<MAXLEN>(A, S, ar, st, n, fSorted, fAvail, order, ordBase, fDone, cnt, kf);
+                    wBase = fDone;
+                    wEnd = fDone + cnt;
+                    PH_CNT(A, S, PH_NFILTER, 1);
+                }
+            }
+            posb = fDone;
             nb = fAvail - fDone < (uint32_t)EB ? fAvail - fDone : (uint32_t)EB;
             if ((uint32_t)lane < nb)
                 G.eidx[lane] = fSorted ? (uint32_t)fSorted[fAvail - 1 - (fDone + (uint32_t)lane)]
@@ -827,6 +967,13 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, El
                     pend = (((uint64_t)ec[1] << 32) | ec[0]) & ~(((uint64_t)ec[3] << 32) | ec[2]);
             }
             const uint32_t cnt = (uint32_t)__popcll(pend);
+            // the filter's result for this element (pop-order position posb + lane), if in its window
+            const uint32_t wl = posb + (uint32_t)lane - wBase;
+            const uint32_t fr = (uint32_t)shfl_idx((int)fres, (int)(2u * (wl & (FWIN - 1))));
+            const bool inWin = forced && posb + (uint32_t)lane >= wBase && posb + (uint32_t)lane < wEnd &&
+                               (uint32_t)lane < nb && (fr & FRES_VALID);
+            const uint32_t known = inWin ? (1u << 9) | ((fr >> 8) & 7u) << 10 | ((fr >> 11) & 7u) << 13 : 0u;
+            const uint32_t kbit = fr & 63u;
             // exclusive prefix sum over lanes 0..EB-1
             uint32_t pos = 0;
 #pragma unroll
@@ -838,7 +985,7 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, El
             while (pend) {
                 const int bit = __builtin_ctzll(pend);
                 pend &= pend - 1;
-                G.cand[pos++] = (uint16_t)(lane << 8 | bit);
+                G.cand[pos++] = (uint16_t)((uint32_t)bit | (uint32_t)lane << 6 | ((uint32_t)bit == kbit ? known : 0u));
             }
             wave_sync();
         }
@@ -849,21 +996,40 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, El
         PH_T(A, tpl);
         uint32_t lastSlot = NONE;   // element of the last candidate reached, and its lps decision
         bool lastSkip = false;
+        // the LV list of a pass (positions into cand, list order) in an LV row the scorer never
+        // reaches at the limits that fill it (k <= 15 uses rows 1..15)
+        uint16_t *lvIdx = reinterpret_cast<uint16_t *>(&S.u.sc.rows8[MAX_K - 2][0]);
         for (uint32_t i0 = 0; i0 < nc;) {
             if (overdue(A, st, 2)) return true;
             const int k = st.scoreLimit < (uint32_t)(MAX_K - 1) ? (int)st.scoreLimit : MAX_K - 1;
             const int GS = k <= 3 ? 8 : (k <= 7 ? 16 : (k <= 15 ? 32 : 64));
             const int Gn = 64 / GS;
-            const int m = (int)(nc - i0) < Gn ? (int)(nc - i0) : Gn;
-            PH_CNT(A, S, PH_NPASS, 1);
-            if (forced) PH_CNT(A, S, PH_NPASSF, 1);
+            // the next Gn candidates that need LV (unknown distances, or filter distances that can still
+            // succeed at k); the pass applies everything up to the last of them (the end when fewer)
+            int m = 0;
+            for (uint32_t c0 = i0; c0 < nc && m < Gn; c0 += WAVE) {
+                const int lane = lane_id();
+                const uint32_t p = c0 + (uint32_t)lane;
+                const bool need = p < nc && cand_needs_lv(G.cand[p], k);
+                const uint64_t nm = ballot(need);
+                const int r = m + __popcll(nm & ((1ull << lane) - 1));
+                if (need && r < Gn) lvIdx[r] = (uint16_t)p;
+                m += __popcll(nm);
+                m = m < Gn ? m : Gn;
+            }
+            wave_sync();
+            const uint32_t iEnd = m == Gn ? (uint32_t)lvIdx[Gn - 1] + 1u : nc;
+            if (m > 0) {
+                PH_CNT(A, S, PH_NPASS, 1);
+                if (forced) PH_CNT(A, S, PH_NPASSF, 1);
+            }
             bool fin;
-            if (GS == 8) fin = pass_apply<8, EXT>(A, S, ar, st, i0, m, k, n, nb, lastSlot, lastSkip, result);
-            else if (GS == 16) fin = pass_apply<16, EXT>(A, S, ar, st, i0, m, k, n, nb, lastSlot, lastSkip, result);
-            else if (GS == 32) fin = pass_apply<32, EXT>(A, S, ar, st, i0, m, k, n, nb, lastSlot, lastSkip, result);
-            else fin = pass_apply<64, EXT>(A, S, ar, st, i0, m, k, n, nb, lastSlot, lastSkip, result);
+            if (GS == 8) fin = pass_apply<8, EXT>(A, S, ar, st, i0, iEnd, lvIdx, m, k, n, nb, lastSlot, lastSkip, result);
+            else if (GS == 16) fin = pass_apply<16, EXT>(A, S, ar, st, i0, iEnd, lvIdx, m, k, n, nb, lastSlot, lastSkip, result);
+            else if (GS == 32) fin = pass_apply<32, EXT>(A, S, ar, st, i0, iEnd, lvIdx, m, k, n, nb, lastSlot, lastSkip, result);
+            else fin = pass_apply<64, EXT>(A, S, ar, st, i0, iEnd, lvIdx, m, k, n, nb, lastSlot, lastSkip, result);
             if (fin) return true;
-            i0 += (uint32_t)m;
+            i0 = iEnd;
         }
         PH_ADD(A, S, PH_PASSLOOP, tpl);
         if (forced) { PH_ADD(A, S, PH_PASSLOOPF, tpl); PH_CNT(A, S, PH_NCANDF, nc); }

@@ -737,9 +737,11 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
 }
 
 template <int MAXLEN, bool EXT>
-// amdgpu_waves_per_eu(3): keep <= 168 VGPRs (3 waves/SIMD, 12 per CU); a few cold spills
-// are cheaper than dropping to 2 waves/SIMD.
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MAXLEN <= 256 ? 4 : 3))) void align_kernel(KArgs A) {
+// amdgpu_waves_per_eu: <128> at 5 waves/SIMD (<= 96 VGPRs: the forced-mode prefilter's peak costs
+// ~10 VGPRs of spills around it, 2.5 % faster than 4 waves without them,
+// profiles/r05/ab/prefilter_pairs_r05l.txt), <256> at 4, <512> at 3 (<= 168 VGPRs: a few cold
+// spills are cheaper than dropping to 2 waves/SIMD).
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MAXLEN <= 128 ? 5 : (MAXLEN <= 256 ? 4 : 3)))) void align_kernel(KArgs A) {
     __shared__ Lds<MAXLEN> S;
     ElemOf<MAXLEN> *ar = reinterpret_cast<ElemOf<MAXLEN> *>(A.arena) + (uint64_t)blockIdx.x * A.arenaElems;
     const int lane = lane_id();

@@ -30,16 +30,33 @@ __host__ __device__ __forceinline__ int ll_first_from(uint64_t w0, uint64_t w1, 
     return 64 + __builtin_ctzll(w1);
 }
 
-__host__ __device__ __forceinline__ uint64_t ll_brev64(uint64_t x) {
-    return ((uint64_t)__builtin_bitreverse32((uint32_t)x) << 32) | __builtin_bitreverse32((uint32_t)(x >> 32));
+// last set position <= m1 of a 128-bit mask, -1 if none; m1 in [-1, 127]
+__host__ __device__ __forceinline__ int ll_last_upto(uint64_t w0, uint64_t w1, int m1) {
+    if (m1 < 0) return -1;
+    const uint64_t x1 = m1 >= 64 ? w1 & (~0ull >> (127 - m1)) : 0ull;
+    if (x1) return 127 - __builtin_clzll(x1);
+    const uint64_t x0 = w0 & (m1 >= 63 ? ~0ull : ~0ull >> (63 - m1));
+    return x0 ? 63 - __builtin_clzll(x0) : -1;
+}
+
+// "first set position >= p" of the direction's mask of diagonal d.  DIR = 1: the forward mask
+// M[d].  DIR = -1: the bit-reversed mask of forward diagonal -d (R[p] = F[127 - p], as lv_pass's
+// mk_reverse builds it), read from the forward mask by a "last set <= 127 - p" query, so no reversed
+// copy is held.  p in [0, 128]; 128 if none.
+template <int KM, int DIR>
+__host__ __device__ __forceinline__ int ll_first_dir(const uint64_t (&M)[2 * KM + 1][2], int d, int p) {
+    if (DIR > 0) return ll_first_from(M[d + KM][0], M[d + KM][1], p);
+    return 127 - ll_last_upto(M[KM - d][0], M[KM - d][1], 127 - p);
 }
 
 // Distance of pattern mask positions q0 .. q0 + patternLen against the text (diagonal d of the
-// lane's mask M[d + KM], d in [-KM, KM]), limit k <= KM; -1 when above k.  `act` false: -1.
+// lane's masks, d in [-KM, KM], through ll_first_dir<KM, DIR>: for DIR = -1 the positions are those
+// of the reversed masks, q0 = 127 - (first pattern base's forward position)), limit k <= KM; -1 when
+// above k.  `act` false: -1.
 // Mirrors lv_group<1, GS, 2>: end0 / exact prefix (LandauVishkin.h:290-305), then rows 1..k with
 // best = max(L[d-1], L[d] + 1, L[d+1] + 1), the slide capped at endd = min(patternLen, textLen - d),
 // and the `best >= endd` case as there.
-template <int KM>
+template <int KM, int DIR = 1>
 __host__ __device__ __forceinline__ int lv_lane_dist(const uint64_t (&M)[2 * KM + 1][2], bool act, int q0, int patternLen,
                                                     int textLen, int k) {
     constexpr int NBITS = 128;
@@ -47,7 +64,7 @@ __host__ __device__ __forceinline__ int lv_lane_dist(const uint64_t (&M)[2 * KM 
     if (k > KM) k = KM;
     const int end0 = patternLen < textLen ? patternLen : textLen;
     {
-        const int fm = ll_first_from(M[KM][0], M[KM][1], q0) - q0;
+        const int fm = ll_first_dir<KM, DIR>(M, 0, q0) - q0;
         const int v0 = fm < end0 ? fm : end0;
         if (v0 == end0) {
             const int result = patternLen > end0 ? patternLen - end0 : 0;
@@ -62,48 +79,107 @@ __host__ __device__ __forceinline__ int lv_lane_dist(const uint64_t (&M)[2 * KM 
 #pragma unroll
         for (int e = 1; e <= KM; e++) {
             if (e > k) break;
-            int Bn[2 * KM + 3];
-#pragma unroll
-            for (int i = 0; i < 2 * KM + 3; i++) Bn[i] = B[i];
+            // row e from row e-1 in place: `left` carries the old value of the diagonal below
             bool hit = false;
+            int left = B[KM - e];   // old B[d - 1] of the band's first diagonal d = -e
 #pragma unroll
             for (int d = -KM; d <= KM; d++) {
                 if (d < -e || d > e) continue;   // compile-time: the band of row e
                 const int i = d + KM + 1;
-                const int leftB = B[i - 1], rightB = B[i + 1] + 1, x1B = B[i] + 1;
+                const int old = B[i];
+                const int leftB = left, rightB = B[i + 1] + 1, x1B = old + 1;
+                left = old;
                 const int bxdB = leftB > x1B ? leftB : x1B;
                 const int bestB = rightB > bxdB ? rightB : bxdB;
                 const int endd = patternLen < textLen - d ? patternLen : textLen - d;
                 const int enddB = endd + 2;
                 const int mpos = q0m2 + bestB;
                 const int mposc = mpos < NBITS ? mpos : NBITS;
-                const int fa = ll_first_from(M[d + KM][0], M[d + KM][1], mposc);
+                const int fa = ll_first_dir<KM, DIR>(M, d, mposc);
                 const int fB = fa - q0m2;
                 const int slidB = fB < enddB ? fB : enddB;
                 const int bnewB = bestB < enddB ? slidB : (fa == mposc ? bestB : enddB);
-                Bn[i] = bnewB;
+                B[i] = bnewB;
                 hit = hit || bnewB == patB;
             }
             if (hit) return e;
-#pragma unroll
-            for (int i = 0; i < 2 * KM + 3; i++) B[i] = Bn[i];
         }
     }
     return -1;
 }
 
-// The reverse LV's masks from the forward ones: reverse diagonal d reads the forward mask of
-// x = -d, bit-reversed (lv_pass: mk_reverse, lane li holds x = li - c, d = -x).
-template <int KM>
-__host__ __device__ __forceinline__ void lv_lane_reverse(uint64_t (&M)[2 * KM + 1][2]) {
-    uint64_t R[2 * KM + 1][2];
-#pragma unroll
-    for (int d = -KM; d <= KM; d++) {
-        R[d + KM][0] = ll_brev64(M[-d + KM][1]);
-        R[d + KM][1] = ll_brev64(M[-d + KM][0]);
+// ------------------------------------------------------------ two lanes per candidate
+// lv_lane_dist with a candidate's diagonals split over a lane pair (lanes 2c, 2c + 1): half h holds
+// forward diagonals x = 0, -1, .., -KM (h = 0) or 0, 1, .., KM (h = 1) at local index i = |x|, so
+// each lane keeps KM + 1 masks instead of 2 KM + 1 (the registers a 64-candidate pass cannot spare
+// inside align_kernel<128>) and the row loop runs over i = 0 .. e in both halves.  Diagonal 0 is
+// computed by both; the one value a row needs across the pair -- the partner's diagonal +-1, the far
+// neighbour of diagonal 0 -- and the row's "reached patternLen" flag cross by a DPP lane swap.  Both
+// lanes of a pair must call it together with the same act / k (their element is the same); the
+// distance comes out in both.  For DIR = -1 reverse diagonal d reads forward diagonal -d (the same
+// mask index i; ll_first_dir's reversed view), so the halves swap roles.
+__device__ __forceinline__ int ll_pair_swap(int v) {
+    return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, false);   // quad_perm [1, 0, 3, 2]: lane ^ 1
+}
+
+template <int KM, int DIR>
+__device__ __forceinline__ int lv_pair_dist(const uint64_t (&M)[KM + 1][2], int h, bool act, int q0, int patternLen,
+                                            int textLen, int k) {
+    constexpr int NBITS = 128;
+    if (!act) return -1;
+    if (k > KM) k = KM;
+    const bool up = DIR > 0 ? h != 0 : h == 0;   // local i is diagonal +i (else -i)
+    auto first = [&](int i, int p) -> int {
+        if (DIR > 0) return ll_first_from(M[i][0], M[i][1], p);
+        return 127 - ll_last_upto(M[i][0], M[i][1], 127 - p);
+    };
+    const int end0 = patternLen < textLen ? patternLen : textLen;
+    const int fm = first(0, q0) - q0;
+    const int v0 = fm < end0 ? fm : end0;
+    if (v0 == end0) {
+        const int result = patternLen > end0 ? patternLen - end0 : 0;
+        return result > k ? -1 : result;
     }
+    // B[i + 1] = local i (B = L + 2, 0: no value); B[0] = the partner's local 1; B[KM + 2] stays 0
+    int B[KM + 3];
 #pragma unroll
-    for (int i = 0; i < 2 * KM + 1; i++) { M[i][0] = R[i][0]; M[i][1] = R[i][1]; }
+    for (int i = 0; i < KM + 3; i++) B[i] = 0;
+    B[1] = v0 + 2;
+    const int patB = patternLen + 2, q0m2 = q0 - 2;
+#pragma unroll
+    for (int e = 1; e <= KM; e++) {
+        if (e > k) break;
+        B[0] = ll_pair_swap(B[2]);
+        bool hit = false;
+        int prev = B[0];   // old value of local i - 1
+#pragma unroll
+        for (int i = 0; i <= KM; i++) {
+            if (i > e) continue;   // compile-time: |d| <= e
+            const int d = up ? i : -i;
+            const int old = B[i + 1], lo = prev, hi = B[i + 2];
+            prev = old;
+            const int leftB = up ? lo : hi;              // B[d - 1]
+            const int rightB = (up ? hi : lo) + 1;       // B[d + 1] + 1
+            const int x1B = old + 1;
+            const int bxdB = leftB > x1B ? leftB : x1B;
+            const int bestB = rightB > bxdB ? rightB : bxdB;
+            const int endd = patternLen < textLen - d ? patternLen : textLen - d;
+            const int enddB = endd + 2;
+            const int mpos = q0m2 + bestB;
+            const int mposc = mpos < NBITS ? mpos : NBITS;
+            const int fa = first(i, mposc);
+            const int fB = fa - q0m2;
+            const int slidB = fB < enddB ? fB : enddB;
+            const int bnewB = bestB < enddB ? slidB : (fa == mposc ? bestB : enddB);
+            B[i + 1] = bnewB;
+            hit = hit || bnewB == patB;
+        }
+        // (the swap is evaluated by both lanes: under a short-circuit `||` a lane that already hit
+        // would skip it, and its partner's DPP would read a lane outside EXEC)
+        const int partnerHit = ll_pair_swap(hit ? 1 : 0);
+        if (hit || partnerHit != 0) return e;
+    }
+    return -1;
 }
 
 }  // namespace sgk

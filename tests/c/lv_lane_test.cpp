@@ -23,6 +23,67 @@ static uint64_t rng = 88172645463325252ull;
 static uint32_t rnd() { rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17; return (uint32_t)rng; }
 static bool acgt(char c) { return c == 'A' || c == 'C' || c == 'G' || c == 'T'; }
 
+
+// Host lockstep emulation of lv_pair_dist (lv_lane.h, device-only: it swaps values across a lane
+// pair by DPP): the same per-half arithmetic, both halves advanced row by row, the swaps done by
+// hand.  Local i of half h is forward diagonal x = h ? i : -i.
+template <int KM, int DIR>
+static int pair_emul(const uint64_t (&F)[2 * KM + 1][2], int q0, int patternLen, int textLen, int k) {
+    uint64_t M[2][KM + 1][2];
+    for (int h = 0; h < 2; h++)
+        for (int i = 0; i <= KM; i++) {
+            const int x = h ? i : -i;
+            M[h][i][0] = F[x + KM][0];
+            M[h][i][1] = F[x + KM][1];
+        }
+    if (k > KM) k = KM;
+    auto first = [&](int h, int i, int p) -> int {
+        if (DIR > 0) return ll_first_from(M[h][i][0], M[h][i][1], p);
+        return 127 - ll_last_upto(M[h][i][0], M[h][i][1], 127 - p);
+    };
+    const int end0 = patternLen < textLen ? patternLen : textLen;
+    const int fm = first(0, 0, q0) - q0;
+    const int v0 = fm < end0 ? fm : end0;
+    if (v0 == end0) {
+        const int result = patternLen > end0 ? patternLen - end0 : 0;
+        return result > k ? -1 : result;
+    }
+    int B[2][KM + 3] = {};
+    B[0][1] = B[1][1] = v0 + 2;
+    const int patB = patternLen + 2, q0m2 = q0 - 2;
+    for (int e = 1; e <= KM; e++) {
+        if (e > k) break;
+        const int s0 = B[1][2], s1 = B[0][2];
+        B[0][0] = s0;
+        B[1][0] = s1;
+        bool hit[2] = {false, false};
+        for (int h = 0; h < 2; h++) {
+            const bool up = DIR > 0 ? h != 0 : h == 0;
+            int prev = B[h][0];
+            for (int i = 0; i <= e && i <= KM; i++) {
+                const int d = up ? i : -i;
+                const int old = B[h][i + 1], lo = prev, hi = B[h][i + 2];
+                prev = old;
+                const int leftB = up ? lo : hi, rightB = (up ? hi : lo) + 1, x1B = old + 1;
+                const int bxdB = leftB > x1B ? leftB : x1B;
+                const int bestB = rightB > bxdB ? rightB : bxdB;
+                const int endd = patternLen < textLen - d ? patternLen : textLen - d;
+                const int enddB = endd + 2;
+                const int mpos = q0m2 + bestB;
+                const int mposc = mpos < 128 ? mpos : 128;
+                const int fa = first(h, i, mposc);
+                const int fB = fa - q0m2;
+                const int slidB = fB < enddB ? fB : enddB;
+                const int bnewB = bestB < enddB ? slidB : (fa == mposc ? bestB : enddB);
+                B[h][i + 1] = bnewB;
+                hit[h] = hit[h] || bnewB == patB;
+            }
+        }
+        if (hit[0] || hit[1]) return e;
+    }
+    return -1;
+}
+
 int main(int argc, char **argv) {
     const int cases = argc > 1 ? atoi(argv[1]) : 200000;
     static const char B4[] = "ACGT";
@@ -79,22 +140,21 @@ int main(int argc, char **argv) {
             int ni;
             const int want1 = oracle_lv(1, g + loc + t, glen - t, read + t, qual, n - t, k, &p, &ni);
             const int got1 = lv_lane_dist<KM>(F, true, t, n - t, glen - t, k);
+            const int pair1 = pair_emul<KM, 1>(F, t, n - t, glen - t, k);
             checked++;
-            if (want1 != got1) {
-                if (bad++ < 10) printf("fwd n=%d s=%d k=%d glen=%d: oracle %d lane %d\n", n, s, k, glen, want1, got1);
+            if (want1 != got1 || want1 != pair1) {
+                if (bad++ < 10) printf("fwd n=%d s=%d k=%d glen=%d: oracle %d lane %d pair %d\n", n, s, k, glen, want1, got1, pair1);
             }
             if (want1 < 0) continue;
             // reverse: pattern = read[s-1 .. 0], text = genome backwards from loc + s - 1, k2 = k - e1
             char rev[N + 16];
             for (int i = 0; i < s; i++) rev[i] = read[s - 1 - i];
-            uint64_t R[2 * KM + 1][2];
-            memcpy(R, F, sizeof R);
-            lv_lane_reverse<KM>(R);
             const int k2 = k - want1;
             const int want2 = oracle_lv(-1, g + loc + s, s + MAXK, rev, qual, s, k2, &p, &ni);
-            const int got2 = lv_lane_dist<KM>(R, true, 127 - (s - 1), s, s + MAXK, k2);
+            const int got2 = lv_lane_dist<KM, -1>(F, true, 127 - (s - 1), s, s + MAXK, k2);
+            const int pair2 = pair_emul<KM, -1>(F, 127 - (s - 1), s, s + MAXK, k2);
             checked++;
-            if (want2 != got2) {
+            if (want2 != got2 || want2 != pair2) {
                 if (bad++ < 10) printf("rev n=%d s=%d k2=%d: oracle %d lane %d\n", n, s, k2, want2, got2);
             }
             succ += want2 >= 0;
