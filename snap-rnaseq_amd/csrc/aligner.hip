@@ -1957,7 +1957,7 @@ static int launch_passes(snapgpu_aligner_t *a, int li, const PassIO &io, const A
                        L.lookupStats);
     HIPCHK(hipGetLastError());
     if (A.orderTmp && io.maxLen > 128) {
-        hipLaunchKernelGGL(order_long_kernel, dim3(1), dim3(1024), 0, L.stream, A.orderTmp, A.longCount, A.deferList);
+        hipLaunchKernelGGL(order_long_kernel, dim3(1), dim3(256), 0, L.stream, A.orderTmp, A.longCount, A.deferList);
         HIPCHK(hipGetLastError());
     }
     A.orderTmp = nullptr;

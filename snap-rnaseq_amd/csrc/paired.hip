@@ -1041,7 +1041,7 @@ static int runIntersect(snapgpu_paired_aligner_t *pa, const snapgpu_reads_t *r0,
             const unsigned blocks = (unsigned)std::min<uint64_t>((longL.size() + 7) / 8, 2048);
             hipLaunchKernelGGL(pair_weight_kernel, dim3(blocks), dim3(256), 0, s, P, pa->dOrder, pa->dCounter + 2, pa->dOrderW);
             PCHK(hipGetLastError());
-            hipLaunchKernelGGL(order_long_kernel, dim3(1), dim3(1024), 0, s, pa->dOrderW, pa->dCounter + 2, pa->dDefer);
+            hipLaunchKernelGGL(order_long_kernel, dim3(1), dim3(256), 0, s, pa->dOrderW, pa->dCounter + 2, pa->dDefer);
             PCHK(hipGetLastError());
         }
         if (!shortL.empty()) PCHK(hipMemcpyAsync(pa->dDefer2, shortL.data(), shortL.size() * 4, hipMemcpyHostToDevice, s));
