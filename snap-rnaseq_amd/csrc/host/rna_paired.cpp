@@ -17,6 +17,7 @@
 #include "internal.h"
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -68,6 +69,23 @@ void parallel(uint64_t n, F &&f) {
     if (nt == 1) { f(0u, (uint64_t)0, n); return; }
     std::vector<std::thread> th;
     for (unsigned t = 0; t < nt; t++) th.emplace_back([&, t] { f(t, n * t / nt, n * (t + 1) / nt); });
+    for (auto &x : th) x.join();
+}
+
+// The same over chunks of `chunk` items handed out by an atomic counter: for stages whose per-item
+// cost is skewed (a pair's filter work grows with its alignments, up to 1000 transcriptome hits per
+// read) and whose results go to per-item slots (a thread may take any chunks, in any order).
+template <class F>
+void parallelDyn(uint64_t n, uint64_t chunk, F &&f) {
+    const unsigned nt = n < 2048 ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (nt == 1) { f(0u, (uint64_t)0, n); return; }
+    std::atomic<uint64_t> next{0};
+    auto work = [&](unsigned t) {
+        for (uint64_t b; (b = next.fetch_add(chunk)) < n;) f(t, b, std::min(n, b + chunk));
+    };
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < nt; t++) th.emplace_back(work, t);
+    work(0);
     for (auto &x : th) x.join();
 }
 
@@ -492,7 +510,7 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
     auto t0 = std::chrono::steady_clock::now();
     X.fs.assign(nu + 1, FilterState());
     std::vector<Err> errs(16);
-    parallel(nu, [&](unsigned t, uint64_t b, uint64_t e) {
+    parallelDyn(nu, 512, [&](unsigned t, uint64_t b, uint64_t e) {
         AlignmentMap mate0, mate1;
         PairLists lists;
         for (uint64_t j = b; j < e && errs[t].msg.empty(); j++) {
@@ -553,7 +571,7 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
             }
         X.seedRuns = runs->nRuns;
         std::vector<uint8_t> hit(need.size(), 0);
-        parallel(need.size(), [&](unsigned t, uint64_t b, uint64_t e) {
+        parallelDyn(need.size(), 256, [&](unsigned t, uint64_t b, uint64_t e) {
             for (uint64_t i = b; i < e; i++)
                 hit[i] = partialMatch(C, runs, 2 * i, 2 * i + 1, X.ul[0][need[i]], X.ul[1][need[i]], errs[t]);
         });
@@ -697,7 +715,7 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
     std::vector<std::string> splice[2];
     for (int k = 0; k < 2; k++) {
         splice[k].assign(nb, std::string());
-        parallel(nb, [&](unsigned, uint64_t b, uint64_t e) {
+        parallelDyn(nb, 1024, [&](unsigned, uint64_t b, uint64_t e) {
             std::vector<std::pair<uint32_t, char>> tk;
             static const char kOp[] = "MIDNSHP=X";
             for (uint64_t q = b; q < e; q++) {
