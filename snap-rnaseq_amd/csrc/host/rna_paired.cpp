@@ -747,7 +747,10 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
     // writePair (ReadWriter.cpp:133-217): the end at the lower location first
     t0 = std::chrono::steady_clock::now();
     const unsigned ntd = nb < 2048 ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    std::vector<std::string> parts(ntd);
+    // the records in chunks of WCH pairs handed out dynamically, one part per chunk: the parts
+    // concatenate in chunk order, i.e. input order, whichever thread wrote them
+    constexpr uint64_t WCH = 1024;
+    std::vector<std::string> parts((nb + WCH - 1) / WCH);
     std::vector<uint64_t> cnt(3 * ntd, 0);
     // BAM: NM is set only for a record with a location; the others repeat the previous record's
     // value, so a serial pass in write order fixes each record's NM
@@ -768,8 +771,8 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
         }
     }
     const Genome &gg = *Rr.gi->genome;
-    parallel(nb, [&](unsigned t, uint64_t b, uint64_t e) {
-        std::string &o = parts[t];
+    parallelDyn(nb, WCH, [&](unsigned t, uint64_t b, uint64_t e) {
+        std::string &o = parts[b / WCH];
         o.reserve((e - b) * 640);
         for (uint64_t q = b; q < e; q++) {
             const PairOut &r = X.po[q];
