@@ -22,6 +22,7 @@
 #include <cstdio>
 #include <cstring>
 #include <condition_variable>
+#include <future>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -532,6 +533,97 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
     });
     for (auto &e : errs) if (!e.msg.empty()) { X.fail(SNAPGPU_EFORMAT, "rna_paired_align: " + e.msg); return; }
     X.filterMs = msSince(t0);
+    // CIGARs on the GPU (writeRead, SAM.cpp:1040-1066): genome records at the location, the
+    // transcriptome records on the transcriptome at tlocation.  Only the records with a location
+    // go to the GPU, as compact batches (a read without one has no CIGAR: edit distance -1, no
+    // ops).  Which records have a location, where and on which index is settled by the filter:
+    // FindPartialMatches only turns a pair with both ends SingleHit into MultipleHits, and the
+    // spacing adjustment only takes locations away (a row computed for such a record is never
+    // read: its line has no location).  So the CIGAR batches are launched here, on a host thread
+    // of their own, and run on the GPU while this thread does the seed census, the contamination
+    // pass and the count events; the genome (ga) and transcriptome (ta) batches overlap each other
+    // when the aligners are distinct.
+    auto tc0 = std::chrono::steady_clock::now();
+    // Both ends of the sub-batch in one set per aligner, one GPU call each: a row is addressed by
+    // its end's buffer and its offset there (no copy of the batch, no pointer arithmetic across the
+    // two allocations).
+    const char *const cbase[2] = {R[0]->bases, R[1]->bases};
+    struct CigarSet {
+        std::vector<int64_t> slot[2];   // end k, record -> row in ed/nOps/ops, -1: no location
+        std::vector<uint64_t> off;      // in the row's end's buffer
+        std::vector<uint8_t> mate;      // the row's end
+        std::vector<uint32_t> len, loc, nOps;
+        std::unique_ptr<uint32_t[]> ops;   // [rows][SNAPGPU_CIGAR_MAX_OPS], every row written by the download
+        std::vector<uint8_t> dir;
+        std::vector<int32_t> ed;
+        int32_t edOf(int k, uint64_t i) const { return slot[k][i] >= 0 ? ed[slot[k][i]] : -1; }
+        uint32_t nOpsOf(int k, uint64_t i) const { return slot[k][i] >= 0 ? nOps[slot[k][i]] : 0u; }
+        const uint32_t *opsOf(int k, uint64_t i) const {
+            static const uint32_t kNone[1] = {0};
+            return slot[k][i] >= 0 ? ops.get() + slot[k][i] * SNAPGPU_CIGAR_MAX_OPS : kNone;
+        }
+        void add(int k, uint64_t i, uint64_t o, uint32_t ln, uint32_t l, uint8_t d) {
+            slot[k][i] = (int64_t)loc.size();
+            off.push_back(o);
+            mate.push_back((uint8_t)k);
+            len.push_back(ln);
+            loc.push_back(l);
+            dir.push_back(d);
+        }
+        uint64_t rows() const { return loc.size(); }
+        int run(snapgpu_aligner_t *a, const char *const base[2], int useM, std::mutex &m) {
+            const uint64_t cnt = loc.size();
+            ed.assign(cnt + 1, -1);
+            nOps.assign(cnt + 1, 0);
+            ops.reset(new uint32_t[(cnt + 1) * SNAPGPU_CIGAR_MAX_OPS]);
+            if (!cnt) return SNAPGPU_OK;
+            std::lock_guard<std::mutex> lk(m);
+            return snapgpu_internal_cigar_view(a, base, mate.data(), off.data(), len.data(), cnt, loc.data(), dir.data(), useM, ed.data(),
+                                               nOps.data(), ops.get());
+        }
+    };
+    CigarSet gc, tc;
+    for (int k = 0; k < 2; k++) {
+        gc.slot[k].assign(nb, -1);
+        tc.slot[k].assign(nb, -1);
+        for (uint64_t j = 0; j < nu; j++) {
+            const PairOut &r = X.fs[j].r;
+            const uint64_t i = X.ui[j], q = i - X.a;
+            const uint32_t loc = r.status[k] != SNAPGPU_NOT_FOUND ? r.location[k] : kInvalidLocation;
+            if (loc == kInvalidLocation) continue;
+            const uint64_t o = R[k]->offsets[i];
+            if (r.isTranscriptome[k]) tc.add(k, q, o, R[k]->lengths[i], r.tlocation[k], (uint8_t)r.direction[k]);
+            else gc.add(k, q, o, R[k]->lengths[i], loc, (uint8_t)r.direction[k]);
+        }
+    }
+    double cigarBuildMs = msSince(tc0);
+    int grc = SNAPGPU_OK, trc = SNAPGPU_OK;
+    std::string gerr, terr;
+    // the seed census below is on this thread's critical path and shares the genome aligner's side
+    // stream with the genome CIGARs: those wait until the census has been issued and returned
+    std::promise<void> censusDone;
+    std::shared_future<void> censusDoneF = censusDone.get_future().share();
+    struct Joiner {
+        std::promise<void> *census;
+        std::thread t;
+        bool released = false;
+        void release() { if (!released) { released = true; census->set_value(); } }
+        ~Joiner() { release(); if (t.joinable()) t.join(); }   // every return below waits for the GPU calls
+    } cig{&censusDone};
+    cig.t = std::thread([&] {
+        const auto tg0 = std::chrono::steady_clock::now();
+        // one aligner's stream, events and upload state serve one host thread at a time (mTs is mGs
+        // when the transcriptome and genome aligners are one)
+        if (Rr.ta == Rr.ga) censusDoneF.wait();
+        trc = tc.run(Rr.ta, cbase, (int)opt->useM, *Rr.mTs);
+        if (trc) terr = snapgpu_last_error();
+        censusDoneF.wait();
+        if (trc == SNAPGPU_OK) {
+            grc = gc.run(Rr.ga, cbase, (int)opt->useM, *Rr.mGs);
+            if (grc) gerr = snapgpu_last_error();
+        }
+        X.cigarGpuMs = msSince(tg0);
+    });
     // FindPartialMatches: CharacterizeSeeds of both reads of the pairs that need it, one GPU batch
     t0 = std::chrono::steady_clock::now();
     std::vector<uint64_t> need;
@@ -562,6 +654,7 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
             if (!runs) X.fail(SNAPGPU_EDEVICE, snapgpu_last_error());
         }
         snapgpu_reads_free(both);
+        cig.release();
         if (!runs) return;
         std::unique_ptr<snapgpu_seed_runs_t, void (*)(snapgpu_seed_runs_t *)> hold(runs, snapgpu_seed_runs_free);
         for (uint64_t i = 0; i < 2 * need.size(); i++)
@@ -584,6 +677,7 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
                 X.partialMatches++;
             }
     }
+    cig.release();   // (no census batch)
     X.seedMs = msSince(t0);
     t0 = std::chrono::steady_clock::now();
     // -ct (PairedAligner.cpp:632-645): pairs still NotFound on both ends through the contamination
@@ -627,88 +721,21 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
     X.po.assign(nb, PairOut());
     for (uint64_t j = 0; j < nu; j++) X.po[X.ui[j] - X.a] = X.fs[j].r;
     X.countMs = msSince(t0);
-    // CIGARs on the GPU (writeRead, SAM.cpp:1040-1066): genome records at the location, the
-    // transcriptome records on the transcriptome at tlocation.  Only the records with a location
-    // go to the GPU, as compact batches (a read without one has no CIGAR: edit distance -1, no
-    // ops); the genome (ga) and transcriptome (ta) batches run on two host threads.
+    // the final records' index: transcriptome records are the ones with a location on it
     t0 = std::chrono::steady_clock::now();
-    // Both ends of the sub-batch in one set per aligner, one GPU call each: a row is addressed by
-    // its end's buffer and its offset there (no copy of the batch, no pointer arithmetic across the
-    // two allocations).
-    const char *const cbase[2] = {R[0]->bases, R[1]->bases};
-    struct CigarSet {
-        std::vector<int64_t> slot[2];   // end k, record -> row in ed/nOps/ops, -1: no location
-        std::vector<uint64_t> off;      // in the row's end's buffer
-        std::vector<uint8_t> mate;      // the row's end
-        std::vector<uint32_t> len, loc, nOps;
-        std::unique_ptr<uint32_t[]> ops;   // [rows][SNAPGPU_CIGAR_MAX_OPS], every row written by the download
-        std::vector<uint8_t> dir;
-        std::vector<int32_t> ed;
-        int32_t edOf(int k, uint64_t i) const { return slot[k][i] >= 0 ? ed[slot[k][i]] : -1; }
-        uint32_t nOpsOf(int k, uint64_t i) const { return slot[k][i] >= 0 ? nOps[slot[k][i]] : 0u; }
-        const uint32_t *opsOf(int k, uint64_t i) const {
-            static const uint32_t kNone[1] = {0};
-            return slot[k][i] >= 0 ? ops.get() + slot[k][i] * SNAPGPU_CIGAR_MAX_OPS : kNone;
-        }
-        void add(int k, uint64_t i, uint64_t o, uint32_t ln, uint32_t l, uint8_t d) {
-            slot[k][i] = (int64_t)loc.size();
-            off.push_back(o);
-            mate.push_back((uint8_t)k);
-            len.push_back(ln);
-            loc.push_back(l);
-            dir.push_back(d);
-        }
-        uint64_t rows() const { return loc.size(); }
-        int run(snapgpu_aligner_t *a, const char *const base[2], int useM, std::mutex &m) {
-            const uint64_t cnt = loc.size();
-            ed.assign(cnt + 1, -1);
-            nOps.assign(cnt + 1, 0);
-            ops.reset(new uint32_t[(cnt + 1) * SNAPGPU_CIGAR_MAX_OPS]);
-            if (!cnt) return SNAPGPU_OK;
-            std::lock_guard<std::mutex> lk(m);
-            return snapgpu_internal_cigar_view(a, base, mate.data(), off.data(), len.data(), cnt, loc.data(), dir.data(), useM, ed.data(),
-                                               nOps.data(), ops.get());
-        }
-    };
-    CigarSet gc, tc;
     std::vector<uint8_t> isT[2];
     for (int k = 0; k < 2; k++) {
         isT[k].assign(nb, 0);
-        gc.slot[k].assign(nb, -1);
-        tc.slot[k].assign(nb, -1);
         for (uint64_t q = 0; q < nb; q++) {
             const PairOut &r = X.po[q];
-            const uint64_t i = X.a + q;
             const uint32_t loc = r.status[k] != SNAPGPU_NOT_FOUND ? r.location[k] : kInvalidLocation;
-            const bool t = loc != kInvalidLocation && r.isTranscriptome[k];
-            isT[k][q] = t;
-            const uint64_t o = R[k]->offsets[i];
-            if (t) tc.add(k, q, o, R[k]->lengths[i], r.tlocation[k], (uint8_t)r.direction[k]);
-            else if (loc != kInvalidLocation) gc.add(k, q, o, R[k]->lengths[i], loc, (uint8_t)r.direction[k]);
+            isT[k][q] = loc != kInvalidLocation && r.isTranscriptome[k];
+            X.transcriptomeRecords += isT[k][q];
         }
     }
-    X.transcriptomeRecords += tc.rows();
-    {
-        const auto tg0 = std::chrono::steady_clock::now();
-        int grc = SNAPGPU_OK, rc = SNAPGPU_OK;
-        std::string gerr, terr;
-        auto genomeCigars = [&] {
-            grc = gc.run(Rr.ga, cbase, (int)opt->useM, *Rr.mGs);
-            if (grc) gerr = snapgpu_last_error();
-        };
-        // one aligner's stream, events and upload state serve one host thread at a time: the two
-        // CIGAR calls overlap only when the transcriptome and genome aligners are distinct
-        const bool overlap = Rr.ta != Rr.ga;
-        std::thread gt;
-        if (overlap) gt = std::thread(genomeCigars);
-        rc = tc.run(Rr.ta, cbase, (int)opt->useM, *Rr.mTs);
-        if (rc) terr = snapgpu_last_error();
-        if (overlap) gt.join();
-        else if (rc == SNAPGPU_OK) genomeCigars();
-        if (rc) { X.fail(rc, terr); return; }
-        if (grc) { X.fail(grc, gerr); return; }
-        X.cigarGpuMs = msSince(tg0);
-    }
+    cig.t.join();
+    if (trc) { X.fail(trc, terr); return; }
+    if (grc) { X.fail(grc, gerr); return; }
     // transcriptome records: computeCigarString's tokens through insertSpliceJunctions
     const auto ts0 = std::chrono::steady_clock::now();
     const Genome &tg = *Rr.ti->genome;
@@ -743,7 +770,7 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
         });
     }
     X.spliceMs = msSince(ts0);
-    X.cigarMs = msSince(t0);
+    X.cigarMs = cigarBuildMs + msSince(t0);
     // writePair (ReadWriter.cpp:133-217): the end at the lower location first
     t0 = std::chrono::steady_clock::now();
     const unsigned ntd = nb < 2048 ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));

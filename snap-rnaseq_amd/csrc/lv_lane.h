@@ -20,23 +20,26 @@
 namespace sgk {
 
 // first set position >= m0 of a 128-bit mask (w0 = positions 0..63), 128 if none; m0 in [0, 128]
-// (mk_first<2> of align_score.h with the suffix answer computed inline)
+// (mk_first<2> of align_score.h with the suffix answer computed inline).  Written as selects, not
+// early returns: inlined into lv_pair_dist's row loop, returns become exec-mask branches whose
+// live ranges (the clamped start across both sides) spilled to scratch in align_kernel<128>.
 __host__ __device__ __forceinline__ int ll_first_from(uint64_t w0, uint64_t w1, int m0) {
-    if (m0 >= 128) return 128;
     const bool hw = m0 >= 64;
-    const uint64_t x = (hw ? w1 : w0) >> (m0 & 63);
-    if (x) return m0 + __builtin_ctzll(x);
-    if (hw || !w1) return 128;
-    return 64 + __builtin_ctzll(w1);
+    const uint64_t x = (hw ? w1 : w0) >> (m0 & 63);   // m0 = 128: m0 & 63 = 0, cleared below
+    const int inWord = m0 + (x ? __builtin_ctzll(x) : 0);
+    const int inHigh = !hw && w1 ? 64 + __builtin_ctzll(w1) : 128;
+    const int r = x ? inWord : inHigh;
+    return m0 >= 128 ? 128 : r;
 }
 
-// last set position <= m1 of a 128-bit mask, -1 if none; m1 in [-1, 127]
+// last set position <= m1 of a 128-bit mask, -1 if none; m1 in [-1, 127] (selects, as above)
 __host__ __device__ __forceinline__ int ll_last_upto(uint64_t w0, uint64_t w1, int m1) {
-    if (m1 < 0) return -1;
-    const uint64_t x1 = m1 >= 64 ? w1 & (~0ull >> (127 - m1)) : 0ull;
-    if (x1) return 127 - __builtin_clzll(x1);
-    const uint64_t x0 = w0 & (m1 >= 63 ? ~0ull : ~0ull >> (63 - m1));
-    return x0 ? 63 - __builtin_clzll(x0) : -1;
+    const bool hw = m1 >= 64;
+    const uint64_t x = (hw ? w1 : w0) << (63 - (m1 & 63));   // m1's bit at 63; m1 = -1: cleared below
+    const int inWord = m1 - (x ? __builtin_clzll(x) : 0);
+    const int inLow = hw && w0 ? 63 - __builtin_clzll(w0) : -1;
+    const int r = x ? inWord : inLow;
+    return m1 < 0 ? -1 : r;
 }
 
 // "first set position >= p" of the direction's mask of diagonal d.  DIR = 1: the forward mask

@@ -84,8 +84,35 @@ static int pair_emul(const uint64_t (&F)[2 * KM + 1][2], int q0, int patternLen,
     return -1;
 }
 
+// ll_first_from / ll_last_upto (select forms) against a plain bit scan, every start, sparse and
+// dense masks (empty words, single bits at the word edges)
+static long scanCheck() {
+    long bad = 0;
+    for (int c = 0; c < 4000; c++) {
+        uint64_t w[2];
+        for (int j = 0; j < 2; j++) {
+            const uint32_t kind = rnd() % 5;
+            w[j] = kind == 0 ? 0ull : kind == 1 ? 1ull << (rnd() % 64) : kind == 2 ? 1ull << (63 - (rnd() % 2) * 63)
+                 : ((uint64_t)rnd() << 32 | rnd()) & ((uint64_t)rnd() << 32 | rnd());
+        }
+        auto bit = [&](int p) { return (w[p >> 6] >> (p & 63)) & 1; };
+        for (int m = 0; m <= 128; m++) {
+            int f = 128;
+            for (int p = m; p < 128; p++) if (bit(p)) { f = p; break; }
+            if (ll_first_from(w[0], w[1], m) != f) bad++;
+        }
+        for (int m = -1; m <= 127; m++) {
+            int l = -1;
+            for (int p = m; p >= 0; p--) if (bit(p)) { l = p; break; }
+            if (ll_last_upto(w[0], w[1], m) != l) bad++;
+        }
+    }
+    return bad;
+}
+
 int main(int argc, char **argv) {
     const int cases = argc > 1 ? atoi(argv[1]) : 200000;
+    if (const long sb = scanCheck()) { printf("mask scans: %ld wrong\n", sb); return 1; }
     static const char B4[] = "ACGT";
     long bad = 0, checked = 0, succ = 0;
     for (int c = 0; c < cases; c++) {
