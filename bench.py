@@ -653,19 +653,19 @@ def main():
             # no align kernel shares the GPU with it: read bytes + offsets/lengths + 16 records of
             # 16 B per read, then per looked-up seed its table's (bucket base, count), 64 B per
             # bucket line loaded, 4 B per saturated overflow count re-read from its list
+            # (own lists: `launches` / `busy_ms` of the timed steps feed the align kernel's roofline)
             aligner.set_overlap(False)
-            lookup_ms, lk_busy_ms, launches = [], [], []
+            lk_busy_ms, lk_launches = [], []
             for _ in range(3):
                 dev.run()
                 dev.synchronize()
                 t = aligner.timing()
-                lookup_ms.append(t["lookupKernelMs"])
                 lk_busy_ms.append(t["lookupKernelBusyMs"])
-                launches.append(t["nLaunches"])
+                lk_launches.append(t["nLaunches"])
             aligner.set_overlap(True)
             lk_bytes = int(wl["reads"] * (READ_LEN + 12 + 256) + 12 * t["lookupSeeds"] + 64 * t["lookupProbes"] +
                            4 * t["lookupOverflowReads"]) / t["nLaunches"]
-            lk_s = float(np.mean(lk_busy_ms)) / float(np.mean(launches)) / 1000.0
+            lk_s = float(np.mean(lk_busy_ms)) / float(np.mean(lk_launches)) / 1000.0
             lookup = {"kernel": "seed_lookup_kernel", "kernel_ms_per_launch": lk_s * 1000.0,
                       "achieved": lk_bytes / lk_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                       "frac": lk_bytes / lk_s / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": lk_bytes,
