@@ -1,0 +1,15 @@
+#!/bin/bash
+# RNA leg A/B of the order sort: the current library (multi-block order_long.h) against
+# libsnapgpu_prev.so (single-block), alternating, tools/rna_sub_probe.py with 1 and 2 sub-batches.
+export TMPDIR=/tmp SNAPGPU_TIMEOUT_S=120
+T=${1:?tag}; O=gpurun_out/$T; mkdir -p $O
+L=$PWD/snap-rnaseq_amd/snapgpu
+timeout -k 10 300 python -u -m pytest tests/test_order_long.py -x -v -m gpu --timeout 200 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+for i in 1 2; do
+  for v in cur prev; do
+    if [ $v = cur ]; then lib=$L/libsnapgpu.so; else lib=$L/libsnapgpu_prev.so; fi
+    echo "== $v $i"
+    SNAPGPU_LIB=$lib timeout -k 10 300 python -u tools/rna_sub_probe.py 100000 1,2 2> $O/probe_${v}_$i.err || { tail $O/probe_${v}_$i.err; exit 1; }
+  done
+done

@@ -1,7 +1,7 @@
 """Sub-batch pipeline of the RNA paired path (snapgpu_rna_paired_align, SNAPGPU_RNA_SUBBATCH): the
 bench extras.rna_paired workload (100k 2 x 150 pairs, C2 genome, 2,000-gene GTF) in 1, 2, 3 and 4
 sub-batches, best of 3 calls each, with the stage times of the best call.
-  python tools/rna_sub_probe.py [n_pairs]"""
+  python tools/rna_sub_probe.py [n_pairs] [sub-batch counts, e.g. 1,2]"""
 import os
 import shutil
 import sys
@@ -31,7 +31,8 @@ def main():
         R0, R1 = snapgpu.Reads.from_fastq(fq0), snapgpu.Reads.from_fastq(fq1)
         gtf.reset_counts()
         snapgpu.rna_paired_align(pa, ta, gtf, R0, R1)   # warm-up
-        for subs in (1, 2, 3, 4):
+        counts = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [1, 2, 3, 4]
+        for subs in counts:
             os.environ["SNAPGPU_RNA_SUBBATCH"] = str((n + subs - 1) // subs)
             best = None
             for _ in range(3):
