@@ -2251,23 +2251,37 @@ static int finishChunk(snapgpu_aligner_t *a, ChunkSlot &L) {
     const unsigned nt = n >= 65536 ? std::max(1u, std::min(4u, std::thread::hardware_concurrency())) : 1u;
     std::vector<snapgpu_aligner_stats_t> st(nt, snapgpu_aligner_stats_t{});
     std::vector<uint64_t> fixed(nt, 0), nul(nt, 0), unwritten(nt, 0), first(nt, 0);
+    // per-thread sums in locals, stored once: the threads' slots of st / fixed / nul share cache
+    // lines, and updating them per record made the lines bounce between cores -- 7.6-11.6 ms per
+    // 1M-record chunk on the MI355X host, 1.3-1.5 ms without (the copy alone is ~0.9 ms,
+    // tools/probe/pinned_read.cpp; profiles/r05/ab/host_tail_fs_r05t2.txt).  The last chunk's tail
+    // is paid after the GPU is done, once per stream.
     auto work = [&](unsigned t) {
         const uint64_t b = n * t / nt, e = n * (t + 1) / nt;
         memcpy(dst + b, L.hOut + b, (e - b) * sizeof(snapgpu_result_t));
+        uint64_t lk = 0, sc = 0, ig = 0, tm = 0, fx = 0, nu = 0, uw = 0, f0 = 0;
         for (uint64_t i = b; i < e; i++) {
             snapgpu_result_t &o = dst[i];
-            if (o.result > SNAPGPU_UNKNOWN) { if (!unwritten[t]++) first[t] = L.chunkBegin + i; continue; }
-            nul[t] += (o.flags & SNAPGPU_FLAG_NUL_BYTE) ? 1 : 0;
+            if (o.result > SNAPGPU_UNKNOWN) { if (!uw++) f0 = L.chunkBegin + i; continue; }
+            nu += (o.flags & SNAPGPU_FLAG_NUL_BYTE) ? 1 : 0;
             if (o.flags & SNAPGPU_FLAG_MAPQ_FIXED) {
                 o.mapq = hostMapq(o.probabilityOfAllCandidates, o.probabilityOfBestCandidate, o.score, o.popularSeedsSkipped);
                 o.result = o.mapq >= 10 ? SNAPGPU_SINGLE_HIT : SNAPGPU_MULTIPLE_HITS;
-                fixed[t]++;
+                fx++;
             }
-            st[t].nHashTableLookups += o.nLookups;
-            st[t].nLocationsScored += o.nLocationsScored;
-            st[t].nHitsIgnoredBecauseOfTooHighPopularity += o.nHitsIgnored;
-            st[t].nReadsIgnoredBecauseOfTooManyNs += (o.flags & SNAPGPU_FLAG_TOO_MANY_NS) ? 1 : 0;
+            lk += o.nLookups;
+            sc += o.nLocationsScored;
+            ig += o.nHitsIgnored;
+            tm += (o.flags & SNAPGPU_FLAG_TOO_MANY_NS) ? 1 : 0;
         }
+        st[t].nHashTableLookups = lk;
+        st[t].nLocationsScored = sc;
+        st[t].nHitsIgnoredBecauseOfTooHighPopularity = ig;
+        st[t].nReadsIgnoredBecauseOfTooManyNs = tm;
+        fixed[t] = fx;
+        nul[t] = nu;
+        unwritten[t] = uw;
+        first[t] = f0;
     };
     if (nt == 1) work(0);
     else {

@@ -778,7 +778,7 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
     // concatenate in chunk order, i.e. input order, whichever thread wrote them
     constexpr uint64_t WCH = 1024;
     std::vector<std::string> parts((nb + WCH - 1) / WCH);
-    std::vector<uint64_t> cnt(3 * ntd, 0);
+    std::vector<uint64_t> cnt(16 * ntd, 0);   // thread t's three counters at 16 t: a cache line of their own
     // BAM: NM is set only for a record with a location; the others repeat the previous record's
     // value, so a serial pass in write order fixes each record's NM
     std::vector<int32_t> bamNm;
@@ -846,7 +846,7 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
                 L.mateFullLen = R[m]->unclippedLength[i];
                 if (!Rr.bam) samAppendLine(o, gg, L);
                 else if (!bamAppendRecord(o, gg, L, bamNm[2 * q + w])) bamBad[t] = 1;
-                cnt[3 * t + (r.status[k] == SNAPGPU_SINGLE_HIT ? 0 : r.status[k] == SNAPGPU_MULTIPLE_HITS ? 1 : 2)]++;
+                cnt[16 * t + (r.status[k] == SNAPGPU_SINGLE_HIT ? 0 : r.status[k] == SNAPGPU_MULTIPLE_HITS ? 1 : 2)]++;
             }
         }
     });
@@ -855,7 +855,7 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
             X.fail(SNAPGPU_EINVAL, "rna_paired_align: BAM record not written (QNAME longer than 254 characters, Bam.cpp:723-726)");
             return;
         }
-    for (unsigned t = 0; t < ntd; t++) { X.single += cnt[3 * t]; X.multi += cnt[3 * t + 1]; X.notFound += cnt[3 * t + 2]; }
+    for (unsigned t = 0; t < ntd; t++) { X.single += cnt[16 * t]; X.multi += cnt[16 * t + 1]; X.notFound += cnt[16 * t + 2]; }
     X.parts.swap(parts);
     X.writeMs = msSince(t0);
 }

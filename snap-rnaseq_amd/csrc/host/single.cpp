@@ -319,7 +319,7 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
     for (uint64_t j = 0; j < nu; j++) uidx[ui[j]] = (int64_t)j;
     const unsigned nt = n < 4096 ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     std::vector<std::string> parts(nt);
-    std::vector<uint64_t> cnt(3 * nt, 0);
+    std::vector<uint64_t> cnt(16 * nt, 0);   // thread t's three counters at 16 t: a cache line of their own
     // BAMFormat::writeRead sets NM only for a record with a location; the others repeat the
     // previous record's value -- a serial pass in output order fixes each record's NM.
     std::vector<int32_t> bamNm;
@@ -366,7 +366,7 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
                     L.nOps = gn[j];
                 }
                 // updateStats (SingleAligner.cpp:338-365)
-                cnt[3 * t + (f.result == SNAPGPU_SINGLE_HIT ? 0 : f.result == SNAPGPU_MULTIPLE_HITS ? 1 : 2)]++;
+                cnt[16 * t + (f.result == SNAPGPU_SINGLE_HIT ? 0 : f.result == SNAPGPU_MULTIPLE_HITS ? 1 : 2)]++;
             }
             if (bam && L.result == SNAPGPU_NOT_FOUND) L.loc = kInvalidLocation;   // BAM: FilterSingle's NotFound
                                                                                // location 0 gives no CIGAR, bin (-1, 0)
@@ -379,7 +379,7 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
             setError("single_align: BAM record not written (QNAME longer than 254 characters, Bam.cpp:723-726)");
             return fail(SNAPGPU_EINVAL);
         }
-    for (unsigned t = 0; t < nt; t++) { st.singleHits += cnt[3 * t]; st.multiHits += cnt[3 * t + 1]; st.notFound += cnt[3 * t + 2]; }
+    for (unsigned t = 0; t < nt; t++) { st.singleHits += cnt[16 * t]; st.multiHits += cnt[16 * t + 1]; st.notFound += cnt[16 * t + 2]; }
     FILE *f = fopen(samPath, "w");
     if (!f) { setError(std::string("cannot write ") + samPath); return fail(SNAPGPU_EIO); }
     uint64_t hlen = 0;
