@@ -64,9 +64,21 @@ int pieceAt(const Genome &g, uint32_t loc) {   // Genome::getPieceAtLocation (Ge
     return -1;
 }
 
+// Host worker threads of a stage: 16 (the job's CPU share on the GPU box), fewer on a smaller host,
+// SNAPGPU_HOST_THREADS to override.  The stage threads share the CPU quota with the threads that
+// drive the GPU (stage A of the next sub-batch, the CIGAR calls).
+static unsigned hostWorkers() {
+    static const unsigned w = [] {
+        unsigned v = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        if (const char *t = getenv("SNAPGPU_HOST_THREADS"); t && atoi(t) > 0) v = (unsigned)atoi(t);
+        return v;
+    }();
+    return w;
+}
+
 template <class F>
 void parallel(uint64_t n, F &&f) {
-    const unsigned nt = n < 2048 ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const unsigned nt = n < 2048 ? 1u : hostWorkers();
     if (nt == 1) { f(0u, (uint64_t)0, n); return; }
     std::vector<std::thread> th;
     for (unsigned t = 0; t < nt; t++) th.emplace_back([&, t] { f(t, n * t / nt, n * (t + 1) / nt); });
@@ -78,7 +90,7 @@ void parallel(uint64_t n, F &&f) {
 // read) and whose results go to per-item slots (a thread may take any chunks, in any order).
 template <class F>
 void parallelDyn(uint64_t n, uint64_t chunk, F &&f) {
-    const unsigned nt = n < 2048 ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const unsigned nt = n < 2048 ? 1u : hostWorkers();
     if (nt == 1) { f(0u, (uint64_t)0, n); return; }
     std::atomic<uint64_t> next{0};
     auto work = [&](unsigned t) {
@@ -773,7 +785,7 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
     X.cigarMs = cigarBuildMs + msSince(t0);
     // writePair (ReadWriter.cpp:133-217): the end at the lower location first
     t0 = std::chrono::steady_clock::now();
-    const unsigned ntd = nb < 2048 ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const unsigned ntd = nb < 2048 ? 1u : hostWorkers();
     // the records in chunks of WCH pairs handed out dynamically, one part per chunk: the parts
     // concatenate in chunk order, i.e. input order, whichever thread wrote them
     constexpr uint64_t WCH = 1024;

@@ -97,3 +97,31 @@ def test_nul_bytes_are_flagged_not_silent(gpu_available, small_world):
     got = snapgpu.PairedAligner(idx).intersect(r0, r1)
     assert list((got["flags"] & snapgpu.PFLAG_NUL_BYTE) != 0) == [False, True]
     assert list(got["writtenBy"]) == [1, 1]
+
+
+def test_stats_match_records_on_every_record_path(gpu_available, small_world):
+    """Aligner.h:62-77's getters summed over the records: the stream path's host tail splits a
+    1M-record chunk over host threads (aligner.hip finishChunk, per-thread sums in locals), the
+    resident download sums on one thread (finishRecords); both must equal the records' own sums."""
+    idx = small_world["index"]
+    reads = snapgpu.Reads.synthetic(small_world["genome"], 200_000, seed=7, random_read_fraction=0.02)
+
+    def want(res):
+        return {"nHashTableLookups": int(res["nLookups"].astype(np.int64).sum()),
+                "nLocationsScored": int(res["nLocationsScored"].astype(np.int64).sum()),
+                "nHitsIgnoredBecauseOfTooHighPopularity": int(res["nHitsIgnored"].astype(np.int64).sum()),
+                "nReadsIgnoredBecauseOfTooManyNs": int(((res["flags"] & snapgpu.FLAG_TOO_MANY_NS) != 0).sum())}
+
+    a = snapgpu.BaseAligner(idx)
+    res = a.AlignReads(reads)
+    got = a.stats()
+    for k, v in want(res).items():
+        assert got[k] == v, (k, got[k], v)
+    b = snapgpu.BaseAligner(idx)
+    dev = b.upload(reads)
+    dev.run()
+    res2 = dev.results()
+    assert np.array_equal(res.view(np.uint8), res2.view(np.uint8))
+    got2 = b.stats()
+    for k, v in want(res2).items():
+        assert got2[k] == v, (k, got2[k], v)
