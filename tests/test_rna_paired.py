@@ -203,3 +203,56 @@ def test_rna_paired_through_big_arena_pass_matches_reference(gpu_available, tmp_
     r0.clip(3)
     ta.AlignReadsEx(r0, maxHitsToGet=1000)
     assert ta.timing()["nArenaOverflow"] > 0   # the cap really sent reads through the big-arena pass
+
+
+@pytest.mark.gpu
+def test_rna_paired_force_spacing_matches_reference(gpu_available, tmp_path):
+    """`snap-rna paired ... -fs` (PairedAligner.cpp:274-275; the chimeric aligner keeps a pair with
+    a NotFound end as it is, ChimericPairedEndAligner.cpp:93-96, and a pair with exactly one end
+    SingleHit becomes NotFound on both ends, PairedAligner.cpp:648-651): SAM records of the blocks
+    the reference completes with -fs (it segfaults in the others, make_golden.py --only-rna-fs).
+    The CIGAR batches are issued before the spacing adjustment (rna_paired.cpp, stage B), so this is
+    also the test that a record losing its location there is written without one.
+
+    Excluded: the pairs IntersectingPairedEndAligner::align leaves without writing a location (a
+    mate shorter than 50 bases or more than maxK Ns in the pair, IntersectingPairedEndAligner.cpp:
+    185-187, 226-228).  With -fs the chimeric aligner returns them as they are (:93-100), so
+    PairedAligner.cpp:577's uninitialised `result` hands the filter whatever the stack slot held --
+    the previous pair's locations (the reference writes such a pair mapped with CIGAR `*` and NM -1).
+    That is undefined behaviour, not a rule to restate; every other pair must match."""
+    import json
+    meta = json.load(open(os.path.join(G, "expected_rna_paired_fs_blocks.json")))
+    assert meta["records_differing_from_plain"] > 100   # -fs really changes the records
+    gtf, gidx, tidx = _indexes(tmp_path)
+    pa = snapgpu.PairedAligner(gidx, device=0, forceSpacing=1)
+    ta = snapgpu.BaseAligner(tidx, maxHitsToConsider=16000, maxK=15, maxSeedsToUse=8, extraSearchDepth=2)
+    n = sum(1 for _ in open(os.path.join(G, "rna_1.fq"))) // 4
+    body = []
+    for b, a0 in enumerate(meta["starts"]):
+        a1 = min(n, a0 + meta["block"])
+        f0, f1 = tmp_path / "b_1.fq", tmp_path / "b_2.fq"
+        _fastq_block(os.path.join(G, "rna_1.fq"), a0, a1, f0)
+        _fastq_block(os.path.join(G, "rna_2.fq"), a0, a1, f1)
+        r0, r1 = snapgpu.Reads.from_fastq(f0), snapgpu.Reads.from_fastq(f1)
+        gtf.reset_counts()
+        sam = tmp_path / "b.sam"
+        snapgpu.rna_paired_align(pa, ta, gtf, r0, r1, sam, forceSpacing=1)
+        lines = open(sam).read().splitlines(keepends=True)
+        if b == 0:
+            body += [l for l in lines if l.startswith("@") and not l.startswith("@PG")]
+        body += [l for l in lines if not l.startswith("@")]
+    want = [l for l in gzip.open(os.path.join(G, "expected_rna_paired_fs.sam.gz"), "rt").read().splitlines(keepends=True)
+            if not l.startswith("@PG")]
+    got = "".join(body).splitlines(keepends=True)
+    assert len(got) == len(want)
+    recs = [open(os.path.join(G, f"rna_{k}.fq")).read().splitlines() for k in (1, 2)]
+    early = set()
+    for a0 in meta["starts"]:
+        for i in range(a0, min(n, a0 + meta["block"])):
+            s0, s1 = recs[0][4 * i + 1], recs[1][4 * i + 1]
+            if len(s0) < 50 or len(s1) < 50 or sum(c in "Nn" for c in s0 + s1) > pa.params.maxK:
+                early.add(recs[0][4 * i][1:].split()[0].split("/")[0])
+    assert 0 < len(early) < 0.05 * len(want) / 2
+    bad = [i for i in range(len(want)) if got[i] != want[i] and want[i].split("\t")[0] not in early]
+    assert not bad, f"{len(bad)} SAM lines differ, first:\n got  {got[bad[0]]} want {want[bad[0]]}"
+    assert sum(1 for i in range(len(want)) if got[i] == want[i]) >= len(want) - 2 * len(early)
