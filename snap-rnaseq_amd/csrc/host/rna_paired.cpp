@@ -811,7 +811,9 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
     }
     const Genome &gg = *Rr.gi->genome;
     parallelDyn(nb, WCH, [&](unsigned t, uint64_t b, uint64_t e) {
-        std::string &o = parts[b / WCH];
+        // a local string swapped in at the end (the parts' headers share cache lines: appending
+        // through them bounced those lines between the writer threads)
+        std::string o;
         o.reserve((e - b) * 640);
         for (uint64_t q = b; q < e; q++) {
             const PairOut &r = X.po[q];
@@ -861,6 +863,7 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
                 cnt[16 * t + (r.status[k] == SNAPGPU_SINGLE_HIT ? 0 : r.status[k] == SNAPGPU_MULTIPLE_HITS ? 1 : 2)]++;
             }
         }
+        parts[b / WCH].swap(o);
     });
     for (unsigned t = 0; t < ntd; t++)
         if (bamBad[t]) {

@@ -316,8 +316,12 @@ extern "C" int snapgpu_sam_format_clipped(const snapgpu_index_t *idx, const snap
     for (unsigned t = 0; t < nt; t++)
         th.emplace_back([&, t] {
             const uint64_t a = n * t / nt, b = n * (t + 1) / nt;
-            parts[t].reserve((b - a) * 320);
-            for (uint64_t i = a; i < b; i++) formatOne(J, i, parts[t]);
+            // a local string, swapped in at the end: the parts' headers share cache lines, and
+            // appending through them bounced those lines between the threads
+            std::string o;
+            o.reserve((b - a) * 320);
+            for (uint64_t i = a; i < b; i++) formatOne(J, i, o);
+            parts[t].swap(o);
         });
     for (auto &x : th) x.join();
     uint64_t total = 0;

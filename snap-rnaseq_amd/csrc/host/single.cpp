@@ -335,7 +335,10 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
     }
     std::vector<uint8_t> bamBad(nt, 0);
     parallel(n, [&](unsigned t, uint64_t b, uint64_t e) {
-        std::string &o = parts[t];
+        // built in a local string and swapped in at the end: the parts' string headers sit side by
+        // side in the vector, and appending through them moved their shared cache lines between
+        // the writer threads on every field
+        std::string o;
         o.reserve((e - b) * 320);
         for (uint64_t i = b; i < e; i++) {
             SamLine L;
@@ -373,6 +376,7 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
             if (!bam) samAppendLine(o, *gi->genome, L);
             else if (!bamAppendRecord(o, *gi->genome, L, bamNm[i])) bamBad[t] = 1;
         }
+        parts[t].swap(o);
     });
     for (unsigned t = 0; t < nt; t++)
         if (bamBad[t]) {
