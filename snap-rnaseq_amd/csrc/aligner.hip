@@ -1728,7 +1728,16 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
             return fail("pinned lookup stats", e);
     }
     if ((e = hipStreamCreateWithFlags(&a->copyStream, hipStreamNonBlocking)) != hipSuccess) return fail("stream", e);
-    if ((e = hipStreamCreateWithFlags(&a->sideStream, hipStreamNonBlocking)) != hipSuccess) return fail("stream", e);
+    {
+        // the side stream's calls (CIGARs, seed census) sit on a caller's critical path while the
+        // lanes' persistent kernels hold the CUs: its queue gets the device's highest priority, so
+        // its kernels are dispatched ahead of the lanes' next ones (SNAPGPU_SIDE_PRIORITY=0: normal)
+        int least = 0, greatest = 0;
+        const char *t = getenv("SNAPGPU_SIDE_PRIORITY");
+        const bool high = !(t && atoi(t) == 0) && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess;
+        if ((e = high ? hipStreamCreateWithPriority(&a->sideStream, hipStreamNonBlocking, greatest)
+                      : hipStreamCreateWithFlags(&a->sideStream, hipStreamNonBlocking)) != hipSuccess) return fail("stream", e);
+    }
     for (auto &ev : a->cev) if ((e = hipEventCreate(&ev)) != hipSuccess) return fail("event", e);
     hipStream_t s0 = a->stream();
     // Every buffer is initialised on the stream of its first consumer or before the device-wide
