@@ -771,6 +771,11 @@ int snapgpu_compute_mapq(double pAll, double pBest, int score, int popularSeedsS
 
 const char *snapgpu_last_error(void);
 int snapgpu_abi_version(void);
+/* This rank's host thread budget, which every host stage of the library stays within: the CPUs of
+ * the affinity mask, capped by the cgroup CPU quota, divided by LOCAL_WORLD_SIZE (the ranks of the
+ * node); SNAPGPU_HOST_THREADS overrides.  Read once per process.  (The reference takes `-t`,
+ * ParallelTask.h:104-161.) */
+int snapgpu_host_threads(void);
 
 #ifdef __cplusplus
 }

@@ -1128,6 +1128,11 @@ struct snapgpu_aligner {
     bool failed = false;
     hipError_t (*eventQuery)(hipEvent_t) = hipEventQuery;   // test hook (snapgpu_selftest_timeout_path)
     hipEvent_t cev[2] = {};       // cigar_kernel timing
+    // snapgpu_cigar_resident reads a resident batch's records (d->dOut) on the side stream; the
+    // next pass set over resident reads (launch_resident: its 0xff pre-fill and the passes rewrite
+    // those records) waits for this event on both lanes first
+    hipEvent_t residentSideDone = nullptr;
+    bool residentSidePending = false;
     int cigarGrid = 0;
     // snapgpu_align_batch_ex buffers, kept across calls (grow-only): search windows, multi-hit
     // scratch per block, found counts, hit rows, compaction offsets and the packed hits
@@ -1482,7 +1487,7 @@ int uploadLarge(hipStream_t s, void *dst, const void *src, uint64_t bytes) {
         if ((e = hipHostMalloc(&stg[i], CH, hipHostMallocDefault)) != hipSuccess) fail(e);
         else if ((e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming)) != hipSuccess) fail(e);
     }
-    const unsigned nt = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    const unsigned nt = snapgpu::hostThreads(8);
     for (uint64_t off = 0, k = 0; off < bytes && rc == SNAPGPU_OK; off += CH, k++) {
         const int b = (int)(k & 1);
         const uint64_t len = std::min(CH, bytes - off);
@@ -1680,6 +1685,7 @@ void snapgpu_aligner_free(snapgpu_aligner_t *a) {
         hostPinnedFree(v.hCounter);
     }
     for (auto &e : a->cev) if (e) hipEventDestroy(e);
+    if (a->residentSideDone) hipEventDestroy(a->residentSideDone);
     for (auto *b : {&a->cgIn, &a->cgOut}) devFree(a, b->p);
     for (auto &b : a->aux) devFree(a, b.p);
     hostPinnedFree(a->cgPin);
@@ -1739,6 +1745,7 @@ snapgpu_aligner_t *snapgpu_aligner_create(int device, const snapgpu_index_t *idx
                       : hipStreamCreateWithFlags(&a->sideStream, hipStreamNonBlocking)) != hipSuccess) return fail("stream", e);
     }
     for (auto &ev : a->cev) if ((e = hipEventCreate(&ev)) != hipSuccess) return fail("event", e);
+    if ((e = hipEventCreateWithFlags(&a->residentSideDone, hipEventDisableTiming)) != hipSuccess) return fail("event", e);
     hipStream_t s0 = a->stream();
     // Every buffer is initialised on the stream of its first consumer or before the device-wide
     // synchronisation at the end of this function (stream audit): no
@@ -2097,6 +2104,10 @@ static int launch_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, cons
     if (rc) return rc;
     rc = beginCall(a);
     if (rc) return rc;
+    if (a->residentSidePending) {   // a CIGAR call may still read resident records on the side stream
+        for (auto &L : a->lane) HIPCHK(hipStreamWaitEvent(L.stream, a->residentSideDone, 0));
+        a->residentSidePending = false;
+    }
     const bool ext = x.search || x.maxHitsToGet;
     const uint64_t n = d->n;
     const uint64_t nChunks = ext || n == 0 ? 1 : (n + a->residentChunk - 1) / a->residentChunk;
@@ -2257,7 +2268,7 @@ static int finishChunk(snapgpu_aligner_t *a, ChunkSlot &L) {
     const auto t0 = std::chrono::steady_clock::now();
     const uint64_t n = L.chunkN;
     snapgpu_result_t *dst = out + L.chunkBegin;
-    const unsigned nt = n >= 65536 ? std::max(1u, std::min(4u, std::thread::hardware_concurrency())) : 1u;
+    const unsigned nt = n >= 65536 ? snapgpu::hostThreads(4) : 1u;
     std::vector<snapgpu_aligner_stats_t> st(nt, snapgpu_aligner_stats_t{});
     std::vector<uint64_t> fixed(nt, 0), nul(nt, 0), unwritten(nt, 0), first(nt, 0);
     // per-thread sums in locals, stored once: the threads' slots of st / fixed / nul share cache
@@ -2924,7 +2935,11 @@ int snapgpu_cigar_resident(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, int 
     }
     CigarArgs C = cigar_args(a, d, useM);
     C.records = d->dOut;
-    return cigar_launch(a, d, C);
+    const int rc = cigar_launch(a, d, C);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(a->residentSideDone, a->sideStream));
+    a->residentSidePending = true;
+    return SNAPGPU_OK;
 }
 
 int snapgpu_cigar_download(snapgpu_aligner_t *a, snapgpu_device_reads_t *d, int32_t *editDistance, uint32_t *nOps,
@@ -3013,7 +3028,7 @@ int snapgpu_internal_cigar_view(snapgpu_aligner_t *a, const char *const base[2],
     memcpy(h + oDir, directions, n);
     {
         // pack the bases (several threads for big batches: the copy is the host's part of the call)
-        const unsigned nt = n < 16384 ? 1u : std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+        const unsigned nt = n < 16384 ? 1u : snapgpu::hostThreads(8);
         auto pack = [&](uint64_t b, uint64_t e) {
             for (uint64_t i = b; i < e; i++) memcpy(h + oBases + hOff[i], base[mate ? mate[i] & 1 : 0] + offsets[i], lengths[i]);
         };

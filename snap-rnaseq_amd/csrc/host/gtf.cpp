@@ -494,7 +494,7 @@ bool gtfCountPair(snapgpu_gtf_t *g, const std::string &tid0, uint32_t tstart0, u
 int64_t gtfCountPairs(snapgpu_gtf_t *g, const std::vector<GtfPairQuery> &q) {
     const uint64_t n = q.size();
     std::vector<GtfPairEvent> ev(n);
-    const unsigned nt = n < 4096 ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const unsigned nt = n < 4096 ? 1u : hostThreads(16);
     std::vector<std::thread> th;
     for (unsigned t = 0; t < nt; t++)
         th.emplace_back([&, t] {

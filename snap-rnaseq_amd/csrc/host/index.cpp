@@ -68,8 +68,7 @@ namespace {
 
 unsigned hwThreads(int n) {
     if (n > 0) return (unsigned)n;
-    unsigned h = std::thread::hardware_concurrency();
-    return h ? h : 4;
+    return snapgpu::hostThreadBudget();   // threads.cpp: affinity, cgroup quota, ranks of the node
 }
 
 // f(thread, begin, end) over [0, n) in nThreads static slices

@@ -20,6 +20,11 @@ constexpr unsigned kQuadraticChainingDepth = 5;      // HashTable.h:115
 
 void setError(const std::string &msg);
 
+// threads.cpp: this rank's host thread budget -- the affinity mask capped by the cgroup CPU quota,
+// divided by LOCAL_WORLD_SIZE (SNAPGPU_HOST_THREADS overrides) -- and a stage's share of it
+unsigned hostThreadBudget();
+unsigned hostThreads(unsigned cap);
+
 // Host buffers the GPU copies from (read bases/qualities): page-locked when a HIP device is
 // present, so the aligner's chunked H2D copies run asynchronously at PCIe speed; plain
 // zeroed heap memory otherwise (build container).  *pinned says which one hostFree must undo.

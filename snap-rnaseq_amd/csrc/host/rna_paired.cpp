@@ -64,15 +64,12 @@ int pieceAt(const Genome &g, uint32_t loc) {   // Genome::getPieceAtLocation (Ge
     return -1;
 }
 
-// Host worker threads of a stage: 16 (the job's CPU share on the GPU box), fewer on a smaller host,
-// SNAPGPU_HOST_THREADS to override.  The stage threads share the CPU quota with the threads that
-// drive the GPU (stage A of the next sub-batch, the CIGAR calls).
+// Host worker threads of a stage: this rank's thread budget (threads.cpp: affinity, cgroup quota,
+// LOCAL_WORLD_SIZE; SNAPGPU_HOST_THREADS overrides), at most 16.  The stage threads share the budget
+// with the threads that drive the GPU (stage A of the next sub-batch, the CIGAR calls).  Per-thread
+// arrays are sized by this, never by a constant.
 static unsigned hostWorkers() {
-    static const unsigned w = [] {
-        unsigned v = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-        if (const char *t = getenv("SNAPGPU_HOST_THREADS"); t && atoi(t) > 0) v = (unsigned)atoi(t);
-        return v;
-    }();
+    static const unsigned w = snapgpu::hostThreads(16);
     return w;
 }
 
@@ -522,7 +519,7 @@ void rnaStageB(const RnaRun &Rr, RnaSub &X, int32_t &lastNm) {
     const uint64_t nu = X.ui.size(), nb = X.b - X.a;
     auto t0 = std::chrono::steady_clock::now();
     X.fs.assign(nu + 1, FilterState());
-    std::vector<Err> errs(16);
+    std::vector<Err> errs(hostWorkers());
     parallelDyn(nu, 512, [&](unsigned t, uint64_t b, uint64_t e) {
         AlignmentMap mate0, mate1;
         PairLists lists;
@@ -919,7 +916,7 @@ int snapgpu_rna_paired_align(snapgpu_paired_aligner_t *pa, snapgpu_aligner_t *ta
         if (rc) return rc;
     }
     if (!opt->ignoreMismatchedIDs) {   // Read::checkIdMatch (Read.cpp:37-49): the reference exits
-        std::vector<uint64_t> bad(16, n);   // first mismatching pair of each thread's range
+        std::vector<uint64_t> bad(hostWorkers(), n);   // first mismatching pair of each thread's range
         parallel(n, [&](unsigned t, uint64_t b, uint64_t e) {
             for (uint64_t i = b; i < e; i++)
                 if (!idsMatch(reads0->ids + reads0->idOffsets[i], reads0->idLengths[i],

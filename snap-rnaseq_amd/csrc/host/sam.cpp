@@ -309,7 +309,7 @@ extern "C" int snapgpu_sam_format_clipped(const snapgpu_index_t *idx, const snap
     Job J{idx, reads, ids, idOffsets, idLengths, results, editDistance, nOps, ops, readGroup,
           unclippedLength ? frontClipped : nullptr, unclippedLength};
     const uint64_t n = reads->n;
-    unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    unsigned nt = hostThreads(16);
     if (n < 4096) nt = 1;
     std::vector<std::string> parts(nt);
     std::vector<std::thread> th;

@@ -143,7 +143,7 @@ bool filterSingle(const Ctx &C, const std::map<std::string, Alignment> &mate0, F
 
 template <class F>
 void parallel(uint64_t n, F &&f) {
-    const unsigned nt = n < 4096 ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const unsigned nt = n < 4096 ? 1u : hostThreads(16);
     if (nt == 1) { f(0u, (uint64_t)0, n); return; }
     std::vector<std::thread> th;
     for (unsigned t = 0; t < nt; t++) th.emplace_back([&, t] { f(t, n * t / nt, n * (t + 1) / nt); });
@@ -232,7 +232,7 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
     t0 = std::chrono::steady_clock::now();
     Ctx C{gi->genome, ti->genome, gtf, {}, opt->maxDist, opt->confDiff};
     for (size_t p = 0; p < gi->genome->pieceNames.size(); p++) C.pieceByName.insert({gi->genome->pieceNames[p], gi->genome->pieceOffsets[p]});
-    std::vector<std::string> errs(16);
+    std::vector<std::string> errs(hostThreads(16));
     parallel(nu, [&](unsigned t, uint64_t b, uint64_t e) {
         std::map<std::string, Alignment> mate0;
         for (uint64_t j = b; j < e && errs[t].empty(); j++) {
@@ -317,7 +317,7 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
     t0 = std::chrono::steady_clock::now();
     std::vector<int64_t> uidx(n, -1);
     for (uint64_t j = 0; j < nu; j++) uidx[ui[j]] = (int64_t)j;
-    const unsigned nt = n < 4096 ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const unsigned nt = n < 4096 ? 1u : hostThreads(16);
     std::vector<std::string> parts(nt);
     std::vector<uint64_t> cnt(16 * nt, 0);   // thread t's three counters at 16 t: a cache line of their own
     // BAMFormat::writeRead sets NM only for a record with a location; the others repeat the

@@ -96,6 +96,12 @@ def device_count():
     return lib().snapgpu_device_count()
 
 
+def host_threads():
+    """This rank's host thread budget (snapgpu_host_threads): affinity mask capped by the cgroup
+    CPU quota, divided by LOCAL_WORLD_SIZE; SNAPGPU_HOST_THREADS overrides."""
+    return lib().snapgpu_host_threads()
+
+
 class Genome:
     """Whole-genome byte string with contig padding (SNAPLib/Genome.h)."""
 

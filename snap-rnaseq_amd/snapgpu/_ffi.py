@@ -239,6 +239,7 @@ class BucketInfo(C.Structure):   # snapgpu_bucket_info_t
 _PROTOS = [
     ("snapgpu_abi_version", C.c_int, []),
     ("snapgpu_last_error", C.c_char_p, []),
+    ("snapgpu_host_threads", C.c_int, []),
     ("snapgpu_aligner_params_default", None, [C.POINTER(AlignerParams)]),
     ("snapgpu_genome_from_fasta", C.c_void_p, [C.c_char_p, C.c_uint32]),
     ("snapgpu_genome_synthetic", C.c_void_p, [C.POINTER(SynthGenomeParams)]),

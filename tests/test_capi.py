@@ -1,5 +1,5 @@
-"""CPU tests of the C ABI boundary (include/snapgpu.h): the library loads, exports
-every declared entry point, and the host-side (no GPU) calls behave."""
+"""Tests of the C ABI boundary (include/snapgpu.h): the library loads, exports every declared
+entry point, and the host-side (no GPU) calls behave; on a GPU, a plain C program aligns through it."""
 import ctypes as C
 import os
 import re
@@ -112,15 +112,57 @@ def test_plain_c_caller(tmp_path):
     """tests/c/abi_smoke.c: the header compiles as C99 (-Wall -Wextra -pedantic) and a C
     program linked against the library runs the host-side entry points."""
     import subprocess
+    exe = _build_abi_smoke(tmp_path)
+    env = dict(os.environ)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, env=env, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "ok 1" in out.stdout
+
+
+def _build_abi_smoke(tmp_path):
+    import subprocess
     exe = tmp_path / "abi_smoke"
     libdir = os.path.dirname(_ffi.LIB_PATH)
     subprocess.run(["gcc", "-std=c99", "-Wall", "-Wextra", "-pedantic", "-Werror", "-I", os.path.join(ROOT, "include"),
                     os.path.join(ROOT, "tests", "c", "abi_smoke.c"), "-o", str(exe), "-L", libdir, "-lsnapgpu",
                     "-Wl,-rpath," + libdir], check=True)
-    env = dict(os.environ)
-    out = subprocess.run([str(exe)], capture_output=True, text=True, env=env, timeout=120)
-    assert out.returncode == 0, out.stdout + out.stderr
-    assert "ok 1" in out.stdout
+    return exe
+
+
+@pytest.mark.gpu
+def test_plain_c_caller_aligns_on_gpu(gpu_available, tmp_path):
+    """a native C program (tests/c/abi_smoke.c, no Python in the process) creates the
+    aligner on the GPU and aligns 3,000 synthetic reads through snapgpu_align_batch -- the call a
+    SNAPLib-side binding makes (Aligner.h:54-80) --, printing every compared record field; the
+    records equal the oracle's on the same genome, index and reads, doubles bit for bit."""
+    import subprocess
+    from oracle_ffi import oracle_align
+    exe = _build_abi_smoke(tmp_path)
+    out = subprocess.run([str(exe), "3000"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+    rows = [l.split() for l in out.stdout.splitlines() if l.startswith("R ")]
+    assert len(rows) == 3000 and "aligned 3000" in out.stdout
+    g = snapgpu.Genome.synthetic(200000, seed=7, n_contigs=2, n_repeat_families=10, repeat_fraction=0.3,
+                                 max_divergence=0.1, n_run_fraction=0.001, chromosome_padding=500)
+    g2 = snapgpu.Genome.synthetic(200000, seed=7, n_contigs=2, n_repeat_families=10, repeat_fraction=0.3,
+                                  max_divergence=0.1, n_run_fraction=0.001, chromosome_padding=500)
+    idx = snapgpu.GenomeIndex.build(g, 20, 2)
+    reads = snapgpu.Reads.synthetic(g2, 3000, seed=31, random_read_fraction=0.02)
+    want = oracle_align(idx, reads, snapgpu.default_params(), n_threads=4)
+    ints = ("result", "location", "direction", "score", "mapq", "nLookups", "nLocationsScored",
+            "popularSeedsSkipped", "nHitsIgnored", "nHitWords", "nOverflowLists", "nElements")
+    bad = []
+    for r in rows:
+        i = int(r[1])
+        w = want[i]
+        got = [int(x) for x in r[2:2 + len(ints)]]
+        exp = [int(w[f]) for f in ints]
+        gp = [int(x, 16) for x in r[2 + len(ints):]]
+        ep = [int(np.float64(w[f]).view(np.uint64)) for f in ("probabilityOfAllCandidates", "probabilityOfBestCandidate")]
+        if got != exp or gp != ep:
+            bad.append((i, got, exp))
+    assert not bad, f"{len(bad)} records differ, e.g. {bad[:2]}"
+    assert sum(1 for r in rows if r[2] == "1") > 2000   # SingleHit: the reads really aligned
 
 
 def test_multihit_copy_out_is_clamped(tmp_path):

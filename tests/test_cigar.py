@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 
 import snapgpu
-from oracle_ffi import oracle_align, oracle_cigars, sam_pattern
+from oracle_ffi import mismatches, oracle_align, oracle_cigars, sam_pattern
 
 G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
@@ -273,3 +273,29 @@ def test_gpu_cigar_batch_views_and_buffer_reuse(gpu_available, small_world):
             for j in range(c):   # snapgpu_cigar_batch writes each row's first nOps entries
                 k = int(part.nOps[j])
                 assert np.array_equal(part.ops[j, :k], whole.ops[s + j, :k])
+
+
+@pytest.mark.gpu
+def test_gpu_resident_cigars_ordered_before_next_run(gpu_available, small_world):
+    """run(); run_cigars(); run(); cigars() on one resident batch: the CIGAR kernel reads
+    the batch's records on the aligner's side stream, and the second run's 0xff pre-fill and passes
+    rewrite those records on the lane streams -- the lanes wait for the side stream's CIGAR first, so
+    the CIGARs equal those of a clean run() / run_cigars() / cigars() sequence, repeated 3 times."""
+    idx, reads = small_world["index"], small_world["reads"]
+    al = snapgpu.BaseAligner(idx)
+    clean = al.upload(reads)
+    clean.run()
+    clean.run_cigars()
+    want, want_res = clean.cigars(), clean.results()
+    dev = al.upload(reads)
+    for _ in range(3):
+        dev.run()
+        dev.run_cigars()
+        dev.run()
+        got = dev.cigars()
+        assert np.array_equal(got.editDistance, want.editDistance)
+        assert np.array_equal(got.nOps, want.nOps)
+        for j in range(reads.n):
+            k = int(want.nOps[j])
+            assert np.array_equal(got.ops[j, :k], want.ops[j, :k]), j
+        assert mismatches(dev.results(), want_res).size == 0
