@@ -334,10 +334,13 @@ def rna_parity(args, pa, ta, gtf, r0, r1, work):
                     "pairs, genome, GTF"}
 
 
-def rna_roofline(ta, r0):
+def rna_roofline(ta, r0, tidx=None, n_threads=1):
     """Roofline of the RNA leg's dominant kernel, align_kernel<256> (the 2 x 150 mates' pass), on the
     transcriptome aligner over end 0 (untimed extra call): SURVEY 8(d) d3 algorithmic bytes of the
-    records (each read at its own length) / the pass-2+3 kernel time (HIP events)."""
+    records (each read at its own length) / the pass-2+3 kernel time (HIP events).  P is in the
+    headline's unit: the reference's SNAPHashTable slot probes at 12 B, counted by the oracle on the
+    same reads with the same parameters (`tidx` given: the CPU-baseline leg), else the device's bucket
+    lines at 12 B each (marked unpinned)."""
     res = ta.AlignReads(r0)
     ks, ovf = [], 0
     for _ in range(3):
@@ -347,16 +350,31 @@ def rna_roofline(ta, r0):
         ovf = int(t["nArenaOverflow"])
     lens = np.array([len(r0.get(i)[0]) for i in range(r0.n)], dtype=np.int64)
     P = res["nProbes"].astype(np.int64)
+    p_unit = "device bucket lines at 12 B (no oracle run: P unpinned)"
+    if tidx is not None:
+        from oracle_ffi import mismatches, oracle_align
+        c0 = time.perf_counter()
+        cres = oracle_align(tidx, r0, ta.params, n_threads=n_threads)
+        oracle_s = time.perf_counter() - c0
+        bad = int(len(mismatches(res, cres)))
+        P = cres["nProbes"].astype(np.int64)
+        p_unit = (f"reference slot probes at 12 B (oracle on the same {r0.n} reads, {oracle_s:.1f} s on "
+                  f"{n_threads} threads; {bad} records differ from the GPU's)")
     H = res["nHitWords"].astype(np.int64)
     V = res["nOverflowLists"].astype(np.int64)
     S = res["nLocationsScored"].astype(np.int64)
-    b = int((2 * lens + 16 + 64 * P + 4 * (H + V) + (lens + MAX_K) * S).sum())
+    b = int((2 * lens + 16 + 12 * P + 4 * (H + V) + (lens + MAX_K) * S).sum())
+    b_planes = int((2 * lens + 16 + 12 * P + 4 * (H + V) + -(-(lens + MAX_K) * 3 // 8) * S).sum())
     ms = float(min(ks))
     return {"kernel": "align_kernel<256, false> (+ the <512> byte pass and the big-arena pass over the reads "
                       "that outgrew a capped arena)", "reads": int(r0.n), "arena_overflow_reads": ovf,
             "kernel_ms": ms, "algorithmic_bytes": b, "achieved": b / (ms / 1000.0) / 1e9, "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": b / (ms / 1000.0) / 1e9 / HBM_PEAK_GBS,
             "per_read": {"P": float(P.mean()), "H": float(H.mean()), "V": float(V.mean()), "S": float(S.mean())},
+            "algorithmic_bytes_note": "SURVEY 8(d) d3 in the headline's units: P = " + p_unit + ", a byte-genome "
+                                      "window of readLen + MAX_K bytes per scored candidate",
+            "plane_layout": {"algorithmic_bytes": b_planes, "frac": b_planes / (ms / 1000.0) / 1e9 / HBM_PEAK_GBS,
+                             "note": "the same formula on the 3-bit genome planes the device reads"},
             "params": "transcriptome aligner of the RNA path: maxHits 16000, maxK 15, 8 seeds, extra 2",
             "note": "end 0 of the batch through snapgpu_align_batch (plain AlignRead; the product path's "
                     "multi-hit calls run the EXT twin of the same kernel)"}
@@ -372,11 +390,104 @@ def rna_cpu_baseline(args):
     runs = json.load(open(path))
     out = {}
     for key, r in sorted(runs.items()):
-        out[key] = {x: r[x] for x in ("value", "unit", "cores", "kind", "sample", "host", "crashed_blocks")}
-    one = runs.get("threads_1")
+        out[key] = {x: r.get(x) for x in ("value", "unit", "cores", "kind", "sample", "host", "crashed_blocks",
+                                          "base_aligner_opt", "records_equal_to_O0")}
+    # the headline: one thread, BaseAligner.cpp at the highest optimisation that completes (clang -O3
+    # -fno-strict-return; every g++ level above -O0 aborts on CharacterizeSeeds' missing return)
+    one = runs.get("threads_1_O3c") or runs.get("threads_1")
     if one:
-        out.update({x: one[x] for x in ("value", "unit", "cores", "kind", "sample")})
+        out.update({x: one.get(x) for x in ("value", "unit", "cores", "kind", "sample", "base_aligner_opt")})
+        out["note"] = ("snap-rna's own build of BaseAligner.cpp at -O0 is listed as threads_1; g++ -O1/-O2/-O3 "
+                       "builds abort ('double free') on every block (oracle/Makefile.ref rna-variants)")
     return out
+
+
+def single_leg(args, idx, local, build_threads):
+    """SURVEY.md 8(f) f1, timed (verdict r5 #4): the `snap-rna single` product path (SingleAligner.cpp:
+    140-320; the reference's product metric is this end-to-end Reads/s, AlignerContext.cpp:382-393) on the
+    C2 genome, the RNA leg's 2,000-gene GTF and transcriptome, and 1M 100-bp single-end reads
+    (tests/rna_synth.py): host FASTQ file in -> SAM file out.  Timed per call: FASTQ parsing
+    (snapgpu_reads_from_fastq) + snapgpu_single_align (clipping, pre-filter, transcriptome and genome
+    AlignRead batches, AlignmentFilter::FilterSingle, both CIGAR batches, splice junctions, SAM lines,
+    the file write, gene read counts); median of 3 calls after a warm-up.  Parity: SHA-256 of the SAM
+    records against the reference CLI's own output on the same reads (golden.json "single_bench",
+    tests/golden/make_golden.py --only-single-bench)."""
+    import shutil
+    import tempfile
+    import snapgpu
+    from rna_synth import synth_single_reads
+    work = tempfile.mkdtemp(prefix="snapgpu_single_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+    try:
+        t0 = time.time()
+        gtf_path, fq, info = synth_single_reads(idx.genome_handle(), work, n_reads=args.single_reads)
+        gtf = snapgpu.Gtf.load(gtf_path)
+        tfa = os.path.join(work, "transcriptome.fa")
+        gtf.write_transcriptome(idx.genome_handle(), tfa)
+        tidx = snapgpu.GenomeIndex.build(snapgpu.Genome.from_fasta(tfa, 500), 20, build_threads)
+        t_prep = time.time() - t0
+        ga = snapgpu.BaseAligner(idx, device=local)     # `snap-rna single` defaults for both aligners
+        ta = snapgpu.BaseAligner(tidx, device=local)
+        sam = os.path.join(work, "out.sam")
+        ts, sts, parse = [], [], []
+        for it in range(4):   # a warm-up, then 3 timed calls
+            gtf.reset_counts()
+            c0 = time.perf_counter()
+            reads = snapgpu.Reads.from_fastq(fq)
+            c1 = time.perf_counter()
+            st = snapgpu.single_align(ga, ta, gtf, reads, sam)
+            c2 = time.perf_counter()
+            del reads
+            if it:
+                ts.append(c2 - c0)
+                parse.append(c1 - c0)
+                sts.append(st)
+        k = int(np.argsort(ts)[1])
+        dt, st = ts[k], sts[k]
+        n = int(st["totalReads"])
+        ref = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json"))).get("single_bench")
+        if not ref:
+            parity = {"compared": False, "why": "no single_bench digest in tests/golden/golden.json"}
+        elif args.workload != "c2" or args.genome_bases or ref["reads"] != args.single_reads:
+            parity = {"compared": False, "why": f"the reference digest covers the default C2 workload with "
+                                                f"{ref['reads']} reads only"}
+        else:
+            drop = {f"rp{i}" for i in ref["dropped_reads"]}
+            h = hashlib.sha256()
+            nrec = 0
+            with open(sam) as f:
+                for line in f:
+                    if line.startswith("@") or line.split("\t", 1)[0].split("/")[0] in drop:
+                        continue
+                    h.update(line.encode())
+                    nrec += 1
+            parity = {"compared": True, "records": nrec, "reference_records": ref["records"],
+                      "sha256_match": h.hexdigest() == ref["sha256"], "reference_runs": ref["reference_runs"],
+                      "dropped_reads": len(ref["dropped_reads"]),
+                      "what": "SAM records of the whole batch vs the reference CLI (`snap-rna single -t 1`) on the "
+                              "same reads, genome, GTF"}
+        cpu = None
+        if ref and args.workload == "c2" and not args.genome_bases:
+            cb = ref.get("cpu_baseline") or {}
+            one = cb.get("threads_1")
+            if one:
+                cpu = {x: one.get(x) for x in ("value", "unit", "cores", "kind", "sample", "base_aligner_opt",
+                                               "records_equal_to_O0")}
+                cpu["threads_8"] = {x: (cb.get("threads_8") or {}).get(x) for x in ("value", "cores", "sample")}
+        return {"value": n / dt, "unit": "reads/s", "reads": n, "ms_per_batch": dt * 1e3,
+                "read_len": 100, "workload": info, "transcriptome_bases": tidx.info()["nBases"],
+                "stage_ms": {"fastq_parse": round(float(parse[k]) * 1e3, 2),
+                             **{x: round(st[x], 2) for x in ("alignMs", "filterMs", "cigarMs", "writeMs", "wallMs")}},
+                "records": {x: int(st[x]) for x in ("usefulReads", "singleHits", "multiHits", "notFound",
+                                                    "transcriptomeRecords")},
+                "sam_bytes": os.path.getsize(sam), "prep_s": round(t_prep, 1),
+                "parity": parity, "cpu_baseline": cpu,
+                "params": "`snap-rna single` defaults: both aligners maxHits 300, maxK 14, 25 seeds, extra 2; "
+                          "filter maxDist 14, confDiff 2",
+                "boundary": "host FASTQ file in -> SAM file out (" + ("/dev/shm" if work.startswith("/dev/shm")
+                                                                       else "temp dir") + "), the gene read counters "
+                            "advanced (snapgpu_reads_from_fastq + snapgpu_single_align)"}
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
 
 
 def rna_leg(args, idx, local, build_threads):
@@ -413,7 +524,7 @@ def rna_leg(args, idx, local, build_threads):
         dt, st = ts[k], sts[k]
         n = r0.n
         parity = rna_parity(args, pa, ta, gtf, r0, r1, work)
-        roof = rna_roofline(ta, r0)
+        roof = rna_roofline(ta, r0, None if args.no_cpu_baseline else tidx, build_threads)
         return {"parity": parity, "roofline": roof, "cpu_baseline": rna_cpu_baseline(args), "value": 2 * n / dt, "unit": "reads/s", "pairs_per_s": n / dt, "pairs": n, "ms_per_batch": dt * 1e3,
                 "read_len": 150, "workload": info, "transcriptome_bases": tidx.info()["nBases"],
                 "stage_ms": {x: round(st[x], 2) for x in ("prepMs", "alignMs", "filterMs", "seedMs", "countMs", "cigarMs",
@@ -527,6 +638,8 @@ def main():
                          "the workload's -- 500k on c2, configs[3]'s per-GPU shard of 3,125,000 on c3)")
     ap.add_argument("--rna-pairs", type=int, default=100_000,
                     help="extras.rna_paired: 2 x 150 bp pairs through the RNA paired product path (0: skip)")
+    ap.add_argument("--single-reads", type=int, default=1_000_000,
+                    help="reads of the `snap-rna single` product-path leg (extras.single_e2e; 0 = skip)")
     ap.add_argument("--mode", choices=("stream", "sync"), default="stream",
                     help="stream: submit every step, wait once (a streaming caller); sync: one blocking call per step")
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="reads timed on the CPU baseline")
@@ -720,6 +833,9 @@ def main():
             del sam, dev
             if args.paired_pairs:
                 extras["paired"] = paired_leg(args, idx, local, rank, cpus)
+            if args.single_reads:
+                extras["single_e2e"] = single_leg(args, idx, local, build_threads)
+                log(rank, "single_e2e done")
             if args.rna_pairs:
                 extras["rna_paired"] = rna_leg(args, idx, local, build_threads)
         log(rank, "extras done")

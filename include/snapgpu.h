@@ -749,6 +749,8 @@ typedef struct snapgpu_rna_paired_stats {
                               stage times above are sums over them and overlap one another in wallMs */
     double cigarGpuMs;  /* of cigarMs: the CIGAR batches (genome and transcriptome threads) */
     double spliceMs;    /* of cigarMs: insertSpliceJunctions of the transcriptome records */
+    uint64_t countedPairs;  /* GTFReader::IncrementReadCount (pair form) events applied: the intragene
+                               SingleHit pairs (AlignmentFilter.cpp:302-740) */
 } snapgpu_rna_paired_stats_t;
 
 /* pairedAligner: the genome aligner (snapgpu_paired_aligner_create with the paired CLI defaults);

@@ -1039,6 +1039,7 @@ int snapgpu_rna_paired_align(snapgpu_paired_aligner_t *pa, snapgpu_aligner_t *ta
             return SNAPGPU_EFORMAT;
         }
         if (!contamLocs.empty()) contaminantsAddAll(opt->contaminants, contamLocs);   // checked above
+        st.countedPairs = cq.size();
         st.countMs += msSince(t1);
     }
     for (auto &x : subs) {

@@ -196,7 +196,7 @@ class RnaPairedStats(C.Structure):
                                           "transcriptomeRecords", "partialPairs", "partialMatches", "seedRuns")] + \
                [(f, C.c_double) for f in ("alignMs", "filterMs", "seedMs", "cigarMs", "writeMs", "wallMs", "prepMs",
                                            "countMs")] + [("subBatches", C.c_uint64)] + \
-               [(f, C.c_double) for f in ("cigarGpuMs", "spliceMs")]
+               [(f, C.c_double) for f in ("cigarGpuMs", "spliceMs")] + [("countedPairs", C.c_uint64)]
 
 
 class SingleStats(C.Structure):

@@ -20,6 +20,7 @@ TSV/JSON expected outputs.
     python3 tests/golden/make_golden.py --only-contam    # `snap-rna single|paired ... -ct <contamination index>`
     python3 tests/golden/make_golden.py --only-sorted    # `snap-rna single|paired ... -so` (sorted SAM)
     python3 tests/golden/make_golden.py --only-rna-bench # digest of the reference on bench.py's RNA workload
+    python3 tests/golden/make_golden.py --only-single-bench # digest + CPU rate of the reference on bench.py's single-end leg
     python3 tests/golden/make_golden.py --only-rna-bam   # `snap-rna paired ... -o out.bam` records (both RNA sets)
     python3 tests/golden/make_golden.py --only-rna-fs    # `snap-rna paired ... -fs` SAM records (2 x <=101 set)
 """
@@ -971,6 +972,128 @@ def rna_bench_digest(work, n_pairs=100_000, jobs=8):
     return out
 
 
+SINGLE_BENCH_BLOCK = 20000
+SINGLE_STATS = r"\t(\d+)\t(\d+) \(at: (\d+)\)"   # AlignerContext::printStats (AlignerContext.cpp:372-393)
+
+
+def single_bench_reads(work, n_reads=1_000_000):
+    """bench.py's `extras.single_e2e` inputs: the C2 genome and tests/rna_synth.py's workload with
+    n_reads 100-bp fragments -- the same 2,000-gene GTF as the RNA paired leg (the genes are drawn
+    before the reads) -- whose first ends are the single-end reads."""
+    from rna_synth import synth_single_reads
+    gg = snapgpu.Genome.synthetic(**C2["genome"])
+    gtf, fq, info = synth_single_reads(gg._h, work, n_reads)
+    return gg, gtf, fq, info
+
+
+def single_bench_digest(work, n_reads=1_000_000, jobs=8):
+    """Reference output and CPU baseline for bench.py's `extras.single_e2e` (`snap-rna single`, SURVEY
+    8(f) f1, on the C2 genome): the C2 genome indexed by `snap-rna index`, the transcriptome by `snap-rna
+    transcriptome`, and `snap-rna single <gidx> <tidx> synth.gtf reads.fq -t 1` over blocks of reads
+    (halved where a run crashes; a read that still crashes alone is left out).  Stores SHA-256 of the
+    concatenated SAM records (no header) in golden.json["single_bench"], and the reference's own
+    Reads/s (its stats line, alignment time without index load) on a bounded sample: -t 1 and -t 8 with
+    BaseAligner.cpp at clang -O3 -fno-strict-return (snap-rna-O3c, oracle/Makefile.ref rna-variants;
+    records checked equal to the -O0 build's on the sample)."""
+    import re
+    from concurrent.futures import ThreadPoolExecutor
+    gg, gtf, fq, info = single_bench_reads(work, n_reads)
+    gfa = os.path.join(work, "c2.fa")
+    gg.write_fasta(gfa)
+    gidx = os.path.join(work, "gidx")
+    ref_index(gfa, gidx)
+    twd = os.path.join(work, "tx")
+    os.makedirs(twd, exist_ok=True)
+    run([SNAP, "transcriptome", gtf, gfa, "tidx", "-O1000"], cwd=twd)
+    recs = open(fq).read().splitlines()
+    n = len(recs) // 4
+    assert n == n_reads
+
+    def attempt(idx, binary=SNAP, threads=1, timed=False):
+        d = tempfile.mkdtemp(dir=work, prefix="blk")
+        try:
+            with open(os.path.join(d, "r.fq"), "w") as f:
+                f.write("".join("\n".join(recs[4 * i:4 * i + 4]) + "\n" for i in idx))
+            r = subprocess.run([binary, "single", gidx, os.path.join(twd, "tidx"), gtf, os.path.join(d, "r.fq"),
+                                "-t", str(threads), "-o", os.path.join(d, "out.sam")], capture_output=True, text=True,
+                               cwd=d)
+            if r.returncode != 0:
+                return None
+            lines = [l for l in open(os.path.join(d, "out.sam")).read().splitlines(keepends=True)
+                     if not l.startswith("@")]
+            if len(lines) != len(idx):
+                return None
+            if timed:
+                m = re.search(SINGLE_STATS, r.stdout)
+                return lines, (int(m.group(1)), int(m.group(2)), int(m.group(3))) if m else None
+            return lines
+        finally:
+            shutil.rmtree(d, ignore_errors=True)
+
+    def solve(idx):
+        got = attempt(idx)
+        if got is not None:
+            return [(idx[0], got)], []
+        if len(idx) == 1:
+            return [], [idx[0]]
+        h = len(idx) // 2
+        a, da = solve(idx[:h])
+        b, db = solve(idx[h:])
+        return a + b, da + db
+
+    with ThreadPoolExecutor(jobs) as ex:
+        parts = list(ex.map(solve, [list(range(c, min(n, c + SINGLE_BENCH_BLOCK)))
+                                    for c in range(0, n, SINGLE_BENCH_BLOCK)]))
+    blocks = sorted(b for p, _ in parts for b in p)
+    drop = sorted(x for _, d in parts for x in d)
+    by_first = dict(blocks)
+    h = hashlib.sha256()
+    nrec = 0
+    for _, lines in blocks:
+        for l in lines:
+            h.update(l.encode())
+            nrec += 1
+    # CPU baseline: the reference CLI's own rate on a bounded sample, one block at a time (no other load)
+    snap_o3c = SNAP + "-O3c"
+    cpu = {}
+    for threads, nblk, blk in ((1, 3, SINGLE_BENCH_BLOCK), (8, 2, 5 * SINGLE_BENCH_BLOCK)):
+        runs, same = [], True
+        for b in range(nblk):
+            first = b * (n // nblk) // SINGLE_BENCH_BLOCK * SINGLE_BENCH_BLOCK   # on the digest's block grid
+            idx = list(range(first, min(n, first + blk)))
+            got = attempt(idx, snap_o3c, threads, timed=True)
+            if got is None or got[1] is None:
+                continue
+            lines, (tot, rps, ms) = got
+            runs.append({"first_read": first, "reads": tot, "reads_per_s_printed": rps, "align_ms": ms})
+            if threads == 1:   # the -O0 build's records on the same reads (the digest's blocks)
+                ref = [l for f0 in range(first, first + blk, SINGLE_BENCH_BLOCK) for l in by_first.get(f0, [])]
+                same = same and ref == lines
+        reads = sum(r["reads"] for r in runs)
+        ms = sum(r["align_ms"] for r in runs)
+        cpu[f"threads_{threads}"] = {
+            "value": reads / (ms / 1000.0) if ms else None, "unit": "reads/s", "cores": threads,
+            "kind": "reference, build container", "base_aligner_opt": "-O3c",
+            "sample": f"{reads} of the {n} reads ({len(runs)} blocks of {blk}, spread over the set), `snap-rna "
+                      f"single <C2 index> <transcriptome> synth.gtf reads.fq -t {threads}` with BaseAligner.cpp at "
+                      "clang -O3 -fno-strict-return (oracle/Makefile.ref rna-variants); time = the reference's own "
+                      "alignment time (AlignerContext::printStats), index load excluded",
+            "blocks": runs, "host": {"nproc": os.cpu_count()}}
+        if threads == 1:
+            cpu["threads_1"]["records_equal_to_O0"] = same
+    out = {"sha256": h.hexdigest(), "records": nrec, "reads": n, "dropped_reads": drop,
+           "reference_runs": len(blocks), "workload": info, "cpu_baseline": cpu,
+           "what": "SHA-256 of the SAM records (header lines excluded) of `snap-rna single <C2 index> "
+                   "<transcriptome> synth.gtf reads.fq -t 1` over the first ends of tests/rna_synth.py's "
+                   f"{n} 100-bp fragments on the C2 genome, in read order; dropped reads excluded"}
+    gj = os.path.join(HERE, "golden.json")
+    meta = json.load(open(gj))
+    meta["single_bench"] = out
+    with open(gj, "w") as f:
+        json.dump(meta, f, indent=1)
+    return out
+
+
 def _bam_unpack(raw):
     """-> (reference list [[name, l_ref]], record bytes) of a decompressed BAM stream."""
     import struct
@@ -1196,6 +1319,12 @@ def main():
     if "--only-rna-bench" in sys.argv:
         n = int(sys.argv[sys.argv.index("--only-rna-bench") + 1]) if len(sys.argv) > 2 else 100_000
         print(json.dumps({k: v for k, v in rna_bench_digest(work, n).items() if k != "workload"}))
+        shutil.rmtree(work, ignore_errors=True)
+        return
+    if "--only-single-bench" in sys.argv:
+        i = sys.argv.index("--only-single-bench")
+        n = int(sys.argv[i + 1]) if len(sys.argv) > i + 1 else 1_000_000
+        print(json.dumps({k: v for k, v in single_bench_digest(work, n).items() if k != "workload"}))
         shutil.rmtree(work, ignore_errors=True)
         return
     if "--only-rna-fs" in sys.argv:

@@ -114,3 +114,14 @@ def synth_rna_workload(genome_handle, workdir, n_genes=2000, n_pairs=100_000, re
     info = {"genes": n_genes, "transcripts": len(spliced), "pairs": n_pairs, "read_len": read_len,
             "kinds": kind_counts}
     return gtf_path, paths[0], paths[1], info
+
+
+def synth_single_reads(genome_handle, workdir, n_reads=1_000_000, read_len=100):
+    """The single-end workload of bench.py's `extras.single_e2e` (`snap-rna single`) and of
+    tests/golden/make_golden.py --only-single-bench: synth_rna_workload's fragments at 100 bp, whose
+    first ends are the reads; the GTF is the RNA paired leg's (the genes are drawn before the reads).
+    -> (gtf_path, fastq, info)."""
+    gtf, fq0, fq1, info = synth_rna_workload(genome_handle, workdir, n_pairs=n_reads, read_len=read_len)
+    os.unlink(fq1)
+    info = dict(info, reads=info.pop("pairs"))
+    return gtf, fq0, info

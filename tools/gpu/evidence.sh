@@ -11,6 +11,6 @@ tail -1 $O/smoke.log
 timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err || { tail $O/bench.err; exit 1; }
 python3 -c "import json; d=json.loads(open('$O/bench.json').readline()); print('bench', round(d['value']/1e6,3), 'M reads/s; kernel', round(d['roofline']['kernel_ms_per_launch'],3), 'ms/launch; paired', round(d['paired']['value']/1e6,3), 'rna', round(d['rna_paired']['value']/1e6,3))"
 if [ "$2" = c3 ]; then
-  timeout -k 10 900 python bench.py --workload c3 --steps 5 --warmup 1 --rna-pairs 0 > $O/c3_bench.json 2> $O/c3_bench.err || { tail $O/c3_bench.err; exit 1; }
+  timeout -k 10 900 python bench.py --workload c3 --steps 5 --warmup 1 --rna-pairs 0 --single-reads 0 > $O/c3_bench.json 2> $O/c3_bench.err || { tail $O/c3_bench.err; exit 1; }
   python3 -c "import json; d=json.loads(open('$O/c3_bench.json').readline()); print('c3', round(d['value']/1e6,3), 'M reads/s', 'paired', round(d['paired']['value']/1e6,3))"
 fi
