@@ -185,7 +185,13 @@ def cpu_info():
         if q != "max":
             quota = int(q) / int(per)
     except (OSError, ValueError):
-        pass
+        try:   # cgroup v1 (csrc/host/threads.cpp reads the same two files)
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0 and per > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
     usable = min(aff, int(quota)) if quota else aff
     model = None
     try:

@@ -1535,7 +1535,7 @@ int uploadLarge(hipStream_t s, void *dst, const void *src, uint64_t bytes) {
 }  // namespace
 
 namespace snapgpu {
-void *hostAlloc(size_t bytes, bool *pinned) {
+void *hostAlloc(size_t bytes, bool *pinned, bool zero) {
     *pinned = false;
     int nd = g_hostDevices.load();
     if (nd == -2) {
@@ -1546,12 +1546,12 @@ void *hostAlloc(size_t bytes, bool *pinned) {
     if (nd > 0 && bytes >= (1u << 20)) {
         void *p = nullptr;
         if (hipHostMalloc(&p, bytes, hipHostMallocPortable) == hipSuccess && p) {
-            memset(p, 0, bytes);
+            if (zero) memset(p, 0, bytes);
             *pinned = true;
             return p;
         }
     }
-    return calloc(bytes, 1);
+    return zero ? calloc(bytes, 1) : malloc(bytes ? bytes : 1);
 }
 void hostFree(void *p, bool pinned) {
     if (!p) return;
@@ -2995,11 +2995,14 @@ int snapgpu_cigar_batch(snapgpu_aligner_t *a, const snapgpu_reads_t *reads, cons
 
 // snapgpu_cigar_batch over read i = base[mate[i]][offsets[i] .. + lengths[i]) (the product paths pass
 // both ends of a pair batch at once: two buffers, each row tagged with its end), without a batch copy
-int snapgpu_internal_cigar_view(snapgpu_aligner_t *a, const char *const base[2], const uint8_t *mate,
-                                const uint64_t *offsets, const uint32_t *lengths,
-                                uint64_t n, const uint32_t *locations, const uint8_t *directions, int useM,
-                                int32_t *editDistance, uint32_t *nOps, uint32_t *ops) {
+// The CIGAR call itself; its results stay in the aligner's pinned output buffer: *outEd / *outNOps
+// (n entries) and *outOps (n rows of CIG_MAX_OPS, each row's first nOps written), valid until the
+// aligner's next CIGAR call.
+static int cigarPinned(snapgpu_aligner_t *a, const char *const base[2], const uint8_t *mate, const uint64_t *offsets,
+                       const uint32_t *lengths, uint64_t n, const uint32_t *locations, const uint8_t *directions,
+                       int useM, const int32_t **outEd, const uint32_t **outNOps, const uint32_t **outOps) {
     if (a->failed) { snapgpu::setError("aligner failed earlier (device timeout)"); return SNAPGPU_EDEVICE; }
+    *outEd = nullptr; *outNOps = nullptr; *outOps = nullptr;
     if (n == 0) return SNAPGPU_OK;
     if (n > 0xffffffffull) { snapgpu::setError("batch too large"); return SNAPGPU_EINVAL; }
     HIPCHK(hipSetDevice(a->device));
@@ -3081,13 +3084,43 @@ int snapgpu_internal_cigar_view(snapgpu_aligner_t *a, const char *const base[2],
     char *ho = (char *)a->cgPinOut;
     HIPCHK(hipMemcpyAsync(ho, dOut, outBytes, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    memcpy(editDistance, ho + rEd, n * 4);
-    memcpy(nOps, ho + rN, n * 4);
-    const uint32_t *hops = (const uint32_t *)(ho + rOps);
-    for (uint64_t i = 0; i < n; i++) {
-        const uint32_t k = std::min<uint32_t>(nOps[i], (uint32_t)CIG_MAX_OPS);
-        memcpy(ops + i * CIG_MAX_OPS, hops + i * CIG_MAX_OPS, k * 4);
-    }
+    *outEd = (const int32_t *)(ho + rEd);
+    *outNOps = (const uint32_t *)(ho + rN);
+    *outOps = (const uint32_t *)(ho + rOps);
+    return SNAPGPU_OK;
+}
+
+int snapgpu_internal_cigar_pinned(snapgpu_aligner_t *a, const char *const base[2], const uint8_t *mate,
+                                  const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
+                                  const uint32_t *locations, const uint8_t *directions, int useM,
+                                  const int32_t **editDistance, const uint32_t **nOps, const uint32_t **ops) {
+    if (!a || !base || !offsets || !lengths || !locations || !directions || !editDistance || !nOps || !ops)
+        return SNAPGPU_EINVAL;
+    return cigarPinned(a, base, mate, offsets, lengths, n, locations, directions, useM, editDistance, nOps, ops);
+}
+
+int snapgpu_internal_cigar_view(snapgpu_aligner_t *a, const char *const base[2], const uint8_t *mate,
+                                const uint64_t *offsets, const uint32_t *lengths,
+                                uint64_t n, const uint32_t *locations, const uint8_t *directions, int useM,
+                                int32_t *editDistance, uint32_t *nOps, uint32_t *ops) {
+    const int32_t *ed = nullptr;
+    const uint32_t *no = nullptr, *hops = nullptr;
+    const int rc = cigarPinned(a, base, mate, offsets, lengths, n, locations, directions, useM, &ed, &no, &hops);
+    if (rc || n == 0) return rc;
+    // only each row's nOps ops to the caller (rows hold a few of their 64 slots), on host threads
+    const unsigned nt = n < 65536 ? 1u : snapgpu::hostThreads(8);
+    auto copy = [&](uint64_t b, uint64_t e) {
+        memcpy(editDistance + b, ed + b, (e - b) * 4);
+        memcpy(nOps + b, no + b, (e - b) * 4);
+        for (uint64_t i = b; i < e; i++) {
+            const uint32_t k = std::min<uint32_t>(no[i], (uint32_t)CIG_MAX_OPS);
+            memcpy(ops + i * CIG_MAX_OPS, hops + i * CIG_MAX_OPS, k * 4);
+        }
+    };
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < nt; t++) th.emplace_back(copy, n * t / nt, n * (t + 1) / nt);
+    copy(0, n / nt);
+    for (auto &x : th) x.join();
     return SNAPGPU_OK;
 }
 

@@ -28,7 +28,8 @@ unsigned hostThreads(unsigned cap);
 // Host buffers the GPU copies from (read bases/qualities): page-locked when a HIP device is
 // present, so the aligner's chunked H2D copies run asynchronously at PCIe speed; plain
 // zeroed heap memory otherwise (build container).  *pinned says which one hostFree must undo.
-void *hostAlloc(size_t bytes, bool *pinned);
+// zero = false: the caller writes every byte itself (the FASTQ parser's parallel copy).
+void *hostAlloc(size_t bytes, bool *pinned, bool zero = true);
 void hostFree(void *p, bool pinned);
 
 // snapgpu_reads_t::hostFlags bit 2: a view of another batch's buffers (readsView), which it does not free
@@ -162,6 +163,12 @@ extern "C" int snapgpu_internal_cigar_view(snapgpu_aligner_t *a, const char *con
                                            const uint32_t *lengths, uint64_t n, const uint32_t *locations,
                                            const uint8_t *directions, int useM, int32_t *editDistance, uint32_t *nOps,
                                            uint32_t *ops);
+// ... the same, results left in the aligner's pinned output buffer (valid until its next CIGAR call):
+// editDistance / nOps (n entries), ops (n rows of SNAPGPU_CIGAR_MAX_OPS, the first nOps of a row written)
+extern "C" int snapgpu_internal_cigar_pinned(snapgpu_aligner_t *a, const char *const base[2], const uint8_t *mate,
+                                             const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
+                                             const uint32_t *locations, const uint8_t *directions, int useM,
+                                             const int32_t **editDistance, const uint32_t **nOps, const uint32_t **ops);
 // aligner.hip: snapgpu_align_batch_ex with the multi-hits packed (read i: dense[off[i] .. off[i+1]))
 int snapgpu_internal_align_batch_packed(snapgpu_aligner_t *a, const snapgpu_reads_t *reads,
                                         const snapgpu_search_t *search, uint32_t maxHitsToGet,

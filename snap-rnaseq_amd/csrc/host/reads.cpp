@@ -1,23 +1,29 @@
 // reads.cpp -- read batches: wgsim-like simulator, FASTQ in/out, caller arrays.
 #include "internal.h"
 
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 using namespace snapgpu;
 
 namespace {
 
-snapgpu_reads_t *allocReads(uint64_t n, uint64_t totalBytes, bool truth) {
+snapgpu_reads_t *allocReads(uint64_t n, uint64_t totalBytes, bool truth, bool zero = true) {
     auto *r = new snapgpu_reads_t();
     r->n = n;
     r->totalBytes = totalBytes;
     bool pb = false, pq = false;
-    r->bases = (char *)hostAlloc(totalBytes + 64, &pb);
-    r->quals = (char *)hostAlloc(totalBytes + 64, &pq);
+    r->bases = (char *)hostAlloc(totalBytes + 64, &pb, zero);
+    r->quals = (char *)hostAlloc(totalBytes + 64, &pq, zero);
     r->hostFlags = (pb ? 1u : 0u) | (pq ? 2u : 0u);
     r->offsets = new uint64_t[n + 1]();
     r->lengths = new uint32_t[n + 1]();
@@ -274,50 +280,112 @@ extern "C" {
 
 snapgpu_reads_t *snapgpu_reads_from_fastq(const char *path) {
     // FASTQReader::getNextRead (FASTQ.cpp:196-253): 4-line records, id = header line without
-    // '@' (trailing CR/LF removed), bases, '+' line, qualities.
-    FILE *f = fopen(path, "r");
-    if (!f) { setError(std::string("cannot open ") + path); return nullptr; }
-    std::vector<std::string> b, q, ids;
-    std::string lines[4];
-    char buf[1 << 16];
-    int k = 0;
-    while (fgets(buf, sizeof(buf), f)) {
-        std::string s(buf);
-        while (!s.empty() && (s.back() == '\n' || s.back() == '\r')) s.pop_back();
-        lines[k++] = s;
-        if (k == 4) {
-            if (lines[0].empty() || lines[0][0] != '@') {
-                fclose(f);
-                setError(std::string("FASTQ record without '@' header in ") + path);
-                return nullptr;
-            }
-            ids.push_back(lines[0].substr(1));
-            b.push_back(lines[1]);
-            q.push_back(lines[3]);
-            k = 0;
+    // '@' (trailing CR/LF removed), bases, '+' line, qualities (a quality line shorter than the
+    // bases leaves NUL bytes: SAM's %.*s then ends early, as the reference's would).  A trailing
+    // partial record is ignored.  The file is mapped and parsed in parallel (this rank's host thread
+    // budget): the newline positions per byte range, then per record its lengths, prefix sums,
+    // and the copies into the batch -- 1M 100-bp reads: 306 ms with one thread and per-line strings.
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) { setError(std::string("cannot open ") + path); return nullptr; }
+    struct stat sb;
+    if (fstat(fd, &sb) != 0) { close(fd); setError(std::string("cannot stat ") + path); return nullptr; }
+    const uint64_t size = (uint64_t)sb.st_size;
+    const char *base = nullptr;
+    if (size) {
+        void *m = mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0);
+        if (m == MAP_FAILED) { close(fd); setError(std::string("cannot map ") + path); return nullptr; }
+        base = (const char *)m;
+    }
+    close(fd);
+    struct Unmap {
+        const char *p; uint64_t n;
+        ~Unmap() { if (p) munmap(const_cast<char *>(p), n); }
+    } unmap{base, size};
+    const unsigned nt = size < (8u << 20) ? 1u : hostThreads(16);
+    auto parallel = [&](uint64_t n, auto &&fn) {
+        if (nt == 1 || n < 4096) { fn(0u, (uint64_t)0, n); return; }
+        std::vector<std::thread> th;
+        for (unsigned t = 0; t < nt; t++) th.emplace_back([&, t] { fn(t, n * t / nt, n * (t + 1) / nt); });
+        for (auto &x : th) x.join();
+    };
+    // newline positions, per byte range, then concatenated in file order
+    std::vector<std::vector<uint64_t>> part(nt);
+    parallel(size, [&](unsigned t, uint64_t b, uint64_t e) {
+        auto &v = part[t];
+        v.reserve((e - b) / 48 + 16);
+        for (const char *p = base + b, *end = base + e; p < end;) {
+            const char *q = (const char *)memchr(p, '\n', end - p);
+            if (!q) break;
+            v.push_back((uint64_t)(q - base));
+            p = q + 1;
         }
+    });
+    std::vector<uint64_t> nl;
+    {
+        uint64_t tot = 0;
+        for (auto &v : part) tot += v.size();
+        nl.reserve(tot + 1);
+        for (auto &v : part) { nl.insert(nl.end(), v.begin(), v.end()); std::vector<uint64_t>().swap(v); }
     }
-    fclose(f);
+    const uint64_t nLines = nl.size() + ((nl.empty() ? size : size - nl.back() - 1) > 0 ? 1 : 0);
+    if (nLines > nl.size()) nl.push_back(size);   // the last line, without its newline
+    const uint64_t n = nLines / 4;
+    // line i: [start, end), cut at its first NUL byte (the C-string reading of FASTQReader's lines: a
+    // reader never hands the aligner a NUL inside a read) and without its trailing CR/LF bytes
+    auto line = [&](uint64_t i, uint64_t &b, uint64_t &e) {
+        b = i ? nl[i - 1] + 1 : 0;
+        e = nl[i];
+        if (const char *z = (const char *)memchr(base + b, 0, e - b)) e = (uint64_t)(z - base);
+        while (e > b && (base[e - 1] == '\r' || base[e - 1] == '\n')) e--;
+    };
+    std::vector<uint32_t> blen(n + 1, 0), qlen(n + 1, 0), ilen(n + 1, 0);
+    std::vector<uint64_t> badAt(nt, n);
+    parallel(n, [&](unsigned t, uint64_t a, uint64_t z) {
+        for (uint64_t r = a; r < z; r++) {
+            uint64_t b, e;
+            line(4 * r, b, e);
+            if (e == b || base[b] != '@') { badAt[t] = std::min(badAt[t], r); break; }
+            ilen[r] = (uint32_t)(e - b - 1);
+            line(4 * r + 1, b, e);
+            blen[r] = (uint32_t)(e - b);
+            line(4 * r + 3, b, e);
+            qlen[r] = (uint32_t)(e - b);
+        }
+    });
+    if (*std::min_element(badAt.begin(), badAt.end()) < n) {
+        setError(std::string("FASTQ record without '@' header in ") + path);
+        return nullptr;
+    }
     uint64_t total = 0, idTotal = 0;
-    for (auto &s : b) total += s.size();
-    for (auto &s : ids) idTotal += s.size();
-    snapgpu_reads_t *r = allocReads(b.size(), total, false);
-    r->ids = new char[idTotal + 1]();
-    r->idOffsets = new uint64_t[b.size() + 1]();
-    r->idLengths = new uint32_t[b.size() + 1]();
-    uint64_t o = 0, io = 0;
-    for (size_t i = 0; i < b.size(); i++) {
-        memcpy(r->bases + o, b[i].data(), b[i].size());
-        memcpy(r->quals + o, q[i].data(), std::min(q[i].size(), b[i].size()));
-        r->offsets[i] = o;
-        r->lengths[i] = (uint32_t)b[i].size();
-        o += b[i].size();
-        memcpy(r->ids + io, ids[i].data(), ids[i].size());
-        r->idOffsets[i] = io;
-        r->idLengths[i] = (uint32_t)ids[i].size();
-        io += ids[i].size();
+    for (uint64_t r = 0; r < n; r++) { total += blen[r]; idTotal += ilen[r]; }
+    snapgpu_reads_t *rd = allocReads(n, total, false, /*zero=*/false);
+    rd->ids = new char[idTotal + 1]();
+    rd->idOffsets = new uint64_t[n + 1]();
+    rd->idLengths = new uint32_t[n + 1]();
+    for (uint64_t r = 0, o = 0, io = 0; r < n; r++) {
+        rd->offsets[r] = o;
+        rd->lengths[r] = blen[r];
+        o += blen[r];
+        rd->idOffsets[r] = io;
+        rd->idLengths[r] = ilen[r];
+        io += ilen[r];
     }
-    return r;
+    parallel(n, [&](unsigned, uint64_t a, uint64_t z) {
+        for (uint64_t r = a; r < z; r++) {
+            uint64_t b, e;
+            line(4 * r, b, e);
+            memcpy(rd->ids + rd->idOffsets[r], base + b + 1, ilen[r]);
+            line(4 * r + 1, b, e);
+            memcpy(rd->bases + rd->offsets[r], base + b, blen[r]);
+            line(4 * r + 3, b, e);
+            const uint32_t nq = std::min(qlen[r], blen[r]);
+            memcpy(rd->quals + rd->offsets[r], base + b, nq);
+            if (nq < blen[r]) memset(rd->quals + rd->offsets[r] + nq, 0, blen[r] - nq);
+        }
+    });
+    memset(rd->bases + total, 0, 64);   // the batch's zero slack
+    memset(rd->quals + total, 0, 64);
+    return rd;
 }
 
 int snapgpu_reads_write_fastq(const snapgpu_reads_t *r, const char *path) {

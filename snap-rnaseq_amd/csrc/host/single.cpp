@@ -18,6 +18,8 @@
 #include <thread>
 #include <vector>
 
+#include <unistd.h>
+
 namespace snapgpu {
 struct GtfTranscript;
 const GtfTranscript *gtfTranscript(const snapgpu_gtf_t *g, const std::string &id);
@@ -49,15 +51,16 @@ int pieceAt(const Genome &g, uint32_t loc) {
     return -1;
 }
 
-// Alignment (AlignmentFilter.h:41-70), the fields FilterSingle reads
+// Alignment (AlignmentFilter.h:41-70), the fields FilterSingle reads.  The names point into storage
+// that outlives the call (the genome's and the transcriptome's piece names, the GTF's chromosome
+// names), so a read's filter allocates nothing.
 struct Alignment {
     uint32_t location = 0;
     int direction = 0;
     int score = 0;
-    std::string rname, transcriptId;
+    const std::string *rname = nullptr, *transcriptId = nullptr;
     uint32_t pos = 0;
     bool isTranscriptome = false;
-    bool operator<(const Alignment &r) const { return score < r.score; }   // AlignmentFilter.cpp:55-57
 };
 
 struct FilterOut {
@@ -75,24 +78,43 @@ struct Ctx {
     uint32_t maxDist, confDiff;
 };
 
+// AlignmentFilter's mate-0 map (AlignmentFilter.cpp:113-214), keyed by rname + '_' + pos: a single-end
+// read adds at most two alignments (transcriptome, then genome), so the map is two slots, and its
+// iteration order -- the order FilterSingle sorts from -- is the keys' std::string order.
+struct Mate0 {
+    Alignment a[2];
+    int n = 0;
+};
+// key(x) < key(y) as std::string compares rname + "_" + decimal pos (char_traits<char>: unsigned bytes)
+bool keyLess(const Alignment &x, const Alignment &y) {
+    char kx[320], ky[320];
+    const int lx = snprintf(kx, sizeof kx, "%s_%u", x.rname->c_str(), x.pos);
+    const int ly = snprintf(ky, sizeof ky, "%s_%u", y.rname->c_str(), y.pos);
+    if (lx < (int)sizeof kx && ly < (int)sizeof ky) {
+        const int c = memcmp(kx, ky, (size_t)std::min(lx, ly));
+        return c != 0 ? c < 0 : lx < ly;
+    }
+    return *x.rname + '_' + std::to_string(x.pos) < *y.rname + '_' + std::to_string(y.pos);   // (names > 300 bytes)
+}
+
 // AlignmentFilter::AddAlignment + HashAlignment (AlignmentFilter.cpp:113-214), mate 0
-int addAlignment(const Ctx &C, std::map<std::string, Alignment> &mate0, uint32_t location, int direction, int score,
-                 bool isTranscriptome, uint32_t readLen, std::string *err) {
+int addAlignment(const Ctx &C, Mate0 &mate0, uint32_t location, int direction, int score, bool isTranscriptome,
+                 uint32_t readLen, std::string *err) {
     if (score > (int)C.maxDist) return -1;   // `score > maxDist`: unsigned comparison in the reference
-    std::string rname = "*";
+    static const std::string kStar = "*";
+    const std::string *rname = &kStar, *tid = nullptr;
     uint32_t pos = 0;
-    std::string tid;
     if (location != kInvalidLocation) {
         const Genome &g = isTranscriptome ? *C.transcriptome : *C.genome;
         const int p = pieceAt(g, location);
         if (p < 0) return 0;   // before the first piece (the reference dereferences NULL)
-        rname = g.pieceNames[p];
+        rname = &g.pieceNames[p];
         pos = location - g.pieceOffsets[p] + 1;
         if (isTranscriptome) {
-            const GtfTranscript *t = gtfTranscript(C.gtf, rname);
-            if (!t) { *err = "No transcript " + rname; return -2; }   // GTFReader::GetTranscript exits
+            const GtfTranscript *t = gtfTranscript(C.gtf, *rname);
+            if (!t) { *err = "No transcript " + *rname; return -2; }   // GTFReader::GetTranscript exits
             tid = rname;
-            rname = gtfTranscriptChr(t);
+            rname = &gtfTranscriptChr(t);
             pos = gtfGenomicPosition(t, pos, readLen);
         }
     }
@@ -101,26 +123,31 @@ int addAlignment(const Ctx &C, std::map<std::string, Alignment> &mate0, uint32_t
     a.location = location; a.direction = direction; a.score = score; a.rname = rname; a.pos = pos;
     a.isTranscriptome = isTranscriptome;
     a.transcriptId = tid;
-    const std::string key = rname + '_' + std::to_string(pos);
-    auto it = mate0.find(key);
-    if (it == mate0.end()) mate0.insert({key, a});
-    else if (a.score < it->second.score) it->second = a;
-    else if (a.score == it->second.score && a.isTranscriptome) it->second = a;
+    for (int i = 0; i < mate0.n; i++) {
+        Alignment &o = mate0.a[i];
+        if (o.pos == pos && *o.rname == *rname) {   // the same key
+            if (a.score < o.score) o = a;
+            else if (a.score == o.score && a.isTranscriptome) o = a;
+            return 0;
+        }
+    }
+    mate0.a[mate0.n++] = a;
     return 0;
 }
 
 // AlignmentFilter::FilterSingle (AlignmentFilter.cpp:216-300)
-bool filterSingle(const Ctx &C, const std::map<std::string, Alignment> &mate0, FilterOut &o, std::string *err,
-                  std::string &countTranscript) {
-    std::vector<Alignment> al;
-    for (auto &m : mate0)
-        if (!(m.second.score > (int)C.maxDist)) al.push_back(m.second);
-    if (al.empty()) { o = FilterOut(); return true; }
-    if (al.size() > 1) std::sort(al.begin(), al.end());
-    const Alignment &a = al[0];
+bool filterSingle(const Ctx &C, Mate0 &mate0, FilterOut &o, std::string *err) {
+    if (mate0.n == 2 && keyLess(mate0.a[1], mate0.a[0])) std::swap(mate0.a[0], mate0.a[1]);   // map order
+    const Alignment *al[2];
+    int na = 0;
+    for (int i = 0; i < mate0.n; i++)
+        if (!(mate0.a[i].score > (int)C.maxDist)) al[na++] = &mate0.a[i];
+    if (na == 0) { o = FilterOut(); return true; }
+    if (na == 2 && al[1]->score < al[0]->score) std::swap(al[0], al[1]);   // std::sort of two: stable
+    const Alignment &a = *al[0];
     if (a.isTranscriptome) {
-        auto po = C.pieceByName.find(a.rname);
-        if (po == C.pieceByName.end()) { *err = "chromosome " + a.rname + " not in the genome"; return false; }
+        auto po = C.pieceByName.find(*a.rname);
+        if (po == C.pieceByName.end()) { *err = "chromosome " + *a.rname + " not in the genome"; return false; }
         o.tlocation = a.location;
         o.location = po->second + a.pos - 1;
     } else {
@@ -130,10 +157,11 @@ bool filterSingle(const Ctx &C, const std::map<std::string, Alignment> &mate0, F
     o.direction = a.direction;
     o.score = a.score;
     o.isTranscriptome = a.isTranscriptome;
-    if (al.size() == 1 || (uint32_t)(al[1].score - al[0].score) >= C.confDiff) {
+    o.countTranscript = nullptr;
+    if (na == 1 || (uint32_t)(al[1]->score - al[0]->score) >= C.confDiff) {
         o.mapq = 70;   // min(maxMAPQ, genome_mapq), both 70
         o.result = SNAPGPU_SINGLE_HIT;
-        if (a.isTranscriptome) { countTranscript = a.transcriptId; o.countTranscript = &countTranscript; }
+        if (a.isTranscriptome) o.countTranscript = a.transcriptId;
     } else {
         o.mapq = 1;
         o.result = SNAPGPU_MULTIPLE_HITS;
@@ -214,19 +242,33 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
     for (uint64_t j = 0; j < nu; j++) { uo[j] = reads->offsets[ui[j]]; ul[j] = reads->lengths[ui[j]]; }
     snapgpu_reads_t *ub = readsView(reads, nu, uo.data(), ul.data());   // the useful reads, no copy
     if (!ub) return SNAPGPU_ENOMEM;
-    std::vector<snapgpu_result_t> tr(nu + 1), gr(nu + 1);
+    // per-read arrays the stages below write in full are left uninitialised (the two CIGAR op tables
+    // alone are 2 x 256 MB per 1M reads, and zero-filling them was most of the call's preparation)
+    std::unique_ptr<snapgpu_result_t[]> tr(new snapgpu_result_t[nu + 1]), gr(new snapgpu_result_t[nu + 1]);
     std::vector<FilterOut> fo(nu + 1);
-    std::vector<std::string> countTid(nu + 1);
-    std::vector<int32_t> ged(nu + 1, -1), ted(nu + 1, -1);
-    std::vector<uint32_t> gn(nu + 1, 0), tn(nu + 1, 0), gops((nu + 1) * SNAPGPU_CIGAR_MAX_OPS),
-        tops((nu + 1) * SNAPGPU_CIGAR_MAX_OPS);
+    std::vector<int32_t> ted(nu + 1, -1);   // NM of the transcriptome records
+    // the genome records' CIGARs stay in the genome aligner's pinned output buffer (NM, op counts,
+    // rows of SNAPGPU_CIGAR_MAX_OPS ops): no copy of 1M rows of 64 slots
+    const int32_t *ged = nullptr;
+    const uint32_t *gn = nullptr, *gops = nullptr;
     std::vector<std::string> splice(nu + 1);
     auto fail = [&](int code) { snapgpu_reads_free(ub); return code; };
+    st.prepMs = msSince(w0);
     auto t0 = std::chrono::steady_clock::now();
     if (nu) {
-        // t_aligner then g_aligner (SingleAligner.cpp:270-276), each over the whole batch
-        if ((rc = snapgpu_align_batch(ta, ub, tr.data()))) return fail(rc);
-        if ((rc = snapgpu_align_batch(ga, ub, gr.data()))) return fail(rc);
+        // t_aligner then g_aligner (SingleAligner.cpp:270-276), each over the whole batch; the two
+        // aligners have their own streams, so both batches are submitted before either is waited for
+        // (the genome batch's upload and kernels overlap the transcriptome batch's tail and host work)
+        if ((rc = snapgpu_align_batch_submit(ta, ub, tr.get()))) { snapgpu_align_batch_wait(ta); return fail(rc); }
+        if (ga != ta && (rc = snapgpu_align_batch_submit(ga, ub, gr.get()))) {
+            snapgpu_align_batch_wait(ta);
+            snapgpu_align_batch_wait(ga);
+            return fail(rc);
+        }
+        const int rt = snapgpu_align_batch_wait(ta);
+        const int rg = ga != ta ? snapgpu_align_batch_wait(ga) : SNAPGPU_OK;
+        if ((rc = rt ? rt : rg)) return fail(rc);
+        if (ga == ta && (rc = snapgpu_align_batch(ga, ub, gr.get()))) return fail(rc);   // one aligner for both
     }
     st.alignMs = msSince(t0);
     t0 = std::chrono::steady_clock::now();
@@ -234,13 +276,12 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
     for (size_t p = 0; p < gi->genome->pieceNames.size(); p++) C.pieceByName.insert({gi->genome->pieceNames[p], gi->genome->pieceOffsets[p]});
     std::vector<std::string> errs(hostThreads(16));
     parallel(nu, [&](unsigned t, uint64_t b, uint64_t e) {
-        std::map<std::string, Alignment> mate0;
         for (uint64_t j = b; j < e && errs[t].empty(); j++) {
-            mate0.clear();
+            Mate0 mate0;
             // AlignmentFilter (AlignmentFilter.cpp:107-109); AddAlignment uses read1 = the read
             if (addAlignment(C, mate0, tr[j].location, tr[j].direction, tr[j].score, true, ul[j], &errs[t]) == -2) break;
             if (addAlignment(C, mate0, gr[j].location, gr[j].direction, gr[j].score, false, ul[j], &errs[t]) == -2) break;
-            if (!filterSingle(C, mate0, fo[j], &errs[t], countTid[j])) break;
+            if (!filterSingle(C, mate0, fo[j], &errs[t])) break;
         }
     });
     for (auto &e : errs) if (!e.empty()) { setError("single_align: " + e); return fail(SNAPGPU_EFORMAT); }
@@ -280,27 +321,57 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
             nt += isT;
         }
         st.transcriptomeRecords = nt;
-        if ((rc = snapgpu_cigar_batch(ga, ub, gl.data(), gd.data(), (int)opt->useM, ged.data(), gn.data(), gops.data())))
-            return fail(rc);
-        if (nt && (rc = snapgpu_cigar_batch(ta, ub, tl.data(), td.data(), (int)opt->useM, ted.data(), tn.data(), tops.data())))
-            return fail(rc);
+        // the transcriptome records only (a compact batch, copied out), and the genome batch over every
+        // record (left pinned); on two host threads when the aligners differ (each has its own side
+        // stream and buffers)
+        std::vector<uint64_t> tj, to;
+        std::vector<uint32_t> tlen, tloc;
+        std::vector<uint8_t> tdir;
+        tj.reserve(nt); to.reserve(nt); tlen.reserve(nt); tloc.reserve(nt); tdir.reserve(nt);
+        for (uint64_t j = 0; j < nu; j++)
+            if (tl[j] != kInvalidLocation) {
+                tj.push_back(j); to.push_back(uo[j]); tlen.push_back(ul[j]); tloc.push_back(tl[j]); tdir.push_back(td[j]);
+            }
+        std::vector<int32_t> tedc(nt + 1, -1);
+        std::vector<uint32_t> tnc(nt + 1, 0);
+        std::unique_ptr<uint32_t[]> topsc(new uint32_t[(nt + 1) * SNAPGPU_CIGAR_MAX_OPS]);
+        const char *const bb[2] = {reads->bases, reads->bases};
+        int rcT = SNAPGPU_OK, rcG = SNAPGPU_OK;
+        auto runT = [&] {
+            if (nt) rcT = snapgpu_internal_cigar_view(ta, bb, nullptr, to.data(), tlen.data(), nt, tloc.data(), tdir.data(),
+                                                      (int)opt->useM, tedc.data(), tnc.data(), topsc.get());
+        };
+        auto runG = [&] {
+            rcG = snapgpu_internal_cigar_pinned(ga, bb, nullptr, uo.data(), ul.data(), nu, gl.data(), gd.data(),
+                                                (int)opt->useM, &ged, &gn, &gops);
+        };
+        if (ga != ta && nt) {
+            std::thread th(runT);
+            runG();
+            th.join();
+        } else {
+            runT();   // (first: with one aligner for both, the genome call reuses its output buffer)
+            runG();
+        }
+        if (rcT || rcG) return fail(rcT ? rcT : rcG);
+        for (uint64_t k = 0; k < nt; k++) ted[tj[k]] = tedc[k];
         // transcriptome records: computeCigarString's tokens (soft clips around the ops) through
         // insertSpliceJunctions (SAM.cpp:1049-1064); an unsuccessful LV leaves no tokens
-        parallel(nu, [&](unsigned, uint64_t b, uint64_t e) {
+        parallel(nt, [&](unsigned, uint64_t b, uint64_t e) {
             std::vector<std::pair<uint32_t, char>> tk;
             static const char kOp[] = "MIDNSHP=X";
-            for (uint64_t j = b; j < e; j++) {
-                if (tl[j] == kInvalidLocation) continue;
+            for (uint64_t k = b; k < e; k++) {
+                const uint64_t j = tj[k];
                 tk.clear();
                 const uint64_t i = ui[j];
-                if (ted[j] >= 0) {
+                if (tedc[k] >= 0) {
                     const uint32_t full = reads->unclippedLength[i], front = reads->frontClipped[i];
                     const uint32_t back = full - ul[j] - front;
                     const bool rcd = fo[j].direction == SNAPGPU_RC;
                     const uint32_t before = rcd ? back : front, after = rcd ? front : back;
                     if (before) tk.push_back({before, 'S'});
-                    for (uint32_t k = 0; k < tn[j]; k++) {
-                        const uint32_t op = tops[j * SNAPGPU_CIGAR_MAX_OPS + k];
+                    for (uint32_t q = 0; q < tnc[k]; q++) {
+                        const uint32_t op = topsc[k * SNAPGPU_CIGAR_MAX_OPS + q];
                         tk.push_back({op >> 4, kOp[op & 15]});
                     }
                     if (after) tk.push_back({after, 'S'});
@@ -365,7 +436,7 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
                     L.ed = ted[j];
                 } else {
                     L.ed = ged[j];
-                    L.ops = gops.data() + j * SNAPGPU_CIGAR_MAX_OPS;
+                    L.ops = gops + j * SNAPGPU_CIGAR_MAX_OPS;
                     L.nOps = gn[j];
                 }
                 // updateStats (SingleAligner.cpp:338-365)
@@ -407,7 +478,26 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
             const std::string sorted = samSortRecords(*gi->genome, parts);
             ok = ok && fwrite(sorted.data(), 1, sorted.size(), f) == sorted.size();
         } else {
-            for (auto &p : parts) ok = ok && fwrite(p.data(), 1, p.size(), f) == p.size();
+            // the parts at their offsets after the header, one pwrite per writer thread (a single
+            // fwrite of 270 MB of lines was ~70 ms of the 1M-read call's record stage)
+            ok = ok && fflush(f) == 0;
+            const int fd = fileno(f);
+            std::vector<uint64_t> at(parts.size() + 1, hdr.size());
+            for (size_t p = 0; p < parts.size(); p++) at[p + 1] = at[p] + parts[p].size();
+            std::vector<uint8_t> wok(parts.size(), 1);
+            auto put = [&](size_t p) {
+                for (uint64_t w = 0; w < parts[p].size();) {
+                    const ssize_t r = pwrite(fd, parts[p].data() + w, parts[p].size() - w, (off_t)(at[p] + w));
+                    if (r <= 0) { wok[p] = 0; break; }
+                    w += (uint64_t)r;
+                }
+            };
+            std::vector<std::thread> wt;
+            for (size_t p = 1; p < parts.size(); p++) wt.emplace_back(put, p);
+            if (!parts.empty()) put(0);
+            for (auto &x : wt) x.join();
+            for (auto x : wok) ok = ok && x;
+            ok = ok && fseeko(f, (off_t)at.back(), SEEK_SET) == 0;
         }
     }
     ok = (fclose(f) == 0) && ok;

@@ -263,3 +263,64 @@ def test_library_identity_matches_sources():
 
     with pytest.raises(F.StaleLibraryError):
         F.check_source_identity(Stale())
+
+
+def _fastq_reference_parse(data):
+    """The FASTQ reading rules, restated line by line (FASTQReader::getNextRead, FASTQ.cpp:196-253, as
+    snapgpu_reads_from_fastq applies them): a line is cut at its first NUL byte and loses its trailing
+    CR/LF bytes; every four lines are a record (a trailing partial record is ignored); id = header
+    without '@'; a quality line shorter than the bases is NUL-padded."""
+    lines = data.split(b"\n")
+    if lines and lines[-1] == b"":
+        lines.pop()
+    out = []
+    for r in range(len(lines) // 4):
+        rec = [l.split(b"\0", 1)[0].rstrip(b"\r\n") for l in lines[4 * r:4 * r + 4]]
+        assert rec[0].startswith(b"@")
+        b, q = rec[1], rec[3][:len(rec[1])]
+        out.append((rec[0][1:], b, q + b"\0" * (len(b) - len(q))))
+    return out
+
+
+@pytest.mark.parametrize("case", ["plain", "crlf", "no_final_newline", "partial_record", "nul_and_short_quals",
+                                  "big"])
+def test_fastq_parser_rules(tmp_path, case):
+    """snapgpu_reads_from_fastq (mapped file, newline index and copies on host threads) against the
+    line-by-line rules on edge cases and on a 60 MB file that takes the parallel path."""
+    import random
+    rng = random.Random(7)
+
+    def rec(i, L):
+        s = bytes(rng.choice(b"ACGTN") for _ in range(L))
+        return b"@r%d extra\n%s\n+\n%s\n" % (i, s, bytes(rng.choice(b"!#5I") for _ in range(L)))
+    if case == "big":
+        one = [rec(i, 90 + i % 40) for i in range(2000)]
+        data = b"".join(one) * 150   # 300k records, ~60 MB
+    else:
+        data = b"".join(rec(i, 50 + 7 * i) for i in range(40))
+        if case == "crlf":
+            data = data.replace(b"\n", b"\r\n")
+        elif case == "no_final_newline":
+            data = data[:-1]
+        elif case == "partial_record":
+            data += b"@tail\nACGT\n"
+        elif case == "nul_and_short_quals":
+            data = data.replace(b"+\n!", b"+\n!\0junk", 3).replace(b"@r5 extra", b"@r5\0hidden")
+            data += b"@short\nACGTACGT\n+\nII\n"
+    p = tmp_path / "x.fq"
+    p.write_bytes(data)
+    want = _fastq_reference_parse(data)
+    r = snapgpu.Reads.from_fastq(p)
+    assert r.n == len(want)
+    ids = r.ids()
+    idx = range(len(want)) if len(want) < 1000 else list(range(0, len(want), 997)) + [len(want) - 1]
+    for i in idx:
+        b, q = r.get(i)
+        assert (ids[i].encode() if isinstance(ids[i], str) else ids[i], bytes(b), bytes(q)) == want[i], i
+
+
+def test_fastq_parser_refuses_a_record_without_header(tmp_path):
+    p = tmp_path / "bad.fq"
+    p.write_bytes(b"@a\nACGT\n+\nIIII\nb\nACGT\n+\nIIII\n")
+    with pytest.raises(snapgpu.SnapGpuError):
+        snapgpu.Reads.from_fastq(p)
