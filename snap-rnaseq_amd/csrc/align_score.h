@@ -314,6 +314,68 @@ __device__ __forceinline__ void lv_prob_pair(const DevTables *tab, const GroupLd
     net2 = __popcll(ins) - __popcll(del);
 }
 
+// The same match probabilities for every group of a pass at once, right after its LV calls (verdict
+// r5 #2: the factor loads of all the pass's possible successes are issued together, before the
+// in-order apply, instead of one success at a time inside it).  Lane l: direction dx = l >> 5, path
+// slot sl = l & 31 of group g = sl / S (S = GS / 2 slots per group, G.pa / G.pm layout), step j = sl % S
+// (steps 1..e; the slot j = 0 is never a step and its lane leads the segment).  Per segment the
+// arithmetic of lv_prob_pair: offsets from a segmented inclusive scan of the step deltas, indel run
+// lengths back to the segment's previous run end, one factor per step, multiplied in step order at the
+// leader (after i wave_shl:1 moves it holds step i's factor), then the perfect-match factor.  gok: the
+// lane's group succeeded in both directions (its paths are recorded); s0 / rcRead: its seed offset and
+// direction.  -> leader lanes: qv = product * perfect (lane g*S forward, 32 + g*S reverse); reverse
+// leaders: netv = insertions - deletions of the reverse path.
+template <int GS, int NW>
+__device__ __forceinline__ void lv_prob_groups(const GroupLdsT<NW> &G, bool gok, int n, int s0, int seedLen,
+                                               uint32_t rcRead, const char *fwdQ, double &qv, int &netv) {
+    constexpr int S = GS / 2;
+    const int lane = lane_id();
+    const int dx = lane >> 5, sl = lane & 31, g = sl / S, j = sl % S;
+    const int e = gok ? (int)G.plen[dx][g] : 0;
+    const int L0 = G.pL0[dx][g];
+    const bool valid = j >= 1 && j <= e;
+    const int a = valid ? G.pa[dx][sl] : -1;
+    const int pmv = valid ? G.pm[dx][sl] : 0;
+    const int an = valid && j + 1 <= e ? G.pa[dx][sl + 1] : -2;
+    const bool runEnd = valid && (j == e || pmv != 0 || an != a);
+    const int delta = valid ? (a == 1 ? -1 : 1) + pmv : 0;
+    int incl = delta;   // segmented inclusive scan: row shifts masked at the segment start
+    { const int t = __builtin_amdgcn_update_dpp(0, incl, 0x111, 0xf, 0xf, true); incl += j >= 1 ? t : 0; }   // row_shr:1
+    if constexpr (S > 2) { const int t = __builtin_amdgcn_update_dpp(0, incl, 0x112, 0xf, 0xf, true); incl += j >= 2 ? t : 0; }
+    if constexpr (S > 4) { const int t = __builtin_amdgcn_update_dpp(0, incl, 0x114, 0xf, 0xf, true); incl += j >= 4 ? t : 0; }
+    if constexpr (S > 8) { const int t = __builtin_amdgcn_update_dpp(0, incl, 0x118, 0xf, 0xf, true); incl += j >= 8 ? t : 0; }
+    if constexpr (S > 16) incl += __builtin_amdgcn_update_dpp(0, incl, 0x142, 0xa, 0xf, false);   // row_bcast:15 into rows 1, 3
+    const int offset = L0 + incl - delta;
+    const uint64_t ends = ballot(runEnd);
+    const uint64_t below = (ends >> (lane - j)) & ((1ull << j) - 1) & ~1ull;   // run ends at steps 1..j-1
+    const int cnt = j - (below ? 63 - (int)__builtin_clzll(below) : 0);
+    const int t0 = s0 + seedLen;
+    const int patternLen = dx ? s0 : n - t0;
+    const int p0 = dx ? s0 - 1 : t0;
+    int qi = offset < 0 ? 0 : offset;
+    if (qi > patternLen - 1) qi = patternLen - 1;
+    const int DIR = dx ? -1 : 1;
+    double f = 1.0;
+    if (valid && a == 0) {
+        const int p = p0 + DIR * qi;
+        f = g_tab.phred[(uint8_t)fwdQ[rcRead ? n - 1 - p : p]];
+    } else if (runEnd) f = g_tab.indel[cnt];
+    const double perf = j == 0 && gok ? g_tab.perfect[patternLen - e] : 1.0;
+    const int emax = (int)max_reduce32((uint32_t)e);
+    double q = 1.0;
+    uint64_t fb = (uint64_t)__double_as_longlong(f);
+    for (int i = 1; i <= emax; i++) {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)fb, 0x130, 0xf, 0xf, false);          // wave_shl:1
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(fb >> 32), 0x130, 0xf, 0xf, false);
+        fb = ((uint64_t)hi << 32) | lo;
+        if (i <= e) q *= __longlong_as_double((long long)fb);
+    }
+    qv = q * perf;
+    constexpr uint64_t SEG = S >= 64 ? ~0ull : (1ull << S) - 1;
+    const uint64_t ins = ballot(valid && dx == 1 && a == 2), del = ballot(valid && dx == 1 && a == 1);
+    netv = __popcll((ins >> lane) & SEG) - __popcll((del >> lane) & SEG);
+}
+
 // Terminal branch of score() (BaseAligner.cpp:1081-1103) + computeMAPQ (mapq.h:32-65).
 __device__ __forceinline__ void finalize_read(const KArgs &A, ReadState &st, int *result, uint32_t *flags) {
     st.outScore = (int32_t)st.bestScore;
@@ -452,7 +514,19 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem6
     PassLane P;
     int e1 = -1, e2 = -1;
     P.act = false; P.s = 0;
-    if (m > 0) lv_pass<GS, MAXLEN>(A, S, ar, lvIdx, m, k, n, P, e1, e2);
+    double qv = 1.0;   // the groups' match probabilities (lv_prob_groups), at their leader lanes
+    int netv = 0;
+    if (m > 0) {
+        lv_pass<GS, MAXLEN>(A, S, ar, lvIdx, m, k, n, P, e1, e2);
+        PH_T(A, tpr);
+        // this lane's segment's group: its distances, act, seed offset and direction in one ds_bpermute
+        const int gsrc = ((lane_id() & 31) / (GS / 2)) * GS;
+        const int gpk = shfl_idx((e1 + 1) | (e2 + 1) << 5 | (P.act ? 1 << 10 : 0) | P.dir << 11 | P.s << 12, gsrc);
+        const bool gok = (gpk & 31) != 0 && ((gpk >> 5) & 31) != 0 && ((gpk >> 10) & 1) != 0;
+        lv_prob_groups<GS, Lds<MAXLEN>::NW>(G, gok, (int)n, gpk >> 12, (int)A.seedLen, (uint32_t)(gpk >> 11) & 1u, S.fwdQ,
+                                            qv, netv);
+        PH_ADD(A, S, PH_PROB, tpr);
+    }
     PH_T(A, tapp);
     // ---- apply in order with the limit in force at each candidate.  A failure only sets its scored
     // bit and, for an element's first scored candidate, bestLoc/bestScore/prob (BaseAligner.cpp:
@@ -526,7 +600,6 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem6
             const uint32_t cKey = rl(ev, 6), cBest = rl(ev, 8);
             const uint32_t sc = (uint32_t)(r1 + r2);
             PH_CNT(A, S, PH_NSUCC, 1);
-            const int s0 = readlane(P.s, gs * GS), t0 = s0 + (int)A.seedLen;
             const uint32_t dir = cKey & 1;
             const uint32_t ebase = (cKey >> 1) * ELEM;
             const uint32_t elemLoc = ebase + cbit;
@@ -549,12 +622,9 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem6
                 }
             }
             PH_ADD(A, S, PH_NEARBY, tnb);
-            PH_T(A, tpr);
-            double q1, q2;
-            int net2;
-            lv_prob_pair(tab, G, gs, gs * (GS / 2), (int)n, s0, t0, S.fwdQ, dir, q1, q2, net2);
+            const double q1 = readlaned(qv, gs * (GS / 2)), q2 = readlaned(qv, 32 + gs * (GS / 2));
+            const int net2 = readlane(netv, 32 + gs * (GS / 2));
             const double prob = q1 * q2 * tab->seedProb;
-            PH_ADD(A, S, PH_PROB, tpr);
             PH_T(A, twt);
             const uint32_t loc = elemLoc + (uint32_t)net2;
             const bool anyNearby0 = cScored != 0;

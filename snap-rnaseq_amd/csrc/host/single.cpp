@@ -18,6 +18,7 @@
 #include <thread>
 #include <vector>
 
+#include <sys/mman.h>
 #include <unistd.h>
 
 namespace snapgpu {
@@ -455,7 +456,7 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
             return fail(SNAPGPU_EINVAL);
         }
     for (unsigned t = 0; t < nt; t++) { st.singleHits += cnt[16 * t]; st.multiHits += cnt[16 * t + 1]; st.notFound += cnt[16 * t + 2]; }
-    FILE *f = fopen(samPath, "w");
+    FILE *f = fopen(samPath, "w+");   // (read + write: the records are copied into a shared mapping of the file)
     if (!f) { setError(std::string("cannot write ") + samPath); return fail(SNAPGPU_EIO); }
     uint64_t hlen = 0;
     const int so = opt->sortOutput ? 1 : 0;   // @HD SO:coordinate (SAMFormat::writeHeader, sorted)
@@ -478,26 +479,29 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
             const std::string sorted = samSortRecords(*gi->genome, parts);
             ok = ok && fwrite(sorted.data(), 1, sorted.size(), f) == sorted.size();
         } else {
-            // the parts at their offsets after the header, one pwrite per writer thread (a single
-            // fwrite of 270 MB of lines was ~70 ms of the 1M-read call's record stage)
+            // the file sized once and mapped, the parts copied in at their offsets by their writer
+            // threads (page allocation in parallel); a target that cannot be mapped (a pipe) takes the
+            // sequential writes.  (One fwrite of the 270 MB of a 1M-read call was ~70 ms of its record
+            // stage; parallel pwrites serialise on the file's lock on tmpfs and were slower still.)
             ok = ok && fflush(f) == 0;
             const int fd = fileno(f);
             std::vector<uint64_t> at(parts.size() + 1, hdr.size());
             for (size_t p = 0; p < parts.size(); p++) at[p + 1] = at[p] + parts[p].size();
-            std::vector<uint8_t> wok(parts.size(), 1);
-            auto put = [&](size_t p) {
-                for (uint64_t w = 0; w < parts[p].size();) {
-                    const ssize_t r = pwrite(fd, parts[p].data() + w, parts[p].size() - w, (off_t)(at[p] + w));
-                    if (r <= 0) { wok[p] = 0; break; }
-                    w += (uint64_t)r;
-                }
-            };
-            std::vector<std::thread> wt;
-            for (size_t p = 1; p < parts.size(); p++) wt.emplace_back(put, p);
-            if (!parts.empty()) put(0);
-            for (auto &x : wt) x.join();
-            for (auto x : wok) ok = ok && x;
-            ok = ok && fseeko(f, (off_t)at.back(), SEEK_SET) == 0;
+            void *m = MAP_FAILED;
+            if (ok && at.back() > hdr.size() && ftruncate(fd, (off_t)at.back()) == 0)
+                m = mmap(nullptr, at.back(), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+            if (m != MAP_FAILED) {
+                char *dst = (char *)m;
+                std::vector<std::thread> wt;
+                for (size_t p = 1; p < parts.size(); p++)
+                    wt.emplace_back([&, p] { memcpy(dst + at[p], parts[p].data(), parts[p].size()); });
+                if (!parts.empty()) memcpy(dst + at[0], parts[0].data(), parts[0].size());
+                for (auto &x : wt) x.join();
+                ok = munmap(m, at.back()) == 0 && ok;
+                ok = ok && fseeko(f, (off_t)at.back(), SEEK_SET) == 0;
+            } else {
+                for (auto &p : parts) ok = ok && fwrite(p.data(), 1, p.size(), f) == p.size();
+            }
         }
     }
     ok = (fclose(f) == 0) && ok;
