@@ -482,7 +482,8 @@ def single_leg(args, idx, local, build_threads):
         return {"value": n / dt, "unit": "reads/s", "reads": n, "ms_per_batch": dt * 1e3,
                 "read_len": 100, "workload": info, "transcriptome_bases": tidx.info()["nBases"],
                 "stage_ms": {"fastq_parse": round(float(parse[k]) * 1e3, 2),
-                             **{x: round(st[x], 2) for x in ("alignMs", "filterMs", "cigarMs", "writeMs", "wallMs")}},
+                             **{x: round(st[x], 2) for x in ("prepMs", "alignMs", "filterMs", "cigarMs", "writeMs",
+                                                              "formatMs", "ioMs", "wallMs")}},
                 "records": {x: int(st[x]) for x in ("usefulReads", "singleHits", "multiHits", "notFound",
                                                     "transcriptomeRecords")},
                 "sam_bytes": os.path.getsize(sam), "prep_s": round(t_prep, 1),

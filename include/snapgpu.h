@@ -517,6 +517,7 @@ typedef struct snapgpu_single_stats {   /* AlignerStats (AlignerStats.h:40-69) *
     uint64_t totalReads, usefulReads, singleHits, multiHits, notFound, transcriptomeRecords;
     double alignMs, cigarMs, filterMs, writeMs, wallMs;
     double prepMs;   /* clipping, pre-filter, the batch view and the per-read arrays (before alignMs) */
+    double formatMs, ioMs;   /* of writeMs: the records' text (host threads), the file output */
 } snapgpu_single_stats_t;
 
 /* reads: a FASTQ batch with ids (snapgpu_reads_from_fastq), clipped here.  samPath receives

@@ -399,11 +399,18 @@ bool gtfGeneCheckBoundary(const GtfGene *ge, const std::string &chr, uint32_t po
 }
 
 // GTFReader::IncrementReadCount(transcript, ...) single-read form (:1388-1407): the gene only
+uint32_t *gtfGeneCounter(snapgpu_gtf_t *g, const std::string &transcriptId);
 void gtfCountSingle(snapgpu_gtf_t *g, const std::string &transcriptId) {
+    if (uint32_t *c = gtfGeneCounter(g, transcriptId)) (*c)++;
+}
+
+// the read counter of the gene of a transcript (GTFReader::IncrementReadCount, single form), or
+// nullptr: resolved once per transcript by a caller that counts many reads
+uint32_t *gtfGeneCounter(snapgpu_gtf_t *g, const std::string &transcriptId) {
     auto t = g->transcripts.find(transcriptId);
-    if (t == g->transcripts.end()) return;
+    if (t == g->transcripts.end()) return nullptr;
     auto ge = g->genes.find(t->second.geneId);
-    if (ge != g->genes.end()) ge->second.readCount++;
+    return ge != g->genes.end() ? &ge->second.readCount : nullptr;
 }
 
 // the transcripts whose features cover every segment of one read (:1417-1486)

@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <unordered_map>
 #include <string>
 #include <thread>
 #include <vector>
@@ -29,6 +30,7 @@ uint32_t gtfGenomicPosition(const GtfTranscript *t, uint32_t pos, uint32_t span)
 bool gtfSpliceCigar(const GtfTranscript *t, uint32_t pos, const std::vector<std::pair<uint32_t, char>> &tokens,
                     std::string &out);
 void gtfCountSingle(snapgpu_gtf_t *g, const std::string &transcriptId);
+uint32_t *gtfGeneCounter(snapgpu_gtf_t *g, const std::string &transcriptId);
 }  // namespace snapgpu
 
 using namespace snapgpu;
@@ -456,6 +458,8 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
             return fail(SNAPGPU_EINVAL);
         }
     for (unsigned t = 0; t < nt; t++) { st.singleHits += cnt[16 * t]; st.multiHits += cnt[16 * t + 1]; st.notFound += cnt[16 * t + 2]; }
+    st.formatMs = msSince(t0);
+    const auto tio = std::chrono::steady_clock::now();
     FILE *f = fopen(samPath, "w+");   // (read + write: the records are copied into a shared mapping of the file)
     if (!f) { setError(std::string("cannot write ") + samPath); return fail(SNAPGPU_EIO); }
     uint64_t hlen = 0;
@@ -488,7 +492,8 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
             std::vector<uint64_t> at(parts.size() + 1, hdr.size());
             for (size_t p = 0; p < parts.size(); p++) at[p + 1] = at[p] + parts[p].size();
             void *m = MAP_FAILED;
-            if (ok && at.back() > hdr.size() && ftruncate(fd, (off_t)at.back()) == 0)
+            static const bool useMap = !(getenv("SNAPGPU_SAM_WRITE") && !strcmp(getenv("SNAPGPU_SAM_WRITE"), "fwrite"));
+            if (useMap && ok && at.back() > hdr.size() && ftruncate(fd, (off_t)at.back()) == 0)
                 m = mmap(nullptr, at.back(), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
             if (m != MAP_FAILED) {
                 char *dst = (char *)m;
@@ -505,12 +510,20 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
         }
     }
     ok = (fclose(f) == 0) && ok;
+    st.ioMs = msSince(tio);
     if (!ok) { setError(std::string("write failed: ") + samPath); return fail(SNAPGPU_EIO); }
     // the call's counts, all or nothing: gene read counts (FilterSingle :260-262, :290-292) and
     // the -ct contaminants (ContaminationFilter::AddAlignment)
     if (!contamLocs.empty() && (rc = contaminantsAddAll(opt->contaminants, contamLocs))) return fail(rc);
-    for (uint64_t j = 0; j < nu; j++)
-        if (fo[j].countTranscript) gtfCountSingle(gtf, *fo[j].countTranscript);
+    {   // (each transcript's gene counter resolved once: the names are the transcriptome's piece names)
+        std::unordered_map<const std::string *, uint32_t *> ctr;
+        for (uint64_t j = 0; j < nu; j++)
+            if (const std::string *tid = fo[j].countTranscript) {
+                auto it = ctr.find(tid);
+                if (it == ctr.end()) it = ctr.emplace(tid, gtfGeneCounter(gtf, *tid)).first;
+                if (it->second) (*it->second)++;
+            }
+    }
     st.writeMs = msSince(t0);
     st.wallMs = msSince(w0);
     if (stats) *stats = st;

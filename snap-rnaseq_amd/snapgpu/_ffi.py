@@ -202,7 +202,7 @@ class RnaPairedStats(C.Structure):
 class SingleStats(C.Structure):
     _fields_ = [(f, C.c_uint64) for f in ("totalReads", "usefulReads", "singleHits", "multiHits", "notFound",
                                           "transcriptomeRecords")] + \
-               [(f, C.c_double) for f in ("alignMs", "cigarMs", "filterMs", "writeMs", "wallMs", "prepMs")]
+               [(f, C.c_double) for f in ("alignMs", "cigarMs", "filterMs", "writeMs", "wallMs", "prepMs", "formatMs", "ioMs")]
 
 
 class SeedRuns(C.Structure):
