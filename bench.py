@@ -450,6 +450,11 @@ def single_leg(args, idx, local, build_threads):
         k = int(np.argsort(ts)[1])
         dt, st = ts[k], sts[k]
         n = int(st["totalReads"])
+        kern = {}
+        for name, al in (("transcriptome", ta), ("genome", ga)):   # the last call's GPU passes per aligner
+            t = al.timing()
+            kern[name] = {"align_kernel_busy_ms": round(t["mainKernelBusyMs"], 2), "lookup_busy_ms": round(t["lookupKernelBusyMs"], 2),
+                          "call_wall_ms": round(t["wallMs"], 2)}
         ref = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json"))).get("single_bench")
         if not ref:
             parity = {"compared": False, "why": "no single_bench digest in tests/golden/golden.json"}
@@ -486,6 +491,7 @@ def single_leg(args, idx, local, build_threads):
                                                               "formatMs", "ioMs", "wallMs")}},
                 "records": {x: int(st[x]) for x in ("usefulReads", "singleHits", "multiHits", "notFound",
                                                     "transcriptomeRecords")},
+                "aligners": kern,
                 "sam_bytes": os.path.getsize(sam), "prep_s": round(t_prep, 1),
                 "parity": parity, "cpu_baseline": cpu,
                 "params": "`snap-rna single` defaults: both aligners maxHits 300, maxK 14, 25 seeds, extra 2; "

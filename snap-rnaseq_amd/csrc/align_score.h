@@ -516,6 +516,7 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem6
     P.act = false; P.s = 0;
     double qv = 1.0;   // the groups' match probabilities (lv_prob_groups), at their leader lanes
     int netv = 0;
+    uint32_t nbv = NONE;   // lane g: the nearby element of group g's candidate
     if (m > 0) {
         lv_pass<GS, MAXLEN>(A, S, ar, lvIdx, m, k, n, P, e1, e2);
         PH_T(A, tpr);
@@ -526,6 +527,21 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem6
         lv_prob_groups<GS, Lds<MAXLEN>::NW>(G, gok, (int)n, gpk >> 12, (int)A.seedLen, (uint32_t)(gpk >> 11) & 1u, S.fwdQ,
                                             qv, netv);
         PH_ADD(A, S, PH_PROB, tpr);
+        PH_T(A, tnb);
+        // the nearby element of every group's candidate (BaseAligner.cpp:1272-1331): lane g walks group g's
+        // chain, all groups at once (no element is inserted while scoring, so the index stays valid; its
+        // header is read at the success, where it may have changed)
+        {
+            const int gl = lane_id();
+            const int src = (gl < 64 / GS ? gl : 0) * GS;
+            const uint32_t gloc = (uint32_t)shfl_idx((int)P.loc, src);
+            const int gk = shfl_idx((e1 >= 0 && e2 >= 0 && P.act ? 2 : 0) | P.dir, src);
+            if (gl < 64 / GS && (gk & 2)) {
+                const uint32_t nl = gloc + (2 * (gloc % ELEM / (ELEM / 2)) - 1) * (ELEM / 2);
+                nbv = chain_find(A, S, ar, ((nl / ELEM) << 1) | (uint32_t)(gk & 1), (uint32_t)A.arenaElems);
+            }
+        }
+        PH_ADD(A, S, PH_NEARBY, tnb);
     }
     PH_T(A, tapp);
     // ---- apply in order with the limit in force at each candidate.  A failure only sets its scored
@@ -608,11 +624,8 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem6
             uint32_t nbPre;
             int csPre = -1;
             uint32_t nvPre = 0;
-            PH_T(A, tnb);
             {
-                const uint32_t nl = elemLoc + (2 * (elemLoc % ELEM / (ELEM / 2)) - 1) * (ELEM / 2);
-                const uint32_t nkey = ((nl / ELEM) << 1) | dir;
-                nbPre = uni(chain_find(A, S, ar, nkey, (uint32_t)A.arenaElems));
+                nbPre = readlaneu(nbv, gs);   // (found for every group after the LV pass)
                 if (nbPre != NONE) {
                     const uint64_t inb = ballot((uint32_t)lane < nb && G.eidx[lane < EB ? lane : 0] == nbPre);
                     csPre = inb ? (int)__builtin_ctzll(inb) : -1;
@@ -621,7 +634,6 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem6
                     else nvPre = lane < 12 ? ((const uint32_t *)(ar + nbPre))[lane] : 0u;
                 }
             }
-            PH_ADD(A, S, PH_NEARBY, tnb);
             const double q1 = readlaned(qv, gs * (GS / 2)), q2 = readlaned(qv, 32 + gs * (GS / 2));
             const int net2 = readlane(netv, 32 + gs * (GS / 2));
             const double prob = q1 * q2 * tab->seedProb;

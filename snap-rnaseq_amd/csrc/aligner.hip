@@ -1447,6 +1447,16 @@ namespace {
 
 std::atomic<int> g_hostDevices{-2};   // HIP devices visible to hostAlloc (-2: not probed yet)
 
+// Page-locked batch buffers are parked on free and reused by the next hostAlloc of a similar size
+// (a FASTQ batch of 1M reads pins 2 x 100 MB; hipHostMalloc + hipHostFree of them was most of a
+// parse).  At most kPinParkBytes stay parked; larger frees go back to the runtime.  A batch must not
+// be freed while a submitted call still reads it -- as with the runtime's free.
+constexpr size_t kPinParkBytes = 2ull << 30;
+std::mutex g_pinMu;
+std::vector<std::pair<void *, size_t>> g_pinParked;            // (block, capacity)
+std::vector<std::pair<void *, size_t>> g_pinLive;              // blocks handed out, with their capacity
+size_t g_pinParkedBytes = 0;
+
 // Every device free goes through here: after a timeout the aligner's buffers may still be
 // in use by a running kernel, so they are left alone (see snapgpu_aligner::failed).
 void devFree(const snapgpu_aligner_t *a, void *p) {
@@ -1545,8 +1555,26 @@ void *hostAlloc(size_t bytes, bool *pinned, bool zero) {
     // batches of >= 1 MB that a GPU will copy from live in page-locked memory
     if (nd > 0 && bytes >= (1u << 20)) {
         void *p = nullptr;
-        if (hipHostMalloc(&p, bytes, hipHostMallocPortable) == hipSuccess && p) {
+        size_t cap = bytes;
+        {
+            std::lock_guard<std::mutex> lk(g_pinMu);
+            int best = -1;
+            for (size_t i = 0; i < g_pinParked.size(); i++)   // the smallest parked block that fits, within 2x
+                if (g_pinParked[i].second >= bytes && g_pinParked[i].second <= 2 * bytes &&
+                    (best < 0 || g_pinParked[i].second < g_pinParked[(size_t)best].second))
+                    best = (int)i;
+            if (best >= 0) {
+                p = g_pinParked[(size_t)best].first;
+                cap = g_pinParked[(size_t)best].second;
+                g_pinParkedBytes -= cap;
+                g_pinParked.erase(g_pinParked.begin() + best);
+            }
+        }
+        if (!p && (hipHostMalloc(&p, bytes, hipHostMallocPortable) != hipSuccess || !p)) p = nullptr;
+        if (p) {
             if (zero) memset(p, 0, bytes);
+            std::lock_guard<std::mutex> lk(g_pinMu);
+            g_pinLive.push_back({p, cap});
             *pinned = true;
             return p;
         }
@@ -1555,8 +1583,22 @@ void *hostAlloc(size_t bytes, bool *pinned, bool zero) {
 }
 void hostFree(void *p, bool pinned) {
     if (!p) return;
-    if (pinned) hipHostFree(p);
-    else free(p);
+    if (!pinned) { free(p); return; }
+    {
+        std::lock_guard<std::mutex> lk(g_pinMu);
+        for (size_t i = 0; i < g_pinLive.size(); i++)
+            if (g_pinLive[i].first == p) {
+                const size_t cap = g_pinLive[i].second;
+                g_pinLive.erase(g_pinLive.begin() + i);
+                if (g_pinParkedBytes + cap <= kPinParkBytes) {
+                    g_pinParked.push_back({p, cap});
+                    g_pinParkedBytes += cap;
+                    return;
+                }
+                break;
+            }
+    }
+    hipHostFree(p);
 }
 }  // namespace snapgpu
 

@@ -19,8 +19,6 @@
 #include <thread>
 #include <vector>
 
-#include <sys/mman.h>
-#include <unistd.h>
 
 namespace snapgpu {
 struct GtfTranscript;
@@ -245,272 +243,314 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
     for (uint64_t j = 0; j < nu; j++) { uo[j] = reads->offsets[ui[j]]; ul[j] = reads->lengths[ui[j]]; }
     snapgpu_reads_t *ub = readsView(reads, nu, uo.data(), ul.data());   // the useful reads, no copy
     if (!ub) return SNAPGPU_ENOMEM;
-    // per-read arrays the stages below write in full are left uninitialised (the two CIGAR op tables
-    // alone are 2 x 256 MB per 1M reads, and zero-filling them was most of the call's preparation)
+    // per-read arrays the stages below write in full are left uninitialised (zero-filling the CIGAR
+    // op tables of 1M reads was most of the call's preparation)
     std::unique_ptr<snapgpu_result_t[]> tr(new snapgpu_result_t[nu + 1]), gr(new snapgpu_result_t[nu + 1]);
     std::vector<FilterOut> fo(nu + 1);
     std::vector<int32_t> ted(nu + 1, -1);   // NM of the transcriptome records
-    // the genome records' CIGARs stay in the genome aligner's pinned output buffer (NM, op counts,
-    // rows of SNAPGPU_CIGAR_MAX_OPS ops): no copy of 1M rows of 64 slots
-    const int32_t *ged = nullptr;
-    const uint32_t *gn = nullptr, *gops = nullptr;
     std::vector<std::string> splice(nu + 1);
+    std::vector<int64_t> uidx(n, -1);
+    for (uint64_t j = 0; j < nu; j++) uidx[ui[j]] = (int64_t)j;
     auto fail = [&](int code) { snapgpu_reads_free(ub); return code; };
+    Ctx C{gi->genome, ti->genome, gtf, {}, opt->maxDist, opt->confDiff};
+    for (size_t p = 0; p < gi->genome->pieceNames.size(); p++) C.pieceByName.insert({gi->genome->pieceNames[p], gi->genome->pieceOffsets[p]});
+    // Sub-batches (SNAPGPU_SINGLE_SUBBATCH useful reads each; default two halves from 200k reads, one
+    // for BAM and sorted output, whose records are written as one block): stage A aligns sub-batch s
+    // (both aligners in flight) on this thread while a stage-B thread runs sub-batch s - 1's filter,
+    // CIGARs (the aligners' side streams), records and their write -- the file in input order, the
+    // counts of the whole call applied at the end, all or nothing.
+    uint64_t sub = nu;
+    if (const char *e = getenv("SNAPGPU_SINGLE_SUBBATCH"); e && atoll(e) > 0) sub = (uint64_t)atoll(e);
+    else if (nu >= 200000) sub = (nu + 1) / 2;
+    if (bam || opt->sortOutput || sub == 0) sub = nu ? nu : 1;
+    const uint64_t nSub = nu ? (nu + sub - 1) / sub : 1;
+    std::vector<snapgpu_reads_t *> views(nSub, nullptr);
+    for (uint64_t b = 0; b < nSub; b++) {
+        const uint64_t ja = b * sub, jb = std::min(nu, ja + sub);
+        views[b] = readsView(reads, jb - ja, uo.data() + ja, ul.data() + ja);
+        if (!views[b]) { for (auto *v : views) snapgpu_reads_free(v); return fail(SNAPGPU_ENOMEM); }
+    }
+    auto freeViews = [&] { for (auto *&v : views) { snapgpu_reads_free(v); v = nullptr; } };
     st.prepMs = msSince(w0);
-    auto t0 = std::chrono::steady_clock::now();
-    if (nu) {
-        // t_aligner then g_aligner (SingleAligner.cpp:270-276), each over the whole batch; the two
-        // aligners have their own streams, so both batches are submitted before either is waited for
-        // (the genome batch's upload and kernels overlap the transcriptome batch's tail and host work)
-        if ((rc = snapgpu_align_batch_submit(ta, ub, tr.get()))) { snapgpu_align_batch_wait(ta); return fail(rc); }
-        if (ga != ta && (rc = snapgpu_align_batch_submit(ga, ub, gr.get()))) {
+    // stage A of sub-batch b: t_aligner then g_aligner (SingleAligner.cpp:270-276), both submitted
+    // before either is waited for (their own streams: one's upload and kernels overlap the other's)
+    auto stageA = [&](uint64_t b) -> int {
+        const uint64_t ja = b * sub, jb = std::min(nu, ja + sub);
+        if (jb <= ja) return SNAPGPU_OK;
+        snapgpu_reads_t *v = views[b];
+        int r;
+        if ((r = snapgpu_align_batch_submit(ta, v, tr.get() + ja))) { snapgpu_align_batch_wait(ta); return r; }
+        if (ga != ta && (r = snapgpu_align_batch_submit(ga, v, gr.get() + ja))) {
             snapgpu_align_batch_wait(ta);
             snapgpu_align_batch_wait(ga);
-            return fail(rc);
+            return r;
         }
         const int rt = snapgpu_align_batch_wait(ta);
         const int rg = ga != ta ? snapgpu_align_batch_wait(ga) : SNAPGPU_OK;
-        if ((rc = rt ? rt : rg)) return fail(rc);
-        if (ga == ta && (rc = snapgpu_align_batch(ga, ub, gr.get()))) return fail(rc);   // one aligner for both
-    }
-    st.alignMs = msSince(t0);
-    t0 = std::chrono::steady_clock::now();
-    Ctx C{gi->genome, ti->genome, gtf, {}, opt->maxDist, opt->confDiff};
-    for (size_t p = 0; p < gi->genome->pieceNames.size(); p++) C.pieceByName.insert({gi->genome->pieceNames[p], gi->genome->pieceOffsets[p]});
-    std::vector<std::string> errs(hostThreads(16));
-    parallel(nu, [&](unsigned t, uint64_t b, uint64_t e) {
-        for (uint64_t j = b; j < e && errs[t].empty(); j++) {
-            Mate0 mate0;
-            // AlignmentFilter (AlignmentFilter.cpp:107-109); AddAlignment uses read1 = the read
-            if (addAlignment(C, mate0, tr[j].location, tr[j].direction, tr[j].score, true, ul[j], &errs[t]) == -2) break;
-            if (addAlignment(C, mate0, gr[j].location, gr[j].direction, gr[j].score, false, ul[j], &errs[t]) == -2) break;
-            if (!filterSingle(C, mate0, fo[j], &errs[t])) break;
-        }
-    });
-    for (auto &e : errs) if (!e.empty()) { setError("single_align: " + e); return fail(SNAPGPU_EFORMAT); }
-    // -ct (SingleAligner.cpp:282-293): the reads still NotFound through the contamination
-    // BaseAligner, one GPU batch; every read it aligns counts its contig (ContaminationFilter)
-    std::vector<uint32_t> contamLocs;   // added with the GTF counts once nothing can fail any more
-    if (opt->contaminationAligner && opt->contaminants && nu) {
-        std::vector<uint64_t> co;
-        std::vector<uint32_t> cl;
-        for (uint64_t j = 0; j < nu; j++)
-            if (fo[j].result == SNAPGPU_NOT_FOUND) { co.push_back(uo[j]); cl.push_back(ul[j]); }
-        if (!co.empty()) {
-            snapgpu_reads_t *cb = readsView(reads, co.size(), co.data(), cl.data());
-            if (!cb) return fail(SNAPGPU_ENOMEM);
-            std::vector<snapgpu_result_t> cr(co.size());
-            rc = snapgpu_align_batch(opt->contaminationAligner, cb, cr.data());
-            snapgpu_reads_free(cb);
-            if (rc) return fail(rc);
-            for (auto &r : cr)
-                if (r.result != SNAPGPU_NOT_FOUND) contamLocs.push_back(r.location);
-        }
-    }
-    st.filterMs = msSince(t0);
-    // CIGARs on the GPU: genome records at the filter's location (NotFound keeps location 0 and
-    // the forward read, SAM.cpp:1040-1048), transcriptome records on the transcriptome at tlocation
-    t0 = std::chrono::steady_clock::now();
-    if (nu) {
-        std::vector<uint32_t> gl(nu), tl(nu);
-        std::vector<uint8_t> gd(nu), td(nu);
-        uint64_t nt = 0;
-        for (uint64_t j = 0; j < nu; j++) {
-            const bool isT = fo[j].result != SNAPGPU_NOT_FOUND && fo[j].isTranscriptome;
-            gl[j] = isT ? kInvalidLocation : fo[j].location;
-            gd[j] = (uint8_t)(fo[j].result == SNAPGPU_NOT_FOUND ? 0 : fo[j].direction);
-            tl[j] = isT ? fo[j].tlocation : kInvalidLocation;
-            td[j] = (uint8_t)fo[j].direction;
-            nt += isT;
-        }
-        st.transcriptomeRecords = nt;
-        // the transcriptome records only (a compact batch, copied out), and the genome batch over every
-        // record (left pinned); on two host threads when the aligners differ (each has its own side
-        // stream and buffers)
-        std::vector<uint64_t> tj, to;
-        std::vector<uint32_t> tlen, tloc;
-        std::vector<uint8_t> tdir;
-        tj.reserve(nt); to.reserve(nt); tlen.reserve(nt); tloc.reserve(nt); tdir.reserve(nt);
-        for (uint64_t j = 0; j < nu; j++)
-            if (tl[j] != kInvalidLocation) {
-                tj.push_back(j); to.push_back(uo[j]); tlen.push_back(ul[j]); tloc.push_back(tl[j]); tdir.push_back(td[j]);
-            }
-        std::vector<int32_t> tedc(nt + 1, -1);
-        std::vector<uint32_t> tnc(nt + 1, 0);
-        std::unique_ptr<uint32_t[]> topsc(new uint32_t[(nt + 1) * SNAPGPU_CIGAR_MAX_OPS]);
-        const char *const bb[2] = {reads->bases, reads->bases};
-        int rcT = SNAPGPU_OK, rcG = SNAPGPU_OK;
-        auto runT = [&] {
-            if (nt) rcT = snapgpu_internal_cigar_view(ta, bb, nullptr, to.data(), tlen.data(), nt, tloc.data(), tdir.data(),
-                                                      (int)opt->useM, tedc.data(), tnc.data(), topsc.get());
-        };
-        auto runG = [&] {
-            rcG = snapgpu_internal_cigar_pinned(ga, bb, nullptr, uo.data(), ul.data(), nu, gl.data(), gd.data(),
-                                                (int)opt->useM, &ged, &gn, &gops);
-        };
-        if (ga != ta && nt) {
-            std::thread th(runT);
-            runG();
-            th.join();
-        } else {
-            runT();   // (first: with one aligner for both, the genome call reuses its output buffer)
-            runG();
-        }
-        if (rcT || rcG) return fail(rcT ? rcT : rcG);
-        for (uint64_t k = 0; k < nt; k++) ted[tj[k]] = tedc[k];
-        // transcriptome records: computeCigarString's tokens (soft clips around the ops) through
-        // insertSpliceJunctions (SAM.cpp:1049-1064); an unsuccessful LV leaves no tokens
-        parallel(nt, [&](unsigned, uint64_t b, uint64_t e) {
-            std::vector<std::pair<uint32_t, char>> tk;
-            static const char kOp[] = "MIDNSHP=X";
-            for (uint64_t k = b; k < e; k++) {
-                const uint64_t j = tj[k];
-                tk.clear();
-                const uint64_t i = ui[j];
-                if (tedc[k] >= 0) {
-                    const uint32_t full = reads->unclippedLength[i], front = reads->frontClipped[i];
-                    const uint32_t back = full - ul[j] - front;
-                    const bool rcd = fo[j].direction == SNAPGPU_RC;
-                    const uint32_t before = rcd ? back : front, after = rcd ? front : back;
-                    if (before) tk.push_back({before, 'S'});
-                    for (uint32_t q = 0; q < tnc[k]; q++) {
-                        const uint32_t op = topsc[k * SNAPGPU_CIGAR_MAX_OPS + q];
-                        tk.push_back({op >> 4, kOp[op & 15]});
-                    }
-                    if (after) tk.push_back({after, 'S'});
-                }
-                const Genome &tg = *ti->genome;
-                const int p = pieceAt(tg, tl[j]);
-                const GtfTranscript *t = p >= 0 ? gtfTranscript(gtf, tg.pieceNames[p]) : nullptr;
-                if (t) gtfSpliceCigar(t, tl[j] - tg.pieceOffsets[p] + 1, tk, splice[j]);
-            }
-        });
-    }
-    st.cigarMs = msSince(t0);
-    // lines in input order (writeRead, SingleAligner.cpp:322-336; filtered reads :250-254)
-    t0 = std::chrono::steady_clock::now();
-    std::vector<int64_t> uidx(n, -1);
-    for (uint64_t j = 0; j < nu; j++) uidx[ui[j]] = (int64_t)j;
-    const unsigned nt = n < 4096 ? 1u : hostThreads(16);
-    std::vector<std::string> parts(nt);
-    std::vector<uint64_t> cnt(16 * nt, 0);   // thread t's three counters at 16 t: a cache line of their own
-    // BAMFormat::writeRead sets NM only for a record with a location; the others repeat the
-    // previous record's value -- a serial pass in output order fixes each record's NM.
-    std::vector<int32_t> bamNm;
-    if (bam) {
-        bamNm.resize(n);
-        int32_t last = 0;   // before any mapped record the reference writes its stack's leftover
-        for (uint64_t i = 0; i < n; i++) {
-            const int64_t j = uidx[i];
-            if (j >= 0 && fo[j].result != SNAPGPU_NOT_FOUND)
-                last = fo[j].isTranscriptome ? ted[j] : ged[j];
-            bamNm[i] = last;
-        }
-    }
-    std::vector<uint8_t> bamBad(nt, 0);
-    parallel(n, [&](unsigned t, uint64_t b, uint64_t e) {
-        // built in a local string and swapped in at the end: the parts' string headers sit side by
-        // side in the vector, and appending through them moved their shared cache lines between
-        // the writer threads on every field
-        std::string o;
-        o.reserve((e - b) * 320);
-        for (uint64_t i = b; i < e; i++) {
-            SamLine L;
-            L.id = reads->ids + reads->idOffsets[i];
-            L.idLen = reads->idLengths[i];
-            L.front = reads->frontClipped[i];
-            L.clippedLen = reads->lengths[i];
-            L.fullLen = reads->unclippedLength[i];
-            L.bases = reads->bases + reads->offsets[i] - L.front;
-            L.quals = reads->quals + reads->offsets[i] - L.front;
-            L.rg = opt->readGroup;
-            const int64_t j = uidx[i];
-            if (j < 0) {   // readWriter->writeRead(read, NotFound, 0, InvalidGenomeLocation, ...)
-                L.result = SNAPGPU_NOT_FOUND;
-                L.loc = kInvalidLocation;
-            } else {
-                const FilterOut &f = fo[j];
-                L.result = f.result;
-                L.loc = f.location;
-                L.dir = f.direction;
-                L.mapq = f.mapq;
-                if (f.result != SNAPGPU_NOT_FOUND && f.isTranscriptome) {
-                    L.cigar = &splice[j];
-                    L.ed = ted[j];
-                } else {
-                    L.ed = ged[j];
-                    L.ops = gops + j * SNAPGPU_CIGAR_MAX_OPS;
-                    L.nOps = gn[j];
-                }
-                // updateStats (SingleAligner.cpp:338-365)
-                cnt[16 * t + (f.result == SNAPGPU_SINGLE_HIT ? 0 : f.result == SNAPGPU_MULTIPLE_HITS ? 1 : 2)]++;
-            }
-            if (bam && L.result == SNAPGPU_NOT_FOUND) L.loc = kInvalidLocation;   // BAM: FilterSingle's NotFound
-                                                                               // location 0 gives no CIGAR, bin (-1, 0)
-            if (!bam) samAppendLine(o, *gi->genome, L);
-            else if (!bamAppendRecord(o, *gi->genome, L, bamNm[i])) bamBad[t] = 1;
-        }
-        parts[t].swap(o);
-    });
-    for (unsigned t = 0; t < nt; t++)
-        if (bamBad[t]) {
-            setError("single_align: BAM record not written (QNAME longer than 254 characters, Bam.cpp:723-726)");
-            return fail(SNAPGPU_EINVAL);
-        }
-    for (unsigned t = 0; t < nt; t++) { st.singleHits += cnt[16 * t]; st.multiHits += cnt[16 * t + 1]; st.notFound += cnt[16 * t + 2]; }
-    st.formatMs = msSince(t0);
-    const auto tio = std::chrono::steady_clock::now();
-    FILE *f = fopen(samPath, "w+");   // (read + write: the records are copied into a shared mapping of the file)
-    if (!f) { setError(std::string("cannot write ") + samPath); return fail(SNAPGPU_EIO); }
+        if ((r = rt ? rt : rg)) return r;
+        if (ga == ta) r = snapgpu_align_batch(ga, v, gr.get() + ja);   // one aligner for both
+        return r;
+    };
+    // the output file and its header (SAM text; BAM after all records)
+    FILE *f = fopen(samPath, "w");
+    if (!f) { setError(std::string("cannot write ") + samPath); freeViews(); return fail(SNAPGPU_EIO); }
     uint64_t hlen = 0;
     const int so = opt->sortOutput ? 1 : 0;   // @HD SO:coordinate (SAMFormat::writeHeader, sorted)
     snapgpu_sam_header(gi, so, opt->commandLine ? opt->commandLine : "", opt->version ? opt->version : "", nullptr,
                        nullptr, 0, &hlen);
     std::string hdr(hlen, '\0');
     if ((rc = snapgpu_sam_header(gi, so, opt->commandLine ? opt->commandLine : "", opt->version ? opt->version : "",
-                                 nullptr, &hdr[0], hlen, &hlen))) { fclose(f); return fail(rc); }
+                                 nullptr, &hdr[0], hlen, &hlen))) { fclose(f); freeViews(); return fail(rc); }
     bool ok = true;
+    if (!bam) ok = fwrite(hdr.data(), 1, hdr.size(), f) == hdr.size();
+    std::vector<std::string> allParts;   // BAM / sorted: every record part, written at the end
+    std::vector<uint32_t> contamLocs;    // added with the GTF counts once nothing can fail any more
+    std::string errMsg;
+    int32_t lastNm = 0;                  // BAM NM carry-over (before any mapped record: the stack's leftover)
+    const unsigned nw = n < 4096 ? 1u : hostThreads(16);
+    std::vector<uint64_t> cnt(16 * nw, 0);   // thread t's three counters at 16 t: a cache line of their own
+    // stage B of sub-batch b (useful reads [ja, jb), input reads [ia, ib))
+    auto stageB = [&](uint64_t b) -> int {
+        const uint64_t ja = b * sub, jb = std::min(nu, ja + sub), m = jb - ja;
+        const uint64_t ia = b == 0 ? 0 : ui[ja], ib = b + 1 >= nSub ? n : ui[jb];
+        auto t0 = std::chrono::steady_clock::now();
+        std::vector<std::string> errs(hostThreads(16));
+        parallel(m, [&](unsigned t, uint64_t x, uint64_t y) {
+            for (uint64_t j = ja + x; j < ja + y && errs[t].empty(); j++) {
+                Mate0 mate0;
+                // AlignmentFilter (AlignmentFilter.cpp:107-109); AddAlignment uses read1 = the read
+                if (addAlignment(C, mate0, tr[j].location, tr[j].direction, tr[j].score, true, ul[j], &errs[t]) == -2) break;
+                if (addAlignment(C, mate0, gr[j].location, gr[j].direction, gr[j].score, false, ul[j], &errs[t]) == -2) break;
+                if (!filterSingle(C, mate0, fo[j], &errs[t])) break;
+            }
+        });
+        for (auto &e : errs) if (!e.empty()) { errMsg = "single_align: " + e; return SNAPGPU_EFORMAT; }
+        // -ct (SingleAligner.cpp:282-293): the reads still NotFound through the contamination
+        // BaseAligner, one GPU batch; every read it aligns counts its contig (ContaminationFilter)
+        if (opt->contaminationAligner && opt->contaminants && m) {
+            std::vector<uint64_t> co;
+            std::vector<uint32_t> cl;
+            for (uint64_t j = ja; j < jb; j++)
+                if (fo[j].result == SNAPGPU_NOT_FOUND) { co.push_back(uo[j]); cl.push_back(ul[j]); }
+            if (!co.empty()) {
+                snapgpu_reads_t *cb = readsView(reads, co.size(), co.data(), cl.data());
+                if (!cb) return SNAPGPU_ENOMEM;
+                std::vector<snapgpu_result_t> cr(co.size());
+                const int r = snapgpu_align_batch(opt->contaminationAligner, cb, cr.data());
+                snapgpu_reads_free(cb);
+                if (r) return r;
+                for (auto &x : cr)
+                    if (x.result != SNAPGPU_NOT_FOUND) contamLocs.push_back(x.location);
+            }
+        }
+        st.filterMs += msSince(t0);
+        // CIGARs on the GPU: genome records at the filter's location (NotFound keeps location 0 and
+        // the forward read, SAM.cpp:1040-1048), transcriptome records on the transcriptome at tlocation
+        t0 = std::chrono::steady_clock::now();
+        const int32_t *ged = nullptr;   // the genome records' CIGARs, left in the genome aligner's pinned
+        const uint32_t *gn = nullptr, *gops = nullptr;   // output buffer (indexed j - ja) until its next call
+        if (m) {
+            std::vector<uint32_t> gl(m), tl(m);
+            std::vector<uint8_t> gd(m), td(m);
+            uint64_t nt = 0;
+            for (uint64_t j = ja; j < jb; j++) {
+                const bool isT = fo[j].result != SNAPGPU_NOT_FOUND && fo[j].isTranscriptome;
+                gl[j - ja] = isT ? kInvalidLocation : fo[j].location;
+                gd[j - ja] = (uint8_t)(fo[j].result == SNAPGPU_NOT_FOUND ? 0 : fo[j].direction);
+                tl[j - ja] = isT ? fo[j].tlocation : kInvalidLocation;
+                td[j - ja] = (uint8_t)fo[j].direction;
+                nt += isT;
+            }
+            st.transcriptomeRecords += nt;
+            // the transcriptome records only (a compact batch, copied out), and the genome batch over
+            // every record (left pinned); on two host threads when the aligners differ (each has its
+            // own side stream and buffers)
+            std::vector<uint64_t> tj, to;
+            std::vector<uint32_t> tlen, tloc;
+            std::vector<uint8_t> tdir;
+            tj.reserve(nt); to.reserve(nt); tlen.reserve(nt); tloc.reserve(nt); tdir.reserve(nt);
+            for (uint64_t j = ja; j < jb; j++)
+                if (tl[j - ja] != kInvalidLocation) {
+                    tj.push_back(j); to.push_back(uo[j]); tlen.push_back(ul[j]); tloc.push_back(tl[j - ja]);
+                    tdir.push_back(td[j - ja]);
+                }
+            std::vector<int32_t> tedc(nt + 1, -1);
+            std::vector<uint32_t> tnc(nt + 1, 0);
+            std::unique_ptr<uint32_t[]> topsc(new uint32_t[(nt + 1) * SNAPGPU_CIGAR_MAX_OPS]);
+            const char *const bb[2] = {reads->bases, reads->bases};
+            int rcT = SNAPGPU_OK, rcG = SNAPGPU_OK;
+            auto runT = [&] {
+                if (nt) rcT = snapgpu_internal_cigar_view(ta, bb, nullptr, to.data(), tlen.data(), nt, tloc.data(),
+                                                          tdir.data(), (int)opt->useM, tedc.data(), tnc.data(), topsc.get());
+            };
+            auto runG = [&] {
+                rcG = snapgpu_internal_cigar_pinned(ga, bb, nullptr, uo.data() + ja, ul.data() + ja, m, gl.data(), gd.data(),
+                                                    (int)opt->useM, &ged, &gn, &gops);
+            };
+            if (ga != ta && nt) {
+                std::thread th(runT);
+                runG();
+                th.join();
+            } else {
+                runT();   // (first: with one aligner for both, the genome call reuses its output buffer)
+                runG();
+            }
+            if (rcT || rcG) return rcT ? rcT : rcG;
+            for (uint64_t k = 0; k < nt; k++) ted[tj[k]] = tedc[k];
+            // transcriptome records: computeCigarString's tokens (soft clips around the ops) through
+            // insertSpliceJunctions (SAM.cpp:1049-1064); an unsuccessful LV leaves no tokens
+            parallel(nt, [&](unsigned, uint64_t x, uint64_t y) {
+                std::vector<std::pair<uint32_t, char>> tk;
+                static const char kOp[] = "MIDNSHP=X";
+                for (uint64_t k = x; k < y; k++) {
+                    const uint64_t j = tj[k];
+                    tk.clear();
+                    const uint64_t i = ui[j];
+                    if (tedc[k] >= 0) {
+                        const uint32_t full = reads->unclippedLength[i], front = reads->frontClipped[i];
+                        const uint32_t back = full - ul[j] - front;
+                        const bool rcd = fo[j].direction == SNAPGPU_RC;
+                        const uint32_t before = rcd ? back : front, after = rcd ? front : back;
+                        if (before) tk.push_back({before, 'S'});
+                        for (uint32_t q = 0; q < tnc[k]; q++) {
+                            const uint32_t op = topsc[k * SNAPGPU_CIGAR_MAX_OPS + q];
+                            tk.push_back({op >> 4, kOp[op & 15]});
+                        }
+                        if (after) tk.push_back({after, 'S'});
+                    }
+                    const Genome &tg = *ti->genome;
+                    const int p = pieceAt(tg, tl[j - ja]);
+                    const GtfTranscript *t = p >= 0 ? gtfTranscript(gtf, tg.pieceNames[p]) : nullptr;
+                    if (t) gtfSpliceCigar(t, tl[j - ja] - tg.pieceOffsets[p] + 1, tk, splice[j]);
+                }
+            });
+        }
+        st.cigarMs += msSince(t0);
+        // lines of input reads [ia, ib) in input order (writeRead, SingleAligner.cpp:322-336; filtered
+        // reads :250-254)
+        t0 = std::chrono::steady_clock::now();
+        const uint64_t nIn = ib - ia;
+        const unsigned nt = nIn < 4096 ? 1u : nw;
+        std::vector<std::string> parts(nt);
+        // BAMFormat::writeRead sets NM only for a record with a location; the others repeat the
+        // previous record's value -- a serial pass in output order fixes each record's NM.
+        std::vector<int32_t> bamNm;
+        if (bam) {
+            bamNm.resize(nIn);
+            for (uint64_t i = ia; i < ib; i++) {
+                const int64_t j = uidx[i];
+                if (j >= 0 && fo[j].result != SNAPGPU_NOT_FOUND)
+                    lastNm = fo[j].isTranscriptome ? ted[j] : ged[j - ja];
+                bamNm[i - ia] = lastNm;
+            }
+        }
+        std::vector<uint8_t> bamBad(nt, 0);
+        auto fmt = [&](unsigned t, uint64_t x, uint64_t y) {
+            // built in a local string and swapped in at the end: the parts' string headers sit side by
+            // side in the vector, and appending through them moved their shared cache lines between
+            // the writer threads on every field
+            std::string o;
+            o.reserve((y - x) * 320);
+            for (uint64_t i = ia + x; i < ia + y; i++) {
+                SamLine L;
+                L.id = reads->ids + reads->idOffsets[i];
+                L.idLen = reads->idLengths[i];
+                L.front = reads->frontClipped[i];
+                L.clippedLen = reads->lengths[i];
+                L.fullLen = reads->unclippedLength[i];
+                L.bases = reads->bases + reads->offsets[i] - L.front;
+                L.quals = reads->quals + reads->offsets[i] - L.front;
+                L.rg = opt->readGroup;
+                const int64_t j = uidx[i];
+                if (j < 0) {   // readWriter->writeRead(read, NotFound, 0, InvalidGenomeLocation, ...)
+                    L.result = SNAPGPU_NOT_FOUND;
+                    L.loc = kInvalidLocation;
+                } else {
+                    const FilterOut &fr = fo[j];
+                    L.result = fr.result;
+                    L.loc = fr.location;
+                    L.dir = fr.direction;
+                    L.mapq = fr.mapq;
+                    if (fr.result != SNAPGPU_NOT_FOUND && fr.isTranscriptome) {
+                        L.cigar = &splice[j];
+                        L.ed = ted[j];
+                    } else {
+                        L.ed = ged[j - ja];
+                        L.ops = gops + (j - ja) * SNAPGPU_CIGAR_MAX_OPS;
+                        L.nOps = gn[j - ja];
+                    }
+                    // updateStats (SingleAligner.cpp:338-365)
+                    cnt[16 * t + (fr.result == SNAPGPU_SINGLE_HIT ? 0 : fr.result == SNAPGPU_MULTIPLE_HITS ? 1 : 2)]++;
+                }
+                if (bam && L.result == SNAPGPU_NOT_FOUND) L.loc = kInvalidLocation;   // BAM: FilterSingle's NotFound
+                                                                                   // location 0 gives no CIGAR, bin (-1, 0)
+                if (!bam) samAppendLine(o, *gi->genome, L);
+                else if (!bamAppendRecord(o, *gi->genome, L, bamNm[i - ia])) bamBad[t] = 1;
+            }
+            parts[t].swap(o);
+        };
+        if (nt == 1) fmt(0, 0, nIn);
+        else {
+            std::vector<std::thread> th;
+            for (unsigned t = 0; t < nt; t++) th.emplace_back(fmt, t, nIn * t / nt, nIn * (t + 1) / nt);
+            for (auto &x : th) x.join();
+        }
+        for (unsigned t = 0; t < nt; t++)
+            if (bamBad[t]) {
+                errMsg = "single_align: BAM record not written (QNAME longer than 254 characters, Bam.cpp:723-726)";
+                return SNAPGPU_EINVAL;
+            }
+        st.formatMs += msSince(t0);
+        t0 = std::chrono::steady_clock::now();
+        if (bam || opt->sortOutput) {
+            for (auto &p : parts) allParts.push_back(std::move(p));
+        } else {
+            // one sequential write per sub-batch, in order (the file output is ~80 ms of a 1M-read call on
+            // the box's tmpfs; parallel pwrites and a shared mapping filled by the writer threads measured
+            // slower, profiles/r06/ab/single_write_r06h.txt)
+            for (auto &p : parts) ok = ok && fwrite(p.data(), 1, p.size(), f) == p.size();
+        }
+        st.ioMs += msSince(t0);
+        return SNAPGPU_OK;
+    };
+    // the pipeline: A(0); then A(b + 1) here while B(b) runs on the stage-B thread
+    int rcA = SNAPGPU_OK, rcB = SNAPGPU_OK;
+    {
+        auto ta0 = std::chrono::steady_clock::now();
+        rcA = stageA(0);
+        st.alignMs += msSince(ta0);
+        for (uint64_t b = 0; b < nSub && rcA == SNAPGPU_OK && rcB == SNAPGPU_OK; b++) {
+            std::thread tb([&, b] { rcB = stageB(b); });
+            if (b + 1 < nSub) {
+                auto t1 = std::chrono::steady_clock::now();
+                rcA = stageA(b + 1);
+                st.alignMs += msSince(t1);
+            }
+            tb.join();
+        }
+    }
+    if (rcA || rcB) {
+        fclose(f);
+        freeViews();
+        if (!errMsg.empty()) setError(errMsg);
+        return fail(rcA ? rcA : rcB);
+    }
+    for (unsigned t = 0; t < nw; t++) { st.singleHits += cnt[16 * t]; st.multiHits += cnt[16 * t + 1]; st.notFound += cnt[16 * t + 2]; }
+    auto t0 = std::chrono::steady_clock::now();
     if (bam) {   // BGZF stream: header, then the records (64 KB blocks), then the EOF block
         hdr.resize(strnlen(hdr.data(), hdr.size()));
         const std::string bh = bamHeader(*gi->genome, hdr);
         ok = bgzfWrite(f, bh.data(), bh.size(), false);
         std::string all;
-        for (auto &p : parts) all += p;
+        for (auto &p : allParts) all += p;
         ok = ok && bgzfWrite(f, all.data(), all.size(), true);
-    } else {
-        ok = fwrite(hdr.data(), 1, hdr.size(), f) == hdr.size();
-        if (opt->sortOutput) {
-            const std::string sorted = samSortRecords(*gi->genome, parts);
-            ok = ok && fwrite(sorted.data(), 1, sorted.size(), f) == sorted.size();
-        } else {
-            // the file sized once and mapped, the parts copied in at their offsets by their writer
-            // threads (page allocation in parallel); a target that cannot be mapped (a pipe) takes the
-            // sequential writes.  (One fwrite of the 270 MB of a 1M-read call was ~70 ms of its record
-            // stage; parallel pwrites serialise on the file's lock on tmpfs and were slower still.)
-            ok = ok && fflush(f) == 0;
-            const int fd = fileno(f);
-            std::vector<uint64_t> at(parts.size() + 1, hdr.size());
-            for (size_t p = 0; p < parts.size(); p++) at[p + 1] = at[p] + parts[p].size();
-            void *m = MAP_FAILED;
-            static const bool useMap = !(getenv("SNAPGPU_SAM_WRITE") && !strcmp(getenv("SNAPGPU_SAM_WRITE"), "fwrite"));
-            if (useMap && ok && at.back() > hdr.size() && ftruncate(fd, (off_t)at.back()) == 0)
-                m = mmap(nullptr, at.back(), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
-            if (m != MAP_FAILED) {
-                char *dst = (char *)m;
-                std::vector<std::thread> wt;
-                for (size_t p = 1; p < parts.size(); p++)
-                    wt.emplace_back([&, p] { memcpy(dst + at[p], parts[p].data(), parts[p].size()); });
-                if (!parts.empty()) memcpy(dst + at[0], parts[0].data(), parts[0].size());
-                for (auto &x : wt) x.join();
-                ok = munmap(m, at.back()) == 0 && ok;
-                ok = ok && fseeko(f, (off_t)at.back(), SEEK_SET) == 0;
-            } else {
-                for (auto &p : parts) ok = ok && fwrite(p.data(), 1, p.size(), f) == p.size();
-            }
-        }
+    } else if (opt->sortOutput) {
+        const std::string sorted = samSortRecords(*gi->genome, allParts);
+        ok = ok && fwrite(sorted.data(), 1, sorted.size(), f) == sorted.size();
     }
     ok = (fclose(f) == 0) && ok;
-    st.ioMs = msSince(tio);
+    st.ioMs += msSince(t0);
+    freeViews();
     if (!ok) { setError(std::string("write failed: ") + samPath); return fail(SNAPGPU_EIO); }
     // the call's counts, all or nothing: gene read counts (FilterSingle :260-262, :290-292) and
     // the -ct contaminants (ContaminationFilter::AddAlignment)
@@ -524,7 +564,7 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
                 if (it->second) (*it->second)++;
             }
     }
-    st.writeMs = msSince(t0);
+    st.writeMs = st.formatMs + st.ioMs;
     st.wallMs = msSince(w0);
     if (stats) *stats = st;
     snapgpu_reads_free(ub);

@@ -65,7 +65,11 @@ def _records(text):
 
 
 @pytest.mark.gpu
-def test_single_contamination_matches_reference(gpu_available, tmp_path):
+@pytest.mark.parametrize("sub", [None, 53])
+def test_single_contamination_matches_reference(gpu_available, tmp_path, monkeypatch, sub):
+    """(sub: SNAPGPU_SINGLE_SUBBATCH -- the contamination batches and counts of a pipelined call)"""
+    if sub:
+        monkeypatch.setenv("SNAPGPU_SINGLE_SUBBATCH", str(sub))
     gtf, gidx, tidx, cidx = _indexes(tmp_path)
     ga, ta, ca = snapgpu.BaseAligner(gidx), snapgpu.BaseAligner(tidx), snapgpu.BaseAligner(cidx)
     counts = snapgpu.Contaminants(cidx)

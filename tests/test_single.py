@@ -55,9 +55,22 @@ def _records(text):
     return [l for l in lines if not l.startswith("@PG")]
 
 
+@pytest.fixture
+def single_sub(request, monkeypatch):
+    """SNAPGPU_SINGLE_SUBBATCH: useful reads per pipelined sub-batch of snapgpu_single_align (None: the
+    default, one sub-batch below 200k reads -- this fixture -- and two halves above; small values cut
+    the fixture into many: stage A of sub-batch s + 1 runs while stage B writes sub-batch s)."""
+    if request.param:
+        monkeypatch.setenv("SNAPGPU_SINGLE_SUBBATCH", str(request.param))
+    else:
+        monkeypatch.delenv("SNAPGPU_SINGLE_SUBBATCH", raising=False)
+    return request.param
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("use_m,fixture", [(0, "expected_single.sam.gz"), (1, "expected_single_M.sam.gz")])
-def test_single_end_product_path_matches_reference(gpu_available, tmp_path, use_m, fixture):
+@pytest.mark.parametrize("use_m,fixture,single_sub", [(0, "expected_single.sam.gz", None), (1, "expected_single_M.sam.gz", None),
+                                                      (0, "expected_single.sam.gz", 97)], indirect=["single_sub"])
+def test_single_end_product_path_matches_reference(gpu_available, tmp_path, use_m, fixture, single_sub):
     gtf, gidx, tidx = _indexes(tmp_path)
     ga = snapgpu.BaseAligner(gidx)
     ta = snapgpu.BaseAligner(tidx)
