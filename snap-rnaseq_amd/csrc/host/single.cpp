@@ -64,12 +64,15 @@ struct Alignment {
     bool isTranscriptome = false;
 };
 
+// (no default member initialisers: a 1M-read call allocates these uninitialised; filterSingle writes
+// every field of every read's entry)
 struct FilterOut {
-    const std::string *countTranscript = nullptr;   // GTFReader::IncrementReadCount (:261, :291)
-    int result = SNAPGPU_NOT_FOUND;
-    uint32_t location = 0, tlocation = 0;
-    int direction = 0, score = 0, mapq = 0;
-    bool isTranscriptome = false;
+    const std::string *countTranscript;   // GTFReader::IncrementReadCount (:261, :291)
+    int result;
+    uint32_t location, tlocation;
+    int direction, score, mapq;
+    bool isTranscriptome;
+    static FilterOut notFound() { return FilterOut{nullptr, SNAPGPU_NOT_FOUND, 0, 0, 0, 0, 0, false}; }
 };
 
 struct Ctx {
@@ -143,7 +146,7 @@ bool filterSingle(const Ctx &C, Mate0 &mate0, FilterOut &o, std::string *err) {
     int na = 0;
     for (int i = 0; i < mate0.n; i++)
         if (!(mate0.a[i].score > (int)C.maxDist)) al[na++] = &mate0.a[i];
-    if (na == 0) { o = FilterOut(); return true; }
+    if (na == 0) { o = FilterOut::notFound(); return true; }
     if (na == 2 && al[1]->score < al[0]->score) std::swap(al[0], al[1]);   // std::sort of two: stable
     const Alignment &a = *al[0];
     if (a.isTranscriptome) {
@@ -246,9 +249,8 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
     // per-read arrays the stages below write in full are left uninitialised (zero-filling the CIGAR
     // op tables of 1M reads was most of the call's preparation)
     std::unique_ptr<snapgpu_result_t[]> tr(new snapgpu_result_t[nu + 1]), gr(new snapgpu_result_t[nu + 1]);
-    std::vector<FilterOut> fo(nu + 1);
+    std::unique_ptr<FilterOut[]> fo(new FilterOut[nu + 1]);
     std::vector<int32_t> ted(nu + 1, -1);   // NM of the transcriptome records
-    std::vector<std::string> splice(nu + 1);
     std::vector<int64_t> uidx(n, -1);
     for (uint64_t j = 0; j < nu; j++) uidx[ui[j]] = (int64_t)j;
     auto fail = [&](int code) { snapgpu_reads_free(ub); return code; };
@@ -310,6 +312,8 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
     const unsigned nw = n < 4096 ? 1u : hostThreads(16);
     std::vector<uint64_t> cnt(16 * nw, 0);   // thread t's three counters at 16 t: a cache line of their own
     // stage B of sub-batch b (useful reads [ja, jb), input reads [ia, ib))
+    std::vector<std::string> splice;   // stage B's current sub-batch: transcriptome CIGARs (compact)
+    std::vector<int32_t> spliceAt;     //   and each useful read's index into them (-1: none)
     auto stageB = [&](uint64_t b) -> int {
         const uint64_t ja = b * sub, jb = std::min(nu, ja + sub), m = jb - ja;
         const uint64_t ia = b == 0 ? 0 : ui[ja], ib = b + 1 >= nSub ? n : ui[jb];
@@ -374,6 +378,9 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
                     tj.push_back(j); to.push_back(uo[j]); tlen.push_back(ul[j]); tloc.push_back(tl[j - ja]);
                     tdir.push_back(td[j - ja]);
                 }
+            splice.assign(nt, std::string());   // this sub-batch's transcriptome CIGARs, by compact index
+            spliceAt.assign(m, -1);
+            for (uint64_t k = 0; k < nt; k++) spliceAt[tj[k] - ja] = (int32_t)k;
             std::vector<int32_t> tedc(nt + 1, -1);
             std::vector<uint32_t> tnc(nt + 1, 0);
             std::unique_ptr<uint32_t[]> topsc(new uint32_t[(nt + 1) * SNAPGPU_CIGAR_MAX_OPS]);
@@ -421,7 +428,7 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
                     const Genome &tg = *ti->genome;
                     const int p = pieceAt(tg, tl[j - ja]);
                     const GtfTranscript *t = p >= 0 ? gtfTranscript(gtf, tg.pieceNames[p]) : nullptr;
-                    if (t) gtfSpliceCigar(t, tl[j - ja] - tg.pieceOffsets[p] + 1, tk, splice[j]);
+                    if (t) gtfSpliceCigar(t, tl[j - ja] - tg.pieceOffsets[p] + 1, tk, splice[k]);
                 }
             });
         }
@@ -472,7 +479,7 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
                     L.dir = fr.direction;
                     L.mapq = fr.mapq;
                     if (fr.result != SNAPGPU_NOT_FOUND && fr.isTranscriptome) {
-                        L.cigar = &splice[j];
+                        L.cigar = &splice[(size_t)spliceAt[j - ja]];
                         L.ed = ted[j];
                     } else {
                         L.ed = ged[j - ja];
