@@ -519,6 +519,7 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem6
     uint32_t nbv = NONE;   // lane g: the nearby element of group g's candidate
     if (m > 0) {
         lv_pass<GS, MAXLEN>(A, S, ar, lvIdx, m, k, n, P, e1, e2);
+      if (ballot(P.act && e1 >= 0 && e2 >= 0) != 0) {   // (a pass whose LV calls all failed applies no success)
         PH_T(A, tpr);
         // this lane's segment's group: its distances, act, seed offset and direction in one ds_bpermute
         const int gsrc = ((lane_id() & 31) / (GS / 2)) * GS;
@@ -542,6 +543,7 @@ __device__ __forceinline__ bool pass_apply(const KArgs &A, Lds<MAXLEN> &S, Elem6
             }
         }
         PH_ADD(A, S, PH_NEARBY, tnb);
+      }
     }
     PH_T(A, tapp);
     // ---- apply in order with the limit in force at each candidate.  A failure only sets its scored
