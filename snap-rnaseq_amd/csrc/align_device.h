@@ -752,7 +752,7 @@ enum : int { PH_SETUP = 0, PH_LOOKUP, PH_INSERT, PH_SCORE, PH_POP, PH_DESC, PH_S
              PH_WB, PH_OUT, PH_NPASS, PH_NCAND, PH_NREAD, PH_NPASS16, PH_NPASS32, PH_NPASS64, PH_ROWSF, PH_ROWSR,
              PH_NSCORECALL, PH_NFORCED, PH_NPOPPED, PH_NSUCC, PH_PASSLOOP, PH_SEL, PH_FETCH, PH_SEEDLOOP, PH_NBATCH,
              PH_RANK, PH_NELEMSF, PH_CANDL, PH_SUCC, PH_NEARBY, PH_PROB, PH_FAILS, PH_NFAILSTEP, PH_SUCCWB,
-             PH_NPASSF, PH_PASSLOOPF, PH_HEAVYCYC, PH_NHEAVY, PH_NCANDF, PH_READCYC, PH_NFILTER,
+             PH_NPASSF, PH_PASSLOOPF, PH_HEAVYCYC, PH_NHEAVY, PH_NCANDF, PH_READCYC, PH_NFILTER, PH_NLVF, PH_NLVFK, PH_NFRES,
              PH_SLOTS = 48 };
 __device__ __forceinline__ uint64_t clk() { return __builtin_amdgcn_s_memtime(); }
 #if SNAPGPU_PHASE_TIMERS

@@ -808,7 +808,7 @@ __device__ __forceinline__ bool forced_sort(const KArgs &A, Lds<MAXLEN> &S, Elem
 // bases at a contig end, whose text bound lv_group handles).
 constexpr int FKM = 5;                     // lv_lane.h KM: the filter runs at limits k <= 5 (6 and 7 cut more
                                            // instructions, but their masks' spills cost more: prefilter_range_r05m.txt)
-constexpr uint32_t FILTER_MIN = 16;        // elements left in the order for a filter pass to pay off
+constexpr uint32_t FILTER_MIN = 2;         // elements left in the order for a filter pass to pay off
 constexpr uint32_t FWIN = WAVE / 2;        // pop-order positions per filter pass (a lane pair each)
 constexpr uint32_t FRES_VALID = 1u << 31;
 
@@ -1001,6 +1001,10 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, El
                     wBase = fDone;
                     wEnd = fDone + cnt;
                     PH_CNT(A, S, PH_NFILTER, 1);
+#if SNAPGPU_PHASE_TIMERS
+                    const uint32_t nfr = (uint32_t)__popcll(ballot((fres & FRES_VALID) != 0u)) / 2u;
+                    PH_CNT(A, S, PH_NFRES, nfr);
+#endif
                 }
             }
             posb = fDone;
@@ -1106,6 +1110,14 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, El
             if (m > 0) {
                 PH_CNT(A, S, PH_NPASS, 1);
                 if (forced) PH_CNT(A, S, PH_NPASSF, 1);
+#if SNAPGPU_PHASE_TIMERS
+                if (forced) {   // LV'd candidates of forced passes, and those with filter distances (possible successes)
+                    const int ln = lane_id();
+                    const uint32_t nk = (uint32_t)__popcll(ballot(ln < m && cand_known(G.cand[lvIdx[ln < m ? ln : 0]])));
+                    PH_CNT(A, S, PH_NLVF, m);
+                    PH_CNT(A, S, PH_NLVFK, nk);
+                }
+#endif
             }
             bool fin;
             if (GS == 8) fin = pass_apply<8, EXT>(A, S, ar, st, i0, iEnd, lvIdx, m, k, n, nb, lastSlot, lastSkip, result);

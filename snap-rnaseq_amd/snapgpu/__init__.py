@@ -479,7 +479,7 @@ class BaseAligner:
               "rows_rev", "n_score_calls", "n_forced", "n_popped", "n_succ", "passloop", "select", "fetch", "seedloop",
               "n_batch", "rank", "n_elems_forced", "candlist", "succ", "nearby", "prob", "fails", "n_fail_steps",
               "succ_tail", "n_pass_forced", "passloop_forced", "heavy_read_cycles", "n_heavy_reads", "n_cand_forced",
-              "read_cycles", "n_filter")
+              "read_cycles", "n_filter", "n_lv_forced", "n_lv_forced_known", "n_filter_results")
 
     def phase_cycles(self, reset=True):
         """Diagnostic per-phase shader-cycle sums (needs SNAPGPU_PHASES=1 at construction)."""

@@ -47,6 +47,9 @@ out["cycles_per_success"] = {k: round(ph[k] / n, 1) for k in ("succ", "nearby", 
 out["cycles_per_pass"] = {k: round(ph[k] / max(ph["n_pass"], 1), 1) for k in ("passloop", "stage", "lv_fwd", "lv_rev", "apply", "fails", "succ")}
 out["forced"] = {"passes_per_read": ph["n_pass_forced"] / args.reads, "passloop_cycles_per_read": ph["passloop_forced"] / args.reads,
                  "candidates_per_read": ph["n_cand_forced"] / args.reads,
+                 "filter_results_per_read": ph["n_filter_results"] / args.reads,
+                 "lv_candidates_per_read": ph["n_lv_forced"] / args.reads,
+                 "lv_candidates_with_filter_distances_per_read": ph["n_lv_forced_known"] / args.reads,
                  "nonforced_passes_per_read": (ph["n_pass"] - ph["n_pass_forced"]) / args.reads,
                  "nonforced_passloop_cycles_per_read": (ph["passloop"] - ph["passloop_forced"]) / args.reads}
 out["heavy_reads"] = {"def": ">= 64 candidate elements", "share_of_reads": ph["n_heavy_reads"] / args.reads,
