@@ -748,8 +748,8 @@ __device__ __forceinline__ uint32_t count_above_desc(const uint32_t *L, uint32_t
 // event counts) to its block's slice with no-return atomics (snapgpu_phase_cycles).
 // Compiled in only with -DSNAPGPU_PHASE_TIMERS=1 (`make PHASE_TIMERS=1`): even switched off
 // at run time, the timestamps held across loops cost SGPR spills in the production kernel.
-enum : int { PH_SETUP = 0, PH_LOOKUP, PH_INSERT, PH_SCORE, PH_POP, PH_DESC, PH_STAGE, PH_LVF, PH_LVR, PH_APPLY,
-             PH_WB, PH_OUT, PH_NPASS, PH_NCAND, PH_NREAD, PH_NPASS16, PH_NPASS32, PH_NPASS64, PH_ROWSF, PH_ROWSR,
+enum : int { PH_SETUP = 0, PH_LOOKUP, PH_INSERT, PH_SCORE, PH_POP, PH_NLVFU, PH_STAGE, PH_LVF, PH_LVR, PH_APPLY,
+             PH_WB, PH_OUT, PH_NPASS, PH_NCAND, PH_NLVF2, PH_NPASS16, PH_NPASS32, PH_NPASS64, PH_ROWSF, PH_ROWSR,
              PH_NSCORECALL, PH_NFORCED, PH_NPOPPED, PH_NSUCC, PH_PASSLOOP, PH_SEL, PH_FETCH, PH_SEEDLOOP, PH_NBATCH,
              PH_RANK, PH_NELEMSF, PH_CANDL, PH_SUCC, PH_NEARBY, PH_PROB, PH_FAILS, PH_NFAILSTEP, PH_SUCCWB,
              PH_NPASSF, PH_PASSLOOPF, PH_HEAVYCYC, PH_NHEAVY, PH_NCANDF, PH_READCYC, PH_NFILTER, PH_NLVF, PH_NLVFK, PH_NFRES,

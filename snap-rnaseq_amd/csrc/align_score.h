@@ -1113,9 +1113,16 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, El
 #if SNAPGPU_PHASE_TIMERS
                 if (forced) {   // LV'd candidates of forced passes, and those with filter distances (possible successes)
                     const int ln = lane_id();
-                    const uint32_t nk = (uint32_t)__popcll(ballot(ln < m && cand_known(G.cand[lvIdx[ln < m ? ln : 0]])));
+                    const uint32_t lp = lvIdx[ln < m ? ln : 0];
+                    const uint32_t cwl = G.cand[lp];
+                    const bool second = lp > 0 && cand_slot(G.cand[lp - 1]) == cand_slot(cwl);
+                    const uint32_t nk = (uint32_t)__popcll(ballot(ln < m && cand_known(cwl)));
+                    const uint32_t nu = (uint32_t)__popcll(ballot(ln < m && !cand_known(cwl) && k <= FKM));
+                    const uint32_t n2 = (uint32_t)__popcll(ballot(ln < m && !cand_known(cwl) && second));
                     PH_CNT(A, S, PH_NLVF, m);
                     PH_CNT(A, S, PH_NLVFK, nk);
+                    PH_CNT(A, S, PH_NLVFU, nu);
+                    PH_CNT(A, S, PH_NLVF2, n2);
                 }
 #endif
             }

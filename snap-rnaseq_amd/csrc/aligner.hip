@@ -519,7 +519,6 @@ __device__ __forceinline__ void align_one(const KArgs &A, Lds<MAXLEN> &S, ElemOf
         if (nN > A.maxK) { flags |= SNAPGPU_FLAG_TOO_MANY_NS; run = false; }
     }
     PH_ADD(A, S, PH_SETUP, tsetup);
-    PH_CNT(A, S, PH_NREAD, 1);
     if (run) {
         st.lps[0] = st.lps[1] = 0;
         st.mostSeeds[0] = st.mostSeeds[1] = 1;

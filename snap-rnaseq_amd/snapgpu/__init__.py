@@ -474,8 +474,8 @@ class BaseAligner:
         lib().snapgpu_last_timing(self._h, C.byref(t))
         return {f: getattr(t, f) for f, _ in t._fields_}
 
-    PHASES = ("setup", "lookup", "insert", "score", "pop", "desc", "stage", "lv_fwd", "lv_rev", "apply",
-              "writeback", "out", "n_pass", "n_cand", "n_read", "n_pass16", "n_pass32", "n_pass64", "rows_fwd",
+    PHASES = ("setup", "lookup", "insert", "score", "pop", "n_lv_forced_unknown_lowk", "stage", "lv_fwd", "lv_rev", "apply",
+              "writeback", "out", "n_pass", "n_cand", "n_lv_forced_unknown_second", "n_pass16", "n_pass32", "n_pass64", "rows_fwd",
               "rows_rev", "n_score_calls", "n_forced", "n_popped", "n_succ", "passloop", "select", "fetch", "seedloop",
               "n_batch", "rank", "n_elems_forced", "candlist", "succ", "nearby", "prob", "fails", "n_fail_steps",
               "succ_tail", "n_pass_forced", "passloop_forced", "heavy_read_cycles", "n_heavy_reads", "n_cand_forced",

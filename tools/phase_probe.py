@@ -38,7 +38,7 @@ ms = al.timing()["mainKernelMs"]
 tot = sum(ph[k] for k in ("setup", "lookup", "insert", "score", "out"))
 ph["cycles_per_read_total"] = tot
 out = {"kernel_ms": ms, "reads": args.reads, "cycles_per_read": {k: ph[k] / args.reads for k in ph}}
-out["share_of_wave_time"] = {k: round(ph[k] / tot, 4) for k in ("setup", "lookup", "insert", "score", "pop", "desc",
+out["share_of_wave_time"] = {k: round(ph[k] / tot, 4) for k in ("setup", "lookup", "insert", "score", "pop",
                                                                  "stage", "lv_fwd", "lv_rev", "apply", "writeback", "out",
                                                                  "select", "fetch", "passloop", "rank", "candlist", "succ",
                                                                  "nearby", "prob", "fails", "succ_tail")}
@@ -50,6 +50,8 @@ out["forced"] = {"passes_per_read": ph["n_pass_forced"] / args.reads, "passloop_
                  "filter_results_per_read": ph["n_filter_results"] / args.reads,
                  "lv_candidates_per_read": ph["n_lv_forced"] / args.reads,
                  "lv_candidates_with_filter_distances_per_read": ph["n_lv_forced_known"] / args.reads,
+                 "lv_unknown_at_k_le_5_per_read": ph["n_lv_forced_unknown_lowk"] / args.reads,
+                 "lv_unknown_not_first_of_element_per_read": ph["n_lv_forced_unknown_second"] / args.reads,
                  "nonforced_passes_per_read": (ph["n_pass"] - ph["n_pass_forced"]) / args.reads,
                  "nonforced_passloop_cycles_per_read": (ph["passloop"] - ph["passloop_forced"]) / args.reads}
 out["heavy_reads"] = {"def": ">= 64 candidate elements", "share_of_reads": ph["n_heavy_reads"] / args.reads,
