@@ -259,8 +259,9 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
     // Sub-batches (SNAPGPU_SINGLE_SUBBATCH useful reads each; default two halves from 200k reads, one
     // for BAM and sorted output, whose records are written as one block): stage A aligns sub-batch s
     // (both aligners in flight) on this thread while a stage-B thread runs sub-batch s - 1's filter,
-    // CIGARs (the aligners' side streams), records and their write -- the file in input order, the
-    // counts of the whole call applied at the end, all or nothing.
+    // CIGARs (the aligners' side streams) and records, and a writer thread writes sub-batch s - 2's
+    // records -- the file in input order, the counts of the whole call applied at the end, all or
+    // nothing.
     uint64_t sub = nu;
     if (const char *e = getenv("SNAPGPU_SINGLE_SUBBATCH"); e && atoll(e) > 0) sub = (uint64_t)atoll(e);
     else if (nu >= 200000) sub = (nu + 1) / 2;
@@ -306,6 +307,11 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
     bool ok = true;
     if (!bam) ok = fwrite(hdr.data(), 1, hdr.size(), f) == hdr.size();
     std::vector<std::string> allParts;   // BAM / sorted: every record part, written at the end
+    // SAM: a sub-batch's records are written by their own thread while the next sub-batch is
+    // filtered and formatted (one writer at a time, in sub-batch order)
+    std::thread writer;
+    bool writeOk = true;
+    double writeMs = 0;
     std::vector<uint32_t> contamLocs;    // added with the GTF counts once nothing can fail any more
     std::string errMsg;
     int32_t lastNm = 0;                  // BAM NM carry-over (before any mapped record: the stack's leftover)
@@ -512,10 +518,15 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
         if (bam || opt->sortOutput) {
             for (auto &p : parts) allParts.push_back(std::move(p));
         } else {
-            // one sequential write per sub-batch, in order (the file output is ~80 ms of a 1M-read call on
-            // the box's tmpfs; parallel pwrites and a shared mapping filled by the writer threads measured
-            // slower, profiles/r06/ab/single_write_r06h.txt)
-            for (auto &p : parts) ok = ok && fwrite(p.data(), 1, p.size(), f) == p.size();
+            // one sequential write per sub-batch, in order, on the writer thread (the file output is
+            // ~50 ms of a 1M-read call on the box's tmpfs; parallel pwrites and a shared mapping filled
+            // by the formatting threads measured slower, profiles/r06/ab/single_write_r06h.txt)
+            if (writer.joinable()) writer.join();
+            writer = std::thread([&, ps = std::move(parts)]() {
+                const auto tw = std::chrono::steady_clock::now();
+                for (auto &p : ps) writeOk = writeOk && fwrite(p.data(), 1, p.size(), f) == p.size();
+                writeMs += msSince(tw);
+            });
         }
         st.ioMs += msSince(t0);
         return SNAPGPU_OK;
@@ -535,6 +546,9 @@ int snapgpu_single_align(snapgpu_aligner_t *ga, snapgpu_aligner_t *ta, snapgpu_g
             }
             tb.join();
         }
+        if (writer.joinable()) writer.join();
+        ok = ok && writeOk;
+        st.ioMs += writeMs;
     }
     if (rcA || rcB) {
         fclose(f);
