@@ -800,26 +800,35 @@ __device__ __forceinline__ bool forced_sort(const KArgs &A, Lds<MAXLEN> &S, Elem
 // just to establish "distance > k".  forced_filter takes the next 32 elements of the order, one per
 // lane pair, and computes the distances of each one's first unscored candidate with lv_lane.h
 // (lv_pair_dist: a pair's 11 diagonals as 128-bit masks in registers, 6 per lane) at the limit k of
-// the moment.  The limit only shrinks, so a distance above it fails at every later limit too: those
+// the moment; at limits 6 and 7 the next 16, one per lane quad (lv_quad_dist: 15 diagonals, 4 masks
+// per lane; round 6: forced mode's LV calls at those limits were 5.0 per C2 read and 10.4 per C3 read).  The limit only shrinks, so a distance above it fails at every later limit too: those
 // candidates are applied as failures without an LV pass (pass_apply); the rest -- possible successes,
 // which need their LV path for the match probability -- still go through lv_group.  Result per lane:
 // FRES_VALID | bit | e1 << 8 | e2 << 11 (7: above the limit), 0 when the lane's element has no
 // candidate the filter can settle (none unscored, lps above the limit, or a window short of n + MAX_K
 // bases at a contig end, whose text bound lv_group handles).
-constexpr int FKM = 5;                     // lv_lane.h KM: the filter runs at limits k <= 5 (6 and 7 cut more
-                                           // instructions, but their masks' spills cost more: prefilter_range_r05m.txt)
+constexpr int FKM = 5;                     // lv_lane.h KM: the pair filter runs at limits k <= 5 (6 and 7 on pairs
+                                           // spill more than they save: prefilter_range_r05m.txt); limits 6 and 7
+                                           // take the quad form (LQ_K)
 constexpr uint32_t FILTER_MIN = 2;         // elements left in the order for a filter pass to pay off
-constexpr uint32_t FWIN = WAVE / 2;        // pop-order positions per filter pass (a lane pair each)
+constexpr uint32_t FWIN = WAVE / 2;        // pop-order positions per pair filter pass (a lane pair each; quads: FWIN / 2)
 constexpr uint32_t FRES_VALID = 1u << 31;
 
-template <int MAXLEN>
+// QUAD: one candidate per lane quad (lv_quad_dist, limits 6 and 7: 16 positions per pass), else per lane
+// pair (lv_pair_dist, limits <= 5: 32 positions).  Distances above the limit are encoded 7; at limit 7 a
+// 7 is also an exact distance, which cand_needs_lv still sends through lv_group (7 <= k), so the
+// encoding stays sound: a candidate it lets fail without LV has e1 > k or e2 > k - e1.
+template <int MAXLEN, bool QUAD>
 __device__ __forceinline__ uint32_t forced_filter(const KArgs &A, Lds<MAXLEN> &S, const Elem64 *ar, const ReadState &st,
                                                   uint32_t n, const uint64_t *fSorted, uint32_t fAvail,
                                                   const uint16_t *order, uint32_t ordBase, uint32_t pos0, uint32_t cnt,
                                                   int k) {
     static_assert(Lds<MAXLEN>::NW == 2, "forced_filter: 128-bit masks");
+    constexpr int LPC = QUAD ? 4 : 2;          // lanes per candidate
+    constexpr int NM = QUAD ? 4 : FKM + 1;     // masks per lane
+    constexpr int KB = QUAD ? LQ_K : FKM;      // the window starts at loc - KB
     const int lane = lane_id();
-    const int c = lane >> 1, h = lane & 1;   // the lane pair (2c, 2c + 1) takes pop-order position pos0 + c
+    const int c = lane / LPC, h = lane % LPC;  // lanes LPC*c .. take pop-order position pos0 + c
     const uint32_t pos = pos0 + (uint32_t)c;
     bool act = (uint32_t)c < cnt;
     uint32_t e = 0;
@@ -842,11 +851,11 @@ __device__ __forceinline__ uint32_t forced_filter(const KArgs &A, Lds<MAXLEN> &S
     int s = 0;
     if (act) s = (int)(sp ? (uint32_t)reinterpret_cast<const uint8_t *>(ar + sp)[bit] : slot_offset(h3.x, h3.y, h3.z, h3.w, bit));
     act = act && substring_ok(A, loc, n + MAX_K);
-    // this half's masks: local i = forward diagonal x = h ? i : -i,
-    // F_x[m] = read[dir][m] != genome[loc + x + m] on the bit planes
-    uint64_t F[FKM + 1][2];
+    // this lane's masks, F_x[m] = read[dir][m] != genome[loc + x + m] on the bit planes: pair half h holds
+    // forward diagonal x = h ? i : -i at local i; quad lane h holds x = 4h + i - LQ_K at local i
+    uint64_t F[NM][2];
     {
-        const int64_t gp = (int64_t)loc - FKM + PACK_GUARD;
+        const int64_t gp = (int64_t)loc - KB + PACK_GUARD;
         const GPlane *src = A.gpl + (act ? (gp >> 5) : 0);
         const uint32_t sh = (uint32_t)gp & 31;
         uint32_t wh[6], wl[6], wm[6];
@@ -855,7 +864,7 @@ __device__ __forceinline__ uint32_t forced_filter(const KArgs &A, Lds<MAXLEN> &S
             const GPlane w = src[j];
             wh[j] = w.hi; wl[j] = w.lo; wm[j] = w.nm;
         }
-        uint32_t ah[5], al[5], am[5];   // the genome planes from position loc - FKM, 160 bits
+        uint32_t ah[5], al[5], am[5];   // the genome planes from position loc - KB, 160 bits
 #pragma unroll
         for (int j = 0; j < 5; j++) {
             ah[j] = __builtin_amdgcn_alignbit(wh[j + 1], wh[j], sh);
@@ -871,8 +880,8 @@ __device__ __forceinline__ uint32_t forced_filter(const KArgs &A, Lds<MAXLEN> &S
             rm[j] = (uint32_t)(rp[4 + j / 2] >> (32 * (j & 1)));
         }
 #pragma unroll
-        for (int i = 0; i <= FKM; i++) {   // the window shifted by FKM + x bits
-            const uint32_t cs = (uint32_t)(h ? FKM + i : FKM - i);
+        for (int i = 0; i < NM; i++) {   // the window shifted by KB + x bits
+            const uint32_t cs = QUAD ? (uint32_t)(4 * h + i) : (uint32_t)(h ? FKM + i : FKM - i);
             uint32_t f[4];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
@@ -886,11 +895,13 @@ __device__ __forceinline__ uint32_t forced_filter(const KArgs &A, Lds<MAXLEN> &S
         }
     }
     const int t = s + (int)A.seedLen;
-    const int e1 = lv_pair_dist<FKM, 1>(F, h, act, t, (int)n - t, (int)n + MAX_K - t, k);
-    int e2 = -1;
+    int e1, e2 = -1;
+    if constexpr (QUAD) e1 = lv_quad_dist<1>(F, h, act, t, (int)n - t, (int)n + MAX_K - t, k);
+    else e1 = lv_pair_dist<FKM, 1>(F, h, act, t, (int)n - t, (int)n + MAX_K - t, k);
     if (ballot(e1 >= 0)) {
         // reverse LV: pattern = read[s-1 .. 0], text = genome backwards from loc + s - 1 (BaseAligner.cpp:1216-1220)
-        e2 = lv_pair_dist<FKM, -1>(F, h, e1 >= 0, 127 - (s - 1), s, s + MAX_K, k - e1);
+        if constexpr (QUAD) e2 = lv_quad_dist<-1>(F, h, e1 >= 0, 127 - (s - 1), s, s + MAX_K, k - e1);
+        else e2 = lv_pair_dist<FKM, -1>(F, h, e1 >= 0, 127 - (s - 1), s, s + MAX_K, k - e1);
     }
     return act ? FRES_VALID | bit | (uint32_t)(e1 < 0 ? 7 : e1) << 8 | (uint32_t)(e2 < 0 ? 7 : e2) << 11 : 0u;
 }
@@ -918,8 +929,8 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, El
     uint32_t fDone = 0, fAvail = 0, ordBase = 0;
     bool fMore = true;   // a ranking window came back full: elements of lower rank may remain
     const uint64_t *fSorted = nullptr;   // radix-sorted pop order (reads with >= A.radixMin elements)
-    // forced_filter's window over pop-order positions [wBase, wEnd): lanes 2j, 2j + 1 hold position wBase + j
-    uint32_t fres = 0, wBase = 0, wEnd = 0;
+    // forced_filter's window over pop-order positions [wBase, wEnd): lanes j << fShift .. hold position wBase + j
+    uint32_t fres = 0, wBase = 0, wEnd = 0, fShift = 1;   // fShift: log2 of the lanes per position (pairs 1, quads 2)
     for (uint32_t guard = 0;; guard++) {
         // lane id re-read per batch (volatile asm): masks and addresses derived from it are
         // recomputed in the batch instead of hoisted and kept live, spilled, across the pass loop
@@ -995,14 +1006,18 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, El
             }
             if constexpr (Lds<MAXLEN>::NW == 2) {
                 const int kf = st.scoreLimit < (uint32_t)(MAX_K - 1) ? (int)st.scoreLimit : MAX_K - 1;
-                if (fDone >= wEnd && kf <= FKM && fAvail - fDone >= FILTER_MIN) {
-                    const uint32_t cnt = fAvail - fDone < (uint32_t)FWIN ? fAvail - fDone : (uint32_t)FWIN;
-                    fres = forced_filter<MAXLEN>(A, S, ar, st, n, fSorted, fAvail, order, ordBase, fDone, cnt, kf);
+                if (fDone >= wEnd && kf <= LQ_K && fAvail - fDone >= FILTER_MIN) {
+                    const bool quad = kf > FKM;
+                    const uint32_t fw = quad ? FWIN / 2 : FWIN;
+                    const uint32_t cnt = fAvail - fDone < fw ? fAvail - fDone : fw;
+                    if (quad) fres = forced_filter<MAXLEN, true>(A, S, ar, st, n, fSorted, fAvail, order, ordBase, fDone, cnt, kf);
+                    else fres = forced_filter<MAXLEN, false>(A, S, ar, st, n, fSorted, fAvail, order, ordBase, fDone, cnt, kf);
+                    fShift = quad ? 2u : 1u;
                     wBase = fDone;
                     wEnd = fDone + cnt;
                     PH_CNT(A, S, PH_NFILTER, 1);
 #if SNAPGPU_PHASE_TIMERS
-                    const uint32_t nfr = (uint32_t)__popcll(ballot((fres & FRES_VALID) != 0u)) / 2u;
+                    const uint32_t nfr = (uint32_t)__popcll(ballot((fres & FRES_VALID) != 0u)) >> fShift;
                     PH_CNT(A, S, PH_NFRES, nfr);
 #endif
                 }
@@ -1057,7 +1072,7 @@ __device__ __forceinline__ bool score_batched(const KArgs &A, Lds<MAXLEN> &S, El
             const uint32_t cnt = (uint32_t)__popcll(pend);
             // the filter's result for this element (pop-order position posb + lane), if in its window
             const uint32_t wl = posb + (uint32_t)lane - wBase;
-            const uint32_t fr = (uint32_t)shfl_idx((int)fres, (int)(2u * (wl & (FWIN - 1))));
+            const uint32_t fr = (uint32_t)shfl_idx((int)fres, (int)((wl << fShift) & 63u));
             const bool inWin = forced && posb + (uint32_t)lane >= wBase && posb + (uint32_t)lane < wEnd &&
                                (uint32_t)lane < nb && (fr & FRES_VALID);
             const uint32_t known = inWin ? (1u << 9) | ((fr >> 8) & 7u) << 10 | ((fr >> 11) & 7u) << 13 : 0u;

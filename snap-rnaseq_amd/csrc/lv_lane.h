@@ -13,7 +13,8 @@
 // Exactness: lv_group's row e reads row e-1 only, so a lane evaluating row e's diagonals from its
 // own copy of row e-1 computes the same values; the first row in which a diagonal reaches
 // patternLen is the distance in both.  KM bounds k at compile time (register arrays, no dynamic
-// indexing); callers use it only for k <= KM.
+// indexing); callers use it only for k <= KM.  The kernel runs the distance split over a lane pair
+// (limits <= 5) or a lane quad (limits 6 and 7), below; lv_lane_dist is the single-lane reference form.
 #pragma once
 #include <stdint.h>
 
@@ -181,6 +182,94 @@ __device__ __forceinline__ int lv_pair_dist(const uint64_t (&M)[KM + 1][2], int 
         // would skip it, and its partner's DPP would read a lane outside EXEC)
         const int partnerHit = ll_pair_swap(hit ? 1 : 0);
         if (hit || partnerHit != 0) return e;
+    }
+    return -1;
+}
+
+// ------------------------------------------------------------ four lanes per candidate
+// The same distance with a candidate's 2 KQ + 1 = 15 diagonals over a lane quad (lanes 4c .. 4c + 3),
+// for limits 6 and 7, where a lane pair would hold 8 masks per lane (the registers spill).  Lane q holds
+// slots s = 4q + j (j = 0..3), forward diagonal x = s - KQ (x = -7 .. 8; slot x = 8 is never in a row's
+// band), 4 masks per lane.  A row reads its neighbours x - 1 / x + 1 of the previous row: inside the lane,
+// or -- for j = 0 / j = 3 -- the neighbour lane's j = 3 / j = 0, moved by a DPP quad permute.  DIR = -1:
+// reverse diagonal d = -x reads forward diagonal x's mask through the "last set <= 127 - p" view (as the
+// pair form does), so its d - 1 / d + 1 are slots s + 1 / s - 1.
+//
+// quad_row: row e of lane q, every slot from the previous row's values (Bl[0]: the lower neighbour lane's
+// slot 3, 0 for q = 0; Bl[1..4]: own slots; Bl[5]: the upper neighbour's slot 0, 0 for q = 3), in place.
+// Out-of-band slots (|x| > e) keep their value.  Returns whether a slot reached patternLen.  The per-slot
+// arithmetic is lv_lane_dist's.  Shared by lv_quad_dist and the host lockstep emulation
+// (tests/c/lv_lane_test.cpp).
+constexpr int LQ_K = 7;
+template <int DIR>
+__host__ __device__ __forceinline__ bool quad_row(const uint64_t (&M)[4][2], int q, int e, int (&Bl)[6], int q0m2, int patB,
+                                                  int patternLen, int textLen) {
+    constexpr int NBITS = 128;
+    int nb[4];
+    bool hit = false;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int x = 4 * q + j - LQ_K;
+        const int ax = x < 0 ? -x : x;
+        const int d = DIR > 0 ? x : -x;
+        const int old = Bl[j + 1], lowB = Bl[j], highB = Bl[j + 2];   // slots x - 1, x + 1
+        const int leftB = DIR > 0 ? lowB : highB;                      // B[d - 1]
+        const int rightB = (DIR > 0 ? highB : lowB) + 1;               // B[d + 1] + 1
+        const int x1B = old + 1;
+        const int bxdB = leftB > x1B ? leftB : x1B;
+        const int bestB = rightB > bxdB ? rightB : bxdB;
+        const int endd = patternLen < textLen - d ? patternLen : textLen - d;
+        const int enddB = endd + 2;
+        const int mpos = q0m2 + bestB;
+        const int mposc = mpos < NBITS ? mpos : NBITS;
+        const int fa = DIR > 0 ? ll_first_from(M[j][0], M[j][1], mposc) : 127 - ll_last_upto(M[j][0], M[j][1], 127 - mposc);
+        const int fB = fa - q0m2;
+        const int slidB = fB < enddB ? fB : enddB;
+        const int bnewB = bestB < enddB ? slidB : (fa == mposc ? bestB : enddB);
+        const bool in = ax <= e;
+        nb[j] = in ? bnewB : old;
+        hit = hit || (in && bnewB == patB);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) Bl[j + 1] = nb[j];
+    return hit;
+}
+// first set position >= p of lane-local slot j in the direction's view (see ll_first_dir)
+template <int DIR>
+__host__ __device__ __forceinline__ int quad_first(const uint64_t (&M)[4][2], int j, int p) {
+    return DIR > 0 ? ll_first_from(M[j][0], M[j][1], p) : 127 - ll_last_upto(M[j][0], M[j][1], 127 - p);
+}
+
+// All four lanes of a quad call it together with the same act / k (one candidate); the distance (or -1
+// above k) comes out in all four.  Divergence between quads is fine: every DPP stays inside the quad.
+template <int DIR>
+__device__ __forceinline__ int lv_quad_dist(const uint64_t (&M)[4][2], int q, bool act, int q0, int patternLen, int textLen,
+                                            int k) {
+    if (!act) return -1;
+    if (k > LQ_K) k = LQ_K;
+    const int end0 = patternLen < textLen ? patternLen : textLen;
+    // diagonal 0 is slot 7: lane 1, j = 3 (broadcast over the quad: quad_perm [1, 1, 1, 1])
+    const int f0 = __builtin_amdgcn_mov_dpp(quad_first<DIR>(M, 3, q0), 0x55, 0xf, 0xf, false);
+    const int fm = f0 - q0;
+    const int v0 = fm < end0 ? fm : end0;
+    if (v0 == end0) {
+        const int result = patternLen > end0 ? patternLen - end0 : 0;
+        return result > k ? -1 : result;
+    }
+    int Bl[6] = {0, 0, 0, 0, 0, 0};
+    if (q == 1) Bl[4] = v0 + 2;
+    const int patB = patternLen + 2, q0m2 = q0 - 2;
+#pragma unroll
+    for (int e = 1; e <= LQ_K; e++) {
+        if (e > k) break;
+        const int lo = __builtin_amdgcn_mov_dpp(Bl[4], 0x90, 0xf, 0xf, false);   // quad_perm [0, 0, 1, 2]: lane q - 1's slot 3
+        const int hi = __builtin_amdgcn_mov_dpp(Bl[1], 0xF9, 0xf, 0xf, false);   // quad_perm [1, 2, 3, 3]: lane q + 1's slot 0
+        Bl[0] = q == 0 ? 0 : lo;
+        Bl[5] = q == 3 ? 0 : hi;
+        int h = quad_row<DIR>(M, q, e, Bl, q0m2, patB, patternLen, textLen) ? 1 : 0;
+        h |= __builtin_amdgcn_mov_dpp(h, 0xB1, 0xf, 0xf, false);   // quad_perm [1, 0, 3, 2]
+        h |= __builtin_amdgcn_mov_dpp(h, 0x4E, 0xf, 0xf, false);   // quad_perm [2, 3, 0, 1]
+        if (h) return e;
     }
     return -1;
 }

@@ -84,6 +84,40 @@ static int pair_emul(const uint64_t (&F)[2 * KM + 1][2], int q0, int patternLen,
     return -1;
 }
 
+// Host lockstep emulation of lv_quad_dist (lv_lane.h, device-only: DPP quad permutes): four lane states,
+// the neighbour slots moved by hand, every lane's row through the shared quad_row.  F16[s] is forward
+// diagonal x = s - LQ_K (s = 0..15); lane q holds slots 4q .. 4q + 3.
+template <int DIR>
+static int quad_emul(const uint64_t (&F16)[16][2], int q0, int patternLen, int textLen, int k) {
+    uint64_t M[4][4][2];
+    for (int q = 0; q < 4; q++)
+        for (int j = 0; j < 4; j++) { M[q][j][0] = F16[4 * q + j][0]; M[q][j][1] = F16[4 * q + j][1]; }
+    if (k > LQ_K) k = LQ_K;
+    const int end0 = patternLen < textLen ? patternLen : textLen;
+    const int fm = quad_first<DIR>(M[1], 3, q0) - q0;
+    const int v0 = fm < end0 ? fm : end0;
+    if (v0 == end0) {
+        const int result = patternLen > end0 ? patternLen - end0 : 0;
+        return result > k ? -1 : result;
+    }
+    int Bl[4][6] = {};
+    Bl[1][4] = v0 + 2;
+    const int patB = patternLen + 2, q0m2 = q0 - 2;
+    for (int e = 1; e <= LQ_K; e++) {
+        if (e > k) break;
+        int lo[4], hi[4];
+        for (int q = 0; q < 4; q++) { lo[q] = q == 0 ? 0 : Bl[q - 1][4]; hi[q] = q == 3 ? 0 : Bl[q + 1][1]; }
+        bool h = false;
+        for (int q = 0; q < 4; q++) {
+            Bl[q][0] = lo[q];
+            Bl[q][5] = hi[q];
+            h = quad_row<DIR>(M[q], q, e, Bl[q], q0m2, patB, patternLen, textLen) || h;
+        }
+        if (h) return e;
+    }
+    return -1;
+}
+
 // ll_first_from / ll_last_upto (select forms) against a plain bit scan, every start, sparse and
 // dense masks (empty words, single bits at the word edges)
 static long scanCheck() {
@@ -114,7 +148,7 @@ int main(int argc, char **argv) {
     const int cases = argc > 1 ? atoi(argv[1]) : 200000;
     if (const long sb = scanCheck()) { printf("mask scans: %ld wrong\n", sb); return 1; }
     static const char B4[] = "ACGT";
-    long bad = 0, checked = 0, succ = 0;
+    long bad = 0, checked = 0, succ = 0, qsucc = 0;
     for (int c = 0; c < cases; c++) {
         // genome window g[0 .. n + MAXK + KM) around loc = KM (so x = -KM .. KM stay inside)
         const int n = 40 + (int)(rnd() % 89);       // read length 40..128
@@ -155,6 +189,20 @@ int main(int argc, char **argv) {
             F[x + KM][0] = w[0];
             F[x + KM][1] = w[1];
         }
+        // the quad form's slots: forward diagonals x = -LQ_K .. LQ_K + 1
+        uint64_t F16[16][2];
+        for (int sl = 0; sl < 16; sl++) {
+            const int x = sl - LQ_K;
+            uint64_t w[2] = {0, 0};
+            for (int m = 0; m < N; m++) {
+                const char rc = m < n ? read[m] : 0;
+                const int gp = loc + x + m;
+                const char gc = gp >= 0 && gp < (int)sizeof g ? g[gp] : 'n';
+                if (!acgt(rc) || !acgt(gc) || rc != gc) w[m >> 6] |= 1ull << (m & 63);
+            }
+            F16[sl][0] = w[0];
+            F16[sl][1] = w[1];
+        }
         // the genome substring of a full window (BaseAligner.cpp:1161-1162); the shorter windows of the
         // contig-end fallback (:1163-1185) never take the per-lane filter (forced_filter routes them to
         // lv_group, whose text bound there depends on bytes past the window)
@@ -162,6 +210,27 @@ int main(int argc, char **argv) {
         const int t = s + seedLen;
         char qual[N + 16];
         memset(qual, 'I', sizeof qual);
+        for (int k = 0; k <= LQ_K; k++) {
+            double p;
+            int ni;
+            const int want1 = oracle_lv(1, g + loc + t, glen - t, read + t, qual, n - t, k, &p, &ni);
+            const int quad1 = quad_emul<1>(F16, t, n - t, glen - t, k);
+            checked++;
+            if (want1 != quad1) {
+                if (bad++ < 10) printf("quad fwd n=%d s=%d k=%d: oracle %d quad %d\n", n, s, k, want1, quad1);
+            }
+            if (want1 < 0) continue;
+            char rev[N + 16];
+            for (int i = 0; i < s; i++) rev[i] = read[s - 1 - i];
+            const int k2 = k - want1;
+            const int want2 = oracle_lv(-1, g + loc + s, s + MAXK, rev, qual, s, k2, &p, &ni);
+            const int quad2 = quad_emul<-1>(F16, 127 - (s - 1), s, s + MAXK, k2);
+            checked++;
+            if (want2 != quad2) {
+                if (bad++ < 10) printf("quad rev n=%d s=%d k2=%d: oracle %d quad %d\n", n, s, k2, want2, quad2);
+            }
+            qsucc += want2 >= 0;
+        }
         for (int k = 0; k <= KM; k++) {
             double p;
             int ni;
@@ -187,6 +256,7 @@ int main(int argc, char **argv) {
             succ += want2 >= 0;
         }
     }
-    printf("lv_lane: %ld calls, %ld full successes, %ld mismatches\n", checked, succ, bad);
+    printf("lv_lane: %ld calls, %ld full successes (pair form, k <= %d), %ld (quad form, k <= %d), %ld mismatches\n", checked,
+           succ, KM, qsucc, LQ_K, bad);
     return bad != 0;
 }
