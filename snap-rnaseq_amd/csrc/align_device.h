@@ -41,10 +41,11 @@ constexpr uint32_t UNUSED_SCORE = 0xffffu;
 constexpr uint32_t FAIL_SCORE = 0xffffffffu;
 constexpr int ELEM = 48;                  // hashTableElementSize == maxMergeDist
 constexpr uint32_t NPAD = 100;            // Genome::N_PADDING
-constexpr int NBUCKET_LOG2 = 8;
+constexpr int NBUCKET_LOG2 = 9;         // (512 u16 heads: C3 -2.2 %, C2 -0.9 % against 256; 128 was C3 +3.8 %,
+                                         // profiles/r06/ab/hash_buckets_r06h9.txt)
 constexpr int NBUCKET = 1 << NBUCKET_LOG2;  // element hash buckets (LDS)
-constexpr uint32_t SKCAP = 256;           // selection keys kept in LDS
-constexpr uint32_t MIRCAP = 256;          // elements whose key / chain link are mirrored in LDS
+constexpr uint32_t SKCAP = 192;           // selection keys kept in LDS (192 + 192 mirrors pay for the 512 heads)
+constexpr uint32_t MIRCAP = 192;          // elements whose key / chain link are mirrored in LDS
 constexpr int ELEM_DWORDS = 36;           // dwords of Elem512 (byte path)
 constexpr int BT = 128;                   // insertion-batch dedupe table (LDS)
 constexpr uint32_t NONE = 0xffffffffu;
